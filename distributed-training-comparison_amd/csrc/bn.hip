@@ -1,0 +1,336 @@
+// BatchNorm2d (training mode) forward/backward with fused ReLU and residual add, NHWC bf16.
+//
+// Replaces `nn.BatchNorm2d` (reference src/*/net.py:21,25,37,92), `F.relu` and
+// `out += self.shortcut(x)` (net.py:41-44, 108). Semantics follow torch's training-mode
+// batch norm: batch statistics over N*H*W with biased variance for normalisation,
+// unbiased variance for running_var, running = (1-momentum)*running + momentum*batch,
+// num_batches_tracked += 1. Under autocast the conv output is bf16, BN computes in fp32
+// and emits bf16, ReLU's backward masks with its own (bf16) output.
+//
+// Statistics: the forward sums (sum x, sum x^2) are produced by the conv epilogue into
+// fp64 slots (igemm.hip); here they are finalised. Backward sums (sum dz, sum dz*xhat)
+// are reduced per workgroup through LDS and then added into fp64 slots.
+#include "common.h"
+#include "kernels.h"
+
+namespace dtc {
+
+static inline int ceil_div_i(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+__global__ void bn_fwd_finalize_kernel(double* __restrict__ stats, int C, double count, const float* __restrict__ gamma,
+                                       const float* __restrict__ beta, float* __restrict__ rmean,
+                                       float* __restrict__ rvar, int64_t* __restrict__ nbt, float momentum,
+                                       float eps, float* __restrict__ mean, float* __restrict__ invstd,
+                                       float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < DTC_STAT_SLOTS; ++k) {
+    double* p = stats + (size_t)k * 2 * C;
+    s += p[c];
+    q += p[C + c];
+    p[c] = 0.0;
+    p[C + c] = 0.0;
+  }
+  const double mu = s / count;
+  double var = q / count - mu * mu;
+  if (var < 0.0) var = 0.0;
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  mean[c] = (float)mu;
+  invstd[c] = is;
+  if (rmean) {
+    const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mu);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unbiased);
+  }
+  const float a = gamma[c] * is;
+  scale[c] = a;
+  shift[c] = beta[c] - (float)mu * a;
+}
+
+int bn_fwd_finalize(double* stats, int C, int64_t count, const float* gamma, const float* beta, float* running_mean,
+                    float* running_var, int64_t* num_batches, float momentum, float eps, float* mean, float* invstd,
+                    float* scale, float* shift, hipStream_t st) {
+  DTC_CHECK_ARG(stats && gamma && beta && mean && invstd && scale && shift && C > 0 && count > 0,
+                "bn_fwd_finalize: bad args");
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(ceil_div_i(C, 256)), dim3(256), 0, st, stats, C, (double)count,
+                     gamma, beta, running_mean, running_var, num_batches, momentum, eps, mean, invstd, scale, shift);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                    const float* __restrict__ rm, const float* __restrict__ rv, float eps,
+                                    float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale,
+                                    float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float is = 1.f / sqrtf(rv[c] + eps);
+  mean[c] = rm[c];
+  invstd[c] = is;
+  const float a = gamma[c] * is;
+  scale[c] = a;
+  shift[c] = beta[c] - rm[c] * a;
+}
+
+int bn_eval_coef(int C, const float* gamma, const float* beta, const float* running_mean, const float* running_var,
+                 float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st) {
+  DTC_CHECK_ARG(gamma && beta && running_mean && running_var && mean && invstd && scale && shift && C > 0,
+                "bn_eval_coef: bad args");
+  hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(ceil_div_i(C, 256)), dim3(256), 0, st, C, gamma, beta, running_mean,
+                     running_var, eps, mean, invstd, scale, shift);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+// ------------------------------------------------------------------ forward apply
+enum { APPLY_PLAIN = 0, APPLY_RELU = 1, APPLY_ADD_RELU = 2, APPLY_DUAL_RELU = 3 };
+
+template <int MODE>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const u16* __restrict__ x, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, const u16* __restrict__ x2,
+                                                      const float* __restrict__ scale2,
+                                                      const float* __restrict__ shift2, u16* __restrict__ y,
+                                                      int64_t nvec, int cvec) {
+  for (int64_t v = blockIdx.x * (int64_t)256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % cvec) * 8;
+    float a[8], o[8];
+    unpack8(*(const uint4*)(x + v * 8), a);
+    const f32x4 s0 = *(const f32x4*)(scale + c0), s1 = *(const f32x4*)(scale + c0 + 4);
+    const f32x4 h0 = *(const f32x4*)(shift + c0), h1 = *(const f32x4*)(shift + c0 + 4);
+    const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = a[k] * sc[k] + sh[k];
+    if constexpr (MODE == APPLY_ADD_RELU) {
+      float r[8];
+      unpack8(*(const uint4*)(x2 + v * 8), r);
+      // torch rounds the BN output to bf16 before `out += shortcut(x)` (autocast)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = round_bf(o[k]) + r[k];
+    }
+    if constexpr (MODE == APPLY_DUAL_RELU) {
+      float r[8];
+      unpack8(*(const uint4*)(x2 + v * 8), r);
+      const f32x4 t0 = *(const f32x4*)(scale2 + c0), t1 = *(const f32x4*)(scale2 + c0 + 4);
+      const f32x4 u0 = *(const f32x4*)(shift2 + c0), u1 = *(const f32x4*)(shift2 + c0 + 4);
+      const float sc2[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+      const float sh2[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+      // torch rounds each BN output to bf16 before the residual add (autocast)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = round_bf(o[k]) + round_bf(r[k] * sc2[k] + sh2[k]);
+    }
+    if constexpr (MODE != APPLY_PLAIN) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = fmaxf(o[k], 0.f);
+    }
+    *(uint4*)(y + v * 8) = pack8(o);
+  }
+}
+
+template <int MODE>
+static int launch_apply(const u16* x, const float* s, const float* h, const u16* x2, const float* s2, const float* h2,
+                        u16* y, int64_t M, int C, hipStream_t st) {
+  DTC_CHECK_ARG(x && s && h && y && C % 8 == 0 && M > 0, "bn_apply: bad args (C=%d)", C);
+  const int64_t nvec = M * C / 8;
+  const int blocks = (int)std::min<int64_t>(4096, (nvec + 255) / 256);
+  hipLaunchKernelGGL((bn_apply_kernel<MODE>), dim3(blocks), dim3(256), 0, st, x, s, h, x2, s2, h2, y, nvec, C / 8);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+int bn_apply(const u16* x, const float* s, const float* h, u16* y, int64_t M, int C, hipStream_t st) {
+  return launch_apply<APPLY_PLAIN>(x, s, h, nullptr, nullptr, nullptr, y, M, C, st);
+}
+int bn_apply_relu(const u16* x, const float* s, const float* h, u16* y, int64_t M, int C, hipStream_t st) {
+  return launch_apply<APPLY_RELU>(x, s, h, nullptr, nullptr, nullptr, y, M, C, st);
+}
+int bn_apply_add_relu(const u16* x, const float* s, const float* h, const u16* res, u16* y, int64_t M, int C,
+                      hipStream_t st) {
+  DTC_CHECK_ARG(res != nullptr, "bn_apply_add_relu: residual required");
+  return launch_apply<APPLY_ADD_RELU>(x, s, h, res, nullptr, nullptr, y, M, C, st);
+}
+int bn_apply_dual_relu(const u16* x, const float* s, const float* h, const u16* x2, const float* s2, const float* h2,
+                       u16* y, int64_t M, int C, hipStream_t st) {
+  DTC_CHECK_ARG(x2 && s2 && h2, "bn_apply_dual_relu: second branch required");
+  return launch_apply<APPLY_DUAL_RELU>(x, s, h, x2, s2, h2, y, M, C, st);
+}
+
+// ------------------------------------------------------------------ backward
+template <bool MASK, bool DUAL>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
+    const u16* __restrict__ dy, const u16* __restrict__ ym, const u16* __restrict__ x1,
+    const float* __restrict__ mean1, const float* __restrict__ invstd1, double* __restrict__ acc1,
+    const u16* __restrict__ x2, const float* __restrict__ mean2, const float* __restrict__ invstd2,
+    double* __restrict__ acc2, u16* __restrict__ dz, int64_t M, int C, int rows_per_block) {
+  __shared__ float red[256 * 24];
+  const int tpr = C >> 3, rpp = 256 / tpr;
+  const int t = threadIdx.x, g = t % tpr, rr = t / tpr;
+  const int c0 = g * 8;
+  float m1[8], i1[8], m2[8], i2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    m1[k] = mean1[c0 + k];
+    i1[k] = invstd1[c0 + k];
+    if constexpr (DUAL) {
+      m2[k] = mean2[c0 + k];
+      i2[k] = invstd2[c0 + k];
+    }
+  }
+  float sd[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t m_begin = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t m_end = std::min<int64_t>(M, m_begin + rows_per_block);
+  for (int64_t m = m_begin + rr; m < m_end; m += rpp) {
+    const int64_t o = m * C + c0;
+    float d[8], a[8];
+    unpack8(*(const uint4*)(dy + o), d);
+    if constexpr (MASK) {
+      float yv[8];
+      unpack8(*(const uint4*)(ym + o), yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
+      *(uint4*)(dz + o) = pack8(d);  // exact: masking a bf16 value is exact
+    }
+    unpack8(*(const uint4*)(x1 + o), a);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sd[k] += d[k];
+      s1[k] += d[k] * ((a[k] - m1[k]) * i1[k]);
+    }
+    if constexpr (DUAL) {
+      float b[8];
+      unpack8(*(const uint4*)(x2 + o), b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s2[k] += d[k] * ((b[k] - m2[k]) * i2[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[t * 24 + k] = sd[k];
+    red[t * 24 + 8 + k] = s1[k];
+    red[t * 24 + 16 + k] = s2[k];
+  }
+  __syncthreads();
+  const size_t slot = (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * C;
+  for (int c = t; c < C; c += 256) {
+    const int gg = c >> 3, k = c & 7;
+    float a = 0.f, b = 0.f, e = 0.f;
+    for (int r2 = 0; r2 < rpp; ++r2) {
+      const float* q = red + (r2 * tpr + gg) * 24;
+      a += q[k];
+      b += q[8 + k];
+      e += q[16 + k];
+    }
+    unsafeAtomicAdd(acc1 + slot + c, (double)a);
+    unsafeAtomicAdd(acc1 + slot + C + c, (double)b);
+    if constexpr (DUAL) {
+      unsafeAtomicAdd(acc2 + slot + c, (double)a);
+      unsafeAtomicAdd(acc2 + slot + C + c, (double)e);
+    }
+  }
+}
+
+int bn_bwd_reduce(const u16* dy, const u16* ymask, const u16* x1, const float* mean1, const float* invstd1,
+                  double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, u16* dz,
+                  int64_t M, int C, hipStream_t st) {
+  DTC_CHECK_ARG(dy && x1 && mean1 && invstd1 && acc1 && C % 8 == 0 && C <= 2048 && M > 0, "bn_bwd_reduce: bad args");
+  DTC_CHECK_ARG(!ymask || dz, "bn_bwd_reduce: masked reduce needs a dz output");
+  const int tpr = C / 8, rpp = 256 / tpr;
+  // about 1024 workgroups, each a whole number of passes
+  int64_t rpb = std::max<int64_t>(rpp, (M + 1023) / 1024);
+  rpb = ((rpb + rpp - 1) / rpp) * rpp;
+  const int blocks = ceil_div_i(M, rpb);
+  const bool dual = x2 != nullptr;
+  if (dual) DTC_CHECK_ARG(mean2 && invstd2 && acc2, "bn_bwd_reduce: dual branch args");
+  if (ymask && dual)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, true>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1, invstd1,
+                       acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
+  else if (ymask)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, false>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
+                       invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
+  else if (dual)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, true>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
+                       invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
+                       invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void bn_bwd_finalize_kernel(double* __restrict__ acc, int C, double count, const float* __restrict__ gamma,
+                                       const float* __restrict__ mean, const float* __restrict__ invstd, float gscale,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sd = 0.0, sx = 0.0;
+  for (int k = 0; k < DTC_STAT_SLOTS; ++k) {
+    double* p = acc + (size_t)k * 2 * C;
+    sd += p[c];
+    sx += p[C + c];
+    p[c] = 0.0;
+    p[C + c] = 0.0;
+  }
+  if (dgamma) dgamma[c] = (float)(sx * gscale);
+  if (dbeta) dbeta[c] = (float)(sd * gscale);
+  const double is = invstd[c];
+  const double A = (double)gamma[c] * is;
+  const double B = -A * is * sx / count;
+  const double Cc = -A * sd / count - B * (double)mean[c];
+  coef[c] = (float)A;
+  coef[C + c] = (float)B;
+  coef[2 * C + c] = (float)Cc;
+}
+
+int bn_bwd_finalize(double* acc, int C, int64_t count, const float* gamma, const float* mean, const float* invstd,
+                    float gscale, float* dgamma, float* dbeta, float* coef, hipStream_t st) {
+  DTC_CHECK_ARG(acc && gamma && mean && invstd && coef && C > 0 && count > 0, "bn_bwd_finalize: bad args");
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div_i(C, 256)), dim3(256), 0, st, acc, C, (double)count, gamma,
+                     mean, invstd, gscale, dgamma, dbeta, coef);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+template <bool DUAL>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const u16* __restrict__ dz, const u16* __restrict__ x1,
+                                                          const float* __restrict__ coef1, u16* __restrict__ dx1,
+                                                          const u16* __restrict__ x2, const float* __restrict__ coef2,
+                                                          u16* __restrict__ dx2, int64_t nvec, int C) {
+  const int cvec = C >> 3;
+  for (int64_t v = blockIdx.x * (int64_t)256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % cvec) * 8;
+    float d[8], a[8], o[8];
+    unpack8(*(const uint4*)(dz + v * 8), d);
+    unpack8(*(const uint4*)(x1 + v * 8), a);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = coef1[c0 + k] * d[k] + coef1[C + c0 + k] * a[k] + coef1[2 * C + c0 + k];
+    *(uint4*)(dx1 + v * 8) = pack8(o);
+    if constexpr (DUAL) {
+      unpack8(*(const uint4*)(x2 + v * 8), a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = coef2[c0 + k] * d[k] + coef2[C + c0 + k] * a[k] + coef2[2 * C + c0 + k];
+      *(uint4*)(dx2 + v * 8) = pack8(o);
+    }
+  }
+}
+
+int bn_bwd_apply(const u16* dz, const u16* x1, const float* coef1, u16* dx1, const u16* x2, const float* coef2,
+                 u16* dx2, int64_t M, int C, hipStream_t st) {
+  DTC_CHECK_ARG(dz && x1 && coef1 && dx1 && C % 8 == 0 && M > 0, "bn_bwd_apply: bad args");
+  const int64_t nvec = M * C / 8;
+  const int blocks = (int)std::min<int64_t>(4096, (nvec + 255) / 256);
+  if (x2) {
+    DTC_CHECK_ARG(coef2 && dx2, "bn_bwd_apply: dual branch args");
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(blocks), dim3(256), 0, st, dz, x1, coef1, dx1, x2, coef2, dx2,
+                       nvec, C);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(blocks), dim3(256), 0, st, dz, x1, coef1, dx1, x2, coef2,
+                       dx2, nvec, C);
+  }
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace dtc

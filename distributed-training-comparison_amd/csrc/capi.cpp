@@ -1,0 +1,149 @@
+// extern "C" entry points of libdtc_amd.so (declared in include/dtc.h) and the thread-local
+// error channel. Each wrapper validates arguments, forwards to the C++ launcher and returns
+// its status; no exception or exit() crosses this boundary.
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include "../../include/dtc.h"
+#include "comm.h"
+#include "kernels.h"
+
+namespace dtc {
+static thread_local std::string g_err;
+int set_error(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+const char* last_error() { return g_err.c_str(); }
+}  // namespace dtc
+
+using namespace dtc;
+
+static inline hipStream_t S(void* s) { return (hipStream_t)s; }
+static inline ConvShape shape_of(const dtc_conv_desc* d) {
+  return ConvShape{d->n, d->h, d->w, d->c, d->k, d->r, d->s, d->stride, d->pad};
+}
+
+#define GUARD(body)                                                          \
+  try {                                                                      \
+    body                                                                     \
+  } catch (...) {                                                            \
+    return set_error(DTC_EINVAL, "%s: unexpected C++ exception", __func__); \
+  }
+
+extern "C" {
+
+int dtc_abi_version(void) { return DTC_ABI_VERSION; }
+const char* dtc_last_error(void) { return last_error(); }
+
+size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass) {
+  if (!d || pass < 0 || pass > 2) return 0;
+  return plan_conv(shape_of(d), pass).slab_bytes;
+}
+
+int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, void* ws,
+                   size_t ws_bytes, void* stream) {
+  DTC_CHECK_ARG(d && x && w && y, "dtc_conv2d_fwd: null argument");
+  GUARD(return conv_fwd(shape_of(d), x, w, y, stats, (float*)ws, ws ? ws_bytes : 0, S(stream));)
+}
+
+int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx, const uint16_t* res,
+                     void* ws, size_t ws_bytes, void* stream) {
+  DTC_CHECK_ARG(d && dy && w && dx, "dtc_conv2d_dgrad: null argument");
+  GUARD(return conv_dgrad(shape_of(d), dy, w, dx, res, (float*)ws, ws ? ws_bytes : 0, S(stream));)
+}
+
+int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* dw, float scale, void* ws,
+                     size_t ws_bytes, void* stream) {
+  DTC_CHECK_ARG(d && x && dy && dw && ws, "dtc_conv2d_wgrad: null argument (workspace is required)");
+  GUARD(return conv_wgrad(shape_of(d), x, dy, dw, 0, 0, scale, (float*)ws, ws_bytes, S(stream));)
+}
+
+int dtc_bn_fwd_finalize(double* stats, int c, int64_t count, const float* gamma, const float* beta,
+                        float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, float* mean,
+                        float* invstd, float* scale, float* shift, void* stream) {
+  return bn_fwd_finalize(stats, c, count, gamma, beta, running_mean, running_var, nbt, momentum, eps, mean, invstd,
+                         scale, shift, S(stream));
+}
+int dtc_bn_apply_relu(const uint16_t* x, const float* scale, const float* shift, uint16_t* y, int64_t m, int c,
+                      void* stream) {
+  return bn_apply_relu(x, scale, shift, y, m, c, S(stream));
+}
+int dtc_bn_apply_add_relu(const uint16_t* x, const float* scale, const float* shift, const uint16_t* res, uint16_t* y,
+                          int64_t m, int c, void* stream) {
+  return bn_apply_add_relu(x, scale, shift, res, y, m, c, S(stream));
+}
+int dtc_bn_apply_dual_relu(const uint16_t* x, const float* scale, const float* shift, const uint16_t* x2,
+                           const float* scale2, const float* shift2, uint16_t* y, int64_t m, int c, void* stream) {
+  return bn_apply_dual_relu(x, scale, shift, x2, scale2, shift2, y, m, c, S(stream));
+}
+int dtc_bn_bwd_reduce(const uint16_t* dy, const uint16_t* ymask, const uint16_t* x1, const float* mean1,
+                      const float* invstd1, double* acc1, const uint16_t* x2, const float* mean2, const float* invstd2,
+                      double* acc2, uint16_t* dz, int64_t m, int c, void* stream) {
+  return bn_bwd_reduce(dy, ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, m, c, S(stream));
+}
+int dtc_bn_bwd_finalize(double* acc, int c, int64_t count, const float* gamma, const float* mean, const float* invstd,
+                        float gscale, float* dgamma, float* dbeta, float* coef, void* stream) {
+  return bn_bwd_finalize(acc, c, count, gamma, mean, invstd, gscale, dgamma, dbeta, coef, S(stream));
+}
+int dtc_bn_bwd_apply(const uint16_t* dz, const uint16_t* x1, const float* coef1, uint16_t* dx1, const uint16_t* x2,
+                     const float* coef2, uint16_t* dx2, int64_t m, int c, void* stream) {
+  return bn_bwd_apply(dz, x1, coef1, dx1, x2, coef2, dx2, m, c, S(stream));
+}
+
+int dtc_stem_im2col(const float* x, uint16_t* cols, int n, int h, int w, void* stream) {
+  return stem_im2col(x, cols, n, h, w, S(stream));
+}
+int dtc_stem_pack_weight(const uint16_t* w27, uint16_t* w64, int k, void* stream) {
+  return stem_pack_weight(w27, w64, k, S(stream));
+}
+int dtc_head_fwd(const uint16_t* act, int n, int hw, int c, const uint16_t* wfc, const float* bfc, int ncls,
+                 float* feat, float* logits, void* stream) {
+  return head_fwd(act, n, hw, c, wfc, bfc, ncls, feat, logits, S(stream));
+}
+int dtc_head_bwd(const float* dlogits, const float* feat, const uint16_t* wfc, int n, int hw, int c, int ncls,
+                 float scale, float* dw, float* db, uint16_t* dact, void* stream) {
+  return head_bwd(dlogits, feat, wfc, n, hw, c, ncls, scale, dw, db, dact, S(stream));
+}
+int dtc_xent_fwd(const float* logits, const int64_t* labels, int n, int ncls, float* loss, float* lse, void* stream) {
+  return xent_fwd(logits, labels, n, ncls, loss, lse, S(stream));
+}
+int dtc_xent_bwd(const float* logits, const int64_t* labels, const float* lse, const float* gscale, int n, int ncls,
+                 float* dlogits, void* stream) {
+  return xent_bwd(logits, labels, lse, gscale, n, ncls, dlogits, S(stream));
+}
+
+int dtc_sgd_nesterov_flat(float* p, const float* g, float* mom, uint16_t* pb, int64_t n, float lr, float wd, float mu,
+                          const float* inv_scale, const int* found_inf, void* stream) {
+  return sgd_nesterov(p, g, mom, pb, n, lr, wd, mu, inv_scale, found_inf, S(stream));
+}
+int dtc_cast_f32_bf16(const float* src, uint16_t* dst, int64_t n, void* stream) {
+  return cast_f32_bf16(src, dst, n, S(stream));
+}
+int dtc_amp_check_finite(const float* g, int64_t n, int* found_inf, void* stream) {
+  return amp_check_finite(g, n, found_inf, S(stream));
+}
+int dtc_amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, int* found_inf, float growth,
+                         float backoff, int interval, void* stream) {
+  return amp_update_scale(scale, inv_scale, growth_tracker, found_inf, growth, backoff, interval, S(stream));
+}
+
+size_t dtc_comm_unique_id_bytes(void) { return comm_unique_id_bytes(); }
+int dtc_comm_get_unique_id(void* out) { GUARD(return comm_get_unique_id(out);) }
+int dtc_comm_init(dtc_comm** out, int rank, int world, const void* id, int device) {
+  GUARD(return comm_init((Comm**)out, rank, world, id, device);)
+}
+int dtc_comm_allreduce_sum(dtc_comm* comm, void* buf, size_t count, int dtype, void* stream) {
+  return comm_allreduce((Comm*)comm, buf, count, dtype, S(stream));
+}
+int dtc_comm_broadcast(dtc_comm* comm, void* buf, size_t count, int dtype, int root, void* stream) {
+  return comm_broadcast((Comm*)comm, buf, count, dtype, root, S(stream));
+}
+int dtc_comm_destroy(dtc_comm* comm) { return comm_destroy((Comm*)comm); }
+
+}  // extern "C"

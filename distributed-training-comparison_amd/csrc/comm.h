@@ -1,0 +1,20 @@
+// Internal RCCL communicator interface (see comm.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace dtc {
+struct Comm;
+size_t comm_unique_id_bytes();
+int comm_get_unique_id(void* out);
+int comm_init(Comm** out, int rank, int world, const void* uid, int device);
+int comm_destroy(Comm* c);
+// blocking-order collectives on the given stream
+int comm_allreduce(Comm* c, void* buf, size_t count, int dtype, hipStream_t st);
+int comm_broadcast(Comm* c, void* buf, size_t count, int dtype, int root, hipStream_t st);
+// Reducer primitives: fp32 SUM all-reduce of a bucket on the side stream after everything
+// enqueued so far on `compute`; join orders `compute` after all outstanding buckets.
+int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute);
+int comm_join(Comm* c, hipStream_t compute);
+int comm_world(const Comm* c);
+}  // namespace dtc

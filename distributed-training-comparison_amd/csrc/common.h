@@ -1,0 +1,103 @@
+// Shared device/host helpers for the MI355X (gfx950) ResNet-18 data-parallel step.
+//
+// Conventions used by every kernel in this library:
+//   * activations are NHWC bf16 (raw 16-bit words, `u16`), channels innermost;
+//   * master parameters / gradients are fp32 in one flat buffer (see resnet.cpp);
+//   * conv weights are K x R x S x C ("KRSC"), so one output channel's filter is a
+//     contiguous row of R*S*C elements: that row is the GEMM operand directly;
+//   * every launch takes the caller's hipStream_t; nothing here allocates memory.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+typedef uint16_t u16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+// ---------------------------------------------------------------- errors
+namespace dtc {
+int set_error(int code, const char* fmt, ...);
+const char* last_error();
+}  // namespace dtc
+
+#define DTC_EINVAL (-1)
+#define DTC_CHECK_ARG(cond, ...)                                   \
+  do {                                                             \
+    if (!(cond)) return ::dtc::set_error(DTC_EINVAL, __VA_ARGS__); \
+  } while (0)
+#define DTC_HIP(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return ::dtc::set_error((int)e_, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                              __FILE__, __LINE__);                                           \
+  } while (0)
+#define DTC_LAUNCH_CHECK() DTC_HIP(hipGetLastError())
+#define DTC_TRY(expr)      \
+  do {                     \
+    int r_ = (expr);       \
+    if (r_ != 0) return r_; \
+  } while (0)
+
+// ---------------------------------------------------------------- bf16 <-> f32
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((uint32_t)v << 16); }
+// Round-to-nearest-even (v_cvt_pk_bf16_f32 on gfx950; keeps NaN a NaN).
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+
+// unpack 8 bf16 held in a uint4 into floats
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = bf_lo(v.x); f[1] = bf_hi(v.x); f[2] = bf_lo(v.y); f[3] = bf_hi(v.y);
+  f[4] = bf_lo(v.z); f[5] = bf_hi(v.z); f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack_bf2(f[0], f[1]); v.y = pack_bf2(f[2], f[3]);
+  v.z = pack_bf2(f[4], f[5]); v.w = pack_bf2(f[6], f[7]);
+  return v;
+}
+
+// ---------------------------------------------------------------- fast unsigned division
+// q = (umulhi(n, m) + n) >> s, exact for n < 2^31 (pixel indices here are < 2^31).
+struct FastDiv {
+  uint32_t d, m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  if (d <= 1) { f.d = 1; f.m = 0; f.s = 0; return f; }
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+  f.s = l;
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+// ---------------------------------------------------------------- wave reductions (wave64)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Number of fp64 accumulator slots per statistics buffer: producers spread their
+// atomics over slots (blockIdx & (SLOTS-1)) so that thousands of workgroups do not
+// contend on the same 1 KB; the finalize kernels sum the slots in a fixed order.
+#define DTC_STAT_SLOTS 32
+

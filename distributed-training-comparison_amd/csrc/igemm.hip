@@ -1,0 +1,654 @@
+// Implicit-GEMM convolution on bf16 MFMA (v_mfma_f32_16x16x32_bf16) for gfx950.
+//
+// Replaces the cuDNN kernels that `nn.Conv2d` (reference src/*/net.py:18-24, 29-35, 91)
+// launches for forward, data-gradient and weight-gradient. One kernel template serves
+// all three; only the tile LOADERS differ:
+//
+//   mode   D (MFMA rows x cols)     A-side operand (rows)           B-side operand (cols)        reduction
+//   FWD    y[kout][pixel]           W  (KRSC rows)   row image      im2col(x)        row image   (r,s,c)
+//   DGRAD  dx[c][pixel]             W^T (k rows,c)   tr image       im2col^T(dy)     row image   (r,s,k)
+//   WGRAD  dW[(r,s,c)][kout]        im2col(x) (m,c)  tr image       dy (m,kout)      tr image    pixels m
+//
+// LDS images: 128-byte rows (64 bf16). A "row image" holds one GEMM row per LDS row with
+// the reduction index contiguous; fragments are read with ds_read_b128. A "tr image"
+// holds the REDUCTION index as the LDS row (64 rows x 64 columns per 8 KiB image);
+// fragments are read with ds_read_b64_tr_b16 (gfx950 transposing LDS read), so NHWC
+// tensors are staged exactly as they lie in HBM and never transposed in memory.
+// Tiles are filled by global_load_lds (LDS-DMA, 16 B per lane, lane-linear destination);
+// bank-conflict swizzles are applied on the per-lane SOURCE address and the matching
+// XOR on the read (guide §5.4 rule 21). Padding rows read a 1 KiB zero page.
+#include "common.h"
+#include "kernels.h"
+
+static __device__ __attribute__((aligned(1024))) uint4 g_zero_page[64];
+
+namespace dtc {
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+struct IGemmParams {
+  const u16* src0;  // FWD: x (NHWC)   DGRAD: dy (NPQK)   WGRAD: x (NHWC)
+  const u16* src1;  // FWD: W (KRSC)   DGRAD: W (KRSC)    WGRAD: dy (NPQK)
+  u16* out;         // bf16 output (non-slab epilogue): FWD y (NPQK), DGRAD dx (NHWC)
+  float* slab;      // fp32 split-K partials
+  const u16* res;   // DGRAD: optional residual added in the epilogue
+  double* stats;    // FWD: optional per-channel (sum, sumsq) accumulators [SLOTS][2][K]
+  int N, H, W, C, K, R, S, P, Q, stride, pad;
+  int M;            // GEMM pixel extent: FWD/WGRAD N*P*Q, DGRAD N*H*W
+  int RSC;
+  FastDiv fd_q, fd_pq;  // FWD/WGRAD: Q, P*Q ; DGRAD: W, H*W
+  FastDiv fd_cc;        // reduction chunks per tap: FWD C/64, DGRAD K/64
+  int num_kt, kt_per_split, tiles_a;
+};
+
+__device__ __forceinline__ int rowswz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int trswz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
+}
+
+// Row-image fragment: lane holds row (lane&15), reduction chunk (ks*4 + lane>>4).
+__device__ __forceinline__ bf16x8 frag_row(const char* region, int row0, int ks, int lane) {
+  const int row = row0 + (lane & 15);
+  const int ch = (ks * 4 + (lane >> 4)) ^ rowswz(row);
+  uint4 v = *(const uint4*)(region + row * 128 + (ch << 4));
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Tr-image fragment: lane holds column (cb + lane&15), reduction rows ks*32 + 8*(lane>>4) + 0..7.
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x8 frag_tr(const char* region, int cb, int ks, int lane) {
+  const int img = cb >> 6, cin = cb & 63;
+  const int i = lane & 15, q = i >> 2, pp = i & 3, g = lane >> 4;
+  const int unit = (cin >> 2) + pp;
+  const char* base = region + img * 8192;
+  const int kr0 = ks * 32 + g * 8 + q;
+  const int kr1 = kr0 + 4;
+  const int f0 = (((kr0 >> 1) & 1) << 2) | (((kr0 >> 3) & 1) << 3);
+  const int f1 = (((kr1 >> 1) & 1) << 2) | (((kr1 >> 3) & 1) << 3);
+  typedef __attribute__((address_space(3))) bf16x4_t lds_v4;
+  bf16x4_t t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(base + kr0 * 128 + ((unit ^ f0) << 3)));
+  bf16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(base + kr1 * 128 + ((unit ^ f1) << 3)));
+  return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int MODE, int BM, int BN, int WR, int WC, bool SLAB>
+__global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
+  constexpr int FM = BM / (WR * 16);
+  constexpr int FN = BN / (WC * 16);
+  constexpr int A_BYTES = BM * 128;
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int NIA = BM / 32;  // glds instructions per wave per stage, A side
+  constexpr int NIB = BN / 32;  // B side
+  constexpr bool A_TR = (MODE != MODE_FWD);
+  constexpr bool B_TR = (MODE == MODE_WGRAD);
+  static_assert(WR * WC == 4, "4 waves");
+  static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
+
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int ta = blockIdx.x % p.tiles_a;
+  const int tb = blockIdx.x / p.tiles_a;
+  const int a0 = ta * BM, b0 = tb * BN;
+  const int kt_begin = blockIdx.y * p.kt_per_split;
+  const int kt_end = min(p.num_kt, kt_begin + p.kt_per_split);
+  const int lrow = lane >> 3, pc = lane & 7;
+  const u16* zp = (const u16*)g_zero_page + pc * 8;
+
+  // ------------------------------------------------------------ loader state
+  // A side
+  int offA[NIA];
+  // B side (FWD: pixel of y; DGRAD: pixel of dx)
+  int64_t baseB[NIB];
+  int hB[NIB], wB[NIB];
+  // WGRAD: block-uniform tap, per-lane columns
+  int colA[NIA], colB[NIB];
+  int tap_r = 0, tap_s = 0;
+
+  if constexpr (MODE == MODE_FWD) {
+#pragma unroll
+    for (int j = 0; j < NIA; ++j) {
+      const int row = (wave + 4 * j) * 8 + lrow;
+      const int lc = pc ^ rowswz(row);
+      offA[j] = (a0 + row) * p.RSC + lc * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < NIB; ++j) {
+      const int row = (wave + 4 * j) * 8 + lrow;
+      const int lc = pc ^ rowswz(row);
+      const int pix = b0 + row;
+      int ih0 = -(1 << 20), iw0 = -(1 << 20);
+      int64_t base = 0;
+      if (pix < p.M) {
+        const int n = (int)fdiv((uint32_t)pix, p.fd_pq);
+        const int rem = pix - n * p.P * p.Q;
+        const int pp = (int)fdiv((uint32_t)rem, p.fd_q);
+        const int qq = rem - pp * p.Q;
+        ih0 = pp * p.stride - p.pad;
+        iw0 = qq * p.stride - p.pad;
+        base = (((int64_t)n * p.H + ih0) * p.W + iw0) * p.C + lc * 8;
+      }
+      baseB[j] = base; hB[j] = ih0; wB[j] = iw0;
+    }
+  } else if constexpr (MODE == MODE_DGRAD) {
+#pragma unroll
+    for (int j = 0; j < NIA; ++j) {
+      const int ia = wave + 4 * j;
+      const int img = ia >> 3, rowin = (ia & 7) * 8 + lrow;
+      const int lc = pc ^ trswz(rowin);
+      offA[j] = rowin * p.RSC + a0 + img * 64 + lc * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < NIB; ++j) {
+      const int row = (wave + 4 * j) * 8 + lrow;
+      const int lc = pc ^ rowswz(row);
+      const int pix = b0 + row;
+      int h = -(1 << 20), w = -(1 << 20), nP = 0;
+      if (pix < p.M) {
+        const int n = (int)fdiv((uint32_t)pix, p.fd_pq);
+        const int rem = pix - n * p.H * p.W;
+        h = (int)fdiv((uint32_t)rem, p.fd_q);
+        w = rem - h * p.W;
+        nP = n * p.P;
+      }
+      baseB[j] = nP;
+      colB[j] = lc * 8;
+      hB[j] = h; wB[j] = w;
+    }
+  } else {  // WGRAD
+    const int rs = a0 / p.C;
+    const int c0 = a0 - rs * p.C;
+    tap_r = rs / p.S;
+    tap_s = rs - tap_r * p.S;
+#pragma unroll
+    for (int j = 0; j < NIA; ++j) {
+      const int ia = wave + 4 * j;
+      const int img = ia >> 3, rowin = (ia & 7) * 8 + lrow;
+      colA[j] = c0 + img * 64 + ((pc ^ trswz(rowin)) * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < NIB; ++j) {
+      const int ib = wave + 4 * j;
+      const int img = ib >> 3, rowin = (ib & 7) * 8 + lrow;
+      colB[j] = b0 + img * 64 + ((pc ^ trswz(rowin)) * 8);
+    }
+  }
+
+  // reduction-step decomposition (FWD/DGRAD): kt -> (r, s, chunk); kept incrementally
+  int st_r = 0, st_s = 0, st_c = 0;
+  const int nchunk = (int)p.fd_cc.d;
+  if constexpr (MODE != MODE_WGRAD) {
+    const int rs = (int)fdiv((uint32_t)kt_begin, p.fd_cc);
+    st_c = kt_begin - rs * nchunk;
+    st_r = rs / p.S;
+    st_s = rs - st_r * p.S;
+  }
+
+  auto stage = [&](char* sb, int kt, int r, int s, int cc) {
+    if constexpr (MODE == MODE_FWD) {
+      const int wadd = (r * p.S + s) * p.C + cc * 64;
+#pragma unroll
+      for (int j = 0; j < NIA; ++j)
+        glds16(p.src1 + offA[j] + wadd, sb + (wave + 4 * j) * 1024);
+      const int64_t xadd = ((int64_t)r * p.W + s) * p.C + cc * 64;
+#pragma unroll
+      for (int j = 0; j < NIB; ++j) {
+        const int ih = hB[j] + r, iw = wB[j] + s;
+        const bool ok = ((unsigned)ih < (unsigned)p.H) && ((unsigned)iw < (unsigned)p.W);
+        const u16* src = ok ? (p.src0 + baseB[j] + xadd) : zp;
+        glds16(src, sb + A_BYTES + (wave + 4 * j) * 1024);
+      }
+    } else if constexpr (MODE == MODE_DGRAD) {
+      const int64_t wadd = (int64_t)cc * 64 * p.RSC + (r * p.S + s) * p.C;
+#pragma unroll
+      for (int j = 0; j < NIA; ++j)
+        glds16(p.src1 + offA[j] + wadd, sb + (wave + 4 * j) * 1024);
+#pragma unroll
+      for (int j = 0; j < NIB; ++j) {
+        int ph = hB[j] + p.pad - r, pw = wB[j] + p.pad - s;
+        bool ok = (ph >= 0) && (pw >= 0);
+        if (p.stride == 2) {
+          ok = ok && !(ph & 1) && !(pw & 1);
+          ph >>= 1; pw >>= 1;
+        }
+        ok = ok && (ph < p.P) && (pw < p.Q);
+        const u16* src = ok ? (p.src0 + ((baseB[j] + ph) * p.Q + pw) * p.K + cc * 64 + colB[j]) : zp;
+        glds16(src, sb + A_BYTES + (wave + 4 * j) * 1024);
+      }
+    } else {  // WGRAD: pixels kt*64 .. kt*64+63
+      const int m0 = kt * 64;
+      int64_t xo[2];
+      int64_t dyo[2];
+      bool okx[2], okd[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int pix = m0 + (wave + 4 * h) * 8 + lrow;
+        okd[h] = pix < p.M;
+        dyo[h] = (int64_t)pix * p.K;
+        const int n = (int)fdiv((uint32_t)pix, p.fd_pq);
+        const int rem = pix - n * p.P * p.Q;
+        const int pp = (int)fdiv((uint32_t)rem, p.fd_q);
+        const int qq = rem - pp * p.Q;
+        const int ih = pp * p.stride - p.pad + tap_r;
+        const int iw = qq * p.stride - p.pad + tap_s;
+        okx[h] = okd[h] && ((unsigned)ih < (unsigned)p.H) && ((unsigned)iw < (unsigned)p.W);
+        xo[h] = (((int64_t)n * p.H + ih) * p.W + iw) * p.C;
+      }
+#pragma unroll
+      for (int j = 0; j < NIA; ++j) {
+        const int h = j & 1;
+        const u16* src = okx[h] ? (p.src0 + xo[h] + colA[j]) : zp;
+        glds16(src, sb + (wave + 4 * j) * 1024);
+      }
+#pragma unroll
+      for (int j = 0; j < NIB; ++j) {
+        const int h = j & 1;
+        const u16* src = okd[h] ? (p.src1 + dyo[h] + colB[j]) : zp;
+        glds16(src, sb + A_BYTES + (wave + 4 * j) * 1024);
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int wr = wave / WC, wc = wave % WC;
+  const int arow0 = wr * (BM / WR), bcol0 = wc * (BN / WC);
+
+  auto advance = [&](int& r, int& s, int& cc) {
+    if (++cc == nchunk) {
+      cc = 0;
+      if (++s == p.S) { s = 0; ++r; }
+    }
+  };
+
+  if (kt_begin < kt_end) {
+    int r = st_r, s = st_s, cc = st_c;
+    stage(smem, kt_begin, r, s, cc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int buf = 0;
+    for (int kt = kt_begin; kt < kt_end; ++kt) {
+      char* cur = smem + buf * STAGE;
+      if (kt + 1 < kt_end) {
+        int r2 = r, s2 = s, c2 = cc;
+        if constexpr (MODE != MODE_WGRAD) advance(r2, s2, c2);
+        stage(smem + (buf ^ 1) * STAGE, kt + 1, r2, s2, c2);
+        r = r2; s = s2; cc = c2;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          if constexpr (A_TR) af[i] = frag_tr(cur, arow0 + i * 16, ks, lane);
+          else af[i] = frag_row(cur, arow0 + i * 16, ks, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if constexpr (B_TR) bfr[j] = frag_tr(cur + A_BYTES, bcol0 + j * 16, ks, lane);
+          else bfr[j] = frag_row(cur + A_BYTES, bcol0 + j * 16, ks, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  // ------------------------------------------------------------ epilogue
+  // D[row][col]: row = A-side index (4 consecutive per lane), col = B-side index.
+  const int rq = (lane >> 4) * 4;
+  const int cl = lane & 15;
+  if constexpr (MODE == MODE_WGRAD) {
+    // slab[split][kout][rsc]
+    float* slab = p.slab + (size_t)blockIdx.y * p.K * p.RSC;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int rsc = a0 + arow0 + i * 16 + rq;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int kout = b0 + bcol0 + j * 16 + cl;
+        *(f32x4*)(slab + (size_t)kout * p.RSC + rsc) = acc[i][j];
+      }
+    }
+  } else if constexpr (SLAB) {
+    const int ncols = (MODE == MODE_FWD) ? p.K : p.C;
+    float* slab = p.slab + (size_t)blockIdx.y * p.M * ncols;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ch = a0 + arow0 + i * 16 + rq;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int pix = b0 + bcol0 + j * 16 + cl;
+        if (pix < p.M) *(f32x4*)(slab + (size_t)pix * ncols + ch) = acc[i][j];
+      }
+    }
+  } else if constexpr (MODE == MODE_FWD) {
+    float* red = (float*)smem;  // [WC][BM][2]
+    const bool want_stats = (p.stats != nullptr);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int chl = arow0 + i * 16 + rq;
+      const int ch = a0 + chl;
+      float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int pix = b0 + bcol0 + j * 16 + cl;
+        float v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          v[t] = round_bf(acc[i][j][t]);
+          s4[t] += v[t];
+          q4[t] += v[t] * v[t];
+        }
+        if (pix < p.M) {
+          uint2 w;
+          w.x = pack_bf2(v[0], v[1]);
+          w.y = pack_bf2(v[2], v[3]);
+          *(uint2*)(p.out + (size_t)pix * p.K + ch) = w;
+        }
+      }
+      if (want_stats) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s4[t] += __shfl_xor(s4[t], o, 64);
+            q4[t] += __shfl_xor(q4[t], o, 64);
+          }
+        }
+        if (cl == 0) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            red[(wc * BM + chl + t) * 2 + 0] = s4[t];
+            red[(wc * BM + chl + t) * 2 + 1] = q4[t];
+          }
+        }
+      }
+    }
+    if (want_stats) {
+      __syncthreads();
+      if ((int)threadIdx.x < BM) {
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < WC; ++w) {
+          s += red[(w * BM + threadIdx.x) * 2 + 0];
+          q += red[(w * BM + threadIdx.x) * 2 + 1];
+        }
+        double* st = p.stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * p.K;
+        unsafeAtomicAdd(st + a0 + threadIdx.x, (double)s);
+        unsafeAtomicAdd(st + p.K + a0 + threadIdx.x, (double)q);
+      }
+    }
+  } else {  // DGRAD bf16 (+ residual)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ch = a0 + arow0 + i * 16 + rq;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int pix = b0 + bcol0 + j * 16 + cl;
+        if (pix < p.M) {
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          const size_t o = (size_t)pix * p.C + ch;
+          if (p.res) {
+            const uint2 rr = *(const uint2*)(p.res + o);
+            v[0] += bf_lo(rr.x); v[1] += bf_hi(rr.x); v[2] += bf_lo(rr.y); v[3] += bf_hi(rr.y);
+          }
+          uint2 w;
+          w.x = pack_bf2(v[0], v[1]);
+          w.y = pack_bf2(v[2], v[3]);
+          *(uint2*)(p.out + o) = w;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- split-K reduction (FWD / DGRAD)
+// out[m][n] = bf16( sum_s slab[s][m][n] (+ res[m][n]) ); optional per-channel stats of the
+// bf16-rounded output (same semantics as the non-split epilogue).
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int splits,
+                                                            int M, int Nc, u16* __restrict__ out,
+                                                            const u16* __restrict__ res,
+                                                            double* __restrict__ stats, int rows_per_block) {
+  __shared__ float red[256 * 16];
+  const int tpr = Nc >> 3;           // threads per row (8 channels each)
+  const int rpp = 256 / tpr;         // rows per pass
+  const int t = threadIdx.x;
+  const int g = t % tpr, rr = t / tpr;
+  const int m_begin = blockIdx.x * rows_per_block;
+  const int m_end = min(M, m_begin + rows_per_block);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const size_t plane = (size_t)M * Nc;
+  if (rr < rpp) {
+    for (int m = m_begin + rr; m < m_end; m += rpp) {
+      const size_t o = (size_t)m * Nc + g * 8;
+      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int sp = 0; sp < splits; ++sp) {
+        const f32x4 a = *(const f32x4*)(slab + sp * plane + o);
+        const f32x4 b = *(const f32x4*)(slab + sp * plane + o + 4);
+        v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
+        v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
+      }
+      if (res) {
+        float rv[8];
+        unpack8(*(const uint4*)(res + o), rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] += rv[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[k] = round_bf(v[k]);
+        s[k] += v[k];
+        q[k] += v[k] * v[k];
+      }
+      *(uint4*)(out + o) = pack8(v);
+    }
+  }
+  if (!stats) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[t * 16 + k] = s[k];
+    red[t * 16 + 8 + k] = q[k];
+  }
+  __syncthreads();
+  double* st = stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * Nc;
+  for (int c = t; c < Nc; c += 256) {
+    const int gg = c >> 3, k = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int r2 = 0; r2 < rpp; ++r2) {
+      a += red[(r2 * tpr + gg) * 16 + k];
+      b += red[(r2 * tpr + gg) * 16 + 8 + k];
+    }
+    unsafeAtomicAdd(st + c, (double)a);
+    unsafeAtomicAdd(st + Nc + c, (double)b);
+  }
+}
+
+// ---------------------------------------------------------------- wgrad split reduction
+// grad[k][c] (row stride ld_out, first ncols columns) = scale * sum_s slab[s][k][c] (row stride ld_in)
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K,
+                                                           int ld_in, int ncols, int ld_out, float scale,
+                                                           float* __restrict__ grad) {
+  const size_t plane = (size_t)K * ld_in;
+  if (ncols == ld_in && ld_out == ld_in && (ld_in & 3) == 0) {
+    const size_t n4 = plane >> 2;
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+      f32x4 a = *(const f32x4*)(slab + i * 4);
+      for (int sp = 1; sp < splits; ++sp) a += *(const f32x4*)(slab + sp * plane + i * 4);
+      *(f32x4*)(grad + i * 4) = a * scale;
+    }
+  } else {
+    const size_t n = (size_t)K * ncols;
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+      const int k = (int)(i / ncols), c = (int)(i % ncols);
+      float a = 0.f;
+      for (int sp = 0; sp < splits; ++sp) a += slab[sp * plane + (size_t)k * ld_in + c];
+      grad[(size_t)k * ld_out + c] = a * scale;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- host launchers
+static int fill_common(IGemmParams& p, const ConvShape& s) {
+  p.N = s.N; p.H = s.H; p.W = s.W; p.C = s.C; p.K = s.K; p.R = s.R; p.S = s.S;
+  p.stride = s.stride; p.pad = s.pad;
+  p.P = (s.H + 2 * s.pad - s.R) / s.stride + 1;
+  p.Q = (s.W + 2 * s.pad - s.S) / s.stride + 1;
+  p.RSC = s.R * s.S * s.C;
+  DTC_CHECK_ARG(s.C % 64 == 0 && s.K % 64 == 0, "conv: C (%d) and K (%d) must be multiples of 64", s.C, s.K);
+  DTC_CHECK_ARG(s.stride == 1 || s.stride == 2, "conv: stride must be 1 or 2");
+  DTC_CHECK_ARG(s.N > 0 && s.H > 0 && s.W > 0 && p.P > 0 && p.Q > 0, "conv: bad geometry");
+  return 0;
+}
+
+template <int MODE, int BM, int BN, int WR, int WC, bool SLAB>
+static int launch_igemm(IGemmParams& p, int tiles_b, int splits, hipStream_t st) {
+  dim3 grid(p.tiles_a * tiles_b, splits);
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB>), grid, dim3(256), 0, st, p);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+// Choose split-K so that the grid holds about `target` workgroups while each split keeps
+// at least `min_kt` reduction steps.
+static int pick_splits(int tiles, int num_kt, int target, int min_kt) {
+  int s = ceil_div(target, tiles);
+  s = std::min(s, std::max(1, num_kt / min_kt));
+  return std::max(1, s);
+}
+
+ConvPlan plan_conv(const ConvShape& s, int mode) {
+  ConvPlan pl{};
+  const int P = (s.H + 2 * s.pad - s.R) / s.stride + 1;
+  const int Q = (s.W + 2 * s.pad - s.S) / s.stride + 1;
+  if (mode == CONV_FWD || mode == CONV_DGRAD) {
+    const int M = (mode == CONV_FWD) ? s.N * P * Q : s.N * s.H * s.W;
+    const int A = (mode == CONV_FWD) ? s.K : s.C;
+    const int num_kt = s.R * s.S * ((mode == CONV_FWD) ? s.C : s.K) / 64;
+    pl.bm = (A == 64) ? 64 : 128;
+    pl.bn = (A == 64) ? 256 : 128;
+    const int tiles = (A / pl.bm) * ceil_div(M, pl.bn);
+    pl.splits = pick_splits(tiles, num_kt, 480, 8);
+    pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * M * A * 4 : 0;
+    pl.num_kt = num_kt;
+  } else {
+    const int M = s.N * P * Q;
+    const int num_kt = ceil_div(M, 64);
+    pl.bm = (s.C == 64 || s.K == 64) ? 64 : 128;
+    pl.bn = pl.bm;
+    const int tiles = (s.R * s.S * s.C / pl.bm) * (s.K / pl.bn);
+    pl.splits = pick_splits(tiles, num_kt, 512, 16);
+    pl.slab_bytes = (size_t)pl.splits * s.K * s.R * s.S * s.C * 4;
+    pl.num_kt = num_kt;
+  }
+  return pl;
+}
+
+int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
+             size_t slab_bytes, hipStream_t st) {
+  IGemmParams p{};
+  DTC_TRY(fill_common(p, s));
+  ConvPlan pl = plan_conv(s, CONV_FWD);
+  p.src0 = x; p.src1 = w; p.out = y; p.stats = stats;
+  p.M = s.N * p.P * p.Q;
+  p.fd_q = make_fastdiv(p.Q); p.fd_pq = make_fastdiv(p.P * p.Q); p.fd_cc = make_fastdiv(s.C / 64);
+  p.num_kt = pl.num_kt;
+  p.tiles_a = s.K / pl.bm;
+  const int tiles_b = ceil_div(p.M, pl.bn);
+  int splits = pl.splits;
+  if (splits > 1 && (slab == nullptr || slab_bytes < pl.slab_bytes)) splits = 1;
+  p.kt_per_split = ceil_div(p.num_kt, splits);
+  splits = ceil_div(p.num_kt, p.kt_per_split);
+  if (splits > 1) {
+    p.slab = slab;
+    if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_FWD, 64, 256, 1, 4, true>(p, tiles_b, splits, st)));
+    else DTC_TRY((launch_igemm<MODE_FWD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
+    return splitk_reduce(slab, splits, p.M, s.K, y, nullptr, stats, st);
+  }
+  if (pl.bm == 64) return launch_igemm<MODE_FWD, 64, 256, 1, 4, false>(p, tiles_b, 1, st);
+  return launch_igemm<MODE_FWD, 128, 128, 2, 2, false>(p, tiles_b, 1, st);
+}
+
+int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
+               size_t slab_bytes, hipStream_t st) {
+  IGemmParams p{};
+  DTC_TRY(fill_common(p, s));
+  ConvPlan pl = plan_conv(s, CONV_DGRAD);
+  p.src0 = dy; p.src1 = w; p.out = dx; p.res = res;
+  p.M = s.N * s.H * s.W;
+  p.fd_q = make_fastdiv(s.W); p.fd_pq = make_fastdiv(s.H * s.W); p.fd_cc = make_fastdiv(s.K / 64);
+  p.num_kt = pl.num_kt;
+  p.tiles_a = s.C / pl.bm;
+  const int tiles_b = ceil_div(p.M, pl.bn);
+  int splits = pl.splits;
+  if (splits > 1 && (slab == nullptr || slab_bytes < pl.slab_bytes)) splits = 1;
+  p.kt_per_split = ceil_div(p.num_kt, splits);
+  splits = ceil_div(p.num_kt, p.kt_per_split);
+  if (splits > 1) {
+    p.slab = slab;
+    if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 256, 1, 4, true>(p, tiles_b, splits, st)));
+    else DTC_TRY((launch_igemm<MODE_DGRAD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
+    return splitk_reduce(slab, splits, p.M, s.C, dx, res, nullptr, st);
+  }
+  if (pl.bm == 64) return launch_igemm<MODE_DGRAD, 64, 256, 1, 4, false>(p, tiles_b, 1, st);
+  return launch_igemm<MODE_DGRAD, 128, 128, 2, 2, false>(p, tiles_b, 1, st);
+}
+
+int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
+               float* slab, size_t slab_bytes, hipStream_t st) {
+  IGemmParams p{};
+  DTC_TRY(fill_common(p, s));
+  ConvPlan pl = plan_conv(s, CONV_WGRAD);
+  DTC_CHECK_ARG(slab != nullptr && slab_bytes >= (size_t)s.K * p.RSC * 4, "wgrad: slab workspace too small");
+  p.src0 = x; p.src1 = dy; p.slab = slab;
+  p.M = s.N * p.P * p.Q;
+  p.fd_q = make_fastdiv(p.Q); p.fd_pq = make_fastdiv(p.P * p.Q); p.fd_cc = make_fastdiv(1);
+  p.num_kt = pl.num_kt;
+  p.tiles_a = p.RSC / pl.bm;
+  const int tiles_b = s.K / pl.bn;
+  int splits = pl.splits;
+  while (splits > 1 && (size_t)splits * s.K * p.RSC * 4 > slab_bytes) --splits;
+  p.kt_per_split = ceil_div(p.num_kt, splits);
+  splits = ceil_div(p.num_kt, p.kt_per_split);
+  if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_WGRAD, 64, 64, 2, 2, true>(p, tiles_b, splits, st)));
+  else DTC_TRY((launch_igemm<MODE_WGRAD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
+  const int ncols = dw_cols > 0 ? dw_cols : p.RSC;
+  const int ldo = dw_ld > 0 ? dw_ld : p.RSC;
+  const size_t work = (size_t)s.K * ncols / 4 + 1;
+  const int blocks = (int)std::min<size_t>(2048, (work + 255) / 256);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo,
+                     scale, dw);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
+                  hipStream_t st) {
+  DTC_CHECK_ARG(Nc % 8 == 0 && Nc <= 2048, "splitk_reduce: channels %d", Nc);
+  const int tpr = Nc / 8;
+  const int rpp = 256 / tpr;
+  int rows_per_block = std::max(rpp, 64);
+  rows_per_block = ((rows_per_block + rpp - 1) / rpp) * rpp;
+  const int blocks = ceil_div(M, rows_per_block);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, splits, M, Nc, out, res, stats,
+                     rows_per_block);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace dtc

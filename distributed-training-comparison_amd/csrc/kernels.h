@@ -1,0 +1,94 @@
+// Internal host-side launcher declarations (C++). The public C ABI is include/dtc.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <algorithm>
+#include "common.h"
+
+namespace dtc {
+
+// ------------------------------------------------------------------ convolution
+struct ConvShape {
+  int N, H, W, C;  // input NHWC
+  int K, R, S;     // filters KRSC
+  int stride, pad;
+};
+enum { CONV_FWD = 0, CONV_DGRAD = 1, CONV_WGRAD = 2 };
+struct ConvPlan {
+  int bm, bn, splits, num_kt;
+  size_t slab_bytes;  // fp32 workspace the plan wants (0 = none)
+};
+ConvPlan plan_conv(const ConvShape& s, int mode);
+
+// y = conv(x, w) (bf16 NHWC out); optional BN statistics of the bf16 output into
+// stats[SLOTS][2][K] (sum, sum of squares; fp64, accumulated).
+int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
+             size_t slab_bytes, hipStream_t st);
+// dx = conv_transpose(dy, w) (+ res), bf16 NHWC
+int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
+               size_t slab_bytes, hipStream_t st);
+// dw[k][0:dw_cols] (row stride dw_ld) = scale * sum_pixels dy (x) im2col(x); fp32
+int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
+               float* slab, size_t slab_bytes, hipStream_t st);
+int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
+                  hipStream_t st);
+
+// ------------------------------------------------------------------ batch norm (NHWC, C channels, M pixels)
+// forward finalize: mean/invstd/scale/shift from stats; running-stat update; stats re-zeroed.
+int bn_fwd_finalize(double* stats, int C, int64_t count, const float* gamma, const float* beta,
+                    float* running_mean, float* running_var, int64_t* num_batches, float momentum, float eps,
+                    float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
+// eval mode: scale/shift from running statistics (mean/invstd also written for reference)
+int bn_eval_coef(int C, const float* gamma, const float* beta, const float* running_mean, const float* running_var,
+                 float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
+// y = relu(x*scale + shift)
+int bn_apply_relu(const u16* x, const float* scale, const float* shift, u16* y, int64_t M, int C, hipStream_t st);
+// y = relu(x*scale + shift + res)            (identity shortcut)
+int bn_apply_add_relu(const u16* x, const float* scale, const float* shift, const u16* res, u16* y, int64_t M,
+                      int C, hipStream_t st);
+// y = relu(x*scale + shift + x2*scale2 + shift2)   (projection shortcut: two BNs)
+int bn_apply_dual_relu(const u16* x, const float* scale, const float* shift, const u16* x2, const float* scale2,
+                       const float* shift2, u16* y, int64_t M, int C, hipStream_t st);
+// y = x*scale + shift (no activation; eval helpers / tests)
+int bn_apply(const u16* x, const float* scale, const float* shift, u16* y, int64_t M, int C, hipStream_t st);
+
+// backward: dz = dy * [y > 0] (mask optional); accumulates sum(dz), sum(dz*xhat1) [, sum(dz*xhat2)]
+int bn_bwd_reduce(const u16* dy, const u16* ymask, const u16* x1, const float* mean1, const float* invstd1,
+                  double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, u16* dz,
+                  int64_t M, int C, hipStream_t st);
+// dgamma/dbeta (scaled by gscale) into the flat grad buffer; apply coefficients coef[3][C]; acc re-zeroed.
+int bn_bwd_finalize(double* acc, int C, int64_t count, const float* gamma, const float* mean,
+                    const float* invstd, float gscale, float* dgamma, float* dbeta, float* coef, hipStream_t st);
+// dx1 = A1*dz + B1*x1 + C1 [; dx2 = A2*dz + B2*x2 + C2]
+int bn_bwd_apply(const u16* dz, const u16* x1, const float* coef1, u16* dx1, const u16* x2, const float* coef2,
+                 u16* dx2, int64_t M, int C, hipStream_t st);
+
+// ------------------------------------------------------------------ stem / head / loss
+// x fp32 NCHW [N][3][H][W] -> im2col bf16 [N*H*W][64] (3x3 pad 1 taps, (r,s,c) order, zero padded)
+int stem_im2col(const float* x, u16* cols, int N, int H, int W, hipStream_t st);
+// w bf16 [64][27] -> [64][64] zero padded
+int stem_pack_weight(const u16* w27, u16* w64, int K, hipStream_t st);
+// feat[n][c] = bf16round(mean_hw act); logits[n][j] = feat . W[j] + b[j]
+int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
+             float* logits, hipStream_t st);
+// mean cross entropy; lse per row
+int xent_fwd(const float* logits, const int64_t* labels, int N, int ncls, float* loss, float* lse,
+             hipStream_t st);
+// dlogits = (softmax - onehot) * (*gscale) / N
+int xent_bwd(const float* logits, const int64_t* labels, const float* lse, const float* gscale, int N, int ncls,
+             float* dlogits, hipStream_t st);
+// dW = scale*dlogits^T feat ; db = scale*sum dlogits ; dact[n][hw][c] = (dlogits . W)[c] / HW
+int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int HW, int C, int ncls, float scale,
+             float* dw, float* db, u16* dact, hipStream_t st);
+
+// ------------------------------------------------------------------ optimizer / amp / casts
+// Nesterov SGD over a flat buffer (torch.optim.SGD semantics, dampening 0).
+int sgd_nesterov(float* p, const float* g, float* mom, u16* p_bf16, int64_t n, float lr, float wd, float mu,
+                 const float* inv_scale, const int* found_inf, hipStream_t st);
+int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st);
+int amp_check_finite(const float* g, int64_t n, int* found_inf, hipStream_t st);
+int amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, int* found_inf, float growth,
+                     float backoff, int interval, hipStream_t st);
+
+}  // namespace dtc

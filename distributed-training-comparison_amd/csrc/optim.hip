@@ -1,0 +1,108 @@
+// Fused flat-bucket SGD (Nesterov momentum) and the GradScaler device-side kernels.
+//
+// Replaces `optim.SGD(params, lr, weight_decay, momentum=0.9, nesterov=True).step()`
+// (reference src/ddp/trainer.py:92-98, 158/165) and the AMP helpers behind
+// `GradScaler.step/update` (main.py:25, trainer.py:157-159). torch.optim.SGD, dampening 0:
+//     d = g + wd*p ; buf = mu*buf + d   (first step: buf = d) ; d = d + mu*buf ; p -= lr*d
+// The first-step special case needs no flag: buffers start at zero and mu*0 + d == d exactly.
+// GradScaler semantics (torch._amp_update_scale_): a step whose gradients hold inf/NaN is
+// skipped entirely; scale *= backoff on overflow, *= growth after `interval` clean steps.
+// The step also refreshes the bf16 shadow of every parameter (the GEMM operand layout).
+#include "common.h"
+#include "kernels.h"
+
+namespace dtc {
+
+__global__ void __launch_bounds__(256) sgd_nesterov_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                          float* __restrict__ m, u16* __restrict__ pb, int64_t n4,
+                                                          float lr, float wd, float mu,
+                                                          const float* __restrict__ inv_scale,
+                                                          const int* __restrict__ found_inf) {
+  if (found_inf && *found_inf) return;  // GradScaler: skip the whole step
+  const float is = inv_scale ? *inv_scale : 1.f;
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    f32x4 pv = *(const f32x4*)(p + i * 4);
+    const f32x4 gv = *(const f32x4*)(g + i * 4);
+    f32x4 mv = *(const f32x4*)(m + i * 4);
+    f32x4 d = gv * is + pv * wd;
+    mv = mv * mu + d;
+    d = d + mv * mu;
+    pv = pv - d * lr;
+    *(f32x4*)(p + i * 4) = pv;
+    *(f32x4*)(m + i * 4) = mv;
+    uint2 w;
+    w.x = pack_bf2(pv[0], pv[1]);
+    w.y = pack_bf2(pv[2], pv[3]);
+    *(uint2*)(pb + i * 4) = w;
+  }
+}
+
+int sgd_nesterov(float* p, const float* g, float* mom, u16* p_bf16, int64_t n, float lr, float wd, float mu,
+                 const float* inv_scale, const int* found_inf, hipStream_t st) {
+  DTC_CHECK_ARG(p && g && mom && p_bf16 && n > 0 && (n % 4) == 0, "sgd_nesterov: bad args (n=%lld)", (long long)n);
+  const int64_t n4 = n / 4;
+  const int blocks = (int)std::min<int64_t>(2048, (n4 + 255) / 256);
+  hipLaunchKernelGGL(sgd_nesterov_kernel, dim3(blocks), dim3(256), 0, st, p, g, mom, p_bf16, n4, lr, wd, mu, inv_scale,
+                     found_inf);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ s, u16* __restrict__ d, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) d[i] = f2bf(s[i]);
+}
+
+int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st) {
+  DTC_CHECK_ARG(src && dst && n > 0, "cast_f32_bf16: bad args");
+  const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(blocks), dim3(256), 0, st, src, dst, n);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void amp_check_finite_kernel(const float* __restrict__ g, int64_t n, int* __restrict__ found) {
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    bad |= !isfinite(g[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) *found = 1;
+}
+
+int amp_check_finite(const float* g, int64_t n, int* found_inf, hipStream_t st) {
+  DTC_CHECK_ARG(g && found_inf && n > 0, "amp_check_finite: bad args");
+  const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(amp_check_finite_kernel, dim3(blocks), dim3(256), 0, st, g, n, found_inf);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void amp_update_scale_kernel(float* scale, float* inv_scale, int* tracker, int* found, float growth,
+                                        float backoff, int interval) {
+  float s = *scale;
+  if (*found) {
+    s *= backoff;
+    *tracker = 0;
+  } else {
+    const int k = *tracker + 1;
+    if (k >= interval) {
+      const float ns = s * growth;
+      if (isfinite(ns)) s = ns;
+      *tracker = 0;
+    } else {
+      *tracker = k;
+    }
+  }
+  *scale = s;
+  if (inv_scale) *inv_scale = 1.f / s;
+  *found = 0;
+}
+
+int amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, int* found_inf, float growth, float backoff,
+                     int interval, hipStream_t st) {
+  DTC_CHECK_ARG(scale && growth_tracker && found_inf && interval > 0, "amp_update_scale: bad args");
+  hipLaunchKernelGGL(amp_update_scale_kernel, dim3(1), dim3(1), 0, st, scale, inv_scale, growth_tracker, found_inf,
+                     growth, backoff, interval);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace dtc

@@ -1,0 +1,510 @@
+// ResNet-18 (CIFAR variant) training-step executor.
+//
+// Mirrors the module structure of the reference (src/ddp/net.py:13-45 BasicBlock,
+// net.py:86-116 ResNet, net.py:119-120 ResNet18) and runs its forward and backward as two
+// calls that enqueue hand-written kernels on one stream:
+//
+//   forward : stem im2col -> conv(+BN stats) -> BN finalize -> BN+ReLU -> 8 BasicBlocks
+//             [conv1 -> bn1+relu -> conv2 -> (shortcut conv) -> bn2 (+bn_sc) + add + relu]
+//             -> global avg pool + Linear
+//   backward: head -> blocks in reverse [BN2 reduce/finalize/apply -> conv2 wgrad/dgrad ->
+//             BN1 ... -> conv1 wgrad/dgrad (+shortcut) with the residual gradient fused into
+//             the dgrad epilogue] -> stem BN -> stem wgrad, issuing each gradient bucket's
+//             RCCL all-reduce on the communicator's side stream as soon as it is complete.
+//
+// Parameter memory: one flat fp32 buffer in REVERSE registration order, 64-element aligned.
+// Backward visits layers from the head to the stem, i.e. it finishes gradients in increasing
+// address order, so every DDP bucket is a contiguous prefix-extension of the buffer.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "comm.h"
+#include "kernels.h"
+
+namespace dtc {
+
+static inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+struct ParamEntry {
+  std::string name;
+  int64_t offset = 0, numel = 0;
+  int ndim = 0;
+  int64_t shape[4] = {0, 0, 0, 0};
+  int64_t stride[4] = {0, 0, 0, 0};
+};
+
+struct ConvL {
+  ConvShape s{};
+  int P = 0, Q = 0;
+  int pidx = -1;  // param index of the weight
+};
+
+struct BNL {
+  std::string prefix;
+  int C = 0;
+  int gidx = -1, bidx = -1;  // param indices of weight (gamma) and bias (beta)
+  int64_t rm_off = 0, rv_off = 0;
+  int nbt = 0;
+  size_t stats = 0, acc = 0, mean = 0, invstd = 0, scale = 0, shift = 0, coef = 0;  // workspace byte offsets
+};
+
+struct BlockL {
+  ConvL c1, c2, sc;
+  BNL b1, b2, bsc;
+  bool proj = false;
+  int Cin = 0, Cout = 0, Hin = 0, Win = 0, Hout = 0, Wout = 0;
+  size_t C1 = 0, A1 = 0, C2 = 0, S = 0, OUT = 0;  // activation buffers (workspace byte offsets)
+  int64_t grad_hi = 0;  // end of this block's flat region: after its backward, [0, grad_hi) is complete
+};
+
+struct Net {
+  int B = 0, H = 0, W = 0, ncls = 100;
+  std::vector<ParamEntry> params;
+  int64_t flat_numel = 0;
+  int64_t bufs_numel = 0;
+  ConvL stem;
+  BNL bn0;
+  std::vector<BlockL> blocks;
+  std::vector<BNL*> bns;  // registration order
+  int fc_w = -1, fc_b = -1;
+  // workspace
+  size_t ws_bytes = 0;
+  size_t X0 = 0, WSTEM = 0, C0 = 0, A0 = 0, FEAT = 0, G[6] = {0, 0, 0, 0, 0, 0}, SLAB = 0;
+  size_t slab_bytes = 0;
+  size_t stats_lo = 0, stats_hi = 0;  // region that must start zeroed
+  // buckets: [offset, numel) in flat elements, and the block index after whose backward it fires
+  std::vector<int64_t> bucket_off, bucket_len;
+  std::vector<int> bucket_after_block;  // -1 = after the stem (last)
+  // bound memory
+  char* ws = nullptr;
+  float* p = nullptr;
+  float* g = nullptr;
+  u16* pb = nullptr;
+  float* bufs = nullptr;
+  int64_t* nbt = nullptr;
+
+  template <typename T>
+  T* at(size_t off) const { return (T*)(ws + off); }
+  const u16* wbf(int pidx) const { return pb + params[pidx].offset; }
+  float* pf(int pidx) const { return p + params[pidx].offset; }
+  float* gf(int pidx) const { return g + params[pidx].offset; }
+};
+
+// ------------------------------------------------------------------ construction
+static int add_param(Net& n, const std::string& name, std::vector<int64_t> shape, bool conv_krsc) {
+  ParamEntry e;
+  e.name = name;
+  e.ndim = (int)shape.size();
+  e.numel = 1;
+  for (int i = 0; i < e.ndim; ++i) {
+    e.shape[i] = shape[i];
+    e.numel *= shape[i];
+  }
+  if (conv_krsc) {  // logical [K][C][R][S] stored as K R S C
+    const int64_t K = shape[0], C = shape[1], R = shape[2], S = shape[3];
+    (void)K;
+    e.stride[0] = R * S * C;
+    e.stride[1] = 1;
+    e.stride[2] = S * C;
+    e.stride[3] = C;
+  } else {
+    int64_t s = 1;
+    for (int i = e.ndim - 1; i >= 0; --i) {
+      e.stride[i] = s;
+      s *= shape[i];
+    }
+  }
+  n.params.push_back(e);
+  return (int)n.params.size() - 1;
+}
+
+static void make_conv(Net& n, ConvL& c, const std::string& name, int N, int H, int W, int Cin, int Cout, int k,
+                      int stride) {
+  c.s = ConvShape{N, H, W, Cin, Cout, k, k, stride, k == 3 ? 1 : 0};
+  c.P = (H + 2 * c.s.pad - k) / stride + 1;
+  c.Q = (W + 2 * c.s.pad - k) / stride + 1;
+  c.pidx = add_param(n, name, {Cout, Cin, k, k}, true);
+}
+
+static void make_bn(Net& n, BNL& b, const std::string& prefix, int C) {
+  b.prefix = prefix;
+  b.C = C;
+  b.gidx = add_param(n, prefix + ".weight", {C}, false);
+  b.bidx = add_param(n, prefix + ".bias", {C}, false);
+}
+
+static int build(Net& n) {
+  const int B = n.B;
+  // stem: registered as conv1.weight [64,3,3,3], bn1.{weight,bias}   (net.py:91-92)
+  n.stem.s = ConvShape{B, n.H, n.W, 64, 64, 1, 1, 1, 0};  // GEMM over the 64-column im2col image
+  n.stem.P = n.H;
+  n.stem.Q = n.W;
+  n.stem.pidx = add_param(n, "conv1.weight", {64, 3, 3, 3}, true);
+  make_bn(n, n.bn0, "bn1", 64);
+  // layers (net.py:93-96, _make_layer net.py:99-105)
+  int in_planes = 64, H = n.H, W = n.W;
+  const int planes[4] = {64, 128, 256, 512};
+  const int strides[4] = {1, 2, 2, 2};
+  for (int L = 0; L < 4; ++L) {
+    for (int bi = 0; bi < 2; ++bi) {
+      const int stride = bi == 0 ? strides[L] : 1;
+      BlockL blk;
+      const std::string pre = "layer" + std::to_string(L + 1) + "." + std::to_string(bi);
+      blk.Cin = in_planes;
+      blk.Cout = planes[L];
+      blk.Hin = H;
+      blk.Win = W;
+      make_conv(n, blk.c1, pre + ".conv1.weight", B, H, W, in_planes, planes[L], 3, stride);
+      make_bn(n, blk.b1, pre + ".bn1", planes[L]);
+      blk.Hout = blk.c1.P;
+      blk.Wout = blk.c1.Q;
+      make_conv(n, blk.c2, pre + ".conv2.weight", B, blk.Hout, blk.Wout, planes[L], planes[L], 3, 1);
+      make_bn(n, blk.b2, pre + ".bn2", planes[L]);
+      blk.proj = (stride != 1 || in_planes != planes[L]);  // net.py:28
+      if (blk.proj) {
+        make_conv(n, blk.sc, pre + ".shortcut.0.weight", B, H, W, in_planes, planes[L], 1, stride);
+        make_bn(n, blk.bsc, pre + ".shortcut.1", planes[L]);
+      }
+      n.blocks.push_back(blk);
+      in_planes = planes[L];
+      H = blk.Hout;
+      W = blk.Wout;
+    }
+  }
+  n.fc_w = add_param(n, "linear.weight", {n.ncls, 512}, false);  // net.py:97
+  n.fc_b = add_param(n, "linear.bias", {n.ncls}, false);
+  if (H < 1 || W < 1) return set_error(DTC_EINVAL, "rn18: input %dx%d too small", n.H, n.W);
+
+  // flat layout: reverse registration order, 64-element alignment
+  int64_t off = 0;
+  for (int i = (int)n.params.size() - 1; i >= 0; --i) {
+    n.params[i].offset = off;
+    off = align_up(off + n.params[i].numel, 64);
+  }
+  n.flat_numel = off;
+
+  // BN registry in registration order and buffer layout
+  n.bns.push_back(&n.bn0);
+  for (auto& b : n.blocks) {
+    n.bns.push_back(&b.b1);
+    n.bns.push_back(&b.b2);
+    if (b.proj) n.bns.push_back(&b.bsc);
+  }
+  int64_t boff = 0;
+  for (size_t i = 0; i < n.bns.size(); ++i) {
+    BNL* b = n.bns[i];
+    b->rm_off = boff;
+    boff = align_up(boff + b->C, 64);
+    b->rv_off = boff;
+    boff = align_up(boff + b->C, 64);
+    b->nbt = (int)i;
+  }
+  n.bufs_numel = boff;
+  for (auto& b : n.blocks)  // conv1.weight is the block's first-registered, hence highest, param
+    b.grad_hi = align_up(n.params[b.c1.pidx].offset + n.params[b.c1.pidx].numel, 64);
+  return 0;
+}
+
+static void plan_workspace(Net& n, float bucket_cap_mb) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off = (size_t)align_up((int64_t)(off + bytes), 256);
+    return o;
+  };
+  const int64_t B = n.B;
+  const int64_t M0 = B * n.H * n.W;
+  n.X0 = take(M0 * 64 * 2);
+  n.WSTEM = take(64 * 64 * 2);
+  n.C0 = take(M0 * 64 * 2);
+  n.A0 = take(M0 * 64 * 2);
+  int64_t gmax = M0 * 64;
+  for (auto& b : n.blocks) {
+    const int64_t M = B * b.Hout * b.Wout;
+    const size_t bytes = M * b.Cout * 2;
+    b.C1 = take(bytes);
+    b.A1 = take(bytes);
+    b.C2 = take(bytes);
+    if (b.proj) b.S = take(bytes);
+    b.OUT = take(bytes);
+    gmax = std::max<int64_t>(gmax, std::max<int64_t>(M * b.Cout, B * b.Hin * b.Win * b.Cin));
+  }
+  const int64_t HWl = n.blocks.back().Hout * n.blocks.back().Wout;
+  (void)HWl;
+  n.FEAT = take(B * 512 * 4);
+  for (int i = 0; i < 6; ++i) n.G[i] = take(gmax * 2);
+  // BN per-layer state
+  n.stats_lo = off;
+  for (BNL* b : n.bns) {
+    b->stats = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
+    b->acc = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
+  }
+  n.stats_hi = off;
+  for (BNL* b : n.bns) {
+    b->mean = take(b->C * 4);
+    b->invstd = take(b->C * 4);
+    b->scale = take(b->C * 4);
+    b->shift = take(b->C * 4);
+    b->coef = take(3 * b->C * 4);
+  }
+  // split-K slabs: max over every conv pass
+  size_t slab = (size_t)64 * 64 * 4;
+  auto consider = [&](const ConvShape& s) {
+    for (int m = 0; m < 3; ++m) slab = std::max(slab, plan_conv(s, m).slab_bytes);
+  };
+  consider(n.stem.s);
+  for (auto& b : n.blocks) {
+    consider(b.c1.s);
+    consider(b.c2.s);
+    if (b.proj) consider(b.sc.s);
+  }
+  n.slab_bytes = slab;
+  n.SLAB = take(slab);
+  n.ws_bytes = off;
+
+  // gradient buckets at block granularity in backward order (head + layer4.1 first); a bucket
+  // closes once it holds >= bucket_cap_mb, the rest (down to the stem) forms the last bucket
+  const int64_t cap = (int64_t)(bucket_cap_mb * 1024.0 * 1024.0 / 4.0);
+  int64_t start = 0;
+  for (int bi = (int)n.blocks.size() - 1; bi >= 0 && cap > 0; --bi) {
+    const int64_t hi = n.blocks[bi].grad_hi;
+    if (hi - start >= cap) {
+      n.bucket_off.push_back(start);
+      n.bucket_len.push_back(hi - start);
+      n.bucket_after_block.push_back(bi);
+      start = hi;
+    }
+  }
+  n.bucket_off.push_back(start);
+  n.bucket_len.push_back(n.flat_numel - start);
+  n.bucket_after_block.push_back(-1);
+}
+
+// ------------------------------------------------------------------ forward / backward
+static int bn_finalize_fwd(Net& n, BNL& b, int64_t count, bool train, hipStream_t st) {
+  if (train) {
+    return bn_fwd_finalize(n.at<double>(b.stats), b.C, count, n.pf(b.gidx), n.pf(b.bidx), n.bufs + b.rm_off,
+                           n.bufs + b.rv_off, n.nbt ? n.nbt + b.nbt : nullptr, 0.1f, 1e-5f, n.at<float>(b.mean),
+                           n.at<float>(b.invstd), n.at<float>(b.scale), n.at<float>(b.shift), st);
+  }
+  return bn_eval_coef(b.C, n.pf(b.gidx), n.pf(b.bidx), n.bufs + b.rm_off, n.bufs + b.rv_off, 1e-5f,
+                      n.at<float>(b.mean), n.at<float>(b.invstd), n.at<float>(b.scale), n.at<float>(b.shift), st);
+}
+
+static int forward(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
+  const int64_t M0 = (int64_t)n.B * n.H * n.W;
+  u16* X0 = n.at<u16>(n.X0);
+  DTC_TRY(stem_pack_weight(n.wbf(n.stem.pidx), n.at<u16>(n.WSTEM), 64, st));
+  DTC_TRY(stem_im2col(x, X0, n.B, n.H, n.W, st));
+  DTC_TRY(conv_fwd(n.stem.s, X0, n.at<u16>(n.WSTEM), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
+                   n.at<float>(n.SLAB), n.slab_bytes, st));
+  DTC_TRY(bn_finalize_fwd(n, n.bn0, M0, train, st));
+  DTC_TRY(bn_apply_relu(n.at<u16>(n.C0), n.at<float>(n.bn0.scale), n.at<float>(n.bn0.shift), n.at<u16>(n.A0), M0, 64,
+                        st));
+  const u16* in = n.at<u16>(n.A0);
+  for (auto& b : n.blocks) {
+    const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
+    float* slab = n.at<float>(n.SLAB);
+    DTC_TRY(conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
+                     n.slab_bytes, st));
+    DTC_TRY(bn_finalize_fwd(n, b.b1, M, train, st));
+    DTC_TRY(bn_apply_relu(n.at<u16>(b.C1), n.at<float>(b.b1.scale), n.at<float>(b.b1.shift), n.at<u16>(b.A1), M,
+                          b.Cout, st));
+    DTC_TRY(conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
+                     train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st));
+    DTC_TRY(bn_finalize_fwd(n, b.b2, M, train, st));
+    if (b.proj) {
+      DTC_TRY(conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr,
+                       slab, n.slab_bytes, st));
+      DTC_TRY(bn_finalize_fwd(n, b.bsc, M, train, st));
+      DTC_TRY(bn_apply_dual_relu(n.at<u16>(b.C2), n.at<float>(b.b2.scale), n.at<float>(b.b2.shift), n.at<u16>(b.S),
+                                 n.at<float>(b.bsc.scale), n.at<float>(b.bsc.shift), n.at<u16>(b.OUT), M, b.Cout, st));
+    } else {
+      DTC_TRY(bn_apply_add_relu(n.at<u16>(b.C2), n.at<float>(b.b2.scale), n.at<float>(b.b2.shift), in,
+                                n.at<u16>(b.OUT), M, b.Cout, st));
+    }
+    in = n.at<u16>(b.OUT);
+  }
+  const BlockL& last = n.blocks.back();
+  return head_fwd(in, n.B, last.Hout * last.Wout, 512, n.wbf(n.fc_w), n.pf(n.fc_b), n.ncls, n.at<float>(n.FEAT),
+                  logits, st);
+}
+
+static int maybe_bucket(Net& n, int after_block, Comm* comm, hipStream_t st) {
+  if (!comm) return 0;
+  for (size_t i = 0; i < n.bucket_off.size(); ++i) {
+    if (n.bucket_after_block[i] == after_block)
+      DTC_TRY(comm_allreduce_async(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st));
+  }
+  return 0;
+}
+
+static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st) {
+  u16* G[6];
+  for (int i = 0; i < 6; ++i) G[i] = n.at<u16>(n.G[i]);
+  float* slab = n.at<float>(n.SLAB);
+  const BlockL& last = n.blocks.back();
+  DTC_TRY(head_bwd(dlogits, n.at<float>(n.FEAT), n.wbf(n.fc_w), n.B, last.Hout * last.Wout, 512, n.ncls, gs,
+                   n.gf(n.fc_w), n.gf(n.fc_b), G[0], st));
+  for (int bi = (int)n.blocks.size() - 1; bi >= 0; --bi) {
+    BlockL& b = n.blocks[bi];
+    const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
+    const u16* in = bi > 0 ? n.at<u16>(n.blocks[bi - 1].OUT) : n.at<u16>(n.A0);
+    // out = relu(bn2(c2) + shortcut): dz = dy * [out > 0]
+    DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(b.OUT), n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
+                          n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
+                          b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
+                          b.proj ? n.at<double>(b.bsc.acc) : nullptr, G[1], M, b.Cout, st));
+    DTC_TRY(bn_bwd_finalize(n.at<double>(b.b2.acc), b.Cout, M, n.pf(b.b2.gidx), n.at<float>(b.b2.mean),
+                            n.at<float>(b.b2.invstd), gs, n.gf(b.b2.gidx), n.gf(b.b2.bidx), n.at<float>(b.b2.coef),
+                            st));
+    if (b.proj)
+      DTC_TRY(bn_bwd_finalize(n.at<double>(b.bsc.acc), b.Cout, M, n.pf(b.bsc.gidx), n.at<float>(b.bsc.mean),
+                              n.at<float>(b.bsc.invstd), gs, n.gf(b.bsc.gidx), n.gf(b.bsc.bidx),
+                              n.at<float>(b.bsc.coef), st));
+    DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(b.C2), n.at<float>(b.b2.coef), G[2], b.proj ? n.at<u16>(b.S) : nullptr,
+                         b.proj ? n.at<float>(b.bsc.coef) : nullptr, b.proj ? G[3] : nullptr, M, b.Cout, st));
+    // conv2: dW2 and da1
+    DTC_TRY(conv_wgrad(b.c2.s, n.at<u16>(b.A1), G[2], n.gf(b.c2.pidx), 0, 0, gs, slab, n.slab_bytes, st));
+    DTC_TRY(conv_dgrad(b.c2.s, G[2], n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st));
+    // a1 = relu(bn1(c1))
+    DTC_TRY(bn_bwd_reduce(G[4], n.at<u16>(b.A1), n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
+                          n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, G[4], M, b.Cout, st));
+    DTC_TRY(bn_bwd_finalize(n.at<double>(b.b1.acc), b.Cout, M, n.pf(b.b1.gidx), n.at<float>(b.b1.mean),
+                            n.at<float>(b.b1.invstd), gs, n.gf(b.b1.gidx), n.gf(b.b1.bidx), n.at<float>(b.b1.coef),
+                            st));
+    DTC_TRY(bn_bwd_apply(G[4], n.at<u16>(b.C1), n.at<float>(b.b1.coef), G[2], nullptr, nullptr, nullptr, M, b.Cout,
+                         st));
+    // conv1 (+ shortcut): weight grads, then the block-input gradient with the residual fused
+    DTC_TRY(conv_wgrad(b.c1.s, in, G[2], n.gf(b.c1.pidx), 0, 0, gs, slab, n.slab_bytes, st));
+    if (b.proj) {
+      DTC_TRY(conv_wgrad(b.sc.s, in, G[3], n.gf(b.sc.pidx), 0, 0, gs, slab, n.slab_bytes, st));
+      DTC_TRY(conv_dgrad(b.sc.s, G[3], n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st));
+      DTC_TRY(conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st));
+    } else {
+      DTC_TRY(conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[1], slab, n.slab_bytes, st));
+    }
+    DTC_TRY(maybe_bucket(n, bi, comm, st));
+  }
+  // stem: a0 = relu(bn1(conv1(x)))
+  const int64_t M0 = (int64_t)n.B * n.H * n.W;
+  DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(n.A0), n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
+                        n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, G[1], M0, 64, st));
+  DTC_TRY(bn_bwd_finalize(n.at<double>(n.bn0.acc), 64, M0, n.pf(n.bn0.gidx), n.at<float>(n.bn0.mean),
+                          n.at<float>(n.bn0.invstd), gs, n.gf(n.bn0.gidx), n.gf(n.bn0.bidx), n.at<float>(n.bn0.coef),
+                          st));
+  DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(n.C0), n.at<float>(n.bn0.coef), G[2], nullptr, nullptr, nullptr, M0, 64, st));
+  DTC_TRY(conv_wgrad(n.stem.s, n.at<u16>(n.X0), G[2], n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st));
+  DTC_TRY(maybe_bucket(n, -1, comm, st));
+  if (comm) DTC_TRY(comm_join(comm, st));
+  return 0;
+}
+
+}  // namespace dtc
+
+// ------------------------------------------------------------------ C ABI (executor part)
+#include "../../include/dtc.h"
+
+struct dtc_net {
+  dtc::Net n;
+};
+
+using namespace dtc;
+
+extern "C" {
+
+int dtc_rn18_create(dtc_net** out, int batch, int height, int width, int num_classes, float bucket_cap_mb) {
+  DTC_CHECK_ARG(out != nullptr, "dtc_rn18_create: null out");
+  DTC_CHECK_ARG(batch > 0 && height >= 8 && width >= 8 && num_classes > 0, "dtc_rn18_create: bad shape");
+  DTC_CHECK_ARG((int64_t)batch * height * width * 64 < (1ll << 31), "dtc_rn18_create: activation too large");
+  dtc_net* h = new dtc_net();
+  h->n.B = batch;
+  h->n.H = height;
+  h->n.W = width;
+  h->n.ncls = num_classes;
+  int r = build(h->n);
+  if (r) {
+    delete h;
+    return r;
+  }
+  plan_workspace(h->n, bucket_cap_mb);
+  *out = h;
+  return 0;
+}
+
+int dtc_rn18_destroy(dtc_net* net) {
+  delete net;
+  return 0;
+}
+
+int dtc_rn18_num_params(const dtc_net* net) { return net ? (int)net->n.params.size() : DTC_EINVAL; }
+
+int dtc_rn18_param_info(const dtc_net* net, int idx, const char** name, int64_t* offset, int64_t* numel, int* ndim,
+                        int64_t* shape4, int64_t* stride4) {
+  DTC_CHECK_ARG(net && idx >= 0 && idx < (int)net->n.params.size(), "dtc_rn18_param_info: bad index");
+  const ParamEntry& e = net->n.params[idx];
+  if (name) *name = e.name.c_str();
+  if (offset) *offset = e.offset;
+  if (numel) *numel = e.numel;
+  if (ndim) *ndim = e.ndim;
+  for (int i = 0; i < 4; ++i) {
+    if (shape4) shape4[i] = e.shape[i];
+    if (stride4) stride4[i] = e.stride[i];
+  }
+  return 0;
+}
+
+int64_t dtc_rn18_flat_numel(const dtc_net* net) { return net ? net->n.flat_numel : DTC_EINVAL; }
+int dtc_rn18_num_bn(const dtc_net* net) { return net ? (int)net->n.bns.size() : DTC_EINVAL; }
+
+int dtc_rn18_bn_info(const dtc_net* net, int idx, const char** prefix, int* channels, int64_t* mean_offset,
+                     int64_t* var_offset) {
+  DTC_CHECK_ARG(net && idx >= 0 && idx < (int)net->n.bns.size(), "dtc_rn18_bn_info: bad index");
+  const BNL* b = net->n.bns[idx];
+  if (prefix) *prefix = b->prefix.c_str();
+  if (channels) *channels = b->C;
+  if (mean_offset) *mean_offset = b->rm_off;
+  if (var_offset) *var_offset = b->rv_off;
+  return 0;
+}
+
+int64_t dtc_rn18_bufs_numel(const dtc_net* net) { return net ? net->n.bufs_numel : DTC_EINVAL; }
+size_t dtc_rn18_workspace_bytes(const dtc_net* net) { return net ? net->n.ws_bytes : 0; }
+int dtc_rn18_num_buckets(const dtc_net* net) { return net ? (int)net->n.bucket_off.size() : DTC_EINVAL; }
+
+int dtc_rn18_bucket_info(const dtc_net* net, int idx, int64_t* offset, int64_t* numel) {
+  DTC_CHECK_ARG(net && idx >= 0 && idx < (int)net->n.bucket_off.size(), "dtc_rn18_bucket_info: bad index");
+  if (offset) *offset = net->n.bucket_off[idx];
+  if (numel) *numel = net->n.bucket_len[idx];
+  return 0;
+}
+
+int dtc_rn18_bind(dtc_net* net, void* workspace, float* params, float* grads, uint16_t* params_bf16, float* bufs,
+                  int64_t* num_batches_tracked, void* stream) {
+  DTC_CHECK_ARG(net && workspace && params && grads && params_bf16 && bufs, "dtc_rn18_bind: null pointer");
+  DTC_CHECK_ARG(((uintptr_t)workspace & 255) == 0, "dtc_rn18_bind: workspace must be 256-byte aligned");
+  DTC_CHECK_ARG(((uintptr_t)params_bf16 & 15) == 0 && ((uintptr_t)params & 15) == 0 && ((uintptr_t)grads & 15) == 0,
+                "dtc_rn18_bind: parameter buffers must be 16-byte aligned");
+  Net& n = net->n;
+  n.ws = (char*)workspace;
+  n.p = params;
+  n.g = grads;
+  n.pb = params_bf16;
+  n.bufs = bufs;
+  n.nbt = num_batches_tracked;
+  DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.stats_hi - n.stats_lo, (hipStream_t)stream));
+  return 0;
+}
+
+int dtc_rn18_forward(dtc_net* net, const float* x, float* logits, int train, void* stream) {
+  DTC_CHECK_ARG(net && net->n.ws && x && logits, "dtc_rn18_forward: unbound net or null pointer");
+  return forward(net->n, x, logits, train != 0, (hipStream_t)stream);
+}
+
+int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_comm* comm, void* stream) {
+  DTC_CHECK_ARG(net && net->n.ws && dlogits, "dtc_rn18_backward: unbound net or null pointer");
+  return backward(net->n, dlogits, grad_scale, (Comm*)comm, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,167 @@
+/*
+ * dtc.h — C ABI of libdtc_amd.so: the MI355X-native (gfx950) kernels and executor for the
+ * ResNet-18 / CIFAR-100 data-parallel training step of youngerous/distributed-training-comparison.
+ *
+ * The reference has no FFI of its own: its operator boundary is the PyTorch module API that
+ * src/{single,dp,ddp}/net.py and trainer.py call (nn.Conv2d, nn.BatchNorm2d, F.relu,
+ * F.avg_pool2d, nn.Linear, nn.CrossEntropyLoss, optim.SGD, GradScaler, DDP). Every entry
+ * point below names the reference call it replaces (file:line under the reference tree).
+ *
+ * Conventions
+ *   - plain C types only; bf16 tensors are uint16_t words (IEEE bfloat16 bit patterns);
+ *   - activations are NHWC; conv filters are KRSC ([out][kh][kw][in], in innermost);
+ *   - every compute call takes `stream` = a hipStream_t (void* here) and only enqueues work;
+ *   - the CALLER owns every device buffer, workspaces included; the library never allocates
+ *     or frees caller memory inside a call. Handles (dtc_comm, dtc_net) are library-owned and
+ *     released by their destroy function;
+ *   - return value: 0 = ok, > 0 = hipError_t / ncclResult_t passed through, < 0 = invalid
+ *     argument. dtc_last_error() gives the message (thread-local). Nothing throws or exits;
+ *   - reentrant: no unguarded global mutable state; calls for different devices may be made
+ *     from different threads (the device is the one current on the calling thread).
+ */
+#ifndef DTC_AMD_H
+#define DTC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DTC_ABI_VERSION 1
+
+/* ------------------------------------------------------------------ library */
+int dtc_abi_version(void);
+const char* dtc_last_error(void);
+
+/* ------------------------------------------------------------------ convolution
+ * Replaces nn.Conv2d(bias=False) forward / backward (reference src/ddp/net.py:18-24,
+ * net.py:29-35, net.py:91) as launched by autocast (cuDNN in the reference).
+ * Requirements: c % 64 == 0, k % 64 == 0, stride in {1, 2} (the stem uses
+ * dtc_stem_im2col + a 1x1 "conv" over 64 im2col channels). */
+typedef struct {
+  int n, h, w, c; /* input  [n][h][w][c]  bf16 */
+  int k, r, s;    /* filter [k][r][s][c]  bf16 */
+  int stride, pad;
+} dtc_conv_desc;
+
+enum { DTC_CONV_FWD = 0, DTC_CONV_DGRAD = 1, DTC_CONV_WGRAD = 2 };
+
+/* bytes of fp32 workspace the given pass wants (split-K partial slabs); 0 is valid for FWD/DGRAD */
+size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass);
+/* y[n][p][q][k] = conv(x, w); if stats != NULL, per-channel (sum, sum^2) of the bf16 output are
+ * ADDED into stats[32][2][k] (fp64) — the batch statistics BatchNorm2d needs (net.py:21). */
+int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats,
+                   void* ws, size_t ws_bytes, void* stream);
+/* dx = conv^T(dy, w) (+ res if non-NULL): the input gradient of Conv2d */
+int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
+                     const uint16_t* res, void* ws, size_t ws_bytes, void* stream);
+/* dw[k][r][s][c] (fp32) = scale * sum over pixels of dy (x) im2col(x): the weight gradient */
+int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* dw, float scale,
+                     void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------ batch norm (training)
+ * Replaces nn.BatchNorm2d train-mode forward/backward (net.py:21,25,37,92) with the F.relu and
+ * residual add of BasicBlock.forward (net.py:41-44) and ResNet.forward (net.py:108) fused.
+ * x is NHWC bf16 with m = n*h*w pixels and c channels (c % 8 == 0). */
+int dtc_bn_fwd_finalize(double* stats, int c, int64_t count, const float* gamma, const float* beta,
+                        float* running_mean, float* running_var, int64_t* num_batches_tracked, float momentum,
+                        float eps, float* mean, float* invstd, float* scale, float* shift, void* stream);
+int dtc_bn_apply_relu(const uint16_t* x, const float* scale, const float* shift, uint16_t* y, int64_t m, int c,
+                      void* stream);
+int dtc_bn_apply_add_relu(const uint16_t* x, const float* scale, const float* shift, const uint16_t* res,
+                          uint16_t* y, int64_t m, int c, void* stream);
+int dtc_bn_apply_dual_relu(const uint16_t* x, const float* scale, const float* shift, const uint16_t* x2,
+                           const float* scale2, const float* shift2, uint16_t* y, int64_t m, int c, void* stream);
+/* dz = dy * [ymask > 0] (ymask may be NULL: no ReLU); acc1 += (sum dz, sum dz*xhat1) and, if x2,
+ * acc2 += (sum dz, sum dz*xhat2); acc* are [32][2][c] fp64 */
+int dtc_bn_bwd_reduce(const uint16_t* dy, const uint16_t* ymask, const uint16_t* x1, const float* mean1,
+                      const float* invstd1, double* acc1, const uint16_t* x2, const float* mean2,
+                      const float* invstd2, double* acc2, uint16_t* dz, int64_t m, int c, void* stream);
+/* dgamma = gscale*sum dz*xhat, dbeta = gscale*sum dz; coef[3][c] for dtc_bn_bwd_apply; acc re-zeroed */
+int dtc_bn_bwd_finalize(double* acc, int c, int64_t count, const float* gamma, const float* mean,
+                        const float* invstd, float gscale, float* dgamma, float* dbeta, float* coef, void* stream);
+int dtc_bn_bwd_apply(const uint16_t* dz, const uint16_t* x1, const float* coef1, uint16_t* dx1, const uint16_t* x2,
+                     const float* coef2, uint16_t* dx2, int64_t m, int c, void* stream);
+
+/* ------------------------------------------------------------------ stem, head, loss
+ * stem: self.conv1 = nn.Conv2d(3, 64, 3, 1, 1) (net.py:91) as im2col [n*h*w][64] + GEMM.
+ * head: F.avg_pool2d(out, 4) + view + self.linear (net.py:113-115), global pool.
+ * loss: nn.CrossEntropyLoss() (trainer.py:40, 155), mean reduction. */
+int dtc_stem_im2col(const float* x_nchw, uint16_t* cols, int n, int h, int w, void* stream);
+int dtc_stem_pack_weight(const uint16_t* w27, uint16_t* w64, int k, void* stream);
+int dtc_head_fwd(const uint16_t* act, int n, int hw, int c, const uint16_t* wfc, const float* bfc, int ncls,
+                 float* feat, float* logits, void* stream);
+int dtc_head_bwd(const float* dlogits, const float* feat, const uint16_t* wfc, int n, int hw, int c, int ncls,
+                 float scale, float* dw, float* db, uint16_t* dact, void* stream);
+int dtc_xent_fwd(const float* logits, const int64_t* labels, int n, int ncls, float* loss, float* lse,
+                 void* stream);
+int dtc_xent_bwd(const float* logits, const int64_t* labels, const float* lse, const float* gscale, int n, int ncls,
+                 float* dlogits, void* stream);
+
+/* ------------------------------------------------------------------ optimizer / AMP
+ * sgd: optim.SGD(lr, weight_decay, momentum, nesterov=True).step() (trainer.py:92-98, 158) over a
+ * flat fp32 buffer; grads are multiplied by *inv_scale (GradScaler.unscale_) and the step is skipped
+ * when *found_inf != 0 (GradScaler.step); p_bf16 receives the bf16 shadow of the new parameters.
+ * amp: GradScaler's _amp_foreach_non_finite_check_and_unscale_ / _amp_update_scale_ (main.py:25). */
+int dtc_sgd_nesterov_flat(float* p, const float* g, float* momentum_buf, uint16_t* p_bf16, int64_t n, float lr,
+                          float weight_decay, float momentum, const float* inv_scale, const int* found_inf,
+                          void* stream);
+int dtc_cast_f32_bf16(const float* src, uint16_t* dst, int64_t n, void* stream);
+int dtc_amp_check_finite(const float* g, int64_t n, int* found_inf, void* stream);
+int dtc_amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, int* found_inf, float growth_factor,
+                         float backoff_factor, int growth_interval, void* stream);
+
+/* ------------------------------------------------------------------ RCCL communicator
+ * Replaces the NCCL traffic of DistributedDataParallel (trainer.py:31): the construction-time
+ * parameter broadcast, the per-forward buffer broadcast and the bucketed gradient all-reduce.
+ * Bootstrap: rank 0 calls dtc_comm_get_unique_id, the id travels over the existing
+ * torch.distributed rendezvous (init_process_group, ddp/main.py:18-23), every rank calls
+ * dtc_comm_init. dtype: 0 = fp32, 1 = bf16, 2 = int64. */
+typedef struct dtc_comm dtc_comm;
+size_t dtc_comm_unique_id_bytes(void);
+int dtc_comm_get_unique_id(void* out);
+int dtc_comm_init(dtc_comm** out, int rank, int world, const void* unique_id, int device);
+int dtc_comm_allreduce_sum(dtc_comm* comm, void* buf, size_t count, int dtype, void* stream);
+int dtc_comm_broadcast(dtc_comm* comm, void* buf, size_t count, int dtype, int root, void* stream);
+int dtc_comm_destroy(dtc_comm* comm);
+
+/* ------------------------------------------------------------------ ResNet-18 executor
+ * The whole forward (ResNet.forward, net.py:107-116) and backward of ResNet18() (net.py:119-120)
+ * as one call each, for a fixed per-rank batch and input size. Parameters live in ONE flat fp32
+ * buffer laid out in reverse registration order (so backward produces gradients in increasing
+ * address order and DDP buckets are contiguous); conv weights are stored KRSC and exposed to
+ * Python as strided [k][c][r][s] views. dtc_rn18_param_info lists the 62 parameters in
+ * registration order (net.py:86-105) with names identical to ResNet18().state_dict() keys. */
+typedef struct dtc_net dtc_net;
+int dtc_rn18_create(dtc_net** out, int batch, int height, int width, int num_classes, float bucket_cap_mb);
+int dtc_rn18_destroy(dtc_net* net);
+int dtc_rn18_num_params(const dtc_net* net);
+int dtc_rn18_param_info(const dtc_net* net, int idx, const char** name, int64_t* offset, int64_t* numel, int* ndim,
+                        int64_t* shape4, int64_t* stride4);
+int64_t dtc_rn18_flat_numel(const dtc_net* net);
+/* BN buffers: running_mean/running_var in one fp32 flat buffer; num_batches_tracked in an int64 array */
+int dtc_rn18_num_bn(const dtc_net* net);
+int dtc_rn18_bn_info(const dtc_net* net, int idx, const char** prefix, int* channels, int64_t* mean_offset,
+                     int64_t* var_offset);
+int64_t dtc_rn18_bufs_numel(const dtc_net* net);
+size_t dtc_rn18_workspace_bytes(const dtc_net* net);
+int dtc_rn18_num_buckets(const dtc_net* net);
+int dtc_rn18_bucket_info(const dtc_net* net, int idx, int64_t* offset, int64_t* numel);
+/* Attach caller-owned device memory. Zeroes the workspace statistics areas (enqueued on stream). */
+int dtc_rn18_bind(dtc_net* net, void* workspace, float* params, float* grads, uint16_t* params_bf16, float* bufs,
+                  int64_t* num_batches_tracked, void* stream);
+/* x: NCHW fp32 [batch][3][h][w]; logits fp32 [batch][ncls]. train != 0: batch statistics +
+ * running-stat update; train == 0: running statistics (eval mode). */
+int dtc_rn18_forward(dtc_net* net, const float* x, float* logits, int train, void* stream);
+/* Gradients of every parameter, scaled by grad_scale (1/world for DDP's mean), written (not
+ * accumulated) into the bound flat grad buffer. If comm != NULL each bucket is all-reduced (sum)
+ * on the communicator's side stream as soon as backward has produced it; the call returns with
+ * `stream` ordered after the last all-reduce. */
+int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_comm* comm, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DTC_AMD_H */
