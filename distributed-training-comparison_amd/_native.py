@@ -1,0 +1,138 @@
+"""ctypes binding of libdtc_amd.so (C ABI: include/dtc.h).
+
+The library is loaded AFTER ``import torch`` so that its DT_NEEDED ``libamdhip64.so.7`` and
+``librccl.so.1`` resolve to the copies torch already mapped: one HIP runtime and one RCCL per
+process. There is no fallback: if the shared object is missing or does not
+export a symbol the package raises at import time.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libdtc_amd.so")
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(or `make -C distributed-training-comparison_amd/csrc`)."
+        )
+    return C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+
+
+lib = _load()
+
+vp = C.c_void_p
+i32 = C.c_int
+i64 = C.c_int64
+f32 = C.c_float
+sz = C.c_size_t
+P64 = C.POINTER(C.c_int64)
+Pi32 = C.POINTER(C.c_int)
+cstr = C.c_char_p
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("n", "h", "w", "c", "k", "r", "s", "stride", "pad")]
+
+
+PConv = C.POINTER(ConvDesc)
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "dtc_abi_version": (i32, []),
+    "dtc_last_error": (cstr, []),
+    "dtc_conv2d_workspace_size": (sz, [PConv, i32]),
+    "dtc_conv2d_fwd": (i32, [PConv, vp, vp, vp, vp, vp, sz, vp]),
+    "dtc_conv2d_dgrad": (i32, [PConv, vp, vp, vp, vp, vp, sz, vp]),
+    "dtc_conv2d_wgrad": (i32, [PConv, vp, vp, vp, f32, vp, sz, vp]),
+    "dtc_bn_fwd_finalize": (i32, [vp, i32, i64, vp, vp, vp, vp, vp, f32, f32, vp, vp, vp, vp, vp]),
+    "dtc_bn_apply_relu": (i32, [vp, vp, vp, vp, i64, i32, vp]),
+    "dtc_bn_apply_add_relu": (i32, [vp, vp, vp, vp, vp, i64, i32, vp]),
+    "dtc_bn_apply_dual_relu": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
+    "dtc_bn_bwd_reduce": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
+    "dtc_bn_bwd_finalize": (i32, [vp, i32, i64, vp, vp, vp, f32, vp, vp, vp, vp]),
+    "dtc_bn_bwd_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
+    "dtc_stem_im2col": (i32, [vp, vp, i32, i32, i32, vp]),
+    "dtc_stem_pack_weight": (i32, [vp, vp, i32, vp]),
+    "dtc_head_fwd": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp]),
+    "dtc_head_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp]),
+    "dtc_xent_fwd": (i32, [vp, vp, i32, i32, vp, vp, vp]),
+    "dtc_xent_bwd": (i32, [vp, vp, vp, vp, i32, i32, vp, vp]),
+    "dtc_sgd_nesterov_flat": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, vp, vp, vp]),
+    "dtc_cast_f32_bf16": (i32, [vp, vp, i64, vp]),
+    "dtc_amp_check_finite": (i32, [vp, i64, vp, vp]),
+    "dtc_amp_update_scale": (i32, [vp, vp, vp, vp, f32, f32, i32, vp]),
+    "dtc_comm_unique_id_bytes": (sz, []),
+    "dtc_comm_get_unique_id": (i32, [vp]),
+    "dtc_comm_init": (i32, [C.POINTER(vp), i32, i32, vp, i32]),
+    "dtc_comm_allreduce_sum": (i32, [vp, vp, sz, i32, vp]),
+    "dtc_comm_broadcast": (i32, [vp, vp, sz, i32, i32, vp]),
+    "dtc_comm_destroy": (i32, [vp]),
+    "dtc_rn18_create": (i32, [C.POINTER(vp), i32, i32, i32, i32, f32]),
+    "dtc_rn18_destroy": (i32, [vp]),
+    "dtc_rn18_num_params": (i32, [vp]),
+    "dtc_rn18_param_info": (i32, [vp, i32, C.POINTER(cstr), P64, P64, Pi32, P64, P64]),
+    "dtc_rn18_flat_numel": (i64, [vp]),
+    "dtc_rn18_num_bn": (i32, [vp]),
+    "dtc_rn18_bn_info": (i32, [vp, i32, C.POINTER(cstr), Pi32, P64, P64]),
+    "dtc_rn18_bufs_numel": (i64, [vp]),
+    "dtc_rn18_workspace_bytes": (sz, [vp]),
+    "dtc_rn18_num_buckets": (i32, [vp]),
+    "dtc_rn18_bucket_info": (i32, [vp, i32, P64, P64]),
+    "dtc_rn18_bind": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
+    "dtc_rn18_num_activations": (i32, [vp]),
+    "dtc_rn18_activation_info": (i32, [vp, i32, C.POINTER(cstr), C.POINTER(sz), Pi32]),
+    "dtc_rn18_profile_begin": (i32, [vp, i32]),
+    "dtc_rn18_profile_end": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), Pi32]),
+    "dtc_rn18_forward": (i32, [vp, vp, vp, i32, vp]),
+    "dtc_rn18_backward": (i32, [vp, vp, f32, vp, vp]),
+}
+
+SYMBOLS = tuple(_SIGS)
+
+for _name, (_res, _args) in _SIGS.items():
+    _fn = getattr(lib, _name)  # AttributeError here = library does not export the ABI
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+def last_error() -> str:
+    s = lib.dtc_last_error()
+    return s.decode() if s else ""
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        raise NativeError(f"{what or 'dtc call'} failed (code {rc}): {last_error()}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib, name)(*args), name)
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None passes NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def require_cuda(*tensors) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise NativeError("dtc kernels run on the GPU only: got a tensor on " + str(t.device))

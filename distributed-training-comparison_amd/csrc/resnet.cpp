@@ -76,6 +76,14 @@ struct Net {
   // buckets: [offset, numel) in flat elements, and the block index after whose backward it fires
   std::vector<int64_t> bucket_off, bucket_len;
   std::vector<int> bucket_after_block;  // -1 = after the stem (last)
+  // live conv timing (bench roofline): event pairs around every conv call on the compute stream
+  struct ProfPair { hipEvent_t a = nullptr, b = nullptr; double flops = 0; int kind = 0; };
+  std::vector<ProfPair> prof;
+  size_t prof_used = 0;
+  bool profiling = false;
+  // activation registry (per-layer parity): name, workspace byte offset, N,H,W,C
+  struct Act { std::string name; size_t off; int n, h, w, c; };
+  std::vector<Act> acts;
   // bound memory
   char* ws = nullptr;
   float* p = nullptr;
@@ -230,9 +238,20 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
     b.OUT = take(bytes);
     gmax = std::max<int64_t>(gmax, std::max<int64_t>(M * b.Cout, B * b.Hin * b.Win * b.Cin));
   }
-  const int64_t HWl = n.blocks.back().Hout * n.blocks.back().Wout;
-  (void)HWl;
+  n.acts.push_back({"stem.im2col", n.X0, (int)B, n.H, n.W, 64});
+  n.acts.push_back({"stem.conv", n.C0, (int)B, n.H, n.W, 64});
+  n.acts.push_back({"stem.out", n.A0, (int)B, n.H, n.W, 64});
+  for (size_t i = 0; i < n.blocks.size(); ++i) {
+    const BlockL& b = n.blocks[i];
+    const std::string pre = "layer" + std::to_string(i / 2 + 1) + "." + std::to_string(i % 2);
+    n.acts.push_back({pre + ".conv1", b.C1, (int)B, b.Hout, b.Wout, b.Cout});
+    n.acts.push_back({pre + ".relu1", b.A1, (int)B, b.Hout, b.Wout, b.Cout});
+    n.acts.push_back({pre + ".conv2", b.C2, (int)B, b.Hout, b.Wout, b.Cout});
+    if (b.proj) n.acts.push_back({pre + ".shortcut", b.S, (int)B, b.Hout, b.Wout, b.Cout});
+    n.acts.push_back({pre + ".out", b.OUT, (int)B, b.Hout, b.Wout, b.Cout});
+  }
   n.FEAT = take(B * 512 * 4);
+  n.acts.push_back({"head.feat_f32", n.FEAT, (int)B, 1, 1, 512});
   for (int i = 0; i < 6; ++i) n.G[i] = take(gmax * 2);
   // BN per-layer state
   n.stats_lo = off;
@@ -281,6 +300,32 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.bucket_after_block.push_back(-1);
 }
 
+// ------------------------------------------------------------------ profiling helpers
+static double conv_flops(const ConvShape& s) {
+  const int P = (s.H + 2 * s.pad - s.R) / s.stride + 1, Q = (s.W + 2 * s.pad - s.S) / s.stride + 1;
+  return 2.0 * s.N * P * Q * (double)s.K * s.R * s.S * s.C;
+}
+static int prof_begin(Net& n, hipStream_t st) {
+  if (!n.profiling) return 0;
+  if (n.prof_used >= n.prof.size()) return set_error(DTC_EINVAL, "profile event capacity exhausted");
+  DTC_HIP(hipEventRecord(n.prof[n.prof_used].a, st));
+  return 0;
+}
+static int prof_end(Net& n, hipStream_t st, double flops, int kind) {
+  if (!n.profiling) return 0;
+  auto& e = n.prof[n.prof_used++];
+  e.flops = flops;
+  e.kind = kind;
+  DTC_HIP(hipEventRecord(e.b, st));
+  return 0;
+}
+#define PROF(kind, flops, call)                    \
+  do {                                             \
+    DTC_TRY(prof_begin(n, st));                    \
+    DTC_TRY(call);                                 \
+    DTC_TRY(prof_end(n, st, (flops), (kind)));     \
+  } while (0)
+
 // ------------------------------------------------------------------ forward / backward
 static int bn_finalize_fwd(Net& n, BNL& b, int64_t count, bool train, hipStream_t st) {
   if (train) {
@@ -297,8 +342,9 @@ static int forward(Net& n, const float* x, float* logits, bool train, hipStream_
   u16* X0 = n.at<u16>(n.X0);
   DTC_TRY(stem_pack_weight(n.wbf(n.stem.pidx), n.at<u16>(n.WSTEM), 64, st));
   DTC_TRY(stem_im2col(x, X0, n.B, n.H, n.W, st));
-  DTC_TRY(conv_fwd(n.stem.s, X0, n.at<u16>(n.WSTEM), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
-                   n.at<float>(n.SLAB), n.slab_bytes, st));
+  PROF(0, 2.0 * M0 * 64 * 27,
+       conv_fwd(n.stem.s, X0, n.at<u16>(n.WSTEM), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
+                n.at<float>(n.SLAB), n.slab_bytes, st));
   DTC_TRY(bn_finalize_fwd(n, n.bn0, M0, train, st));
   DTC_TRY(bn_apply_relu(n.at<u16>(n.C0), n.at<float>(n.bn0.scale), n.at<float>(n.bn0.shift), n.at<u16>(n.A0), M0, 64,
                         st));
@@ -306,17 +352,20 @@ static int forward(Net& n, const float* x, float* logits, bool train, hipStream_
   for (auto& b : n.blocks) {
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
     float* slab = n.at<float>(n.SLAB);
-    DTC_TRY(conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
-                     n.slab_bytes, st));
+    PROF(0, conv_flops(b.c1.s),
+         conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
+                  n.slab_bytes, st));
     DTC_TRY(bn_finalize_fwd(n, b.b1, M, train, st));
     DTC_TRY(bn_apply_relu(n.at<u16>(b.C1), n.at<float>(b.b1.scale), n.at<float>(b.b1.shift), n.at<u16>(b.A1), M,
                           b.Cout, st));
-    DTC_TRY(conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
-                     train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st));
+    PROF(0, conv_flops(b.c2.s),
+         conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
+                  train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st));
     DTC_TRY(bn_finalize_fwd(n, b.b2, M, train, st));
     if (b.proj) {
-      DTC_TRY(conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr,
-                       slab, n.slab_bytes, st));
+      PROF(0, conv_flops(b.sc.s),
+           conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr,
+                    slab, n.slab_bytes, st));
       DTC_TRY(bn_finalize_fwd(n, b.bsc, M, train, st));
       DTC_TRY(bn_apply_dual_relu(n.at<u16>(b.C2), n.at<float>(b.b2.scale), n.at<float>(b.b2.shift), n.at<u16>(b.S),
                                  n.at<float>(b.bsc.scale), n.at<float>(b.bsc.shift), n.at<u16>(b.OUT), M, b.Cout, st));
@@ -366,8 +415,8 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
     DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(b.C2), n.at<float>(b.b2.coef), G[2], b.proj ? n.at<u16>(b.S) : nullptr,
                          b.proj ? n.at<float>(b.bsc.coef) : nullptr, b.proj ? G[3] : nullptr, M, b.Cout, st));
     // conv2: dW2 and da1
-    DTC_TRY(conv_wgrad(b.c2.s, n.at<u16>(b.A1), G[2], n.gf(b.c2.pidx), 0, 0, gs, slab, n.slab_bytes, st));
-    DTC_TRY(conv_dgrad(b.c2.s, G[2], n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st));
+    PROF(2, conv_flops(b.c2.s), conv_wgrad(b.c2.s, n.at<u16>(b.A1), G[2], n.gf(b.c2.pidx), 0, 0, gs, slab, n.slab_bytes, st));
+    PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, G[2], n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st));
     // a1 = relu(bn1(c1))
     DTC_TRY(bn_bwd_reduce(G[4], n.at<u16>(b.A1), n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
                           n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, G[4], M, b.Cout, st));
@@ -377,13 +426,13 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
     DTC_TRY(bn_bwd_apply(G[4], n.at<u16>(b.C1), n.at<float>(b.b1.coef), G[2], nullptr, nullptr, nullptr, M, b.Cout,
                          st));
     // conv1 (+ shortcut): weight grads, then the block-input gradient with the residual fused
-    DTC_TRY(conv_wgrad(b.c1.s, in, G[2], n.gf(b.c1.pidx), 0, 0, gs, slab, n.slab_bytes, st));
+    PROF(2, conv_flops(b.c1.s), conv_wgrad(b.c1.s, in, G[2], n.gf(b.c1.pidx), 0, 0, gs, slab, n.slab_bytes, st));
     if (b.proj) {
-      DTC_TRY(conv_wgrad(b.sc.s, in, G[3], n.gf(b.sc.pidx), 0, 0, gs, slab, n.slab_bytes, st));
-      DTC_TRY(conv_dgrad(b.sc.s, G[3], n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st));
-      DTC_TRY(conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st));
+      PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, G[3], n.gf(b.sc.pidx), 0, 0, gs, slab, n.slab_bytes, st));
+      PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, G[3], n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st));
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st));
     } else {
-      DTC_TRY(conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[1], slab, n.slab_bytes, st));
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[1], slab, n.slab_bytes, st));
     }
     DTC_TRY(maybe_bucket(n, bi, comm, st));
   }
@@ -395,7 +444,8 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
                           n.at<float>(n.bn0.invstd), gs, n.gf(n.bn0.gidx), n.gf(n.bn0.bidx), n.at<float>(n.bn0.coef),
                           st));
   DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(n.C0), n.at<float>(n.bn0.coef), G[2], nullptr, nullptr, nullptr, M0, 64, st));
-  DTC_TRY(conv_wgrad(n.stem.s, n.at<u16>(n.X0), G[2], n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st));
+  PROF(2, 2.0 * M0 * 64 * 27,
+       conv_wgrad(n.stem.s, n.at<u16>(n.X0), G[2], n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st));
   DTC_TRY(maybe_bucket(n, -1, comm, st));
   if (comm) DTC_TRY(comm_join(comm, st));
   return 0;
@@ -434,6 +484,11 @@ int dtc_rn18_create(dtc_net** out, int batch, int height, int width, int num_cla
 }
 
 int dtc_rn18_destroy(dtc_net* net) {
+  if (net)
+    for (auto& p : net->n.prof) {
+      if (p.a) (void)hipEventDestroy(p.a);
+      if (p.b) (void)hipEventDestroy(p.b);
+    }
   delete net;
   return 0;
 }
@@ -494,6 +549,55 @@ int dtc_rn18_bind(dtc_net* net, void* workspace, float* params, float* grads, ui
   n.bufs = bufs;
   n.nbt = num_batches_tracked;
   DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.stats_hi - n.stats_lo, (hipStream_t)stream));
+  return 0;
+}
+
+int dtc_rn18_num_activations(const dtc_net* net) { return net ? (int)net->n.acts.size() : DTC_EINVAL; }
+
+int dtc_rn18_activation_info(const dtc_net* net, int idx, const char** name, size_t* ws_offset, int* shape4) {
+  DTC_CHECK_ARG(net && idx >= 0 && idx < (int)net->n.acts.size(), "dtc_rn18_activation_info: bad index");
+  const auto& a = net->n.acts[idx];
+  if (name) *name = a.name.c_str();
+  if (ws_offset) *ws_offset = a.off;
+  if (shape4) {
+    shape4[0] = a.n; shape4[1] = a.h; shape4[2] = a.w; shape4[3] = a.c;
+  }
+  return 0;
+}
+
+int dtc_rn18_profile_begin(dtc_net* net, int capacity) {
+  DTC_CHECK_ARG(net && capacity > 0, "dtc_rn18_profile_begin: bad args");
+  Net& n = net->n;
+  while ((int)n.prof.size() < capacity) {
+    Net::ProfPair p;
+    DTC_HIP(hipEventCreate(&p.a));
+    DTC_HIP(hipEventCreate(&p.b));
+    n.prof.push_back(p);
+  }
+  n.prof_used = 0;
+  n.profiling = true;
+  return 0;
+}
+
+int dtc_rn18_profile_end(dtc_net* net, double* ms_by_kind, double* flops_by_kind, int* count_by_kind) {
+  DTC_CHECK_ARG(net != nullptr, "dtc_rn18_profile_end: null net");
+  Net& n = net->n;
+  n.profiling = false;
+  for (int k = 0; k < 3; ++k) {
+    if (ms_by_kind) ms_by_kind[k] = 0;
+    if (flops_by_kind) flops_by_kind[k] = 0;
+    if (count_by_kind) count_by_kind[k] = 0;
+  }
+  for (size_t i = 0; i < n.prof_used; ++i) {
+    auto& e = n.prof[i];
+    DTC_HIP(hipEventSynchronize(e.b));
+    float ms = 0.f;
+    DTC_HIP(hipEventElapsedTime(&ms, e.a, e.b));
+    if (ms_by_kind) ms_by_kind[e.kind] += ms;
+    if (flops_by_kind) flops_by_kind[e.kind] += e.flops;
+    if (count_by_kind) count_by_kind[e.kind] += 1;
+  }
+  n.prof_used = 0;
   return 0;
 }
 

@@ -1,0 +1,337 @@
+"""ResNet-18 and CrossEntropyLoss modules backed by the native executor.
+
+Mirror of the reference's operator boundary (src/ddp/net.py, trainer.py:40):
+
+* ``ResNet18()`` builds the module tree with the SAME ``nn.Conv2d`` / ``nn.BatchNorm2d`` /
+  ``nn.Linear`` constructors in the SAME order as net.py:86-105 and net.py:16-38, so a given
+  ``torch.manual_seed`` yields bit-identical initial parameters and ``state_dict()`` keys
+  (``layer2.0.shortcut.0.weight`` ...). Construction is ordinary PyTorch on the host.
+* ``.to('cuda')`` moves those parameters into one flat fp32 device buffer laid out by the
+  native executor (reverse registration order, KRSC conv filters exposed as strided
+  [K,C,R,S] views) plus its bf16 shadow; gradients are views into a flat grad buffer.
+* ``forward`` runs the whole network through ``dtc_rn18_forward`` and ``backward`` through
+  ``dtc_rn18_backward`` (one autograd node). Nothing falls back to torch compute: the module
+  refuses to run on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import weakref
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._native import NativeError, call, lib, ptr, require_cuda, stream_ptr
+
+
+# ----------------------------------------------------------------------------- layout
+@dataclass
+class ParamInfo:
+    name: str
+    offset: int
+    numel: int
+    shape: Tuple[int, ...]
+    stride: Tuple[int, ...]
+
+
+@dataclass
+class BNInfo:
+    prefix: str
+    channels: int
+    mean_offset: int
+    var_offset: int
+
+
+class Layout:
+    """Batch-independent parameter / buffer / bucket layout reported by the executor."""
+
+    def __init__(self, num_classes: int = 100, bucket_cap_mb: float = 25.0):
+        h = C.c_void_p()
+        call("dtc_rn18_create", C.byref(h), 1, 32, 32, num_classes, float(bucket_cap_mb))
+        try:
+            self.params: List[ParamInfo] = []
+            for i in range(lib.dtc_rn18_num_params(h)):
+                name = C.c_char_p()
+                off, numel = C.c_int64(), C.c_int64()
+                nd = C.c_int()
+                shp = (C.c_int64 * 4)()
+                strd = (C.c_int64 * 4)()
+                call("dtc_rn18_param_info", h, i, C.byref(name), C.byref(off), C.byref(numel), C.byref(nd), shp, strd)
+                self.params.append(ParamInfo(name.value.decode(), off.value, numel.value,
+                                             tuple(shp[: nd.value]), tuple(strd[: nd.value])))
+            self.bns: List[BNInfo] = []
+            for i in range(lib.dtc_rn18_num_bn(h)):
+                pre = C.c_char_p()
+                ch = C.c_int()
+                mo, vo = C.c_int64(), C.c_int64()
+                call("dtc_rn18_bn_info", h, i, C.byref(pre), C.byref(ch), C.byref(mo), C.byref(vo))
+                self.bns.append(BNInfo(pre.value.decode(), ch.value, mo.value, vo.value))
+            self.flat_numel = lib.dtc_rn18_flat_numel(h)
+            self.bufs_numel = lib.dtc_rn18_bufs_numel(h)
+            self.buckets = []
+            for i in range(lib.dtc_rn18_num_buckets(h)):
+                o, n = C.c_int64(), C.c_int64()
+                call("dtc_rn18_bucket_info", h, i, C.byref(o), C.byref(n))
+                self.buckets.append((o.value, n.value))
+        finally:
+            lib.dtc_rn18_destroy(h)
+
+
+class FlatState:
+    """Device buffers shared by every executor of one model."""
+
+    def __init__(self, layout: Layout, device: torch.device):
+        self.layout = layout
+        self.device = device
+        self.params = torch.zeros(layout.flat_numel, dtype=torch.float32, device=device)
+        self.grads = torch.zeros(layout.flat_numel, dtype=torch.float32, device=device)
+        self.params_bf16 = torch.zeros(layout.flat_numel, dtype=torch.bfloat16, device=device)
+        self.bufs = torch.zeros(layout.bufs_numel, dtype=torch.float32, device=device)
+        self.nbt = torch.zeros(len(layout.bns), dtype=torch.int64, device=device)
+
+    def refresh_bf16(self):
+        ops.cast_f32_bf16(self.params, self.params_bf16)
+
+
+class Executor:
+    """One native executor (plan + workspace) for a fixed (batch, height, width)."""
+
+    def __init__(self, flat: FlatState, batch: int, height: int, width: int, num_classes: int, bucket_cap_mb: float):
+        self.handle = C.c_void_p()
+        call("dtc_rn18_create", C.byref(self.handle), batch, height, width, num_classes, float(bucket_cap_mb))
+        nbytes = lib.dtc_rn18_workspace_bytes(self.handle)
+        # 256-byte aligned workspace (the caching allocator returns 512-byte aligned blocks)
+        self.workspace = torch.empty(nbytes + 256, dtype=torch.uint8, device=flat.device)
+        base = self.workspace.data_ptr()
+        self.ws_ptr = (base + 255) // 256 * 256
+        self.flat = flat
+        self.batch, self.height, self.width, self.num_classes = batch, height, width, num_classes
+        self.generation = 0
+        call("dtc_rn18_bind", self.handle, self.ws_ptr, ptr(flat.params), ptr(flat.grads), ptr(flat.params_bf16),
+             ptr(flat.bufs), ptr(flat.nbt), stream_ptr())
+
+    def forward(self, x: torch.Tensor, logits: torch.Tensor, train: bool) -> int:
+        call("dtc_rn18_forward", self.handle, ptr(x), ptr(logits), int(bool(train)), stream_ptr())
+        self.generation += 1
+        return self.generation
+
+    def backward(self, dlogits: torch.Tensor, grad_scale: float, comm) -> None:
+        call("dtc_rn18_backward", self.handle, ptr(dlogits), float(grad_scale), comm.handle if comm else None,
+             stream_ptr())
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            lib.dtc_rn18_destroy(h)
+            self.handle = None
+
+
+# ----------------------------------------------------------------------------- autograd nodes
+class _NetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, model, exe):
+        logits = torch.empty(x.shape[0], model.num_classes, dtype=torch.float32, device=x.device)
+        ctx.gen = exe.forward(x, logits, model.training)
+        ctx.model, ctx.exe = model, exe
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        model, exe = ctx.model, ctx.exe
+        if exe.generation != ctx.gen:
+            raise NativeError("ResNet backward: the executor ran another forward since this graph was built "
+                              "(one forward per backward is supported)")
+        exe.backward(dlogits.contiguous().float(), model._grad_scale, model._comm)
+        model._ensure_grads()
+        return None, None, None, None
+
+
+class _XentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        loss, lse = ops.xent_fwd(logits, labels)
+        ctx.save_for_backward(logits, labels, lse)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        logits, labels, lse = ctx.saved_tensors
+        g = gloss.reshape(1).float().contiguous()
+        return ops.xent_bwd(logits, labels, lse, g), None
+
+
+class CrossEntropyLoss(nn.Module):
+    """nn.CrossEntropyLoss() with mean reduction (reference trainer.py:40) on the native kernel."""
+
+    def forward(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        require_cuda(logits, labels)
+        if logits.dtype != torch.float32:
+            logits = logits.float()
+        return _XentFn.apply(logits.contiguous(), labels.long().contiguous())
+
+
+# ----------------------------------------------------------------------------- modules
+class BasicBlock(nn.Module):
+    """Parameter container with reference net.py:13-38's construction order and names."""
+
+    expansion = 1
+
+    def __init__(self, in_planes, planes, stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_planes, planes, kernel_size=3, stride=stride, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, kernel_size=3, stride=1, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.shortcut = nn.Sequential()
+        if stride != 1 or in_planes != self.expansion * planes:
+            self.shortcut = nn.Sequential(
+                nn.Conv2d(in_planes, self.expansion * planes, kernel_size=1, stride=stride, bias=False),
+                nn.BatchNorm2d(self.expansion * planes),
+            )
+
+    def forward(self, x):  # pragma: no cover - the network runs as a whole in ResNet.forward
+        raise NativeError("BasicBlock runs inside the native ResNet executor; call the ResNet module")
+
+
+class ResNet(nn.Module):
+    """CIFAR ResNet (net.py:86-116) whose forward/backward run on the MI355X executor."""
+
+    def __init__(self, block=BasicBlock, num_blocks=(2, 2, 2, 2), num_classes=100, bucket_cap_mb: float = 25.0):
+        super().__init__()
+        if block is not BasicBlock or tuple(num_blocks) != (2, 2, 2, 2):
+            raise NotImplementedError("only ResNet18 (BasicBlock, [2,2,2,2]) is built natively (reference main.py:26)")
+        self.in_planes = 64
+        self.num_classes = num_classes
+        self.conv1 = nn.Conv2d(3, 64, kernel_size=3, stride=1, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.layer1 = self._make_layer(block, 64, num_blocks[0], stride=1)
+        self.layer2 = self._make_layer(block, 128, num_blocks[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, num_blocks[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, num_blocks[3], stride=2)
+        self.linear = nn.Linear(512 * block.expansion, num_classes)
+        self._flat: Optional[FlatState] = None
+        self._layout: Optional[Layout] = None
+        self._executors: Dict[Tuple[int, int, int], Executor] = {}
+        self._anchor: Optional[torch.Tensor] = None
+        self._comm = None
+        self._grad_scale = 1.0
+        self._bucket_cap_mb = float(bucket_cap_mb)
+        self._dirty = False
+
+    def _make_layer(self, block, planes, num_blocks, stride):
+        strides = [stride] + [1] * (num_blocks - 1)
+        layers = []
+        for s in strides:
+            layers.append(block(self.in_planes, planes, s))
+            self.in_planes = planes * block.expansion
+        return nn.Sequential(*layers)
+
+    # ------------------------------------------------------------------ device placement
+    def _apply(self, fn, recurse=True):
+        if self._flat is not None:
+            return self  # parameters are pinned in the flat device buffers
+        out = super()._apply(fn, recurse)
+        dev = self.conv1.weight.device
+        if dev.type == "cuda":
+            self._materialize(dev)
+        return out
+
+    def _resolve(self, dotted: str):
+        parts = dotted.split(".")
+        mod = self
+        for p in parts[:-1]:
+            mod = getattr(mod, p)
+        return mod, parts[-1]
+
+    def _materialize(self, device: torch.device):
+        layout = Layout(self.num_classes, self._bucket_cap_mb)
+        names = [n for n, _ in self.named_parameters()]
+        if names != [p.name for p in layout.params]:
+            raise NativeError("module parameters do not match the executor layout")
+        flat = FlatState(layout, device)
+        with torch.no_grad():
+            for info in layout.params:
+                mod, attr = self._resolve(info.name)
+                old = getattr(mod, attr)
+                view = torch.as_strided(flat.params, info.shape, info.stride, info.offset)
+                view.copy_(old.detach().to(device))
+                newp = nn.Parameter(view, requires_grad=old.requires_grad)
+                newp._dtc_model = weakref.ref(self)
+                mod._parameters[attr] = newp
+            for i, bn in enumerate(layout.bns):
+                mod, _ = self._resolve(bn.prefix + ".x")
+                rm = flat.bufs.narrow(0, bn.mean_offset, bn.channels)
+                rv = flat.bufs.narrow(0, bn.var_offset, bn.channels)
+                rm.copy_(mod.running_mean.to(device))
+                rv.copy_(mod.running_var.to(device))
+                flat.nbt[i].copy_(mod.num_batches_tracked.to(device))
+                mod._buffers["running_mean"] = rm
+                mod._buffers["running_var"] = rv
+                mod._buffers["num_batches_tracked"] = flat.nbt[i]
+        self._layout = layout
+        self._flat = flat
+        self._anchor = torch.zeros(1, device=device, requires_grad=True)
+        self._attach_grads()
+        flat.refresh_bf16()
+
+    def _attach_grads(self):
+        for info in self._layout.params:
+            mod, attr = self._resolve(info.name)
+            mod._parameters[attr].grad = torch.as_strided(self._flat.grads, info.shape, info.stride, info.offset)
+
+    def _ensure_grads(self):
+        if self.linear.bias.grad is None or self.conv1.weight.grad is None:
+            self._attach_grads()
+
+    @property
+    def flat(self) -> FlatState:
+        if self._flat is None:
+            raise NativeError("ResNet must be moved to a GPU (`.to('cuda')`) before use")
+        return self._flat
+
+    def sync_weights(self):
+        """Re-derive the bf16 shadow after parameters were modified outside the native SGD."""
+        self.flat.refresh_bf16()
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        if assign:
+            raise NotImplementedError("assign=True would detach parameters from the flat buffer")
+        res = super().load_state_dict(state_dict, strict=strict)
+        if self._flat is not None:
+            self._flat.refresh_bf16()
+        return res
+
+    def buckets(self):
+        """Gradient buckets [(flat offset, numel)] in the order backward completes them."""
+        return Layout(self.num_classes, self._bucket_cap_mb).buckets
+
+    def set_bucket_cap_mb(self, mb: float):
+        self._bucket_cap_mb = float(mb)
+        self._executors.clear()
+
+    def executor(self, batch: int, height: int, width: int) -> Executor:
+        key = (batch, height, width)
+        exe = self._executors.get(key)
+        if exe is None:
+            exe = Executor(self.flat, batch, height, width, self.num_classes, self._bucket_cap_mb)
+            self._executors[key] = exe
+        return exe
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        flat = self.flat
+        require_cuda(x)
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise ValueError(f"expected [N,3,H,W] input, got {tuple(x.shape)}")
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.float().contiguous()
+        exe = self.executor(x.shape[0], x.shape[2], x.shape[3])
+        return _NetFn.apply(x, self._anchor, self, exe)
+
+
+def ResNet18(num_classes: int = 100) -> ResNet:
+    """net.py:119-120."""
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes=num_classes)

@@ -1,0 +1,204 @@
+"""Tensor-level wrappers over the per-op C ABI (include/dtc.h).
+
+Each function takes torch tensors that already live on the GPU (torch is the allocator and
+stream provider only), enqueues the native kernel on the current stream and returns output
+tensors. bf16 tensors are passed as torch.bfloat16 (same bits as the ABI's uint16_t words).
+Nothing here computes on the host and there is no fallback path.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._native import ConvDesc, call, lib, ptr, require_cuda, stream_ptr
+
+STAT_SLOTS = 32
+
+
+def conv_desc(n, h, w, c, k, r, s, stride, pad) -> ConvDesc:
+    return ConvDesc(n, h, w, c, k, r, s, stride, pad)
+
+
+def conv_out_hw(h, w, r, s, stride, pad):
+    return (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
+
+
+def _ws(desc, mode, device):
+    nbytes = lib.dtc_conv2d_workspace_size(desc, mode)
+    if nbytes == 0:
+        return None, 0
+    return torch.empty(nbytes // 4 + 1, dtype=torch.float32, device=device), nbytes
+
+
+def conv2d_fwd(x, w, stride, pad, stats=None):
+    """x [N,H,W,C] bf16, w [K,R,S,C] bf16 -> y [N,P,Q,K] bf16 (nn.Conv2d forward, net.py:18)."""
+    require_cuda(x, w)
+    N, H, W, Cc = x.shape
+    K, R, S, _ = w.shape
+    d = conv_desc(N, H, W, Cc, K, R, S, stride, pad)
+    P, Q = conv_out_hw(H, W, R, S, stride, pad)
+    y = torch.empty(N, P, Q, K, dtype=torch.bfloat16, device=x.device)
+    ws, nb = _ws(d, 0, x.device)
+    call("dtc_conv2d_fwd", d, ptr(x), ptr(w), ptr(y), ptr(stats), ptr(ws), nb, stream_ptr())
+    return y
+
+
+def conv2d_dgrad(dy, w, in_hw, stride, pad, res=None):
+    """dy [N,P,Q,K] bf16, w [K,R,S,C] -> dx [N,H,W,C] bf16 (+ res)."""
+    require_cuda(dy, w)
+    N = dy.shape[0]
+    K, R, S, Cc = w.shape
+    H, W = in_hw
+    d = conv_desc(N, H, W, Cc, K, R, S, stride, pad)
+    dx = torch.empty(N, H, W, Cc, dtype=torch.bfloat16, device=dy.device)
+    ws, nb = _ws(d, 1, dy.device)
+    call("dtc_conv2d_dgrad", d, ptr(dy), ptr(w), ptr(dx), ptr(res), ptr(ws), nb, stream_ptr())
+    return dx
+
+
+def conv2d_wgrad(x, dy, r, s, stride, pad, scale=1.0):
+    """x [N,H,W,C] bf16, dy [N,P,Q,K] bf16 -> dw [K,R,S,C] fp32 (scaled)."""
+    require_cuda(x, dy)
+    N, H, W, Cc = x.shape
+    K = dy.shape[3]
+    d = conv_desc(N, H, W, Cc, K, r, s, stride, pad)
+    dw = torch.empty(K, r, s, Cc, dtype=torch.float32, device=x.device)
+    ws, nb = _ws(d, 2, x.device)
+    call("dtc_conv2d_wgrad", d, ptr(x), ptr(dy), ptr(dw), float(scale), ptr(ws), nb, stream_ptr())
+    return dw
+
+
+def new_stats(c, device):
+    return torch.zeros(STAT_SLOTS, 2, c, dtype=torch.float64, device=device)
+
+
+def bn_fwd_finalize(stats, count, gamma, beta, running_mean=None, running_var=None, nbt=None, momentum=0.1,
+                    eps=1e-5):
+    c = gamma.numel()
+    dev = gamma.device
+    mean, invstd, scale, shift = (torch.empty(c, dtype=torch.float32, device=dev) for _ in range(4))
+    call("dtc_bn_fwd_finalize", ptr(stats), c, int(count), ptr(gamma), ptr(beta), ptr(running_mean),
+         ptr(running_var), ptr(nbt), float(momentum), float(eps), ptr(mean), ptr(invstd), ptr(scale), ptr(shift),
+         stream_ptr())
+    return mean, invstd, scale, shift
+
+
+def bn_apply_relu(x, scale, shift):
+    y = torch.empty_like(x)
+    m, c = x.numel() // x.shape[-1], x.shape[-1]
+    call("dtc_bn_apply_relu", ptr(x), ptr(scale), ptr(shift), ptr(y), m, c, stream_ptr())
+    return y
+
+
+def bn_apply_add_relu(x, scale, shift, res):
+    y = torch.empty_like(x)
+    m, c = x.numel() // x.shape[-1], x.shape[-1]
+    call("dtc_bn_apply_add_relu", ptr(x), ptr(scale), ptr(shift), ptr(res), ptr(y), m, c, stream_ptr())
+    return y
+
+
+def bn_apply_dual_relu(x, scale, shift, x2, scale2, shift2):
+    y = torch.empty_like(x)
+    m, c = x.numel() // x.shape[-1], x.shape[-1]
+    call("dtc_bn_apply_dual_relu", ptr(x), ptr(scale), ptr(shift), ptr(x2), ptr(scale2), ptr(shift2), ptr(y), m, c,
+         stream_ptr())
+    return y
+
+
+def bn_bwd_reduce(dy, ymask, x1, mean1, invstd1, x2=None, mean2=None, invstd2=None):
+    c = x1.shape[-1]
+    m = x1.numel() // c
+    acc1 = new_stats(c, x1.device)
+    acc2 = new_stats(c, x1.device) if x2 is not None else None
+    dz = torch.empty_like(dy) if ymask is not None else None
+    call("dtc_bn_bwd_reduce", ptr(dy), ptr(ymask), ptr(x1), ptr(mean1), ptr(invstd1), ptr(acc1), ptr(x2), ptr(mean2),
+         ptr(invstd2), ptr(acc2), ptr(dz), m, c, stream_ptr())
+    return (dz if dz is not None else dy), acc1, acc2
+
+
+def bn_bwd_finalize(acc, count, gamma, mean, invstd, gscale=1.0):
+    c = gamma.numel()
+    dev = gamma.device
+    dgamma = torch.empty(c, dtype=torch.float32, device=dev)
+    dbeta = torch.empty(c, dtype=torch.float32, device=dev)
+    coef = torch.empty(3, c, dtype=torch.float32, device=dev)
+    call("dtc_bn_bwd_finalize", ptr(acc), c, int(count), ptr(gamma), ptr(mean), ptr(invstd), float(gscale),
+         ptr(dgamma), ptr(dbeta), ptr(coef), stream_ptr())
+    return dgamma, dbeta, coef
+
+
+def bn_bwd_apply(dz, x1, coef1, x2=None, coef2=None):
+    c = x1.shape[-1]
+    m = x1.numel() // c
+    dx1 = torch.empty_like(x1)
+    dx2 = torch.empty_like(x2) if x2 is not None else None
+    call("dtc_bn_bwd_apply", ptr(dz), ptr(x1), ptr(coef1), ptr(dx1), ptr(x2), ptr(coef2), ptr(dx2), m, c, stream_ptr())
+    return dx1, dx2
+
+
+def stem_im2col(x):
+    n, _, h, w = x.shape
+    cols = torch.empty(n, h, w, 64, dtype=torch.bfloat16, device=x.device)
+    call("dtc_stem_im2col", ptr(x), ptr(cols), n, h, w, stream_ptr())
+    return cols
+
+
+def stem_pack_weight(w27):
+    k = w27.shape[0]
+    w64 = torch.empty(k, 64, dtype=torch.bfloat16, device=w27.device)
+    call("dtc_stem_pack_weight", ptr(w27), ptr(w64), k, stream_ptr())
+    return w64
+
+
+def head_fwd(act, wfc, bfc):
+    """act [N,h,w,C] bf16, wfc [ncls,C] bf16, bfc [ncls] fp32 -> (feat fp32 [N,C], logits fp32 [N,ncls])."""
+    n, h, w, c = act.shape
+    ncls = wfc.shape[0]
+    feat = torch.empty(n, c, dtype=torch.float32, device=act.device)
+    logits = torch.empty(n, ncls, dtype=torch.float32, device=act.device)
+    call("dtc_head_fwd", ptr(act), n, h * w, c, ptr(wfc), ptr(bfc), ncls, ptr(feat), ptr(logits), stream_ptr())
+    return feat, logits
+
+
+def head_bwd(dlogits, feat, wfc, hw, scale=1.0):
+    n, c = feat.shape
+    ncls = wfc.shape[0]
+    dw = torch.empty(ncls, c, dtype=torch.float32, device=feat.device)
+    db = torch.empty(ncls, dtype=torch.float32, device=feat.device)
+    h, w = hw
+    dact = torch.empty(n, h, w, c, dtype=torch.bfloat16, device=feat.device)
+    call("dtc_head_bwd", ptr(dlogits), ptr(feat), ptr(wfc), n, h * w, c, ncls, float(scale), ptr(dw), ptr(db),
+         ptr(dact), stream_ptr())
+    return dw, db, dact
+
+
+def xent_fwd(logits, labels):
+    n, ncls = logits.shape
+    loss = torch.empty((), dtype=torch.float32, device=logits.device)
+    lse = torch.empty(n, dtype=torch.float32, device=logits.device)
+    call("dtc_xent_fwd", ptr(logits), ptr(labels), n, ncls, ptr(loss), ptr(lse), stream_ptr())
+    return loss, lse
+
+
+def xent_bwd(logits, labels, lse, gscale=None):
+    n, ncls = logits.shape
+    dl = torch.empty_like(logits)
+    call("dtc_xent_bwd", ptr(logits), ptr(labels), ptr(lse), ptr(gscale), n, ncls, ptr(dl), stream_ptr())
+    return dl
+
+
+def sgd_nesterov_flat(p, g, mom, pb, lr, weight_decay, momentum, inv_scale=None, found_inf=None):
+    call("dtc_sgd_nesterov_flat", ptr(p), ptr(g), ptr(mom), ptr(pb), p.numel(), float(lr), float(weight_decay),
+         float(momentum), ptr(inv_scale), ptr(found_inf), stream_ptr())
+
+
+def cast_f32_bf16(src, dst):
+    call("dtc_cast_f32_bf16", ptr(src), ptr(dst), src.numel(), stream_ptr())
+
+
+def amp_check_finite(g, found_inf):
+    call("dtc_amp_check_finite", ptr(g), g.numel(), ptr(found_inf), stream_ptr())
+
+
+def amp_update_scale(scale, inv_scale, tracker, found_inf, growth, backoff, interval):
+    call("dtc_amp_update_scale", ptr(scale), ptr(inv_scale), ptr(tracker), ptr(found_inf), float(growth),
+         float(backoff), int(interval), stream_ptr())

@@ -161,6 +161,16 @@ int dtc_rn18_forward(dtc_net* net, const float* x, float* logits, int train, voi
  * `stream` ordered after the last all-reduce. */
 int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_comm* comm, void* stream);
 
+/* Per-layer activations held in the workspace after dtc_rn18_forward (NHWC bf16 except the
+ * fp32 "head.feat_f32"): name, byte offset into the workspace, {n, h, w, c}. For parity tests. */
+int dtc_rn18_num_activations(const dtc_net* net);
+int dtc_rn18_activation_info(const dtc_net* net, int idx, const char** name, size_t* ws_offset, int* shape4);
+/* Live timing of every convolution call (forward, dgrad, wgrad incl. split-K reductions) with HIP
+ * events on the compute stream, between begin and end; end() synchronizes on the recorded events
+ * and returns per-pass totals: index 0 = forward, 1 = dgrad, 2 = wgrad (ms, algorithmic FLOPs, calls). */
+int dtc_rn18_profile_begin(dtc_net* net, int capacity);
+int dtc_rn18_profile_end(dtc_net* net, double* ms_by_kind, double* flops_by_kind, int* count_by_kind);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,240 @@
+"""Per-op parity of the native HIP kernels against the numpy oracle (oracle/ops.py).
+
+Inputs are drawn at bf16-representable values so the kernel and the oracle see identical
+operands; the oracle accumulates in float64. Tolerances: bf16 outputs 1e-2 relative (north_star
+"per-layer activations and gradients within 1e-2 relative (bf16)"); fp32-output kernels
+(wgrad, BN statistics, SGD) tighter where the arithmetic allows.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ops as O
+from tests.conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+CONV_CASES = [
+    # (N, H, W, C, K, R, stride)  -> pad = 1 for 3x3, 0 for 1x1
+    (2, 8, 8, 64, 64, 3, 1),      # layer1 conv
+    (2, 8, 8, 64, 128, 3, 2),     # layer2.0.conv1 (stride 2)
+    (2, 8, 8, 64, 128, 1, 2),     # layer2.0.shortcut (1x1 s2)
+    (2, 8, 8, 128, 128, 3, 1),    # layer2 conv
+    (3, 4, 4, 256, 512, 3, 2),    # layer4.0.conv1 (ragged pixel count, split-K)
+    (4, 4, 4, 512, 512, 3, 1),    # layer4 conv (deep reduction, split-K)
+    (2, 32, 32, 64, 64, 1, 1),    # stem GEMM over the 64-column im2col image
+    (1, 5, 7, 64, 64, 3, 1),      # odd spatial size, M not a tile multiple
+]
+
+
+def _rand_bf16(shape, gen, scale=1.0):
+    return O.bf16(gen.standard_normal(shape).astype(np.float32) * scale)
+
+
+def _to_dev_bf16(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd(dtc, cuda, case):
+    N, H, W, C, K, R, st = case
+    pad = 1 if R == 3 else 0
+    g = np.random.default_rng(1)
+    x = _rand_bf16((N, H, W, C), g)
+    w = _rand_bf16((K, R, R, C), g, 0.05)
+    stats = dtc.ops.new_stats(K, cuda)
+    y = dtc.ops.conv2d_fwd(_to_dev_bf16(x, cuda), _to_dev_bf16(w, cuda), st, pad, stats=stats)
+    ref = O.conv2d_fwd(x, w, st, pad)
+    yk = y.float().cpu().numpy()
+    assert yk.shape == ref.shape
+    assert rel_err(yk, ref) < 1e-2
+    # BN statistics of the bf16 output, accumulated in fp64 slots
+    s = stats.sum(0).cpu().numpy()
+    yb = yk.reshape(-1, K).astype(np.float64)
+    np.testing.assert_allclose(s[0], yb.sum(0), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("case", CONV_CASES[:6] + CONV_CASES[7:])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_conv_dgrad(dtc, cuda, case, with_res):
+    N, H, W, C, K, R, st = case
+    pad = 1 if R == 3 else 0
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+    g = np.random.default_rng(2)
+    dy = _rand_bf16((N, P, Q, K), g)
+    w = _rand_bf16((K, R, R, C), g, 0.05)
+    res = _rand_bf16((N, H, W, C), g) if with_res else None
+    dx = dtc.ops.conv2d_dgrad(_to_dev_bf16(dy, cuda), _to_dev_bf16(w, cuda), (H, W), st, pad,
+                              res=_to_dev_bf16(res, cuda) if with_res else None)
+    ref = O.conv2d_dgrad(dy, w, (H, W), st, pad)
+    if with_res:
+        ref = ref + res
+    assert rel_err(dx.float().cpu().numpy(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_wgrad(dtc, cuda, case):
+    N, H, W, C, K, R, st = case
+    pad = 1 if R == 3 else 0
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+    g = np.random.default_rng(3)
+    x = _rand_bf16((N, H, W, C), g)
+    dy = _rand_bf16((N, P, Q, K), g)
+    dw = dtc.ops.conv2d_wgrad(_to_dev_bf16(x, cuda), _to_dev_bf16(dy, cuda), R, R, st, pad, scale=0.5)
+    ref = 0.5 * O.conv2d_wgrad(x, dy, R, R, st, pad)
+    # fp32 accumulation of exact bf16 products: only summation-order differences remain
+    assert rel_err(dw.cpu().numpy(), ref) < 1e-5
+
+
+def test_mfma_layout_identity(dtc, cuda):
+    """A = I-style check with an asymmetric operand (guide §3): a 1x1 conv with the identity
+    filter must reproduce x exactly, and a permutation filter must permute channels."""
+    g = np.random.default_rng(4)
+    x = _rand_bf16((2, 4, 4, 64), g)
+    perm = g.permutation(64)
+    w = np.zeros((64, 1, 1, 64), np.float32)
+    w[np.arange(64), 0, 0, perm] = 1.0
+    y = dtc.ops.conv2d_fwd(_to_dev_bf16(x, cuda), _to_dev_bf16(w, cuda), 1, 0).float().cpu().numpy()
+    np.testing.assert_array_equal(y, x[..., perm])
+
+
+@pytest.mark.parametrize("C", [64, 512])
+def test_bn_forward(dtc, cuda, C):
+    M = 300
+    g = np.random.default_rng(5)
+    x = _rand_bf16((M, C), g, 2.0) + 0.5
+    gamma = g.uniform(0.5, 1.5, C).astype(np.float32)
+    beta = g.uniform(-0.5, 0.5, C).astype(np.float32)
+    rm = np.zeros(C, np.float32)
+    rv = np.ones(C, np.float32)
+    dev = cuda
+    stats = dtc.ops.new_stats(C, dev)
+    xs = x.astype(np.float64)
+    stats[0, 0] = torch.from_numpy(xs.sum(0))
+    stats[0, 1] = torch.from_numpy((xs * xs).sum(0))
+    t = lambda a: torch.from_numpy(a).to(dev)
+    rm_d, rv_d = t(rm.copy()), t(rv.copy())
+    nbt = torch.zeros(1, dtype=torch.int64, device=dev)
+    mean, invstd, scale, shift = dtc.ops.bn_fwd_finalize(stats, M, t(gamma), t(beta), rm_d, rv_d, nbt)
+    y_ref, m_ref, is_ref, rm_ref, rv_ref = O.bn_train_fwd(x, gamma, beta, rm, rv)
+    np.testing.assert_allclose(mean.cpu().numpy(), m_ref, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(invstd.cpu().numpy(), is_ref, rtol=1e-5)
+    np.testing.assert_allclose(rm_d.cpu().numpy(), rm_ref, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(rv_d.cpu().numpy(), rv_ref, rtol=1e-5)
+    assert int(nbt.item()) == 1
+    assert float(stats.abs().sum()) == 0.0  # finalize re-zeroes the slots
+    xd = _to_dev_bf16(x, dev)
+    y = dtc.ops.bn_apply_relu(xd, scale, shift).float().cpu().numpy()
+    assert rel_err(y, O.relu(y_ref)) < 1e-2
+    r = _rand_bf16((M, C), g)
+    y2 = dtc.ops.bn_apply_add_relu(xd, scale, shift, _to_dev_bf16(r, dev)).float().cpu().numpy()
+    assert rel_err(y2, O.relu(O.bf16(y_ref) + r)) < 1e-2
+    y3 = dtc.ops.bn_apply_dual_relu(xd, scale, shift, _to_dev_bf16(r, dev), scale, shift).float().cpu().numpy()
+    y_r, *_ = O.bn_train_fwd(x, gamma, beta)
+    yr2 = (r - m_ref) * is_ref * gamma + beta
+    assert rel_err(y3, O.relu(O.bf16(y_ref) + O.bf16(yr2))) < 1e-2
+
+
+@pytest.mark.parametrize("C,dual", [(64, False), (128, True), (512, False)])
+def test_bn_backward(dtc, cuda, C, dual):
+    M = 256
+    g = np.random.default_rng(6)
+    x = _rand_bf16((M, C), g, 1.5) + 0.2
+    x2 = _rand_bf16((M, C), g, 0.7) - 0.1
+    y = _rand_bf16((M, C), g)  # relu output stand-in (mask)
+    dy = _rand_bf16((M, C), g)
+    gamma = g.uniform(0.5, 1.5, C).astype(np.float32)
+    gamma2 = g.uniform(0.5, 1.5, C).astype(np.float32)
+    _, mean, invstd, _, _ = O.bn_train_fwd(x, gamma, np.zeros(C))
+    _, mean2, invstd2, _, _ = O.bn_train_fwd(x2, gamma2, np.zeros(C))
+    dev = cuda
+    t = lambda a: torch.from_numpy(np.asarray(a, np.float32)).to(dev)
+    b = lambda a: _to_dev_bf16(a, dev)
+    dz, acc1, acc2 = dtc.ops.bn_bwd_reduce(b(dy), b(y), b(x), t(mean), t(invstd),
+                                           b(x2) if dual else None, t(mean2) if dual else None,
+                                           t(invstd2) if dual else None)
+    dz_ref = np.where(y > 0, dy, 0)
+    np.testing.assert_array_equal(dz.float().cpu().numpy(), dz_ref)
+    dg, db, coef = dtc.ops.bn_bwd_finalize(acc1, M, t(gamma), t(mean), t(invstd), gscale=0.5)
+    dx_ref, dg_ref, db_ref = O.bn_train_bwd(dz_ref, x, gamma, mean, invstd)
+    np.testing.assert_allclose(dg.cpu().numpy(), 0.5 * dg_ref, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(db.cpu().numpy(), 0.5 * db_ref, rtol=1e-4, atol=1e-4)
+    coef2 = None
+    if dual:
+        dg2, db2, coef2 = dtc.ops.bn_bwd_finalize(acc2, M, t(gamma2), t(mean2), t(invstd2))
+        dx2_ref, dg2_ref, db2_ref = O.bn_train_bwd(dz_ref, x2, gamma2, mean2, invstd2)
+        np.testing.assert_allclose(dg2.cpu().numpy(), dg2_ref, rtol=1e-4, atol=1e-4)
+    dx1, dx2 = dtc.ops.bn_bwd_apply(dz, b(x), coef, b(x2) if dual else None, coef2)
+    assert rel_err(dx1.float().cpu().numpy(), dx_ref) < 1e-2
+    if dual:
+        assert rel_err(dx2.float().cpu().numpy(), dx2_ref) < 1e-2
+
+
+def test_head_and_loss(dtc, cuda):
+    N, C, ncls = 6, 512, 100
+    g = np.random.default_rng(7)
+    act = O.relu(_rand_bf16((N, 4, 4, C), g))
+    w = _rand_bf16((ncls, C), g, 0.05)
+    bias = g.standard_normal(ncls).astype(np.float32) * 0.1
+    labels = g.integers(0, ncls, N)
+    dev = cuda
+    feat, logits = dtc.ops.head_fwd(_to_dev_bf16(act, dev), _to_dev_bf16(w, dev), torch.from_numpy(bias).to(dev))
+    f_ref, l_ref = O.head_fwd(act, w, bias, bf16_mode=True)
+    assert rel_err(feat.cpu().numpy(), f_ref) < 1e-5
+    assert rel_err(logits.cpu().numpy(), l_ref) < 1e-2
+    lab = torch.from_numpy(labels).to(dev)
+    loss, lse = dtc.ops.xent_fwd(logits, lab)
+    loss_ref, dl_ref, lse_ref = O.cross_entropy(logits.cpu().numpy(), labels)
+    assert abs(float(loss) - loss_ref) < 1e-5 * max(1.0, abs(loss_ref))
+    gs = torch.full((1,), 4.0, device=dev)
+    dl = dtc.ops.xent_bwd(logits, lab, lse, gs)
+    np.testing.assert_allclose(dl.cpu().numpy(), 4.0 * dl_ref, rtol=1e-4, atol=1e-6)
+    dw, db, dact = dtc.ops.head_bwd(dl, feat, _to_dev_bf16(w, dev), (4, 4), scale=0.25)
+    dw_ref, db_ref, dact_ref = O.head_bwd(dl.cpu().numpy(), feat.cpu().numpy(), w, (4, 4))
+    assert rel_err(dw.cpu().numpy(), 0.25 * dw_ref) < 1e-5
+    assert rel_err(db.cpu().numpy(), 0.25 * db_ref) < 1e-5
+    assert rel_err(dact.float().cpu().numpy(), dact_ref) < 1e-2
+
+
+def test_stem_im2col(dtc, cuda):
+    g = np.random.default_rng(8)
+    x = g.standard_normal((2, 3, 6, 5)).astype(np.float32)
+    cols = dtc.ops.stem_im2col(torch.from_numpy(x).to(cuda)).float().cpu().numpy()
+    ref = O._im2col(O.nchw_to_nhwc(x), 3, 3, 1, 1).reshape(2, 6, 5, 27)
+    np.testing.assert_array_equal(cols[..., :27], O.bf16(ref))
+    assert not cols[..., 27:].any()
+
+
+def test_sgd_and_amp(dtc, cuda):
+    n = 4096
+    g = np.random.default_rng(9)
+    p = g.standard_normal(n).astype(np.float32)
+    dev = cuda
+    P = torch.from_numpy(p.copy()).to(dev)
+    M = torch.zeros(n, device=dev)
+    PB = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    inv = torch.full((1,), 0.25, device=dev)
+    found = torch.zeros(1, dtype=torch.int32, device=dev)
+    pr, buf = p.copy(), None
+    for step in range(3):
+        grad = g.standard_normal(n).astype(np.float32)
+        dtc.ops.sgd_nesterov_flat(P, torch.from_numpy(grad * 4).to(dev), M, PB, 0.1, 1e-4, 0.9, inv, found)
+        pr, buf = O.sgd_nesterov(pr, grad, buf, 0.1, 1e-4, 0.9, step == 0)
+    np.testing.assert_allclose(P.cpu().numpy(), pr, rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(PB.float().cpu().numpy(), O.bf16(P.cpu().numpy()))
+    # overflow: check sets found_inf, the step is skipped, the scale backs off
+    bad = torch.zeros(n, device=dev)
+    bad[17] = float("inf")
+    dtc.ops.amp_check_finite(bad, found)
+    assert int(found.item()) == 1
+    before = P.clone()
+    dtc.ops.sgd_nesterov_flat(P, bad, M, PB, 0.1, 1e-4, 0.9, inv, found)
+    assert torch.equal(before, P)
+    scale = torch.full((1,), 65536.0, device=dev)
+    tracker = torch.zeros(1, dtype=torch.int32, device=dev)
+    dtc.ops.amp_update_scale(scale, inv, tracker, found, 2.0, 0.5, 3)
+    assert float(scale) == 32768.0 and int(found.item()) == 0
+    for _ in range(3):
+        dtc.ops.amp_update_scale(scale, inv, tracker, found, 2.0, 0.5, 3)
+    assert float(scale) == 65536.0 and abs(float(inv) - 1 / 65536.0) < 1e-12
