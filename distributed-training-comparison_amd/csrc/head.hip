@@ -61,70 +61,98 @@ int stem_pack_weight(const u16* w27, u16* w64, int K, hipStream_t st) {
   return 0;
 }
 
-// one workgroup per image
-__global__ void __launch_bounds__(256) head_fwd_kernel(const u16* __restrict__ act, int HW, int C,
+// 4 images per workgroup: pooled features in LDS, then one thread per class computes the 4 dot
+// products with 16-byte weight loads (C % 8 == 0).
+constexpr int HEAD_IMGS = 4;
+__global__ void __launch_bounds__(256) head_fwd_kernel(const u16* __restrict__ act, int N, int HW, int C,
                                                       const u16* __restrict__ wfc, const float* __restrict__ bfc,
                                                       int ncls, float* __restrict__ feat,
                                                       float* __restrict__ logits) {
-  extern __shared__ float f[];
-  const int n = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const u16* a = act + (int64_t)n * HW * C;
+  extern __shared__ float f[];  // [HEAD_IMGS][C]
+  const int n0 = blockIdx.x * HEAD_IMGS, t = threadIdx.x;
   const float inv = 1.f / (float)HW;
-  for (int c = t; c < C; c += 256) {
-    float s = 0.f;
-    for (int p = 0; p < HW; ++p) s += bf2f(a[(int64_t)p * C + c]);
-    const float v = round_bf(s * inv);  // avg_pool2d output is bf16 under autocast
-    f[c] = v;
-    feat[(int64_t)n * C + c] = v;
+  for (int e = t; e < HEAD_IMGS * C; e += 256) {
+    const int i = e / C, c = e - i * C;
+    float v = 0.f;
+    if (n0 + i < N) {
+      const u16* a = act + (int64_t)(n0 + i) * HW * C + c;
+      float s = 0.f;
+      for (int p = 0; p < HW; ++p) s += bf2f(a[(int64_t)p * C]);
+      v = round_bf(s * inv);  // avg_pool2d output is bf16 under autocast
+      feat[(int64_t)(n0 + i) * C + c] = v;
+    }
+    f[e] = v;
   }
   __syncthreads();
-  for (int j = wave; j < ncls; j += 4) {
-    float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += f[c] * bf2f(wfc[(int64_t)j * C + c]);
-    s = wave_sum(s);
-    if (lane == 0) logits[(int64_t)n * ncls + j] = round_bf(s + round_bf(bfc[j]));  // bf16 linear under autocast
+  for (int j = t; j < ncls; j += 256) {
+    float acc[HEAD_IMGS] = {0.f, 0.f, 0.f, 0.f};
+    const uint4* w = (const uint4*)(wfc + (int64_t)j * C);
+    for (int c8 = 0; c8 < C / 8; ++c8) {
+      float wv[8];
+      unpack8(w[c8], wv);
+#pragma unroll
+      for (int i = 0; i < HEAD_IMGS; ++i) {
+        const float* fi = f + i * C + c8 * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[i] += fi[k] * wv[k];
+      }
+    }
+    const float b = round_bf(bfc[j]);
+#pragma unroll
+    for (int i = 0; i < HEAD_IMGS; ++i)
+      if (n0 + i < N) logits[(int64_t)(n0 + i) * ncls + j] = round_bf(acc[i] + b);  // bf16 linear under autocast
   }
 }
 
 int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st) {
-  DTC_CHECK_ARG(act && wfc && bfc && feat && logits && N > 0 && HW > 0 && C > 0 && ncls > 0, "head_fwd: bad args");
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(N), dim3(256), C * sizeof(float), st, act, HW, C, wfc, bfc, ncls, feat,
-                     logits);
+  DTC_CHECK_ARG(act && wfc && bfc && feat && logits && N > 0 && HW > 0 && C > 0 && C % 8 == 0 && ncls > 0,
+                "head_fwd: bad args");
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((N + HEAD_IMGS - 1) / HEAD_IMGS), dim3(256),
+                     HEAD_IMGS * C * sizeof(float), st, act, N, HW, C, wfc, bfc, ncls, feat, logits);
   DTC_LAUNCH_CHECK();
   return 0;
 }
 
-// single workgroup: deterministic mean over the batch
-__global__ void __launch_bounds__(256) xent_fwd_kernel(const float* __restrict__ logits,
-                                                      const int64_t* __restrict__ labels, int N, int ncls,
-                                                      float* __restrict__ loss, float* __restrict__ lse) {
+// per-row log-sum-exp: one wave per row
+__global__ void __launch_bounds__(256) xent_lse_kernel(const float* __restrict__ logits, int N, int ncls,
+                                                      float* __restrict__ lse) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= N) return;
+  const float* z = logits + (int64_t)b * ncls;
+  float m = -INFINITY;
+  for (int j = lane; j < ncls; j += 64) m = fmaxf(m, z[j]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int j = lane; j < ncls; j += 64) s += expf(z[j] - m);
+  s = wave_sum(s);
+  if (lane == 0) lse[b] = m + logf(s);
+}
+
+// loss = mean_b (lse[b] - z[b][y_b]); one workgroup, fixed summation order
+__global__ void __launch_bounds__(256) xent_mean_kernel(const float* __restrict__ logits,
+                                                       const int64_t* __restrict__ labels,
+                                                       const float* __restrict__ lse, int N, int ncls,
+                                                       float* __restrict__ loss) {
   __shared__ float part[4];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x;
   float acc = 0.f;
-  for (int b = wave; b < N; b += 4) {
-    const float* z = logits + (int64_t)b * ncls;
-    float m = -INFINITY;
-    for (int j = lane; j < ncls; j += 64) m = fmaxf(m, z[j]);
-    m = wave_max(m);
-    float s = 0.f;
-    for (int j = lane; j < ncls; j += 64) s += expf(z[j] - m);
-    s = wave_sum(s);
-    const float l = m + logf(s);
-    if (lane == 0) {
-      lse[b] = l;
-      const int64_t y = labels[b];
-      acc += (y >= 0 && y < ncls) ? (l - z[y]) : NAN;
-    }
+  for (int b = t; b < N; b += 256) {
+    const int64_t y = labels[b];
+    acc += (y >= 0 && y < ncls) ? (lse[b] - logits[(int64_t)b * ncls + y]) : NAN;
   }
-  if (lane == 0) part[wave] = acc;
+  acc = wave_sum(acc);
+  if ((t & 63) == 0) part[t >> 6] = acc;
   __syncthreads();
   if (t == 0) *loss = (part[0] + part[1] + part[2] + part[3]) / (float)N;
 }
 
 int xent_fwd(const float* logits, const int64_t* labels, int N, int ncls, float* loss, float* lse, hipStream_t st) {
   DTC_CHECK_ARG(logits && labels && loss && lse && N > 0 && ncls > 0, "xent_fwd: bad args");
-  hipLaunchKernelGGL(xent_fwd_kernel, dim3(1), dim3(256), 0, st, logits, labels, N, ncls, loss, lse);
+  hipLaunchKernelGGL(xent_lse_kernel, dim3((N + 3) / 4), dim3(256), 0, st, logits, N, ncls, lse);
+  DTC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(xent_mean_kernel, dim3(1), dim3(256), 0, st, logits, labels, lse, N, ncls, loss);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -153,21 +181,41 @@ int xent_bwd(const float* logits, const int64_t* labels, const float* lse, const
 }
 
 // dW[j][c] = scale * sum_n dl[n][j] * feat[n][c]; db[j] = scale * sum_n dl[n][j]
+// workgroup tile: 16 classes x 64 channels; thread = 1 channel x 4 classes; images streamed in order.
 __global__ void __launch_bounds__(256) head_bwd_w_kernel(const float* __restrict__ dl, const float* __restrict__ feat,
                                                         int N, int C, int ncls, float scale, float* __restrict__ dw,
                                                         float* __restrict__ db) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  const int j = blockIdx.y;
+  __shared__ float dls[64][16];
+  const int t = threadIdx.x;
+  const int c = blockIdx.x * 64 + (t & 63);
+  const int j0 = blockIdx.y * 16 + (t >> 6) * 4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.f;
+  for (int nb = 0; nb < N; nb += 64) {
+    __syncthreads();
+    for (int e = t; e < 64 * 16; e += 256) {
+      const int n = nb + (e >> 4), j = blockIdx.y * 16 + (e & 15);
+      dls[e >> 4][e & 15] = (n < N && j < ncls) ? dl[(int64_t)n * ncls + j] : 0.f;
+    }
+    __syncthreads();
+    const int nn = min(64, N - nb);
+    if (c < C) {
+#pragma unroll 8
+      for (int i = 0; i < nn; ++i) {
+        const float fv = feat[(int64_t)(nb + i) * C + c];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] += dls[i][(t >> 6) * 4 + q] * fv;
+      }
+    }
+    if (blockIdx.x == 0 && t < 16)
+      for (int i = 0; i < nn; ++i) dbs += dls[i][t];
+  }
   if (c < C) {
-    float s = 0.f;
-    for (int n = 0; n < N; ++n) s += dl[(int64_t)n * ncls + j] * feat[(int64_t)n * C + c];
-    dw[(int64_t)j * C + c] = s * scale;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (j0 + q < ncls) dw[(int64_t)(j0 + q) * C + c] = acc[q] * scale;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float s = 0.f;
-    for (int n = 0; n < N; ++n) s += dl[(int64_t)n * ncls + j];
-    db[j] = s * scale;
-  }
+  if (blockIdx.x == 0 && t < 16 && blockIdx.y * 16 + t < ncls) db[blockIdx.y * 16 + t] = dbs * scale;
 }
 
 // dact[n][p][c] = (sum_j dl[n][j] * W[j][c]) / HW
@@ -191,8 +239,8 @@ int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int
              float* dw, float* db, u16* dact, hipStream_t st) {
   DTC_CHECK_ARG(dlogits && feat && wfc && dw && db && dact && N > 0 && HW > 0 && C > 0 && ncls > 0,
                 "head_bwd: bad args");
-  hipLaunchKernelGGL(head_bwd_w_kernel, dim3((C + 255) / 256, ncls), dim3(256), 0, st, dlogits, feat, N, C, ncls,
-                     scale, dw, db);
+  hipLaunchKernelGGL(head_bwd_w_kernel, dim3((C + 63) / 64, (ncls + 15) / 16), dim3(256), 0, st, dlogits, feat, N,
+                     C, ncls, scale, dw, db);
   DTC_LAUNCH_CHECK();
   hipLaunchKernelGGL(head_bwd_x_kernel, dim3(N), dim3(256), ncls * sizeof(float), st, dlogits, wfc, HW, C, ncls,
                      dact);

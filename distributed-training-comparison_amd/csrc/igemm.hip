@@ -478,25 +478,39 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 }
 
 // ---------------------------------------------------------------- wgrad split reduction
-// grad[k][c] (row stride ld_out, first ncols columns) = scale * sum_s slab[s][k][c] (row stride ld_in)
+// grad[k][c] (row stride ld_out, first ncols columns) = scale * sum_s slab[s][k][c] (row stride ld_in).
+// A workgroup owns 256/SG output float4s; SG lanes per output stride over the splits (independent
+// loads in flight), then combine through LDS in a fixed order (deterministic).
+template <int SG>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K,
                                                            int ld_in, int ncols, int ld_out, float scale,
                                                            float* __restrict__ grad) {
+  constexpr int OPB = 256 / SG;  // outputs (float4) per block
+  __shared__ f32x4 red[256];
   const size_t plane = (size_t)K * ld_in;
-  if (ncols == ld_in && ld_out == ld_in && (ld_in & 3) == 0) {
-    const size_t n4 = plane >> 2;
-    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
-      f32x4 a = *(const f32x4*)(slab + i * 4);
-      for (int sp = 1; sp < splits; ++sp) a += *(const f32x4*)(slab + sp * plane + i * 4);
-      *(f32x4*)(grad + i * 4) = a * scale;
-    }
-  } else {
-    const size_t n = (size_t)K * ncols;
-    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-      const int k = (int)(i / ncols), c = (int)(i % ncols);
-      float a = 0.f;
-      for (int sp = 0; sp < splits; ++sp) a += slab[sp * plane + (size_t)k * ld_in + c];
-      grad[(size_t)k * ld_out + c] = a * scale;
+  const int t = threadIdx.x;
+  const int o = t / SG, sg = t % SG;
+  const size_t v = (size_t)blockIdx.x * OPB + o;  // float4 index over [K][ld_in]
+  const size_t nv = plane >> 2;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (v < nv) {
+#pragma unroll 4
+    for (int sp = sg; sp < splits; sp += SG) a += *(const f32x4*)(slab + sp * plane + v * 4);
+  }
+  red[t] = a;
+  __syncthreads();
+  if (sg == 0 && v < nv) {
+#pragma unroll
+    for (int k = 1; k < SG; ++k) a += red[t + k];
+    a *= scale;
+    if (ncols == ld_in && ld_out == ld_in) {
+      *(f32x4*)(grad + v * 4) = a;
+    } else {
+      const size_t e = v * 4;
+      const int k = (int)(e / ld_in), c = (int)(e % ld_in);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (c + j < ncols) grad[(size_t)k * ld_out + c + j] = a[j];
     }
   }
 }
@@ -540,10 +554,12 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
     const int M = (mode == CONV_FWD) ? s.N * P * Q : s.N * s.H * s.W;
     const int A = (mode == CONV_FWD) ? s.K : s.C;
     const int num_kt = s.R * s.S * ((mode == CONV_FWD) ? s.C : s.K) / 64;
-    pl.bm = (A == 64) ? 64 : 128;
-    pl.bn = (A == 64) ? 256 : 128;
+    // big tiles while they fill the chip (>= ~2 waves of 256 CUs), else 64x64 tiles, else split-K
+    if (A == 64) { pl.bm = 64; pl.bn = 256; }
+    else { pl.bm = 128; pl.bn = 128; }
+    if ((A / pl.bm) * ceil_div(M, pl.bn) < 400) { pl.bm = 64; pl.bn = 64; }
     const int tiles = (A / pl.bm) * ceil_div(M, pl.bn);
-    pl.splits = pick_splits(tiles, num_kt, 480, 8);
+    pl.splits = tiles >= 256 ? 1 : pick_splits(tiles, num_kt, 480, 8);
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * M * A * 4 : 0;
     pl.num_kt = num_kt;
   } else {
@@ -552,7 +568,7 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
     pl.bm = (s.C == 64 || s.K == 64) ? 64 : 128;
     pl.bn = pl.bm;
     const int tiles = (s.R * s.S * s.C / pl.bm) * (s.K / pl.bn);
-    pl.splits = pick_splits(tiles, num_kt, 512, 16);
+    pl.splits = pick_splits(tiles, num_kt, 512, 32);
     pl.slab_bytes = (size_t)pl.splits * s.K * s.R * s.S * s.C * 4;
     pl.num_kt = num_kt;
   }
@@ -576,10 +592,12 @@ int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* sta
   splits = ceil_div(p.num_kt, p.kt_per_split);
   if (splits > 1) {
     p.slab = slab;
-    if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_FWD, 64, 256, 1, 4, true>(p, tiles_b, splits, st)));
+    if (pl.bn == 64) DTC_TRY((launch_igemm<MODE_FWD, 64, 64, 2, 2, true>(p, tiles_b, splits, st)));
+    else if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_FWD, 64, 256, 1, 4, true>(p, tiles_b, splits, st)));
     else DTC_TRY((launch_igemm<MODE_FWD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
     return splitk_reduce(slab, splits, p.M, s.K, y, nullptr, stats, st);
   }
+  if (pl.bn == 64) return launch_igemm<MODE_FWD, 64, 64, 2, 2, false>(p, tiles_b, 1, st);
   if (pl.bm == 64) return launch_igemm<MODE_FWD, 64, 256, 1, 4, false>(p, tiles_b, 1, st);
   return launch_igemm<MODE_FWD, 128, 128, 2, 2, false>(p, tiles_b, 1, st);
 }
@@ -601,10 +619,12 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
   splits = ceil_div(p.num_kt, p.kt_per_split);
   if (splits > 1) {
     p.slab = slab;
-    if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 256, 1, 4, true>(p, tiles_b, splits, st)));
+    if (pl.bn == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 64, 2, 2, true>(p, tiles_b, splits, st)));
+    else if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 256, 1, 4, true>(p, tiles_b, splits, st)));
     else DTC_TRY((launch_igemm<MODE_DGRAD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
     return splitk_reduce(slab, splits, p.M, s.C, dx, res, nullptr, st);
   }
+  if (pl.bn == 64) return launch_igemm<MODE_DGRAD, 64, 64, 2, 2, false>(p, tiles_b, 1, st);
   if (pl.bm == 64) return launch_igemm<MODE_DGRAD, 64, 256, 1, 4, false>(p, tiles_b, 1, st);
   return launch_igemm<MODE_DGRAD, 128, 128, 2, 2, false>(p, tiles_b, 1, st);
 }
@@ -629,10 +649,17 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
   else DTC_TRY((launch_igemm<MODE_WGRAD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
   const int ncols = dw_cols > 0 ? dw_cols : p.RSC;
   const int ldo = dw_ld > 0 ? dw_ld : p.RSC;
-  const size_t work = (size_t)s.K * ncols / 4 + 1;
-  const int blocks = (int)std::min<size_t>(2048, (work + 255) / 256);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo,
-                     scale, dw);
+  const size_t nv = (size_t)s.K * p.RSC / 4;
+  int sg = 1;
+  while (sg < 16 && sg * 2 <= splits && (nv * sg) / 256 < 1024) sg *= 2;
+  const int blocks = (int)((nv + (256 / sg) - 1) / (256 / sg));
+  switch (sg) {
+    case 1: hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw); break;
+    case 2: hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw); break;
+    case 4: hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw); break;
+    case 8: hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw); break;
+    default: hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw); break;
+  }
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -642,7 +669,8 @@ int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const 
   DTC_CHECK_ARG(Nc % 8 == 0 && Nc <= 2048, "splitk_reduce: channels %d", Nc);
   const int tpr = Nc / 8;
   const int rpp = 256 / tpr;
-  int rows_per_block = std::max(rpp, 64);
+  // about 1024 workgroups; each a whole number of 256-thread passes
+  int rows_per_block = std::max(rpp, (M + 1023) / 1024);
   rows_per_block = ((rows_per_block + rpp - 1) / rpp) * rpp;
   const int blocks = ceil_div(M, rows_per_block);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, splits, M, Nc, out, res, stats,

@@ -122,6 +122,23 @@ class Executor:
         call("dtc_rn18_backward", self.handle, ptr(dlogits), float(grad_scale), comm.handle if comm else None,
              stream_ptr())
 
+    def activations(self) -> Dict[str, torch.Tensor]:
+        """Views of the per-layer activations the last forward left in the workspace (NHWC)."""
+        base = self.ws_ptr - self.workspace.data_ptr()
+        out = {}
+        for i in range(lib.dtc_rn18_num_activations(self.handle)):
+            name = C.c_char_p()
+            off = C.c_size_t()
+            shp = (C.c_int * 4)()
+            call("dtc_rn18_activation_info", self.handle, i, C.byref(name), C.byref(off), shp)
+            nm = name.value.decode()
+            dt = torch.float32 if nm.endswith("_f32") else torch.bfloat16
+            numel = shp[0] * shp[1] * shp[2] * shp[3]
+            nbytes = numel * (4 if dt == torch.float32 else 2)
+            o = base + off.value
+            out[nm] = self.workspace[o:o + nbytes].view(dt).view(shp[0], shp[1], shp[2], shp[3])
+        return out
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h:

@@ -103,7 +103,7 @@ def test_mfma_layout_identity(dtc, cuda):
 def test_bn_forward(dtc, cuda, C):
     M = 300
     g = np.random.default_rng(5)
-    x = _rand_bf16((M, C), g, 2.0) + 0.5
+    x = O.bf16(_rand_bf16((M, C), g, 2.0) + 0.5)
     gamma = g.uniform(0.5, 1.5, C).astype(np.float32)
     beta = g.uniform(-0.5, 0.5, C).astype(np.float32)
     rm = np.zeros(C, np.float32)
@@ -140,8 +140,8 @@ def test_bn_forward(dtc, cuda, C):
 def test_bn_backward(dtc, cuda, C, dual):
     M = 256
     g = np.random.default_rng(6)
-    x = _rand_bf16((M, C), g, 1.5) + 0.2
-    x2 = _rand_bf16((M, C), g, 0.7) - 0.1
+    x = O.bf16(_rand_bf16((M, C), g, 1.5) + 0.2)
+    x2 = O.bf16(_rand_bf16((M, C), g, 0.7) - 0.1)
     y = _rand_bf16((M, C), g)  # relu output stand-in (mask)
     dy = _rand_bf16((M, C), g)
     gamma = g.uniform(0.5, 1.5, C).astype(np.float32)
@@ -221,7 +221,8 @@ def test_sgd_and_amp(dtc, cuda):
         grad = g.standard_normal(n).astype(np.float32)
         dtc.ops.sgd_nesterov_flat(P, torch.from_numpy(grad * 4).to(dev), M, PB, 0.1, 1e-4, 0.9, inv, found)
         pr, buf = O.sgd_nesterov(pr, grad, buf, 0.1, 1e-4, 0.9, step == 0)
-    np.testing.assert_allclose(P.cpu().numpy(), pr, rtol=1e-6, atol=1e-7)
+    # fp32 update; FMA contraction may move the last bit
+    np.testing.assert_allclose(P.cpu().numpy(), pr, rtol=1e-6, atol=1e-6)
     np.testing.assert_array_equal(PB.float().cpu().numpy(), O.bf16(P.cpu().numpy()))
     # overflow: check sets found_inf, the step is skipped, the scale backs off
     bad = torch.zeros(n, device=dev)
