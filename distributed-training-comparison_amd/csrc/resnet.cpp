@@ -84,6 +84,9 @@ struct Net {
   // activation registry (per-layer parity): name, workspace byte offset, N,H,W,C
   struct Act { std::string name; size_t off; int n, h, w, c; };
   std::vector<Act> acts;
+  // optional capture of backward intermediates (parity tests): name -> slot in the workspace
+  bool capture = false;
+  std::vector<Act> caps;
   // bound memory
   char* ws = nullptr;
   float* p = nullptr;
@@ -215,6 +218,11 @@ static int build(Net& n) {
 }
 
 static void plan_workspace(Net& n, float bucket_cap_mb) {
+  n.acts.clear();
+  n.caps.clear();
+  n.bucket_off.clear();
+  n.bucket_len.clear();
+  n.bucket_after_block.clear();
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -280,6 +288,23 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   }
   n.slab_bytes = slab;
   n.SLAB = take(slab);
+  if (n.capture) {
+    auto cap = [&](const std::string& nm, int h, int w, int c) {
+      n.caps.push_back({nm, take((size_t)B * h * w * c * 2), (int)B, h, w, c});
+    };
+    for (size_t i = 0; i < n.blocks.size(); ++i) {
+      const BlockL& b = n.blocks[i];
+      const std::string pre = "grad.layer" + std::to_string(i / 2 + 1) + "." + std::to_string(i % 2);
+      for (const char* k : {".dy", ".dz", ".dc2", ".da1", ".dz1", ".dc1"}) cap(pre + k, b.Hout, b.Wout, b.Cout);
+      if (b.proj) {
+        cap(pre + ".ds", b.Hout, b.Wout, b.Cout);
+        cap(pre + ".dxs", b.Hin, b.Win, b.Cin);
+      }
+      cap(pre + ".dx", b.Hin, b.Win, b.Cin);
+    }
+    cap("grad.stem.dz", n.H, n.W, 64);
+    cap("grad.stem.dc", n.H, n.W, 64);
+  }
   n.ws_bytes = off;
 
   // gradient buckets at block granularity in backward order (head + layer4.1 first); a bucket
@@ -389,6 +414,16 @@ static int maybe_bucket(Net& n, int after_block, Comm* comm, hipStream_t st) {
   return 0;
 }
 
+static int cap(Net& n, const std::string& name, const void* src, hipStream_t st) {
+  if (!n.capture) return 0;
+  for (const auto& a : n.caps)
+    if (a.name == name) {
+      DTC_HIP(hipMemcpyAsync(n.ws + a.off, src, (size_t)a.n * a.h * a.w * a.c * 2, hipMemcpyDeviceToDevice, st));
+      return 0;
+    }
+  return set_error(DTC_EINVAL, "capture slot %s missing", name.c_str());
+}
+
 static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st) {
   u16* G[6];
   for (int i = 0; i < 6; ++i) G[i] = n.at<u16>(n.G[i]);
@@ -400,6 +435,8 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
     BlockL& b = n.blocks[bi];
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
     const u16* in = bi > 0 ? n.at<u16>(n.blocks[bi - 1].OUT) : n.at<u16>(n.A0);
+    const std::string cp = n.capture ? "grad.layer" + std::to_string(bi / 2 + 1) + "." + std::to_string(bi % 2) : "";
+    DTC_TRY(cap(n, cp + ".dy", G[0], st));
     // out = relu(bn2(c2) + shortcut): dz = dy * [out > 0]
     DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(b.OUT), n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
                           n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
@@ -414,17 +451,23 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
                               n.at<float>(b.bsc.coef), st));
     DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(b.C2), n.at<float>(b.b2.coef), G[2], b.proj ? n.at<u16>(b.S) : nullptr,
                          b.proj ? n.at<float>(b.bsc.coef) : nullptr, b.proj ? G[3] : nullptr, M, b.Cout, st));
+    DTC_TRY(cap(n, cp + ".dz", G[1], st));
+    DTC_TRY(cap(n, cp + ".dc2", G[2], st));
+    if (b.proj) DTC_TRY(cap(n, cp + ".ds", G[3], st));
     // conv2: dW2 and da1
     PROF(2, conv_flops(b.c2.s), conv_wgrad(b.c2.s, n.at<u16>(b.A1), G[2], n.gf(b.c2.pidx), 0, 0, gs, slab, n.slab_bytes, st));
     PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, G[2], n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st));
+    DTC_TRY(cap(n, cp + ".da1", G[4], st));
     // a1 = relu(bn1(c1))
     DTC_TRY(bn_bwd_reduce(G[4], n.at<u16>(b.A1), n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
                           n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, G[4], M, b.Cout, st));
     DTC_TRY(bn_bwd_finalize(n.at<double>(b.b1.acc), b.Cout, M, n.pf(b.b1.gidx), n.at<float>(b.b1.mean),
                             n.at<float>(b.b1.invstd), gs, n.gf(b.b1.gidx), n.gf(b.b1.bidx), n.at<float>(b.b1.coef),
                             st));
+    DTC_TRY(cap(n, cp + ".dz1", G[4], st));
     DTC_TRY(bn_bwd_apply(G[4], n.at<u16>(b.C1), n.at<float>(b.b1.coef), G[2], nullptr, nullptr, nullptr, M, b.Cout,
                          st));
+    DTC_TRY(cap(n, cp + ".dc1", G[2], st));
     // conv1 (+ shortcut): weight grads, then the block-input gradient with the residual fused
     PROF(2, conv_flops(b.c1.s), conv_wgrad(b.c1.s, in, G[2], n.gf(b.c1.pidx), 0, 0, gs, slab, n.slab_bytes, st));
     if (b.proj) {
@@ -434,6 +477,8 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
     } else {
       PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[1], slab, n.slab_bytes, st));
     }
+    if (b.proj) DTC_TRY(cap(n, cp + ".dxs", G[5], st));
+    DTC_TRY(cap(n, cp + ".dx", G[0], st));
     DTC_TRY(maybe_bucket(n, bi, comm, st));
   }
   // stem: a0 = relu(bn1(conv1(x)))
@@ -444,6 +489,8 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
                           n.at<float>(n.bn0.invstd), gs, n.gf(n.bn0.gidx), n.gf(n.bn0.bidx), n.at<float>(n.bn0.coef),
                           st));
   DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(n.C0), n.at<float>(n.bn0.coef), G[2], nullptr, nullptr, nullptr, M0, 64, st));
+  DTC_TRY(cap(n, "grad.stem.dz", G[1], st));
+  DTC_TRY(cap(n, "grad.stem.dc", G[2], st));
   PROF(2, 2.0 * M0 * 64 * 27,
        conv_wgrad(n.stem.s, n.at<u16>(n.X0), G[2], n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st));
   DTC_TRY(maybe_bucket(n, -1, comm, st));
@@ -458,6 +505,7 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
 
 struct dtc_net {
   dtc::Net n;
+  float bucket_cap_mb = 25.f;
 };
 
 using namespace dtc;
@@ -478,6 +526,7 @@ int dtc_rn18_create(dtc_net** out, int batch, int height, int width, int num_cla
     delete h;
     return r;
   }
+  h->bucket_cap_mb = bucket_cap_mb;
   plan_workspace(h->n, bucket_cap_mb);
   *out = h;
   return 0;
@@ -549,6 +598,26 @@ int dtc_rn18_bind(dtc_net* net, void* workspace, float* params, float* grads, ui
   n.bufs = bufs;
   n.nbt = num_batches_tracked;
   DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.stats_hi - n.stats_lo, (hipStream_t)stream));
+  return 0;
+}
+
+int dtc_rn18_enable_capture(dtc_net* net) {
+  DTC_CHECK_ARG(net && net->n.ws == nullptr, "dtc_rn18_enable_capture: call before dtc_rn18_bind");
+  net->n.capture = true;
+  plan_workspace(net->n, net->bucket_cap_mb);
+  return 0;
+}
+
+int dtc_rn18_num_captures(const dtc_net* net) { return net ? (int)net->n.caps.size() : DTC_EINVAL; }
+
+int dtc_rn18_capture_info(const dtc_net* net, int idx, const char** name, size_t* ws_offset, int* shape4) {
+  DTC_CHECK_ARG(net && idx >= 0 && idx < (int)net->n.caps.size(), "dtc_rn18_capture_info: bad index");
+  const auto& a = net->n.caps[idx];
+  if (name) *name = a.name.c_str();
+  if (ws_offset) *ws_offset = a.off;
+  if (shape4) {
+    shape4[0] = a.n; shape4[1] = a.h; shape4[2] = a.w; shape4[3] = a.c;
+  }
   return 0;
 }
 

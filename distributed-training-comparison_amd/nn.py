@@ -99,9 +99,12 @@ class FlatState:
 class Executor:
     """One native executor (plan + workspace) for a fixed (batch, height, width)."""
 
-    def __init__(self, flat: FlatState, batch: int, height: int, width: int, num_classes: int, bucket_cap_mb: float):
+    def __init__(self, flat: FlatState, batch: int, height: int, width: int, num_classes: int, bucket_cap_mb: float,
+                 capture: bool = False):
         self.handle = C.c_void_p()
         call("dtc_rn18_create", C.byref(self.handle), batch, height, width, num_classes, float(bucket_cap_mb))
+        if capture:
+            call("dtc_rn18_enable_capture", self.handle)
         nbytes = lib.dtc_rn18_workspace_bytes(self.handle)
         # 256-byte aligned workspace (the caching allocator returns 512-byte aligned blocks)
         self.workspace = torch.empty(nbytes + 256, dtype=torch.uint8, device=flat.device)
@@ -122,15 +125,18 @@ class Executor:
         call("dtc_rn18_backward", self.handle, ptr(dlogits), float(grad_scale), comm.handle if comm else None,
              stream_ptr())
 
-    def activations(self) -> Dict[str, torch.Tensor]:
-        """Views of the per-layer activations the last forward left in the workspace (NHWC)."""
+    def activations(self, captures: bool = False) -> Dict[str, torch.Tensor]:
+        """Views of the per-layer activations the last forward left in the workspace (NHWC); with
+        captures=True the backward intermediates recorded by a capture-enabled executor."""
         base = self.ws_ptr - self.workspace.data_ptr()
         out = {}
-        for i in range(lib.dtc_rn18_num_activations(self.handle)):
+        count = lib.dtc_rn18_num_captures if captures else lib.dtc_rn18_num_activations
+        info = "dtc_rn18_capture_info" if captures else "dtc_rn18_activation_info"
+        for i in range(count(self.handle)):
             name = C.c_char_p()
             off = C.c_size_t()
             shp = (C.c_int * 4)()
-            call("dtc_rn18_activation_info", self.handle, i, C.byref(name), C.byref(off), shp)
+            call(info, self.handle, i, C.byref(name), C.byref(off), shp)
             nm = name.value.decode()
             dt = torch.float32 if nm.endswith("_f32") else torch.bfloat16
             numel = shp[0] * shp[1] * shp[2] * shp[3]
@@ -236,7 +242,7 @@ class ResNet(nn.Module):
         self._comm = None
         self._grad_scale = 1.0
         self._bucket_cap_mb = float(bucket_cap_mb)
-        self._dirty = False
+        self._capture = False
 
     def _make_layer(self, block, planes, num_blocks, stride):
         strides = [stride] + [1] * (num_blocks - 1)
@@ -333,9 +339,15 @@ class ResNet(nn.Module):
         key = (batch, height, width)
         exe = self._executors.get(key)
         if exe is None:
-            exe = Executor(self.flat, batch, height, width, self.num_classes, self._bucket_cap_mb)
+            exe = Executor(self.flat, batch, height, width, self.num_classes, self._bucket_cap_mb,
+                           capture=self._capture)
             self._executors[key] = exe
         return exe
+
+    def enable_capture(self, on: bool = True):
+        """Keep backward intermediates for per-layer parity tests (new executors only)."""
+        self._capture = on
+        self._executors.clear()
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor) -> torch.Tensor:

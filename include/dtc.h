@@ -165,6 +165,12 @@ int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_
  * fp32 "head.feat_f32"): name, byte offset into the workspace, {n, h, w, c}. For parity tests. */
 int dtc_rn18_num_activations(const dtc_net* net);
 int dtc_rn18_activation_info(const dtc_net* net, int idx, const char** name, size_t* ws_offset, int* shape4);
+/* Opt-in (before dtc_rn18_bind): keep copies of the backward's activation gradients per block
+ * ("grad.layer2.0.dz", ".dc2", ".ds", ".da1", ".dz1", ".dc1", ".dxs", ".dx", "grad.stem.dz/dc") in
+ * extra workspace, for teacher-forced per-layer parity tests. */
+int dtc_rn18_enable_capture(dtc_net* net);
+int dtc_rn18_num_captures(const dtc_net* net);
+int dtc_rn18_capture_info(const dtc_net* net, int idx, const char** name, size_t* ws_offset, int* shape4);
 /* Live timing of every convolution call (forward, dgrad, wgrad incl. split-K reductions) with HIP
  * events on the compute stream, between begin and end; end() synchronizes on the recorded events
  * and returns per-pass totals: index 0 = forward, 1 = dgrad, 2 = wgrad (ms, algorithmic FLOPs, calls). */

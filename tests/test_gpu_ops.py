@@ -24,6 +24,9 @@ CONV_CASES = [
     (4, 4, 4, 512, 512, 3, 1),    # layer4 conv (deep reduction, split-K)
     (2, 32, 32, 64, 64, 1, 1),    # stem GEMM over the 64-column im2col image
     (1, 5, 7, 64, 64, 3, 1),      # odd spatial size, M not a tile multiple
+    (16, 16, 16, 256, 256, 3, 1),  # 64x64 tiles, no split (fused-stats epilogue)
+    (26, 32, 32, 128, 256, 3, 1),  # 128x128 tiles, no split, ragged last pixel tile
+    (100, 32, 32, 64, 64, 3, 1),   # 64x256 tiles (K=64 layers), no split
 ]
 
 
