@@ -7,8 +7,10 @@ executor), so each comparison isolates one layer. bf16-valued outputs: 1e-2; fp3
 gradients computed from identical bf16 operands: 1e-4 (summation order only).
 
 End-to-end checks compare free-running forward/backward. Two CORRECT bf16 implementations drift
-apart with depth (measured oracle-vs-oracle, fp32 vs fp64 accumulation, batch 2: 1.8% at layer4,
-0.6% on logits), so those bounds are looser and documented inline.
+apart with depth: the oracle run twice with fp32 vs fp64 conv accumulation differs by 1.8% at
+layer4 and 0.6% on logits (batch 2), and by 21% on the concatenated parameter gradient (batch 2
+and 8 alike; the stem/layer1 weight gradients of a freshly initialised BN network are dominated
+by amplified rounding noise). The free-running bounds below are set from those measurements.
 """
 import numpy as np
 import pytest
@@ -160,8 +162,8 @@ def test_per_layer_teacher_forced(dtc, cuda, batch):
 
 @pytest.mark.parametrize("batch", [2, 8])
 def test_end_to_end_drift_bounded(dtc, cuda, batch):
-    """Free-running forward/backward vs the oracle. Bounds: logits/loss 3e-2 / 1e-2 and every
-    activation 5e-2 (measured oracle-vs-oracle drift at batch 2: <= 1.8%)."""
+    """Free-running forward/backward vs the oracle. Bounds: logits/loss 3e-2 / 1e-2, every
+    activation 5e-2, concatenated gradient 0.35 (oracle-vs-oracle: 1.8%, 0.6%, 21%)."""
     model, sd, x, y = _setup(dtc, cuda, batch)
     crit = dtc.CrossEntropyLoss()
     logits = model(torch.from_numpy(x).to(cuda))
@@ -177,7 +179,10 @@ def test_end_to_end_drift_bounded(dtc, cuda, batch):
     assert worst < 5e-2
     g_exe = np.concatenate([_np(p.grad).ravel() for _, p in model.named_parameters()])
     g_ref = np.concatenate([ref["grads"][k].ravel() for k, _ in model.named_parameters()])
-    assert rel_err(g_exe, g_ref) < 0.1
+    assert rel_err(g_exe, g_ref) < 0.35
+    # the head and layer4 gradients are far from the noise floor: hold them to 2e-2
+    for k in ("linear.weight", "linear.bias", "layer4.1.conv2.weight", "layer4.1.bn2.weight"):
+        assert rel_err(_np(dict(model.named_parameters())[k].grad), ref["grads"][k]) < 2e-2, k
     sd2 = model.state_dict()
     for k, v in ref["buffers"].items():  # running statistics after one training forward
         assert rel_err(sd2[k].cpu().numpy(), v) < 2e-2, k

@@ -1,0 +1,90 @@
+"""The C-ABI library loads and exports every symbol include/dtc.h declares; host-side planning
+(layout, buckets, workspaces, conv plans) is consistent. No GPU compute here."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    text = open(os.path.join(ROOT, "include", "dtc.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(dtc_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol(dtc):
+    lib = dtc._native.lib
+    names = _header_functions()
+    assert len(names) >= 50
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the Python binding covers exactly the header
+    assert sorted(dtc._native.SYMBOLS) == names
+
+
+def test_abi_version_and_error_channel(dtc):
+    lib = dtc._native.lib
+    assert lib.dtc_abi_version() == 1
+    rc = lib.dtc_rn18_create(None, 1, 32, 32, 100, 25.0)
+    assert rc < 0
+    assert "null" in dtc._native.last_error()
+    h = C.c_void_p()
+    assert lib.dtc_rn18_create(C.byref(h), 0, 32, 32, 100, 25.0) < 0  # bad batch -> invalid argument
+    assert "bad shape" in dtc._native.last_error()
+
+
+def test_layout_matches_module_tree(dtc):
+    import torch
+    torch.manual_seed(0)
+    m = dtc.ResNet18()
+    lay = dtc.nn.Layout()
+    assert [p.name for p in lay.params] == [n for n, _ in m.named_parameters()]
+    assert sum(p.numel for p in lay.params) == 11_220_132
+    # reverse registration order, 64-element aligned, non-overlapping
+    offs = [p.offset for p in lay.params]
+    assert offs == sorted(offs, reverse=True)
+    for p in lay.params:
+        assert p.offset % 64 == 0
+    spans = sorted((p.offset, p.offset + p.numel) for p in lay.params)
+    assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))
+    assert lay.flat_numel >= spans[-1][1] and lay.flat_numel % 64 == 0
+    conv = {p.name: p for p in lay.params}["layer2.0.conv1.weight"]
+    assert conv.shape == (128, 64, 3, 3) and conv.stride == (576, 1, 192, 64)  # KRSC storage
+    assert [b.prefix for b in lay.bns][:3] == ["bn1", "layer1.0.bn1", "layer1.0.bn2"]
+    assert len(lay.bns) == 20 and sum(b.channels for b in lay.bns) * 2 == 9600
+
+
+@pytest.mark.parametrize("cap_mb", [1, 5, 25, 100, 1000])
+def test_buckets_tile_the_gradient_buffer(dtc, cap_mb):
+    lay = dtc.nn.Layout(100, cap_mb)
+    pos = 0
+    for off, n in lay.buckets:
+        assert off == pos and n > 0
+        pos += n
+    assert pos == lay.flat_numel
+    # every bucket but the last closes at a block boundary at or above the cap
+    for off, n in lay.buckets[:-1]:
+        assert n * 4 >= cap_mb * 2 ** 20
+    # the first bucket starts with the head (linear.bias at offset 0): it is ready first
+    names_at_0 = [p.name for p in lay.params if p.offset == 0]
+    assert names_at_0 == ["linear.bias"]
+
+
+def test_workspace_and_conv_plans(dtc):
+    lib = dtc._native.lib
+    h = C.c_void_p()
+    dtc._native.call("dtc_rn18_create", C.byref(h), 256, 32, 32, 100, 25.0)
+    ws = lib.dtc_rn18_workspace_bytes(h)
+    assert 0.3e9 < ws < 3e9, ws
+    assert lib.dtc_rn18_num_activations(h) == 3 + 8 * 4 + 3 + 1
+    lib.dtc_rn18_destroy(h)
+    d = dtc._native.ConvDesc(256, 4, 4, 512, 512, 3, 3, 1, 1)
+    assert lib.dtc_conv2d_workspace_size(d, 2) > 0  # wgrad always wants split-K slabs
+    d = dtc._native.ConvDesc(256, 32, 32, 64, 64, 3, 3, 1, 1)
+    assert lib.dtc_conv2d_workspace_size(d, 0) == 0  # big layer: no split in forward
+    # 224x224 (BASELINE config 5) plans too
+    dtc._native.call("dtc_rn18_create", C.byref(h), 8, 224, 224, 100, 25.0)
+    lib.dtc_rn18_destroy(h)

@@ -1,0 +1,187 @@
+"""Pin the oracle (and the host-side data plumbing) to golden vectors produced by the reference's
+own code (tests/golden/make_golden.py, run in the build container against /root/reference).
+
+CPU only. These tests are what makes the oracle a trustworthy checker for the GPU parity tests.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ops as O
+from oracle import resnet as R
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def _sha(xs):
+    return hashlib.sha256(np.asarray(xs, dtype=np.int64).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def model_sd(dtc):
+    torch.manual_seed(42)
+    m = dtc.ResNet18()
+    return {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}
+
+
+def test_init_matches_reference(model_sd):
+    """ResNet18() built by this package under seed 42 is bit-identical to reference net.py's."""
+    gold = _load("resnet18_b2.json")["init"]
+    assert set(gold) <= set(model_sd)
+    for k, s in gold.items():
+        a = model_sd[k].astype(np.float64).ravel()
+        np.testing.assert_array_equal(a[s["idx"]].astype(np.float32), np.asarray(s["val"], np.float32), err_msg=k)
+        assert abs(np.linalg.norm(a) - s["norm"]) <= 1e-9 * max(1.0, s["norm"]), k
+
+
+def test_state_dict_keys_match_reference(model_sd):
+    gold = _load("resnet18_b2.json")
+    assert set(gold["fp32"]["grads"]) == {k for k in model_sd if not (
+        k.endswith("running_mean") or k.endswith("running_var") or k.endswith("num_batches_tracked"))}
+
+
+def _oracle_run(model_sd, bf16_mode):
+    params = {k: v for k, v in model_sd.items() if "running" not in k and "num_batches" not in k}
+    bufs = {k: v for k, v in model_sd.items() if "running" in k}
+    g = np.random.default_rng(0)  # make_golden.py: x_seed 0, batch 2
+    x = g.standard_normal((2, 3, 32, 32)).astype(np.float32)
+    y = g.integers(0, 100, 2)
+    return R.forward_backward(params, bufs, x, y, bf16_mode=bf16_mode, train=True, want_acts=True)
+
+
+def test_oracle_fp32_matches_reference_forward_backward(model_sd):
+    gold = _load("resnet18_b2.json")["fp32"]
+    r = _oracle_run(model_sd, False)
+    assert abs(r["loss"] - gold["loss"]) < 1e-5
+    np.testing.assert_allclose(r["logits"], np.asarray(gold["logits"]), rtol=1e-4, atol=1e-5)
+    for k, s in gold["grads"].items():
+        g = r["grads"][k].astype(np.float64).ravel()
+        assert abs(np.linalg.norm(g) - s["norm"]) <= 1e-4 * s["norm"] + 1e-7, k
+        np.testing.assert_allclose(g[s["idx"]], s["val"], rtol=1e-3, atol=1e-6 * max(1.0, s["norm"]), err_msg=k)
+    for k, s in gold["running"].items():
+        v = r["buffers"][k].astype(np.float64).ravel()
+        np.testing.assert_allclose(v[s["idx"]], s["val"], rtol=1e-5, atol=1e-7, err_msg=k)
+
+
+def test_oracle_fp32_matches_reference_activations(model_sd):
+    """Reference module outputs (forward hooks, NHWC) vs the oracle's per-layer activations."""
+    gold = _load("resnet18_b2.json")["fp32"]["acts"]
+    r = _oracle_run(model_sd, False)
+    acts = r["acts"]
+    pairs = {"conv1": "stem.conv"}
+    for L in range(1, 5):
+        for b in range(2):
+            pre = f"layer{L}.{b}"
+            pairs[pre + ".conv1"] = pre + ".conv1"
+            pairs[pre + ".conv2"] = pre + ".conv2"
+            pairs[pre] = pre + ".out"
+            if f"{pre}.shortcut.0" in gold:
+                pairs[pre + ".shortcut.0"] = pre + ".shortcut"
+    for gk, ok in pairs.items():
+        s = gold[gk]
+        a = acts[ok].astype(np.float64).ravel()
+        assert abs(np.linalg.norm(a) - s["norm"]) <= 1e-5 * s["norm"], gk
+        np.testing.assert_allclose(a[s["idx"]], s["val"], rtol=1e-4, atol=1e-5, err_msg=gk)
+
+
+def test_oracle_bf16_close_to_reference_autocast(model_sd):
+    """bf16 mode vs torch CPU bf16 autocast of the reference net: same rounding regime, different
+    summation orders -> bounded drift (loss 1e-2, logits 5e-2)."""
+    gold = _load("resnet18_b2.json")["bf16"]
+    r = _oracle_run(model_sd, True)
+    assert abs(r["loss"] - gold["loss"]) < 1e-2 * max(1.0, gold["loss"])
+    lg = np.asarray(gold["logits"])
+    assert np.linalg.norm(r["logits"] - lg) / np.linalg.norm(lg) < 5e-2
+
+
+def test_split_and_shards_match_reference(dtc):
+    """45k/5k split (ddp/dataset.py:85-96) and DistributedSampler shards (dataset.py:98) bit-exact."""
+    gold = _load("sampler.json")
+    data = dtc.data
+    data.fix_seed(42)
+    dtc.ResNet18()  # ddp/main.py builds the model before the loaders (torch RNG only)
+    train_idx, valid_idx = data.train_valid_split(50000, 0.1, True)
+    assert len(train_idx) == gold["train_len"] and len(valid_idx) == gold["valid_len"]
+    assert train_idx[:16] == gold["train_head"] and valid_idx[:16] == gold["valid_head"]
+    assert _sha(train_idx) == gold["train_sha256"] and _sha(valid_idx) == gold["valid_sha256"]
+    for key, s in gold["shards"].items():
+        W, e, r = (int(p[1:]) for p in key.split("_"))
+        idx = data.shard_indices(len(train_idx), W, r, e)
+        assert len(idx) == s["len"] and idx[:8] == s["head"] and _sha(idx) == s["sha256"], key
+    # steps per epoch at global batch 256 (int(256/W) per rank, drop_last)
+    for W, steps in gold["steps_per_epoch_global256"].items():
+        W = int(W)
+        assert len(data.shard_indices(len(train_idx), W, 0, 0)) // (256 // W) == steps
+
+
+def test_survey_known_answers(dtc):
+    """SURVEY.md §8 a14 probed heads."""
+    data = dtc.data
+    data.fix_seed(42)
+    tr, _ = data.train_valid_split()
+    assert tr[:5] == [40877, 18057, 19066, 20525, 5847]
+    assert data.shard_indices(45000, 2, 0, 0)[:4] == [36044, 16461, 4107, 27505]
+    assert data.shard_indices(45000, 8, 0, 0)[:4] == [36044, 17041, 12200, 9728]
+
+
+def test_sgd_oracle_matches_torch_sgd():
+    gold = _load("optim.json")["sgd"]
+    p = np.asarray(gold["p0"], np.float32)
+    buf = None
+    for step, (g, want) in enumerate(zip(gold["grads"], gold["traj"])):
+        p, buf = O.sgd_nesterov(p, np.asarray(g, np.float32), buf, gold["lr"], gold["wd"], gold["mu"], step == 0)
+        np.testing.assert_allclose(p, want, rtol=1e-6, atol=1e-7)
+
+
+def test_grad_scaler_oracle_matches_torch():
+    gold = _load("optim.json")["scaler"]
+    scale, tracker = gold["init"], 0
+    for bad, want in zip(gold["pattern"], gold["scales"]):
+        scale, tracker = O.grad_scaler_update(scale, tracker, bad, interval=gold["interval"])
+        assert scale == want
+
+
+def test_ddp_gradient_is_mean_of_local(dtc):
+    """Reference DDP on 2 gloo ranks: the all-reduced gradient equals the mean of the two local
+    gradients; the package's bucketed reducer math reproduces it on the same numbers."""
+    gold = _load("ddp_2rank.json")["per_rank"]
+    r0, r1 = gold["0"], gold["1"]
+    for k in r0["ddp"]:
+        l0, l1 = np.asarray(r0["local"][k]["val"]), np.asarray(r1["local"][k]["val"])
+        want = (l0 + l1) / 2
+        np.testing.assert_allclose(r0["ddp"][k]["val"], want, rtol=1e-5, atol=1e-8, err_msg=k)
+        np.testing.assert_allclose(r1["ddp"][k]["val"], r0["ddp"][k]["val"], rtol=0, atol=0, err_msg=k)
+    # same numbers through parallel.bucketed_allreduce_mean_ with an in-process "transport"
+    flat0 = torch.tensor(np.concatenate([r0["local"][k]["val"] for k in r0["local"]]), dtype=torch.float32)
+    flat1 = torch.tensor(np.concatenate([r1["local"][k]["val"] for k in r1["local"]]), dtype=torch.float32)
+    n = flat0.numel()
+    buckets = [(0, n // 3), (n // 3, n - n // 3)]
+    other = flat1 / 2
+
+    def allreduce(t):  # rank-0 view of a SUM all-reduce with rank 1's pre-divided buffer
+        off = t.storage_offset()
+        t.add_(other[off:off + t.numel()])
+
+    out = dtc.parallel.bucketed_allreduce_mean_(flat0.clone(), buckets, 2, allreduce)
+    want = np.concatenate([(np.asarray(r0["local"][k]["val"]) + np.asarray(r1["local"][k]["val"])) / 2
+                           for k in r0["local"]])
+    np.testing.assert_allclose(out.numpy(), want, rtol=1e-6, atol=1e-9)
+
+
+def test_synthetic_stream_matches_golden_generator(dtc):
+    lc = _load("loss_curve.json") if os.path.exists(os.path.join(GOLD, "loss_curve.json")) else None
+    if lc is None:
+        pytest.skip("loss curve fixture not generated")
+    x, y = dtc.data.synthetic_batch(0, lc["batch"])
+    assert y.tolist()[:16] == lc["stream_check"]["y0"]
+    assert abs(float(x.sum()) - lc["stream_check"]["x0_sum"]) < 1e-3
+    np.testing.assert_allclose(x[0, 0, 0, :8].numpy(), lc["stream_check"]["x0_00"], rtol=1e-6)
