@@ -51,6 +51,8 @@ PConv = C.POINTER(ConvDesc)
 _SIGS = {
     "dtc_abi_version": (i32, []),
     "dtc_last_error": (cstr, []),
+    "dtc_set_option": (i32, [cstr, i32]),
+    "dtc_get_option": (i32, [cstr]),
     "dtc_conv2d_workspace_size": (sz, [PConv, i32]),
     "dtc_conv2d_fwd": (i32, [PConv, vp, vp, vp, vp, vp, sz, vp]),
     "dtc_conv2d_dgrad": (i32, [PConv, vp, vp, vp, vp, vp, sz, vp]),

@@ -8,7 +8,22 @@
 #include "comm.h"
 #include "kernels.h"
 
+#include <atomic>
+#include <cstring>
+
 namespace dtc {
+static std::atomic<int> g_opts[OPT_COUNT] = {{3}, {1}};
+static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap"};
+int option_get(int id) { return g_opts[id].load(std::memory_order_relaxed); }
+int option_set(const char* name, int value) {
+  for (int i = 0; i < OPT_COUNT; ++i)
+    if (name && strcmp(name, g_opt_names[i]) == 0) {
+      g_opts[i].store(value, std::memory_order_relaxed);
+      return 0;
+    }
+  return set_error(DTC_EINVAL, "unknown option %s", name ? name : "(null)");
+}
+
 static thread_local std::string g_err;
 int set_error(int code, const char* fmt, ...) {
   char buf[1024];
@@ -39,6 +54,12 @@ static inline ConvShape shape_of(const dtc_conv_desc* d) {
 extern "C" {
 
 int dtc_abi_version(void) { return DTC_ABI_VERSION; }
+int dtc_set_option(const char* name, int value) { return option_set(name, value); }
+int dtc_get_option(const char* name) {
+  for (int i = 0; i < OPT_COUNT; ++i)
+    if (name && strcmp(name, g_opt_names[i]) == 0) return option_get(i);
+  return set_error(DTC_EINVAL, "unknown option %s", name ? name : "(null)");
+}
 const char* dtc_last_error(void) { return last_error(); }
 
 size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass) {

@@ -39,6 +39,7 @@ struct IGemmParams {
   FastDiv fd_q, fd_pq;  // FWD/WGRAD: Q, P*Q ; DGRAD: W, H*W
   FastDiv fd_cc;        // reduction chunks per tap: FWD C/64, DGRAD K/64
   int num_kt, kt_per_split, tiles_a;
+  int xcd_remap;
 };
 
 __device__ __forceinline__ int rowswz(int row) { return (row >> 1) & 7; }
@@ -73,7 +74,7 @@ __device__ __forceinline__ bf16x8 frag_tr(const char* region, int cb, int ks, in
   return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <int MODE, int BM, int BN, int WR, int WC, bool SLAB>
+template <int MODE, int BM, int BN, int WR, int WC, bool SLAB, int NSTAGE>
 __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   constexpr int FM = BM / (WR * 16);
   constexpr int FN = BN / (WC * 16);
@@ -86,12 +87,20 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   static_assert(WR * WC == 4, "4 waves");
   static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
 
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "stages");
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int ta = blockIdx.x % p.tiles_a;
-  const int tb = blockIdx.x / p.tiles_a;
+  // XCD-aware remap (guide T1): blocks b and b+8 share an XCD's L2; give each XCD a contiguous
+  // run of tile ids so the tiles that share a pixel tile (consecutive ids) share an L2.
+  int bid = blockIdx.x;
+  if (p.xcd_remap && gridDim.x >= 16) {
+    const int nwg = gridDim.x, x8 = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    bid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + (bid >> 3);
+  }
+  const int ta = bid % p.tiles_a;
+  const int tb = bid / p.tiles_a;
   const int a0 = ta * BM, b0 = tb * BN;
   const int kt_begin = blockIdx.y * p.kt_per_split;
   const int kt_end = min(p.num_kt, kt_begin + p.kt_per_split);
@@ -268,43 +277,66 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
     }
   };
 
-  if (kt_begin < kt_end) {
-    int r = st_r, s = st_s, cc = st_c;
-    stage(smem, kt_begin, r, s, cc);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int buf = 0;
-    for (int kt = kt_begin; kt < kt_end; ++kt) {
-      char* cur = smem + buf * STAGE;
-      if (kt + 1 < kt_end) {
-        int r2 = r, s2 = s, c2 = cc;
-        if constexpr (MODE != MODE_WGRAD) advance(r2, s2, c2);
-        stage(smem + (buf ^ 1) * STAGE, kt + 1, r2, s2, c2);
-        r = r2; s = s2; cc = c2;
+  auto compute = [&](const char* cur) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        if constexpr (A_TR) af[i] = frag_tr(cur, arow0 + i * 16, ks, lane);
+        else af[i] = frag_row(cur, arow0 + i * 16, ks, lane);
       }
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[FM], bfr[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          if constexpr (A_TR) af[i] = frag_tr(cur, arow0 + i * 16, ks, lane);
-          else af[i] = frag_row(cur, arow0 + i * 16, ks, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          if constexpr (B_TR) bfr[j] = frag_tr(cur + A_BYTES, bcol0 + j * 16, ks, lane);
-          else bfr[j] = frag_row(cur + A_BYTES, bcol0 + j * 16, ks, lane);
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (B_TR) bfr[j] = frag_tr(cur + A_BYTES, bcol0 + j * 16, ks, lane);
+        else bfr[j] = frag_row(cur + A_BYTES, bcol0 + j * 16, ks, lane);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      buf ^= 1;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+  };
+
+  // K loop over an NSTAGE-deep LDS ring filled by LDS-DMA. Iteration `it`: wait (counted
+  // vmcnt: each wave issues NIA+NIB DMAs per stage) until stage `it` has landed for this wave,
+  // barrier (then every wave's DMAs for `it` have landed and every wave finished reading the
+  // buffer of stage it-1), refill that buffer with stage it+NSTAGE-1, compute stage `it`.
+  // A raw s_barrier is used: __syncthreads() would also drain vmcnt to 0 (guide §5).
+  if (kt_begin < kt_end) {
+    const int nk = kt_end - kt_begin;
+    int r = st_r, s = st_s, cc = st_c;
+#pragma unroll
+    for (int i = 0; i < NSTAGE - 1; ++i) {
+      if (i < nk) {
+        stage(smem + i * STAGE, kt_begin + i, r, s, cc);
+        if constexpr (MODE != MODE_WGRAD) advance(r, s, cc);
+      }
+    }
+    int cur = 0;
+    for (int it = 0; it < nk; ++it) {
+      if constexpr (NSTAGE == 3) {
+        if (it + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIA + NIB) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int nxt = it + NSTAGE - 1;
+      if (nxt < nk) {
+        int slot = cur + NSTAGE - 1;
+        if (slot >= NSTAGE) slot -= NSTAGE;
+        stage(smem + slot * STAGE, kt_begin + nxt, r, s, cc);
+        if constexpr (MODE != MODE_WGRAD) advance(r, s, cc);
+      }
+      compute(smem + cur * STAGE);
+      cur = (cur + 1 == NSTAGE) ? 0 : cur + 1;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // all LDS reads done before the epilogue reuses smem
+    asm volatile("" ::: "memory");
   }
 
   // ------------------------------------------------------------ epilogue
@@ -531,7 +563,11 @@ static int fill_common(IGemmParams& p, const ConvShape& s) {
 template <int MODE, int BM, int BN, int WR, int WC, bool SLAB>
 static int launch_igemm(IGemmParams& p, int tiles_b, int splits, hipStream_t st) {
   dim3 grid(p.tiles_a * tiles_b, splits);
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB>), grid, dim3(256), 0, st, p);
+  p.xcd_remap = option_get(OPT_XCD_REMAP);
+  if (option_get(OPT_IGEMM_STAGES) == 3)
+    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 3>), grid, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 2>), grid, dim3(256), 0, st, p);
   DTC_LAUNCH_CHECK();
   return 0;
 }

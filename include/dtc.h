@@ -34,6 +34,10 @@ extern "C" {
 /* ------------------------------------------------------------------ library */
 int dtc_abi_version(void);
 const char* dtc_last_error(void);
+/* Process-wide kernel tuning knobs (atomic; for benchmarking): "igemm_stages" (2 or 3 LDS stages
+ * in the conv main loop, default 3), "xcd_remap" (XCD-aware tile order, default 1). */
+int dtc_set_option(const char* name, int value);
+int dtc_get_option(const char* name);
 
 /* ------------------------------------------------------------------ convolution
  * Replaces nn.Conv2d(bias=False) forward / backward (reference src/ddp/net.py:18-24,
