@@ -12,7 +12,7 @@
 #include <cstring>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{3}, {1}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap"};
 int option_get(int id) { return g_opts[id].load(std::memory_order_relaxed); }
 int option_set(const char* name, int value) {

@@ -603,8 +603,9 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
     const int num_kt = ceil_div(M, 64);
     pl.bm = (s.C == 64 || s.K == 64) ? 64 : 128;
     pl.bn = pl.bm;
+    if ((s.R * s.S * s.C / pl.bm) * (s.K / pl.bn) < 64) pl.bm = pl.bn = 64;  // few output tiles: more of them
     const int tiles = (s.R * s.S * s.C / pl.bm) * (s.K / pl.bn);
-    pl.splits = pick_splits(tiles, num_kt, 512, 32);
+    pl.splits = pick_splits(tiles, num_kt, 512, 8);
     pl.slab_bytes = (size_t)pl.splits * s.K * s.R * s.S * s.C * 4;
     pl.num_kt = num_kt;
   }

@@ -211,7 +211,7 @@ def synthetic_stream(step, batch, seed=1234, templates=None):
     return x, y
 
 
-def gen_loss_curve(steps=200, batch=32, modes=("fp32", "bf16")):
+def gen_loss_curve(steps=200, batch=128, modes=("fp32", "bf16")):
     utils = _import_from("single", "utils")
     net = _import_from("single", "net")
     templates = torch.randn(100, 3, 32, 32, generator=torch.Generator().manual_seed(1234))
