@@ -40,6 +40,7 @@ struct IGemmParams {
   FastDiv fd_cc;        // reduction chunks per tap: FWD C/64, DGRAD K/64
   int num_kt, kt_per_split, tiles_a;
   int xcd_remap;
+  int cls;  // DGRAD, stride 2: blockIdx.z = output parity class (h%2, w%2); M counts class pixels
 };
 
 __device__ __forceinline__ int rowswz(int row) { return (row >> 1) & 7; }
@@ -102,8 +103,26 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   const int ta = bid % p.tiles_a;
   const int tb = bid / p.tiles_a;
   const int a0 = ta * BM, b0 = tb * BN;
+  // DGRAD stride-2 parity class: only taps r = r0 + 2i (s = s0 + 2j) reach pixels with
+  // h % 2 == ph, and they read dy row p = hh + dr - i for h = 2*hh + ph (a dense stride-1 GEMM)
+  int cls_ph = 0, cls_pw = 0, r0 = 0, s0 = 0, tstep = 1, dr = 0, dsh = 0, Sdim = p.S;
+  int num_kt = p.num_kt;
+  if constexpr (MODE == MODE_DGRAD) {
+    if (p.cls) {
+      cls_ph = blockIdx.z >> 1;
+      cls_pw = blockIdx.z & 1;
+      r0 = (cls_ph + p.pad) & 1;
+      s0 = (cls_pw + p.pad) & 1;
+      const int Rdim = (p.R - r0 + 1) >> 1;
+      Sdim = (p.S - s0 + 1) >> 1;
+      tstep = 2;
+      dr = (cls_ph + p.pad - r0) >> 1;
+      dsh = (cls_pw + p.pad - s0) >> 1;
+      num_kt = Rdim * Sdim * (int)p.fd_cc.d;
+    }
+  }
   const int kt_begin = blockIdx.y * p.kt_per_split;
-  const int kt_end = min(p.num_kt, kt_begin + p.kt_per_split);
+  const int kt_end = min(num_kt, kt_begin + p.kt_per_split);
   const int lrow = lane >> 3, pc = lane & 7;
   const u16* zp = (const u16*)g_zero_page + pc * 8;
 
@@ -156,11 +175,11 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
       const int lc = pc ^ rowswz(row);
       const int pix = b0 + row;
       int h = -(1 << 20), w = -(1 << 20), nP = 0;
-      if (pix < p.M) {
+      if (pix < p.M) {  // (h, w) of dx, or (hh, ww) of the parity-class grid
         const int n = (int)fdiv((uint32_t)pix, p.fd_pq);
-        const int rem = pix - n * p.H * p.W;
+        const int rem = pix - n * (int)p.fd_pq.d;
         h = (int)fdiv((uint32_t)rem, p.fd_q);
-        w = rem - h * p.W;
+        w = rem - h * (int)p.fd_q.d;
         nP = n * p.P;
       }
       baseB[j] = nP;
@@ -192,8 +211,8 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   if constexpr (MODE != MODE_WGRAD) {
     const int rs = (int)fdiv((uint32_t)kt_begin, p.fd_cc);
     st_c = kt_begin - rs * nchunk;
-    st_r = rs / p.S;
-    st_s = rs - st_r * p.S;
+    st_r = rs / Sdim;
+    st_s = rs - st_r * Sdim;
   }
 
   auto stage = [&](char* sb, int kt, int r, int s, int cc) {
@@ -211,19 +230,29 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
         glds16(src, sb + A_BYTES + (wave + 4 * j) * 1024);
       }
     } else if constexpr (MODE == MODE_DGRAD) {
-      const int64_t wadd = (int64_t)cc * 64 * p.RSC + (r * p.S + s) * p.C;
+      const int wr_ = r0 + tstep * r, ws_ = s0 + tstep * s;  // filter tap
+      const int64_t wadd = (int64_t)cc * 64 * p.RSC + (wr_ * p.S + ws_) * p.C;
 #pragma unroll
       for (int j = 0; j < NIA; ++j)
         glds16(p.src1 + offA[j] + wadd, sb + (wave + 4 * j) * 1024);
 #pragma unroll
       for (int j = 0; j < NIB; ++j) {
-        int ph = hB[j] + p.pad - r, pw = wB[j] + p.pad - s;
-        bool ok = (ph >= 0) && (pw >= 0);
-        if (p.stride == 2) {
-          ok = ok && !(ph & 1) && !(pw & 1);
-          ph >>= 1; pw >>= 1;
+        int ph, pw;
+        bool ok;
+        if (p.cls) {
+          ph = hB[j] + dr - r;
+          pw = wB[j] + dsh - s;
+          ok = true;
+        } else {
+          ph = hB[j] + p.pad - r;
+          pw = wB[j] + p.pad - s;
+          ok = (ph >= 0) && (pw >= 0);
+          if (p.stride == 2) {
+            ok = ok && !(ph & 1) && !(pw & 1);
+            ph >>= 1; pw >>= 1;
+          }
         }
-        ok = ok && (ph < p.P) && (pw < p.Q);
+        ok = ok && ((unsigned)ph < (unsigned)p.P) && ((unsigned)pw < (unsigned)p.Q);
         const u16* src = ok ? (p.src0 + ((baseB[j] + ph) * p.Q + pw) * p.K + cc * 64 + colB[j]) : zp;
         glds16(src, sb + A_BYTES + (wave + 4 * j) * 1024);
       }
@@ -273,7 +302,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   auto advance = [&](int& r, int& s, int& cc) {
     if (++cc == nchunk) {
       cc = 0;
-      if (++s == p.S) { s = 0; ++r; }
+      if (++s == Sdim) { s = 0; ++r; }
     }
   };
 
@@ -426,14 +455,22 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
     }
   } else {  // DGRAD bf16 (+ residual)
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int ch = a0 + arow0 + i * 16 + rq;
+    for (int j = 0; j < FN; ++j) {
+      const int pix = b0 + bcol0 + j * 16 + cl;
+      size_t orow = (size_t)pix;
+      if (p.cls && pix < p.M) {  // class pixel -> dx pixel (2*hh + ph, 2*ww + pw)
+        const int n = (int)fdiv((uint32_t)pix, p.fd_pq);
+        const int rem = pix - n * (int)p.fd_pq.d;
+        const int hh = (int)fdiv((uint32_t)rem, p.fd_q);
+        const int ww = rem - hh * (int)p.fd_q.d;
+        orow = ((size_t)n * p.H + 2 * hh + cls_ph) * p.W + 2 * ww + cls_pw;
+      }
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int pix = b0 + bcol0 + j * 16 + cl;
+      for (int i = 0; i < FM; ++i) {
+        const int ch = a0 + arow0 + i * 16 + rq;
         if (pix < p.M) {
           float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-          const size_t o = (size_t)pix * p.C + ch;
+          const size_t o = orow * p.C + ch;
           if (p.res) {
             const uint2 rr = *(const uint2*)(p.res + o);
             v[0] += bf_lo(rr.x); v[1] += bf_hi(rr.x); v[2] += bf_lo(rr.y); v[3] += bf_hi(rr.y);
@@ -561,8 +598,8 @@ static int fill_common(IGemmParams& p, const ConvShape& s) {
 }
 
 template <int MODE, int BM, int BN, int WR, int WC, bool SLAB>
-static int launch_igemm(IGemmParams& p, int tiles_b, int splits, hipStream_t st) {
-  dim3 grid(p.tiles_a * tiles_b, splits);
+static int launch_igemm(IGemmParams& p, int tiles_b, int splits, hipStream_t st, int gz = 1) {
+  dim3 grid(p.tiles_a * tiles_b, splits, gz);
   p.xcd_remap = option_get(OPT_XCD_REMAP);
   if (option_get(OPT_IGEMM_STAGES) == 3)
     hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 3>), grid, dim3(256), 0, st, p);
@@ -582,12 +619,17 @@ static int pick_splits(int tiles, int num_kt, int target, int min_kt) {
   return std::max(1, s);
 }
 
+static bool dgrad_class_mode(const ConvShape& s) {
+  return s.stride == 2 && (s.H % 2) == 0 && (s.W % 2) == 0 && option_get(OPT_DGRAD_CLASSES) != 0;
+}
+
 ConvPlan plan_conv(const ConvShape& s, int mode) {
   ConvPlan pl{};
   const int P = (s.H + 2 * s.pad - s.R) / s.stride + 1;
   const int Q = (s.W + 2 * s.pad - s.S) / s.stride + 1;
+  const bool cls = (mode == CONV_DGRAD) && dgrad_class_mode(s);
   if (mode == CONV_FWD || mode == CONV_DGRAD) {
-    const int M = (mode == CONV_FWD) ? s.N * P * Q : s.N * s.H * s.W;
+    const int M = (mode == CONV_FWD) ? s.N * P * Q : (cls ? s.N * (s.H / 2) * (s.W / 2) : s.N * s.H * s.W);
     const int A = (mode == CONV_FWD) ? s.K : s.C;
     const int num_kt = s.R * s.S * ((mode == CONV_FWD) ? s.C : s.K) / 64;
     // big tiles while they fill the chip (>= ~2 waves of 256 CUs), else 64x64 tiles, else split-K
@@ -595,7 +637,7 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
     else { pl.bm = 128; pl.bn = 128; }
     if ((A / pl.bm) * ceil_div(M, pl.bn) < 400) { pl.bm = 64; pl.bn = 64; }
     const int tiles = (A / pl.bm) * ceil_div(M, pl.bn);
-    pl.splits = tiles >= 256 ? 1 : pick_splits(tiles, num_kt, 480, 8);
+    pl.splits = (tiles >= 256 || cls) ? 1 : pick_splits(tiles, num_kt, 480, 8);
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * M * A * 4 : 0;
     pl.num_kt = num_kt;
   } else {
@@ -605,7 +647,7 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
     pl.bn = pl.bm;
     if ((s.R * s.S * s.C / pl.bm) * (s.K / pl.bn) < 64) pl.bm = pl.bn = 64;  // few output tiles: more of them
     const int tiles = (s.R * s.S * s.C / pl.bm) * (s.K / pl.bn);
-    pl.splits = pick_splits(tiles, num_kt, 512, 8);
+    pl.splits = pick_splits(tiles, num_kt, 512, tiles < 64 ? 8 : 16);
     pl.slab_bytes = (size_t)pl.splits * s.K * s.R * s.S * s.C * 4;
     pl.num_kt = num_kt;
   }
@@ -645,10 +687,22 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
   DTC_TRY(fill_common(p, s));
   ConvPlan pl = plan_conv(s, CONV_DGRAD);
   p.src0 = dy; p.src1 = w; p.out = dx; p.res = res;
-  p.M = s.N * s.H * s.W;
-  p.fd_q = make_fastdiv(s.W); p.fd_pq = make_fastdiv(s.H * s.W); p.fd_cc = make_fastdiv(s.K / 64);
+  p.fd_cc = make_fastdiv(s.K / 64);
   p.num_kt = pl.num_kt;
   p.tiles_a = s.C / pl.bm;
+  if (dgrad_class_mode(s)) {  // four parity-class GEMMs in one launch (blockIdx.z), no split-K
+    p.cls = 1;
+    p.M = s.N * (s.H / 2) * (s.W / 2);
+    p.fd_q = make_fastdiv(s.W / 2);
+    p.fd_pq = make_fastdiv((s.H / 2) * (s.W / 2));
+    p.kt_per_split = p.num_kt;
+    const int tb = ceil_div(p.M, pl.bn);
+    if (pl.bn == 64) return launch_igemm<MODE_DGRAD, 64, 64, 2, 2, false>(p, tb, 1, st, 4);
+    if (pl.bm == 64) return launch_igemm<MODE_DGRAD, 64, 256, 1, 4, false>(p, tb, 1, st, 4);
+    return launch_igemm<MODE_DGRAD, 128, 128, 2, 2, false>(p, tb, 1, st, 4);
+  }
+  p.M = s.N * s.H * s.W;
+  p.fd_q = make_fastdiv(s.W); p.fd_pq = make_fastdiv(s.H * s.W);
   const int tiles_b = ceil_div(p.M, pl.bn);
   int splits = pl.splits;
   if (splits > 1 && (slab == nullptr || slab_bytes < pl.slab_bytes)) splits = 1;

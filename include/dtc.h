@@ -35,7 +35,8 @@ extern "C" {
 int dtc_abi_version(void);
 const char* dtc_last_error(void);
 /* Process-wide kernel tuning knobs (atomic; for benchmarking): "igemm_stages" (2 or 3 LDS stages
- * in the conv main loop, default 2), "xcd_remap" (XCD-aware tile order, default 1). */
+ * in the conv main loop, default 2), "xcd_remap" (XCD-aware tile order, default 1),
+ * "dgrad_classes" (stride-2 data-gradient as 4 parity-class GEMMs, default 1). */
 int dtc_set_option(const char* name, int value);
 int dtc_get_option(const char* name);
 

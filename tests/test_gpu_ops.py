@@ -27,6 +27,7 @@ CONV_CASES = [
     (16, 16, 16, 256, 256, 3, 1),  # 64x64 tiles, no split (fused-stats epilogue)
     (26, 32, 32, 128, 256, 3, 1),  # 128x128 tiles, no split, ragged last pixel tile
     (100, 32, 32, 64, 64, 3, 1),   # 64x256 tiles (K=64 layers), no split
+    (64, 16, 16, 64, 128, 3, 2),   # stride-2 class GEMMs big enough for 64x256 tiles
 ]
 
 
@@ -88,6 +89,27 @@ def test_conv_wgrad(dtc, cuda, case):
     ref = 0.5 * O.conv2d_wgrad(x, dy, R, R, st, pad)
     # fp32 accumulation of exact bf16 products: only summation-order differences remain
     assert rel_err(dw.cpu().numpy(), ref) < 1e-5
+
+
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[6] == 2])
+@pytest.mark.parametrize("classes", [0, 1])
+def test_conv_dgrad_stride2_paths(dtc, cuda, case, classes):
+    """Stride-2 data gradient: parity-class decomposition (default) and the generic masked path."""
+    N, H, W, C, K, R, st = case
+    pad = 1 if R == 3 else 0
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+    g = np.random.default_rng(12)
+    dy = _rand_bf16((N, P, Q, K), g)
+    w = _rand_bf16((K, R, R, C), g, 0.05)
+    res = _rand_bf16((N, H, W, C), g)
+    dtc._native.call("dtc_set_option", b"dgrad_classes", classes)
+    try:
+        dx = dtc.ops.conv2d_dgrad(_to_dev_bf16(dy, cuda), _to_dev_bf16(w, cuda), (H, W), st, pad,
+                                  res=_to_dev_bf16(res, cuda))
+    finally:
+        dtc._native.call("dtc_set_option", b"dgrad_classes", 1)
+    ref = O.conv2d_dgrad(dy, w, (H, W), st, pad) + res
+    assert rel_err(dx.float().cpu().numpy(), ref) < 1e-2
 
 
 def test_mfma_layout_identity(dtc, cuda):
