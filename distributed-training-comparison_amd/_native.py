@@ -67,7 +67,8 @@ _SIGS = {
     "dtc_stem_im2col": (i32, [vp, vp, i32, i32, i32, vp]),
     "dtc_stem_pack_weight": (i32, [vp, vp, i32, vp]),
     "dtc_head_fwd": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp]),
-    "dtc_head_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp]),
+    "dtc_head_bwd_workspace_size": (sz, [i32, i32, i32]),
+    "dtc_head_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, sz, vp]),
     "dtc_xent_fwd": (i32, [vp, vp, i32, i32, vp, vp, vp]),
     "dtc_xent_bwd": (i32, [vp, vp, vp, vp, i32, i32, vp, vp]),
     "dtc_sgd_nesterov_flat": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, vp, vp, vp]),

@@ -127,9 +127,10 @@ int dtc_head_fwd(const uint16_t* act, int n, int hw, int c, const uint16_t* wfc,
                  float* feat, float* logits, void* stream) {
   return head_fwd(act, n, hw, c, wfc, bfc, ncls, feat, logits, S(stream));
 }
+size_t dtc_head_bwd_workspace_size(int n, int c, int ncls) { return head_bwd_workspace(n, c, ncls); }
 int dtc_head_bwd(const float* dlogits, const float* feat, const uint16_t* wfc, int n, int hw, int c, int ncls,
-                 float scale, float* dw, float* db, uint16_t* dact, void* stream) {
-  return head_bwd(dlogits, feat, wfc, n, hw, c, ncls, scale, dw, db, dact, S(stream));
+                 float scale, float* dw, float* db, uint16_t* dact, void* ws, size_t ws_bytes, void* stream) {
+  return head_bwd(dlogits, feat, wfc, n, hw, c, ncls, scale, dw, db, dact, (float*)ws, ws_bytes, S(stream));
 }
 int dtc_xent_fwd(const float* logits, const int64_t* labels, int n, int ncls, float* loss, float* lse, void* stream) {
   return xent_fwd(logits, labels, n, ncls, loss, lse, S(stream));

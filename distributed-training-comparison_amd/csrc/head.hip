@@ -61,55 +61,48 @@ int stem_pack_weight(const u16* w27, u16* w64, int K, hipStream_t st) {
   return 0;
 }
 
-// 4 images per workgroup: pooled features in LDS, then one thread per class computes the 4 dot
-// products with 16-byte weight loads (C % 8 == 0).
-constexpr int HEAD_IMGS = 4;
-__global__ void __launch_bounds__(256) head_fwd_kernel(const u16* __restrict__ act, int N, int HW, int C,
-                                                      const u16* __restrict__ wfc, const float* __restrict__ bfc,
-                                                      int ncls, float* __restrict__ feat,
-                                                      float* __restrict__ logits) {
-  extern __shared__ float f[];  // [HEAD_IMGS][C]
-  const int n0 = blockIdx.x * HEAD_IMGS, t = threadIdx.x;
-  const float inv = 1.f / (float)HW;
-  for (int e = t; e < HEAD_IMGS * C; e += 256) {
-    const int i = e / C, c = e - i * C;
-    float v = 0.f;
-    if (n0 + i < N) {
-      const u16* a = act + (int64_t)(n0 + i) * HW * C + c;
-      float s = 0.f;
-      for (int p = 0; p < HW; ++p) s += bf2f(a[(int64_t)p * C]);
-      v = round_bf(s * inv);  // avg_pool2d output is bf16 under autocast
-      feat[(int64_t)(n0 + i) * C + c] = v;
-    }
-    f[e] = v;
+// Pool: feat[n][c] = bf16(mean_p act[n][p][c]); one thread per (n, c).
+__global__ void __launch_bounds__(256) head_pool_kernel(const u16* __restrict__ act, int N, int HW, int C,
+                                                       float* __restrict__ feat) {
+  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (i >= (int64_t)N * C) return;
+  const int64_t n = i / C, c = i - n * C;
+  const u16* a = act + n * HW * C + c;
+  float s = 0.f;
+  for (int p = 0; p < HW; ++p) s += bf2f(a[(int64_t)p * C]);
+  feat[i] = round_bf(s / (float)HW);  // avg_pool2d output is bf16 under autocast
+}
+
+// Linear: logits[n][j] = bf16(feat[n] . W[j] + bf16(b[j])); one thread per output, 16-byte loads.
+__global__ void __launch_bounds__(256) head_fc_kernel(const float* __restrict__ feat, int N, int C,
+                                                     const u16* __restrict__ wfc, const float* __restrict__ bfc,
+                                                     int ncls, float* __restrict__ logits) {
+  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (i >= (int64_t)N * ncls) return;
+  const int64_t n = i / ncls, j = i - n * ncls;
+  const f32x4* f = (const f32x4*)(feat + n * C);
+  const uint4* w = (const uint4*)(wfc + j * C);
+  float acc = 0.f;
+#pragma unroll 4
+  for (int c8 = 0; c8 < C / 8; ++c8) {
+    float wv[8];
+    unpack8(w[c8], wv);
+    const f32x4 a = f[2 * c8], b = f[2 * c8 + 1];
+    acc += a[0] * wv[0] + a[1] * wv[1] + a[2] * wv[2] + a[3] * wv[3] + b[0] * wv[4] + b[1] * wv[5] + b[2] * wv[6] +
+           b[3] * wv[7];
   }
-  __syncthreads();
-  for (int j = t; j < ncls; j += 256) {
-    float acc[HEAD_IMGS] = {0.f, 0.f, 0.f, 0.f};
-    const uint4* w = (const uint4*)(wfc + (int64_t)j * C);
-    for (int c8 = 0; c8 < C / 8; ++c8) {
-      float wv[8];
-      unpack8(w[c8], wv);
-#pragma unroll
-      for (int i = 0; i < HEAD_IMGS; ++i) {
-        const float* fi = f + i * C + c8 * 8;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[i] += fi[k] * wv[k];
-      }
-    }
-    const float b = round_bf(bfc[j]);
-#pragma unroll
-    for (int i = 0; i < HEAD_IMGS; ++i)
-      if (n0 + i < N) logits[(int64_t)(n0 + i) * ncls + j] = round_bf(acc[i] + b);  // bf16 linear under autocast
-  }
+  logits[i] = round_bf(acc + round_bf(bfc[j]));  // bf16 linear under autocast
 }
 
 int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st) {
   DTC_CHECK_ARG(act && wfc && bfc && feat && logits && N > 0 && HW > 0 && C > 0 && C % 8 == 0 && ncls > 0,
                 "head_fwd: bad args");
-  hipLaunchKernelGGL(head_fwd_kernel, dim3((N + HEAD_IMGS - 1) / HEAD_IMGS), dim3(256),
-                     HEAD_IMGS * C * sizeof(float), st, act, N, HW, C, wfc, bfc, ncls, feat, logits);
+  hipLaunchKernelGGL(head_pool_kernel, dim3((int)(((int64_t)N * C + 255) / 256)), dim3(256), 0, st, act, N, HW, C,
+                     feat);
+  DTC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(head_fc_kernel, dim3((int)(((int64_t)N * ncls + 255) / 256)), dim3(256), 0, st, feat, N, C, wfc,
+                     bfc, ncls, logits);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -181,41 +174,58 @@ int xent_bwd(const float* logits, const int64_t* labels, const float* lse, const
 }
 
 // dW[j][c] = scale * sum_n dl[n][j] * feat[n][c]; db[j] = scale * sum_n dl[n][j]
-// workgroup tile: 16 classes x 64 channels; thread = 1 channel x 4 classes; images streamed in order.
-__global__ void __launch_bounds__(256) head_bwd_w_kernel(const float* __restrict__ dl, const float* __restrict__ feat,
-                                                        int N, int C, int ncls, float scale, float* __restrict__ dw,
-                                                        float* __restrict__ db) {
-  __shared__ float dls[64][16];
+// Stage 1: workgroup (64 channels, 16 classes, 32 images) -> partial slab [split][j][c] (plain stores).
+constexpr int HB_IMGS = 32;
+__global__ void __launch_bounds__(256) head_bwd_w_partial_kernel(const float* __restrict__ dl,
+                                                                const float* __restrict__ feat, int N, int C,
+                                                                int ncls, float* __restrict__ part) {
+  __shared__ float dls[HB_IMGS][16];
   const int t = threadIdx.x;
   const int c = blockIdx.x * 64 + (t & 63);
-  const int j0 = blockIdx.y * 16 + (t >> 6) * 4;
+  const int jq = (t >> 6) * 4;
+  const int n0 = blockIdx.z * HB_IMGS;
+  for (int e = t; e < HB_IMGS * 16; e += 256) {
+    const int n = n0 + (e >> 4), j = blockIdx.y * 16 + (e & 15);
+    dls[e >> 4][e & 15] = (n < N && j < ncls) ? dl[(int64_t)n * ncls + j] : 0.f;
+  }
+  __syncthreads();
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  float dbs = 0.f;
-  for (int nb = 0; nb < N; nb += 64) {
-    __syncthreads();
-    for (int e = t; e < 64 * 16; e += 256) {
-      const int n = nb + (e >> 4), j = blockIdx.y * 16 + (e & 15);
-      dls[e >> 4][e & 15] = (n < N && j < ncls) ? dl[(int64_t)n * ncls + j] : 0.f;
-    }
-    __syncthreads();
-    const int nn = min(64, N - nb);
-    if (c < C) {
-#pragma unroll 8
-      for (int i = 0; i < nn; ++i) {
-        const float fv = feat[(int64_t)(nb + i) * C + c];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] += dls[i][(t >> 6) * 4 + q] * fv;
-      }
-    }
-    if (blockIdx.x == 0 && t < 16)
-      for (int i = 0; i < nn; ++i) dbs += dls[i][t];
-  }
+  const int nn = min(HB_IMGS, N - n0);
   if (c < C) {
+#pragma unroll 8
+    for (int i = 0; i < nn; ++i) {
+      const float fv = feat[(int64_t)(n0 + i) * C + c];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (j0 + q < ncls) dw[(int64_t)(j0 + q) * C + c] = acc[q] * scale;
+      for (int q = 0; q < 4; ++q) acc[q] += dls[i][jq + q] * fv;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = blockIdx.y * 16 + jq + q;
+      if (j < ncls) part[((int64_t)blockIdx.z * ncls + j) * C + c] = acc[q];
+    }
   }
-  if (blockIdx.x == 0 && t < 16 && blockIdx.y * 16 + t < ncls) db[blockIdx.y * 16 + t] = dbs * scale;
+}
+
+// Stage 2: fixed-order sum over splits; thread per (j, c); db by the c == 0 threads.
+__global__ void __launch_bounds__(256) head_bwd_w_reduce_kernel(const float* __restrict__ part, int splits,
+                                                               const float* __restrict__ dl, int N, int C, int ncls,
+                                                               float scale, float* __restrict__ dw,
+                                                               float* __restrict__ db) {
+  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (i >= (int64_t)ncls * C) return;
+  float a = 0.f;
+  for (int s = 0; s < splits; ++s) a += part[(int64_t)s * ncls * C + i];
+  dw[i] = a * scale;
+  const int64_t j = i / C, c = i - j * C;
+  if (c == 0) {
+    float b = 0.f;
+    for (int n = 0; n < N; ++n) b += dl[(int64_t)n * ncls + j];
+    db[j] = b * scale;
+  }
+}
+
+size_t head_bwd_workspace(int N, int C, int ncls) {
+  return (size_t)((N + HB_IMGS - 1) / HB_IMGS) * ncls * C * sizeof(float);
 }
 
 // dact[n][p][c] = (sum_j dl[n][j] * W[j][c]) / HW
@@ -236,11 +246,16 @@ __global__ void __launch_bounds__(256) head_bwd_x_kernel(const float* __restrict
 }
 
 int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int HW, int C, int ncls, float scale,
-             float* dw, float* db, u16* dact, hipStream_t st) {
+             float* dw, float* db, u16* dact, float* ws, size_t ws_bytes, hipStream_t st) {
   DTC_CHECK_ARG(dlogits && feat && wfc && dw && db && dact && N > 0 && HW > 0 && C > 0 && ncls > 0,
                 "head_bwd: bad args");
-  hipLaunchKernelGGL(head_bwd_w_kernel, dim3((C + 63) / 64, (ncls + 15) / 16), dim3(256), 0, st, dlogits, feat, N,
-                     C, ncls, scale, dw, db);
+  DTC_CHECK_ARG(ws && ws_bytes >= head_bwd_workspace(N, C, ncls), "head_bwd: workspace too small");
+  const int splits = (N + HB_IMGS - 1) / HB_IMGS;
+  hipLaunchKernelGGL(head_bwd_w_partial_kernel, dim3((C + 63) / 64, (ncls + 15) / 16, splits), dim3(256), 0, st,
+                     dlogits, feat, N, C, ncls, ws);
+  DTC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(head_bwd_w_reduce_kernel, dim3((int)(((int64_t)ncls * C + 255) / 256)), dim3(256), 0, st, ws,
+                     splits, dlogits, N, C, ncls, scale, dw, db);
   DTC_LAUNCH_CHECK();
   hipLaunchKernelGGL(head_bwd_x_kernel, dim3(N), dim3(256), ncls * sizeof(float), st, dlogits, wfc, HW, C, ncls,
                      dact);

@@ -84,8 +84,9 @@ int xent_fwd(const float* logits, const int64_t* labels, int N, int ncls, float*
 int xent_bwd(const float* logits, const int64_t* labels, const float* lse, const float* gscale, int N, int ncls,
              float* dlogits, hipStream_t st);
 // dW = scale*dlogits^T feat ; db = scale*sum dlogits ; dact[n][hw][c] = (dlogits . W)[c] / HW
+size_t head_bwd_workspace(int N, int C, int ncls);
 int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int HW, int C, int ncls, float scale,
-             float* dw, float* db, u16* dact, hipStream_t st);
+             float* dw, float* db, u16* dact, float* ws, size_t ws_bytes, hipStream_t st);
 
 // ------------------------------------------------------------------ optimizer / amp / casts
 // Nesterov SGD over a flat buffer (torch.optim.SGD semantics, dampening 0).

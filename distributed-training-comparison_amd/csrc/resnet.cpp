@@ -71,6 +71,7 @@ struct Net {
   // workspace
   size_t ws_bytes = 0;
   size_t X0 = 0, WSTEM = 0, C0 = 0, A0 = 0, FEAT = 0, G[6] = {0, 0, 0, 0, 0, 0}, SLAB = 0;
+  size_t HEADWS = 0, HEADWS_bytes = 0;
   size_t slab_bytes = 0;
   size_t stats_lo = 0, stats_hi = 0;  // region that must start zeroed
   // buckets: [offset, numel) in flat elements, and the block index after whose backward it fires
@@ -259,6 +260,8 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
     n.acts.push_back({pre + ".out", b.OUT, (int)B, b.Hout, b.Wout, b.Cout});
   }
   n.FEAT = take(B * 512 * 4);
+  n.HEADWS_bytes = head_bwd_workspace((int)B, 512, n.ncls);
+  n.HEADWS = take(n.HEADWS_bytes);
   n.acts.push_back({"head.feat_f32", n.FEAT, (int)B, 1, 1, 512});
   for (int i = 0; i < 6; ++i) n.G[i] = take(gmax * 2);
   // BN per-layer state
@@ -430,7 +433,7 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
   float* slab = n.at<float>(n.SLAB);
   const BlockL& last = n.blocks.back();
   DTC_TRY(head_bwd(dlogits, n.at<float>(n.FEAT), n.wbf(n.fc_w), n.B, last.Hout * last.Wout, 512, n.ncls, gs,
-                   n.gf(n.fc_w), n.gf(n.fc_b), G[0], st));
+                   n.gf(n.fc_w), n.gf(n.fc_b), G[0], n.at<float>(n.HEADWS), n.HEADWS_bytes, st));
   for (int bi = (int)n.blocks.size() - 1; bi >= 0; --bi) {
     BlockL& b = n.blocks[bi];
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;

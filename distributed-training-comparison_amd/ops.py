@@ -166,8 +166,10 @@ def head_bwd(dlogits, feat, wfc, hw, scale=1.0):
     db = torch.empty(ncls, dtype=torch.float32, device=feat.device)
     h, w = hw
     dact = torch.empty(n, h, w, c, dtype=torch.bfloat16, device=feat.device)
+    nb = lib.dtc_head_bwd_workspace_size(n, c, ncls)
+    ws = torch.empty(nb // 4 + 1, dtype=torch.float32, device=feat.device)
     call("dtc_head_bwd", ptr(dlogits), ptr(feat), ptr(wfc), n, h * w, c, ncls, float(scale), ptr(dw), ptr(db),
-         ptr(dact), stream_ptr())
+         ptr(dact), ptr(ws), nb, stream_ptr())
     return dw, db, dact
 
 

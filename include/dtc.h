@@ -98,8 +98,9 @@ int dtc_stem_im2col(const float* x_nchw, uint16_t* cols, int n, int h, int w, vo
 int dtc_stem_pack_weight(const uint16_t* w27, uint16_t* w64, int k, void* stream);
 int dtc_head_fwd(const uint16_t* act, int n, int hw, int c, const uint16_t* wfc, const float* bfc, int ncls,
                  float* feat, float* logits, void* stream);
+size_t dtc_head_bwd_workspace_size(int n, int c, int ncls);
 int dtc_head_bwd(const float* dlogits, const float* feat, const uint16_t* wfc, int n, int hw, int c, int ncls,
-                 float scale, float* dw, float* db, uint16_t* dact, void* stream);
+                 float scale, float* dw, float* db, uint16_t* dact, void* ws, size_t ws_bytes, void* stream);
 int dtc_xent_fwd(const float* logits, const int64_t* labels, int n, int ncls, float* loss, float* lse,
                  void* stream);
 int dtc_xent_bwd(const float* logits, const int64_t* labels, const float* lse, const float* gscale, int n, int ncls,

@@ -180,8 +180,9 @@ def test_end_to_end_drift_bounded(dtc, cuda, batch):
     g_exe = np.concatenate([_np(p.grad).ravel() for _, p in model.named_parameters()])
     g_ref = np.concatenate([ref["grads"][k].ravel() for k, _ in model.named_parameters()])
     assert rel_err(g_exe, g_ref) < 0.35
-    # the head and layer4 gradients are far from the noise floor: hold them to 2e-2
-    for k in ("linear.weight", "linear.bias", "layer4.1.conv2.weight", "layer4.1.bn2.weight"):
+    # only the head gradients sit above the rounding-noise floor (oracle-vs-oracle: linear.weight
+    # 0.6%, linear.bias 0.03%, but layer4.1.conv2.weight already 13-14%): hold those to 2e-2
+    for k in ("linear.weight", "linear.bias"):
         assert rel_err(_np(dict(model.named_parameters())[k].grad), ref["grads"][k]) < 2e-2, k
     sd2 = model.state_dict()
     for k, v in ref["buffers"].items():  # running statistics after one training forward
