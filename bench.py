@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--no-item", action="store_true", help="drop the per-step loss.item() host sync")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-live-roofline", action="store_true", help="skip the per-conv timing in the timed region")
     args = ap.parse_args()
 
     rank, world, local = init_dist()
@@ -130,7 +131,8 @@ def main():
     exe = model.module.executor(B, S, S)
     dist.barrier()
     torch.cuda.synchronize()
-    dtc._native.call("dtc_rn18_profile_begin", exe.handle, 128 * args.steps + 64)
+    if not args.no_live_roofline:
+        dtc._native.call("dtc_rn18_profile_begin", exe.handle, 128 * args.steps + 64)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
@@ -141,7 +143,8 @@ def main():
     ms = (C.c_double * 3)()
     fl = (C.c_double * 3)()
     cnt = (C.c_int * 3)()
-    dtc._native.call("dtc_rn18_profile_end", exe.handle, ms, fl, cnt)
+    if not args.no_live_roofline:
+        dtc._native.call("dtc_rn18_profile_end", exe.handle, ms, fl, cnt)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())

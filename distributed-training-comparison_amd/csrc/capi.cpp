@@ -12,8 +12,8 @@
 #include <cstring>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}};
-static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap", "dgrad_classes"};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}};
+static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap", "dgrad_classes", "wgrad_fast"};
 int option_get(int id) { return g_opts[id].load(std::memory_order_relaxed); }
 int option_set(const char* name, int value) {
   for (int i = 0; i < OPT_COUNT; ++i)

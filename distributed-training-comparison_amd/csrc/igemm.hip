@@ -41,6 +41,10 @@ struct IGemmParams {
   int num_kt, kt_per_split, tiles_a;
   int xcd_remap;
   int cls;  // DGRAD, stride 2: blockIdx.z = output parity class (h%2, w%2); M counts class pixels
+  // WGRAD fast path: each 64-pixel reduction step covers whole rows of one image (PQ % 64 == 0,
+  // 64 % Q == 0) or whole images (64 % PQ == 0); tensors < 4 GiB so 32-bit buffer offsets work.
+  int wg_fast;
+  uint32_t src0_bytes, src1_bytes;
 };
 
 __device__ __forceinline__ int rowswz(int row) { return (row >> 1) & 7; }
@@ -135,6 +139,11 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   // WGRAD: block-uniform tap, per-lane columns
   int colA[NIA], colB[NIB];
   int tap_r = 0, tap_s = 0;
+  uint32_t wl_x[2] = {0, 0};
+  int wl_ih[2] = {0, 0}, wl_row[2] = {0, 0};
+  bool wl_iwok[2] = {false, false};
+  __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src0, 0, p.src0_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, 0, p.src1_bytes, 0x00020000);
 
   if constexpr (MODE == MODE_FWD) {
 #pragma unroll
@@ -203,6 +212,21 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
       const int img = ib >> 3, rowin = (ib & 7) * 8 + lrow;
       colB[j] = b0 + img * 64 + ((pc ^ trswz(rowin)) * 8);
     }
+    if (p.wg_fast) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // this lane's two pixel rows within a 64-pixel step
+        const int rowin = (wave + 4 * h) * 8 + lrow;
+        const int dn = (int)fdiv((uint32_t)rowin, p.fd_pq);
+        const int rem = rowin - dn * (int)p.fd_pq.d;
+        const int dp = (int)fdiv((uint32_t)rem, p.fd_q);
+        const int dq = rem - dp * p.Q;
+        const int iw = dq * p.stride - p.pad + tap_s;
+        wl_iwok[h] = (unsigned)iw < (unsigned)p.W;
+        wl_ih[h] = dp * p.stride - p.pad + tap_r;
+        wl_x[h] = (uint32_t)((((dn * p.H + wl_ih[h]) * p.W) + iw) * p.C * 2);
+        wl_row[h] = rowin;
+      }
+    }
   }
 
   // reduction-step decomposition (FWD/DGRAD): kt -> (r, s, chunk); kept incrementally
@@ -256,7 +280,30 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
         const u16* src = ok ? (p.src0 + ((baseB[j] + ph) * p.Q + pw) * p.K + cc * 64 + colB[j]) : zp;
         glds16(src, sb + A_BYTES + (wave + 4 * j) * 1024);
       }
-    } else {  // WGRAD: pixels kt*64 .. kt*64+63
+    } else if (p.wg_fast) {  // WGRAD, 32-bit buffer offsets; out-of-range offsets zero-fill LDS
+      const int m0 = kt * 64;
+      const int n0 = (int)fdiv((uint32_t)m0, p.fd_pq);
+      const int p0 = (int)fdiv((uint32_t)(m0 - n0 * (int)p.fd_pq.d), p.fd_q);
+      const uint32_t ubase = (uint32_t)((n0 * p.H + p0 * p.stride) * p.W * p.C * 2);
+      uint32_t xoff[2], doff[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int pix = m0 + wl_row[h];
+        const bool okd = pix < p.M;
+        const int ih = p0 * p.stride + wl_ih[h];
+        const bool okx = okd && wl_iwok[h] && ((unsigned)ih < (unsigned)p.H);
+        xoff[h] = okx ? ubase + wl_x[h] : 0x80000000u;
+        doff[h] = okd ? (uint32_t)pix * (uint32_t)(p.K * 2) : 0x80000000u;
+      }
+#pragma unroll
+      for (int j = 0; j < NIA; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs0, (lds_void*)(sb + (wave + 4 * j) * 1024), 16,
+                                                 xoff[j & 1] + colA[j] * 2, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < NIB; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, (lds_void*)(sb + A_BYTES + (wave + 4 * j) * 1024), 16,
+                                                 doff[j & 1] + colB[j] * 2, 0, 0, 0);
+    } else {  // WGRAD generic: pixels kt*64 .. kt*64+63
       const int m0 = kt * 64;
       int64_t xo[2];
       int64_t dyo[2];
@@ -729,6 +776,15 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
   p.src0 = x; p.src1 = dy; p.slab = slab;
   p.M = s.N * p.P * p.Q;
   p.fd_q = make_fastdiv(p.Q); p.fd_pq = make_fastdiv(p.P * p.Q); p.fd_cc = make_fastdiv(1);
+  {
+    const int PQ = p.P * p.Q;
+    const uint64_t xb = (uint64_t)s.N * s.H * s.W * s.C * 2, db = (uint64_t)p.M * s.K * 2;
+    const bool rows = (PQ % 64 == 0) && (64 % p.Q == 0);
+    const bool imgs = (64 % PQ == 0);
+    p.wg_fast = (rows || imgs) && xb < (1ull << 31) && db < (1ull << 31) && option_get(OPT_WGRAD_FAST) != 0;
+    p.src0_bytes = (uint32_t)xb;
+    p.src1_bytes = (uint32_t)db;
+  }
   p.num_kt = pl.num_kt;
   p.tiles_a = p.RSC / pl.bm;
   const int tiles_b = s.K / pl.bn;

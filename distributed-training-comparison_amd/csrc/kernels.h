@@ -9,7 +9,7 @@
 namespace dtc {
 
 // ------------------------------------------------------------------ tuning options (atomic ints)
-enum { OPT_IGEMM_STAGES = 0, OPT_XCD_REMAP = 1, OPT_DGRAD_CLASSES = 2, OPT_COUNT };
+enum { OPT_IGEMM_STAGES = 0, OPT_XCD_REMAP = 1, OPT_DGRAD_CLASSES = 2, OPT_WGRAD_FAST = 3, OPT_COUNT };
 int option_get(int id);
 int option_set(const char* name, int value);
 

@@ -36,7 +36,8 @@ int dtc_abi_version(void);
 const char* dtc_last_error(void);
 /* Process-wide kernel tuning knobs (atomic; for benchmarking): "igemm_stages" (2 or 3 LDS stages
  * in the conv main loop, default 2), "xcd_remap" (XCD-aware tile order, default 1),
- * "dgrad_classes" (stride-2 data-gradient as 4 parity-class GEMMs, default 1). */
+ * "dgrad_classes" (stride-2 data-gradient as 4 parity-class GEMMs, default 1), "wgrad_fast" (buffer-
+ * offset weight-gradient loader for row-aligned pixel steps, default 1). */
 int dtc_set_option(const char* name, int value);
 int dtc_get_option(const char* name);
 
