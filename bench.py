@@ -126,13 +126,18 @@ def main():
         if not args.no_item:
             losses.append(loss.item())
 
+    # Live conv timing: every conv call stamps its first-workgroup start / last-workgroup end into a
+    # device slot (s_memrealtime), summed on the device once per step; arming it re-captures the
+    # step graphs, so it is armed after the first warmup step and re-zeroed before the timed region.
     for i in range(args.warmup):
         step(i)
+        if i == 0 and not args.no_live_roofline:
+            dtc._native.call("dtc_rn18_profile_begin", model.module.executor(B, S, S).handle, 1)
     exe = model.module.executor(B, S, S)
     dist.barrier()
     torch.cuda.synchronize()
     if not args.no_live_roofline:
-        dtc._native.call("dtc_rn18_profile_begin", exe.handle, 128 * args.steps + 64)
+        dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
@@ -181,7 +186,8 @@ def main():
                 "frac": round(achieved / BF16_PEAK_TFLOPS, 4) if achieved else None,
                 "traffic": None,
                 "kernel": "implicit-GEMM conv (fwd+dgrad+wgrad incl. split-K reduce), all launches in the timed "
-                          "region",
+                          "region; per-call duration = last workgroup end - first workgroup start (s_memrealtime, "
+                          "stamped by the kernels on the compute stream)",
                 "conv_ms_per_step": round(conv_ms / args.steps, 4),
                 "conv_ms_by_pass": [round(v / args.steps, 4) for v in ms],
                 "conv_calls_per_step": n_launch // max(1, args.steps),

@@ -12,13 +12,16 @@
 #include <cstring>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}};
-static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap", "dgrad_classes", "wgrad_fast"};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}};
+static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap", "dgrad_classes", "wgrad_fast", "graphs"};
+static std::atomic<int> g_epoch{0};
 int option_get(int id) { return g_opts[id].load(std::memory_order_relaxed); }
+int option_epoch() { return g_epoch.load(std::memory_order_relaxed); }
 int option_set(const char* name, int value) {
   for (int i = 0; i < OPT_COUNT; ++i)
     if (name && strcmp(name, g_opt_names[i]) == 0) {
       g_opts[i].store(value, std::memory_order_relaxed);
+      g_epoch.fetch_add(1, std::memory_order_relaxed);
       return 0;
     }
   return set_error(DTC_EINVAL, "unknown option %s", name ? name : "(null)");

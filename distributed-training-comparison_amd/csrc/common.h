@@ -12,6 +12,7 @@
 #include <stddef.h>
 
 typedef uint16_t u16;
+typedef unsigned long long u64;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

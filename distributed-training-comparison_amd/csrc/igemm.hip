@@ -45,7 +45,24 @@ struct IGemmParams {
   // 64 % Q == 0) or whole images (64 % PQ == 0); tensors < 4 GiB so 32-bit buffer offsets work.
   int wg_fast;
   uint32_t src0_bytes, src1_bytes;
+  u64* ts;  // optional call timing slot: atomicMin(start), atomicMax(end), s_memrealtime ticks
 };
+
+// 16-byte LDS-DMA through a buffer descriptor over [base, base + bytes): an offset outside the
+// range loads zeros. (Kept out of the loader lambda: the buffer builtins inside a lambda make the
+// host pass drop the kernel's launch stub.)
+__device__ __forceinline__ void buf_lds16(const void* base, uint32_t bytes, char* lds_dst, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_dst, 16, off, 0, 0, 0);
+}
+
+// Call-timing stamps (kernel entry / exit only, one lane per workgroup; nothing on the loop).
+__device__ __forceinline__ void stamp_start(u64* ts) {
+  if (ts != nullptr && threadIdx.x == 0) atomicMin(ts, (u64)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void stamp_end(u64* ts) {
+  if (ts != nullptr && threadIdx.x == 0) atomicMax(ts + 1, (u64)__builtin_amdgcn_s_memrealtime());
+}
 
 __device__ __forceinline__ int rowswz(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int trswz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
@@ -95,6 +112,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   static_assert(NSTAGE == 2 || NSTAGE == 3, "stages");
   __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE];
 
+  stamp_start(p.ts);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   // XCD-aware remap (guide T1): blocks b and b+8 share an XCD's L2; give each XCD a contiguous
@@ -142,8 +160,6 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   uint32_t wl_x[2] = {0, 0};
   int wl_ih[2] = {0, 0}, wl_row[2] = {0, 0};
   bool wl_iwok[2] = {false, false};
-  __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src0, 0, p.src0_bytes, 0x00020000);
-  __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, 0, p.src1_bytes, 0x00020000);
 
   if constexpr (MODE == MODE_FWD) {
 #pragma unroll
@@ -297,12 +313,10 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
       }
 #pragma unroll
       for (int j = 0; j < NIA; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs0, (lds_void*)(sb + (wave + 4 * j) * 1024), 16,
-                                                 xoff[j & 1] + colA[j] * 2, 0, 0, 0);
+        buf_lds16(p.src0, p.src0_bytes, sb + (wave + 4 * j) * 1024, xoff[j & 1] + colA[j] * 2);
 #pragma unroll
       for (int j = 0; j < NIB; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, (lds_void*)(sb + A_BYTES + (wave + 4 * j) * 1024), 16,
-                                                 doff[j & 1] + colB[j] * 2, 0, 0, 0);
+        buf_lds16(p.src1, p.src1_bytes, sb + A_BYTES + (wave + 4 * j) * 1024, doff[j & 1] + colB[j] * 2);
     } else {  // WGRAD generic: pixels kt*64 .. kt*64+63
       const int m0 = kt * 64;
       int64_t xo[2];
@@ -530,6 +544,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
       }
     }
   }
+  stamp_end(p.ts);
 }
 
 // ---------------------------------------------------------------- split-K reduction (FWD / DGRAD)
@@ -538,7 +553,8 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int splits,
                                                             int M, int Nc, u16* __restrict__ out,
                                                             const u16* __restrict__ res,
-                                                            double* __restrict__ stats, int rows_per_block) {
+                                                            double* __restrict__ stats, int rows_per_block,
+                                                            u64* ts) {
   __shared__ float red[256 * 16];
   const int tpr = Nc >> 3;           // threads per row (8 channels each)
   const int rpp = 256 / tpr;         // rows per pass
@@ -573,24 +589,26 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
       *(uint4*)(out + o) = pack8(v);
     }
   }
-  if (!stats) return;
+  if (stats) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    red[t * 16 + k] = s[k];
-    red[t * 16 + 8 + k] = q[k];
-  }
-  __syncthreads();
-  double* st = stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * Nc;
-  for (int c = t; c < Nc; c += 256) {
-    const int gg = c >> 3, k = c & 7;
-    float a = 0.f, b = 0.f;
-    for (int r2 = 0; r2 < rpp; ++r2) {
-      a += red[(r2 * tpr + gg) * 16 + k];
-      b += red[(r2 * tpr + gg) * 16 + 8 + k];
+    for (int k = 0; k < 8; ++k) {
+      red[t * 16 + k] = s[k];
+      red[t * 16 + 8 + k] = q[k];
     }
-    unsafeAtomicAdd(st + c, (double)a);
-    unsafeAtomicAdd(st + Nc + c, (double)b);
+    __syncthreads();
+    double* st = stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * Nc;
+    for (int c = t; c < Nc; c += 256) {
+      const int gg = c >> 3, k = c & 7;
+      float a = 0.f, b = 0.f;
+      for (int r2 = 0; r2 < rpp; ++r2) {
+        a += red[(r2 * tpr + gg) * 16 + k];
+        b += red[(r2 * tpr + gg) * 16 + 8 + k];
+      }
+      unsafeAtomicAdd(st + c, (double)a);
+      unsafeAtomicAdd(st + Nc + c, (double)b);
+    }
   }
+  stamp_end(ts);
 }
 
 // ---------------------------------------------------------------- wgrad split reduction
@@ -600,7 +618,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 template <int SG>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K,
                                                            int ld_in, int ncols, int ld_out, float scale,
-                                                           float* __restrict__ grad) {
+                                                           float* __restrict__ grad, u64* ts) {
   constexpr int OPB = 256 / SG;  // outputs (float4) per block
   __shared__ f32x4 red[256];
   const size_t plane = (size_t)K * ld_in;
@@ -629,6 +647,20 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
         if (c + j < ncols) grad[(size_t)k * ld_out + c + j] = a[j];
     }
   }
+  stamp_end(ts);
+}
+
+// per-call timing slots -> running totals (one launch per training step when profiling)
+__global__ void prof_accumulate_kernel(u64* ts, int n, u64* acc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const u64 a = ts[2 * i], b = ts[2 * i + 1];
+  if (b > a) {
+    acc[2 * i] += b - a;
+    acc[2 * i + 1] += 1;
+  }
+  ts[2 * i] = ~0ull;
+  ts[2 * i + 1] = 0;
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -702,8 +734,9 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
 }
 
 int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
-             size_t slab_bytes, hipStream_t st) {
+             size_t slab_bytes, hipStream_t st, u64* ts) {
   IGemmParams p{};
+  p.ts = ts;
   DTC_TRY(fill_common(p, s));
   ConvPlan pl = plan_conv(s, CONV_FWD);
   p.src0 = x; p.src1 = w; p.out = y; p.stats = stats;
@@ -721,7 +754,7 @@ int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* sta
     if (pl.bn == 64) DTC_TRY((launch_igemm<MODE_FWD, 64, 64, 2, 2, true>(p, tiles_b, splits, st)));
     else if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_FWD, 64, 256, 1, 4, true>(p, tiles_b, splits, st)));
     else DTC_TRY((launch_igemm<MODE_FWD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
-    return splitk_reduce(slab, splits, p.M, s.K, y, nullptr, stats, st);
+    return splitk_reduce(slab, splits, p.M, s.K, y, nullptr, stats, st, ts);
   }
   if (pl.bn == 64) return launch_igemm<MODE_FWD, 64, 64, 2, 2, false>(p, tiles_b, 1, st);
   if (pl.bm == 64) return launch_igemm<MODE_FWD, 64, 256, 1, 4, false>(p, tiles_b, 1, st);
@@ -729,8 +762,9 @@ int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* sta
 }
 
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
-               size_t slab_bytes, hipStream_t st) {
+               size_t slab_bytes, hipStream_t st, u64* ts) {
   IGemmParams p{};
+  p.ts = ts;
   DTC_TRY(fill_common(p, s));
   ConvPlan pl = plan_conv(s, CONV_DGRAD);
   p.src0 = dy; p.src1 = w; p.out = dx; p.res = res;
@@ -760,7 +794,7 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
     if (pl.bn == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 64, 2, 2, true>(p, tiles_b, splits, st)));
     else if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 256, 1, 4, true>(p, tiles_b, splits, st)));
     else DTC_TRY((launch_igemm<MODE_DGRAD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
-    return splitk_reduce(slab, splits, p.M, s.C, dx, res, nullptr, st);
+    return splitk_reduce(slab, splits, p.M, s.C, dx, res, nullptr, st, ts);
   }
   if (pl.bn == 64) return launch_igemm<MODE_DGRAD, 64, 64, 2, 2, false>(p, tiles_b, 1, st);
   if (pl.bm == 64) return launch_igemm<MODE_DGRAD, 64, 256, 1, 4, false>(p, tiles_b, 1, st);
@@ -768,8 +802,9 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
 }
 
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
-               float* slab, size_t slab_bytes, hipStream_t st) {
+               float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
   IGemmParams p{};
+  p.ts = ts;
   DTC_TRY(fill_common(p, s));
   ConvPlan pl = plan_conv(s, CONV_WGRAD);
   DTC_CHECK_ARG(slab != nullptr && slab_bytes >= (size_t)s.K * p.RSC * 4, "wgrad: slab workspace too small");
@@ -801,18 +836,18 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
   while (sg < 16 && sg * 2 <= splits && (nv * sg) / 256 < 1024) sg *= 2;
   const int blocks = (int)((nv + (256 / sg) - 1) / (256 / sg));
   switch (sg) {
-    case 1: hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw); break;
-    case 2: hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw); break;
-    case 4: hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw); break;
-    case 8: hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw); break;
-    default: hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw); break;
+    case 1: hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw, ts); break;
+    case 2: hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw, ts); break;
+    case 4: hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw, ts); break;
+    case 8: hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw, ts); break;
+    default: hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw, ts); break;
   }
   DTC_LAUNCH_CHECK();
   return 0;
 }
 
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
-                  hipStream_t st) {
+                  hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(Nc % 8 == 0 && Nc <= 2048, "splitk_reduce: channels %d", Nc);
   const int tpr = Nc / 8;
   const int rpp = 256 / tpr;
@@ -821,7 +856,13 @@ int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const 
   rows_per_block = ((rows_per_block + rpp - 1) / rpp) * rpp;
   const int blocks = ceil_div(M, rows_per_block);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, splits, M, Nc, out, res, stats,
-                     rows_per_block);
+                     rows_per_block, ts);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+int prof_accumulate(u64* ts, int n, u64* acc, hipStream_t st) {
+  hipLaunchKernelGGL(prof_accumulate_kernel, dim3((n + 63) / 64), dim3(64), 0, st, ts, n, acc);
   DTC_LAUNCH_CHECK();
   return 0;
 }

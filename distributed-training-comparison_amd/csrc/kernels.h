@@ -9,9 +9,10 @@
 namespace dtc {
 
 // ------------------------------------------------------------------ tuning options (atomic ints)
-enum { OPT_IGEMM_STAGES = 0, OPT_XCD_REMAP = 1, OPT_DGRAD_CLASSES = 2, OPT_WGRAD_FAST = 3, OPT_COUNT };
+enum { OPT_IGEMM_STAGES = 0, OPT_XCD_REMAP = 1, OPT_DGRAD_CLASSES = 2, OPT_WGRAD_FAST = 3, OPT_GRAPHS = 4, OPT_COUNT };
 int option_get(int id);
 int option_set(const char* name, int value);
+int option_epoch();  // bumped by every option_set (captured graphs bake the options in)
 
 // ------------------------------------------------------------------ convolution
 struct ConvShape {
@@ -28,16 +29,20 @@ ConvPlan plan_conv(const ConvShape& s, int mode);
 
 // y = conv(x, w) (bf16 NHWC out); optional BN statistics of the bf16 output into
 // stats[SLOTS][2][K] (sum, sum of squares; fp64, accumulated).
+// `ts` (optional, every conv launcher): a [2] u64 slot receiving min(start) / max(end) of the
+// call's workgroups in s_memrealtime ticks (graph-safe per-call timing, see prof_accumulate).
 int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
-             size_t slab_bytes, hipStream_t st);
+             size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 // dx = conv_transpose(dy, w) (+ res), bf16 NHWC
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
-               size_t slab_bytes, hipStream_t st);
+               size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 // dw[k][0:dw_cols] (row stride dw_ld) = scale * sum_pixels dy (x) im2col(x); fp32
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
-               float* slab, size_t slab_bytes, hipStream_t st);
+               float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
-                  hipStream_t st);
+                  hipStream_t st, u64* ts = nullptr);
+// per slot i of ts[n][2]: if end > start, acc[i] += (end - start, 1); slot reset to (~0, 0)
+int prof_accumulate(u64* ts, int n, u64* acc, hipStream_t st);
 
 // ------------------------------------------------------------------ batch norm (NHWC, C channels, M pixels)
 // forward finalize: mean/invstd/scale/shift from stats; running-stat update; stats re-zeroed.

@@ -77,11 +77,27 @@ struct Net {
   // buckets: [offset, numel) in flat elements, and the block index after whose backward it fires
   std::vector<int64_t> bucket_off, bucket_len;
   std::vector<int> bucket_after_block;  // -1 = after the stem (last)
-  // live conv timing (bench roofline): event pairs around every conv call on the compute stream
-  struct ProfPair { hipEvent_t a = nullptr, b = nullptr; double flops = 0; int kind = 0; };
-  std::vector<ProfPair> prof;
-  size_t prof_used = 0;
+  // live conv timing (bench roofline): each conv call stamps min(start)/max(end) of its workgroups
+  // (s_memrealtime) into its own slot; one kernel per step folds the slots into running totals.
+  // Graph-safe: the slot pointers are baked at capture, nothing happens on the host per call.
+  static constexpr int PROF_SLOTS = 128, PROF_BWD0 = 32;  // forward calls use [0,32), backward [32,128)
   bool profiling = false;
+  u64* prof_ts = nullptr;   // [PROF_SLOTS][2] device
+  u64* prof_acc = nullptr;  // [PROF_SLOTS][2] device: (sum ticks, calls)
+  int prof_next = 0;
+  int prof_kind[PROF_SLOTS] = {};
+  double prof_flops[PROF_SLOTS] = {};
+  int prof_khz = 100000;
+  // hipGraph replay (option "graphs"): the forward per train flag, the backward as segments split
+  // at bucket boundaries (the all-reduces stay eager on the communicator's side stream)
+  struct Seg { hipGraphExec_t exec = nullptr; std::vector<int> buckets; };
+  hipStream_t cap_st = nullptr;
+  int graph_epoch = -1;
+  hipGraphExec_t fwd_exec[2] = {nullptr, nullptr};
+  std::vector<Seg> bwd_segs;
+  float bwd_gs = 0.f;
+  bool bwd_comm = false;
+  size_t LOGITS = 0, DLOGITS = 0;  // graph-owned copies of the caller's logits / dlogits
   // activation registry (per-layer parity): name, workspace byte offset, N,H,W,C
   struct Act { std::string name; size_t off; int n, h, w, c; };
   std::vector<Act> acts;
@@ -260,6 +276,8 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
     n.acts.push_back({pre + ".out", b.OUT, (int)B, b.Hout, b.Wout, b.Cout});
   }
   n.FEAT = take(B * 512 * 4);
+  n.LOGITS = take(B * n.ncls * 4);
+  n.DLOGITS = take(B * n.ncls * 4);
   n.HEADWS_bytes = head_bwd_workspace((int)B, 512, n.ncls);
   n.HEADWS = take(n.HEADWS_bytes);
   n.acts.push_back({"head.feat_f32", n.FEAT, (int)B, 1, 1, 512});
@@ -333,26 +351,60 @@ static double conv_flops(const ConvShape& s) {
   const int P = (s.H + 2 * s.pad - s.R) / s.stride + 1, Q = (s.W + 2 * s.pad - s.S) / s.stride + 1;
   return 2.0 * s.N * P * Q * (double)s.K * s.R * s.S * s.C;
 }
-static int prof_begin(Net& n, hipStream_t st) {
-  if (!n.profiling) return 0;
-  if (n.prof_used >= n.prof.size()) return set_error(DTC_EINVAL, "profile event capacity exhausted");
-  DTC_HIP(hipEventRecord(n.prof[n.prof_used].a, st));
-  return 0;
+static u64* prof_slot(Net& n, int kind, double flops) {
+  if (!n.profiling || n.prof_next >= Net::PROF_SLOTS) return nullptr;
+  const int i = n.prof_next++;
+  n.prof_kind[i] = kind;
+  n.prof_flops[i] = flops;
+  return n.prof_ts + 2 * i;
 }
-static int prof_end(Net& n, hipStream_t st, double flops, int kind) {
-  if (!n.profiling) return 0;
-  auto& e = n.prof[n.prof_used++];
-  e.flops = flops;
-  e.kind = kind;
-  DTC_HIP(hipEventRecord(e.b, st));
-  return 0;
-}
-#define PROF(kind, flops, call)                    \
-  do {                                             \
-    DTC_TRY(prof_begin(n, st));                    \
-    DTC_TRY(call);                                 \
-    DTC_TRY(prof_end(n, st, (flops), (kind)));     \
+#define PROF(kind, flops, call)                        \
+  do {                                                 \
+    u64* ts = prof_slot(n, (kind), (flops));           \
+    DTC_TRY(call);                                     \
   } while (0)
+
+// ------------------------------------------------------------------ graph capture helpers
+static void drop_graphs(Net& n) {
+  for (auto& e : n.fwd_exec)
+    if (e) {
+      (void)hipGraphExecDestroy(e);
+      e = nullptr;
+    }
+  for (auto& sg : n.bwd_segs)
+    if (sg.exec) (void)hipGraphExecDestroy(sg.exec);
+  n.bwd_segs.clear();
+}
+static bool graphs_on(Net& n) {
+  if (n.capture || option_get(OPT_GRAPHS) == 0) return false;
+  if (n.graph_epoch != option_epoch()) {  // options are baked into captured launches
+    drop_graphs(n);
+    n.graph_epoch = option_epoch();
+  }
+  return true;
+}
+static int begin_capture(Net& n) {
+  if (!n.cap_st) DTC_HIP(hipStreamCreateWithFlags(&n.cap_st, hipStreamNonBlocking));
+  DTC_HIP(hipStreamBeginCapture(n.cap_st, hipStreamCaptureModeRelaxed));
+  return 0;
+}
+// Ends the capture on n.cap_st (always, also when the captured body failed); *out stays null
+// for an empty capture.
+static int end_capture(Net& n, int body_rc, hipGraphExec_t* out) {
+  *out = nullptr;
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(n.cap_st, &g);
+  if (body_rc != 0 || e != hipSuccess) {
+    if (g) (void)hipGraphDestroy(g);
+    return body_rc != 0 ? body_rc : set_error((int)e, "hipStreamEndCapture: %s", hipGetErrorString(e));
+  }
+  size_t nodes = 0;
+  e = hipGraphGetNodes(g, nullptr, &nodes);
+  if (e == hipSuccess && nodes > 0) e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) return set_error((int)e, "graph instantiate: %s", hipGetErrorString(e));
+  return 0;
+}
 
 // ------------------------------------------------------------------ forward / backward
 static int bn_finalize_fwd(Net& n, BNL& b, int64_t count, bool train, hipStream_t st) {
@@ -365,14 +417,15 @@ static int bn_finalize_fwd(Net& n, BNL& b, int64_t count, bool train, hipStream_
                       n.at<float>(b.mean), n.at<float>(b.invstd), n.at<float>(b.scale), n.at<float>(b.shift), st);
 }
 
-static int forward(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
+// everything after the input im2col (reads only executor-owned memory: capturable)
+static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
   u16* X0 = n.at<u16>(n.X0);
+  n.prof_next = train ? 0 : Net::PROF_SLOTS;  // eval passes are not timed
   DTC_TRY(stem_pack_weight(n.wbf(n.stem.pidx), n.at<u16>(n.WSTEM), 64, st));
-  DTC_TRY(stem_im2col(x, X0, n.B, n.H, n.W, st));
   PROF(0, 2.0 * M0 * 64 * 27,
        conv_fwd(n.stem.s, X0, n.at<u16>(n.WSTEM), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
-                n.at<float>(n.SLAB), n.slab_bytes, st));
+                n.at<float>(n.SLAB), n.slab_bytes, st, ts));
   DTC_TRY(bn_finalize_fwd(n, n.bn0, M0, train, st));
   DTC_TRY(bn_apply_relu(n.at<u16>(n.C0), n.at<float>(n.bn0.scale), n.at<float>(n.bn0.shift), n.at<u16>(n.A0), M0, 64,
                         st));
@@ -382,18 +435,18 @@ static int forward(Net& n, const float* x, float* logits, bool train, hipStream_
     float* slab = n.at<float>(n.SLAB);
     PROF(0, conv_flops(b.c1.s),
          conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
-                  n.slab_bytes, st));
+                  n.slab_bytes, st, ts));
     DTC_TRY(bn_finalize_fwd(n, b.b1, M, train, st));
     DTC_TRY(bn_apply_relu(n.at<u16>(b.C1), n.at<float>(b.b1.scale), n.at<float>(b.b1.shift), n.at<u16>(b.A1), M,
                           b.Cout, st));
     PROF(0, conv_flops(b.c2.s),
          conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
-                  train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st));
+                  train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st, ts));
     DTC_TRY(bn_finalize_fwd(n, b.b2, M, train, st));
     if (b.proj) {
       PROF(0, conv_flops(b.sc.s),
            conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr,
-                    slab, n.slab_bytes, st));
+                    slab, n.slab_bytes, st, ts));
       DTC_TRY(bn_finalize_fwd(n, b.bsc, M, train, st));
       DTC_TRY(bn_apply_dual_relu(n.at<u16>(b.C2), n.at<float>(b.b2.scale), n.at<float>(b.b2.shift), n.at<u16>(b.S),
                                  n.at<float>(b.bsc.scale), n.at<float>(b.bsc.shift), n.at<u16>(b.OUT), M, b.Cout, st));
@@ -408,13 +461,43 @@ static int forward(Net& n, const float* x, float* logits, bool train, hipStream_
                   logits, st);
 }
 
-static int maybe_bucket(Net& n, int after_block, Comm* comm, hipStream_t st) {
-  if (!comm) return 0;
-  for (size_t i = 0; i < n.bucket_off.size(); ++i) {
-    if (n.bucket_after_block[i] == after_block)
-      DTC_TRY(comm_allreduce_async(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st));
+static int forward(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
+  DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
+  if (!graphs_on(n)) return forward_body(n, logits, train, st);
+  hipGraphExec_t& ex = n.fwd_exec[train ? 1 : 0];
+  if (!ex) {
+    DTC_TRY(begin_capture(n));
+    const int rc = forward_body(n, n.at<float>(n.LOGITS), train, n.cap_st);
+    DTC_TRY(end_capture(n, rc, &ex));
   }
+  DTC_HIP(hipGraphLaunch(ex, st));
+  DTC_HIP(hipMemcpyAsync(logits, n.at<float>(n.LOGITS), (size_t)n.B * n.ncls * 4, hipMemcpyDeviceToDevice, st));
   return 0;
+}
+
+// Bucket point after block `after_block` (-1: after the stem). Eager: all-reduce the buckets that
+// are complete now. Capturing: close the current graph segment there and open the next one; the
+// replay issues the all-reduces between segments.
+struct BwdCtx {
+  Comm* comm = nullptr;
+  bool capturing = false;
+  std::vector<Net::Seg>* segs = nullptr;
+};
+static int maybe_bucket(Net& n, int after_block, const BwdCtx& cx, hipStream_t st) {
+  if (!cx.comm) return 0;
+  std::vector<int> ids;
+  for (size_t i = 0; i < n.bucket_off.size(); ++i)
+    if (n.bucket_after_block[i] == after_block) ids.push_back((int)i);
+  if (ids.empty()) return 0;
+  if (!cx.capturing) {
+    for (int i : ids) DTC_TRY(comm_allreduce_async(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st));
+    return 0;
+  }
+  Net::Seg sg;
+  sg.buckets = ids;
+  DTC_TRY(end_capture(n, 0, &sg.exec));
+  cx.segs->push_back(sg);
+  return begin_capture(n);
 }
 
 static int cap(Net& n, const std::string& name, const void* src, hipStream_t st) {
@@ -427,7 +510,8 @@ static int cap(Net& n, const std::string& name, const void* src, hipStream_t st)
   return set_error(DTC_EINVAL, "capture slot %s missing", name.c_str());
 }
 
-static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st) {
+static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& cx, hipStream_t st) {
+  n.prof_next = Net::PROF_BWD0;
   u16* G[6];
   for (int i = 0; i < 6; ++i) G[i] = n.at<u16>(n.G[i]);
   float* slab = n.at<float>(n.SLAB);
@@ -458,8 +542,8 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
     DTC_TRY(cap(n, cp + ".dc2", G[2], st));
     if (b.proj) DTC_TRY(cap(n, cp + ".ds", G[3], st));
     // conv2: dW2 and da1
-    PROF(2, conv_flops(b.c2.s), conv_wgrad(b.c2.s, n.at<u16>(b.A1), G[2], n.gf(b.c2.pidx), 0, 0, gs, slab, n.slab_bytes, st));
-    PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, G[2], n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st));
+    PROF(2, conv_flops(b.c2.s), conv_wgrad(b.c2.s, n.at<u16>(b.A1), G[2], n.gf(b.c2.pidx), 0, 0, gs, slab, n.slab_bytes, st, ts));
+    PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, G[2], n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts));
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
     // a1 = relu(bn1(c1))
     DTC_TRY(bn_bwd_reduce(G[4], n.at<u16>(b.A1), n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
@@ -472,17 +556,17 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
                          st));
     DTC_TRY(cap(n, cp + ".dc1", G[2], st));
     // conv1 (+ shortcut): weight grads, then the block-input gradient with the residual fused
-    PROF(2, conv_flops(b.c1.s), conv_wgrad(b.c1.s, in, G[2], n.gf(b.c1.pidx), 0, 0, gs, slab, n.slab_bytes, st));
+    PROF(2, conv_flops(b.c1.s), conv_wgrad(b.c1.s, in, G[2], n.gf(b.c1.pidx), 0, 0, gs, slab, n.slab_bytes, st, ts));
     if (b.proj) {
-      PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, G[3], n.gf(b.sc.pidx), 0, 0, gs, slab, n.slab_bytes, st));
-      PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, G[3], n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st));
-      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st));
+      PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, G[3], n.gf(b.sc.pidx), 0, 0, gs, slab, n.slab_bytes, st, ts));
+      PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, G[3], n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts));
     } else {
-      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[1], slab, n.slab_bytes, st));
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[1], slab, n.slab_bytes, st, ts));
     }
     if (b.proj) DTC_TRY(cap(n, cp + ".dxs", G[5], st));
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
-    DTC_TRY(maybe_bucket(n, bi, comm, st));
+    DTC_TRY(maybe_bucket(n, bi, cx, st));
   }
   // stem: a0 = relu(bn1(conv1(x)))
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
@@ -495,8 +579,45 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
   DTC_TRY(cap(n, "grad.stem.dz", G[1], st));
   DTC_TRY(cap(n, "grad.stem.dc", G[2], st));
   PROF(2, 2.0 * M0 * 64 * 27,
-       conv_wgrad(n.stem.s, n.at<u16>(n.X0), G[2], n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st));
-  DTC_TRY(maybe_bucket(n, -1, comm, st));
+       conv_wgrad(n.stem.s, n.at<u16>(n.X0), G[2], n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st, ts));
+  DTC_TRY(maybe_bucket(n, -1, cx, st));
+  if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
+  return 0;
+}
+
+static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st) {
+  if (!graphs_on(n)) {
+    BwdCtx cx;
+    cx.comm = comm;
+    DTC_TRY(backward_body(n, dlogits, gs, cx, st));
+  } else {
+    if (!n.bwd_segs.empty() && (n.bwd_gs != gs || n.bwd_comm != (comm != nullptr))) drop_graphs(n);
+    if (n.bwd_segs.empty()) {
+      std::vector<Net::Seg> segs;
+      BwdCtx cx;
+      cx.comm = comm;
+      cx.capturing = true;
+      cx.segs = &segs;
+      Net::Seg tail;
+      int rc = begin_capture(n);
+      if (rc == 0) rc = end_capture(n, backward_body(n, n.at<float>(n.DLOGITS), gs, cx, n.cap_st), &tail.exec);
+      if (rc != 0) {
+        for (auto& sg : segs)
+          if (sg.exec) (void)hipGraphExecDestroy(sg.exec);
+        return rc;
+      }
+      segs.push_back(tail);
+      n.bwd_segs = segs;
+      n.bwd_gs = gs;
+      n.bwd_comm = comm != nullptr;
+    }
+    DTC_HIP(hipMemcpyAsync(n.at<float>(n.DLOGITS), dlogits, (size_t)n.B * n.ncls * 4, hipMemcpyDeviceToDevice, st));
+    for (const auto& sg : n.bwd_segs) {
+      if (sg.exec) DTC_HIP(hipGraphLaunch(sg.exec, st));
+      for (int i : sg.buckets)
+        DTC_TRY(comm_allreduce_async(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st));
+    }
+  }
   if (comm) DTC_TRY(comm_join(comm, st));
   return 0;
 }
@@ -535,12 +656,19 @@ int dtc_rn18_create(dtc_net** out, int batch, int height, int width, int num_cla
   return 0;
 }
 
+static void prof_free(Net& n) {
+  if (n.prof_ts) (void)hipFree(n.prof_ts);
+  if (n.prof_acc) (void)hipFree(n.prof_acc);
+  n.prof_ts = n.prof_acc = nullptr;
+  n.profiling = false;
+}
+
 int dtc_rn18_destroy(dtc_net* net) {
-  if (net)
-    for (auto& p : net->n.prof) {
-      if (p.a) (void)hipEventDestroy(p.a);
-      if (p.b) (void)hipEventDestroy(p.b);
-    }
+  if (net) {
+    drop_graphs(net->n);
+    if (net->n.cap_st) (void)hipStreamDestroy(net->n.cap_st);
+    prof_free(net->n);
+  }
   delete net;
   return 0;
 }
@@ -600,6 +728,7 @@ int dtc_rn18_bind(dtc_net* net, void* workspace, float* params, float* grads, ui
   n.pb = params_bf16;
   n.bufs = bufs;
   n.nbt = num_batches_tracked;
+  drop_graphs(n);  // captured launches hold the previous pointers
   DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.stats_hi - n.stats_lo, (hipStream_t)stream));
   return 0;
 }
@@ -640,13 +769,21 @@ int dtc_rn18_activation_info(const dtc_net* net, int idx, const char** name, siz
 int dtc_rn18_profile_begin(dtc_net* net, int capacity) {
   DTC_CHECK_ARG(net && capacity > 0, "dtc_rn18_profile_begin: bad args");
   Net& n = net->n;
-  while ((int)n.prof.size() < capacity) {
-    Net::ProfPair p;
-    DTC_HIP(hipEventCreate(&p.a));
-    DTC_HIP(hipEventCreate(&p.b));
-    n.prof.push_back(p);
+  const size_t bytes = (size_t)Net::PROF_SLOTS * 2 * sizeof(u64);
+  if (!n.prof_ts) {
+    int dev = 0;
+    DTC_HIP(hipGetDevice(&dev));
+    DTC_HIP(hipDeviceGetAttribute(&n.prof_khz, hipDeviceAttributeWallClockRate, dev));
+    DTC_CHECK_ARG(n.prof_khz > 0, "dtc_rn18_profile_begin: no wall clock rate");
+    DTC_HIP(hipMalloc(&n.prof_ts, bytes));
+    DTC_HIP(hipMalloc(&n.prof_acc, bytes));
+    drop_graphs(n);  // re-capture with the timing slots
   }
-  n.prof_used = 0;
+  // slots -> (~0, 0) (accumulating all-zero slots adds nothing and resets them), totals -> 0
+  DTC_HIP(hipMemset(n.prof_ts, 0, bytes));
+  DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, nullptr));
+  DTC_HIP(hipMemset(n.prof_acc, 0, bytes));
+  DTC_HIP(hipDeviceSynchronize());
   n.profiling = true;
   return 0;
 }
@@ -654,22 +791,25 @@ int dtc_rn18_profile_begin(dtc_net* net, int capacity) {
 int dtc_rn18_profile_end(dtc_net* net, double* ms_by_kind, double* flops_by_kind, int* count_by_kind) {
   DTC_CHECK_ARG(net != nullptr, "dtc_rn18_profile_end: null net");
   Net& n = net->n;
-  n.profiling = false;
   for (int k = 0; k < 3; ++k) {
     if (ms_by_kind) ms_by_kind[k] = 0;
     if (flops_by_kind) flops_by_kind[k] = 0;
     if (count_by_kind) count_by_kind[k] = 0;
   }
-  for (size_t i = 0; i < n.prof_used; ++i) {
-    auto& e = n.prof[i];
-    DTC_HIP(hipEventSynchronize(e.b));
-    float ms = 0.f;
-    DTC_HIP(hipEventElapsedTime(&ms, e.a, e.b));
-    if (ms_by_kind) ms_by_kind[e.kind] += ms;
-    if (flops_by_kind) flops_by_kind[e.kind] += e.flops;
-    if (count_by_kind) count_by_kind[e.kind] += 1;
+  if (!n.prof_ts) return 0;
+  std::vector<u64> acc((size_t)Net::PROF_SLOTS * 2);
+  DTC_HIP(hipDeviceSynchronize());
+  DTC_HIP(hipMemcpy(acc.data(), n.prof_acc, acc.size() * sizeof(u64), hipMemcpyDeviceToHost));
+  for (int i = 0; i < Net::PROF_SLOTS; ++i) {
+    const u64 calls = acc[2 * i + 1];
+    if (calls == 0) continue;
+    const int k = n.prof_kind[i];
+    if (ms_by_kind) ms_by_kind[k] += (double)acc[2 * i] / (double)n.prof_khz;
+    if (flops_by_kind) flops_by_kind[k] += n.prof_flops[i] * (double)calls;
+    if (count_by_kind) count_by_kind[k] += (int)calls;
   }
-  n.prof_used = 0;
+  drop_graphs(n);
+  prof_free(n);
   return 0;
 }
 

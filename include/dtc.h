@@ -37,7 +37,9 @@ const char* dtc_last_error(void);
 /* Process-wide kernel tuning knobs (atomic; for benchmarking): "igemm_stages" (2 or 3 LDS stages
  * in the conv main loop, default 2), "xcd_remap" (XCD-aware tile order, default 1),
  * "dgrad_classes" (stride-2 data-gradient as 4 parity-class GEMMs, default 1), "wgrad_fast" (buffer-
- * offset weight-gradient loader for row-aligned pixel steps, default 1). */
+ * offset weight-gradient loader for row-aligned pixel steps, default 1), "graphs" (the executor
+ * captures its forward / backward into hipGraphs on first use and replays them, default 1; any
+ * option change invalidates captured graphs). */
 int dtc_set_option(const char* name, int value);
 int dtc_get_option(const char* name);
 
@@ -160,7 +162,12 @@ int dtc_rn18_bucket_info(const dtc_net* net, int idx, int64_t* offset, int64_t* 
 int dtc_rn18_bind(dtc_net* net, void* workspace, float* params, float* grads, uint16_t* params_bf16, float* bufs,
                   int64_t* num_batches_tracked, void* stream);
 /* x: NCHW fp32 [batch][3][h][w]; logits fp32 [batch][ncls]. train != 0: batch statistics +
- * running-stat update; train == 0: running statistics (eval mode). */
+ * running-stat update; train == 0: running statistics (eval mode).
+ * Graph mode (option "graphs"): everything after the input im2col is captured once per train flag
+ * (on an internal stream) and replayed into `stream`; logits are copied out of the workspace. The
+ * backward is captured as segments split at bucket boundaries, with the all-reduces issued eagerly
+ * between segment replays; re-captured when grad_scale or the presence of comm changes, and after
+ * dtc_rn18_bind. Capture mode (dtc_rn18_enable_capture) runs eagerly. */
 int dtc_rn18_forward(dtc_net* net, const float* x, float* logits, int train, void* stream);
 /* Gradients of every parameter, scaled by grad_scale (1/world for DDP's mean), written (not
  * accumulated) into the bound flat grad buffer. If comm != NULL each bucket is all-reduced (sum)
@@ -178,9 +185,13 @@ int dtc_rn18_activation_info(const dtc_net* net, int idx, const char** name, siz
 int dtc_rn18_enable_capture(dtc_net* net);
 int dtc_rn18_num_captures(const dtc_net* net);
 int dtc_rn18_capture_info(const dtc_net* net, int idx, const char** name, size_t* ws_offset, int* shape4);
-/* Live timing of every convolution call (forward, dgrad, wgrad incl. split-K reductions) with HIP
- * events on the compute stream, between begin and end; end() synchronizes on the recorded events
- * and returns per-pass totals: index 0 = forward, 1 = dgrad, 2 = wgrad (ms, algorithmic FLOPs, calls). */
+/* Live timing of every convolution call of training steps (forward, dgrad, wgrad incl. split-K
+ * reductions) between begin and end. Each call's kernels stamp the first workgroup start and the
+ * last workgroup end (s_memrealtime, converted with hipDeviceAttributeWallClockRate) into a device
+ * slot; the backward folds the slots into device totals once per step (graph-safe, no host work
+ * per call). begin() arms it (first call: allocation + graph re-capture; later calls: totals
+ * re-zeroed; `capacity` > 0 is unused), end() synchronizes the device, returns per-pass totals
+ * (index 0 = forward, 1 = dgrad, 2 = wgrad: ms, algorithmic FLOPs, calls) and disarms. */
 int dtc_rn18_profile_begin(dtc_net* net, int capacity);
 int dtc_rn18_profile_end(dtc_net* net, double* ms_by_kind, double* flops_by_kind, int* count_by_kind);
 
