@@ -57,6 +57,9 @@ def cpu_baseline(seconds: float):
     threads = os.cpu_count() or 1
     torch.manual_seed(42)
     dtc = dtc_import.load()
+    for kv in args.opt:
+        name, val = kv.split("=")
+        dtc._native.call("dtc_set_option", name.encode(), int(val))
     m = dtc.ResNet18()  # host-side construction only (identical init to the reference)
     params = {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}
     batch = 16
@@ -90,6 +93,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-live-roofline", action="store_true", help="skip the per-conv timing in the timed region")
+    ap.add_argument("--opt", action="append", default=[], help="native option NAME=VALUE (A/B runs)")
     args = ap.parse_args()
 
     rank, world, local = init_dist()
