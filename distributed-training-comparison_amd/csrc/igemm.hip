@@ -57,11 +57,18 @@ __device__ __forceinline__ void buf_lds16(const void* base, uint32_t bytes, char
 }
 
 // Call-timing stamps (kernel entry / exit only, one lane per workgroup; nothing on the loop).
+// Slot layout (u64): [0] start, then DTC_PROF_LINES end cells one 128-B line apart. Workgroups are
+// dispatched in linear order, so the first one's entry is the call's start (a plain store); the
+// end is a max over all workgroups, spread over the lines to keep the atomics uncontended.
 __device__ __forceinline__ void stamp_start(u64* ts) {
-  if (ts != nullptr && threadIdx.x == 0) atomicMin(ts, (u64)__builtin_amdgcn_s_memrealtime());
+  if (ts != nullptr && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+    __hip_atomic_store(ts, (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void stamp_end(u64* ts) {
-  if (ts != nullptr && threadIdx.x == 0) atomicMax(ts + 1, (u64)__builtin_amdgcn_s_memrealtime());
+  if (ts != nullptr && threadIdx.x == 0) {
+    const unsigned lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    atomicMax(ts + DTC_PROF_LINE * (1 + (lin & (DTC_PROF_LINES - 1))), (u64)__builtin_amdgcn_s_memrealtime());
+  }
 }
 
 __device__ __forceinline__ int rowswz(int row) { return (row >> 1) & 7; }
@@ -650,17 +657,23 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   stamp_end(ts);
 }
 
-// per-call timing slots -> running totals (one launch per training step when profiling)
+// per-call timing slots -> running totals (one launch per training step when profiling):
+// slot i: start = ts[i][0], end = max over its end cells; acc[i] += (end - start, 1); slot zeroed.
 __global__ void prof_accumulate_kernel(u64* ts, int n, u64* acc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const u64 a = ts[2 * i], b = ts[2 * i + 1];
-  if (b > a) {
+  u64* slot = ts + (size_t)i * DTC_PROF_SLOT_U64;
+  const u64 a = slot[0];
+  u64 b = 0;
+  for (int l = 1; l <= DTC_PROF_LINES; ++l) {
+    b = max(b, slot[l * DTC_PROF_LINE]);
+    slot[l * DTC_PROF_LINE] = 0;
+  }
+  if (a != 0 && b > a) {
     acc[2 * i] += b - a;
     acc[2 * i + 1] += 1;
   }
-  ts[2 * i] = ~0ull;
-  ts[2 * i + 1] = 0;
+  slot[0] = 0;
 }
 
 // ---------------------------------------------------------------- host launchers

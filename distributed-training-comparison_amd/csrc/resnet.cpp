@@ -82,7 +82,7 @@ struct Net {
   // Graph-safe: the slot pointers are baked at capture, nothing happens on the host per call.
   static constexpr int PROF_SLOTS = 128, PROF_BWD0 = 32;  // forward calls use [0,32), backward [32,128)
   bool profiling = false;
-  u64* prof_ts = nullptr;   // [PROF_SLOTS][2] device
+  u64* prof_ts = nullptr;   // [PROF_SLOTS][DTC_PROF_SLOT_U64] device
   u64* prof_acc = nullptr;  // [PROF_SLOTS][2] device: (sum ticks, calls)
   int prof_next = 0;
   int prof_kind[PROF_SLOTS] = {};
@@ -356,7 +356,7 @@ static u64* prof_slot(Net& n, int kind, double flops) {
   const int i = n.prof_next++;
   n.prof_kind[i] = kind;
   n.prof_flops[i] = flops;
-  return n.prof_ts + 2 * i;
+  return n.prof_ts + (size_t)i * DTC_PROF_SLOT_U64;
 }
 #define PROF(kind, flops, call)                        \
   do {                                                 \
@@ -770,18 +770,18 @@ int dtc_rn18_profile_begin(dtc_net* net, int capacity) {
   DTC_CHECK_ARG(net && capacity > 0, "dtc_rn18_profile_begin: bad args");
   Net& n = net->n;
   const size_t bytes = (size_t)Net::PROF_SLOTS * 2 * sizeof(u64);
+  const size_t ts_bytes = (size_t)Net::PROF_SLOTS * DTC_PROF_SLOT_U64 * sizeof(u64);
   if (!n.prof_ts) {
     int dev = 0;
     DTC_HIP(hipGetDevice(&dev));
     DTC_HIP(hipDeviceGetAttribute(&n.prof_khz, hipDeviceAttributeWallClockRate, dev));
     DTC_CHECK_ARG(n.prof_khz > 0, "dtc_rn18_profile_begin: no wall clock rate");
-    DTC_HIP(hipMalloc(&n.prof_ts, bytes));
+    DTC_HIP(hipMalloc(&n.prof_ts, ts_bytes));
     DTC_HIP(hipMalloc(&n.prof_acc, bytes));
     drop_graphs(n);  // re-capture with the timing slots
   }
-  // slots -> (~0, 0) (accumulating all-zero slots adds nothing and resets them), totals -> 0
-  DTC_HIP(hipMemset(n.prof_ts, 0, bytes));
-  DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, nullptr));
+  // zeroed slots (start 0 = not stamped) and totals
+  DTC_HIP(hipMemset(n.prof_ts, 0, ts_bytes));
   DTC_HIP(hipMemset(n.prof_acc, 0, bytes));
   DTC_HIP(hipDeviceSynchronize());
   n.profiling = true;
