@@ -211,6 +211,46 @@ def synthetic_stream(step, batch, seed=1234, templates=None):
     return x, y
 
 
+def _perturb_ulp(model, seed):
+    """Multiply every float parameter by (1 +- 2^-23): a 1-ulp perturbation of the seed-42 init,
+    to measure how far two numerically equivalent runs of the same recipe drift apart."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for prm in model.parameters():
+            sign = torch.randint(0, 2, prm.shape, generator=g).float() * 2 - 1
+            prm.mul_(1 + sign * 2.0 ** -23)
+
+
+def gen_loss_chaos(steps=200, batch=128, seeds=(1, 2)):
+    """Reference bf16-autocast curves from 1-ulp-perturbed inits (loss_curve.json: bf16_ulp)."""
+    utils = _import_from("single", "utils")
+    net = _import_from("single", "net")
+    templates = torch.randn(100, 3, 32, 32, generator=torch.Generator().manual_seed(1234))
+    path = os.path.join(HERE, "loss_curve.json")
+    out = json.load(open(path))
+    curves = []
+    for sd in seeds:
+        utils.fix_seed(42)
+        m = net.ResNet18()
+        _perturb_ulp(m, sd)
+        opt = torch.optim.SGD(m.parameters(), lr=0.1, weight_decay=1e-4, momentum=0.9, nesterov=True)
+        crit = torch.nn.CrossEntropyLoss()
+        losses = []
+        for s in range(steps):
+            x, y = synthetic_stream(s, batch, templates=templates)
+            opt.zero_grad()
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                loss = crit(m(x), y)
+            loss.backward()
+            opt.step()
+            losses.append(float(loss.detach()))
+        curves.append(losses)
+        print("ulp seed", sd, losses[:3], sum(losses) / len(losses), flush=True)
+    out["bf16_ulp"] = curves
+    with open(path, "w") as f:
+        json.dump(out, f)
+
+
 def gen_loss_curve(steps=200, batch=128, modes=("fp32", "bf16")):
     utils = _import_from("single", "utils")
     net = _import_from("single", "net")
@@ -295,3 +335,5 @@ if __name__ == "__main__":
         gen_ddp()
     if "loss" in which:
         gen_loss_curve()
+    if "loss" in which or "loss_chaos" in which:
+        gen_loss_chaos()

@@ -14,11 +14,23 @@ sys.path.insert(0, ROOT)
 import dtc_import  # noqa: E402
 
 
-def run(dtc, dev, lc, seed=42):
+def perturb_ulp(model, seed):
+    """Same 1-ulp init perturbation as tests/golden/make_golden.py::_perturb_ulp."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for prm in model.parameters():
+            sign = torch.randint(0, 2, prm.shape, generator=g).float() * 2 - 1
+            prm.mul_(1 + sign * 2.0 ** -23)
+
+
+def run(dtc, dev, lc, seed=42, ulp=0):
     batch, steps = lc["batch"], lc["steps"]
     templates = torch.randn(100, 3, 32, 32, generator=torch.Generator().manual_seed(1234))
     torch.manual_seed(seed)
-    model = dtc.ResNet18().to(dev)
+    model = dtc.ResNet18()
+    if ulp:
+        perturb_ulp(model, ulp)
+    model = model.to(dev)
     crit = dtc.CrossEntropyLoss()
     opt = dtc.SGD(model.parameters(), lr=lc["lr"], weight_decay=lc["wd"], momentum=lc["momentum"], nesterov=True)
     losses = []
@@ -39,6 +51,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="", help="';'-separated 'name=v,name=v' option sets")
     ap.add_argument("--seeds", default="42")
+    ap.add_argument("--ulp", default="", help="comma-separated 1-ulp perturbation seeds (seed-42 init)")
     ap.add_argument("--out", default="gpurun_out/loss_curves.json")
     args = ap.parse_args()
     dtc = dtc_import.load()
@@ -60,6 +73,11 @@ def main():
             print("   win20 ours", np.round(w(cur), 3).tolist(), flush=True)
         for k, _ in kv:  # restore defaults
             dtc._native.call("dtc_set_option", k.encode(), {"igemm_stages": 2}.get(k, 1))
+    for u in [int(v) for v in args.ulp.split(",") if v]:
+        cur = run(dtc, dev, lc, 42, u)
+        res[f"ulp{u}"] = cur.tolist()
+        print(f"ulp{u} mean", round(cur.mean(), 4), "rel", round((cur.mean() - ref.mean()) / ref.mean(), 4), flush=True)
+        print("   win20 ours", np.round(cur.reshape(-1, 20).mean(1), 3).tolist(), flush=True)
     print("   win20 ref ", np.round(ref.reshape(-1, 20).mean(1), 3).tolist())
     print("   win20 r32 ", np.round(ref32.reshape(-1, 20).mean(1), 3).tolist())
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
