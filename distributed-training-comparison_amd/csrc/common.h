@@ -101,8 +101,9 @@ __device__ __forceinline__ float wave_max(float v) {
 // atomics over slots (blockIdx & (SLOTS-1)) so that thousands of workgroups do not
 // contend on the same 1 KB; the finalize kernels sum the slots in a fixed order.
 #define DTC_STAT_SLOTS 32
-// conv call-timing slot: u64 [0] = start, [DTC_PROF_LINE * (1 + l)] = end cell l (l < DTC_PROF_LINES)
+// conv call-timing slot (u64): start cell l at [DTC_PROF_LINE * l], end cell l at
+// [DTC_PROF_LINE * (DTC_PROF_LINES + l)], l < DTC_PROF_LINES (one 128-B line per cell)
 #define DTC_PROF_LINE 16
 #define DTC_PROF_LINES 64
-#define DTC_PROF_SLOT_U64 (DTC_PROF_LINE * (DTC_PROF_LINES + 1))
+#define DTC_PROF_SLOT_U64 (DTC_PROF_LINE * DTC_PROF_LINES * 2)
 

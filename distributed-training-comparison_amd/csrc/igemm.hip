@@ -57,17 +57,21 @@ __device__ __forceinline__ void buf_lds16(const void* base, uint32_t bytes, char
 }
 
 // Call-timing stamps (kernel entry / exit only, one lane per workgroup; nothing on the loop).
-// Slot layout (u64): [0] start, then DTC_PROF_LINES end cells one 128-B line apart. Workgroups are
-// dispatched in linear order, so the first one's entry is the call's start (a plain store); the
-// end is a max over all workgroups, spread over the lines to keep the atomics uncontended.
+// Slot layout (u64, one 128-B line per cell): DTC_PROF_LINES start cells, then DTC_PROF_LINES end
+// cells. Dispatch order is not guaranteed, so the start is the min over the entries of the first
+// DTC_PROF_LINES workgroups (the earliest dispatched among them in practice), each in its own
+// line; the end is the max over all workgroups' exits, spread over the end lines. No contention.
 __device__ __forceinline__ void stamp_start(u64* ts) {
-  if (ts != nullptr && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
-    __hip_atomic_store(ts, (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ts != nullptr && threadIdx.x == 0) {
+    const unsigned lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (lin < DTC_PROF_LINES) atomicMin(ts + DTC_PROF_LINE * lin, (u64)__builtin_amdgcn_s_memrealtime());
+  }
 }
 __device__ __forceinline__ void stamp_end(u64* ts) {
   if (ts != nullptr && threadIdx.x == 0) {
     const unsigned lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    atomicMax(ts + DTC_PROF_LINE * (1 + (lin & (DTC_PROF_LINES - 1))), (u64)__builtin_amdgcn_s_memrealtime());
+    atomicMax(ts + DTC_PROF_LINE * (DTC_PROF_LINES + (lin & (DTC_PROF_LINES - 1))),
+              (u64)__builtin_amdgcn_s_memrealtime());
   }
 }
 
@@ -658,22 +662,23 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 }
 
 // per-call timing slots -> running totals (one launch per training step when profiling):
-// slot i: start = ts[i][0], end = max over its end cells; acc[i] += (end - start, 1); slot zeroed.
+// slot i: start = min over its start cells, end = max over its end cells; if stamped,
+// acc[i] += (end - start, 1). Cells reset to (~0, 0).
 __global__ void prof_accumulate_kernel(u64* ts, int n, u64* acc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   u64* slot = ts + (size_t)i * DTC_PROF_SLOT_U64;
-  const u64 a = slot[0];
-  u64 b = 0;
-  for (int l = 1; l <= DTC_PROF_LINES; ++l) {
-    b = max(b, slot[l * DTC_PROF_LINE]);
-    slot[l * DTC_PROF_LINE] = 0;
+  u64 a = ~0ull, b = 0;
+  for (int l = 0; l < DTC_PROF_LINES; ++l) {
+    a = min(a, slot[l * DTC_PROF_LINE]);
+    b = max(b, slot[(DTC_PROF_LINES + l) * DTC_PROF_LINE]);
+    slot[l * DTC_PROF_LINE] = ~0ull;
+    slot[(DTC_PROF_LINES + l) * DTC_PROF_LINE] = 0;
   }
-  if (a != 0 && b > a) {
+  if (a != ~0ull && b > a) {
     acc[2 * i] += b - a;
     acc[2 * i + 1] += 1;
   }
-  slot[0] = 0;
 }
 
 // ---------------------------------------------------------------- host launchers

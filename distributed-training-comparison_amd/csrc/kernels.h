@@ -29,8 +29,8 @@ ConvPlan plan_conv(const ConvShape& s, int mode);
 
 // y = conv(x, w) (bf16 NHWC out); optional BN statistics of the bf16 output into
 // stats[SLOTS][2][K] (sum, sum of squares; fp64, accumulated).
-// `ts` (optional, every conv launcher): a DTC_PROF_SLOT_U64 slot receiving the call's first
-// workgroup start and every workgroup's end in s_memrealtime ticks (graph-safe per-call timing).
+// `ts` (optional, every conv launcher): a DTC_PROF_SLOT_U64 slot receiving the entry times of the
+// first workgroups and every workgroup's exit time in s_memrealtime ticks (graph-safe per-call timing).
 int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
              size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 // dx = conv_transpose(dy, w) (+ res), bf16 NHWC
@@ -41,7 +41,7 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
                float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
                   hipStream_t st, u64* ts = nullptr);
-// per slot i of ts[n][DTC_PROF_SLOT_U64]: acc[i] += (max end - start, 1) if stamped; slot zeroed
+// per slot i of ts[n][DTC_PROF_SLOT_U64]: acc[i] += (max end - min start, 1) if stamped; cells reset
 int prof_accumulate(u64* ts, int n, u64* acc, hipStream_t st);
 
 // ------------------------------------------------------------------ batch norm (NHWC, C channels, M pixels)

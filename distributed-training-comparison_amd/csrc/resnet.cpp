@@ -780,8 +780,9 @@ int dtc_rn18_profile_begin(dtc_net* net, int capacity) {
     DTC_HIP(hipMalloc(&n.prof_acc, bytes));
     drop_graphs(n);  // re-capture with the timing slots
   }
-  // zeroed slots (start 0 = not stamped) and totals
+  // slots -> (~0, 0) (folding all-zero slots adds nothing and resets them), then totals -> 0
   DTC_HIP(hipMemset(n.prof_ts, 0, ts_bytes));
+  DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, nullptr));
   DTC_HIP(hipMemset(n.prof_acc, 0, bytes));
   DTC_HIP(hipDeviceSynchronize());
   n.profiling = true;
