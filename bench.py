@@ -54,12 +54,14 @@ def cpu_baseline(seconds: float):
     """Oracle (numpy restatement) training step on the host cores: a bounded sample."""
     from oracle import resnet as R
 
-    threads = os.cpu_count() or 1
+    try:  # the BLAS pool numpy actually uses (OMP_NUM_THREADS on the box), not the machine's CPU count
+        from threadpoolctl import threadpool_info
+
+        threads = max([p.get("num_threads", 1) for p in threadpool_info() if p.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
     torch.manual_seed(42)
     dtc = dtc_import.load()
-    for kv in args.opt:
-        name, val = kv.split("=")
-        dtc._native.call("dtc_set_option", name.encode(), int(val))
     m = dtc.ResNet18()  # host-side construction only (identical init to the reference)
     params = {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}
     batch = 16
@@ -99,6 +101,9 @@ def main():
     rank, world, local = init_dist()
     dev = torch.device("cuda", local)
     dtc = dtc_import.load()
+    for kv in args.opt:
+        name, val = kv.split("=")
+        dtc._native.call("dtc_set_option", name.encode(), int(val))
 
     torch.manual_seed(42)
     model = dtc.ResNet18().to(dev)

@@ -17,6 +17,30 @@ namespace dtc {
 
 static inline int ceil_div_i(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// Sum the DTC_STAT_SLOTS fp64 partials of channel c (pairs at p[k][c], p[k][C + c]) in fixed slot
+// order and re-zero them. All loads are issued before any store (no load waits behind a store to
+// a possibly aliasing slot), so the kernel costs one memory round trip, not DTC_STAT_SLOTS.
+__device__ __forceinline__ void sum_slots(double* __restrict__ base, int C, int c, double& s, double& q) {
+  double sv[DTC_STAT_SLOTS], qv[DTC_STAT_SLOTS];
+#pragma unroll
+  for (int k = 0; k < DTC_STAT_SLOTS; ++k) {
+    sv[k] = base[(size_t)k * 2 * C + c];
+    qv[k] = base[(size_t)k * 2 * C + C + c];
+  }
+  s = 0.0;
+  q = 0.0;
+#pragma unroll
+  for (int k = 0; k < DTC_STAT_SLOTS; ++k) {
+    s += sv[k];
+    q += qv[k];
+  }
+#pragma unroll
+  for (int k = 0; k < DTC_STAT_SLOTS; ++k) {
+    base[(size_t)k * 2 * C + c] = 0.0;
+    base[(size_t)k * 2 * C + C + c] = 0.0;
+  }
+}
+
 __global__ void bn_fwd_finalize_kernel(double* __restrict__ stats, int C, double count, const float* __restrict__ gamma,
                                        const float* __restrict__ beta, float* __restrict__ rmean,
                                        float* __restrict__ rvar, int64_t* __restrict__ nbt, float momentum,
@@ -25,14 +49,8 @@ __global__ void bn_fwd_finalize_kernel(double* __restrict__ stats, int C, double
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && nbt) *nbt += 1;
   if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int k = 0; k < DTC_STAT_SLOTS; ++k) {
-    double* p = stats + (size_t)k * 2 * C;
-    s += p[c];
-    q += p[C + c];
-    p[c] = 0.0;
-    p[C + c] = 0.0;
-  }
+  double s, q;
+  sum_slots(stats, C, c, s, q);
   const double mu = s / count;
   double var = q / count - mu * mu;
   if (var < 0.0) var = 0.0;
@@ -54,7 +72,7 @@ int bn_fwd_finalize(double* stats, int C, int64_t count, const float* gamma, con
                     float* scale, float* shift, hipStream_t st) {
   DTC_CHECK_ARG(stats && gamma && beta && mean && invstd && scale && shift && C > 0 && count > 0,
                 "bn_fwd_finalize: bad args");
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(ceil_div_i(C, 256)), dim3(256), 0, st, stats, C, (double)count,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(ceil_div_i(C, 64)), dim3(64), 0, st, stats, C, (double)count,
                      gamma, beta, running_mean, running_var, num_batches, momentum, eps, mean, invstd, scale, shift);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -265,14 +283,8 @@ __global__ void bn_bwd_finalize_kernel(double* __restrict__ acc, int C, double c
                                        float* __restrict__ coef) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double sd = 0.0, sx = 0.0;
-  for (int k = 0; k < DTC_STAT_SLOTS; ++k) {
-    double* p = acc + (size_t)k * 2 * C;
-    sd += p[c];
-    sx += p[C + c];
-    p[c] = 0.0;
-    p[C + c] = 0.0;
-  }
+  double sd, sx;
+  sum_slots(acc, C, c, sd, sx);
   if (dgamma) dgamma[c] = (float)(sx * gscale);
   if (dbeta) dbeta[c] = (float)(sd * gscale);
   const double is = invstd[c];
@@ -287,7 +299,7 @@ __global__ void bn_bwd_finalize_kernel(double* __restrict__ acc, int C, double c
 int bn_bwd_finalize(double* acc, int C, int64_t count, const float* gamma, const float* mean, const float* invstd,
                     float gscale, float* dgamma, float* dbeta, float* coef, hipStream_t st) {
   DTC_CHECK_ARG(acc && gamma && mean && invstd && coef && C > 0 && count > 0, "bn_bwd_finalize: bad args");
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div_i(C, 256)), dim3(256), 0, st, acc, C, (double)count, gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div_i(C, 64)), dim3(64), 0, st, acc, C, (double)count, gamma,
                      mean, invstd, gscale, dgamma, dbeta, coef);
   DTC_LAUNCH_CHECK();
   return 0;

@@ -19,6 +19,7 @@
 // XOR on the read (guide §5.4 rule 21). Padding rows read a 1 KiB zero page.
 #include "common.h"
 #include "kernels.h"
+#include "tile_common.h"
 
 static __device__ __attribute__((aligned(1024))) uint4 g_zero_page[64];
 
@@ -47,65 +48,6 @@ struct IGemmParams {
   uint32_t src0_bytes, src1_bytes;
   u64* ts;  // optional call timing slot: atomicMin(start), atomicMax(end), s_memrealtime ticks
 };
-
-// 16-byte LDS-DMA through a buffer descriptor over [base, base + bytes): an offset outside the
-// range loads zeros. (Kept out of the loader lambda: the buffer builtins inside a lambda make the
-// host pass drop the kernel's launch stub.)
-__device__ __forceinline__ void buf_lds16(const void* base, uint32_t bytes, char* lds_dst, uint32_t off) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_dst, 16, off, 0, 0, 0);
-}
-
-// Call-timing stamps (kernel entry / exit only, one lane per workgroup; nothing on the loop).
-// Slot layout (u64, one 128-B line per cell): DTC_PROF_LINES start cells, then DTC_PROF_LINES end
-// cells. Dispatch order is not guaranteed, so the start is the min over the entries of the first
-// DTC_PROF_LINES workgroups (the earliest dispatched among them in practice), each in its own
-// line; the end is the max over all workgroups' exits, spread over the end lines. No contention.
-__device__ __forceinline__ void stamp_start(u64* ts) {
-  if (ts != nullptr && threadIdx.x == 0) {
-    const unsigned lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    if (lin < DTC_PROF_LINES) atomicMin(ts + DTC_PROF_LINE * lin, (u64)__builtin_amdgcn_s_memrealtime());
-  }
-}
-__device__ __forceinline__ void stamp_end(u64* ts) {
-  if (ts != nullptr && threadIdx.x == 0) {
-    const unsigned lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    atomicMax(ts + DTC_PROF_LINE * (DTC_PROF_LINES + (lin & (DTC_PROF_LINES - 1))),
-              (u64)__builtin_amdgcn_s_memrealtime());
-  }
-}
-
-__device__ __forceinline__ int rowswz(int row) { return (row >> 1) & 7; }
-__device__ __forceinline__ int trswz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
-
-__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
-}
-
-// Row-image fragment: lane holds row (lane&15), reduction chunk (ks*4 + lane>>4).
-__device__ __forceinline__ bf16x8 frag_row(const char* region, int row0, int ks, int lane) {
-  const int row = row0 + (lane & 15);
-  const int ch = (ks * 4 + (lane >> 4)) ^ rowswz(row);
-  uint4 v = *(const uint4*)(region + row * 128 + (ch << 4));
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// Tr-image fragment: lane holds column (cb + lane&15), reduction rows ks*32 + 8*(lane>>4) + 0..7.
-typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ bf16x8 frag_tr(const char* region, int cb, int ks, int lane) {
-  const int img = cb >> 6, cin = cb & 63;
-  const int i = lane & 15, q = i >> 2, pp = i & 3, g = lane >> 4;
-  const int unit = (cin >> 2) + pp;
-  const char* base = region + img * 8192;
-  const int kr0 = ks * 32 + g * 8 + q;
-  const int kr1 = kr0 + 4;
-  const int f0 = (((kr0 >> 1) & 1) << 2) | (((kr0 >> 3) & 1) << 3);
-  const int f1 = (((kr1 >> 1) & 1) << 2) | (((kr1 >> 3) & 1) << 3);
-  typedef __attribute__((address_space(3))) bf16x4_t lds_v4;
-  bf16x4_t t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(base + kr0 * 128 + ((unit ^ f0) << 3)));
-  bf16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(base + kr1 * 128 + ((unit ^ f1) << 3)));
-  return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
-}
 
 template <int MODE, int BM, int BN, int WR, int WC, bool SLAB, int NSTAGE>
 __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
@@ -737,6 +679,12 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
     pl.splits = (tiles >= 256 || cls) ? 1 : pick_splits(tiles, num_kt, 480, 8);
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * M * A * 4 : 0;
     pl.num_kt = num_kt;
+  } else if (const int hs = wgrad_halo_splits(s)) {  // halo-tiled kernel (wgrad_halo.hip)
+    pl.bm = 576;
+    pl.bn = 64;
+    pl.splits = hs;
+    pl.num_kt = s.N * P * Q / 64;
+    pl.slab_bytes = (size_t)hs * s.K * s.R * s.S * s.C * 4;
   } else {
     const int M = s.N * P * Q;
     const int num_kt = ceil_div(M, 64);
@@ -838,15 +786,20 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
     p.src0_bytes = (uint32_t)xb;
     p.src1_bytes = (uint32_t)db;
   }
-  p.num_kt = pl.num_kt;
-  p.tiles_a = p.RSC / pl.bm;
-  const int tiles_b = s.K / pl.bn;
   int splits = pl.splits;
-  while (splits > 1 && (size_t)splits * s.K * p.RSC * 4 > slab_bytes) --splits;
-  p.kt_per_split = ceil_div(p.num_kt, splits);
-  splits = ceil_div(p.num_kt, p.kt_per_split);
-  if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_WGRAD, 64, 64, 2, 2, true>(p, tiles_b, splits, st)));
-  else DTC_TRY((launch_igemm<MODE_WGRAD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
+  if (pl.bm == 576 && slab_bytes >= pl.slab_bytes) {
+    DTC_TRY(conv_wgrad_halo(s, x, dy, slab, pl.splits, &splits, st, ts));
+  } else {
+    if (pl.bm == 576) pl = ConvPlan{64, 64, 1, ceil_div(p.M, 64), 0};  // workspace too small for the halo plan
+    p.num_kt = pl.num_kt;
+    p.tiles_a = p.RSC / pl.bm;
+    const int tiles_b = s.K / pl.bn;
+    while (splits > 1 && (size_t)splits * s.K * p.RSC * 4 > slab_bytes) --splits;
+    p.kt_per_split = ceil_div(p.num_kt, splits);
+    splits = ceil_div(p.num_kt, p.kt_per_split);
+    if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_WGRAD, 64, 64, 2, 2, true>(p, tiles_b, splits, st)));
+    else DTC_TRY((launch_igemm<MODE_WGRAD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
+  }
   const int ncols = dw_cols > 0 ? dw_cols : p.RSC;
   const int ldo = dw_ld > 0 ? dw_ld : p.RSC;
   const size_t nv = (size_t)s.K * p.RSC / 4;

@@ -9,7 +9,15 @@
 namespace dtc {
 
 // ------------------------------------------------------------------ tuning options (atomic ints)
-enum { OPT_IGEMM_STAGES = 0, OPT_XCD_REMAP = 1, OPT_DGRAD_CLASSES = 2, OPT_WGRAD_FAST = 3, OPT_GRAPHS = 4, OPT_COUNT };
+enum {
+  OPT_IGEMM_STAGES = 0,
+  OPT_XCD_REMAP = 1,
+  OPT_DGRAD_CLASSES = 2,
+  OPT_WGRAD_FAST = 3,
+  OPT_GRAPHS = 4,
+  OPT_WGRAD_HALO = 5,  // target workgroup count of the halo WGRAD kernel (0 = generic loader only)
+  OPT_COUNT
+};
 int option_get(int id);
 int option_set(const char* name, int value);
 int option_epoch();  // bumped by every option_set (captured graphs bake the options in)
@@ -39,6 +47,11 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
 // dw[k][0:dw_cols] (row stride dw_ld) = scale * sum_pixels dy (x) im2col(x); fp32
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
                float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
+// Halo-tiled WGRAD for 3x3 / stride 1 / pad 1 (wgrad_halo.hip): split count it would use for s
+// (0 = not applicable / disabled), and the launch writing slab[used][K][9C] (reduce separately).
+int wgrad_halo_splits(const ConvShape& s);
+int conv_wgrad_halo(const ConvShape& s, const u16* x, const u16* dy, float* slab, int splits, int* used_splits,
+                    hipStream_t st, u64* ts);
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
                   hipStream_t st, u64* ts = nullptr);
 // per slot i of ts[n][DTC_PROF_SLOT_U64]: acc[i] += (max end - min start, 1) if stamped; cells reset

@@ -1,0 +1,218 @@
+// Halo-tiled weight gradient for 3x3 / stride 1 / pad 1 convolutions on bf16 MFMA (gfx950).
+//
+// Replaces the weight-gradient half of `nn.Conv2d.backward` (reference src/*/net.py:18-24,
+// 29-35) for every 3x3 stride-1 conv of ResNet-18 (13 of the 20 convs). The generic WGRAD
+// loader (igemm.hip) gives each workgroup one tap, so x and dy are re-read from L2 once per tap
+// (9x); here a workgroup owns ALL nine taps of a 64-channel input slice:
+//
+//   D[(r,s,c)][k] (576 x 64) += sum over a 64-pixel step of x(p+r-1, q+s-1, c0+c) * dy(p, q, k0+k)
+//
+// Per step the x rows the 64 output pixels touch are staged ONCE as a zero-padded halo
+// ((rows+2) x (W+2) pixels, 128-B rows of 64 channels, padding zero-filled by out-of-range
+// buffer offsets) and every tap reads it shifted by r*(W+2)+s rows. L2->LDS traffic per step:
+// <= 24 KiB halo + 8 KiB dy for 4.7 MFLOP (~180 FLOP/B, vs ~32 for one tap per workgroup).
+// Operands are read with ds_read_b64_tr_b16 (pixels are the MFMA reduction index); the tr
+// swizzle is a function of the LDS row, so shifted tap windows stay bank-conflict-free.
+// 8 waves: 4 along the 576 rows (9 fragments each) x 2 along the 64 output channels.
+// Pixel steps are split across workgroups; each writes an fp32 slab [split][K][RSC] that the
+// shared deterministic wgrad_reduce kernel (igemm.hip) sums and scales.
+#include "common.h"
+#include "kernels.h"
+#include "tile_common.h"
+
+namespace dtc {
+
+struct HaloParams {
+  const u16* x;    // NHWC [N][H][W][C]
+  const u16* dy;   // NPQK [N][H][W][K] (stride 1, pad 1: P = H, Q = W)
+  float* slab;     // [splits][K][9*C]
+  int N, H, W, C, K;
+  uint32_t x_bytes;
+  FastDiv fd_hw, fd_w;
+  int steps_per_split, nsteps;
+  int rs, hb, nh;  // output rows per image per step, halo rows per image block, halo rows per step
+  int spi;         // pixels per image block of a step (rs * W)
+  u64* ts;
+};
+
+constexpr int HALO_ROWS = 192;                 // LDS rows reserved for the halo (3 DMA rounds)
+constexpr int HALO_BYTES = HALO_ROWS * 128;    // 24 KiB
+constexpr int HSTAGE = HALO_BYTES + 64 * 128;  // + dy tile (64 pixels x 64 channels)
+
+// Tr-image fragment from the halo: lane holds column (channel) cin + lane&15, reduction rows =
+// the pixels whose halo rows are ra (4 pixels) and rb (next 4), already shifted by the tap.
+__device__ __forceinline__ bf16x8 frag_halo(const char* halo, int cin, int ra, int rb, int lane) {
+  const int unit = (cin >> 2) + (lane & 3);
+  const int fa = (((ra >> 1) & 1) << 2) | (((ra >> 3) & 1) << 3);
+  const int fb = (((rb >> 1) & 1) << 2) | (((rb >> 3) & 1) << 3);
+  typedef __attribute__((address_space(3))) bf16x4_t lds_v4;
+  bf16x4_t t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(halo + ra * 128 + ((unit ^ fa) << 3)));
+  bf16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(halo + rb * 128 + ((unit ^ fb) << 3)));
+  return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+__global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * HSTAGE];
+  stamp_start(p.ts);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ktiles = p.K >> 6;
+  const int c0 = (blockIdx.x / ktiles) * 64, k0 = (blockIdx.x % ktiles) * 64;
+  const int split = blockIdx.y;
+  const int st_begin = split * p.steps_per_split;
+  const int st_end = min(p.nsteps, st_begin + p.steps_per_split);
+  const int W2 = p.W + 2;
+
+  // ---- halo DMA: round j covers LDS rows j*64 + wave*8 + lane/8, 16-B chunk lane%8
+  const int nrounds = (p.nh + 63) >> 6;
+  int hrel[3], hrow_in[3];
+  bool hcol[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int hrow = j * 64 + wave * 8 + (lane >> 3);
+    const int ii = hrow / p.hb, rem = hrow - ii * p.hb;
+    const int hr = rem / W2, wc = rem - hr * W2;
+    const int src_chunk = (lane & 7) ^ trswz(hrow);
+    hcol[j] = hrow < p.nh && wc >= 1 && wc <= p.W;
+    hrow_in[j] = hr - 1;  // input row relative to the step's first output row
+    hrel[j] = (((ii * p.H + hr - 1) * p.W + wc - 1) * p.C + c0 + src_chunk * 8) * 2;
+  }
+  // ---- dy DMA: row t = wave*8 + lane/8 of the 64-pixel step
+  const int trow = wave * 8 + (lane >> 3);
+  const int dcol = k0 + (((lane & 7) ^ trswz(trow)) * 8);
+
+  auto stage = [&](char* sb, int step) {
+    const int m0 = step * 64;
+    const int n0 = (int)fdiv((uint32_t)m0, p.fd_hw);
+    const int p0 = (int)fdiv((uint32_t)(m0 - n0 * (int)p.fd_hw.d), p.fd_w);
+    const int base = ((n0 * p.H + p0) * p.W) * p.C * 2;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j < nrounds) {
+        const bool ok = hcol[j] && (unsigned)(p0 + hrow_in[j]) < (unsigned)p.H;
+        buf_lds16(p.x, p.x_bytes, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)(base + hrel[j]) : 0x80000000u);
+      }
+    }
+    glds16(p.dy + (size_t)(m0 + trow) * p.K + dcol, sb + HALO_BYTES + wave * 1024);
+  };
+
+  // ---- per-lane halo rows of the pixels this lane reads: t = ks*32 + 8*(lane>>4) + (lane&15)/4 (+4)
+  int hm[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int t = ks * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2) + 4 * h;
+      const int ii = t / p.spi, rem = t - ii * p.spi;
+      const int pr = rem / p.W, q = rem - pr * p.W;
+      hm[ks][h] = ii * p.hb + pr * W2 + q;
+    }
+
+  const int wm = wave >> 1, wn = wave & 1;
+  f32x4 acc[9][2];
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const char* sb) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 bfr[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = frag_tr(sb + HALO_BYTES, wn * 32 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const int row = wm * 144 + i * 16;  // GEMM row = tap*64 + channel
+        const int tap = row >> 6, cin = row & 63;
+        const int toff = (tap / 3) * W2 + (tap % 3);
+        const bf16x8 af = frag_halo(sb, cin, hm[ks][0] + toff, hm[ks][1] + toff, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // 2-stage LDS ring (as igemm_kernel): wait own DMAs, barrier, refill the other buffer, compute.
+  if (st_begin < st_end) {
+    stage(smem, st_begin);
+    const int nk = st_end - st_begin;
+    for (int it = 0; it < nk; ++it) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (it + 1 < nk) stage(smem + ((it + 1) & 1) * HSTAGE, st_begin + it + 1);
+      compute(smem + (it & 1) * HSTAGE);
+    }
+  }
+
+  // ---- epilogue: slab[split][k][tap*C + c0 + c] (4 consecutive c per lane: one 16-B store)
+  const int RSC = 9 * p.C;
+  float* slab = p.slab + (size_t)split * p.K * RSC;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int row = wm * 144 + i * 16 + 4 * (lane >> 4);
+    const int rsc = (row >> 6) * p.C + c0 + (row & 63);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kout = k0 + wn * 32 + j * 16 + (lane & 15);
+      *(f32x4*)(slab + (size_t)kout * RSC + rsc) = acc[i][j];
+    }
+  }
+  stamp_end(p.ts);
+}
+
+// ---------------------------------------------------------------- host side
+static bool halo_geometry(const ConvShape& s, int& rs, int& imgs) {
+  if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.C % 64 == 0 && s.K % 64 == 0)) return false;
+  if (s.W > 64 || 64 % s.W != 0) return false;
+  const int hw = s.H * s.W;
+  if (hw % 64 == 0) {
+    rs = 64 / s.W;
+    imgs = 1;
+  } else if (64 % hw == 0) {
+    rs = s.H;
+    imgs = 64 / hw;
+  } else {
+    return false;
+  }
+  const int nh = imgs * (rs + 2) * (s.W + 2);
+  return nh <= HALO_ROWS && (uint64_t)s.N * hw * s.C * 2 < (1ull << 31);
+}
+
+int wgrad_halo_splits(const ConvShape& s) {
+  const int target = option_get(OPT_WGRAD_HALO);
+  int rs = 0, imgs = 0;
+  if (target <= 0 || !halo_geometry(s, rs, imgs)) return 0;
+  const int tiles = (s.C / 64) * (s.K / 64);
+  const int nsteps = s.N * s.H * s.W / 64;
+  int splits = std::max(1, target / tiles);
+  splits = std::min(splits, std::max(1, nsteps / 4));  // >= 4 pixel steps per workgroup
+  return splits;
+}
+
+int conv_wgrad_halo(const ConvShape& s, const u16* x, const u16* dy, float* slab, int splits, int* used_splits,
+                    hipStream_t st, u64* ts) {
+  int rs = 0, imgs = 0;
+  DTC_CHECK_ARG(halo_geometry(s, rs, imgs) && splits > 0, "wgrad_halo: unsupported geometry");
+  HaloParams p{};
+  p.x = x; p.dy = dy; p.slab = slab;
+  p.N = s.N; p.H = s.H; p.W = s.W; p.C = s.C; p.K = s.K;
+  p.x_bytes = (uint32_t)((uint64_t)s.N * s.H * s.W * s.C * 2);
+  p.fd_hw = make_fastdiv(s.H * s.W);
+  p.fd_w = make_fastdiv(s.W);
+  p.nsteps = s.N * s.H * s.W / 64;
+  p.steps_per_split = (p.nsteps + splits - 1) / splits;
+  p.rs = rs;
+  p.hb = (rs + 2) * (s.W + 2);
+  p.nh = imgs * p.hb;
+  p.spi = rs * s.W;
+  p.ts = ts;
+  const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
+  dim3 grid((s.C / 64) * (s.K / 64), used);
+  hipLaunchKernelGGL(wgrad_halo_kernel, grid, dim3(512), 0, st, p);
+  DTC_LAUNCH_CHECK();
+  *used_splits = used;
+  return 0;
+}
+
+}  // namespace dtc

@@ -264,3 +264,29 @@ def test_sgd_and_amp(dtc, cuda):
     for _ in range(3):
         dtc.ops.amp_update_scale(scale, inv, tracker, found, 2.0, 0.5, 3)
     assert float(scale) == 65536.0 and abs(float(inv) - 1 / 65536.0) < 1e-12
+
+
+@pytest.mark.parametrize("case", [
+    (4, 32, 32, 64, 64),    # layer1 geometry: 2 output rows per 64-pixel step
+    (3, 8, 8, 64, 128),     # whole 8x8 image per step, 3 steps (ragged split)
+    (8, 16, 16, 128, 128),  # 4 rows per step, 2x2 output tiles
+    (8, 8, 8, 256, 64),     # C > K
+    (12, 4, 4, 512, 512),   # four 4x4 images per step (multi-image halo)
+    (2, 2, 2, 64, 64),      # 2x2 images: halo too tall -> generic loader
+])
+def test_conv_wgrad_halo(dtc, cuda, case):
+    """Halo-tiled 3x3 weight gradient == generic loader == oracle (fp32 sums of exact products)."""
+    N, H, W, C, K = case
+    g = np.random.default_rng(7)
+    x = _rand_bf16((N, H, W, C), g)
+    dy = _rand_bf16((N, H, W, K), g)
+    xd, dyd = _to_dev_bf16(x, cuda), _to_dev_bf16(dy, cuda)
+    ref = O.conv2d_wgrad(x, dy, 3, 3, 1, 1)
+    halo = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
+    dtc._native.lib.dtc_set_option(b"wgrad_halo", 0)
+    try:
+        generic = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
+    finally:
+        dtc._native.lib.dtc_set_option(b"wgrad_halo", 256)
+    assert rel_err(halo, ref) < 1e-5
+    assert rel_err(generic, ref) < 1e-5

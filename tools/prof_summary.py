@@ -1,0 +1,96 @@
+"""Summarise a rocprofv3 --kernel-trace --stats run of bench.py into a markdown file for profiles/.
+
+usage: python tools/prof_summary.py <rocprof output dir> <out.md> [--steps-from-bench bench.json]
+
+Reports: top kernels (calls, total, average), the conv family (igemm + split-K/wgrad reductions:
+the roofline kernel of bench.py) per training step, and the per-step timeline of the steady
+state (busy time vs wall time between the first and last kernel of a step, i.e. launch gaps).
+A training step is delimited by the SGD kernel (one launch per step).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+CONV = ("igemm_kernel", "splitk_reduce_kernel", "wgrad_reduce_kernel")
+
+
+def short(name):
+    n = name.replace("void ", "")
+    return n.split("(")[0]
+
+
+def main():
+    src, out = sys.argv[1], sys.argv[2]
+    trace = glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True)
+    assert trace, f"no kernel_trace.csv under {src}"
+    rows = []
+    with open(trace[0]) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    # steps: delimited by the fused SGD kernel
+    sgd_idx = [i for i, r in enumerate(rows) if "sgd_nesterov" in r[2]]
+    lines = [f"# rocprofv3 kernel trace summary: {os.path.basename(os.path.normpath(src))}", ""]
+    stats = defaultdict(lambda: [0, 0])
+    for s, e, n in rows:
+        stats[short(n)][0] += 1
+        stats[short(n)][1] += e - s
+    tot = sum(v[1] for v in stats.values())
+    lines += ["## All kernels (whole run)", "", "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
+    for k, (c, d) in sorted(stats.items(), key=lambda kv: -kv[1][1])[:25]:
+        lines.append(f"| `{k}` | {c} | {d / 1e6:.3f} | {d / c / 1e3:.2f} | {100 * d / tot:.1f} |")
+    if len(sgd_idx) >= 4:
+        # steady state: skip the first two steps (graph capture / warmup)
+        steps = list(zip(sgd_idx[1:-1], sgd_idx[2:]))[1:]
+        busy, wall, conv, nk = [], [], [], []
+        per_kernel = defaultdict(lambda: [0, 0])
+        for a, b in steps:
+            seg = rows[a + 1:b + 1]
+            t0, t1 = seg[0][0], seg[-1][1]
+            wall.append(t1 - t0)
+            # busy = union of kernel intervals
+            u, cur_s, cur_e = 0, None, None
+            for s, e, n in seg:
+                if cur_e is None or s > cur_e:
+                    if cur_e is not None:
+                        u += cur_e - cur_s
+                    cur_s, cur_e = s, e
+                else:
+                    cur_e = max(cur_e, e)
+            u += cur_e - cur_s
+            busy.append(u)
+            conv.append(sum(e - s for s, e, n in seg if any(c in n for c in CONV)))
+            nk.append(len(seg))
+            for s, e, n in seg:
+                per_kernel[short(n)][0] += 1
+                per_kernel[short(n)][1] += e - s
+        ns = len(steps)
+        avg = lambda v: sum(v) / len(v) / 1e3
+        lines += ["", f"## Steady-state training step (mean of {ns} steps, SGD kernel to SGD kernel)", "",
+                  f"* kernels per step: {avg(nk) * 1e3:.0f}",
+                  f"* wall (first kernel start to last kernel end): {avg(wall):.1f} us",
+                  f"* GPU busy (union of kernel intervals): {avg(busy):.1f} us "
+                  f"({100 * sum(busy) / sum(wall):.1f}% of wall)",
+                  f"* conv family (igemm + split-K / wgrad reductions): {avg(conv):.1f} us per step", "",
+                  "| kernel | calls/step | us/step | avg us |", "|---|---|---|---|"]
+        for k, (c, d) in sorted(per_kernel.items(), key=lambda kv: -kv[1][1]):
+            lines.append(f"| `{k}` | {c / ns:.0f} | {d / ns / 1e3:.1f} | {d / c / 1e3:.2f} |")
+    if len(sys.argv) > 4 and sys.argv[3] == "--bench":
+        try:
+            b = json.loads([l for l in open(sys.argv[4]) if l.startswith("{")][-1])
+            rf = b.get("roofline", {})
+            lines += ["", "## bench.py line of the same run", "", "```", json.dumps(b, indent=1), "```", "",
+                      f"bench live conv time per step: {rf.get('conv_ms_per_step')} ms "
+                      f"(rocprof conv family above: compare)"]
+        except Exception as e:  # keep the summary even if the bench line is missing
+            lines += ["", f"(bench line unavailable: {e!r})"]
+    with open(out, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines[:60]))
+
+
+if __name__ == "__main__":
+    main()
