@@ -176,7 +176,8 @@ static bool halo_geometry(const ConvShape& s, int& rs, int& imgs) {
     return false;
   }
   const int nh = imgs * (rs + 2) * (s.W + 2);
-  return nh <= HALO_ROWS && (uint64_t)s.N * hw * s.C * 2 < (1ull << 31);
+  // whole 64-pixel steps only (multi-image steps need N a multiple of the images per step)
+  return nh <= HALO_ROWS && ((int64_t)s.N * hw) % 64 == 0 && (uint64_t)s.N * hw * s.C * 2 < (1ull << 31);
 }
 
 int wgrad_halo_splits(const ConvShape& s) {

@@ -273,6 +273,8 @@ def test_sgd_and_amp(dtc, cuda):
     (8, 8, 8, 256, 64),     # C > K
     (12, 4, 4, 512, 512),   # four 4x4 images per step (multi-image halo)
     (2, 2, 2, 64, 64),      # 2x2 images: halo too tall -> generic loader
+    (2, 4, 4, 512, 512),    # 32 pixels: no whole 64-pixel step -> generic loader
+    (3, 4, 4, 64, 64),      # 48 pixels (N not a multiple of 4 images) -> generic loader
 ])
 def test_conv_wgrad_halo(dtc, cuda, case):
     """Halo-tiled 3x3 weight gradient == generic loader == oracle (fp32 sums of exact products)."""
