@@ -221,15 +221,16 @@ def _perturb_ulp(model, seed):
             prm.mul_(1 + sign * 2.0 ** -23)
 
 
-def gen_loss_chaos(steps=200, batch=128, seeds=(1, 2)):
-    """Reference bf16-autocast curves from 1-ulp-perturbed inits (loss_curve.json: bf16_ulp)."""
+def gen_loss_chaos(steps=200, batch=128, seeds=tuple(range(1, 9))):
+    """Reference bf16-autocast curves from 1-ulp-perturbed inits (loss_curve.json: bf16_ulp[seed-1]);
+    seeds already present in the fixture are kept, not recomputed."""
     utils = _import_from("single", "utils")
     net = _import_from("single", "net")
     templates = torch.randn(100, 3, 32, 32, generator=torch.Generator().manual_seed(1234))
     path = os.path.join(HERE, "loss_curve.json")
     out = json.load(open(path))
-    curves = []
-    for sd in seeds:
+    curves = list(out.get("bf16_ulp", []))
+    for sd in seeds[len(curves):]:
         utils.fix_seed(42)
         m = net.ResNet18()
         _perturb_ulp(m, sd)
@@ -246,9 +247,9 @@ def gen_loss_chaos(steps=200, batch=128, seeds=(1, 2)):
             losses.append(float(loss.detach()))
         curves.append(losses)
         print("ulp seed", sd, losses[:3], sum(losses) / len(losses), flush=True)
-    out["bf16_ulp"] = curves
-    with open(path, "w") as f:
-        json.dump(out, f)
+        out["bf16_ulp"] = curves
+        with open(path, "w") as f:  # checkpoint after every run
+            json.dump(out, f)
 
 
 def gen_loss_curve(steps=200, batch=128, modes=("fp32", "bf16")):
