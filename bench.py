@@ -50,6 +50,22 @@ def init_dist():
     return dist.get_rank(), dist.get_world_size(), local
 
 
+def _committed_traffic():
+    """HBM bytes per conv call from the newest committed PMC summary (profiles/*conv_traffic.json,
+    written by tools/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench);
+    PMC counters cannot be read live, so the value is the profile's, named in traffic_source."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "*conv_traffic.json")))
+    if not files:
+        return None
+    try:
+        return round(json.load(open(files[-1]))["hbm_bytes_per_call"], 1)
+    except Exception:
+        return None
+
+
 def cpu_baseline(seconds: float):
     """Oracle (numpy restatement) training step on the host cores: a bounded sample."""
     from oracle import resnet as R
@@ -198,11 +214,12 @@ def main():
                 "peak": BF16_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / BF16_PEAK_TFLOPS, 4) if achieved else None,
-                "traffic": None,
+                "traffic": _committed_traffic(),
                 "kernel": "implicit-GEMM conv (fwd+dgrad+wgrad incl. split-K reduce), all launches in the timed "
                           "region; per-call duration = last workgroup end - first workgroup start (s_memrealtime, "
                           "stamped by the kernels on the compute stream); measured over a second timed region of "
                           "the same K steps with the stamps armed (region_ms_per_step), value from the first",
+                "traffic_unit": "HBM bytes per conv call (PMC, profiles/*conv_traffic.json)",
                 "conv_ms_per_step": round(conv_ms / args.steps, 4),
                 "region_ms_per_step": round(prof_elapsed / args.steps * 1e3, 4) if prof_elapsed else None,
                 "conv_ms_by_pass": [round(v / args.steps, 4) for v in ms],

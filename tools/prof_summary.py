@@ -14,7 +14,7 @@ import os
 import sys
 from collections import defaultdict
 
-CONV = ("igemm_kernel", "splitk_reduce_kernel", "wgrad_reduce_kernel")
+CONV = ("igemm_kernel", "wgrad_halo_kernel", "splitk_reduce_kernel", "wgrad_reduce_kernel")
 
 
 def short(name):
@@ -69,6 +69,12 @@ def main():
                 per_kernel[short(n)][1] += e - s
         ns = len(steps)
         avg = lambda v: sum(v) / len(v) / 1e3
+        gaps = defaultdict(lambda: [0, 0])
+        for a, b in steps:
+            seg = rows[a:b + 1]
+            for (s0, e0, n0), (s1, e1, n1) in zip(seg, seg[1:]):
+                gaps[(short(n0), short(n1))][0] += 1
+                gaps[(short(n0), short(n1))][1] += max(0, s1 - e0)
         lines += ["", f"## Steady-state training step (mean of {ns} steps, SGD kernel to SGD kernel)", "",
                   f"* kernels per step: {avg(nk) * 1e3:.0f}",
                   f"* wall (first kernel start to last kernel end): {avg(wall):.1f} us",
@@ -78,6 +84,11 @@ def main():
                   "| kernel | calls/step | us/step | avg us |", "|---|---|---|---|"]
         for k, (c, d) in sorted(per_kernel.items(), key=lambda kv: -kv[1][1]):
             lines.append(f"| `{k}` | {c / ns:.0f} | {d / ns / 1e3:.1f} | {d / c / 1e3:.2f} |")
+        gsum = sum(v[1] for v in gaps.values()) / ns / 1e3
+        lines += ["", f"### Idle gaps between consecutive kernels: {gsum:.1f} us per step; largest", "",
+                  "| after | before | per step | us/step |", "|---|---|---|---|"]
+        for (k0, k1), (c, d) in sorted(gaps.items(), key=lambda kv: -kv[1][1])[:15]:
+            lines.append(f"| `{k0}` | `{k1}` | {c / ns:.1f} | {d / ns / 1e3:.1f} |")
     if len(sys.argv) > 4 and sys.argv[3] == "--bench":
         try:
             b = json.loads([l for l in open(sys.argv[4]) if l.startswith("{")][-1])
