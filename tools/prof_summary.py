@@ -22,14 +22,24 @@ def short(name):
     return n.split("(")[0]
 
 
+def load_rows(src):
+    """(start_ns, end_ns, kernel name) per dispatch from a csv kernel trace or a rocpd sqlite db."""
+    trace = glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True)
+    if trace:
+        with open(trace[0]) as f:
+            return [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                    for r in csv.DictReader(f)]
+    dbs = glob.glob(os.path.join(src, "**", "*results.db"), recursive=True)
+    assert dbs, f"no kernel_trace.csv or rocpd results.db under {src}"
+    import sqlite3
+
+    con = sqlite3.connect(dbs[0])
+    return [(int(a), int(b), n) for a, b, n in con.execute("select start, end, name from kernels")]
+
+
 def main():
     src, out = sys.argv[1], sys.argv[2]
-    trace = glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True)
-    assert trace, f"no kernel_trace.csv under {src}"
-    rows = []
-    with open(trace[0]) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows = load_rows(src)
     rows.sort()
     # steps: delimited by the fused SGD kernel
     sgd_idx = [i for i, r in enumerate(rows) if "sgd_nesterov" in r[2]]
