@@ -18,6 +18,7 @@ import contextlib
 import torch
 
 from . import ops
+from .nn import scaled_loss
 
 
 @contextlib.contextmanager
@@ -54,7 +55,7 @@ class GradScaler:
         if not self._enabled:
             return outputs
         self._lazy_init(outputs.device)
-        return outputs * self._scale
+        return scaled_loss(outputs, self._scale)
 
     def unscale_(self, optimizer) -> None:
         if not self._enabled or self._unscaled:

@@ -177,6 +177,7 @@ class _XentFn(torch.autograd.Function):
     def forward(ctx, logits, labels):
         loss, lse = ops.xent_fwd(logits, labels)
         ctx.save_for_backward(logits, labels, lse)
+        ctx.lse = lse
         return loss
 
     @staticmethod
@@ -186,6 +187,54 @@ class _XentFn(torch.autograd.Function):
         return ops.xent_bwd(logits, labels, lse, g), None
 
 
+class NativeLoss(torch.Tensor):
+    """Scalar loss of ``CrossEntropyLoss`` applied directly to the native ResNet's logits (and its
+    ``GradScaler.scale`` product). Its ``backward()`` runs the known chain
+    xent-backward -> network backward as two native calls, without the autograd engine's thread
+    hand-off and the per-node Python/elementwise launches in between (this runs right after the
+    reference's per-step ``dist.barrier()``, when the GPU queue is empty, so every host
+    microsecond there is GPU idle time). Gradients are identical to the autograd path, which is
+    still taken for any other use (explicit ``gradient``, ``create_graph``, ``inputs``), and any
+    arithmetic on the loss returns a plain autograd tensor."""
+
+    __torch_function__ = torch._C._disabled_torch_function_impl
+
+    def backward(self, gradient=None, retain_graph=None, create_graph=False, inputs=None):
+        fast = self._dtc_fast
+        if fast is None or gradient is not None or create_graph or inputs is not None or not _FAST_BACKWARD[0]:
+            return self._dtc_graph.backward(gradient, retain_graph, create_graph, inputs)
+        node, logits, labels, lse, gscale = fast
+        model, exe = node.model, node.exe
+        if exe.generation != node.gen:
+            raise NativeError("ResNet backward: the executor ran another forward since this graph was built "
+                              "(one forward per backward is supported)")
+        dl = ops.xent_bwd(logits, labels, lse, gscale)
+        exe.backward(dl, model._grad_scale, model._comm)
+        model._ensure_grads()
+        if not retain_graph:
+            self._dtc_fast = None
+        return None
+
+
+_FAST_BACKWARD = [True]  # tests flip this to compare against the autograd-engine path
+
+
+def _wrap_loss(graph: torch.Tensor, fast) -> torch.Tensor:
+    out = torch.Tensor._make_subclass(NativeLoss, graph.detach(), False)
+    out._dtc_graph = graph
+    out._dtc_fast = fast
+    return out
+
+
+def scaled_loss(loss: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """loss * scale (GradScaler.scale); keeps the direct backward chain of a NativeLoss."""
+    if isinstance(loss, NativeLoss):
+        g = loss._dtc_graph * scale
+        f = loss._dtc_fast
+        return _wrap_loss(g, None if f is None else (f[0], f[1], f[2], f[3], scale))
+    return loss * scale
+
+
 class CrossEntropyLoss(nn.Module):
     """nn.CrossEntropyLoss() with mean reduction (reference trainer.py:40) on the native kernel."""
 
@@ -193,7 +242,13 @@ class CrossEntropyLoss(nn.Module):
         require_cuda(logits, labels)
         if logits.dtype != torch.float32:
             logits = logits.float()
-        return _XentFn.apply(logits.contiguous(), labels.long().contiguous())
+        logits = logits.contiguous()
+        labels = labels.long().contiguous()
+        loss = _XentFn.apply(logits, labels)
+        node = logits.grad_fn
+        if torch.is_grad_enabled() and isinstance(node, _NetFn._backward_cls):
+            return _wrap_loss(loss, (node, logits, labels, loss.grad_fn.lse, None))
+        return loss
 
 
 # ----------------------------------------------------------------------------- modules

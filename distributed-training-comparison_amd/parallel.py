@@ -111,7 +111,8 @@ class DistributedDataParallel(nn.Module):
         with torch.cuda.device(device):
             self.comm = Comm.from_process_group(device, process_group)
             module.set_bucket_cap_mb(float(bucket_cap_mb))
-            module._comm = self.comm
+            # a one-rank all-reduce is the identity: no side-stream fork/join inside the backward
+            module._comm = self.comm if self.world_size > 1 else None
             module._grad_scale = 1.0 / self.world_size
             # C1: make every replica start from rank 0's state
             self.comm.broadcast_(flat.params, 0)

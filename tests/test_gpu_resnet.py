@@ -360,3 +360,40 @@ def test_loss_curve_200_steps(dtc, cuda):
     tol = 1e-2 if len(ref_curves) >= 9 else 2e-2
     print(f"ensemble n={len(ref_curves)}: ours {m_ours:.4f} ref {m_ref:.4f} rel {(m_ours - m_ref) / m_ref:+.4f}")
     assert abs(m_ours - m_ref) / m_ref < tol
+
+
+def test_native_loss_backward_matches_autograd(dtc, cuda):
+    """NativeLoss.backward (direct xent-backward -> network-backward chain, plain and
+    GradScaler-scaled) writes the same gradients as the autograd-engine path."""
+    from importlib import import_module
+
+    nnmod = import_module(dtc.__name__ + ".nn")
+    model, _, x, y = _setup(dtc, cuda, 8, seed=11)
+    crit = dtc.CrossEntropyLoss()
+    scaler = dtc.GradScaler()
+    xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
+    out = {}
+    for fast in (True, False):
+        nnmod._FAST_BACKWARD[0] = fast
+        try:
+            loss = crit(model(xd), yd)
+            assert isinstance(loss, nnmod.NativeLoss)
+            loss.backward()
+            g_plain = model.flat.grads.clone()
+            loss = crit(model(xd), yd)
+            scaled = scaler.scale(loss)
+            assert isinstance(scaled, nnmod.NativeLoss)
+            assert abs(float(scaled) - float(loss) * 65536.0) < 1e-3 * float(scaled)
+            scaled.backward()
+            g_scaled = model.flat.grads.clone()
+        finally:
+            nnmod._FAST_BACKWARD[0] = True
+        torch.cuda.synchronize()
+        out[fast] = (g_plain, g_scaled)
+    assert rel_err(out[True][0].cpu().numpy(), out[False][0].cpu().numpy()) < 1e-5
+    assert rel_err(out[True][1].cpu().numpy(), out[False][1].cpu().numpy()) < 1e-5
+    ratio = (out[True][1].norm() / out[True][0].norm()).item()
+    assert abs(ratio - 65536.0) < 1e-2 * 65536.0
+    # arithmetic on the loss leaves the fast path: a plain autograd tensor
+    loss = crit(model(xd), yd)
+    assert type(loss * 2.0) is torch.Tensor
