@@ -1,0 +1,466 @@
+// Halo-tiled 3x3 / stride 1 / pad 1 convolution, forward and data-gradient, on bf16 MFMA (gfx950).
+//
+// Replaces cuDNN's forward and data-gradient kernels for the 13 stride-1 3x3 convs of ResNet-18
+// (reference src/*/net.py:18-24, 29-35; `nn.Conv2d(..., kernel_size=3, stride=1, padding=1)`).
+// The generic implicit-GEMM loader (igemm.hip) gathers one im2col row per (pixel, tap), so each
+// input pixel is fetched from L2 nine times. Here a workgroup owns an output tile of whole image
+// rows (BN pixels) x BM output channels and, per 64-channel reduction chunk, stages the tile's
+// zero-padded input HALO once ((rows+2) x (W+2) pixels per image slice, 128-B LDS rows of 64
+// channels); the nine taps then read the same halo shifted by r*(W+2)+s rows. Weights of one
+// (chunk, tap) step are BM rows of 128 B. L2->LDS bytes per output tile and chunk drop from
+// 9*BN*128 + 9*BM*128 (im2col) to ~1.3*BN*128 + 9*BM*128.
+//
+//   mode   D = A x B (MFMA rows x cols)     A (rows, from LDS)                B (cols)
+//   FWD    y[k][pixel]                       W[k][r][s][c-chunk]  row image    halo(x)  at +( r,  s)
+//   DGRAD  dx[c][pixel]                      W[k-chunk][r][s][c]  tr image     halo(dy) at +(2-r,2-s)
+//
+// (dgrad of a stride-1 pad-1 3x3 conv is the same correlation with the taps mirrored and W
+// transposed; the tr image is read with ds_read_b64_tr_b16, so W is never transposed in HBM.)
+// Epilogues match igemm.hip: FWD rounds to bf16 and reduces the BN batch statistics of the
+// rounded output into fp64 slots; DGRAD optionally adds the residual-branch gradient.
+//
+// Pipeline: weights double-buffered; the halo is double-buffered (NHB = 2: the next chunk's halo
+// arrives in slices during the current chunk's first eight taps) or single (NHB = 1: reloaded
+// at chunk boundaries, a bubble other resident workgroups hide). One s_waitcnt vmcnt(0) +
+// s_barrier per step (the DMA for step it+1 overlaps the MFMAs of step it).
+#include "common.h"
+#include "kernels.h"
+#include "tile_common.h"
+
+namespace dtc {
+
+// Halo LDS swizzle: 16-B chunk c of halo row r is stored at chunk c ^ hswz(r). Every 8 B-fragment
+// lanes that share a reduction chunk read 8 halo rows that are distinct mod 8 (the per-lane pixel
+// order below guarantees it for W = 4 and 8 too), so (row parity, chunk ^ hswz) spreads them over
+// 8 different 16-B bank slots, and the chunk pair (q, q+1) read by one ds_read_b128 lane group
+// lands on even / odd slots: conflict-free for EVERY tap shift (rowswz is only for aligned rows).
+__device__ __forceinline__ int hswz(int r) { return ((r >> 1) & 3) << 1; }
+
+// Pixel of B-fragment column j (0..15) within its 16-pixel block. ds_read_b128 serves lanes in
+// groups {0-3,12-15,20-27}, ...: columns {4..11} and {0..3,12..15} must each map to halo rows
+// distinct mod 8. Contiguous image rows (W >= 16) satisfy it as is; for W = 8 (halo pitch 10) the
+// block's first image row goes to columns 4..11, for W = 4 (pitch 6) image rows 0 and 2 do.
+__device__ __forceinline__ int frag_pixel(int j, int W) {
+  if (W == 8) return (j >= 4 && j < 12) ? j - 4 : (j < 4 ? j + 8 : j);
+  if (W == 4) return (j >= 4 && j < 8) ? j - 4 : (j < 4 ? j + 4 : j);
+  return j;
+}
+
+struct HConvParams {
+  const u16* src;  // FWD: x; DGRAD: dy. NHWC, Cin channels (Cin = reduction channels)
+  const u16* w;    // KRSC [K][3][3][C] (C = conv input channels)
+  u16* out;        // NHWC, Cout channels
+  const u16* res;  // DGRAD: residual added in the epilogue (NHWC, Cout) or null
+  double* stats;   // FWD: BN statistics [SLOTS][2][Cout] or null
+  float* slab;     // split-K: fp32 partial tiles [split][M][Cout]
+  int N, H, W, Cin, Cout, C;
+  uint32_t src_bytes;
+  int rows;     // output rows per image slice
+  int imgs;     // image slices per tile (imgs > 1: whole images, rows == H)
+  int hb;       // halo rows per image slice: (rows + 2) * (W + 2)
+  int nh;       // halo rows per tile
+  int nhi;      // halo DMA instructions per wave (8 rows each, 4 waves)
+  int tiles_y;  // H / rows
+  int tiles_a;  // Cout / BM
+  int nchunk;   // Cin / 64 chunks per split
+  int xcd_remap;
+  FastDiv fd_hb, fd_w2, fd_spx, fd_w;
+  u64* ts;
+};
+
+template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP>
+__global__ void __launch_bounds__(256, 1) conv_halo_kernel(const HConvParams p) {
+  constexpr int FM = BM / (WR * 16);
+  constexpr int FN = BN / (WC * 16);
+  constexpr int WBYTES = BM * 128;
+  constexpr int HBYTES = HCAP * 128;
+  constexpr int NIW = BM / 32;       // weight DMA instructions per wave per step
+  constexpr int NHI = HCAP / 32;     // max halo DMA instructions per wave
+  static_assert(WR * WC == 4 && HCAP % 32 == 0, "shape");
+  __shared__ __attribute__((aligned(1024))) char smem[NHB * HBYTES + 2 * WBYTES];
+  char* const wbase = smem + NHB * HBYTES;
+
+  stamp_start(p.ts);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int bid = blockIdx.x;
+  if (p.xcd_remap && gridDim.x >= 16) {  // consecutive tile ids (same pixel tile) share an XCD's L2
+    const int nwg = gridDim.x, x8 = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    bid = (x8 < rr ? x8 * (q + 1) : rr * (q + 1) + (x8 - rr) * q) + (bid >> 3);
+  }
+  const int ta = bid % p.tiles_a, tb = bid / p.tiles_a;
+  const int a0 = ta * BM;
+  const int split = blockIdx.y, c0 = split * p.nchunk;  // first reduction chunk of this split
+  int n0, y0;
+  if (p.imgs == 1) {
+    n0 = tb / p.tiles_y;
+    y0 = (tb - n0 * p.tiles_y) * p.rows;
+  } else {
+    n0 = tb * p.imgs;
+    y0 = 0;
+  }
+  const int W2 = p.W + 2;
+  const int px0 = (n0 * p.H + y0) * p.W;
+  const int M = p.N * p.H * p.W;
+  const int lrow = lane >> 3, pc = lane & 7;
+  const int RSC = 9 * p.C;
+
+  // ---- weight DMA: per-lane element offsets (add the step's tap / chunk term)
+  int offW[NIW];
+#pragma unroll
+  for (int j = 0; j < NIW; ++j) {
+    if constexpr (MODE == 0) {  // row image: LDS row = output channel, 64 input channels of one tap
+      const int row = (wave + 4 * j) * 8 + lrow;
+      offW[j] = (a0 + row) * RSC + (pc ^ rowswz(row)) * 8;
+    } else {  // tr image(s): LDS row = k within the chunk, 64 output channels c per image
+      const int ia = wave + 4 * j, img = ia >> 3, rowin = (ia & 7) * 8 + lrow;
+      offW[j] = rowin * RSC + a0 + img * 64 + (pc ^ trswz(rowin)) * 8;
+    }
+  }
+  auto stage_w = [&](char* dst, int cc, int tap) {
+    // FWD pairs weight tap (r,s) with halo offset (r,s); DGRAD pairs weight tap (r,s) with (2-r,2-s):
+    // the loop tap index t is the HALO offset, so DGRAD loads weight tap 8-t.
+    const int wt = (MODE == 0) ? tap : 8 - tap;
+    const int add = (MODE == 0) ? (wt * p.C + cc * 64) : (cc * 64 * RSC + wt * p.C);
+#pragma unroll
+    for (int j = 0; j < NIW; ++j) glds16(p.w + offW[j] + add, dst + (wave + 4 * j) * 1024);
+  };
+
+  // ---- halo DMA: instruction q of this wave fills LDS rows (wave + 4q)*8 .. +8
+  uint32_t hoff[NHI];
+#pragma unroll
+  for (int q = 0; q < NHI; ++q) {
+    const int hr = (wave + 4 * q) * 8 + lrow;
+    uint32_t off = 0x80000000u;  // out of the buffer: the DMA writes zeros
+    if (q < p.nhi && hr < p.nh) {
+      const int i = (int)fdiv((uint32_t)hr, p.fd_hb), rem = hr - i * p.hb;
+      const int hy = (int)fdiv((uint32_t)rem, p.fd_w2), hx = rem - hy * W2;
+      const int n = n0 + i, y = y0 + hy - 1, x = hx - 1;
+      if (n < p.N && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W)
+        off = (uint32_t)((((n * p.H + y) * p.W + x) * p.Cin + (pc ^ hswz(hr)) * 8) * 2);
+    }
+    hoff[q] = off;
+  }
+  auto stage_h = [&](char* dst, int cc, int q_lo, int q_hi) {
+#pragma unroll
+    for (int q = 0; q < NHI; ++q) {
+      if (q >= q_lo && q < q_hi && q < p.nhi) {
+        const uint32_t o = hoff[q] == 0x80000000u ? 0x80000000u : hoff[q] + (uint32_t)(cc * 128);
+        buf_lds16(p.src, p.src_bytes, dst + (wave + 4 * q) * 1024, o);
+      }
+    }
+  };
+
+  // ---- B fragments: halo row of each of this lane's pixels (tap (0,0))
+  const int wr = wave / WC, wc = wave % WC;
+  const int arow0 = wr * (BM / WR), bcol0 = wc * (BN / WC);
+  const int spx = p.rows * p.W;  // pixels per image slice
+  const int fpx = frag_pixel(lane & 15, p.W);
+  int hbr[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int l = bcol0 + j * 16 + fpx;
+    const int i = (int)fdiv((uint32_t)l, p.fd_spx), rem = l - i * spx;
+    const int y = (int)fdiv((uint32_t)rem, p.fd_w), x = rem - y * p.W;
+    hbr[j] = i * p.hb + y * W2 + x;
+  }
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const char* hbuf, const char* wb, int tap) {
+    const int r = tap / 3, s = tap - r * 3;
+    const int toff = r * W2 + s;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        if constexpr (MODE == 0) af[i] = frag_row(wb, arow0 + i * 16, ks, lane);
+        else af[i] = frag_tr(wb, arow0 + i * 16, ks, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = hbr[j] + toff;
+        const int ch = (ks * 4 + (lane >> 4)) ^ hswz(row);
+        bfr[j] = __builtin_bit_cast(bf16x8, *(const uint4*)(hbuf + row * 128 + (ch << 4)));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // ---- main loop over (chunk, tap) steps
+  const int nsteps = p.nchunk * 9;
+  stage_h(smem, c0, 0, NHI);
+  stage_w(wbase, c0, 0);
+  int cc = 0, tap = 0;  // chunk relative to c0
+  for (int it = 0; it < nsteps; ++it) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int ntap = tap == 8 ? 0 : tap + 1, ncc = tap == 8 ? cc + 1 : cc;
+    const bool more = it + 1 < nsteps;
+    bool reload = false;
+    if (more) {
+      stage_w(wbase + ((it + 1) & 1) * WBYTES, c0 + ncc, ntap);
+      if constexpr (NHB == 2) {
+        if (cc + 1 < p.nchunk && tap < 8) {  // next chunk's halo, slice `tap` of 8
+          const int q_lo = (tap * p.nhi) >> 3, q_hi = ((tap + 1) * p.nhi) >> 3;
+          stage_h(smem + ((cc + 1) & 1) * HBYTES, c0 + cc + 1, q_lo, q_hi);
+        }
+      } else {
+        reload = (ntap == 0);
+      }
+    }
+    compute(smem + (NHB == 2 ? (cc & 1) * HBYTES : 0), wbase + (it & 1) * WBYTES, tap);
+    if (NHB == 1 && reload) {  // every wave is done with the halo: refill it for chunk ncc
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      stage_h(smem, c0 + ncc, 0, NHI);
+    }
+    cc = ncc;
+    tap = ntap;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // LDS reads done before the epilogue reuses smem
+  asm volatile("" ::: "memory");
+
+  // ---- epilogue: D[row = output channel][col = pixel], 4 consecutive channels per lane
+  const int rq = (lane >> 4) * 4, cl = fpx;  // column -> pixel, as in the B fragments
+  if (p.slab != nullptr) {  // split-K partial: fp32 [split][pixel][Cout], one 16-B store per fragment
+    float* slab = p.slab + (size_t)split * M * p.Cout;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int pix = px0 + bcol0 + j * 16 + cl;
+      if (pix >= M) continue;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        *(f32x4*)(slab + (size_t)pix * p.Cout + a0 + arow0 + i * 16 + rq) = acc[i][j];
+    }
+  } else if constexpr (MODE == 0) {
+    float* red = (float*)smem;  // [WC][BM][2]
+    const bool want_stats = p.stats != nullptr;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int chl = arow0 + i * 16 + rq;
+      const int ch = a0 + chl;
+      float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int pix = px0 + bcol0 + j * 16 + cl;
+        float v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = round_bf(acc[i][j][t]);
+        if (pix < M) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            s4[t] += v[t];
+            q4[t] += v[t] * v[t];
+          }
+          uint2 wv;
+          wv.x = pack_bf2(v[0], v[1]);
+          wv.y = pack_bf2(v[2], v[3]);
+          *(uint2*)(p.out + (size_t)pix * p.Cout + ch) = wv;
+        }
+      }
+      if (want_stats) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          s4[t] = row16_sum(s4[t]);
+          q4[t] = row16_sum(q4[t]);
+        }
+        if ((lane & 15) == 0) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            red[(wc * BM + chl + t) * 2 + 0] = s4[t];
+            red[(wc * BM + chl + t) * 2 + 1] = q4[t];
+          }
+        }
+      }
+    }
+    if (want_stats) {
+      __syncthreads();
+      if ((int)threadIdx.x < BM) {
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < WC; ++w) {
+          s += red[(w * BM + threadIdx.x) * 2 + 0];
+          q += red[(w * BM + threadIdx.x) * 2 + 1];
+        }
+        double* st = p.stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * p.Cout;
+        unsafeAtomicAdd(st + a0 + threadIdx.x, (double)s);
+        unsafeAtomicAdd(st + p.Cout + a0 + threadIdx.x, (double)q);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int pix = px0 + bcol0 + j * 16 + cl;
+      if (pix >= M) continue;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ch = a0 + arow0 + i * 16 + rq;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        const size_t o = (size_t)pix * p.Cout + ch;
+        if (p.res) {
+          const uint2 rr = *(const uint2*)(p.res + o);
+          v[0] += bf_lo(rr.x); v[1] += bf_hi(rr.x); v[2] += bf_lo(rr.y); v[3] += bf_hi(rr.y);
+        }
+        uint2 wv;
+        wv.x = pack_bf2(v[0], v[1]);
+        wv.y = pack_bf2(v[2], v[3]);
+        *(uint2*)(p.out + o) = wv;
+      }
+    }
+  }
+  stamp_end(p.ts);
+}
+
+// ---------------------------------------------------------------- host side
+struct HaloCfg {
+  int bm, bn, nhb, hcap;
+};
+// Template instances (launch_halo below). LDS: NHB * HCAP * 128 + 2 * BM * 128 bytes.
+static const HaloCfg kHaloCfgs[] = {
+    {64, 256, 1, 416},   // 0: 70 KB, 2 WG/CU: big images / many tiles
+    {64, 128, 2, 288},   // 1: 90 KB: double-buffered halo, no chunk bubbles
+    {64, 128, 1, 288},   // 2: 53 KB, 3 WG/CU
+    {128, 256, 1, 416},  // 3: 86 KB: wide output-channel tiles
+    {128, 128, 1, 288},  // 4: 69 KB, 2 WG/CU: 64x64 per wave
+    {128, 128, 2, 288},  // 5: 106 KB: 64x64 per wave, double-buffered halo
+};
+constexpr int kNumHaloCfgs = (int)(sizeof(kHaloCfgs) / sizeof(kHaloCfgs[0]));
+
+static bool halo_geometry(const ConvShape& s, int bn, int hcap, int& rows, int& imgs, int& nh) {
+  const int hw = s.H * s.W;
+  if (hw >= bn) {
+    if (bn % s.W) return false;
+    rows = bn / s.W;
+    if (s.H % rows) return false;
+    imgs = 1;
+  } else {
+    if (bn % hw) return false;
+    imgs = bn / hw;
+    rows = s.H;
+  }
+  nh = imgs * (rows + 2) * (s.W + 2);
+  return nh <= hcap;
+}
+
+static bool halo_shape_ok(const ConvShape& s) {
+  return s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.C % 64 == 0 && s.K % 64 == 0 &&
+         (uint64_t)s.N * s.H * s.W * std::max(s.C, s.K) * 2 < (1ull << 31);
+}
+
+static int halo_tiles_b(const ConvShape& s, int rows, int imgs) {
+  return imgs == 1 ? s.N * (s.H / rows) : (s.N + imgs - 1) / imgs;
+}
+
+static bool cfg_fits(const ConvShape& s, int cfg, int cout) {
+  int rows, imgs, nh;
+  const HaloCfg& c = kHaloCfgs[cfg];
+  return cout % c.bm == 0 && halo_geometry(s, c.bn, c.hcap, rows, imgs, nh);
+}
+
+// Plan for pass `mode` (CONV_FWD / CONV_DGRAD): configuration (-1: not applicable / disabled) and
+// split-K factor over the reduction chunks.
+HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
+  HaloPlan hp{-1, 1};
+  const int opt = option_get(OPT_HALO_CONV);
+  if (opt == 0 || !halo_shape_ok(s)) return hp;
+  const int cout = mode == CONV_FWD ? s.K : s.C;
+  const int cin = mode == CONV_FWD ? s.C : s.K;
+  const int nchunk = cin / 64;
+  auto tiles = [&](int cfg) {
+    int rows = 1, imgs = 1, nh = 0;
+    const HaloCfg& c = kHaloCfgs[cfg];
+    halo_geometry(s, c.bn, c.hcap, rows, imgs, nh);
+    return halo_tiles_b(s, rows, imgs) * (cout / c.bm);
+  };
+  if (opt >= 2) {  // forced configuration opt-2 (tuning)
+    const int cfg = std::min(opt - 2, kNumHaloCfgs - 1);
+    if (!cfg_fits(s, cfg, cout)) return hp;
+    hp.cfg = cfg;
+  } else {
+    // measured (tools/conv_bench.py, B=256): 64x256 tiles while they give >= 2 workgroups per CU
+    // (layer1/2); else 64x128 tiles at 3 workgroups per CU, split-K up to ~2 workgroups per CU
+    // (layer3: 512 tiles; layer4: 256 tiles x 2 splits)
+    if (cfg_fits(s, 0, cout) && tiles(0) >= 512) hp.cfg = 0;
+    else if (cfg_fits(s, 2, cout)) hp.cfg = 2;
+    else if (cfg_fits(s, 0, cout)) hp.cfg = 0;
+    else return hp;
+  }
+  int split = option_get(OPT_HALO_SPLIT);
+  if (split <= 0) {
+    split = 1;
+    while (tiles(hp.cfg) * split * 2 <= 512 && nchunk % (split * 2) == 0 && nchunk / (split * 2) >= 2) split *= 2;
+  }
+  if (nchunk % split != 0) split = 1;
+  hp.split = split;
+  return hp;
+}
+
+size_t conv_halo_slab_bytes(const ConvShape& s, int mode) {
+  const HaloPlan hp = conv_halo_plan(s, mode);
+  if (hp.cfg < 0 || hp.split <= 1) return 0;
+  const int cout = mode == CONV_FWD ? s.K : s.C;
+  return (size_t)hp.split * s.N * s.H * s.W * cout * 4;
+}
+
+template <int MODE>
+static int launch_halo(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
+  switch (cfg) {
+    case 0: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 256, 1, 4, 1, 416>), grid, dim3(256), 0, st, p); break;
+    case 1: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 2, 288>), grid, dim3(256), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 1, 288>), grid, dim3(256), 0, st, p); break;
+    case 3: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 256, 2, 2, 1, 416>), grid, dim3(256), 0, st, p); break;
+    case 4: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 1, 288>), grid, dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 2, 288>), grid, dim3(256), 0, st, p); break;
+  }
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
+              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
+  DTC_CHECK_ARG(hp.cfg >= 0 && hp.cfg < kNumHaloCfgs && halo_shape_ok(s) && (mode == CONV_FWD || mode == CONV_DGRAD),
+                "conv_halo: unsupported shape / configuration");
+  const HaloCfg& c = kHaloCfgs[hp.cfg];
+  HConvParams p{};
+  p.src = src; p.w = w; p.out = out; p.res = res; p.stats = stats;
+  p.N = s.N; p.H = s.H; p.W = s.W; p.C = s.C;
+  p.Cin = mode == CONV_FWD ? s.C : s.K;
+  p.Cout = mode == CONV_FWD ? s.K : s.C;
+  DTC_CHECK_ARG(p.Cout % c.bm == 0, "conv_halo: output channels %d not a multiple of %d", p.Cout, c.bm);
+  DTC_CHECK_ARG(halo_geometry(s, c.bn, c.hcap, p.rows, p.imgs, p.nh), "conv_halo: geometry does not fit config %d",
+                hp.cfg);
+  const int M = s.N * s.H * s.W;
+  int split = hp.split;
+  if (split > 1 && (slab == nullptr || slab_bytes < (size_t)split * M * p.Cout * 4)) split = 1;
+  DTC_CHECK_ARG((p.Cin / 64) % split == 0, "conv_halo: split %d does not divide the reduction", split);
+  p.slab = split > 1 ? slab : nullptr;
+  p.src_bytes = (uint32_t)((uint64_t)M * p.Cin * 2);
+  p.hb = (p.rows + 2) * (s.W + 2);
+  p.nhi = (p.nh + 31) / 32;
+  p.tiles_y = s.H / p.rows;
+  p.tiles_a = p.Cout / c.bm;
+  p.nchunk = p.Cin / 64 / split;
+  p.xcd_remap = option_get(OPT_XCD_REMAP);
+  p.fd_hb = make_fastdiv(p.hb);
+  p.fd_w2 = make_fastdiv(s.W + 2);
+  p.fd_spx = make_fastdiv(p.rows * s.W);
+  p.fd_w = make_fastdiv(s.W);
+  p.ts = ts;
+  const dim3 grid(halo_tiles_b(s, p.rows, p.imgs) * p.tiles_a, split);
+  DTC_TRY(mode == CONV_FWD ? launch_halo<0>(p, hp.cfg, grid, st) : launch_halo<1>(p, hp.cfg, grid, st));
+  if (split > 1) return splitk_reduce(slab, split, M, p.Cout, out, res, stats, st, ts);
+  return 0;
+}
+
+}  // namespace dtc

@@ -678,6 +678,7 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
     const int tiles = (A / pl.bm) * ceil_div(M, pl.bn);
     pl.splits = (tiles >= 256 || cls) ? 1 : pick_splits(tiles, num_kt, 480, 8);
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * M * A * 4 : 0;
+    pl.slab_bytes = std::max(pl.slab_bytes, conv_halo_slab_bytes(s, mode));
     pl.num_kt = num_kt;
   } else if (const int hs = wgrad_halo_splits(s)) {  // halo-tiled kernel (wgrad_halo.hip)
     pl.bm = 576;
@@ -701,6 +702,10 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
 
 int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
              size_t slab_bytes, hipStream_t st, u64* ts) {
+  {
+    const HaloPlan hp = conv_halo_plan(s, CONV_FWD);
+    if (hp.cfg >= 0) return conv_halo(s, CONV_FWD, hp, x, w, y, nullptr, stats, slab, slab_bytes, st, ts);
+  }
   IGemmParams p{};
   p.ts = ts;
   DTC_TRY(fill_common(p, s));
@@ -729,6 +734,10 @@ int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* sta
 
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
                size_t slab_bytes, hipStream_t st, u64* ts) {
+  {
+    const HaloPlan hp = conv_halo_plan(s, CONV_DGRAD);
+    if (hp.cfg >= 0) return conv_halo(s, CONV_DGRAD, hp, dy, w, dx, res, nullptr, slab, slab_bytes, st, ts);
+  }
   IGemmParams p{};
   p.ts = ts;
   DTC_TRY(fill_common(p, s));

@@ -16,6 +16,8 @@ enum {
   OPT_WGRAD_FAST = 3,
   OPT_GRAPHS = 4,
   OPT_WGRAD_HALO = 5,  // target workgroup count of the halo WGRAD kernel (0 = generic loader only)
+  OPT_HALO_CONV = 6,   // halo FWD/DGRAD for 3x3 s1: 0 off, 1 auto, 2+k force configuration k (tuning)
+  OPT_HALO_SPLIT = 7,  // halo FWD/DGRAD split-K over reduction chunks: 0 auto, k forced
   OPT_COUNT
 };
 int option_get(int id);
@@ -52,6 +54,15 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
 int wgrad_halo_splits(const ConvShape& s);
 int conv_wgrad_halo(const ConvShape& s, const u16* x, const u16* dy, float* slab, int splits, int* used_splits,
                     hipStream_t st, u64* ts);
+// Halo-tiled 3x3 / stride 1 FWD and DGRAD (conv_halo.hip): configuration for the pass (-1: not
+// applicable), and the launch (FWD: stats optional; DGRAD: res optional).
+struct HaloPlan {
+  int cfg, split;
+};
+HaloPlan conv_halo_plan(const ConvShape& s, int mode);
+size_t conv_halo_slab_bytes(const ConvShape& s, int mode);  // fp32 split-K slab the plan needs
+int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
+              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts);
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
                   hipStream_t st, u64* ts = nullptr);
 // per slot i of ts[n][DTC_PROF_SLOT_U64]: acc[i] += (max end - min start, 1) if stamped; cells reset

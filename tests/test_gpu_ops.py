@@ -28,6 +28,8 @@ CONV_CASES = [
     (26, 32, 32, 128, 256, 3, 1),  # 128x128 tiles, no split, ragged last pixel tile
     (100, 32, 32, 64, 64, 3, 1),   # 64x256 tiles (K=64 layers), no split
     (64, 16, 16, 64, 128, 3, 2),   # stride-2 class GEMMs big enough for 64x256 tiles
+    (5, 8, 8, 256, 256, 3, 1),     # halo conv: 2 images per tile, ragged last tile
+    (9, 4, 4, 512, 256, 3, 1),     # halo conv: 8 images per tile, C != K
 ]
 
 
@@ -292,3 +294,47 @@ def test_conv_wgrad_halo(dtc, cuda, case):
         dtc._native.lib.dtc_set_option(b"wgrad_halo", 256)
     assert rel_err(halo, ref) < 1e-5
     assert rel_err(generic, ref) < 1e-5
+
+
+HALO_CASES = [
+    # (N, H, W, C, K): 3x3 stride-1 convs for every halo configuration (conv_halo.hip)
+    (2, 32, 32, 64, 64),
+    (3, 16, 16, 128, 128),
+    (5, 8, 8, 256, 128),
+    (9, 4, 4, 128, 256),
+]
+
+
+@pytest.mark.parametrize("split", [0, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv_halo_configs(dtc, cuda, case, cfg, split):
+    """Halo-tiled FWD (+BN statistics) and DGRAD (+residual) in each forced configuration
+    (option halo_conv = 2 + cfg; a geometry the configuration cannot tile falls back to the
+    implicit-GEMM kernel, which must agree as well), unsplit and split-K over reduction chunks
+    (fp32 slab + splitk_reduce epilogue)."""
+    N, H, W, C, K = case
+    g = np.random.default_rng(21 + cfg)
+    x = _rand_bf16((N, H, W, C), g)
+    w = _rand_bf16((K, 3, 3, C), g, 0.05)
+    dy = _rand_bf16((N, H, W, K), g)
+    res = _rand_bf16((N, H, W, C), g)
+    dtc._native.call("dtc_set_option", b"halo_conv", 2 + cfg)
+    dtc._native.call("dtc_set_option", b"halo_split", split)
+    try:
+        stats = dtc.ops.new_stats(K, cuda)
+        y = dtc.ops.conv2d_fwd(_to_dev_bf16(x, cuda), _to_dev_bf16(w, cuda), 1, 1, stats=stats)
+        dx = dtc.ops.conv2d_dgrad(_to_dev_bf16(dy, cuda), _to_dev_bf16(w, cuda), (H, W), 1, 1,
+                                  res=_to_dev_bf16(res, cuda))
+        torch.cuda.synchronize()
+    finally:
+        dtc._native.call("dtc_set_option", b"halo_conv", 1)
+        dtc._native.call("dtc_set_option", b"halo_split", 0)
+    yk = y.float().cpu().numpy()
+    assert rel_err(yk, O.conv2d_fwd(x, w, 1, 1)) < 1e-2
+    s = stats.sum(0).cpu().numpy()
+    yb = yk.reshape(-1, K).astype(np.float64)
+    np.testing.assert_allclose(s[0], yb.sum(0), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
+    ref = O.conv2d_dgrad(dy, w, (H, W), 1, 1) + res
+    assert rel_err(dx.float().cpu().numpy(), ref) < 1e-2

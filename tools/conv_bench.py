@@ -1,5 +1,8 @@
-"""Time every distinct ResNet-18 conv (batch B) for fwd / dgrad / wgrad on the native kernels,
-interleaving kernel-option variants in one process (guide §5.4 rule 24). Prints TFLOP/s
+"""Time every distinct ResNet-18 conv (batch B) for fwd / dgrad / wgrad on the native kernels.
+
+Each (layer, pass) is captured ITERS times into a torch CUDA graph (buffers preallocated, raw
+C-ABI calls), so the replay measures device time only, not Python/allocation overhead. Kernel-
+option variants are interleaved in one process (guide §5.4 rule 24). Prints TFLOP/s
 (algorithmic 2*N*P*Q*K*R*S*C) per pass and the per-step weighted total."""
 import argparse
 import json
@@ -31,46 +34,68 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--variants", default="igemm_stages=2;igemm_stages=3")
+    ap.add_argument("--variants", default="halo_conv=1;halo_conv=0")
+    ap.add_argument("--layers", default="")
+    ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     args = ap.parse_args()
     dtc = dtc_import.load()
-    ops = dtc.ops
+    ops, nat = dtc.ops, dtc._native
     dev = torch.device("cuda:0")
     B = args.batch
     variants = [dict(kv.split("=") for kv in v.split(",")) for v in args.variants.split(";")]
     results = {i: {} for i in range(len(variants))}
-    for (name, H, C, K, R, st, cnt) in LAYERS:
+    layers = [l for l in LAYERS if not args.layers or l[0] in args.layers.split(",")]
+    passes = args.passes.split(",")
+    for (name, H, C, K, R, st, cnt) in layers:
         pad = 1 if R == 3 else 0
         P = (H + 2 * pad - R) // st + 1
         x = torch.randn(B, H, H, C, device=dev).bfloat16()
         w = (torch.randn(K, R, R, C, device=dev) * 0.05).bfloat16()
         dy = torch.randn(B, P, P, K, device=dev).bfloat16()
+        y = torch.empty(B, P, P, K, device=dev).bfloat16()
+        dx = torch.empty(B, H, H, C, device=dev).bfloat16()
+        dw = torch.empty(K, R, R, C, device=dev)
         stats = ops.new_stats(K, dev)
+        d = ops.conv_desc(B, H, H, C, K, R, R, st, pad)
+        wsb = max(nat.lib.dtc_conv2d_workspace_size(d, m) for m in range(3))
+        ws = torch.empty(wsb // 4 + 64, device=dev)
         flops = 2.0 * B * P * P * K * R * R * C
+        P_ = nat.ptr
         fns = {
-            "fwd": lambda: ops.conv2d_fwd(x, w, st, pad, stats=stats),
-            "dgrad": lambda: ops.conv2d_dgrad(dy, w, (H, H), st, pad),
-            "wgrad": lambda: ops.conv2d_wgrad(x, dy, R, R, st, pad),
+            "fwd": lambda: nat.call("dtc_conv2d_fwd", d, P_(x), P_(w), P_(y), P_(stats), P_(ws), wsb, nat.stream_ptr()),
+            "dgrad": lambda: nat.call("dtc_conv2d_dgrad", d, P_(dy), P_(w), P_(dx), None, P_(ws), wsb,
+                                      nat.stream_ptr()),
+            "wgrad": lambda: nat.call("dtc_conv2d_wgrad", d, P_(x), P_(dy), P_(dw), 1.0, P_(ws), wsb,
+                                      nat.stream_ptr()),
         }
         if name == "stem":
             fns.pop("dgrad")
+        fns = {k: v for k, v in fns.items() if k in passes}
         for rnd in range(3):  # interleaved rounds
             for vi, var in enumerate(variants):
                 for k, v in var.items():
-                    dtc._native.call("dtc_set_option", k.encode(), int(v))
+                    nat.call("dtc_set_option", k.encode(), int(v))
                 for pname, fn in fns.items():
                     fn()
                     torch.cuda.synchronize()
+                    g = torch.cuda.CUDAGraph()
+                    s = torch.cuda.Stream()
+                    with torch.cuda.stream(s):
+                        with torch.cuda.graph(g, stream=s):
+                            for _ in range(args.iters):
+                                fn()
+                    g.replay()
+                    torch.cuda.synchronize()
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    for _ in range(args.iters):
-                        fn()
+                    g.replay()
                     e1.record()
                     torch.cuda.synchronize()
                     us = e0.elapsed_time(e1) * 1e3 / args.iters
                     key = (name, pname)
                     prev = results[vi].get(key)
                     results[vi][key] = (min(us, prev[0]) if prev else us, flops, cnt)
+                    del g
     for vi, var in enumerate(variants):
         print(f"=== variant {var}")
         tot_us, tot_fl = 0.0, 0.0
