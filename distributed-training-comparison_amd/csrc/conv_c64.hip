@@ -1,0 +1,282 @@
+// Persistent 3x3 / stride 1 / pad 1 convolution with 64 input and 64 output channels
+// (ResNet-18 layer1: four convs, forward and data-gradient; reference src/*/net.py:18-24,
+// `nn.Conv2d(64, 64, 3, 1, 1)`), bf16 MFMA on gfx950.
+//
+// layer1's reduction is a single 64-channel chunk x 9 taps, so a tile-per-workgroup kernel
+// (conv_halo.hip) spends as long in its prologue / epilogue as in its 9 MFMA steps. Here one
+// 4-wave workgroup per CU stays resident and walks output tiles of 256 pixels (whole image rows),
+// each wave owning all 64 output channels x 64 pixels:
+//   * the whole filter (64 x 9 x 64 = 72 KB) is loaded ONCE per workgroup and stays in LDS as nine
+//     tap images (FWD: W rows, read with ds_read_b128; DGRAD: W^T, read with ds_read_b64_tr_b16);
+//     with two 43 KB halo buffers beside it the workgroup uses 158 KB, one per CU;
+//   * the zero-padded input halo of the NEXT tile is DMA'd into the other LDS buffer while the
+//     current tile runs its 9 taps x 2 k-steps of MFMAs with no barrier in between;
+//   * one barrier per tile; output stores are buffer stores (out-of-range lanes are dropped by
+//     the descriptor bound), so every wave issues the same count and the halo wait is a counted
+//     vmcnt that leaves the tile's stores in flight;
+//   * FWD accumulates the BN batch statistics of the bf16-rounded outputs in registers across
+//     all tiles of the workgroup and adds them to the fp64 slots once.
+// Halo layout, swizzle and DGRAD tap mirroring are those of conv_halo.hip.
+#include "common.h"
+#include "kernels.h"
+#include "tile_common.h"
+
+namespace dtc {
+
+__device__ __forceinline__ int c64_hswz(int r) { return ((r >> 1) & 3) << 1; }
+
+struct C64Params {
+  const u16* src;  // FWD: x, DGRAD: dy (NHWC, 64 channels)
+  const u16* w;    // KRSC [64][3][3][64]
+  u16* out;        // NHWC, 64 channels
+  const u16* res;  // DGRAD residual or null
+  double* stats;   // FWD BN statistics [SLOTS][2][64] or null
+  int N, H, W;
+  uint32_t src_bytes, out_bytes;
+  int rows, imgs, hb, nh, tiles_y, ntiles;
+  FastDiv fd_hb, fd_w2, fd_spx, fd_w;
+  u64* ts;
+};
+
+constexpr int C64_HCAP = 344;                 // halo rows per buffer: 43 DMA wave-instructions of 8 rows
+constexpr int C64_NHI = (C64_HCAP / 8 + 3) / 4;  // per wave (instruction ids wave + 4q < 43)
+constexpr int C64_HBYTES = C64_HCAP * 128;
+constexpr int C64_WBYTES = 9 * 8192;
+
+template <int MODE>
+__global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
+  constexpr int FM = 4, FN = 4;  // wave tile: 64 channels x 64 pixels
+  __shared__ __attribute__((aligned(1024))) char smem[C64_WBYTES + 2 * C64_HBYTES];
+  char* const halo = smem + C64_WBYTES;
+  stamp_start(p.ts);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wc = wave;
+  const int arow0 = 0, bcol0 = wc * 64;
+  const int lrow = lane >> 3, pc = lane & 7;
+  const int W2 = p.W + 2;
+  const int M = p.N * p.H * p.W;
+
+  // ---- filter -> LDS, once: nine tap images of 64 rows x 128 B (read as MFMA A fragments per tap)
+#pragma unroll
+  for (int q = 0; q < 18; ++q) {
+    const int g = wave + 4 * q;  // 72 wave-instructions: tap g/8, row group g%8
+    const int tap = g >> 3, ia = g & 7, row = ia * 8 + lrow;
+    const u16* src = (MODE == 0) ? p.w + row * 576 + tap * 64 + (pc ^ rowswz(row)) * 8
+                                 : p.w + row * 576 + (8 - tap) * 64 + (pc ^ trswz(row)) * 8;
+    glds16(src, smem + tap * 8192 + ia * 1024);
+  }
+  // ---- per-lane constants: B-fragment halo rows (tile independent), halo DMA row decomposition
+  const int spx = p.rows * p.W;
+  const int fpx = lane & 15;  // W >= 16: the 16 pixels of a fragment are contiguous in one image row
+  int hbr[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int l = bcol0 + j * 16 + fpx;
+    const int i = (int)fdiv((uint32_t)l, p.fd_spx), rem = l - i * spx;
+    const int y = (int)fdiv((uint32_t)rem, p.fd_w), x = rem - y * p.W;
+    hbr[j] = i * p.hb + y * W2 + x;
+  }
+  auto stage_halo = [&](char* dst, int tile) {
+    int n0, y0;
+    if (p.imgs == 1) {
+      n0 = (int)((unsigned)tile / (unsigned)p.tiles_y);
+      y0 = (tile - n0 * p.tiles_y) * p.rows;
+    } else {
+      n0 = tile * p.imgs;
+      y0 = 0;
+    }
+#pragma unroll
+    for (int q = 0; q < C64_NHI; ++q) {
+      const int g = wave + 4 * q;
+      if (g >= C64_HCAP / 8) break;
+      const int hr = g * 8 + lrow;
+      const int i = (int)fdiv((uint32_t)hr, p.fd_hb), rem = hr - i * p.hb;
+      const int hy = (int)fdiv((uint32_t)rem, p.fd_w2), hx = rem - hy * W2;
+      const int n = n0 + i, y = y0 + hy - 1, x = hx - 1;
+      const bool ok = hr < p.nh && n < p.N && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+      const uint32_t off = ok ? (uint32_t)((((n * p.H + y) * p.W + x) * 64 + (pc ^ c64_hswz(hr)) * 8) * 2) : 0x80000000u;
+      buf_lds16(p.src, p.src_bytes, dst + g * 1024, off);
+    }
+  };
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.out, 0, p.out_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.res ? p.res : p.out), 0, p.res ? p.out_bytes : 0, 0x00020000);
+
+  const int rq = (lane >> 4) * 4;
+  float ssum[FM][4], ssq[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) ssum[i][t] = ssq[i][t] = 0.f;
+
+  int k = 0;
+  int tile = blockIdx.x;
+  if (tile < p.ntiles) stage_halo(halo, tile);
+  for (; tile < p.ntiles; tile += gridDim.x, ++k) {
+    // this tile's halo has landed (the previous tile's FM*FN stores may still be in flight)
+    if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // FM*FN stores of the previous tile
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* hbuf = halo + (k & 1) * C64_HBYTES;
+    const int tn = tile + gridDim.x;
+    if (tn < p.ntiles) stage_halo(halo + ((k + 1) & 1) * C64_HBYTES, tn);
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int toff = (t / 3) * W2 + (t % 3);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          af[i] = (MODE == 0) ? frag_row(smem + t * 8192, arow0 + i * 16, ks, lane)
+                              : frag_tr(smem + t * 8192, arow0 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = hbr[j] + toff;
+          const int ch = (ks * 4 + (lane >> 4)) ^ c64_hswz(row);
+          bfr[j] = __builtin_bit_cast(bf16x8, *(const uint4*)(hbuf + row * 128 + (ch << 4)));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+
+    // epilogue: exactly FM*FN buffer stores per wave (rows past M are dropped by the bound)
+    const int px0 = tile * 256;  // tiles are 256 consecutive pixels
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int pix = px0 + bcol0 + j * 16 + fpx;
+      const bool ok = pix < M;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ch = arow0 + i * 16 + rq;
+        const uint32_t off = ok ? (uint32_t)((pix * 64 + ch) * 2) : 0x80000000u;
+        float v[4];
+        if constexpr (MODE == 0) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            v[t] = round_bf(acc[i][j][t]);
+            if (ok) {
+              ssum[i][t] += v[t];
+              ssq[i][t] += v[t] * v[t];
+            }
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] = acc[i][j][t];
+          if (p.res) {
+            typedef int i32x2 __attribute__((ext_vector_type(2)));
+            const i32x2 rr = __builtin_amdgcn_raw_buffer_load_b64(rrsrc, off, 0, 0);
+            v[0] += bf_lo((uint32_t)rr.x); v[1] += bf_hi((uint32_t)rr.x);
+            v[2] += bf_lo((uint32_t)rr.y); v[3] += bf_hi((uint32_t)rr.y);
+          }
+        }
+        typedef int i32x2 __attribute__((ext_vector_type(2)));
+        i32x2 wv;
+        wv.x = (int)pack_bf2(v[0], v[1]);
+        wv.y = (int)pack_bf2(v[2], v[3]);
+        __builtin_amdgcn_raw_buffer_store_b64(wv, orsrc, off, 0, 0);
+      }
+    }
+  }
+
+  if constexpr (MODE == 0) {
+    if (p.stats != nullptr) {  // per-channel sums of this workgroup -> fp64 slot (once per workgroup)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      float* red = (float*)halo;  // [4 waves][64 ch][2]
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float s = row16_sum(ssum[i][t]), q = row16_sum(ssq[i][t]);
+          if ((lane & 15) == 0) {
+            const int ch = arow0 + i * 16 + rq + t;
+            red[(wc * 64 + ch) * 2 + 0] = s;
+            red[(wc * 64 + ch) * 2 + 1] = q;
+          }
+        }
+      __syncthreads();
+      if (threadIdx.x < 64) {
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          s += red[(w * 64 + threadIdx.x) * 2 + 0];
+          q += red[(w * 64 + threadIdx.x) * 2 + 1];
+        }
+        double* st = p.stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * 64;
+        unsafeAtomicAdd(st + threadIdx.x, (double)s);
+        unsafeAtomicAdd(st + 64 + threadIdx.x, (double)q);
+      }
+    }
+  }
+  stamp_end(p.ts);
+}
+
+// ---------------------------------------------------------------- host side
+bool conv_c64_ok(const ConvShape& s) {
+  if (option_get(OPT_CONV_C64) == 0) return false;
+  if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.C == 64 && s.K == 64)) return false;
+  if (s.W < 16 || 256 % s.W != 0) return false;  // fragments of 16 contiguous pixels in one image row
+  const int hw = s.H * s.W;
+  int rows, imgs;
+  if (hw >= 256) {
+    rows = 256 / s.W;
+    if (s.H % rows) return false;
+    imgs = 1;
+  } else {
+    if (256 % hw) return false;
+    imgs = 256 / hw;
+    rows = s.H;
+  }
+  const int nh = imgs * (rows + 2) * (s.W + 2);
+  const int64_t M = (int64_t)s.N * hw;
+  return nh <= C64_HCAP && M % 256 == 0 && M * 128 < (1ll << 31);
+}
+
+int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, double* stats,
+             hipStream_t st, u64* ts) {
+  DTC_CHECK_ARG(conv_c64_ok(s) && (mode == CONV_FWD || mode == CONV_DGRAD), "conv_c64: unsupported shape");
+  C64Params p{};
+  p.src = src; p.w = w; p.out = out; p.res = res; p.stats = stats;
+  p.N = s.N; p.H = s.H; p.W = s.W;
+  const int hw = s.H * s.W;
+  if (hw >= 256) {
+    p.rows = 256 / s.W;
+    p.imgs = 1;
+  } else {
+    p.imgs = 256 / hw;
+    p.rows = s.H;
+  }
+  p.hb = (p.rows + 2) * (s.W + 2);
+  p.nh = p.imgs * p.hb;
+  p.tiles_y = s.H / p.rows;
+  const int64_t M = (int64_t)s.N * hw;
+  p.ntiles = (int)(M / 256);
+  p.src_bytes = (uint32_t)(M * 128);
+  p.out_bytes = (uint32_t)(M * 128);
+  p.fd_hb = make_fastdiv(p.hb);
+  p.fd_w2 = make_fastdiv(s.W + 2);
+  p.fd_spx = make_fastdiv(p.rows * s.W);
+  p.fd_w = make_fastdiv(s.W);
+  p.ts = ts;
+  const int grid = std::min(p.ntiles, 256);
+  if (mode == CONV_FWD)
+    hipLaunchKernelGGL(conv_c64_kernel<0>, dim3(grid), dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL(conv_c64_kernel<1>, dim3(grid), dim3(256), 0, st, p);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace dtc

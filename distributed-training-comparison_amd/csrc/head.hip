@@ -204,6 +204,13 @@ __global__ void __launch_bounds__(256) head_bwd_w_partial_kernel(const float* __
       if (j < ncls) part[((int64_t)blockIdx.z * ncls + j) * C + c] = acc[q];
     }
   }
+  // bias partial of this image block (the c-tile 0 workgroups): one thread per class
+  if (blockIdx.x == 0 && t < 16) {
+    const int j = blockIdx.y * 16 + t;
+    float b = 0.f;
+    for (int i = 0; i < nn; ++i) b += dls[i][t];
+    if (j < ncls) part[(int64_t)gridDim.z * ncls * C + (int64_t)blockIdx.z * ncls + j] = b;
+  }
 }
 
 // Stage 2: fixed-order sum over splits; thread per (j, c); db by the c == 0 threads.
@@ -217,15 +224,16 @@ __global__ void __launch_bounds__(256) head_bwd_w_reduce_kernel(const float* __r
   for (int s = 0; s < splits; ++s) a += part[(int64_t)s * ncls * C + i];
   dw[i] = a * scale;
   const int64_t j = i / C, c = i - j * C;
-  if (c == 0) {
+  if (c == 0) {  // bias: fixed-order sum of the per-image-block partials
+    const float* pb = part + (int64_t)splits * ncls * C;
     float b = 0.f;
-    for (int n = 0; n < N; ++n) b += dl[(int64_t)n * ncls + j];
+    for (int s = 0; s < splits; ++s) b += pb[(int64_t)s * ncls + j];
     db[j] = b * scale;
   }
 }
 
 size_t head_bwd_workspace(int N, int C, int ncls) {
-  return (size_t)((N + HB_IMGS - 1) / HB_IMGS) * ncls * C * sizeof(float);
+  return (size_t)((N + HB_IMGS - 1) / HB_IMGS) * ncls * (C + 1) * sizeof(float);
 }
 
 // dact[n][p][c] = (sum_j dl[n][j] * W[j][c]) / HW

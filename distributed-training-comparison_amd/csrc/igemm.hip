@@ -702,6 +702,7 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
 
 int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
              size_t slab_bytes, hipStream_t st, u64* ts) {
+  if (conv_c64_ok(s)) return conv_c64(s, CONV_FWD, x, w, y, nullptr, stats, st, ts);
   {
     const HaloPlan hp = conv_halo_plan(s, CONV_FWD);
     if (hp.cfg >= 0) return conv_halo(s, CONV_FWD, hp, x, w, y, nullptr, stats, slab, slab_bytes, st, ts);
@@ -734,6 +735,7 @@ int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* sta
 
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
                size_t slab_bytes, hipStream_t st, u64* ts) {
+  if (conv_c64_ok(s)) return conv_c64(s, CONV_DGRAD, dy, w, dx, res, nullptr, st, ts);
   {
     const HaloPlan hp = conv_halo_plan(s, CONV_DGRAD);
     if (hp.cfg >= 0) return conv_halo(s, CONV_DGRAD, hp, dy, w, dx, res, nullptr, slab, slab_bytes, st, ts);
@@ -831,8 +833,8 @@ int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const 
   DTC_CHECK_ARG(Nc % 8 == 0 && Nc <= 2048, "splitk_reduce: channels %d", Nc);
   const int tpr = Nc / 8;
   const int rpp = 256 / tpr;
-  // about 1024 workgroups; each a whole number of 256-thread passes
-  int rows_per_block = std::max(rpp, (M + 1023) / 1024);
+  // 256..1024 workgroups of >= 16K outputs where the tensor allows; whole 256-thread passes
+  int rows_per_block = std::max({rpp, (M + 1023) / 1024, std::min((16384 + Nc - 1) / Nc, (M + 255) / 256)});
   rows_per_block = ((rows_per_block + rpp - 1) / rpp) * rpp;
   const int blocks = ceil_div(M, rows_per_block);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, splits, M, Nc, out, res, stats,

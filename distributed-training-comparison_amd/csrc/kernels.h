@@ -18,6 +18,9 @@ enum {
   OPT_WGRAD_HALO = 5,  // target workgroup count of the halo WGRAD kernel (0 = generic loader only)
   OPT_HALO_CONV = 6,   // halo FWD/DGRAD for 3x3 s1: 0 off, 1 auto, 2+k force configuration k (tuning)
   OPT_HALO_SPLIT = 7,  // halo FWD/DGRAD split-K over reduction chunks: 0 auto, k forced
+  OPT_BWD_STREAMS = 8,  // 1: weight gradients on a side stream, overlapped with the dgrad/BN chain
+                        // (off by default: measured 5% slower at B=256, both chains fill the CUs)
+  OPT_CONV_C64 = 9,     // persistent 64->64 channel 3x3 conv (conv_c64.hip) for layer1 FWD/DGRAD
   OPT_COUNT
 };
 int option_get(int id);
@@ -56,6 +59,10 @@ int conv_wgrad_halo(const ConvShape& s, const u16* x, const u16* dy, float* slab
                     hipStream_t st, u64* ts);
 // Halo-tiled 3x3 / stride 1 FWD and DGRAD (conv_halo.hip): configuration for the pass (-1: not
 // applicable), and the launch (FWD: stats optional; DGRAD: res optional).
+// Persistent 64-channel 3x3 stride-1 FWD / DGRAD (conv_c64.hip).
+bool conv_c64_ok(const ConvShape& s);
+int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, double* stats,
+             hipStream_t st, u64* ts);
 struct HaloPlan {
   int cfg, split;
 };

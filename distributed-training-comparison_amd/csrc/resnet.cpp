@@ -55,6 +55,7 @@ struct BlockL {
   bool proj = false;
   int Cin = 0, Cout = 0, Hin = 0, Win = 0, Hout = 0, Wout = 0;
   size_t C1 = 0, A1 = 0, C2 = 0, S = 0, OUT = 0;  // activation buffers (workspace byte offsets)
+  size_t DC2 = 0, DC1 = 0, DSC = 0;  // backward: conv-output gradients read by the (side-stream) wgrads
   int64_t grad_hi = 0;  // end of this block's flat region: after its backward, [0, grad_hi) is complete
 };
 
@@ -72,6 +73,13 @@ struct Net {
   size_t ws_bytes = 0;
   size_t X0 = 0, WSTEM = 0, C0 = 0, A0 = 0, FEAT = 0, G[6] = {0, 0, 0, 0, 0, 0}, SLAB = 0;
   size_t HEADWS = 0, HEADWS_bytes = 0;
+  size_t DC0 = 0, SLABW = 0;  // stem conv-output gradient; split-K slab of the side-stream wgrads
+  // backward weight gradients run on a side stream (option bwd_streams), overlapped with the
+  // data-gradient / BN chain; forked after the conv-output gradient exists, joined at bucket points
+  hipStream_t side_st = nullptr;
+  std::vector<hipEvent_t> evs;
+  int ev_next = 0;
+  bool side_pending = false;
   size_t slab_bytes = 0;
   size_t stats_lo = 0, stats_hi = 0;  // region that must start zeroed
   // buckets: [offset, numel) in flat elements, and the block index after whose backward it fires
@@ -282,6 +290,13 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.HEADWS = take(n.HEADWS_bytes);
   n.acts.push_back({"head.feat_f32", n.FEAT, (int)B, 1, 1, 512});
   for (int i = 0; i < 6; ++i) n.G[i] = take(gmax * 2);
+  for (auto& b : n.blocks) {  // per-block, so a pending side-stream wgrad never sees them overwritten
+    const size_t bytes = (size_t)B * b.Hout * b.Wout * b.Cout * 2;
+    b.DC2 = take(bytes);
+    b.DC1 = take(bytes);
+    if (b.proj) b.DSC = take(bytes);
+  }
+  n.DC0 = take(M0 * 64 * 2);
   // BN per-layer state
   n.stats_lo = off;
   for (BNL* b : n.bns) {
@@ -309,6 +324,7 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   }
   n.slab_bytes = slab;
   n.SLAB = take(slab);
+  n.SLABW = take(slab);
   if (n.capture) {
     auto cap = [&](const std::string& nm, int h, int w, int c) {
       n.caps.push_back({nm, take((size_t)B * h * w * c * 2), (int)B, h, w, c});
@@ -483,12 +499,14 @@ struct BwdCtx {
   bool capturing = false;
   std::vector<Net::Seg>* segs = nullptr;
 };
+static int join_side(Net& n, hipStream_t st);
 static int maybe_bucket(Net& n, int after_block, const BwdCtx& cx, hipStream_t st) {
   if (!cx.comm) return 0;
   std::vector<int> ids;
   for (size_t i = 0; i < n.bucket_off.size(); ++i)
     if (n.bucket_after_block[i] == after_block) ids.push_back((int)i);
   if (ids.empty()) return 0;
+  DTC_TRY(join_side(n, st));  // the bucket's weight gradients come from the side stream
   if (!cx.capturing) {
     for (int i : ids) DTC_TRY(comm_allreduce_async(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st));
     return 0;
@@ -510,11 +528,50 @@ static int cap(Net& n, const std::string& name, const void* src, hipStream_t st)
   return set_error(DTC_EINVAL, "capture slot %s missing", name.c_str());
 }
 
+// Side stream for the weight gradients (fork after their input gradient exists, join before
+// anything reads the weight gradients: bucket all-reduces and the end of backward).
+static bool side_on(const Net& n) { return option_get(OPT_BWD_STREAMS) != 0; }
+static int next_event(Net& n, hipEvent_t* ev) {
+  if (n.evs.empty()) {
+    n.evs.resize(64);
+    for (auto& e : n.evs) DTC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  *ev = n.evs[n.ev_next];
+  n.ev_next = (n.ev_next + 1) % (int)n.evs.size();
+  return 0;
+}
+static int fork_side(Net& n, hipStream_t st, hipStream_t* out) {
+  if (!side_on(n)) {
+    *out = st;
+    return 0;
+  }
+  if (!n.side_st) DTC_HIP(hipStreamCreateWithFlags(&n.side_st, hipStreamNonBlocking));
+  hipEvent_t ev;
+  DTC_TRY(next_event(n, &ev));
+  DTC_HIP(hipEventRecord(ev, st));
+  DTC_HIP(hipStreamWaitEvent(n.side_st, ev, 0));
+  n.side_pending = true;
+  *out = n.side_st;
+  return 0;
+}
+static int join_side(Net& n, hipStream_t st) {
+  if (!n.side_pending) return 0;
+  hipEvent_t ev;
+  DTC_TRY(next_event(n, &ev));
+  DTC_HIP(hipEventRecord(ev, n.side_st));
+  DTC_HIP(hipStreamWaitEvent(st, ev, 0));
+  n.side_pending = false;
+  return 0;
+}
+
 static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& cx, hipStream_t st) {
   n.prof_next = Net::PROF_BWD0;
+  n.ev_next = 0;
   u16* G[6];
   for (int i = 0; i < 6; ++i) G[i] = n.at<u16>(n.G[i]);
   float* slab = n.at<float>(n.SLAB);
+  float* slabw = n.at<float>(n.SLABW);
+  hipStream_t sd = st;  // weight-gradient stream
   const BlockL& last = n.blocks.back();
   DTC_TRY(head_bwd(dlogits, n.at<float>(n.FEAT), n.wbf(n.fc_w), n.B, last.Hout * last.Wout, 512, n.ncls, gs,
                    n.gf(n.fc_w), n.gf(n.fc_b), G[0], n.at<float>(n.HEADWS), n.HEADWS_bytes, st));
@@ -522,6 +579,9 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
     BlockL& b = n.blocks[bi];
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
     const u16* in = bi > 0 ? n.at<u16>(n.blocks[bi - 1].OUT) : n.at<u16>(n.A0);
+    u16* dc2 = n.at<u16>(b.DC2);
+    u16* dc1 = n.at<u16>(b.DC1);
+    u16* dsc = b.proj ? n.at<u16>(b.DSC) : nullptr;
     const std::string cp = n.capture ? "grad.layer" + std::to_string(bi / 2 + 1) + "." + std::to_string(bi % 2) : "";
     DTC_TRY(cap(n, cp + ".dy", G[0], st));
     // out = relu(bn2(c2) + shortcut): dz = dy * [out > 0]
@@ -536,14 +596,15 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
       DTC_TRY(bn_bwd_finalize(n.at<double>(b.bsc.acc), b.Cout, M, n.pf(b.bsc.gidx), n.at<float>(b.bsc.mean),
                               n.at<float>(b.bsc.invstd), gs, n.gf(b.bsc.gidx), n.gf(b.bsc.bidx),
                               n.at<float>(b.bsc.coef), st));
-    DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(b.C2), n.at<float>(b.b2.coef), G[2], b.proj ? n.at<u16>(b.S) : nullptr,
-                         b.proj ? n.at<float>(b.bsc.coef) : nullptr, b.proj ? G[3] : nullptr, M, b.Cout, st));
+    DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(b.C2), n.at<float>(b.b2.coef), dc2, b.proj ? n.at<u16>(b.S) : nullptr,
+                         b.proj ? n.at<float>(b.bsc.coef) : nullptr, dsc, M, b.Cout, st));
     DTC_TRY(cap(n, cp + ".dz", G[1], st));
-    DTC_TRY(cap(n, cp + ".dc2", G[2], st));
-    if (b.proj) DTC_TRY(cap(n, cp + ".ds", G[3], st));
-    // conv2: dW2 and da1
-    PROF(2, conv_flops(b.c2.s), conv_wgrad(b.c2.s, n.at<u16>(b.A1), G[2], n.gf(b.c2.pidx), 0, 0, gs, slab, n.slab_bytes, st, ts));
-    PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, G[2], n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts));
+    DTC_TRY(cap(n, cp + ".dc2", dc2, st));
+    if (b.proj) DTC_TRY(cap(n, cp + ".ds", dsc, st));
+    // conv2: dW2 (side stream) and da1
+    DTC_TRY(fork_side(n, st, &sd));
+    PROF(2, conv_flops(b.c2.s), conv_wgrad(b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+    PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts));
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
     // a1 = relu(bn1(c1))
     DTC_TRY(bn_bwd_reduce(G[4], n.at<u16>(b.A1), n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
@@ -552,17 +613,17 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
                             n.at<float>(b.b1.invstd), gs, n.gf(b.b1.gidx), n.gf(b.b1.bidx), n.at<float>(b.b1.coef),
                             st));
     DTC_TRY(cap(n, cp + ".dz1", G[4], st));
-    DTC_TRY(bn_bwd_apply(G[4], n.at<u16>(b.C1), n.at<float>(b.b1.coef), G[2], nullptr, nullptr, nullptr, M, b.Cout,
-                         st));
-    DTC_TRY(cap(n, cp + ".dc1", G[2], st));
-    // conv1 (+ shortcut): weight grads, then the block-input gradient with the residual fused
-    PROF(2, conv_flops(b.c1.s), conv_wgrad(b.c1.s, in, G[2], n.gf(b.c1.pidx), 0, 0, gs, slab, n.slab_bytes, st, ts));
+    DTC_TRY(bn_bwd_apply(G[4], n.at<u16>(b.C1), n.at<float>(b.b1.coef), dc1, nullptr, nullptr, nullptr, M, b.Cout, st));
+    DTC_TRY(cap(n, cp + ".dc1", dc1, st));
+    // conv1 (+ shortcut): weight grads (side stream), then the block-input gradient with the residual fused
+    DTC_TRY(fork_side(n, st, &sd));
+    PROF(2, conv_flops(b.c1.s), conv_wgrad(b.c1.s, in, dc1, n.gf(b.c1.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
     if (b.proj) {
-      PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, G[3], n.gf(b.sc.pidx), 0, 0, gs, slab, n.slab_bytes, st, ts));
-      PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, G[3], n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
-      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts));
+      PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+      PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts));
     } else {
-      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, G[2], n.wbf(b.c1.pidx), G[0], G[1], slab, n.slab_bytes, st, ts));
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[1], slab, n.slab_bytes, st, ts));
     }
     if (b.proj) DTC_TRY(cap(n, cp + ".dxs", G[5], st));
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
@@ -570,16 +631,18 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   }
   // stem: a0 = relu(bn1(conv1(x)))
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
+  u16* dc0 = n.at<u16>(n.DC0);
   DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(n.A0), n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
                         n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, G[1], M0, 64, st));
   DTC_TRY(bn_bwd_finalize(n.at<double>(n.bn0.acc), 64, M0, n.pf(n.bn0.gidx), n.at<float>(n.bn0.mean),
                           n.at<float>(n.bn0.invstd), gs, n.gf(n.bn0.gidx), n.gf(n.bn0.bidx), n.at<float>(n.bn0.coef),
                           st));
-  DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(n.C0), n.at<float>(n.bn0.coef), G[2], nullptr, nullptr, nullptr, M0, 64, st));
+  DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(n.C0), n.at<float>(n.bn0.coef), dc0, nullptr, nullptr, nullptr, M0, 64, st));
   DTC_TRY(cap(n, "grad.stem.dz", G[1], st));
-  DTC_TRY(cap(n, "grad.stem.dc", G[2], st));
+  DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
+  DTC_TRY(join_side(n, st));  // the stem wgrad is the last kernel: run it on the main stream
   PROF(2, 2.0 * M0 * 64 * 27,
-       conv_wgrad(n.stem.s, n.at<u16>(n.X0), G[2], n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st, ts));
+       conv_wgrad(n.stem.s, n.at<u16>(n.X0), dc0, n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st, ts));
   DTC_TRY(maybe_bucket(n, -1, cx, st));
   if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
   return 0;
@@ -667,6 +730,9 @@ int dtc_rn18_destroy(dtc_net* net) {
   if (net) {
     drop_graphs(net->n);
     if (net->n.cap_st) (void)hipStreamDestroy(net->n.cap_st);
+    if (net->n.side_st) (void)hipStreamDestroy(net->n.side_st);
+    for (auto& e : net->n.evs)
+      if (e) (void)hipEventDestroy(e);
     prof_free(net->n);
   }
   delete net;

@@ -5,12 +5,29 @@
 
 namespace dtc {
 
+// LDS-DMA (16 B per lane, lane-linear LDS destination at a wave-uniform base) is issued through
+// inline asm on purpose. With the builtins, hipcc treats the DMA as a pending write to LDS and
+// emits `s_waitcnt vmcnt(0)` before the next ds_read of ANY LDS buffer, i.e. it drains the
+// prefetch of step k+1 before the MFMAs of step k can read their operands (measured in the .s of
+// every pipelined kernel here). hipcc neither counts nor waits for an asm DMA: completion is each
+// kernel's own counted `s_waitcnt vmcnt(N)` followed by an s_barrier before the data is read.
+// M0 (the DMA's LDS base) is compiler-reserved: saved and restored inside the same statement.
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 // 16-byte LDS-DMA through a buffer descriptor over [base, base + bytes): an offset outside the
-// range loads zeros. (Kept out of the loader lambda: the buffer builtins inside a lambda make the
-// host pass drop the kernel's launch stub.)
+// range loads zeros.
 __device__ __forceinline__ void buf_lds16(const void* base, uint32_t bytes, char* lds_dst, uint32_t off) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_dst, 16, off, 0, 0, 0);
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_u32(lds_dst));
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(off), "s"(r), "s"(dst)
+      : "memory");
 }
 
 // Call-timing stamps (kernel entry / exit only, one lane per workgroup; nothing on the loop).
@@ -35,8 +52,14 @@ __device__ __forceinline__ void stamp_end(u64* ts) {
 __device__ __forceinline__ int rowswz(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int trswz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
 
+// 16-byte LDS-DMA from a per-lane global address (global_load_lds_dwordx4).
 __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_u32(lds_wave_base));
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(dst)
+               : "memory");
 }
 
 // Row-image fragment: lane holds row (lane&15), reduction chunk (ks*4 + lane>>4).

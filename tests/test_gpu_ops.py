@@ -338,3 +338,50 @@ def test_conv_halo_configs(dtc, cuda, case, cfg, split):
     np.testing.assert_allclose(s[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
     ref = O.conv2d_dgrad(dy, w, (H, W), 1, 1) + res
     assert rel_err(dx.float().cpu().numpy(), ref) < 1e-2
+
+
+C64_CASES = [(2, 32, 32), (3, 16, 16), (5, 32, 32)]
+
+
+@pytest.mark.parametrize("case", C64_CASES)
+def test_conv_c64(dtc, cuda, case):
+    """Persistent 64->64 3x3 kernel (conv_c64.hip, layer1): FWD (+BN statistics accumulated per
+    workgroup across tiles) and DGRAD (+residual), with more tiles than workgroups for case 3."""
+    N, H, W = case
+    g = np.random.default_rng(31)
+    x = _rand_bf16((N, H, W, 64), g)
+    w = _rand_bf16((64, 3, 3, 64), g, 0.05)
+    dy = _rand_bf16((N, H, W, 64), g)
+    res = _rand_bf16((N, H, W, 64), g)
+    stats = dtc.ops.new_stats(64, cuda)
+    y = dtc.ops.conv2d_fwd(_to_dev_bf16(x, cuda), _to_dev_bf16(w, cuda), 1, 1, stats=stats)
+    dx = dtc.ops.conv2d_dgrad(_to_dev_bf16(dy, cuda), _to_dev_bf16(w, cuda), (H, W), 1, 1, res=_to_dev_bf16(res, cuda))
+    yk = y.float().cpu().numpy()
+    assert rel_err(yk, O.conv2d_fwd(x, w, 1, 1)) < 1e-2
+    s = stats.sum(0).cpu().numpy()
+    yb = yk.reshape(-1, 64).astype(np.float64)
+    np.testing.assert_allclose(s[0], yb.sum(0), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
+    assert rel_err(dx.float().cpu().numpy(), O.conv2d_dgrad(dy, w, (H, W), 1, 1) + res) < 1e-2
+
+
+def test_conv_c64_large_grid(dtc, cuda):
+    """More tiles than resident workgroups (1024 tiles / 256 workgroups at the bench shape's
+    layer1 geometry, batch 64 here): every tile of every workgroup's walk is computed, against
+    the implicit-GEMM kernel on the same operands (option conv_c64=0)."""
+    g = np.random.default_rng(32)
+    x = torch.from_numpy(_rand_bf16((300, 32, 32, 64), g)).to(cuda).bfloat16()
+    w = torch.from_numpy(_rand_bf16((64, 3, 3, 64), g, 0.05)).to(cuda).bfloat16()
+    y1 = dtc.ops.conv2d_fwd(x, w, 1, 1)
+    d1 = dtc.ops.conv2d_dgrad(x, w, (32, 32), 1, 1)
+    dtc._native.call("dtc_set_option", b"conv_c64", 0)
+    dtc._native.call("dtc_set_option", b"halo_conv", 0)
+    try:
+        y0 = dtc.ops.conv2d_fwd(x, w, 1, 1)
+        d0 = dtc.ops.conv2d_dgrad(x, w, (32, 32), 1, 1)
+    finally:
+        dtc._native.call("dtc_set_option", b"conv_c64", 1)
+        dtc._native.call("dtc_set_option", b"halo_conv", 1)
+    torch.cuda.synchronize()
+    assert rel_err(y1.float().cpu().numpy(), y0.float().cpu().numpy()) < 1e-2
+    assert rel_err(d1.float().cpu().numpy(), d0.float().cpu().numpy()) < 1e-2

@@ -264,6 +264,22 @@ def test_graph_replay_matches_eager(dtc, cuda):
         assert rel_err(bg[k], be[k]) < 1e-4, k
 
 
+@pytest.mark.parametrize("graphs", [True, False])
+def test_side_stream_wgrad_matches_serial(dtc, cuda, graphs):
+    """Weight gradients on the side stream (option bwd_streams=1; off by default), forked/joined by
+    events inside the (captured) backward, vs everything on one stream: the same kernels on the
+    same operands, so results agree up to the order of the fp64 BN-statistics atomics."""
+    lb, gb, pb, _ = _train_steps(dtc, cuda, 3, graphs=graphs)
+    dtc._native.lib.dtc_set_option(b"bwd_streams", 1)
+    try:
+        la, ga, pa, _ = _train_steps(dtc, cuda, 3, graphs=graphs)
+    finally:
+        dtc._native.lib.dtc_set_option(b"bwd_streams", 0)
+    np.testing.assert_allclose(la, lb, rtol=1e-4)
+    assert rel_err(ga, gb) < 1e-3
+    assert rel_err(pa, pb) < 1e-5
+
+
 def test_graph_recapture_on_option_change(dtc, cuda):
     """Options are baked into captured launches: changing one re-captures (results unchanged)."""
     model, _, x, y = _setup(dtc, cuda, 4, seed=6)
