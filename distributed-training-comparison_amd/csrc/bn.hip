@@ -196,6 +196,219 @@ int bn_apply_dual_relu(const u16* x, const float* s, const float* h, const u16* 
   return launch_apply<APPLY_DUAL_RELU>(x, s, h, x2, s2, h2, y, M, C, st);
 }
 
+// ------------------------------------------------------------------ fused finalize + apply (forward)
+// The consumer computes the BN coefficients itself: workgroup (pixel block, 64-channel group)
+// sums the DTC_STAT_SLOTS fp64 slots of its 64 channels (32 KB, L2-resident: every workgroup of
+// the launch reads the same lines) in a fixed order, then normalises its pixels. The first pixel
+// block of each channel group also writes the saved mean / invstd and the running statistics
+// (and num_batches_tracked once). Removes the separate finalize launch and its kernel boundary;
+// the slots are zeroed by a memset node at the start of the executor's forward.
+constexpr int FA_GROUP = 64;  // channels per workgroup
+
+__device__ __forceinline__ void fa_slot_sums(const double* __restrict__ st, int C, int cg, double* part, double& s,
+                                             double& q) {
+  const int t = threadIdx.x, cl = t & 63, g = t >> 6;  // 4 groups of 8 slots
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int j = 0; j < DTC_STAT_SLOTS / 4; ++j) {
+    const size_t k = (size_t)(g * (DTC_STAT_SLOTS / 4) + j);
+    a += st[k * 2 * C + cg + cl];
+    b += st[k * 2 * C + C + cg + cl];
+  }
+  part[(g * 2 + 0) * 64 + cl] = a;
+  part[(g * 2 + 1) * 64 + cl] = b;
+  __syncthreads();
+  s = q = 0.0;
+  if (t < 64) {
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      s += part[(gg * 2 + 0) * 64 + t];
+      q += part[(gg * 2 + 1) * 64 + t];
+    }
+  }
+}
+
+__device__ __forceinline__ void fa_fwd_coef(const BnFwdArgs& A, int C, int cg, double* part, float* sc, float* sh) {
+  double s, q;
+  fa_slot_sums(A.stats, C, cg, part, s, q);
+  const int t = threadIdx.x;
+  if (t < 64) {
+    const int c = cg + t;
+    const double cnt = (double)A.count;
+    const double mu = s / cnt;
+    double var = q / cnt - mu * mu;
+    if (var < 0.0) var = 0.0;
+    const float is = (float)(1.0 / sqrt(var + (double)A.eps));
+    const float a = A.gamma[c] * is;
+    sc[t] = a;
+    sh[t] = A.beta[c] - (float)mu * a;
+    if (blockIdx.x == 0) {
+      A.mean[c] = (float)mu;
+      A.invstd[c] = is;
+      if (A.rmean) {
+        const double unbiased = cnt > 1.0 ? var * cnt / (cnt - 1.0) : var;
+        A.rmean[c] = (float)((1.0 - A.momentum) * A.rmean[c] + A.momentum * mu);
+        A.rvar[c] = (float)((1.0 - A.momentum) * A.rvar[c] + A.momentum * unbiased);
+      }
+      if (t == 0 && blockIdx.y == 0 && A.nbt) *A.nbt += 1;
+    }
+  }
+  __syncthreads();
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) bn_fin_apply_kernel(const u16* __restrict__ x, const BnFwdArgs a1,
+                                                          const u16* __restrict__ x2, const BnFwdArgs a2,
+                                                          u16* __restrict__ y, int64_t M, int C, int rows) {
+  __shared__ double part[4 * 2 * 64];
+  __shared__ float coef[4][64];  // scale1, shift1, scale2, shift2
+  const int cg = blockIdx.y * FA_GROUP;
+  fa_fwd_coef(a1, C, cg, part, coef[0], coef[1]);
+  if constexpr (MODE == APPLY_DUAL_RELU) fa_fwd_coef(a2, C, cg, part, coef[2], coef[3]);
+  const int t = threadIdx.x, q8 = (t & 7) * 8, pr = t >> 3;
+  float sc[8], sh[8], sc2[8], sh2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = coef[0][q8 + k];
+    sh[k] = coef[1][q8 + k];
+    if constexpr (MODE == APPLY_DUAL_RELU) {
+      sc2[k] = coef[2][q8 + k];
+      sh2[k] = coef[3][q8 + k];
+    }
+  }
+  const int64_t m0 = (int64_t)blockIdx.x * rows, m1 = std::min<int64_t>(M, m0 + rows);
+  for (int64_t m = m0 + pr; m < m1; m += 32) {
+    const int64_t o = m * C + cg + q8;
+    float a[8], r[8], v[8];
+    unpack8(*(const uint4*)(x + o), a);
+    if constexpr (MODE != APPLY_RELU) unpack8(*(const uint4*)(x2 + o), r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = a[k] * sc[k] + sh[k];
+      // torch rounds each BN output to bf16 before the residual add (autocast)
+      if constexpr (MODE == APPLY_ADD_RELU) v[k] = round_bf(v[k]) + r[k];
+      if constexpr (MODE == APPLY_DUAL_RELU) v[k] = round_bf(v[k]) + round_bf(r[k] * sc2[k] + sh2[k]);
+      v[k] = fmaxf(v[k], 0.f);
+    }
+    *(uint4*)(y + o) = pack8(v);
+  }
+}
+
+static void fa_grid(int64_t M, int C, int& nblk, int& rows) {
+  const int groups = C / FA_GROUP;
+  nblk = std::max(1, 1024 / groups);
+  rows = (int)((M + nblk - 1) / nblk);
+  rows = std::max(32, (rows + 31) / 32 * 32);
+  nblk = (int)((M + rows - 1) / rows);
+}
+
+int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, const BnFwdArgs* a2, u16* y, int64_t M,
+                 int C, hipStream_t st) {
+  DTC_CHECK_ARG(x && y && a1.stats && a1.gamma && a1.beta && a1.mean && a1.invstd && C % FA_GROUP == 0 && M > 0,
+                "bn_fin_apply: bad args (C=%d)", C);
+  int nblk, rows;
+  fa_grid(M, C, nblk, rows);
+  const dim3 grid(nblk, C / FA_GROUP);
+  const BnFwdArgs none{};
+  switch (mode) {
+    case APPLY_RELU:
+      hipLaunchKernelGGL(bn_fin_apply_kernel<APPLY_RELU>, grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows);
+      break;
+    case APPLY_ADD_RELU:
+      DTC_CHECK_ARG(x2 != nullptr, "bn_fin_apply: residual required");
+      hipLaunchKernelGGL(bn_fin_apply_kernel<APPLY_ADD_RELU>, grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows);
+      break;
+    default:
+      DTC_CHECK_ARG(x2 && a2 && a2->stats, "bn_fin_apply: second branch required");
+      hipLaunchKernelGGL(bn_fin_apply_kernel<APPLY_DUAL_RELU>, grid, dim3(256), 0, st, x, a1, x2, *a2, y, M, C, rows);
+      break;
+  }
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+// ------------------------------------------------------------------ fused finalize + apply (backward)
+// dx = A*dz + B*x + Cc with the coefficients computed per workgroup from the fp64 slots of
+// sum(dz), sum(dz*xhat); the first pixel block writes dgamma / dbeta (x gscale).
+__device__ __forceinline__ void fa_bwd_coef(const BnBwdArgs& A, int C, int cg, double* part, float* ca, float* cb,
+                                            float* cc) {
+  double sd, sx;
+  fa_slot_sums(A.acc, C, cg, part, sd, sx);
+  const int t = threadIdx.x;
+  if (t < 64) {
+    const int c = cg + t;
+    const double cnt = (double)A.count;
+    const double is = A.invstd[c];
+    const double a = (double)A.gamma[c] * is;
+    const double b = -a * is * sx / cnt;
+    ca[t] = (float)a;
+    cb[t] = (float)b;
+    cc[t] = (float)(-a * sd / cnt - b * (double)A.mean[c]);
+    if (blockIdx.x == 0) {
+      if (A.dgamma) A.dgamma[c] = (float)(sx * A.gscale);
+      if (A.dbeta) A.dbeta[c] = (float)(sd * A.gscale);
+    }
+  }
+  __syncthreads();
+}
+
+template <bool DUAL>
+__global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const u16* __restrict__ dz, const u16* __restrict__ x1,
+                                                              const BnBwdArgs a1, u16* __restrict__ dx1,
+                                                              const u16* __restrict__ x2, const BnBwdArgs a2,
+                                                              u16* __restrict__ dx2, int64_t M, int C, int rows) {
+  __shared__ double part[4 * 2 * 64];
+  __shared__ float coef[6][64];
+  const int cg = blockIdx.y * FA_GROUP;
+  fa_bwd_coef(a1, C, cg, part, coef[0], coef[1], coef[2]);
+  if constexpr (DUAL) fa_bwd_coef(a2, C, cg, part, coef[3], coef[4], coef[5]);
+  const int t = threadIdx.x, q8 = (t & 7) * 8, pr = t >> 3;
+  float A1[8], B1[8], C1[8], A2[8], B2[8], C2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    A1[k] = coef[0][q8 + k]; B1[k] = coef[1][q8 + k]; C1[k] = coef[2][q8 + k];
+    if constexpr (DUAL) {
+      A2[k] = coef[3][q8 + k]; B2[k] = coef[4][q8 + k]; C2[k] = coef[5][q8 + k];
+    }
+  }
+  const int64_t m0 = (int64_t)blockIdx.x * rows, m1 = std::min<int64_t>(M, m0 + rows);
+  for (int64_t m = m0 + pr; m < m1; m += 32) {
+    const int64_t o = m * C + cg + q8;
+    float d[8], a[8], v[8];
+    unpack8(*(const uint4*)(dz + o), d);
+    unpack8(*(const uint4*)(x1 + o), a);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = A1[k] * d[k] + B1[k] * a[k] + C1[k];
+    *(uint4*)(dx1 + o) = pack8(v);
+    if constexpr (DUAL) {
+      unpack8(*(const uint4*)(x2 + o), a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = A2[k] * d[k] + B2[k] * a[k] + C2[k];
+      *(uint4*)(dx2 + o) = pack8(v);
+    }
+  }
+}
+
+int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
+                     u16* dx2, int64_t M, int C, hipStream_t st) {
+  DTC_CHECK_ARG(dz && x1 && dx1 && a1.acc && a1.gamma && a1.mean && a1.invstd && C % FA_GROUP == 0 && M > 0,
+                "bn_bwd_fin_apply: bad args (C=%d)", C);
+  int nblk, rows;
+  fa_grid(M, C, nblk, rows);
+  const dim3 grid(nblk, C / FA_GROUP);
+  if (x2) {
+    DTC_CHECK_ARG(a2 && a2->acc && dx2, "bn_bwd_fin_apply: dual branch args");
+    hipLaunchKernelGGL(bn_bwd_fin_apply_kernel<true>, grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, *a2, dx2, M, C,
+                       rows);
+  } else {
+    const BnBwdArgs none{};
+    hipLaunchKernelGGL(bn_bwd_fin_apply_kernel<false>, grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, none, dx2, M, C,
+                       rows);
+  }
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 // ------------------------------------------------------------------ backward
 template <bool MASK, bool DUAL>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(

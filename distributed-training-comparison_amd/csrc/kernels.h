@@ -21,6 +21,7 @@ enum {
   OPT_BWD_STREAMS = 8,  // 1: weight gradients on a side stream, overlapped with the dgrad/BN chain
                         // (off by default: measured 5% slower at B=256, both chains fill the CUs)
   OPT_CONV_C64 = 9,     // persistent 64->64 channel 3x3 conv (conv_c64.hip) for layer1 FWD/DGRAD
+  OPT_BN_FUSED_FIN = 10,  // 1: BN coefficients computed by the apply kernels (no finalize launches)
   OPT_COUNT
 };
 int option_get(int id);
@@ -93,6 +94,37 @@ int bn_apply_dual_relu(const u16* x, const float* scale, const float* shift, con
                        const float* shift2, u16* y, int64_t M, int C, hipStream_t st);
 // y = x*scale + shift (no activation; eval helpers / tests)
 int bn_apply(const u16* x, const float* scale, const float* shift, u16* y, int64_t M, int C, hipStream_t st);
+
+// Fused finalize + apply: the coefficients are computed by the consumer from the fp64 slots
+// (bn.hip); the first pixel block writes the saved / running statistics (forward) or dgamma /
+// dbeta (backward). The slots must be zeroed before their producers run (executor: memset node).
+struct BnFwdArgs {
+  const double* stats = nullptr;  // [SLOTS][2][C] sum, sum of squares of the bf16 conv output
+  int64_t count = 0;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  float* rmean = nullptr;
+  float* rvar = nullptr;
+  int64_t* nbt = nullptr;
+  float momentum = 0.1f, eps = 1e-5f;
+  float* mean = nullptr;    // saved for backward
+  float* invstd = nullptr;
+};
+struct BnBwdArgs {
+  const double* acc = nullptr;  // [SLOTS][2][C] sum(dz), sum(dz*xhat)
+  int64_t count = 0;
+  const float* gamma = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  float gscale = 1.f;
+  float* dgamma = nullptr;
+  float* dbeta = nullptr;
+};
+// mode: 1 relu, 2 add residual x2 + relu, 3 dual BN (x2 normalised by a2) + relu
+int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, const BnFwdArgs* a2, u16* y, int64_t M,
+                 int C, hipStream_t st);
+int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
+                     u16* dx2, int64_t M, int C, hipStream_t st);
 
 // backward: dz = dy * [y > 0] (mask optional); accumulates sum(dz), sum(dz*xhat1) [, sum(dz*xhat2)]
 int bn_bwd_reduce(const u16* dy, const u16* ymask, const u16* x1, const float* mean1, const float* invstd1,

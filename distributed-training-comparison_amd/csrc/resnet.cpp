@@ -81,7 +81,7 @@ struct Net {
   int ev_next = 0;
   bool side_pending = false;
   size_t slab_bytes = 0;
-  size_t stats_lo = 0, stats_hi = 0;  // region that must start zeroed
+  size_t stats_lo = 0, acc_lo = 0, stats_hi = 0;  // BN slot regions [stats_lo, acc_lo), [acc_lo, stats_hi)
   // buckets: [offset, numel) in flat elements, and the block index after whose backward it fires
   std::vector<int64_t> bucket_off, bucket_len;
   std::vector<int> bucket_after_block;  // -1 = after the stem (last)
@@ -298,11 +298,10 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   }
   n.DC0 = take(M0 * 64 * 2);
   // BN per-layer state
-  n.stats_lo = off;
-  for (BNL* b : n.bns) {
-    b->stats = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
-    b->acc = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
-  }
+  n.stats_lo = off;  // forward statistics of every BN, then backward sums: each zeroed by one memset node
+  for (BNL* b : n.bns) b->stats = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
+  n.acc_lo = off;
+  for (BNL* b : n.bns) b->acc = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
   n.stats_hi = off;
   for (BNL* b : n.bns) {
     b->mean = take(b->C * 4);
@@ -433,18 +432,50 @@ static int bn_finalize_fwd(Net& n, BNL& b, int64_t count, bool train, hipStream_
                       n.at<float>(b.mean), n.at<float>(b.invstd), n.at<float>(b.scale), n.at<float>(b.shift), st);
 }
 
+static bool bn_fused() { return option_get(OPT_BN_FUSED_FIN) != 0; }
+
+static BnFwdArgs fwd_args(Net& n, BNL& b, int64_t count) {
+  BnFwdArgs a;
+  a.stats = n.at<double>(b.stats);
+  a.count = count;
+  a.gamma = n.pf(b.gidx);
+  a.beta = n.pf(b.bidx);
+  a.rmean = n.bufs + b.rm_off;
+  a.rvar = n.bufs + b.rv_off;
+  a.nbt = n.nbt ? n.nbt + b.nbt : nullptr;
+  a.mean = n.at<float>(b.mean);
+  a.invstd = n.at<float>(b.invstd);
+  return a;
+}
+
+// BN (+ residual / second BN) + ReLU after the producing conv(s): y = relu(bn(x) [+ x2 | + bn2(x2)])
+static int bn_act(Net& n, int mode, BNL& b, const u16* x, BNL* b2, const u16* x2, u16* y, int64_t M, bool train,
+                  hipStream_t st) {
+  if (train && bn_fused()) {
+    const BnFwdArgs a1 = fwd_args(n, b, M);
+    const BnFwdArgs a2 = b2 ? fwd_args(n, *b2, M) : BnFwdArgs{};
+    return bn_fin_apply(mode, x, a1, x2, b2 ? &a2 : nullptr, y, M, b.C, st);
+  }
+  DTC_TRY(bn_finalize_fwd(n, b, M, train, st));
+  if (b2) DTC_TRY(bn_finalize_fwd(n, *b2, M, train, st));
+  const float* s1 = n.at<float>(b.scale);
+  const float* h1 = n.at<float>(b.shift);
+  if (mode == 1) return bn_apply_relu(x, s1, h1, y, M, b.C, st);
+  if (mode == 2) return bn_apply_add_relu(x, s1, h1, x2, y, M, b.C, st);
+  return bn_apply_dual_relu(x, s1, h1, x2, n.at<float>(b2->scale), n.at<float>(b2->shift), y, M, b.C, st);
+}
+
 // everything after the input im2col (reads only executor-owned memory: capturable)
 static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
   u16* X0 = n.at<u16>(n.X0);
   n.prof_next = train ? 0 : Net::PROF_SLOTS;  // eval passes are not timed
   DTC_TRY(stem_pack_weight(n.wbf(n.stem.pidx), n.at<u16>(n.WSTEM), 64, st));
+  if (train) DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.acc_lo - n.stats_lo, st));
   PROF(0, 2.0 * M0 * 64 * 27,
        conv_fwd(n.stem.s, X0, n.at<u16>(n.WSTEM), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
                 n.at<float>(n.SLAB), n.slab_bytes, st, ts));
-  DTC_TRY(bn_finalize_fwd(n, n.bn0, M0, train, st));
-  DTC_TRY(bn_apply_relu(n.at<u16>(n.C0), n.at<float>(n.bn0.scale), n.at<float>(n.bn0.shift), n.at<u16>(n.A0), M0, 64,
-                        st));
+  DTC_TRY(bn_act(n, 1, n.bn0, n.at<u16>(n.C0), nullptr, nullptr, n.at<u16>(n.A0), M0, train, st));
   const u16* in = n.at<u16>(n.A0);
   for (auto& b : n.blocks) {
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
@@ -452,23 +483,17 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
     PROF(0, conv_flops(b.c1.s),
          conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
                   n.slab_bytes, st, ts));
-    DTC_TRY(bn_finalize_fwd(n, b.b1, M, train, st));
-    DTC_TRY(bn_apply_relu(n.at<u16>(b.C1), n.at<float>(b.b1.scale), n.at<float>(b.b1.shift), n.at<u16>(b.A1), M,
-                          b.Cout, st));
+    DTC_TRY(bn_act(n, 1, b.b1, n.at<u16>(b.C1), nullptr, nullptr, n.at<u16>(b.A1), M, train, st));
     PROF(0, conv_flops(b.c2.s),
          conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
                   train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st, ts));
-    DTC_TRY(bn_finalize_fwd(n, b.b2, M, train, st));
     if (b.proj) {
       PROF(0, conv_flops(b.sc.s),
            conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr,
                     slab, n.slab_bytes, st, ts));
-      DTC_TRY(bn_finalize_fwd(n, b.bsc, M, train, st));
-      DTC_TRY(bn_apply_dual_relu(n.at<u16>(b.C2), n.at<float>(b.b2.scale), n.at<float>(b.b2.shift), n.at<u16>(b.S),
-                                 n.at<float>(b.bsc.scale), n.at<float>(b.bsc.shift), n.at<u16>(b.OUT), M, b.Cout, st));
+      DTC_TRY(bn_act(n, 3, b.b2, n.at<u16>(b.C2), &b.bsc, n.at<u16>(b.S), n.at<u16>(b.OUT), M, train, st));
     } else {
-      DTC_TRY(bn_apply_add_relu(n.at<u16>(b.C2), n.at<float>(b.b2.scale), n.at<float>(b.b2.shift), in,
-                                n.at<u16>(b.OUT), M, b.Cout, st));
+      DTC_TRY(bn_act(n, 2, b.b2, n.at<u16>(b.C2), nullptr, in, n.at<u16>(b.OUT), M, train, st));
     }
     in = n.at<u16>(b.OUT);
   }
@@ -528,6 +553,36 @@ static int cap(Net& n, const std::string& name, const void* src, hipStream_t st)
   return set_error(DTC_EINVAL, "capture slot %s missing", name.c_str());
 }
 
+static BnBwdArgs bwd_args(Net& n, BNL& b, int64_t count, float gs) {
+  BnBwdArgs a;
+  a.acc = n.at<double>(b.acc);
+  a.count = count;
+  a.gamma = n.pf(b.gidx);
+  a.mean = n.at<float>(b.mean);
+  a.invstd = n.at<float>(b.invstd);
+  a.gscale = gs;
+  a.dgamma = n.gf(b.gidx);
+  a.dbeta = n.gf(b.bidx);
+  return a;
+}
+
+// dx1 = BN-backward apply of b1 on (dz, x1) [; dx2 of b2 on (dz, x2)], coefficients from the sums
+// bn_bwd_reduce accumulated; dgamma / dbeta into the flat gradient buffer.
+static int bn_bwd_coef_apply(Net& n, BNL& b1, const u16* dz, const u16* x1, u16* dx1, BNL* b2, const u16* x2, u16* dx2,
+                             int64_t M, float gs, hipStream_t st) {
+  if (bn_fused()) {
+    const BnBwdArgs a1 = bwd_args(n, b1, M, gs);
+    const BnBwdArgs a2 = b2 ? bwd_args(n, *b2, M, gs) : BnBwdArgs{};
+    return bn_bwd_fin_apply(dz, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st);
+  }
+  DTC_TRY(bn_bwd_finalize(n.at<double>(b1.acc), b1.C, M, n.pf(b1.gidx), n.at<float>(b1.mean), n.at<float>(b1.invstd),
+                          gs, n.gf(b1.gidx), n.gf(b1.bidx), n.at<float>(b1.coef), st));
+  if (b2)
+    DTC_TRY(bn_bwd_finalize(n.at<double>(b2->acc), b2->C, M, n.pf(b2->gidx), n.at<float>(b2->mean),
+                            n.at<float>(b2->invstd), gs, n.gf(b2->gidx), n.gf(b2->bidx), n.at<float>(b2->coef), st));
+  return bn_bwd_apply(dz, x1, n.at<float>(b1.coef), dx1, x2, b2 ? n.at<float>(b2->coef) : nullptr, dx2, M, b1.C, st);
+}
+
 // Side stream for the weight gradients (fork after their input gradient exists, join before
 // anything reads the weight gradients: bucket all-reduces and the end of backward).
 static bool side_on(const Net& n) { return option_get(OPT_BWD_STREAMS) != 0; }
@@ -573,6 +628,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   float* slabw = n.at<float>(n.SLABW);
   hipStream_t sd = st;  // weight-gradient stream
   const BlockL& last = n.blocks.back();
+  DTC_HIP(hipMemsetAsync(n.ws + n.acc_lo, 0, n.stats_hi - n.acc_lo, st));
   DTC_TRY(head_bwd(dlogits, n.at<float>(n.FEAT), n.wbf(n.fc_w), n.B, last.Hout * last.Wout, 512, n.ncls, gs,
                    n.gf(n.fc_w), n.gf(n.fc_b), G[0], n.at<float>(n.HEADWS), n.HEADWS_bytes, st));
   for (int bi = (int)n.blocks.size() - 1; bi >= 0; --bi) {
@@ -589,15 +645,8 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
                           n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
                           b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
                           b.proj ? n.at<double>(b.bsc.acc) : nullptr, G[1], M, b.Cout, st));
-    DTC_TRY(bn_bwd_finalize(n.at<double>(b.b2.acc), b.Cout, M, n.pf(b.b2.gidx), n.at<float>(b.b2.mean),
-                            n.at<float>(b.b2.invstd), gs, n.gf(b.b2.gidx), n.gf(b.b2.bidx), n.at<float>(b.b2.coef),
-                            st));
-    if (b.proj)
-      DTC_TRY(bn_bwd_finalize(n.at<double>(b.bsc.acc), b.Cout, M, n.pf(b.bsc.gidx), n.at<float>(b.bsc.mean),
-                              n.at<float>(b.bsc.invstd), gs, n.gf(b.bsc.gidx), n.gf(b.bsc.bidx),
-                              n.at<float>(b.bsc.coef), st));
-    DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(b.C2), n.at<float>(b.b2.coef), dc2, b.proj ? n.at<u16>(b.S) : nullptr,
-                         b.proj ? n.at<float>(b.bsc.coef) : nullptr, dsc, M, b.Cout, st));
+    DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[1], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
+                              b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st));
     DTC_TRY(cap(n, cp + ".dz", G[1], st));
     DTC_TRY(cap(n, cp + ".dc2", dc2, st));
     if (b.proj) DTC_TRY(cap(n, cp + ".ds", dsc, st));
@@ -609,11 +658,8 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
     // a1 = relu(bn1(c1))
     DTC_TRY(bn_bwd_reduce(G[4], n.at<u16>(b.A1), n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
                           n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, G[4], M, b.Cout, st));
-    DTC_TRY(bn_bwd_finalize(n.at<double>(b.b1.acc), b.Cout, M, n.pf(b.b1.gidx), n.at<float>(b.b1.mean),
-                            n.at<float>(b.b1.invstd), gs, n.gf(b.b1.gidx), n.gf(b.b1.bidx), n.at<float>(b.b1.coef),
-                            st));
     DTC_TRY(cap(n, cp + ".dz1", G[4], st));
-    DTC_TRY(bn_bwd_apply(G[4], n.at<u16>(b.C1), n.at<float>(b.b1.coef), dc1, nullptr, nullptr, nullptr, M, b.Cout, st));
+    DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st));
     DTC_TRY(cap(n, cp + ".dc1", dc1, st));
     // conv1 (+ shortcut): weight grads (side stream), then the block-input gradient with the residual fused
     DTC_TRY(fork_side(n, st, &sd));
@@ -634,10 +680,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   u16* dc0 = n.at<u16>(n.DC0);
   DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(n.A0), n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
                         n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, G[1], M0, 64, st));
-  DTC_TRY(bn_bwd_finalize(n.at<double>(n.bn0.acc), 64, M0, n.pf(n.bn0.gidx), n.at<float>(n.bn0.mean),
-                          n.at<float>(n.bn0.invstd), gs, n.gf(n.bn0.gidx), n.gf(n.bn0.bidx), n.at<float>(n.bn0.coef),
-                          st));
-  DTC_TRY(bn_bwd_apply(G[1], n.at<u16>(n.C0), n.at<float>(n.bn0.coef), dc0, nullptr, nullptr, nullptr, M0, 64, st));
+  DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[1], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st));
   DTC_TRY(cap(n, "grad.stem.dz", G[1], st));
   DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
   DTC_TRY(join_side(n, st));  // the stem wgrad is the last kernel: run it on the main stream

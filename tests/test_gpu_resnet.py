@@ -280,6 +280,24 @@ def test_side_stream_wgrad_matches_serial(dtc, cuda, graphs):
     assert rel_err(pa, pb) < 1e-5
 
 
+@pytest.mark.parametrize("graphs", [True, False])
+def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
+    """BN coefficients computed inside the apply kernels (option bn_fused_fin=1, default) vs the
+    separate finalize launches: same fp64 slot sums in a different (fixed) combination order, so
+    losses, gradients, parameters and running statistics agree to rounding."""
+    la, ga, pa, ba = _train_steps(dtc, cuda, 3, graphs=graphs)
+    dtc._native.lib.dtc_set_option(b"bn_fused_fin", 0)
+    try:
+        lb, gb, pb, bb = _train_steps(dtc, cuda, 3, graphs=graphs)
+    finally:
+        dtc._native.lib.dtc_set_option(b"bn_fused_fin", 1)
+    np.testing.assert_allclose(la, lb, rtol=1e-4)
+    assert rel_err(ga, gb) < 1e-3
+    assert rel_err(pa, pb) < 1e-5
+    for k in ba:
+        assert rel_err(ba[k], bb[k]) < 1e-4, k
+
+
 def test_graph_recapture_on_option_change(dtc, cuda):
     """Options are baked into captured launches: changing one re-captures (results unchanged)."""
     model, _, x, y = _setup(dtc, cuda, 4, seed=6)

@@ -1,0 +1,69 @@
+"""Host-side phase timing of the bench step (no added syncs): where does the host wait?
+
+Replicates bench.py's step and stamps time.perf_counter() after each phase; a phase that blocks
+on the device (barrier, item) shows the GPU time it waited for, the others show pure host cost.
+Usage: python tools/host_phases.py [--steps 50] [--no-barrier]"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import bench  # noqa: E402
+import dtc_import  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--no-barrier", action="store_true")
+    args = ap.parse_args()
+    rank, world, local = bench.init_dist()
+    dev = torch.device("cuda", local)
+    dtc = dtc_import.load()
+    torch.manual_seed(42)
+    model = dtc.DDP(dtc.ResNet18().to(dev), device_ids=[local], find_unused_parameters=True)
+    crit = dtc.CrossEntropyLoss()
+    opt = dtc.SGD(model.parameters(), lr=0.1, weight_decay=1e-4, momentum=0.9, nesterov=True)
+    scaler = dtc.GradScaler()
+    tpl = dtc.data.class_templates(100, 32, 32)
+    img, label = dtc.data.synthetic_batch(0, 256, 32, 32, 100, dev, tpl)
+    names = ["zero_grad", "forward", "loss", "barrier", "scale", "backward", "step", "update", "item"]
+    rec = []
+    for i in range(args.steps + 10):
+        t = [time.perf_counter()]
+        opt.zero_grad()
+        t.append(time.perf_counter())
+        with dtc.autocast():
+            logit = model(img)
+            t.append(time.perf_counter())
+            loss = crit(logit, label)
+        t.append(time.perf_counter())
+        if not args.no_barrier:
+            dist.barrier()
+        t.append(time.perf_counter())
+        scaled = scaler.scale(loss)
+        t.append(time.perf_counter())
+        scaled.backward()
+        t.append(time.perf_counter())
+        scaler.step(opt)
+        t.append(time.perf_counter())
+        scaler.update()
+        t.append(time.perf_counter())
+        loss.item()
+        t.append(time.perf_counter())
+        if i >= 10:
+            rec.append(np.diff(t) * 1e6)
+    r = np.array(rec)
+    for k, n in enumerate(names):
+        print(f"{n:10s} mean {r[:, k].mean():8.1f} us  median {np.median(r[:, k]):8.1f} us")
+    print(f"{'total':10s} mean {r.sum(1).mean():8.1f} us")
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

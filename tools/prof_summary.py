@@ -14,7 +14,8 @@ import os
 import sys
 from collections import defaultdict
 
-CONV = ("igemm_kernel", "wgrad_halo_kernel", "splitk_reduce_kernel", "wgrad_reduce_kernel")
+CONV = ("igemm_kernel", "conv_halo_kernel", "conv_c64_kernel", "wgrad_halo_kernel", "splitk_reduce_kernel",
+        "wgrad_reduce_kernel")
 
 
 def short(name):
