@@ -717,7 +717,8 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
       n.bwd_gs = gs;
       n.bwd_comm = comm != nullptr;
     }
-    DTC_HIP(hipMemcpyAsync(n.at<float>(n.DLOGITS), dlogits, (size_t)n.B * n.ncls * 4, hipMemcpyDeviceToDevice, st));
+    if (dlogits != n.at<float>(n.DLOGITS))
+      DTC_HIP(hipMemcpyAsync(n.at<float>(n.DLOGITS), dlogits, (size_t)n.B * n.ncls * 4, hipMemcpyDeviceToDevice, st));
     for (const auto& sg : n.bwd_segs) {
       if (sg.exec) DTC_HIP(hipGraphLaunch(sg.exec, st));
       for (int i : sg.buckets)
@@ -872,6 +873,12 @@ int dtc_rn18_activation_info(const dtc_net* net, int idx, const char** name, siz
   if (shape4) {
     shape4[0] = a.n; shape4[1] = a.h; shape4[2] = a.w; shape4[3] = a.c;
   }
+  return 0;
+}
+
+int dtc_rn18_dlogits_buffer(const dtc_net* net, size_t* ws_offset) {
+  DTC_CHECK_ARG(net && ws_offset, "dtc_rn18_dlogits_buffer: bad args");
+  *ws_offset = net->n.DLOGITS;
   return 0;
 }
 

@@ -113,6 +113,7 @@ class Executor:
         self.flat = flat
         self.batch, self.height, self.width, self.num_classes = batch, height, width, num_classes
         self.generation = 0
+        self._dlogits = None
         call("dtc_rn18_bind", self.handle, self.ws_ptr, ptr(flat.params), ptr(flat.grads), ptr(flat.params_bf16),
              ptr(flat.bufs), ptr(flat.nbt), stream_ptr())
 
@@ -124,6 +125,18 @@ class Executor:
     def backward(self, dlogits: torch.Tensor, grad_scale: float, comm) -> None:
         call("dtc_rn18_backward", self.handle, ptr(dlogits), float(grad_scale), comm.handle if comm else None,
              stream_ptr())
+
+    def dlogits_buffer(self) -> torch.Tensor:
+        """fp32 [batch, num_classes] view of the executor's own dlogits buffer: a loss gradient
+        written here is consumed by backward() without the copy-in."""
+        if self._dlogits is None:
+            off = C.c_size_t()
+            call("dtc_rn18_dlogits_buffer", self.handle, C.byref(off))
+            start = self.ws_ptr - self.workspace.data_ptr() + off.value
+            nbytes = self.batch * self.num_classes * 4
+            self._dlogits = self.workspace[start:start + nbytes].view(torch.float32).view(self.batch,
+                                                                                         self.num_classes)
+        return self._dlogits
 
     def activations(self, captures: bool = False) -> Dict[str, torch.Tensor]:
         """Views of the per-layer activations the last forward left in the workspace (NHWC); with
@@ -208,21 +221,41 @@ class NativeLoss(torch.Tensor):
         if exe.generation != node.gen:
             raise NativeError("ResNet backward: the executor ran another forward since this graph was built "
                               "(one forward per backward is supported)")
-        dl = ops.xent_bwd(logits, labels, lse, gscale)
+        dl = ops.xent_bwd(logits, labels, lse, gscale, out=exe.dlogits_buffer())
         exe.backward(dl, model._grad_scale, model._comm)
         model._ensure_grads()
         if not retain_graph:
             self._dtc_fast = None
         return None
 
+    def item(self):
+        """The loss value from the pinned host copy enqueued right after the loss kernel: waits
+        for the loss, not for the whole stream (a plain ``Tensor.item()`` also waits for the
+        backward and optimizer step issued since). Same value either way."""
+        hc = getattr(self, "_dtc_host", None)
+        if hc is None:
+            return super().item()
+        h, ev = hc
+        ev.synchronize()
+        return h.item()
+
+    def __float__(self):
+        return float(self.item())
+
 
 _FAST_BACKWARD = [True]  # tests flip this to compare against the autograd-engine path
 
 
-def _wrap_loss(graph: torch.Tensor, fast) -> torch.Tensor:
+def _wrap_loss(graph: torch.Tensor, fast, host_copy: bool = False) -> torch.Tensor:
     out = torch.Tensor._make_subclass(NativeLoss, graph.detach(), False)
     out._dtc_graph = graph
     out._dtc_fast = fast
+    if host_copy:
+        h = torch.empty((), dtype=graph.dtype, pin_memory=True)
+        h.copy_(graph.detach(), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        out._dtc_host = (h, ev)
     return out
 
 
@@ -247,7 +280,7 @@ class CrossEntropyLoss(nn.Module):
         loss = _XentFn.apply(logits, labels)
         node = logits.grad_fn
         if torch.is_grad_enabled() and isinstance(node, _NetFn._backward_cls):
-            return _wrap_loss(loss, (node, logits, labels, loss.grad_fn.lse, None))
+            return _wrap_loss(loss, (node, logits, labels, loss.grad_fn.lse, None), host_copy=True)
         return loss
 
 

@@ -181,9 +181,9 @@ def xent_fwd(logits, labels):
     return loss, lse
 
 
-def xent_bwd(logits, labels, lse, gscale=None):
+def xent_bwd(logits, labels, lse, gscale=None, out=None):
     n, ncls = logits.shape
-    dl = torch.empty_like(logits)
+    dl = torch.empty_like(logits) if out is None else out
     call("dtc_xent_bwd", ptr(logits), ptr(labels), ptr(lse), ptr(gscale), n, ncls, ptr(dl), stream_ptr())
     return dl
 

@@ -174,6 +174,10 @@ int dtc_rn18_forward(dtc_net* net, const float* x, float* logits, int train, voi
  * on the communicator's side stream as soon as backward has produced it; the call returns with
  * `stream` ordered after the last all-reduce. */
 int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_comm* comm, void* stream);
+/* Byte offset into the workspace of the executor's own fp32 [batch][num_classes] dlogits buffer.
+ * A caller that writes the loss gradient there (e.g. the fused cross-entropy backward) and passes
+ * that pointer to dtc_rn18_backward saves the graph path's copy-in. */
+int dtc_rn18_dlogits_buffer(const dtc_net* net, size_t* ws_offset);
 
 /* Per-layer activations held in the workspace after dtc_rn18_forward (NHWC bf16 except the
  * fp32 "head.feat_f32"): name, byte offset into the workspace, {n, h, w, c}. For parity tests. */

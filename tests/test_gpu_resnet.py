@@ -434,3 +434,30 @@ def test_native_loss_backward_matches_autograd(dtc, cuda):
     # arithmetic on the loss leaves the fast path: a plain autograd tensor
     loss = crit(model(xd), yd)
     assert type(loss * 2.0) is torch.Tensor
+
+
+def test_native_loss_item_and_dlogits_buffer(dtc, cuda):
+    """NativeLoss.item() reads the pinned host copy taken right after the loss kernel: equal to the
+    device value even when read after the backward and the optimizer step have been issued; the
+    fused xent backward writes the executor's own dlogits buffer (graph path skips the copy-in)."""
+    model, _, x, y = _setup(dtc, cuda, 8, seed=12)
+    crit = dtc.CrossEntropyLoss()
+    opt = dtc.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
+    vals = []
+    for _ in range(3):
+        opt.zero_grad()
+        loss = crit(model(xd), yd)
+        ref = loss.detach().clone()
+        loss.backward()
+        opt.step()
+        v = loss.item()
+        assert v == float(ref.cpu()), (v, float(ref.cpu()))
+        assert float(loss) == v
+        vals.append(v)
+    exe = model.executor(8, 32, 32)
+    dl = exe.dlogits_buffer()
+    assert dl.shape == (8, 100) and dl.dtype == torch.float32
+    # the last backward's dlogits: rows are softmax - onehot over the batch, so each row sums to ~0
+    assert float(dl.sum(1).abs().max()) < 1e-5
+    assert np.isfinite(vals).all()

@@ -21,7 +21,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--no-barrier", action="store_true")
+    ap.add_argument("--cprofile", action="store_true", help="cProfile the timed steps (top functions by tottime)")
+    ap.add_argument("--spin", action="store_true", help="hipSetDeviceFlags(hipDeviceScheduleSpin) before init")
     args = ap.parse_args()
+    if args.spin:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        print("hipSetDeviceFlags(spin) ->", hip.hipSetDeviceFlags(1))
     rank, world, local = bench.init_dist()
     dev = torch.device("cuda", local)
     dtc = dtc_import.load()
@@ -34,7 +40,12 @@ def main():
     img, label = dtc.data.synthetic_batch(0, 256, 32, 32, 100, dev, tpl)
     names = ["zero_grad", "forward", "loss", "barrier", "scale", "backward", "step", "update", "item"]
     rec = []
+    prof = None
     for i in range(args.steps + 10):
+        if i == 10 and args.cprofile:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t = [time.perf_counter()]
         opt.zero_grad()
         t.append(time.perf_counter())
@@ -58,6 +69,10 @@ def main():
         t.append(time.perf_counter())
         if i >= 10:
             rec.append(np.diff(t) * 1e6)
+    if prof is not None:
+        prof.disable()
+        import pstats
+        pstats.Stats(prof).sort_stats("tottime").print_stats(30)
     r = np.array(rec)
     for k, n in enumerate(names):
         print(f"{n:10s} mean {r[:, k].mean():8.1f} us  median {np.median(r[:, k]):8.1f} us")
