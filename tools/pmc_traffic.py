@@ -7,7 +7,7 @@ per run: FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2, they do not fit one pass). 
 notes in MI355X_MICROARCH.md (§HBM): FETCH_SIZE counts half the bytes of wide (16 B/lane)
 coalesced reads, which is every load the conv kernels issue (global_load_lds_dwordx4 /
 buffer_load ... lds), so it is doubled; WRITE_SIZE is exact for 16-B stores. Both are in KiB.
-One conv call = one igemm_kernel or wgrad_halo_kernel dispatch (+ its split-K / wgrad reduction).
+One conv call = one igemm_kernel, conv_halo_kernel, conv_c64_kernel or wgrad_halo_kernel dispatch (+ its split-K / wgrad reduction).
 """
 import csv
 import glob
@@ -16,7 +16,7 @@ import os
 import sys
 from collections import defaultdict
 
-MAIN = ("igemm_kernel", "wgrad_halo_kernel")
+MAIN = ("igemm_kernel", "conv_halo_kernel", "conv_c64_kernel", "wgrad_halo_kernel")
 AUX = ("splitk_reduce_kernel", "wgrad_reduce_kernel")
 
 
