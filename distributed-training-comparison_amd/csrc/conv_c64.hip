@@ -43,15 +43,27 @@ constexpr int C64_NHI = (C64_HCAP / 8 + 3) / 4;  // per wave (instruction ids wa
 constexpr int C64_HBYTES = C64_HCAP * 128;
 constexpr int C64_WBYTES = 9 * 8192;
 
+// 16-B fragment at an LDS byte address (ds_read_b128 with that VGPR address)
+__device__ __forceinline__ bf16x8 lds_frag(uint32_t addr) {
+  typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
+  return *(const lds_bf16x8*)(size_t)addr;
+}
+
+// MODE 0: FWD (+ BN statistics), 1: DGRAD, 2: DGRAD + residual.
+// Software pipelined over tiles: the epilogue of tile k-1 (bf16 rounding, statistics, stores) is
+// issued in the same basic block as tile k's 288 MFMAs, so its VALU work fills MFMA issue gaps
+// instead of running after them on the wave's single SIMD (one wave per SIMD: nothing else would
+// hide it). Per-lane B-fragment LDS offsets for all nine taps and both k-steps, and the
+// tile-invariant part of the halo DMA addressing, are computed once per workgroup.
 template <int MODE>
 __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   constexpr int FM = 4, FN = 4;  // wave tile: 64 channels x 64 pixels
+  constexpr bool FWD = MODE == 0, RES = MODE == 2;
   __shared__ __attribute__((aligned(1024))) char smem[C64_WBYTES + 2 * C64_HBYTES];
   char* const halo = smem + C64_WBYTES;
   stamp_start(p.ts);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wc = wave;
-  const int arow0 = 0, bcol0 = wc * 64;
+  const int bcol0 = wave * 64;
   const int lrow = lane >> 3, pc = lane & 7;
   const int W2 = p.W + 2;
   const int M = p.N * p.H * p.W;
@@ -61,20 +73,40 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   for (int q = 0; q < 18; ++q) {
     const int g = wave + 4 * q;  // 72 wave-instructions: tap g/8, row group g%8
     const int tap = g >> 3, ia = g & 7, row = ia * 8 + lrow;
-    const u16* src = (MODE == 0) ? p.w + row * 576 + tap * 64 + (pc ^ rowswz(row)) * 8
-                                 : p.w + row * 576 + (8 - tap) * 64 + (pc ^ trswz(row)) * 8;
+    const u16* src = FWD ? p.w + row * 576 + tap * 64 + (pc ^ rowswz(row)) * 8
+                         : p.w + row * 576 + (8 - tap) * 64 + (pc ^ trswz(row)) * 8;
     glds16(src, smem + tap * 8192 + ia * 1024);
   }
-  // ---- per-lane constants: B-fragment halo rows (tile independent), halo DMA row decomposition
+  // ---- B fragments: LDS byte offsets within a halo buffer, per tap / k-step / fragment
   const int spx = p.rows * p.W;
   const int fpx = lane & 15;  // W >= 16: the 16 pixels of a fragment are contiguous in one image row
-  int hbr[FN];
+  uint32_t boff[9][2][FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int l = bcol0 + j * 16 + fpx;
     const int i = (int)fdiv((uint32_t)l, p.fd_spx), rem = l - i * spx;
     const int y = (int)fdiv((uint32_t)rem, p.fd_w), x = rem - y * p.W;
-    hbr[j] = i * p.hb + y * W2 + x;
+    const int hbr = i * p.hb + y * W2 + x;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int row = hbr + (t / 3) * W2 + (t % 3);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) boff[t][ks][j] = row * 128 + (((ks * 4 + (lane >> 4)) ^ c64_hswz(row)) << 4);
+    }
+  }
+  // ---- halo DMA: tile-invariant per-lane parts (row decomposition, x range, swizzled channel chunk)
+  int hrel[C64_NHI], hyy[C64_NHI], hii[C64_NHI];
+  bool hok[C64_NHI];
+#pragma unroll
+  for (int q = 0; q < C64_NHI; ++q) {
+    const int g = wave + 4 * q;
+    const int hr = g * 8 + lrow;
+    const int i = (int)fdiv((uint32_t)hr, p.fd_hb), rem = hr - i * p.hb;
+    const int hy = (int)fdiv((uint32_t)rem, p.fd_w2), hx = rem - hy * W2;
+    hok[q] = g < C64_HCAP / 8 && hr < p.nh && (unsigned)(hx - 1) < (unsigned)p.W;
+    hyy[q] = hy - 1;
+    hii[q] = i;
+    hrel[q] = (((i * p.H + hy - 1) * p.W + hx - 1) * 64 + (pc ^ c64_hswz(hr)) * 8) * 2;
   }
   auto stage_halo = [&](char* dst, int tile) {
     int n0, y0;
@@ -85,22 +117,19 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
       n0 = tile * p.imgs;
       y0 = 0;
     }
+    const int tbase = (n0 * p.H + y0) * p.W * 128;
 #pragma unroll
     for (int q = 0; q < C64_NHI; ++q) {
       const int g = wave + 4 * q;
       if (g >= C64_HCAP / 8) break;
-      const int hr = g * 8 + lrow;
-      const int i = (int)fdiv((uint32_t)hr, p.fd_hb), rem = hr - i * p.hb;
-      const int hy = (int)fdiv((uint32_t)rem, p.fd_w2), hx = rem - hy * W2;
-      const int n = n0 + i, y = y0 + hy - 1, x = hx - 1;
-      const bool ok = hr < p.nh && n < p.N && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
-      const uint32_t off = ok ? (uint32_t)((((n * p.H + y) * p.W + x) * 64 + (pc ^ c64_hswz(hr)) * 8) * 2) : 0x80000000u;
-      buf_lds16(p.src, p.src_bytes, dst + g * 1024, off);
+      const bool ok = hok[q] && (unsigned)(y0 + hyy[q]) < (unsigned)p.H && n0 + hii[q] < p.N;
+      buf_lds16(p.src, p.src_bytes, dst + g * 1024, ok ? (uint32_t)(tbase + hrel[q]) : 0x80000000u);
     }
   };
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.out, 0, p.out_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.res ? p.res : p.out), 0, p.res ? p.out_bytes : 0, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(RES ? p.res : p.out), 0, RES ? p.out_bytes : 0, 0x00020000);
+  const uint32_t halo_lds = __builtin_amdgcn_readfirstlane(lds_u32(halo));
 
   const int rq = (lane >> 4) * 4;
   float ssum[FM][4], ssq[FM][4];
@@ -109,72 +138,30 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) ssum[i][t] = ssq[i][t] = 0.f;
 
-  int k = 0;
-  int tile = blockIdx.x;
-  if (tile < p.ntiles) stage_halo(halo, tile);
-  for (; tile < p.ntiles; tile += gridDim.x, ++k) {
-    // this tile's halo has landed (the previous tile's FM*FN stores may still be in flight)
-    if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // FM*FN stores of the previous tile
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const char* hbuf = halo + (k & 1) * C64_HBYTES;
-    const int tn = tile + gridDim.x;
-    if (tn < p.ntiles) stage_halo(halo + ((k + 1) & 1) * C64_HBYTES, tn);
-
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int toff = (t / 3) * W2 + (t % 3);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[FM], bfr[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          af[i] = (MODE == 0) ? frag_row(smem + t * 8192, arow0 + i * 16, ks, lane)
-                              : frag_tr(smem + t * 8192, arow0 + i * 16, ks, lane);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int row = hbr[j] + toff;
-          const int ch = (ks * 4 + (lane >> 4)) ^ c64_hswz(row);
-          bfr[j] = __builtin_bit_cast(bf16x8, *(const uint4*)(hbuf + row * 128 + (ch << 4)));
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      }
-    }
-
-    // epilogue: exactly FM*FN buffer stores per wave (rows past M are dropped by the bound)
+  // epilogue of one finished tile: exactly FM*FN buffer stores per wave (+ as many residual loads);
+  // lanes of pixels past M, or of no tile (have == false), are dropped by the descriptor bound
+  auto epilogue_col = [&](const f32x4 (&a)[FM][FN], int tile, bool have, int j) {
     const int px0 = tile * 256;  // tiles are 256 consecutive pixels
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
+    {
       const int pix = px0 + bcol0 + j * 16 + fpx;
-      const bool ok = pix < M;
+      const bool ok = have && pix < M;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int ch = arow0 + i * 16 + rq;
+        const int ch = i * 16 + rq;
         const uint32_t off = ok ? (uint32_t)((pix * 64 + ch) * 2) : 0x80000000u;
         float v[4];
-        if constexpr (MODE == 0) {
+        if constexpr (FWD) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            v[t] = round_bf(acc[i][j][t]);
-            if (ok) {
-              ssum[i][t] += v[t];
-              ssq[i][t] += v[t] * v[t];
-            }
+            v[t] = round_bf(a[i][j][t]);
+            const float u = ok ? v[t] : 0.f;
+            ssum[i][t] += u;
+            ssq[i][t] += u * u;
           }
         } else {
 #pragma unroll
-          for (int t = 0; t < 4; ++t) v[t] = acc[i][j][t];
-          if (p.res) {
+          for (int t = 0; t < 4; ++t) v[t] = a[i][j][t];
+          if constexpr (RES) {
             typedef int i32x2 __attribute__((ext_vector_type(2)));
             const i32x2 rr = __builtin_amdgcn_raw_buffer_load_b64(rrsrc, off, 0, 0);
             v[0] += bf_lo((uint32_t)rr.x); v[1] += bf_hi((uint32_t)rr.x);
@@ -188,9 +175,67 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
         __builtin_amdgcn_raw_buffer_store_b64(wv, orsrc, off, 0, 0);
       }
     }
-  }
+  };
+  auto epilogue = [&](const f32x4 (&a)[FM][FN], int tile, bool have) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) epilogue_col(a, tile, have, j);
+  };
 
-  if constexpr (MODE == 0) {
+  f32x4 accp[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) accp[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int tilep = 0;
+  int k = 0;
+  int tile = blockIdx.x;
+  if (tile < p.ntiles) stage_halo(halo, tile);
+  for (; tile < p.ntiles; tile += gridDim.x, ++k) {
+    // this tile's halo has landed; the previous iteration's epilogue VMEM ops (FM*FN stores, plus
+    // FM*FN residual loads) were issued after it and may still be in flight
+    if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (RES) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const uint32_t hb = halo_lds + (uint32_t)((k & 1) * C64_HBYTES);
+    const int tn = tile + gridDim.x;
+    if (tn < p.ntiles) stage_halo(halo + ((k + 1) & 1) * C64_HBYTES, tn);
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          af[i] = FWD ? frag_row(smem + t * 8192, i * 16, ks, lane) : frag_tr(smem + t * 8192, i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = lds_frag(hb + boff[t][ks][j]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      // the previous tile's epilogue, one pixel-column group after each odd tap (placed between
+      // MFMA groups so the scheduler spreads it over the MFMA issue gaps)
+      if (t & 1) epilogue_col(accp, tilep, k > 0, t >> 1);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) accp[i][j] = acc[i][j];
+    tilep = tile;
+  }
+  if (k > 0) epilogue(accp, tilep, true);
+
+  if constexpr (FWD) {
     if (p.stats != nullptr) {  // per-channel sums of this workgroup -> fp64 slot (once per workgroup)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __syncthreads();
@@ -201,9 +246,9 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
         for (int t = 0; t < 4; ++t) {
           const float s = row16_sum(ssum[i][t]), q = row16_sum(ssq[i][t]);
           if ((lane & 15) == 0) {
-            const int ch = arow0 + i * 16 + rq + t;
-            red[(wc * 64 + ch) * 2 + 0] = s;
-            red[(wc * 64 + ch) * 2 + 1] = q;
+            const int ch = i * 16 + rq + t;
+            red[(wave * 64 + ch) * 2 + 0] = s;
+            red[(wave * 64 + ch) * 2 + 1] = q;
           }
         }
       __syncthreads();
@@ -273,8 +318,10 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   const int grid = std::min(p.ntiles, 256);
   if (mode == CONV_FWD)
     hipLaunchKernelGGL(conv_c64_kernel<0>, dim3(grid), dim3(256), 0, st, p);
-  else
+  else if (res == nullptr)
     hipLaunchKernelGGL(conv_c64_kernel<1>, dim3(grid), dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL(conv_c64_kernel<2>, dim3(grid), dim3(256), 0, st, p);
   DTC_LAUNCH_CHECK();
   return 0;
 }

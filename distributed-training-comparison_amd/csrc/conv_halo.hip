@@ -69,7 +69,7 @@ struct HConvParams {
 };
 
 template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP>
-__global__ void __launch_bounds__(256, 1) conv_halo_kernel(const HConvParams p) {
+__global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) {
   constexpr int FM = BM / (WR * 16);
   constexpr int FN = BN / (WC * 16);
   constexpr int WBYTES = BM * 128;
@@ -170,62 +170,96 @@ __global__ void __launch_bounds__(256, 1) conv_halo_kernel(const HConvParams p) 
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // B-fragment LDS byte offsets (within a halo buffer) for every tap / k-step / fragment, computed
+  // once: with the taps unrolled and the chunk loop unrolled by two, every buffer base is a
+  // constant the ds_read offset field absorbs, so the MFMA stream carries no address arithmetic.
+  // (k-step 1 reads chunk (4 + g) ^ h = ((g ^ h) ^ 4): its offset is the k-step-0 offset ^ 64)
+  uint32_t boff[9][FN];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = hbr[j] + (t / 3) * W2 + (t % 3);
+      boff[t][j] = (uint32_t)(row * 128 + (((lane >> 4) ^ hswz(row)) << 4));
+    }
+  typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
+
+  // Small wave tiles (< 16 MFMAs per k-step): all 2*(FM+FN) fragments of a step are read first
+  // (the LDS reads overlap each other and the first MFMAs instead of each MFMA pair waiting on its
+  // own reads); sched_barrier keeps the compiler from sinking the reads back next to their uses.
   auto compute = [&](const char* hbuf, const char* wb, int tap) {
-    const int r = tap / 3, s = tap - r * 3;
-    const int toff = r * W2 + s;
+    if constexpr (FM * FN >= 16) {  // 16+ MFMAs per k-step hide its reads: k-step fragments only
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[FM], bfr[FN];
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        if constexpr (MODE == 0) af[i] = frag_row(wb, arow0 + i * 16, ks, lane);
-        else af[i] = frag_tr(wb, arow0 + i * 16, ks, lane);
+        for (int j = 0; j < FN; ++j) bfr[j] = *(const lds_bf16x8*)(hbuf + (boff[tap][j] ^ (uint32_t)(ks * 64)));
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          if constexpr (MODE == 0) af[i] = frag_row(wb, arow0 + i * 16, ks, lane);
+          else af[i] = frag_tr(wb, arow0 + i * 16, ks, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
+    } else {
+      bf16x8 af[2][FM], bfr[2][FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int row = hbr[j] + toff;
-        const int ch = (ks * 4 + (lane >> 4)) ^ hswz(row);
-        bfr[j] = __builtin_bit_cast(bf16x8, *(const uint4*)(hbuf + row * 128 + (ch << 4)));
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[ks][j] = *(const lds_bf16x8*)(hbuf + (boff[tap][j] ^ (uint32_t)(ks * 64)));
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          if constexpr (MODE == 0) af[ks][i] = frag_row(wb, arow0 + i * 16, ks, lane);
+          else af[ks][i] = frag_tr(wb, arow0 + i * 16, ks, lane);
+        }
       }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
     }
   };
 
-  // ---- main loop over (chunk, tap) steps
-  const int nsteps = p.nchunk * 9;
+  // ---- main loop: chunk pairs x 9 unrolled taps; step (c, tap) reads weight buffer (c + tap) & 1
+  // (9 is odd) and, for NHB == 2, halo buffer c & 1 -- both static after the unrolling
   stage_h(smem, c0, 0, NHI);
   stage_w(wbase, c0, 0);
-  int cc = 0, tap = 0;  // chunk relative to c0
-  for (int it = 0; it < nsteps; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const int ntap = tap == 8 ? 0 : tap + 1, ncc = tap == 8 ? cc + 1 : cc;
-    const bool more = it + 1 < nsteps;
-    bool reload = false;
-    if (more) {
-      stage_w(wbase + ((it + 1) & 1) * WBYTES, c0 + ncc, ntap);
-      if constexpr (NHB == 2) {
-        if (cc + 1 < p.nchunk && tap < 8) {  // next chunk's halo, slice `tap` of 8
-          const int q_lo = (tap * p.nhi) >> 3, q_hi = ((tap + 1) * p.nhi) >> 3;
-          stage_h(smem + ((cc + 1) & 1) * HBYTES, c0 + cc + 1, q_lo, q_hi);
+  for (int cc = 0; cc < p.nchunk; cc += 2) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int c = cc + half;
+      if (c >= p.nchunk) break;
+      const char* hbuf = smem + (NHB == 2 ? half * HBYTES : 0);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int par = (half + tap) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (tap < 8) stage_w(wbase + (par ^ 1) * WBYTES, c0 + c, tap + 1);
+        else if (c + 1 < p.nchunk) stage_w(wbase + (par ^ 1) * WBYTES, c0 + c + 1, 0);
+        if constexpr (NHB == 2) {
+          if (c + 1 < p.nchunk && tap < 8) {  // next chunk's halo, slice `tap` of 8
+            const int q_lo = (tap * p.nhi) >> 3, q_hi = ((tap + 1) * p.nhi) >> 3;
+            stage_h(smem + (half ^ 1) * HBYTES, c0 + c + 1, q_lo, q_hi);
+          }
         }
-      } else {
-        reload = (ntap == 0);
+        compute(hbuf, wbase + par * WBYTES, tap);
+        if (NHB == 1 && tap == 8 && c + 1 < p.nchunk) {  // every wave is done with the halo: refill it
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+          stage_h(smem, c0 + c + 1, 0, NHI);
+        }
       }
     }
-    compute(smem + (NHB == 2 ? (cc & 1) * HBYTES : 0), wbase + (it & 1) * WBYTES, tap);
-    if (NHB == 1 && reload) {  // every wave is done with the halo: refill it for chunk ncc
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      stage_h(smem, c0 + ncc, 0, NHI);
-    }
-    cc = ncc;
-    tap = ntap;
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // LDS reads done before the epilogue reuses smem
@@ -334,6 +368,8 @@ static const HaloCfg kHaloCfgs[] = {
     {128, 256, 1, 416},  // 3: 86 KB: wide output-channel tiles
     {128, 128, 1, 288},  // 4: 69 KB, 2 WG/CU: 64x64 per wave
     {128, 128, 2, 288},  // 5: 106 KB: 64x64 per wave, double-buffered halo
+    {64, 128, 2, 224},   // 6: 72 KB, 2 WG/CU: double-buffered halo of up to 224 rows (2 images of 8x8)
+    {64, 64, 2, 160},    // 7: 56 KB: double-buffered halo of up to 160 rows (4 images of 4x4)
 };
 constexpr int kNumHaloCfgs = (int)(sizeof(kHaloCfgs) / sizeof(kHaloCfgs[0]));
 
@@ -392,6 +428,7 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
     // (layer1/2); else 64x128 tiles at 3 workgroups per CU, split-K up to ~2 workgroups per CU
     // (layer3: 512 tiles; layer4: 256 tiles x 2 splits)
     if (cfg_fits(s, 0, cout) && tiles(0) >= 512) hp.cfg = 0;
+    else if (option_get(OPT_HALO_NHB2) && cfg_fits(s, 6, cout)) hp.cfg = 6;
     else if (cfg_fits(s, 2, cout)) hp.cfg = 2;
     else if (cfg_fits(s, 0, cout)) hp.cfg = 0;
     else return hp;
@@ -421,7 +458,9 @@ static int launch_halo(const HConvParams& p, int cfg, dim3 grid, hipStream_t st)
     case 2: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 1, 288>), grid, dim3(256), 0, st, p); break;
     case 3: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 256, 2, 2, 1, 416>), grid, dim3(256), 0, st, p); break;
     case 4: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 1, 288>), grid, dim3(256), 0, st, p); break;
-    default: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 2, 288>), grid, dim3(256), 0, st, p); break;
+    case 5: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 2, 288>), grid, dim3(256), 0, st, p); break;
+    case 6: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 2, 224>), grid, dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 64, 2, 2, 2, 160>), grid, dim3(256), 0, st, p); break;
   }
   DTC_LAUNCH_CHECK();
   return 0;

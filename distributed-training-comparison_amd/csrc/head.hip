@@ -14,34 +14,47 @@ namespace dtc {
 
 __global__ void __launch_bounds__(256) stem_im2col_kernel(const float* __restrict__ x, u16* __restrict__ cols,
                                                          int N, int H, int W) {
-  const int64_t total = (int64_t)N * H * W * 8;  // 8 chunks of 8 columns per pixel
-  for (int64_t t = blockIdx.x * (int64_t)256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
-    const int chunk = (int)(t & 7);
-    const int64_t pix = t >> 3;
+  // One thread per output pixel: its 27 taps (r, s, c with c fastest: KRSC filter order) are read
+  // from NCHW fp32 (per tap the lanes of a wave read consecutive pixels: coalesced) and written as
+  // columns 0..31 of the pixel's row into LDS; the workgroup's 256 rows (32 KB) are then stored as
+  // contiguous 16-B lanes, columns 32..63 as zeros.
+  __shared__ uint4 rows[256 * 4];
+  const int t = threadIdx.x;
+  const int64_t M = (int64_t)N * H * W;
+  const int64_t pix0 = (int64_t)blockIdx.x * 256, pix = pix0 + t;
+  if (pix < M) {
     const int w = (int)(pix % W);
     const int h = (int)((pix / W) % H);
     const int n = (int)(pix / ((int64_t)W * H));
-    float v[8];
+    const float* xn = x + (int64_t)n * 3 * H * W;
+    float v[32];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int j = chunk * 8 + k;  // (r, s, c) with c fastest: KRSC filter order
-      float val = 0.f;
-      if (j < 27) {
-        const int r = j / 9, s = (j / 3) % 3, c = j % 3;
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
         const int ih = h + r - 1, iw = w + s - 1;
-        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-          val = x[(((int64_t)n * 3 + c) * H + ih) * W + iw];
+        const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[(r * 3 + s) * 3 + c] = in ? xn[((int64_t)c * H + ih) * W + iw] : 0.f;
       }
-      v[k] = val;
-    }
-    *(uint4*)(cols + pix * 64 + chunk * 8) = pack8(v);
+#pragma unroll
+    for (int k = 27; k < 32; ++k) v[k] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rows[t * 4 + (q ^ (t & 3))] = pack8(v + q * 8);
+  }
+  __syncthreads();
+  const int64_t nrow = std::min<int64_t>(256, M - pix0);
+  uint4* dst = (uint4*)(cols + pix0 * 64);
+  for (int e = t; e < nrow * 8; e += 256) {
+    const int row = e >> 3, q = e & 7;
+    dst[e] = q < 4 ? rows[row * 4 + (q ^ (row & 3))] : uint4{0u, 0u, 0u, 0u};
   }
 }
 
 int stem_im2col(const float* x, u16* cols, int N, int H, int W, hipStream_t st) {
   DTC_CHECK_ARG(x && cols && N > 0 && H > 0 && W > 0, "stem_im2col: bad args");
-  const int64_t total = (int64_t)N * H * W * 8;
-  const int blocks = (int)std::min<int64_t>(8192, (total + 255) / 256);
+  const int64_t M = (int64_t)N * H * W;
+  const int blocks = (int)((M + 255) / 256);
   hipLaunchKernelGGL(stem_im2col_kernel, dim3(blocks), dim3(256), 0, st, x, cols, N, H, W);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -61,48 +74,77 @@ int stem_pack_weight(const u16* w27, u16* w64, int K, hipStream_t st) {
   return 0;
 }
 
-// Pool: feat[n][c] = bf16(mean_p act[n][p][c]); one thread per (n, c).
-__global__ void __launch_bounds__(256) head_pool_kernel(const u16* __restrict__ act, int N, int HW, int C,
-                                                       float* __restrict__ feat) {
-  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
-  if (i >= (int64_t)N * C) return;
-  const int64_t n = i / C, c = i - n * C;
-  const u16* a = act + n * HW * C + c;
-  float s = 0.f;
-  for (int p = 0; p < HW; ++p) s += bf2f(a[(int64_t)p * C]);
-  feat[i] = round_bf(s / (float)HW);  // avg_pool2d output is bf16 under autocast
-}
-
-// Linear: logits[n][j] = bf16(feat[n] . W[j] + bf16(b[j])); one thread per output, 16-byte loads.
-__global__ void __launch_bounds__(256) head_fc_kernel(const float* __restrict__ feat, int N, int C,
-                                                     const u16* __restrict__ wfc, const float* __restrict__ bfc,
-                                                     int ncls, float* __restrict__ logits) {
-  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
-  if (i >= (int64_t)N * ncls) return;
-  const int64_t n = i / ncls, j = i - n * ncls;
-  const f32x4* f = (const f32x4*)(feat + n * C);
-  const uint4* w = (const uint4*)(wfc + j * C);
-  float acc = 0.f;
-#pragma unroll 4
-  for (int c8 = 0; c8 < C / 8; ++c8) {
-    float wv[8];
-    unpack8(w[c8], wv);
-    const f32x4 a = f[2 * c8], b = f[2 * c8 + 1];
-    acc += a[0] * wv[0] + a[1] * wv[1] + a[2] * wv[2] + a[3] * wv[3] + b[0] * wv[4] + b[1] * wv[5] + b[2] * wv[6] +
-           b[3] * wv[7];
+// Pool + Linear in one launch, one workgroup per image:
+//   feat[n][c] = bf16(mean_p act[n][p][c])                 (avg_pool2d output is bf16 under autocast)
+//   logits[n][j] = bf16(feat[n] . W[j] + bf16(b[j]))         (bf16 linear under autocast)
+// The pool's threads own 8 channels each (16-B loads of consecutive channels, pixels split over
+// the workgroup's row groups and combined in LDS in a fixed order); for the Linear each wave takes
+// channel quarter `wave` and its lanes classes j0 + lane: an independent 8-wide FMA chain per
+// lane (no cross-lane reduction per class), the four quarter sums then added in LDS. Both
+// reductions have a fixed order: deterministic.
+__global__ void __launch_bounds__(256) head_fwd_kernel(const u16* __restrict__ act, int HW, int C,
+                                                      const u16* __restrict__ wfc, const float* __restrict__ bfc,
+                                                      int ncls, float* __restrict__ feat, float* __restrict__ logits) {
+  extern __shared__ float hsm[];  // [C] feat, then [256 / (C/8)][C] pool partials
+  const int n = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int tpr = C >> 3, groups = max(1, 256 / tpr);
+  float* fs = hsm;
+  float* part = hsm + C;
+  const u16* a = act + (int64_t)n * HW * C;
+  for (int c8 = t % tpr; c8 < tpr; c8 += 256) {  // (tpr > 256: threads loop over channel groups)
+    const int g = t / tpr;
+    if (g >= groups) break;
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int p = g; p < HW; p += groups) {
+      float v[8];
+      unpack8(*(const uint4*)(a + (int64_t)p * C + c8 * 8), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[g * C + c8 * 8 + k] = s[k];
   }
-  logits[i] = round_bf(acc + round_bf(bfc[j]));  // bf16 linear under autocast
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float s = 0.f;
+    for (int g = 0; g < groups; ++g) s += part[g * C + c];
+    const float f = round_bf(s / (float)HW);
+    fs[c] = f;
+    feat[(int64_t)n * C + c] = f;
+  }
+  __syncthreads();
+  // part is free again: [4 quarters][64 classes] partial dot products per class block
+  const int q8 = tpr / 4, cb = wave * q8 * 8;  // this wave's channel quarter (C % 32 == 0)
+  for (int j0 = 0; j0 < ncls; j0 += 64) {
+    const int j = j0 + lane;
+    float acc = 0.f;
+    if (j < ncls) {
+      const u16* w = wfc + (int64_t)j * C + cb;
+      for (int c8 = 0; c8 < q8; ++c8) {
+        float wv[8];
+        unpack8(*(const uint4*)(w + c8 * 8), wv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += fs[cb + c8 * 8 + k] * wv[k];
+      }
+    }
+    part[wave * 64 + lane] = acc;
+    __syncthreads();
+    if (t < 64 && j0 + t < ncls) {
+      const float s = part[t] + part[64 + t] + part[128 + t] + part[192 + t];
+      logits[(int64_t)n * ncls + j0 + t] = round_bf(s + round_bf(bfc[j0 + t]));
+    }
+    __syncthreads();
+  }
 }
 
 int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st) {
-  DTC_CHECK_ARG(act && wfc && bfc && feat && logits && N > 0 && HW > 0 && C > 0 && C % 8 == 0 && ncls > 0,
+  DTC_CHECK_ARG(act && wfc && bfc && feat && logits && N > 0 && HW > 0 && C > 0 && C % 32 == 0 && C <= 2048 &&
+                    ncls > 0,
                 "head_fwd: bad args");
-  hipLaunchKernelGGL(head_pool_kernel, dim3((int)(((int64_t)N * C + 255) / 256)), dim3(256), 0, st, act, N, HW, C,
-                     feat);
-  DTC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(head_fc_kernel, dim3((int)(((int64_t)N * ncls + 255) / 256)), dim3(256), 0, st, feat, N, C, wfc,
-                     bfc, ncls, logits);
+  const int groups = std::max(1, 256 / (C / 8));
+  const size_t lds = (size_t)(C + std::max(groups * C, 256)) * sizeof(float);
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(N), dim3(256), lds, st, act, HW, C, wfc, bfc, ncls, feat, logits);
   DTC_LAUNCH_CHECK();
   return 0;
 }

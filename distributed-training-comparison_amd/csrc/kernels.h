@@ -22,6 +22,7 @@ enum {
                         // (off by default: measured 5% slower at B=256, both chains fill the CUs)
   OPT_CONV_C64 = 9,     // persistent 64->64 channel 3x3 conv (conv_c64.hip) for layer1 FWD/DGRAD
   OPT_BN_FUSED_FIN = 10,  // 1: BN coefficients computed by the apply kernels (no finalize launches)
+  OPT_HALO_NHB2 = 11,     // 1: prefer the double-buffered-halo conv_halo tiles where they fit 2 WG/CU
   OPT_COUNT
 };
 int option_get(int id);

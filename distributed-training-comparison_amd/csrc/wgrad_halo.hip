@@ -114,18 +114,54 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Per-lane LDS byte offsets (within a stage) of every fragment half a step reads, computed once:
+  // A = the x halo read transposed at each tap's shift, B = the dy tile read transposed. The step
+  // loop is unrolled by two so the stage base is a constant the ds_read offset field absorbs: the
+  // MFMA stream carries no address arithmetic.
+  uint32_t aoff[2][9][2], boff[2][2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int row = wm * 144 + i * 16;  // GEMM row = tap*64 + channel
+      const int tap = row >> 6, cin = row & 63;
+      const int toff = (tap / 3) * W2 + (tap % 3);
+      const int unit = (cin >> 2) + (lane & 3);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ra = hm[ks][h] + toff;
+        const int f = (((ra >> 1) & 1) << 2) | (((ra >> 3) & 1) << 3);
+        aoff[ks][i][h] = (uint32_t)(ra * 128 + ((unit ^ f) << 3));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cin = wn * 32 + j * 16;
+      const int li = lane & 15, q = li >> 2, pp = li & 3, g = lane >> 4;
+      const int unit = (cin >> 2) + pp;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int kr = ks * 32 + g * 8 + q + 4 * h;
+        const int f = (((kr >> 1) & 1) << 2) | (((kr >> 3) & 1) << 3);
+        boff[ks][j][h] = (uint32_t)(HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
+      }
+    }
+  }
+  typedef __attribute__((address_space(3))) bf16x4_t lds_v4;
+  auto tr8 = [&](const char* sb, uint32_t o0, uint32_t o1) {
+    const bf16x4_t t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(sb + o0));
+    const bf16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(sb + o1));
+    return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
   auto compute = [&](const char* sb) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 bfr[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = frag_tr(sb + HALO_BYTES, wn * 32 + j * 16, ks, lane);
+      for (int j = 0; j < 2; ++j) bfr[j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
 #pragma unroll
       for (int i = 0; i < 9; ++i) {
-        const int row = wm * 144 + i * 16;  // GEMM row = tap*64 + channel
-        const int tap = row >> 6, cin = row & 63;
-        const int toff = (tap / 3) * W2 + (tap % 3);
-        const bf16x8 af = frag_halo(sb, cin, hm[ks][0] + toff, hm[ks][1] + toff, lane);
+        const bf16x8 af = tr8(sb, aoff[ks][i][0], aoff[ks][i][1]);
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
       }
@@ -136,12 +172,16 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   if (st_begin < st_end) {
     stage(smem, st_begin);
     const int nk = st_end - st_begin;
-    for (int it = 0; it < nk; ++it) {
+    auto one = [&](int it, char* cur, char* nxt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (it + 1 < nk) stage(smem + ((it + 1) & 1) * HSTAGE, st_begin + it + 1);
-      compute(smem + (it & 1) * HSTAGE);
+      if (it + 1 < nk) stage(nxt, st_begin + it + 1);
+      compute(cur);
+    };
+    for (int it = 0; it < nk; it += 2) {
+      one(it, smem, smem + HSTAGE);
+      if (it + 1 < nk) one(it + 1, smem + HSTAGE, smem);
     }
   }
 

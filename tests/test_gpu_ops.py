@@ -306,7 +306,7 @@ HALO_CASES = [
 
 
 @pytest.mark.parametrize("split", [0, 2])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", list(range(8)))
 @pytest.mark.parametrize("case", HALO_CASES)
 def test_conv_halo_configs(dtc, cuda, case, cfg, split):
     """Halo-tiled FWD (+BN statistics) and DGRAD (+residual) in each forced configuration
