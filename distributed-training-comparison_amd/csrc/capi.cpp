@@ -12,10 +12,10 @@
 #include <cstring>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {0}, {1}, {1}, {0}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {0}, {1}, {1}, {0}, {0}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
                                              "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
-                                             "conv_c64",     "bn_fused_fin", "halo_nhb2"};
+                                             "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse"};
 static std::atomic<int> g_epoch{0};
 int option_get(int id) { return g_opts[id].load(std::memory_order_relaxed); }
 int option_epoch() { return g_epoch.load(std::memory_order_relaxed); }
@@ -82,6 +82,18 @@ int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t*
                      void* ws, size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && dy && w && dx, "dtc_conv2d_dgrad: null argument");
   GUARD(return conv_dgrad(shape_of(d), dy, w, dx, res, (float*)ws, ws ? ws_bytes : 0, S(stream));)
+}
+
+int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
+                        const uint16_t* res, const uint16_t* ymask, const uint16_t* x1, const float* mean1,
+                        const float* invstd1, double* acc1, const uint16_t* x2, const float* mean2,
+                        const float* invstd2, double* acc2, void* ws, size_t ws_bytes, void* stream) {
+  DTC_CHECK_ARG(d && dy && w && dx && ymask && x1 && mean1 && invstd1 && acc1, "dtc_conv2d_dgrad_bn: null argument");
+  DTC_CHECK_ARG(!x2 || (mean2 && invstd2 && acc2), "dtc_conv2d_dgrad_bn: second BN arguments");
+  BnbArgs a;
+  a.ym = ymask; a.x1 = x1; a.mean1 = mean1; a.invstd1 = invstd1; a.acc1 = acc1;
+  a.x2 = x2; a.mean2 = mean2; a.invstd2 = invstd2; a.acc2 = acc2;
+  GUARD(return conv_dgrad(shape_of(d), dy, w, dx, res, (float*)ws, ws ? ws_bytes : 0, S(stream), nullptr, &a);)
 }
 
 int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* dw, float scale, void* ws,

@@ -31,6 +31,7 @@ struct C64Params {
   u16* out;        // NHWC, 64 channels
   const u16* res;  // DGRAD residual or null
   double* stats;   // FWD BN statistics [SLOTS][2][64] or null
+  BnbArgs bnb;     // DGRAD modes 3/4: fused BN-backward epilogue (one BN, bnb_epi.h)
   int N, H, W;
   uint32_t src_bytes, out_bytes;
   int rows, imgs, hb, nh, tiles_y, ntiles;
@@ -49,7 +50,9 @@ __device__ __forceinline__ bf16x8 lds_frag(uint32_t addr) {
   return *(const lds_bf16x8*)(size_t)addr;
 }
 
-// MODE 0: FWD (+ BN statistics), 1: DGRAD, 2: DGRAD + residual.
+// MODE 0: FWD (+ BN statistics), 1: DGRAD, 2: DGRAD + residual, 3: DGRAD -> BN backward (bnb_epi.h:
+// store dz = bf16(dx) * [ym > 0], accumulate sum(dz), sum(dz * xhat) like FWD's statistics),
+// 4: DGRAD + residual -> BN backward.
 // Software pipelined over tiles: the epilogue of tile k-1 (bf16 rounding, statistics, stores) is
 // issued in the same basic block as tile k's 288 MFMAs, so its VALU work fills MFMA issue gaps
 // instead of running after them on the wave's single SIMD (one wave per SIMD: nothing else would
@@ -58,7 +61,9 @@ __device__ __forceinline__ bf16x8 lds_frag(uint32_t addr) {
 template <int MODE>
 __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   constexpr int FM = 4, FN = 4;  // wave tile: 64 channels x 64 pixels
-  constexpr bool FWD = MODE == 0, RES = MODE == 2;
+  constexpr bool FWD = MODE == 0, RES = MODE == 2 || MODE == 4, BNB = MODE >= 3;
+  // VMEM ops one tile's epilogue leaves in flight per wave: stores (+ residual loads) (+ y, x loads)
+  constexpr int EPI_VM = 16 + (RES ? 16 : 0) + (BNB ? 32 : 0);
   __shared__ __attribute__((aligned(1024))) char smem[C64_WBYTES + 2 * C64_HBYTES];
   char* const halo = smem + C64_WBYTES;
   stamp_start(p.ts);
@@ -130,50 +135,83 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   const __amdgpu_buffer_rsrc_t rrsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)(RES ? p.res : p.out), 0, RES ? p.out_bytes : 0, 0x00020000);
   const uint32_t halo_lds = __builtin_amdgcn_readfirstlane(lds_u32(halo));
+  const __amdgpu_buffer_rsrc_t yrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(BNB ? p.bnb.ym : p.out), 0, BNB ? p.out_bytes : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(BNB ? p.bnb.x1 : p.out), 0, BNB ? p.out_bytes : 0, 0x00020000);
 
   const int rq = (lane >> 4) * 4;
-  float ssum[FM][4], ssq[FM][4];
+  // FWD: sum / sum of squares of the bf16 outputs; BNB: sum(dz) / sum(dz * xhat)
+  float ssum[FM][4], ssq[FM][4], bmean[FM][4], binv[FM][4];
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int i = 0; i < FM; ++i) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) ssum[i][t] = ssq[i][t] = 0.f;
+    for (int t = 0; t < 4; ++t) ssum[i][t] = ssq[i][t] = bmean[i][t] = binv[i][t] = 0.f;
+    if constexpr (BNB) {
+      const f32x4 m = *(const f32x4*)(p.bnb.mean1 + i * 16 + rq), v = *(const f32x4*)(p.bnb.invstd1 + i * 16 + rq);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bmean[i][t] = m[t];
+        binv[i][t] = v[t];
+      }
+    }
+  }
 
   // epilogue of one finished tile: exactly FM*FN buffer stores per wave (+ as many residual loads);
   // lanes of pixels past M, or of no tile (have == false), are dropped by the descriptor bound
   auto epilogue_col = [&](const f32x4 (&a)[FM][FN], int tile, bool have, int j) {
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
     const int px0 = tile * 256;  // tiles are 256 consecutive pixels
-    {
-      const int pix = px0 + bcol0 + j * 16 + fpx;
-      const bool ok = have && pix < M;
+    const int pix = px0 + bcol0 + j * 16 + fpx;
+    const bool ok = have && pix < M;
+    uint32_t off[FM];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int ch = i * 16 + rq;
-        const uint32_t off = ok ? (uint32_t)((pix * 64 + ch) * 2) : 0x80000000u;
-        float v[4];
-        if constexpr (FWD) {
+    for (int i = 0; i < FM; ++i) off[i] = ok ? (uint32_t)((pix * 64 + i * 16 + rq) * 2) : 0x80000000u;
+    // DGRAD operands of all FM fragments issued before any is used (one latency per column group)
+    i32x2 rr[FM], yy[FM], xx[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if constexpr (RES) rr[i] = __builtin_amdgcn_raw_buffer_load_b64(rrsrc, off[i], 0, 0);
+      if constexpr (BNB) {  // out-of-range lanes read zeros (descriptor bound): masked to 0, no sums
+        yy[i] = __builtin_amdgcn_raw_buffer_load_b64(yrsrc, off[i], 0, 0);
+        xx[i] = __builtin_amdgcn_raw_buffer_load_b64(xrsrc, off[i], 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      float v[4];
+      if constexpr (FWD) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          v[t] = round_bf(a[i][j][t]);
+          const float u = ok ? v[t] : 0.f;
+          ssum[i][t] += u;
+          ssq[i][t] += u * u;
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = a[i][j][t];
+        if constexpr (RES) {
+          v[0] += bf_lo((uint32_t)rr[i].x); v[1] += bf_hi((uint32_t)rr[i].x);
+          v[2] += bf_lo((uint32_t)rr[i].y); v[3] += bf_hi((uint32_t)rr[i].y);
+        }
+        if constexpr (BNB) {
+          const float yv[4] = {bf_lo((uint32_t)yy[i].x), bf_hi((uint32_t)yy[i].x), bf_lo((uint32_t)yy[i].y),
+                               bf_hi((uint32_t)yy[i].y)};
+          const float xv[4] = {bf_lo((uint32_t)xx[i].x), bf_hi((uint32_t)xx[i].x), bf_lo((uint32_t)xx[i].y),
+                               bf_hi((uint32_t)xx[i].y)};
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            v[t] = round_bf(a[i][j][t]);
-            const float u = ok ? v[t] : 0.f;
-            ssum[i][t] += u;
-            ssq[i][t] += u * u;
-          }
-        } else {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) v[t] = a[i][j][t];
-          if constexpr (RES) {
-            typedef int i32x2 __attribute__((ext_vector_type(2)));
-            const i32x2 rr = __builtin_amdgcn_raw_buffer_load_b64(rrsrc, off, 0, 0);
-            v[0] += bf_lo((uint32_t)rr.x); v[1] += bf_hi((uint32_t)rr.x);
-            v[2] += bf_lo((uint32_t)rr.y); v[3] += bf_hi((uint32_t)rr.y);
+            v[t] = yv[t] > 0.f ? round_bf(v[t]) : 0.f;
+            ssum[i][t] += v[t];
+            ssq[i][t] += v[t] * ((xv[t] - bmean[i][t]) * binv[i][t]);
           }
         }
-        typedef int i32x2 __attribute__((ext_vector_type(2)));
-        i32x2 wv;
-        wv.x = (int)pack_bf2(v[0], v[1]);
-        wv.y = (int)pack_bf2(v[2], v[3]);
-        __builtin_amdgcn_raw_buffer_store_b64(wv, orsrc, off, 0, 0);
       }
+      i32x2 wv;
+      wv.x = (int)pack_bf2(v[0], v[1]);
+      wv.y = (int)pack_bf2(v[2], v[3]);
+      __builtin_amdgcn_raw_buffer_store_b64(wv, orsrc, off[i], 0, 0);
     }
   };
   auto epilogue = [&](const f32x4 (&a)[FM][FN], int tile, bool have) {
@@ -194,7 +232,9 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     // this tile's halo has landed; the previous iteration's epilogue VMEM ops (FM*FN stores, plus
     // FM*FN residual loads) were issued after it and may still be in flight
     if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (RES) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if constexpr (EPI_VM >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+    else if constexpr (EPI_VM == 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else if constexpr (EPI_VM == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -235,8 +275,9 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   }
   if (k > 0) epilogue(accp, tilep, true);
 
-  if constexpr (FWD) {
-    if (p.stats != nullptr) {  // per-channel sums of this workgroup -> fp64 slot (once per workgroup)
+  if constexpr (FWD || BNB) {
+    double* const sacc = BNB ? p.bnb.acc1 : p.stats;
+    if (sacc != nullptr) {  // per-channel sums of this workgroup -> fp64 slot (once per workgroup)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __syncthreads();
       float* red = (float*)halo;  // [4 waves][64 ch][2]
@@ -259,7 +300,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
           s += red[(w * 64 + threadIdx.x) * 2 + 0];
           q += red[(w * 64 + threadIdx.x) * 2 + 1];
         }
-        double* st = p.stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * 64;
+        double* st = sacc + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * 64;
         unsafeAtomicAdd(st + threadIdx.x, (double)s);
         unsafeAtomicAdd(st + 64 + threadIdx.x, (double)q);
       }
@@ -290,8 +331,10 @@ bool conv_c64_ok(const ConvShape& s) {
 }
 
 int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, double* stats,
-             hipStream_t st, u64* ts) {
+             hipStream_t st, u64* ts, const BnbArgs* bnb) {
   DTC_CHECK_ARG(conv_c64_ok(s) && (mode == CONV_FWD || mode == CONV_DGRAD), "conv_c64: unsupported shape");
+  const bool fuse = mode == CONV_DGRAD && bnb != nullptr && bnb->ym != nullptr;
+  DTC_CHECK_ARG(!fuse || (bnb->x1 && bnb->mean1 && bnb->invstd1 && bnb->acc1), "conv_c64: BN-backward args");
   C64Params p{};
   p.src = src; p.w = w; p.out = out; p.res = res; p.stats = stats;
   p.N = s.N; p.H = s.H; p.W = s.W;
@@ -316,13 +359,22 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   p.fd_w = make_fastdiv(s.W);
   p.ts = ts;
   const int grid = std::min(p.ntiles, 256);
+  const bool in_kernel = fuse && bnb->x2 == nullptr;  // one BN per epilogue (layer1 has no projection)
+  if (in_kernel) p.bnb = *bnb;
   if (mode == CONV_FWD)
     hipLaunchKernelGGL(conv_c64_kernel<0>, dim3(grid), dim3(256), 0, st, p);
+  else if (in_kernel && res == nullptr)
+    hipLaunchKernelGGL(conv_c64_kernel<3>, dim3(grid), dim3(256), 0, st, p);
+  else if (in_kernel)
+    hipLaunchKernelGGL(conv_c64_kernel<4>, dim3(grid), dim3(256), 0, st, p);
   else if (res == nullptr)
     hipLaunchKernelGGL(conv_c64_kernel<1>, dim3(grid), dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(conv_c64_kernel<2>, dim3(grid), dim3(256), 0, st, p);
   DTC_LAUNCH_CHECK();
+  if (fuse && !in_kernel)
+    return bn_bwd_reduce(out, bnb->ym, bnb->x1, bnb->mean1, bnb->invstd1, bnb->acc1, bnb->x2, bnb->mean2,
+                         bnb->invstd2, bnb->acc2, out, M, 64, st);
   return 0;
 }
 

@@ -26,6 +26,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "tile_common.h"
+#include "bnb_epi.h"
 
 namespace dtc {
 
@@ -64,6 +65,7 @@ struct HConvParams {
   int tiles_a;  // Cout / BM
   int nchunk;   // Cin / 64 chunks per split
   int xcd_remap;
+  BnbArgs bnb;  // DGRAD: fused BN-backward prologue (bnb.ym null: off)
   FastDiv fd_hb, fd_w2, fd_spx, fd_w;
   u64* ts;
 };
@@ -332,19 +334,77 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
         unsafeAtomicAdd(st + p.Cout + a0 + threadIdx.x, (double)q);
       }
     }
+  } else if (p.bnb.ym != nullptr) {  // DGRAD (+ residual) -> dz = bf16(dx) * [y > 0] and BN sums
+    const bool dual = p.bnb.x2 != nullptr;
+    const bool has_res = p.res != nullptr;
+    float* red = (float*)smem;  // [WC][BM][3]
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int chl = arow0 + i * 16 + rq, ch = a0 + chl;
+      Bnb4 b;
+      bnb4_init(p.bnb, ch, dual, b);
+      // every operand of this channel group's FN fragments in flight at once (one latency, not FN)
+      uint2 rr[FN], yy[FN], xx[FN], x2[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int pix = px0 + bcol0 + j * 16 + cl;
+        const size_t o = (size_t)(pix < M ? pix : 0) * p.Cout + ch;
+        rr[j] = has_res ? *(const uint2*)(p.res + o) : uint2{0u, 0u};
+        yy[j] = *(const uint2*)(p.bnb.ym + o);
+        xx[j] = *(const uint2*)(p.bnb.x1 + o);
+        x2[j] = dual ? *(const uint2*)(p.bnb.x2 + o) : uint2{0u, 0u};
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int pix = px0 + bcol0 + j * 16 + cl;
+        const bool ok = pix < M;
+        float v[4] = {acc[i][j][0] + bf_lo(rr[j].x), acc[i][j][1] + bf_hi(rr[j].x), acc[i][j][2] + bf_lo(rr[j].y),
+                      acc[i][j][3] + bf_hi(rr[j].y)};
+        bnb4_vals(yy[j], xx[j], x2[j], ok, dual, v, b);
+        if (ok) {
+          uint2 wv;
+          wv.x = pack_bf2(v[0], v[1]);
+          wv.y = pack_bf2(v[2], v[3]);
+          *(uint2*)(p.out + (size_t)pix * p.Cout + ch) = wv;
+        }
+      }
+      bnb4_rowsum(b, dual);
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          red[(wc * BM + chl + t) * 3 + 0] = b.s[t];
+          red[(wc * BM + chl + t) * 3 + 1] = b.q1[t];
+          red[(wc * BM + chl + t) * 3 + 2] = b.q2[t];
+        }
+      }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < BM) {
+      float s = 0.f, q1 = 0.f, q2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WC; ++w) {
+        s += red[(w * BM + threadIdx.x) * 3 + 0];
+        q1 += red[(w * BM + threadIdx.x) * 3 + 1];
+        q2 += red[(w * BM + threadIdx.x) * 3 + 2];
+      }
+      bnb_commit(p.bnb, p.Cout, a0 + threadIdx.x, s, q1, q2, dual);
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int pix = px0 + bcol0 + j * 16 + cl;
       if (pix >= M) continue;
+      uint2 rr[FM];  // the residuals of all FM fragments in flight before the first store
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        rr[i] = p.res ? *(const uint2*)(p.res + (size_t)pix * p.Cout + a0 + arow0 + i * 16 + rq) : uint2{0u, 0u};
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int ch = a0 + arow0 + i * 16 + rq;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         const size_t o = (size_t)pix * p.Cout + ch;
         if (p.res) {
-          const uint2 rr = *(const uint2*)(p.res + o);
-          v[0] += bf_lo(rr.x); v[1] += bf_hi(rr.x); v[2] += bf_lo(rr.y); v[3] += bf_hi(rr.y);
+          v[0] += bf_lo(rr[i].x); v[1] += bf_hi(rr[i].x); v[2] += bf_lo(rr[i].y); v[3] += bf_hi(rr[i].y);
         }
         uint2 wv;
         wv.x = pack_bf2(v[0], v[1]);
@@ -467,7 +527,8 @@ static int launch_halo(const HConvParams& p, int cfg, dim3 grid, hipStream_t st)
 }
 
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
-              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
+              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
+              const BnbArgs* bnb) {
   DTC_CHECK_ARG(hp.cfg >= 0 && hp.cfg < kNumHaloCfgs && halo_shape_ok(s) && (mode == CONV_FWD || mode == CONV_DGRAD),
                 "conv_halo: unsupported shape / configuration");
   const HaloCfg& c = kHaloCfgs[hp.cfg];
@@ -496,9 +557,10 @@ int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, 
   p.fd_spx = make_fastdiv(p.rows * s.W);
   p.fd_w = make_fastdiv(s.W);
   p.ts = ts;
+  if (bnb != nullptr && split <= 1) p.bnb = *bnb;  // (split-K: the reduction kernel applies it)
   const dim3 grid(halo_tiles_b(s, p.rows, p.imgs) * p.tiles_a, split);
   DTC_TRY(mode == CONV_FWD ? launch_halo<0>(p, hp.cfg, grid, st) : launch_halo<1>(p, hp.cfg, grid, st));
-  if (split > 1) return splitk_reduce(slab, split, M, p.Cout, out, res, stats, st, ts);
+  if (split > 1) return splitk_reduce(slab, split, M, p.Cout, out, res, stats, st, ts, bnb);
   return 0;
 }
 

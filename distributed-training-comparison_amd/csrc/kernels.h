@@ -5,6 +5,7 @@
 #include <stddef.h>
 #include <algorithm>
 #include "common.h"
+#include "bnb_epi.h"
 
 namespace dtc {
 
@@ -23,6 +24,10 @@ enum {
   OPT_CONV_C64 = 9,     // persistent 64->64 channel 3x3 conv (conv_c64.hip) for layer1 FWD/DGRAD
   OPT_BN_FUSED_FIN = 10,  // 1: BN coefficients computed by the apply kernels (no finalize launches)
   OPT_HALO_NHB2 = 11,     // 1: prefer the double-buffered-halo conv_halo tiles where they fit 2 WG/CU
+  OPT_BNB_FUSE = 12,      // BN-backward reduction (mask + sums) fused into dgrad epilogues, bit mask of
+                          // kernels: 1 conv_c64, 2 conv_halo, 4 split-K reduce (others: separate pass).
+                          // Default 0: measured neutral (c64, split-K) to -1% (halo) at B=256 -- the
+                          // epilogue's strided 8-B y/x loads cost what the separate pass costs.
   OPT_COUNT
 };
 int option_get(int id);
@@ -48,9 +53,13 @@ ConvPlan plan_conv(const ConvShape& s, int mode);
 // first workgroups and every workgroup's exit time in s_memrealtime ticks (graph-safe per-call timing).
 int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
              size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
-// dx = conv_transpose(dy, w) (+ res), bf16 NHWC
+// dx = conv_transpose(dy, w) (+ res), bf16 NHWC.
+// bnb (optional): dx is the gradient of a post-ReLU BN output; store dz = dx * [bnb->ym > 0] instead
+// and accumulate the BN-backward sums (bn_bwd_reduce's work) -- in the epilogue where the kernel
+// supports it (conv_c64, conv_halo, split-K reduce), else by a bn_bwd_reduce pass after the conv.
+// dx may alias res (in place: each element is read and written by the same lane).
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
-               size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
+               size_t slab_bytes, hipStream_t st, u64* ts = nullptr, const BnbArgs* bnb = nullptr);
 // dw[k][0:dw_cols] (row stride dw_ld) = scale * sum_pixels dy (x) im2col(x); fp32
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
                float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
@@ -64,16 +73,19 @@ int conv_wgrad_halo(const ConvShape& s, const u16* x, const u16* dy, float* slab
 // Persistent 64-channel 3x3 stride-1 FWD / DGRAD (conv_c64.hip).
 bool conv_c64_ok(const ConvShape& s);
 int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, double* stats,
-             hipStream_t st, u64* ts);
+             hipStream_t st, u64* ts, const BnbArgs* bnb = nullptr);
 struct HaloPlan {
   int cfg, split;
 };
 HaloPlan conv_halo_plan(const ConvShape& s, int mode);
 size_t conv_halo_slab_bytes(const ConvShape& s, int mode);  // fp32 split-K slab the plan needs
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
-              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts);
+              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
+              const BnbArgs* bnb = nullptr);
+// bnb (optional, non-null ym): out = dz = bf16(sum + res) * [ym > 0] and the BN-backward sums of
+// dz into bnb->acc1 (/acc2) -- the work of bn_bwd_reduce on the value the reduction holds.
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
-                  hipStream_t st, u64* ts = nullptr);
+                  hipStream_t st, u64* ts = nullptr, const BnbArgs* bnb = nullptr);
 // per slot i of ts[n][DTC_PROF_SLOT_U64]: acc[i] += (max end - min start, 1) if stamped; cells reset
 int prof_accumulate(u64* ts, int n, u64* acc, hipStream_t st);
 

@@ -619,6 +619,24 @@ static int join_side(Net& n, hipStream_t st) {
   return 0;
 }
 
+// BN-backward reduction of the BN(s) whose post-ReLU output is `y`, for a dgrad epilogue (bnb_epi.h):
+// the conv producing dy stores dz = dy * [y > 0] and accumulates the sums bn_bwd_reduce would.
+static BnbArgs bnb_of(Net& n, size_t y, size_t x1, BNL& b1, size_t x2 = 0, BNL* b2 = nullptr) {
+  BnbArgs a;
+  a.ym = n.at<u16>(y);
+  a.x1 = n.at<u16>(x1);
+  a.mean1 = n.at<float>(b1.mean);
+  a.invstd1 = n.at<float>(b1.invstd);
+  a.acc1 = n.at<double>(b1.acc);
+  if (b2 != nullptr) {
+    a.x2 = n.at<u16>(x2);
+    a.mean2 = n.at<float>(b2->mean);
+    a.invstd2 = n.at<float>(b2->invstd);
+    a.acc2 = n.at<double>(b2->acc);
+  }
+  return a;
+}
+
 static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& cx, hipStream_t st) {
   n.prof_next = Net::PROF_BWD0;
   n.ev_next = 0;
@@ -631,6 +649,10 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   DTC_HIP(hipMemsetAsync(n.ws + n.acc_lo, 0, n.stats_hi - n.acc_lo, st));
   DTC_TRY(head_bwd(dlogits, n.at<float>(n.FEAT), n.wbf(n.fc_w), n.B, last.Hout * last.Wout, 512, n.ncls, gs,
                    n.gf(n.fc_w), n.gf(n.fc_b), G[0], n.at<float>(n.HEADWS), n.HEADWS_bytes, st));
+  // fuse: the dgrad producing a BN output's gradient also does that BN's backward reduction
+  // (captures keep the unfused order: they record dy and dz separately)
+  const bool fuse = !n.capture;
+  bool dz_ready = false;  // G[0] already holds the next BN's dz (the previous dgrad's fused epilogue)
   for (int bi = (int)n.blocks.size() - 1; bi >= 0; --bi) {
     BlockL& b = n.blocks[bi];
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
@@ -641,36 +663,57 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
     const std::string cp = n.capture ? "grad.layer" + std::to_string(bi / 2 + 1) + "." + std::to_string(bi % 2) : "";
     DTC_TRY(cap(n, cp + ".dy", G[0], st));
     // out = relu(bn2(c2) + shortcut): dz = dy * [out > 0]
-    DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(b.OUT), n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
-                          n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
-                          b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
-                          b.proj ? n.at<double>(b.bsc.acc) : nullptr, G[1], M, b.Cout, st));
-    DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[1], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
+    u16* dz2 = G[0];
+    if (!dz_ready) {
+      dz2 = G[1];
+      DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(b.OUT), n.at<u16>(b.C2), n.at<float>(b.b2.mean),
+                            n.at<float>(b.b2.invstd), n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
+                            b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
+                            b.proj ? n.at<double>(b.bsc.acc) : nullptr, G[1], M, b.Cout, st));
+    }
+    DTC_TRY(bn_bwd_coef_apply(n, b.b2, dz2, n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
                               b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st));
-    DTC_TRY(cap(n, cp + ".dz", G[1], st));
+    DTC_TRY(cap(n, cp + ".dz", dz2, st));
     DTC_TRY(cap(n, cp + ".dc2", dc2, st));
     if (b.proj) DTC_TRY(cap(n, cp + ".ds", dsc, st));
     // conv2: dW2 (side stream) and da1
     DTC_TRY(fork_side(n, st, &sd));
     PROF(2, conv_flops(b.c2.s), conv_wgrad(b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
-    PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts));
-    DTC_TRY(cap(n, cp + ".da1", G[4], st));
-    // a1 = relu(bn1(c1))
-    DTC_TRY(bn_bwd_reduce(G[4], n.at<u16>(b.A1), n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
-                          n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, G[4], M, b.Cout, st));
+    // a1 = relu(bn1(c1)): da1 -> dz1 (fused into the dgrad, or a separate reduction)
+    {
+      const BnbArgs bz = bnb_of(n, b.A1, b.C1, b.b1);
+      PROF(1, conv_flops(b.c2.s),
+           conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts, fuse ? &bz : nullptr));
+    }
+    if (!fuse) {
+      DTC_TRY(cap(n, cp + ".da1", G[4], st));
+      DTC_TRY(bn_bwd_reduce(G[4], n.at<u16>(b.A1), n.at<u16>(b.C1), n.at<float>(b.b1.mean),
+                            n.at<float>(b.b1.invstd), n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr,
+                            G[4], M, b.Cout, st));
+    }
     DTC_TRY(cap(n, cp + ".dz1", G[4], st));
     DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st));
     DTC_TRY(cap(n, cp + ".dc1", dc1, st));
     // conv1 (+ shortcut): weight grads (side stream), then the block-input gradient with the residual fused
     DTC_TRY(fork_side(n, st, &sd));
     PROF(2, conv_flops(b.c1.s), conv_wgrad(b.c1.s, in, dc1, n.gf(b.c1.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+    // the block input's gradient feeds the previous block's bn2 (+ its projection BN) or the stem BN
+    BnbArgs bp;
+    if (bi > 0) {
+      BlockL& pb = n.blocks[bi - 1];
+      bp = bnb_of(n, pb.OUT, pb.C2, pb.b2, pb.proj ? pb.S : 0, pb.proj ? &pb.bsc : nullptr);
+    } else {
+      bp = bnb_of(n, n.A0, n.C0, n.bn0);
+    }
+    const BnbArgs* bpp = fuse ? &bp : nullptr;
     if (b.proj) {
       PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
       PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
-      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts));
-    } else {
-      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[1], slab, n.slab_bytes, st, ts));
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts, bpp));
+    } else {  // fused: dz2 is G[0] and the dgrad updates it in place (residual read, dz written per element)
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], dz2, slab, n.slab_bytes, st, ts, bpp));
     }
+    dz_ready = fuse;
     if (b.proj) DTC_TRY(cap(n, cp + ".dxs", G[5], st));
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
     DTC_TRY(maybe_bucket(n, bi, cx, st));
@@ -678,10 +721,15 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   // stem: a0 = relu(bn1(conv1(x)))
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
   u16* dc0 = n.at<u16>(n.DC0);
-  DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(n.A0), n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
-                        n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, G[1], M0, 64, st));
-  DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[1], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st));
-  DTC_TRY(cap(n, "grad.stem.dz", G[1], st));
+  u16* dz0 = G[0];
+  if (!dz_ready) {
+    dz0 = G[1];
+    DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(n.A0), n.at<u16>(n.C0), n.at<float>(n.bn0.mean),
+                          n.at<float>(n.bn0.invstd), n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, G[1],
+                          M0, 64, st));
+  }
+  DTC_TRY(bn_bwd_coef_apply(n, n.bn0, dz0, n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st));
+  DTC_TRY(cap(n, "grad.stem.dz", dz0, st));
   DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
   DTC_TRY(join_side(n, st));  // the stem wgrad is the last kernel: run it on the main stream
   PROF(2, 2.0 * M0 * 64 * 27,

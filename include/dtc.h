@@ -65,6 +65,14 @@ int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w,
 /* dx = conv^T(dy, w) (+ res if non-NULL): the input gradient of Conv2d */
 int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
                      const uint16_t* res, void* ws, size_t ws_bytes, void* stream);
+/* The same dgrad when dx is the gradient of a post-ReLU BatchNorm output y = relu(bn(x1) [+ bn2(x2)])
+ * (net.py:41-44, 108): stores dz = bf16(dx) * [ymask > 0] in dx and ADDS the BN-backward sums into
+ * acc1 (and acc2 if x2) exactly as dtc_bn_bwd_reduce would on that dz -- in the conv's epilogue where
+ * the kernel has one (3x3 stride 1 and split-K paths), else as a second pass. dx may alias res. */
+int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
+                        const uint16_t* res, const uint16_t* ymask, const uint16_t* x1, const float* mean1,
+                        const float* invstd1, double* acc1, const uint16_t* x2, const float* mean2,
+                        const float* invstd2, double* acc2, void* ws, size_t ws_bytes, void* stream);
 /* dw[k][r][s][c] (fp32) = scale * sum over pixels of dy (x) im2col(x): the weight gradient */
 int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* dw, float scale,
                      void* ws, size_t ws_bytes, void* stream);

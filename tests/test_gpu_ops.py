@@ -385,3 +385,54 @@ def test_conv_c64_large_grid(dtc, cuda):
     torch.cuda.synchronize()
     assert rel_err(y1.float().cpu().numpy(), y0.float().cpu().numpy()) < 1e-2
     assert rel_err(d1.float().cpu().numpy(), d0.float().cpu().numpy()) < 1e-2
+
+
+BNB_CASES = [
+    # (N, H, W, C, K, R, stride, res, dual): dgrad output [N,H,W,C] feeding a BN backward
+    (3, 32, 32, 64, 64, 3, 1, False, False),   # conv_c64 mode 3
+    (3, 32, 32, 64, 64, 3, 1, True, False),    # conv_c64 mode 4 (in place on the residual)
+    (2, 16, 16, 128, 128, 3, 1, True, True),   # conv_halo, second BN (projection shortcut)
+    (5, 8, 8, 256, 256, 3, 1, True, False),    # conv_halo
+    (9, 4, 4, 512, 512, 3, 1, True, True),     # layer4 geometry (split-K reduce or implicit GEMM)
+    (4, 16, 16, 64, 128, 3, 2, True, True),    # stride-2 parity classes: separate reduction pass
+]
+
+
+@pytest.mark.parametrize("split", [0, 2])
+@pytest.mark.parametrize("case", BNB_CASES)
+def test_conv_dgrad_bn_fused(dtc, cuda, case, split):
+    """dtc_conv2d_dgrad_bn (BN-backward reduction in the dgrad epilogue) against the unfused pair
+    dtc_conv2d_dgrad -> dtc_bn_bwd_reduce on the same operands: dz bit-exact (both round the same
+    fp32 accumulator to bf16 and mask it), the fp64 sums equal up to summation order."""
+    N, H, W, C, K, R, st, with_res, dual = case
+    pad = 1
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+    g = np.random.default_rng(41)
+    b = lambda a: _to_dev_bf16(a, cuda)
+    t = lambda a: torch.from_numpy(np.asarray(a, np.float32)).to(cuda)
+    dy = b(_rand_bf16((N, P, Q, K), g))
+    w = b(_rand_bf16((K, R, R, C), g, 0.05))
+    res = _rand_bf16((N, H, W, C), g) if with_res else None
+    ym = b(_rand_bf16((N, H, W, C), g))
+    x1n = O.bf16(_rand_bf16((N, H, W, C), g, 1.5) + 0.3)
+    x2n = O.bf16(_rand_bf16((N, H, W, C), g, 0.7) - 0.1)
+    _, m1, i1, _, _ = O.bn_train_fwd(x1n.reshape(-1, C), np.ones(C, np.float32), np.zeros(C))
+    _, m2, i2, _, _ = O.bn_train_fwd(x2n.reshape(-1, C), np.ones(C, np.float32), np.zeros(C))
+    x1, x2 = b(x1n), b(x2n) if dual else None
+    mean2, inv2 = (t(m2), t(i2)) if dual else (None, None)
+    dtc._native.call("dtc_set_option", b"halo_split", split)
+    try:
+        dx = dtc.ops.conv2d_dgrad(dy, w, (H, W), st, pad, res=b(res) if with_res else None)
+        dz0, a10, a20 = dtc.ops.bn_bwd_reduce(dx, ym, x1, t(m1), t(i1), x2, mean2, inv2)
+        resd = b(res) if with_res else None
+        dz1, a11, a21 = dtc.ops.conv2d_dgrad_bn(dy, w, (H, W), st, pad, ym, x1, t(m1), t(i1), x2, mean2, inv2,
+                                                res=resd, out=resd)
+        torch.cuda.synchronize()
+    finally:
+        dtc._native.call("dtc_set_option", b"halo_split", 0)
+    np.testing.assert_array_equal(dz1.float().cpu().numpy(), dz0.float().cpu().numpy())
+    if with_res:
+        assert dz1.data_ptr() == resd.data_ptr()
+    for a1, a0 in [(a11, a10)] + ([(a21, a20)] if dual else []):
+        s1, s0 = a1.sum(0).cpu().numpy(), a0.sum(0).cpu().numpy()
+        np.testing.assert_allclose(s1, s0, rtol=1e-5, atol=1e-3 * np.abs(s0).max())

@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--variants", default="halo_conv=1;halo_conv=0")
     ap.add_argument("--layers", default="")
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
+    ap.add_argument("--fresh", action="store_true",
+                    help="re-write each call's input right before it (as the BN kernel does in the training step) "
+                         "and subtract the copy-only time: the conv reads a just-written input, not an L2-warm one")
     args = ap.parse_args()
     dtc = dtc_import.load()
     ops, nat = dtc.ops, dtc._native
@@ -71,6 +74,11 @@ def main():
         if name == "stem":
             fns.pop("dgrad")
         fns = {k: v for k, v in fns.items() if k in passes}
+        if args.fresh:
+            xs, dys = x.clone(), dy.clone()
+            copies = {"fwd": lambda: x.copy_(xs), "dgrad": lambda: dy.copy_(dys), "wgrad": lambda: dy.copy_(dys)}
+            fns = {k: (lambda f=f, c=copies[k]: (c(), f())) for k, f in fns.items()}
+            fns.update({"copy_" + k: copies[k] for k in list(fns)})
         for rnd in range(3):  # interleaved rounds
             for vi, var in enumerate(variants):
                 for k, v in var.items():
@@ -99,7 +107,11 @@ def main():
     for vi, var in enumerate(variants):
         print(f"=== variant {var}")
         tot_us, tot_fl = 0.0, 0.0
-        for (name, pname), (us, fl, cnt) in results[vi].items():
+        for (name, pname), (us, fl, cnt) in list(results[vi].items()):
+            if pname.startswith("copy_"):
+                continue
+            if (name, "copy_" + pname) in results[vi]:
+                us -= results[vi][(name, "copy_" + pname)][0]
             tot_us += us * cnt
             tot_fl += fl * cnt
             print(f"  {name:8s} {pname:6s} {us:8.1f} us  {fl / us / 1e6:7.1f} TF/s  x{cnt}")
