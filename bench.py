@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-live-roofline", action="store_true", help="skip the per-conv timing in the timed region")
+    ap.add_argument("--no-allreduce-probe", action="store_true", help="skip the N>1 all-reduce busBW probe")
+    ap.add_argument("--allreduce-probe", action="store_true", help="run the busBW probe at N=1 too (plumbing check)")
     ap.add_argument("--opt", action="append", default=[], help="native option NAME=VALUE (A/B runs)")
     args = ap.parse_args()
 
@@ -184,6 +186,22 @@ def main():
         prof_elapsed = timed(args.steps, args.warmup + args.steps + 2)
         dtc._native.call("dtc_rn18_profile_end", exe.handle, ms, fl, cnt)
 
+    # C4 all-reduce bus bandwidth on the Reducer's own RCCL communicator: the full gradient
+    # (11,220,132 fp32) and the bucket-size sweep of BASELINE config 5 (N > 1 only: one rank has
+    # no exchange). Runs after both timed regions, so it never overlaps the measured steps.
+    allreduce = None
+    if (world > 1 or args.allreduce_probe) and not args.no_allreduce_probe:
+        par = dtc.parallel
+        try:
+            grad_bytes = int(model.module.flat.grads.numel()) * 4
+            allreduce = {"grad": par.allreduce_probe(model.comm.allreduce_sum_, grad_bytes, dev, world),
+                         "sweep": [par.allreduce_probe(model.comm.allreduce_sum_, int(mb * 2**20), dev, world)
+                                   for mb in (1, 2, 5, 10, 25, 50, 100)],
+                         "transport": "native RCCL communicator (dtc_comm_allreduce_sum), fp32 SUM, device events",
+                         "peak_model": "(W-1) x 153 GB/s xGMI links per GPU (fully connected 8-GPU node)"}
+        except Exception as e:  # report, never hide; the throughput line stands on its own
+            allreduce = {"error": repr(e)}
+
     if rank == 0:
         conv_ms = sum(ms)
         conv_flops = sum(fl)
@@ -230,6 +248,8 @@ def main():
                                                 / BF16_PEAK_TFLOPS, 4),
             "final_loss": round(losses[-1], 4) if losses else None,
         }
+        if allreduce is not None:
+            out["allreduce"] = allreduce
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

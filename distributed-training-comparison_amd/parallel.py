@@ -90,6 +90,59 @@ def bucketed_allreduce_mean_(flat_grads: torch.Tensor, buckets: Sequence[Tuple[i
     return flat_grads
 
 
+XGMI_LINK_GBPS = 153.0  # per xGMI link and direction on MI355X; 7 links per GPU
+
+
+def xgmi_peak_busbw(world: int) -> float:
+    """Ceiling of all-reduce bus bandwidth on one fully connected 8-GPU node: each rank reaches
+    every peer over its own link, so W ranks drive (W-1) links per GPU (GB/s)."""
+    return XGMI_LINK_GBPS * max(0, min(world, 8) - 1)
+
+
+def busbw(nbytes: int, seconds: float, world: int) -> Tuple[float, float]:
+    """(algBW, busBW) in GB/s for a SUM all-reduce of nbytes taking `seconds` (nccl-tests
+    convention: busBW = algBW * 2(W-1)/W, the per-link traffic of a ring)."""
+    alg = nbytes / seconds / 1e9
+    return alg, alg * 2.0 * (world - 1) / world
+
+
+def allreduce_probe(allreduce_fn, nbytes: int, device, world: int, iters: int = 20, warmup: int = 5,
+                    group=None) -> dict:
+    """Time `iters` back-to-back SUM all-reduces of an fp32 buffer of nbytes on the current
+    stream (device events; on CPU wall clock) and return the slowest rank's algBW / busBW
+    against the xGMI ceiling. allreduce_fn(tensor) is the transport under test: the native RCCL
+    communicator the Reducer uses (Comm.allreduce_sum_) on GPUs, dist.all_reduce under gloo."""
+    import time
+
+    n = max(1, nbytes // 4)
+    buf = torch.ones(n, dtype=torch.float32, device=device)
+    cuda = buf.is_cuda
+    for _ in range(warmup):
+        allreduce_fn(buf)
+    if cuda:
+        torch.cuda.synchronize(device)
+    dist.barrier(group=group)
+    if cuda:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        allreduce_fn(buf)
+    if cuda:
+        e1.record()
+        torch.cuda.synchronize(device)
+        sec = e0.elapsed_time(e1) / 1e3 / iters
+    else:
+        sec = (time.perf_counter() - t0) / iters
+    t = torch.tensor([sec], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    sec = float(t.item())
+    alg, bus = busbw(n * 4, sec, world)
+    peak = xgmi_peak_busbw(world)
+    return {"bytes": n * 4, "us": round(sec * 1e6, 2), "algbw_GBps": round(alg, 2), "busbw_GBps": round(bus, 2),
+            "peak_GBps": peak, "frac": round(bus / peak, 4) if peak else None}
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, device_ids=None, output_device=None, dim=0, broadcast_buffers=True,
                  process_group=None, bucket_cap_mb=25, find_unused_parameters=False, **_ignored):

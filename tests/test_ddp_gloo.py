@@ -74,3 +74,35 @@ def test_two_rank_gloo(cap_mb):
     assert set(out.keys()) == {0, 1}
     for r, e in out.items():
         assert e < 1e-6, (r, e)
+
+
+def _probe_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    import dtc_import
+    dtc = dtc_import.load()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r = dtc.parallel.allreduce_probe(lambda t: dist.all_reduce(t), 1 << 20, torch.device("cpu"), world,
+                                         iters=3, warmup=1)
+        out[rank] = r
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_probe_gloo():
+    """The bench's busBW probe (parallel.allreduce_probe) over a 2-rank gloo group: both ranks
+    report the same (max-over-ranks) time and busBW = algBW * 2(W-1)/W against (W-1) xGMI links."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_probe_worker, args=(2, _port(), out), nprocs=2, join=True)
+    r0, r1 = out[0], out[1]
+    assert r0 == r1
+    assert r0["bytes"] == 1 << 20
+    assert abs(r0["busbw_GBps"] - r0["algbw_GBps"]) <= 0.011 + 1e-6 * r0["algbw_GBps"]  # W=2: factor 1
+    assert r0["peak_GBps"] == 153.0
+    import dtc_import
+    dtc = dtc_import.load()
+    alg, bus = dtc.parallel.busbw(8 << 20, 1e-3, 8)
+    assert abs(alg - 8.388608) < 1e-9 and abs(bus - alg * 1.75) < 1e-9
