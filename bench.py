@@ -209,7 +209,8 @@ def main():
         achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
         value = B * world * args.steps / elapsed
         out = {
-            "metric": "images/sec/node ResNet-18 CIFAR-100 DDP (weak-scaled, 256 images/GPU)",
+            "metric": f"images/sec/node ResNet-18 CIFAR-100 DDP (weak-scaled, {B} images/GPU"
+                      + (")" if S == 32 else f", {S}x{S})"),
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -244,7 +245,7 @@ def main():
                 "conv_calls_per_step": n_launch // max(1, args.steps),
                 "algorithmic_gflop_per_step": round(conv_flops / args.steps / 1e9, 3),
             },
-            "step_flop_fraction_of_peak": round(FLOPS_PER_IMAGE * B / (elapsed / args.steps) / 1e12
+            "step_flop_fraction_of_peak": round(FLOPS_PER_IMAGE * (S * S / 1024) * B / (elapsed / args.steps) / 1e12
                                                 / BF16_PEAK_TFLOPS, 4),
             "final_loss": round(losses[-1], 4) if losses else None,
         }

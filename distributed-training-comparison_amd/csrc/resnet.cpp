@@ -794,7 +794,10 @@ extern "C" {
 int dtc_rn18_create(dtc_net** out, int batch, int height, int width, int num_classes, float bucket_cap_mb) {
   DTC_CHECK_ARG(out != nullptr, "dtc_rn18_create: null out");
   DTC_CHECK_ARG(batch > 0 && height >= 8 && width >= 8 && num_classes > 0, "dtc_rn18_create: bad shape");
-  DTC_CHECK_ARG((int64_t)batch * height * width * 64 < (1ll << 31), "dtc_rn18_create: activation too large");
+  // every kernel addresses an activation with 32-bit byte offsets (buffer descriptors): the largest,
+  // [batch, height, width, 64] bf16, must stay below 2 GiB (224x224: batch <= 333)
+  DTC_CHECK_ARG((int64_t)batch * height * width * 64 * 2 < (1ll << 31),
+                "dtc_rn18_create: activation too large (batch*height*width*128 bytes >= 2 GiB)");
   dtc_net* h = new dtc_net();
   h->n.B = batch;
   h->n.H = height;
