@@ -98,6 +98,61 @@ def cpu_baseline(seconds: float):
                       f"{dt:.1f} s"}
 
 
+def bench_dp(args):
+    """BASELINE config 4: DataParallel (src/dp/trainer.py:27) -- ONE process driving every GPU in
+    --dp-devices (default: the first --gpus devices), global batch --batch split across them, the
+    reference DP step (zero_grad, autocast forward, CE, scaler.scale(loss).backward(), step,
+    update, loss.item()) with replicate / scatter / gather / reduce-add each step. Prints one
+    JSON line; `value` is global images/s (strong scaling: total batch fixed)."""
+    dev_ids = [int(d) for d in args.dp_devices.split(",")] if args.dp_devices else list(range(args.gpus))
+    dev = torch.device("cuda", dev_ids[0])
+    torch.cuda.set_device(dev)
+    dtc = dtc_import.load()
+    for kv in args.opt:
+        name, val = kv.split("=")
+        dtc._native.call("dtc_set_option", name.encode(), int(val))
+    torch.manual_seed(42)
+    model = dtc.DataParallel(dtc.ResNet18().to(dev), device_ids=dev_ids)
+    crit = dtc.CrossEntropyLoss()
+    opt = dtc.SGD(model.parameters(), lr=0.1, weight_decay=1e-4, momentum=0.9, nesterov=True)
+    scaler = dtc.GradScaler()
+    B, S = args.batch, args.size
+    templates = dtc.data.class_templates(100, S, S)
+    pool = [dtc.data.synthetic_batch(i, B, S, S, 100, dev, templates) for i in range(4)]
+    losses = []
+
+    def step(i):
+        img, label = pool[i % len(pool)]
+        opt.zero_grad()
+        with dtc.autocast():
+            loss = crit(model(img), label)
+        scaler.scale(loss).backward()
+        scaler.step(opt)
+        scaler.update()
+        losses.append(loss.item())
+
+    for i in range(args.warmup):
+        step(i)
+    for d in set(dev_ids):
+        torch.cuda.synchronize(d)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    for d in set(dev_ids):
+        torch.cuda.synchronize(d)
+    elapsed = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": f"images/sec ResNet-18 CIFAR-100 DataParallel (global batch {B}, one process)",
+        "value": round(B * args.steps / elapsed, 2), "unit": "images/sec", "n_gpus": len(set(dev_ids)),
+        "replicas": len(dev_ids), "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic, resident in HBM",
+        "config": {"workload": f"ResNet-18 DataParallel step, global batch {B}, {S}x{S}", "model": "ResNet18",
+                   "global_batch": B, "seq_len": None, "parallelism": f"dp-single-process x{len(dev_ids)}",
+                   "device_ids": dev_ids},
+        "final_loss": round(losses[-1], 4)}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,10 +166,15 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-live-roofline", action="store_true", help="skip the per-conv timing in the timed region")
+    ap.add_argument("--mode", choices=("ddp", "dp"), default="ddp",
+                    help="dp: BASELINE config 4, single-process DataParallel (global --batch over --gpus devices)")
+    ap.add_argument("--dp-devices", default="", help="dp mode: comma-separated replica devices (may repeat)")
     ap.add_argument("--no-allreduce-probe", action="store_true", help="skip the N>1 all-reduce busBW probe")
     ap.add_argument("--allreduce-probe", action="store_true", help="run the busBW probe at N=1 too (plumbing check)")
     ap.add_argument("--opt", action="append", default=[], help="native option NAME=VALUE (A/B runs)")
     args = ap.parse_args()
+    if args.mode == "dp":
+        return bench_dp(args)
 
     rank, world, local = init_dist()
     dev = torch.device("cuda", local)

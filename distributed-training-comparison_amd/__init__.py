@@ -15,7 +15,8 @@ from . import data, ops  # noqa: F401
 from .amp import GradScaler, autocast  # noqa: F401
 from .nn import BasicBlock, CrossEntropyLoss, ResNet, ResNet18  # noqa: F401
 from .optim import SGD  # noqa: F401
-from .parallel import DDP, Comm, DistributedDataParallel  # noqa: F401
+from .parallel import DDP, Comm, DataParallel, DistributedDataParallel  # noqa: F401
+from . import parallel  # noqa: F401
 from . import trainer  # noqa: F401
 
 _sys.modules.setdefault("dtc_amd", _sys.modules[__name__])

@@ -55,6 +55,24 @@ def conv2d_dgrad(dy, w, in_hw, stride, pad, res=None):
     return dx
 
 
+def conv2d_dgrad_bn(dy, w, in_hw, stride, pad, ymask, x1, mean1, invstd1, x2=None, mean2=None, invstd2=None,
+                    res=None, out=None):
+    """conv2d_dgrad fused with bn_bwd_reduce (dtc_conv2d_dgrad_bn): returns (dz, acc1, acc2) where
+    dz = bf16(dx [+ res]) * [ymask > 0]; `out` may be `res` (in place)."""
+    require_cuda(dy, w)
+    N = dy.shape[0]
+    K, R, S, Cc = w.shape
+    H, W = in_hw
+    d = conv_desc(N, H, W, Cc, K, R, S, stride, pad)
+    dz = out if out is not None else torch.empty(N, H, W, Cc, dtype=torch.bfloat16, device=dy.device)
+    acc1 = new_stats(Cc, dy.device)
+    acc2 = new_stats(Cc, dy.device) if x2 is not None else None
+    ws, nb = _ws(d, 1, dy.device)
+    call("dtc_conv2d_dgrad_bn", d, ptr(dy), ptr(w), ptr(dz), ptr(res), ptr(ymask), ptr(x1), ptr(mean1), ptr(invstd1),
+         ptr(acc1), ptr(x2), ptr(mean2), ptr(invstd2), ptr(acc2), ptr(ws), nb, stream_ptr())
+    return dz, acc1, acc2
+
+
 def conv2d_wgrad(x, dy, r, s, stride, pad, scale=1.0):
     """x [N,H,W,C] bf16, dy [N,P,Q,K] bf16 -> dw [K,R,S,C] fp32 (scaled)."""
     require_cuda(x, dy)

@@ -25,7 +25,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ._native import NativeError, call, lib, ptr, stream_ptr
+from ._native import NativeError, call, lib, ptr, require_cuda, stream_ptr
 
 DTYPE_F32, DTYPE_BF16, DTYPE_I64 = 0, 1, 2
 _DTYPES = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.int64: DTYPE_I64}
@@ -173,6 +173,13 @@ class DistributedDataParallel(nn.Module):
             self.comm.broadcast_(flat.nbt, 0)
             flat.refresh_bf16()
 
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """`module.`-prefixed load (the reference's test() on its DDP model, ddp/trainer.py:108-119);
+        the wrapped module's bf16 shadow is re-derived from the loaded fp32 parameters."""
+        res = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self.module.sync_weights()
+        return res
+
     def forward(self, *inputs, **kwargs):
         if self.broadcast_buffers and self.world_size > 1 and self.module.training:
             flat = self.module.flat
@@ -185,3 +192,140 @@ class DistributedDataParallel(nn.Module):
 
 
 DDP = DistributedDataParallel
+
+
+# ----------------------------------------------------------------------------- DataParallel
+class _Replica:
+    """A non-primary replica of a native ResNet: its own flat parameter / gradient / buffer
+    copies and executors on one device. Parameters and buffers are refreshed from the primary
+    (the wrapped module) by every forward, as torch's replicate() does (C5)."""
+
+    def __init__(self, model, device: torch.device):
+        from .nn import FlatState
+
+        self.model, self.device = model, device
+        with torch.cuda.device(device):
+            self.flat = FlatState(model.flat.layout, device)
+        self._executors = {}
+
+    def executor(self, batch: int, height: int, width: int):
+        from .nn import Executor
+
+        key = (batch, height, width)
+        exe = self._executors.get(key)
+        if exe is None:
+            with torch.cuda.device(self.device):
+                exe = Executor(self.flat, batch, height, width, self.model.num_classes, self.model._bucket_cap_mb)
+            self._executors[key] = exe
+        return exe
+
+    def pull(self, primary) -> None:
+        """Broadcast (replicate) of the primary's fp32 parameters, their bf16 shadow and the BN
+        buffers into this replica (device-to-device copies over xGMI for a peer GPU)."""
+        with torch.cuda.device(self.device):
+            self.flat.params.copy_(primary.params, non_blocking=True)
+            self.flat.params_bf16.copy_(primary.params_bf16, non_blocking=True)
+            self.flat.bufs.copy_(primary.bufs, non_blocking=True)
+            self.flat.nbt.copy_(primary.nbt, non_blocking=True)
+
+
+class _DPFn(torch.autograd.Function):
+    """scatter -> replicate -> parallel_apply -> gather (forward) and its reverse (backward:
+    gather's backward scatters dlogits, replicate's backward reduce-adds the replicas' gradients
+    into the primary's flat gradient buffer on device_ids[0])."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, dp):
+        model = dp.module
+        chunks = x.chunk(len(dp.device_ids))  # torch.nn.parallel.scatter's split of dim 0
+        train = model.training
+        runs = []
+        for i, c in enumerate(chunks):
+            dev = dp.devices[i]
+            with torch.cuda.device(dev):
+                if i == 0:
+                    exe = model.executor(c.shape[0], c.shape[2], c.shape[3])
+                else:
+                    rep = dp._replica(i)
+                    rep.pull(model.flat)
+                    exe = rep.executor(c.shape[0], c.shape[2], c.shape[3])
+                xi = c.to(dev, non_blocking=True).contiguous()
+                logits = torch.empty(c.shape[0], model.num_classes, dtype=torch.float32, device=dev)
+                gen = exe.forward(xi, logits, train)
+                runs.append((exe, gen, logits, xi))
+        ctx.dp, ctx.runs = dp, [(r[0], r[1]) for r in runs]
+        ctx.sizes = [c.shape[0] for c in chunks]
+        return torch.cat([r[2].to(dp.devices[0], non_blocking=True) for r in runs])  # gather (C7)
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        dp = ctx.dp
+        model = dp.module
+        parts = dlogits.contiguous().float().split(ctx.sizes)
+        for i, ((exe, gen), d) in enumerate(zip(ctx.runs, parts)):
+            if exe.generation != gen:
+                raise NativeError("DataParallel backward: a replica ran another forward since this graph was built")
+            dev = dp.devices[i]
+            with torch.cuda.device(dev):
+                exe.backward(d.to(dev, non_blocking=True).contiguous(), 1.0, None)
+        g0 = model.flat.grads
+        for i in range(1, len(ctx.runs)):  # ReduceAddCoalesced onto device_ids[0] (C6)
+            g0.add_(dp._replica(i).flat.grads.to(g0.device, non_blocking=True))
+        model._ensure_grads()
+        return None, None, None
+
+
+class DataParallel(nn.Module):
+    """nn.DataParallel(model) (reference src/dp/trainer.py:27) over native executors: ONE
+    process driving every device in ``device_ids``. Each forward splits the batch along dim 0,
+    refreshes every replica's parameters and BN buffers from the wrapped module (replicate), runs
+    the replicas' native forwards (kernel launches are asynchronous, so the devices run
+    concurrently from one host thread) and gathers the logits on device_ids[0]; backward runs the
+    replicas' native backwards on their logits-gradient slices and sums their gradients into the
+    module's. BatchNorm statistics are per replica, and only replica 0 -- the module itself --
+    keeps its running-statistics update, exactly as torch's replicate() leaves them.
+    A device id may repeat (replicas sharing one GPU) -- the single-GPU test of this path."""
+
+    def __init__(self, module, device_ids=None, output_device=None, dim=0):
+        super().__init__()
+        if dim != 0:
+            raise NotImplementedError("DataParallel scatters along dim 0 only (the reference's use)")
+        self.module = module
+        if device_ids is None:
+            device_ids = list(range(torch.cuda.device_count()))
+        self.device_ids = [d.index if isinstance(d, torch.device) else int(d) for d in device_ids]
+        self.devices = [torch.device("cuda", d) for d in self.device_ids]
+        if output_device is not None:
+            od = output_device.index if isinstance(output_device, torch.device) else int(output_device)
+            if od != self.device_ids[0]:
+                raise NotImplementedError("output_device must be device_ids[0]")
+        flat = module.flat  # raises unless the module already lives on a GPU
+        if flat.device.index != self.device_ids[0]:
+            raise NativeError(f"module must live on device_ids[0] (cuda:{self.device_ids[0]}), not {flat.device}")
+        module._grad_scale = 1.0
+        module._comm = None
+        self._replicas = {}
+
+    def _replica(self, i: int) -> _Replica:
+        rep = self._replicas.get(i)
+        if rep is None:
+            rep = _Replica(self.module, self.devices[i])
+            self._replicas[i] = rep
+        return rep
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        res = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self.module.sync_weights()  # the bf16 shadow the executors read
+        return res
+
+    def forward(self, x, *args, **kwargs):
+        if args or kwargs:
+            raise NotImplementedError("the native ResNet takes one input tensor")
+        if len(self.device_ids) == 1:
+            return self.module(x)
+        require_cuda(x)
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise ValueError(f"expected [N,3,H,W] input, got {tuple(x.shape)}")
+        if x.dtype != torch.float32:
+            x = x.float()
+        return _DPFn.apply(x, self.module._anchor, self)

@@ -23,7 +23,7 @@ from . import data as D
 from .amp import GradScaler, autocast
 from .nn import CrossEntropyLoss, ResNet18
 from .optim import SGD
-from .parallel import DDP
+from .parallel import DDP, DataParallel
 
 
 def load_config(argv=None, mode: str = "ddp"):
@@ -52,6 +52,9 @@ def load_config(argv=None, mode: str = "ddp"):
     p.add_argument("--synthetic-train", type=int, default=50000)
     p.add_argument("--synthetic-test", type=int, default=10000)
     p.add_argument("--max-steps", type=int, default=0, help="stop each epoch after N steps (0 = full epoch)")
+    if mode == "dp":  # not in the reference (nn.DataParallel takes every visible GPU): replica placement
+        p.add_argument("--device-ids", type=lambda v: [int(d) for d in v.split(",")], default=None,
+                       help="comma-separated GPU ids of the replicas (may repeat); default: all visible")
     return p.parse_args(argv)
 
 
@@ -80,12 +83,16 @@ class AverageMeter:
 
 
 class Trainer:
-    def __init__(self, hparams, model, scaler, rank: int = 0, ngpus_per_node: int = 1, distributed: bool = False):
+    def __init__(self, hparams, model, scaler, rank: int = 0, ngpus_per_node: int = 1, distributed: bool = False,
+                 data_parallel: bool = False):
         self.hparams = hparams
         self.rank = rank
         self.distributed = distributed
+        self.data_parallel = data_parallel
         self.device = torch.device("cuda", rank if distributed else torch.cuda.current_device())
         self.model = model.to(self.device)
+        if data_parallel:
+            self.model = DataParallel(self.model, device_ids=getattr(hparams, "device_ids", None))  # dp/trainer.py:27
         if distributed:
             self.model = DDP(self.model, device_ids=[rank], find_unused_parameters=True)   # ddp/trainer.py:31
             hparams.batch_size = int(hparams.batch_size / ngpus_per_node)                  # ddp/trainer.py:34
@@ -175,7 +182,8 @@ class Trainer:
             train_loss.update(loss.item())
             self.global_step += 1
             if self.rank == 0 and self.global_step % self.eval_step == 0:
-                logging.info(f"[{'DDP' if self.distributed else 'Single'} Version {self.version} Epoch {epoch}] "
+                tag = "DDP" if self.distributed else ("DP" if self.data_parallel else "Single")
+                logging.info(f"[{tag} Version {self.version} Epoch {epoch}] "
                              f"global step: {self.global_step}, train loss: {loss.item():.3f}")
         result = {"val_loss": 0.0, "val_acc": 0.0, "train_loss": train_loss.avg}
         if self.rank == 0:
@@ -188,6 +196,8 @@ class Trainer:
         return result
 
     def _module(self):
+        # DDP: rank 0 evaluates the unwrapped module; DP evaluates through the replicas
+        # (dp/trainer.py:121-129 calls self.model, the DataParallel wrapper)
         return self.model.module if self.distributed else self.model
 
     def validate(self, epoch: int) -> Tuple[float, float]:
@@ -222,11 +232,11 @@ class Trainer:
         return {"test_loss": test_loss.avg, "top_1_acc": top1.avg, "top_5_acc": top5.avg}
 
 
-def _run(hparams, rank, ngpus, distributed):
+def _run(hparams, rank, ngpus, distributed, data_parallel=False):
     D.fix_seed(hparams.seed)
     scaler = GradScaler() if hparams.amp else None
     model = ResNet18()
-    trainer = Trainer(hparams, model, scaler, rank, ngpus, distributed)
+    trainer = Trainer(hparams, model, scaler, rank, ngpus, distributed, data_parallel)
     version = trainer.fit()
     if rank == 0 and hparams.contain_test:
         path = glob.glob(os.path.join(hparams.ckpt_path, f"version-{version}/best_model_*.pt"))
@@ -252,8 +262,10 @@ def main(argv=None, mode: str = "ddp"):
     hparams = load_config(argv, mode)
     if mode == "single":
         return _run(hparams, 0, 1, False)
+    if mode == "dp":  # src/dp/main.py: one process, nn.DataParallel over every visible GPU
+        return _run(hparams, 0, torch.cuda.device_count(), False, data_parallel=True)
     if mode != "ddp":
-        raise NotImplementedError("DataParallel (src/dp) is SURVEY §8(f) row 1, not built yet")
+        raise ValueError(f"unknown mode {mode!r} (single, dp, ddp)")
     import torch.multiprocessing as mp
 
     ngpus_per_node = torch.cuda.device_count()

@@ -31,6 +31,10 @@ def test_accuracy_and_meter(dtc):
     assert m.avg == 3.5
 
 
-def test_dp_mode_fails_loudly(dtc):
-    with pytest.raises(NotImplementedError):
-        dtc.trainer.main([], "dp")
+def test_dp_flags_match_reference_defaults(dtc):
+    h = dtc.trainer.load_config([], "dp")  # src/dp/config.py:8-28
+    assert not hasattr(h, "dist_url") and h.device_ids is None
+    assert (h.epoch, h.batch_size, h.lr_decay_step_size, h.ckpt_path) == (100, 128, 60, "src/dp/checkpoints/")
+    assert dtc.trainer.load_config(["--device-ids", "0,0"], "dp").device_ids == [0, 0]
+    with pytest.raises(ValueError):
+        dtc.trainer.main([], "bogus")
