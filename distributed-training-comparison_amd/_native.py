@@ -76,6 +76,8 @@ _SIGS = {
     "dtc_cast_f32_bf16": (i32, [vp, vp, i64, vp]),
     "dtc_amp_check_finite": (i32, [vp, i64, vp, vp]),
     "dtc_amp_update_scale": (i32, [vp, vp, vp, vp, f32, f32, i32, vp]),
+    "dtc_cifar_augment": (i32, [vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, C.POINTER(f32), C.POINTER(f32), vp, vp,
+                                vp, vp]),
     "dtc_comm_unique_id_bytes": (sz, []),
     "dtc_comm_get_unique_id": (i32, [vp]),
     "dtc_comm_init": (i32, [C.POINTER(vp), i32, i32, vp, i32]),

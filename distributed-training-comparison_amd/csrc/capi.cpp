@@ -172,6 +172,13 @@ int dtc_amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, in
   return amp_update_scale(scale, inv_scale, growth_tracker, found_inf, growth, backoff, interval, S(stream));
 }
 
+int dtc_cifar_augment(const uint8_t* images, const int64_t* targets, int64_t n_images, const int64_t* index,
+                      const uint8_t* crop, const uint8_t* flip, int n, int h, int w, int pad, const float* mean,
+                      const float* stdv, float* out, int64_t* labels, int* status, void* stream) {
+  return cifar_augment(images, targets, n_images, index, crop, flip, n, h, w, pad, mean, stdv, out, labels, status,
+                       S(stream));
+}
+
 size_t dtc_comm_unique_id_bytes(void) { return comm_unique_id_bytes(); }
 int dtc_comm_get_unique_id(void* out) { GUARD(return comm_get_unique_id(out);) }
 int dtc_comm_init(dtc_comm** out, int rank, int world, const void* id, int device) {

@@ -178,4 +178,11 @@ int amp_check_finite(const float* g, int64_t n, int* found_inf, hipStream_t st);
 int amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, int* found_inf, float growth,
                      float backoff, int interval, hipStream_t st);
 
+// ------------------------------------------------------------------ input pipeline
+// gather + RandomCrop(pad) + RandomHorizontalFlip + ToTensor + Normalize: uint8 [N][h][w][3] ->
+// fp32 [n][3][h][w]; crop = [n][2] offsets (NULL: centre), flip = [n] (NULL: none).
+int cifar_augment(const uint8_t* images, const int64_t* targets, int64_t n_images, const int64_t* index,
+                  const uint8_t* crop, const uint8_t* flip, int n, int h, int w, int pad, const float* mean,
+                  const float* stdv, float* out, int64_t* labels, int* status, hipStream_t st);
+
 }  // namespace dtc

@@ -159,3 +159,83 @@ def get_tst_loader(batch_size: int, num_workers: int = 0, pin_memory: bool = Fal
     sampler = DistributedSampler(ds) if distributed else None
     return tud.DataLoader(ds, batch_size=batch_size, shuffle=False, sampler=sampler, num_workers=num_workers,
                           pin_memory=pin_memory)
+
+
+# ----------------------------------------------------------------------------- on-device input pipeline
+def synthetic_cifar_u8(n: int = 50000, height: int = 32, width: int = 32, num_classes: int = 100, seed: int = 1234):
+    """CIFAR-100 in its stored form (uint8 [n, h, w, 3] HWC + int64 targets), seeded synthetic:
+    pixel = clip(128 + 48*T[y] + 40*N(0,1)) with per-class templates T (numpy, CPU-deterministic)."""
+    rng = np.random.default_rng(seed)
+    templates = rng.standard_normal((num_classes, height, width, 3), dtype=np.float32)
+    targets = rng.integers(0, num_classes, n, dtype=np.int64)
+    images = np.empty((n, height, width, 3), np.uint8)
+    for s in range(0, n, 4096):  # bounded temporaries
+        e = min(n, s + 4096)
+        v = 128.0 + 48.0 * templates[targets[s:e]] + 40.0 * rng.standard_normal((e - s, height, width, 3),
+                                                                                  dtype=np.float32)
+        images[s:e] = np.clip(np.rint(v), 0, 255).astype(np.uint8)
+    return images, targets
+
+
+class DeviceLoader:
+    """``DataLoader(Subset(dataset, subset_idx), batch_size, sampler=sampler, drop_last=...)`` with
+    the reference's train (or valid/test) transform (src/ddp/dataset.py:43-64, 95-116) executed on
+    the GPU: the uint8 dataset stays resident in HBM (153.6 MB for CIFAR's 50k images); per epoch
+    the sampler's index list (bit-identical to torch's DistributedSampler) is composed with the
+    Subset map on the host and uploaded once; per batch one HIP launch gathers, crops, flips and
+    normalizes (``ops.cifar_augment``). Crop offsets / flips are drawn on the device from a
+    generator seeded with ``seed + epoch`` (torchvision draws them with the worker processes' CPU
+    RNG, which no run reproduces across worker counts either; distributions are the same:
+    offsets uniform on [0, 2*pad], flip with p = 0.5). Out-of-range indices are detected on the
+    device and raised at the end of the epoch (one host sync per epoch)."""
+
+    def __init__(self, images, targets, batch_size: int, subset_idx=None, sampler=None, train: bool = True,
+                 mean=CIFAR_MEAN, std=CIFAR_STD, pad: int = 4, drop_last: bool = True, seed: int = 0,
+                 device=None):
+        from . import ops
+
+        self._ops = ops
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.images = torch.as_tensor(images).to(dev).contiguous()
+        self.targets = torch.as_tensor(targets, dtype=torch.int64).to(dev).contiguous()
+        self.subset_idx = (np.arange(self.images.shape[0], dtype=np.int64) if subset_idx is None
+                           else np.asarray(subset_idx, np.int64))
+        self.batch_size, self.sampler, self.train = int(batch_size), sampler, bool(train)
+        self.mean, self.std, self.pad, self.drop_last = tuple(mean), tuple(std), int(pad), bool(drop_last)
+        self.seed, self.device, self.epoch = int(seed), dev, 0
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.last_params = None  # (index, crop, flip) of the last batch, for tests
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
+        if self.sampler is not None and hasattr(self.sampler, "set_epoch"):
+            self.sampler.set_epoch(epoch)
+
+    def _rows(self) -> np.ndarray:
+        order = np.fromiter(iter(self.sampler), np.int64) if self.sampler is not None else \
+            np.arange(len(self.subset_idx), dtype=np.int64)
+        return self.subset_idx[order]
+
+    def __len__(self) -> int:
+        n = len(self.sampler) if self.sampler is not None else len(self.subset_idx)
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+    def __iter__(self):
+        rows = torch.from_numpy(self._rows()).to(self.device)
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(self.seed + self.epoch)
+        B = self.batch_size
+        for k in range(len(self)):
+            idx = rows[k * B:(k + 1) * B]
+            n = idx.numel()
+            crop = flip = None
+            if self.train:
+                crop = torch.randint(0, 2 * self.pad + 1, (n, 2), dtype=torch.uint8, device=self.device,
+                                     generator=gen)
+                flip = torch.randint(0, 2, (n,), dtype=torch.uint8, device=self.device, generator=gen)
+            self.last_params = (idx, crop, flip)
+            yield self._ops.cifar_augment(self.images, idx, crop, flip, self.mean, self.std, self.pad,
+                                          targets=self.targets, status=self.status)
+        if int(self.status.item()):
+            self.status.zero_()
+            raise IndexError("DeviceLoader: a sampler index or crop offset was out of range this epoch")

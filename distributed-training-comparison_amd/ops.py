@@ -7,6 +7,8 @@ Nothing here computes on the host and there is no fallback path.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from ._native import ConvDesc, call, lib, ptr, require_cuda, stream_ptr
@@ -222,3 +224,28 @@ def amp_check_finite(g, found_inf):
 def amp_update_scale(scale, inv_scale, tracker, found_inf, growth, backoff, interval):
     call("dtc_amp_update_scale", ptr(scale), ptr(inv_scale), ptr(tracker), ptr(found_inf), float(growth),
          float(backoff), int(interval), stream_ptr())
+
+
+def cifar_augment(images, index, crop, flip, mean, std, pad=4, targets=None, out=None, labels=None, status=None):
+    """Gather + RandomCrop(pad) + RandomHorizontalFlip + ToTensor + Normalize on the GPU
+    (reference src/ddp/dataset.py:43-64). images: uint8 [N,H,W,3]; index: int64 [n] (None: 0..n-1);
+    crop: uint8 [n,2] (None: centre); flip: uint8 [n] (None: no flip). Returns (fp32 [n,3,H,W],
+    int64 labels [n] or None)."""
+    require_cuda(images, index, crop, flip, targets, out, labels, status)
+    if images.dtype != torch.uint8 or images.dim() != 4 or images.shape[3] != 3 or not images.is_contiguous():
+        raise ValueError(f"images must be contiguous uint8 [N,H,W,3], got {images.dtype} {tuple(images.shape)}")
+    n_images, h, w, _ = images.shape
+    n = index.numel() if index is not None else (crop.shape[0] if crop is not None else n_images)
+    for t, shape, dt in ((index, (n,), torch.int64), (crop, (n, 2), torch.uint8), (flip, (n,), torch.uint8),
+                         (targets, (n_images,), torch.int64)):
+        if t is not None and (t.dtype != dt or tuple(t.shape) != shape or not t.is_contiguous()):
+            raise ValueError(f"expected contiguous {dt} {shape}, got {t.dtype} {tuple(t.shape)}")
+    if out is None:
+        out = torch.empty(n, 3, h, w, dtype=torch.float32, device=images.device)
+    if targets is not None and labels is None:
+        labels = torch.empty(n, dtype=torch.int64, device=images.device)
+    m = (C.c_float * 3)(*[float(v) for v in mean])
+    s = (C.c_float * 3)(*[float(v) for v in std])
+    call("dtc_cifar_augment", ptr(images), ptr(targets), n_images, ptr(index), ptr(crop), ptr(flip), n, h, w, int(pad),
+         m, s, ptr(out), ptr(labels), ptr(status), stream_ptr())
+    return out, labels

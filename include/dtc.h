@@ -130,6 +130,21 @@ int dtc_amp_check_finite(const float* g, int64_t n, int* found_inf, void* stream
 int dtc_amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, int* found_inf, float growth_factor,
                          float backoff_factor, int growth_interval, void* stream);
 
+/* ------------------------------------------------------------------ input pipeline
+ * Replaces the host DataLoader workers' per-sample transforms (src/ddp/dataset.py:43-64:
+ * RandomCrop(32, padding=4) -> RandomHorizontalFlip -> ToTensor -> Normalize) and the
+ * Subset/DistributedSampler gather (dataset.py:95-98) with one launch per batch.
+ * images: uint8 [n_images][h][w][3] in device memory; targets: int64 [n_images] (may be NULL when
+ * labels is NULL); index: int64 [n] dataset rows (NULL: 0..n-1); crop: uint8 [n][2] (row, col)
+ * offsets into the zero-padded image, each in [0, 2*pad] (NULL: pad, pad = no crop shift);
+ * flip: uint8 [n], non-zero = mirror (NULL: none); mean/std: HOST pointers to 3 floats;
+ * out: fp32 [n][3][h][w]; labels: int64 [n] (NULL: skip); status: device int set to 1 when an index
+ * is out of range or an offset exceeds 2*pad (that image is written as zeros before normalize,
+ * label 0); never cleared by the call (NULL: skip). Requires w % 4 == 0 and h*w*3 <= 12 KiB. */
+int dtc_cifar_augment(const uint8_t* images, const int64_t* targets, int64_t n_images, const int64_t* index,
+                      const uint8_t* crop, const uint8_t* flip, int n, int h, int w, int pad, const float* mean,
+                      const float* std, float* out, int64_t* labels, int* status, void* stream);
+
 /* ------------------------------------------------------------------ RCCL communicator
  * Replaces the NCCL traffic of DistributedDataParallel (trainer.py:31): the construction-time
  * parameter broadcast, the per-forward buffer broadcast and the bucketed gradient all-reduce.

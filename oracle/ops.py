@@ -201,3 +201,41 @@ def grad_scaler_update(scale, tracker, found_inf, growth=2.0, backoff=0.5, inter
     if tracker == interval:
         return scale * growth, 0
     return scale, tracker
+
+
+# ----------------------------------------------------------------------------- input pipeline
+CIFAR_MEAN = (0.4914, 0.4822, 0.4465)  # reference src/ddp/dataset.py:43-46 (train / valid)
+CIFAR_STD = (0.2023, 0.1994, 0.2010)
+IMAGENET_MEAN = (0.485, 0.456, 0.406)  # reference src/ddp/dataset.py:139-142 (test loader)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def cifar_augment(images, targets, index, crop, flip, mean, std, pad=4):
+    """Per-sample host transforms of the reference's DataLoader (src/ddp/dataset.py:57-64, applied
+    through Subset(train_idx) + DistributedSampler, dataset.py:95-98) for explicit crop/flip draws.
+
+    The transforms live in third-party torchvision==0.8.2 (requirements.txt:4; absent here), whose
+    published algorithm is restated: RandomCrop(32, padding=4) = constant-0 pad by `pad` on every
+    side, then crop h x w at (i, j) with i, j drawn from [0, 2*pad]; RandomHorizontalFlip mirrors
+    columns after the crop; ToTensor = uint8 HWC -> fp32 CHW, `img.float().div(255)`; Normalize =
+    `sub_(mean).div_(std)` per channel. All arithmetic fp32 in that order (true divisions).
+    images uint8 [N,H,W,3]; index int [n]; crop int [n,2] or None (centre); flip [n] or None.
+    Returns (fp32 [n,3,H,W], int64 labels [n])."""
+    images = np.asarray(images, np.uint8)
+    n_img, h, w, _ = images.shape
+    index = np.arange(n_img) if index is None else np.asarray(index, np.int64)
+    n = index.shape[0]
+    padded = np.zeros((n_img, h + 2 * pad, w + 2 * pad, 3), np.uint8)
+    padded[:, pad:pad + h, pad:pad + w] = images
+    out = np.empty((n, 3, h, w), np.float32)
+    m = np.asarray(mean, np.float32)[:, None, None]
+    s = np.asarray(std, np.float32)[:, None, None]
+    for b in range(n):
+        i, j = (pad, pad) if crop is None else (int(crop[b][0]), int(crop[b][1]))
+        img = padded[index[b], i:i + h, j:j + w]  # [h, w, 3]
+        if flip is not None and flip[b]:
+            img = img[:, ::-1]
+        t = img.transpose(2, 0, 1).astype(np.float32) / np.float32(255)
+        out[b] = (t - m) / s
+    labels = None if targets is None else np.asarray(targets, np.int64)[index]
+    return out, labels

@@ -185,3 +185,54 @@ def test_synthetic_stream_matches_golden_generator(dtc):
     assert y.tolist()[:16] == lc["stream_check"]["y0"]
     assert abs(float(x.sum()) - lc["stream_check"]["x0_sum"]) < 1e-3
     np.testing.assert_allclose(x[0, 0, 0, :8].numpy(), lc["stream_check"]["x0_00"], rtol=1e-6)
+
+
+def test_augment_oracle_matches_torch_transform_restatement():
+    """oracle.cifar_augment == the tensor-op form of torchvision 0.8.2's train transform
+    (RandomCrop(32, padding=4) -> RandomHorizontalFlip -> ToTensor -> Normalize, dataset.py:57-64),
+    bit-exact. torchvision is absent here (parity for this row is pinned by this restatement and
+    the reference's call-site constants, not by reference-produced vectors)."""
+    import torch.nn.functional as F
+
+    from oracle import ops as O
+
+    g = np.random.default_rng(0)
+    imgs = g.integers(0, 256, (12, 32, 32, 3), dtype=np.uint8)
+    idx = g.integers(0, 12, 9)
+    crop = g.integers(0, 9, (9, 2))
+    crop[0] = (0, 8)
+    flip = g.integers(0, 2, 9)
+    tg = g.integers(0, 100, 12)
+    out, lab = O.cifar_augment(imgs, tg, idx, crop, flip, O.CIFAR_MEAN, O.CIFAR_STD)
+    x = torch.from_numpy(imgs).permute(0, 3, 1, 2)
+    mean = torch.as_tensor(O.CIFAR_MEAN)[:, None, None]
+    std = torch.as_tensor(O.CIFAR_STD)[:, None, None]
+    for b in range(9):
+        p = F.pad(x[idx[b]], (4, 4, 4, 4))
+        c = p[:, crop[b][0]:crop[b][0] + 32, crop[b][1]:crop[b][1] + 32]
+        if flip[b]:
+            c = c.flip(-1)
+        t = c.float().div(255).sub_(mean).div_(std)
+        assert np.array_equal(t.numpy(), out[b]), b
+    assert np.array_equal(lab, tg[idx])
+    # valid transform: no crop shift, no flip
+    out2, _ = O.cifar_augment(imgs, None, None, None, None, O.CIFAR_MEAN, O.CIFAR_STD)
+    t = x.float().div(255).sub_(mean).div_(std)
+    assert np.array_equal(t.numpy(), out2)
+
+
+def test_device_loader_rows_follow_subset_and_sampler(dtc):
+    """Host side of the DeviceLoader (no GPU needed): per-epoch rows = Subset map applied to the
+    DistributedSampler stream; drop_last batch count (dataset.py:95-108)."""
+    imgs, tg = dtc.data.synthetic_cifar_u8(n=100, seed=3)
+    assert imgs.shape == (100, 32, 32, 3) and imgs.dtype == np.uint8
+    imgs2, tg2 = dtc.data.synthetic_cifar_u8(n=100, seed=3)
+    assert np.array_equal(imgs, imgs2) and np.array_equal(tg, tg2)
+    sub = np.arange(100)[::-1][10:]
+    s = dtc.data.DistributedSampler(range(90), num_replicas=4, rank=1)
+    ld = dtc.data.DeviceLoader(imgs, tg, 8, subset_idx=sub, sampler=s, device="cpu")
+    ld.set_epoch(2)
+    assert np.array_equal(ld._rows(), sub[dtc.data.shard_indices(90, 4, 1, epoch=2)])
+    assert len(ld) == 23 // 8
+    ld2 = dtc.data.DeviceLoader(imgs, tg, 8, subset_idx=sub, train=False, drop_last=False, device="cpu")
+    assert len(ld2) == 12 and np.array_equal(ld2._rows(), sub)
