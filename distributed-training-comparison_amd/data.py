@@ -24,6 +24,8 @@ import torch.utils.data as tud
 
 CIFAR_MEAN = (0.4914, 0.4822, 0.4465)  # dataset.py:43-46
 CIFAR_STD = (0.2023, 0.1994, 0.2010)
+IMAGENET_MEAN = (0.485, 0.456, 0.406)  # dataset.py:139-142 (test loader)
+IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
 def fix_seed(seed: int) -> None:

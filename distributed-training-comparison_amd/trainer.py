@@ -52,6 +52,8 @@ def load_config(argv=None, mode: str = "ddp"):
     p.add_argument("--synthetic-train", type=int, default=50000)
     p.add_argument("--synthetic-test", type=int, default=10000)
     p.add_argument("--max-steps", type=int, default=0, help="stop each epoch after N steps (0 = full epoch)")
+    p.add_argument("--device-data", action="store_true", default=False,
+                   help="HBM-resident uint8 dataset + on-GPU crop/flip/normalize (data.DeviceLoader)")
     if mode == "dp":  # not in the reference (nn.DataParallel takes every visible GPU): replica placement
         p.add_argument("--device-ids", type=lambda v: [int(d) for d in v.split(",")], default=None,
                        help="comma-separated GPU ids of the replicas (may repeat); default: all visible")
@@ -99,12 +101,15 @@ class Trainer:
         self.scaler = scaler
         self.optimizer, self.lr_scheduler = self.configure_optimizers()
         self.criterion = CrossEntropyLoss()
-        ds = D.SyntheticCIFAR100(n=hparams.synthetic_train)
-        self.train_loader, self.train_sampler, self.val_loader = D.get_trn_val_loader(
-            batch_size=hparams.batch_size, valid_size=0.1, num_workers=hparams.workers, pin_memory=True,
-            distributed=distributed, dataset=ds)
-        self.test_loader = D.get_tst_loader(batch_size=hparams.batch_size, num_workers=1, pin_memory=True,
-                                            distributed=distributed, n=hparams.synthetic_test)
+        if getattr(hparams, "device_data", False):
+            self._device_loaders(hparams, distributed)
+        else:
+            ds = D.SyntheticCIFAR100(n=hparams.synthetic_train)
+            self.train_loader, self.train_sampler, self.val_loader = D.get_trn_val_loader(
+                batch_size=hparams.batch_size, valid_size=0.1, num_workers=hparams.workers, pin_memory=True,
+                distributed=distributed, dataset=ds)
+            self.test_loader = D.get_tst_loader(batch_size=hparams.batch_size, num_workers=1, pin_memory=True,
+                                                distributed=distributed, n=hparams.synthetic_test)
         self.global_step = 0
         self.global_top1_acc = 0.0
         self.eval_step = hparams.eval_step
@@ -122,6 +127,27 @@ class Trainer:
             with open(os.path.join(self.save_path, "hparams.json"), "w") as f:
                 json.dump(vars(hparams), f, indent=1)
             self._scalars = open(os.path.join(self.save_path, "scalars.jsonl"), "a")
+
+    def _device_loaders(self, hparams, distributed):
+        """--device-data: the loaders of dataset.py:15-168 with the transforms on the GPU
+        (D.DeviceLoader over HBM-resident uint8 CIFAR-shaped data): same 45k/5k split, the same
+        DistributedSampler (DDP) or per-epoch random order (single/dp), drop_last on train, train
+        transform with crop+flip, valid without, test normalized with the ImageNet statistics of
+        dataset.py:139-142 and sharded by a DistributedSampler under DDP (dataset.py:158)."""
+        imgs, tg = D.synthetic_cifar_u8(n=hparams.synthetic_train, seed=hparams.seed)
+        train_idx, valid_idx = D.train_valid_split(len(tg), 0.1, True)
+        sampler = (D.DistributedSampler(train_idx) if distributed
+                   else torch.utils.data.SubsetRandomSampler(list(range(len(train_idx)))))
+        bs = hparams.batch_size
+        self.train_loader = D.DeviceLoader(imgs, tg, bs, subset_idx=train_idx, sampler=sampler, train=True,
+                                           seed=hparams.seed, device=self.device)
+        self.train_sampler = self.train_loader
+        self.val_loader = D.DeviceLoader(imgs, tg, bs, subset_idx=valid_idx, train=False, drop_last=False,
+                                         device=self.device)
+        timgs, ttg = D.synthetic_cifar_u8(n=hparams.synthetic_test, seed=hparams.seed + 1)
+        tsampler = D.DistributedSampler(range(len(ttg)), shuffle=False) if distributed else None
+        self.test_loader = D.DeviceLoader(timgs, ttg, bs, sampler=tsampler, train=False, drop_last=False,
+                                          mean=D.IMAGENET_MEAN, std=D.IMAGENET_STD, device=self.device)
 
     def _log_scalar(self, tag, values, step):
         if self.rank == 0:
@@ -145,7 +171,7 @@ class Trainer:
 
     def fit(self):
         for epoch in range(self.hparams.epoch):
-            if self.distributed:
+            if self.distributed or isinstance(self.train_loader, D.DeviceLoader):
                 self.train_sampler.set_epoch(epoch)                                       # trainer.py:125
             logging.info(f"* Learning Rate: {self.optimizer.param_groups[0]['lr']:.5f}")
             result = self._train_epoch(epoch)

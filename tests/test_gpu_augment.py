@@ -115,3 +115,18 @@ def test_device_loader_trains_native_resnet(dtc, cuda):
         opt.step()
         losses.append(loss.item())
     assert len(losses) == 8 and all(np.isfinite(losses))
+
+
+def test_single_trainer_with_device_data(dtc, cuda, tmp_path):
+    """`train.py single --device-data`: the reference loop fed by DeviceLoaders (train with
+    crop/flip, valid, ImageNet-normalized test) through fit -> validate -> checkpoint -> test."""
+    import os
+
+    t = dtc.trainer.main(["--epoch", "2", "--batch-size", "64", "--max-steps", "3", "--amp", "--contain-test",
+                          "--synthetic-train", "1000", "--synthetic-test", "200", "--device-data",
+                          "--ckpt-path", str(tmp_path)], "single")
+    assert isinstance(t.train_loader, dtc.data.DeviceLoader)
+    assert t.train_loader.epoch == 1 and len(t.train_loader) == 900 // 64
+    assert len(t.val_loader) == 2 and len(t.test_loader) == 4
+    assert t.test_loader.mean == dtc.data.IMAGENET_MEAN
+    assert os.path.exists(os.path.join(str(tmp_path), "version-0", "experiment.log"))
