@@ -171,6 +171,8 @@ def main():
     ap.add_argument("--dp-devices", default="", help="dp mode: comma-separated replica devices (may repeat)")
     ap.add_argument("--no-allreduce-probe", action="store_true", help="skip the N>1 all-reduce busBW probe")
     ap.add_argument("--allreduce-probe", action="store_true", help="run the busBW probe at N=1 too (plumbing check)")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="SyncBatchNorm (off in the reference); at N=1 a one-rank communicator forces the sync path")
     ap.add_argument("--opt", action="append", default=[], help="native option NAME=VALUE (A/B runs)")
     args = ap.parse_args()
     if args.mode == "dp":
@@ -185,7 +187,12 @@ def main():
 
     torch.manual_seed(42)
     model = dtc.ResNet18().to(dev)
+    if args.sync_bn:
+        model = dtc.SyncBatchNorm.convert_sync_batchnorm(model)
     model = dtc.DDP(model, device_ids=[local], find_unused_parameters=True, bucket_cap_mb=args.bucket_mb)
+    if args.sync_bn and world == 1:  # torch keeps local statistics at W=1; force the path to time it
+        model.sync_comm = dtc.parallel.Comm(0, 1, dtc.parallel.Comm.unique_id(), local)
+        model.module.set_sync_bn(model.sync_comm)
     crit = dtc.CrossEntropyLoss()
     opt = dtc.SGD(model.parameters(), lr=0.1, weight_decay=1e-4, momentum=0.9, nesterov=True)
     scaler = dtc.GradScaler()
@@ -286,7 +293,8 @@ def main():
                                    f"SGD-Nesterov + GradScaler, DDP bucket {args.bucket_mb} MB",
                        "model": "ResNet18 (CIFAR, src/ddp/net.py)", "global_batch": B * world, "seq_len": None,
                        "parallelism": f"dp{world}", "per_gpu_batch": B, "image_size": S,
-                       "step_barrier": not args.no_barrier, "loss_item": not args.no_item},
+                       "step_barrier": not args.no_barrier, "loss_item": not args.no_item,
+                       "sync_bn": bool(args.sync_bn)},
             "roofline": {
                 "bound": "mfma",
                 "achieved": round(achieved, 2) if achieved else None,

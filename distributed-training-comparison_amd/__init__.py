@@ -13,7 +13,7 @@ import sys as _sys
 from . import _native  # noqa: F401  (loads libdtc_amd.so; raises if it is missing)
 from . import data, ops  # noqa: F401
 from .amp import GradScaler, autocast  # noqa: F401
-from .nn import BasicBlock, CrossEntropyLoss, ResNet, ResNet18  # noqa: F401
+from .nn import BasicBlock, CrossEntropyLoss, ResNet, ResNet18, SyncBatchNorm  # noqa: F401
 from .optim import SGD  # noqa: F401
 from .parallel import DDP, Comm, DataParallel, DistributedDataParallel  # noqa: F401
 from . import parallel  # noqa: F401

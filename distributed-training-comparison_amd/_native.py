@@ -105,6 +105,7 @@ _SIGS = {
     "dtc_rn18_profile_end": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), Pi32]),
     "dtc_rn18_forward": (i32, [vp, vp, vp, i32, vp]),
     "dtc_rn18_backward": (i32, [vp, vp, f32, vp, vp]),
+    "dtc_rn18_set_sync_bn": (i32, [vp, vp]),
     "dtc_rn18_dlogits_buffer": (i32, [vp, C.POINTER(sz)]),
 }
 

@@ -37,6 +37,7 @@ static ncclDataType_t to_nccl(int dtype) {
   switch (dtype) {
     case 1: return ncclBfloat16;
     case 2: return ncclInt64;
+    case 3: return ncclFloat64;
     default: return ncclFloat32;
   }
 }

@@ -111,6 +111,10 @@ struct Net {
   std::vector<Act> acts;
   // optional capture of backward intermediates (parity tests): name -> slot in the workspace
   bool capture = false;
+  // SyncBatchNorm: per-channel BN sums all-reduced over this communicator
+  // (its own, never the Reducer's, so the two collective streams cannot interleave on one comm)
+  Comm* sync = nullptr;
+  int sync_world = 1;
   std::vector<Act> caps;
   // bound memory
   char* ws = nullptr;
@@ -391,7 +395,7 @@ static void drop_graphs(Net& n) {
   n.bwd_segs.clear();
 }
 static bool graphs_on(Net& n) {
-  if (n.capture || option_get(OPT_GRAPHS) == 0) return false;
+  if (n.capture || n.sync || option_get(OPT_GRAPHS) == 0) return false;
   if (n.graph_epoch != option_epoch()) {  // options are baked into captured launches
     drop_graphs(n);
     n.graph_epoch = option_epoch();
@@ -434,6 +438,13 @@ static int bn_finalize_fwd(Net& n, BNL& b, int64_t count, bool train, hipStream_
 
 static bool bn_fused() { return option_get(OPT_BN_FUSED_FIN) != 0; }
 
+// SUM all-reduce of one BN's fp64 partial-sum slots ([DTC_STAT_SLOTS][2][C]) on the compute
+// stream: every apply kernel folds the slots, so after this each rank folds the global sums
+// (torch SyncBatchNorm's all-gather of per-rank mean/invstd/count, as one reduction).
+static int sync_bn_sums(Net& n, size_t off, int C, hipStream_t st) {
+  return comm_allreduce(n.sync, n.ws + off, (size_t)DTC_STAT_SLOTS * 2 * C, 3, st);
+}
+
 static BnFwdArgs fwd_args(Net& n, BNL& b, int64_t count) {
   BnFwdArgs a;
   a.stats = n.at<double>(b.stats);
@@ -451,13 +462,18 @@ static BnFwdArgs fwd_args(Net& n, BNL& b, int64_t count) {
 // BN (+ residual / second BN) + ReLU after the producing conv(s): y = relu(bn(x) [+ x2 | + bn2(x2)])
 static int bn_act(Net& n, int mode, BNL& b, const u16* x, BNL* b2, const u16* x2, u16* y, int64_t M, bool train,
                   hipStream_t st) {
+  if (train && n.sync) {  // SyncBN: global per-channel (sum, sumsq) slots, global element count
+    DTC_TRY(sync_bn_sums(n, b.stats, b.C, st));
+    if (b2) DTC_TRY(sync_bn_sums(n, b2->stats, b2->C, st));
+  }
+  const int64_t cnt = train && n.sync ? M * n.sync_world : M;  // elements behind each channel's stats
   if (train && bn_fused()) {
-    const BnFwdArgs a1 = fwd_args(n, b, M);
-    const BnFwdArgs a2 = b2 ? fwd_args(n, *b2, M) : BnFwdArgs{};
+    const BnFwdArgs a1 = fwd_args(n, b, cnt);
+    const BnFwdArgs a2 = b2 ? fwd_args(n, *b2, cnt) : BnFwdArgs{};
     return bn_fin_apply(mode, x, a1, x2, b2 ? &a2 : nullptr, y, M, b.C, st);
   }
-  DTC_TRY(bn_finalize_fwd(n, b, M, train, st));
-  if (b2) DTC_TRY(bn_finalize_fwd(n, *b2, M, train, st));
+  DTC_TRY(bn_finalize_fwd(n, b, cnt, train, st));
+  if (b2) DTC_TRY(bn_finalize_fwd(n, *b2, cnt, train, st));
   const float* s1 = n.at<float>(b.scale);
   const float* h1 = n.at<float>(b.shift);
   if (mode == 1) return bn_apply_relu(x, s1, h1, y, M, b.C, st);
@@ -570,15 +586,21 @@ static BnBwdArgs bwd_args(Net& n, BNL& b, int64_t count, float gs) {
 // bn_bwd_reduce accumulated; dgamma / dbeta into the flat gradient buffer.
 static int bn_bwd_coef_apply(Net& n, BNL& b1, const u16* dz, const u16* x1, u16* dx1, BNL* b2, const u16* x2, u16* dx2,
                              int64_t M, float gs, hipStream_t st) {
+  if (n.sync) {  // SyncBN backward: global sum(dz), sum(dz*xhat); dgamma/dbeta stay this rank's share
+    DTC_TRY(sync_bn_sums(n, b1.acc, b1.C, st));
+    if (b2) DTC_TRY(sync_bn_sums(n, b2->acc, b2->C, st));
+    gs /= (float)n.sync_world;
+  }
+  const int64_t cnt = n.sync ? M * n.sync_world : M;
   if (bn_fused()) {
-    const BnBwdArgs a1 = bwd_args(n, b1, M, gs);
-    const BnBwdArgs a2 = b2 ? bwd_args(n, *b2, M, gs) : BnBwdArgs{};
+    const BnBwdArgs a1 = bwd_args(n, b1, cnt, gs);
+    const BnBwdArgs a2 = b2 ? bwd_args(n, *b2, cnt, gs) : BnBwdArgs{};
     return bn_bwd_fin_apply(dz, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st);
   }
-  DTC_TRY(bn_bwd_finalize(n.at<double>(b1.acc), b1.C, M, n.pf(b1.gidx), n.at<float>(b1.mean), n.at<float>(b1.invstd),
+  DTC_TRY(bn_bwd_finalize(n.at<double>(b1.acc), b1.C, cnt, n.pf(b1.gidx), n.at<float>(b1.mean), n.at<float>(b1.invstd),
                           gs, n.gf(b1.gidx), n.gf(b1.bidx), n.at<float>(b1.coef), st));
   if (b2)
-    DTC_TRY(bn_bwd_finalize(n.at<double>(b2->acc), b2->C, M, n.pf(b2->gidx), n.at<float>(b2->mean),
+    DTC_TRY(bn_bwd_finalize(n.at<double>(b2->acc), b2->C, cnt, n.pf(b2->gidx), n.at<float>(b2->mean),
                             n.at<float>(b2->invstd), gs, n.gf(b2->gidx), n.gf(b2->bidx), n.at<float>(b2->coef), st));
   return bn_bwd_apply(dz, x1, n.at<float>(b1.coef), dx1, x2, b2 ? n.at<float>(b2->coef) : nullptr, dx2, M, b1.C, st);
 }
@@ -978,6 +1000,15 @@ int dtc_rn18_profile_end(dtc_net* net, double* ms_by_kind, double* flops_by_kind
   }
   drop_graphs(n);
   prof_free(n);
+  return 0;
+}
+
+int dtc_rn18_set_sync_bn(dtc_net* net, dtc_comm* comm) {
+  DTC_CHECK_ARG(net != nullptr, "dtc_rn18_set_sync_bn: null net");
+  Net& n = net->n;
+  n.sync = (Comm*)comm;
+  n.sync_world = comm ? comm_world((Comm*)comm) : 1;
+  drop_graphs(n);
   return 0;
 }
 

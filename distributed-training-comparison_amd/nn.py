@@ -331,6 +331,8 @@ class ResNet(nn.Module):
         self._grad_scale = 1.0
         self._bucket_cap_mb = float(bucket_cap_mb)
         self._capture = False
+        self._sync_bn = False  # SyncBatchNorm.convert_sync_batchnorm marks the module
+        self._sync_comm = None  # communicator the executors all-reduce BN sums over
 
     def _make_layer(self, block, planes, num_blocks, stride):
         strides = [stride] + [1] * (num_blocks - 1)
@@ -429,8 +431,17 @@ class ResNet(nn.Module):
         if exe is None:
             exe = Executor(self.flat, batch, height, width, self.num_classes, self._bucket_cap_mb,
                            capture=self._capture)
+            if self._sync_comm is not None:
+                call("dtc_rn18_set_sync_bn", exe.handle, self._sync_comm.handle)
             self._executors[key] = exe
         return exe
+
+    def set_sync_bn(self, comm) -> None:
+        """Synchronise training-mode BN statistics over `comm` (a parallel.Comm of its own, not the
+        Reducer's); None restores per-rank statistics. Applies to existing and new executors."""
+        self._sync_comm = comm
+        for exe in self._executors.values():
+            call("dtc_rn18_set_sync_bn", exe.handle, comm.handle if comm is not None else None)
 
     def enable_capture(self, on: bool = True):
         """Keep backward intermediates for per-layer parity tests (new executors only)."""
@@ -447,6 +458,22 @@ class ResNet(nn.Module):
             x = x.float().contiguous()
         exe = self.executor(x.shape[0], x.shape[2], x.shape[3])
         return _NetFn.apply(x, self._anchor, self, exe)
+
+
+class SyncBatchNorm:
+    """``nn.SyncBatchNorm.convert_sync_batchnorm`` for the native ResNet (README.md:40 recommends
+    it; the reference trainers do not call it). The BN modules stay where they are (same
+    state_dict keys); the model is marked, and ``DistributedDataParallel`` gives it a second RCCL
+    communicator over which every training-mode BN all-reduces its per-channel sums
+    (include/dtc.h ``dtc_rn18_set_sync_bn``). As in torch, a one-rank group keeps local statistics."""
+
+    @staticmethod
+    def convert_sync_batchnorm(module, process_group=None):
+        if not isinstance(module, ResNet):
+            raise NotImplementedError("convert_sync_batchnorm: only the native ResNet18 is supported")
+        module._sync_bn = True
+        module._sync_bn_group = process_group
+        return module
 
 
 def ResNet18(num_classes: int = 100) -> ResNet:

@@ -27,8 +27,8 @@ import torch.nn as nn
 
 from ._native import NativeError, call, lib, ptr, require_cuda, stream_ptr
 
-DTYPE_F32, DTYPE_BF16, DTYPE_I64 = 0, 1, 2
-_DTYPES = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.int64: DTYPE_I64}
+DTYPE_F32, DTYPE_BF16, DTYPE_I64, DTYPE_F64 = 0, 1, 2, 3
+_DTYPES = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.int64: DTYPE_I64, torch.float64: DTYPE_F64}
 
 
 class Comm:
@@ -167,6 +167,12 @@ class DistributedDataParallel(nn.Module):
             # a one-rank all-reduce is the identity: no side-stream fork/join inside the backward
             module._comm = self.comm if self.world_size > 1 else None
             module._grad_scale = 1.0 / self.world_size
+            # SyncBatchNorm: a communicator of its own (BN-sum all-reduces run on the compute
+            # stream while the Reducer's bucket all-reduces run on its side stream)
+            self.sync_comm = None
+            if getattr(module, "_sync_bn", False) and self.world_size > 1:
+                self.sync_comm = Comm.from_process_group(device, getattr(module, "_sync_bn_group", None) or process_group)
+                module.set_sync_bn(self.sync_comm)
             # C1: make every replica start from rank 0's state
             self.comm.broadcast_(flat.params, 0)
             self.comm.broadcast_(flat.bufs, 0)

@@ -21,7 +21,7 @@ import torch.distributed as dist
 
 from . import data as D
 from .amp import GradScaler, autocast
-from .nn import CrossEntropyLoss, ResNet18
+from .nn import CrossEntropyLoss, ResNet18, SyncBatchNorm
 from .optim import SGD
 from .parallel import DDP, DataParallel
 
@@ -41,6 +41,8 @@ def load_config(argv=None, mode: str = "ddp"):
         p.add_argument("--rank", type=int, default=0)
         p.add_argument("--dist-backend", type=str, default="nccl")
         p.add_argument("--dist-url", default="tcp://127.0.0.1:3456", type=str)
+        p.add_argument("--sync-bn", action="store_true", default=False,
+                       help="SyncBatchNorm.convert_sync_batchnorm (README.md:40; off in the reference)")
     p.add_argument("--epoch", type=int, default=200 if mode == "single" else 100)
     p.add_argument("--batch-size", type=int, default=128)
     p.add_argument("--model", type=str, default="resnet18")
@@ -262,6 +264,8 @@ def _run(hparams, rank, ngpus, distributed, data_parallel=False):
     D.fix_seed(hparams.seed)
     scaler = GradScaler() if hparams.amp else None
     model = ResNet18()
+    if getattr(hparams, "sync_bn", False):
+        model = SyncBatchNorm.convert_sync_batchnorm(model)
     trainer = Trainer(hparams, model, scaler, rank, ngpus, distributed, data_parallel)
     version = trainer.fit()
     if rank == 0 and hparams.contain_test:

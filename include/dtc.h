@@ -150,7 +150,7 @@ int dtc_cifar_augment(const uint8_t* images, const int64_t* targets, int64_t n_i
  * parameter broadcast, the per-forward buffer broadcast and the bucketed gradient all-reduce.
  * Bootstrap: rank 0 calls dtc_comm_get_unique_id, the id travels over the existing
  * torch.distributed rendezvous (init_process_group, ddp/main.py:18-23), every rank calls
- * dtc_comm_init. dtype: 0 = fp32, 1 = bf16, 2 = int64. */
+ * dtc_comm_init. dtype: 0 = fp32, 1 = bf16, 2 = int64, 3 = fp64. */
 typedef struct dtc_comm dtc_comm;
 size_t dtc_comm_unique_id_bytes(void);
 int dtc_comm_get_unique_id(void* out);
@@ -197,6 +197,15 @@ int dtc_rn18_forward(dtc_net* net, const float* x, float* logits, int train, voi
  * on the communicator's side stream as soon as backward has produced it; the call returns with
  * `stream` ordered after the last all-reduce. */
 int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_comm* comm, void* stream);
+/* SyncBatchNorm (replaces nn.SyncBatchNorm.convert_sync_batchnorm(model), torch/nn/modules/
+ * batchnorm.py, the conversion README.md:40 recommends; not called by the reference trainers).
+ * comm != NULL: every training-mode BN all-reduces its fp64 per-channel partial sums over `comm`
+ * (forward: sum x, sum x^2; backward: sum dz, sum dz*xhat) on the compute stream and normalises
+ * with the global element count (running_var's unbiased factor too); dgamma/dbeta keep this
+ * rank's share (x 1/world) so the Reducer's mean matches DDP over SyncBatchNorm. Use a
+ * communicator of its own, not the one passed to dtc_rn18_backward. Disables graph replay.
+ * comm == NULL: per-rank statistics (the reference's BatchNorm2d). */
+int dtc_rn18_set_sync_bn(dtc_net* net, dtc_comm* comm);
 /* Byte offset into the workspace of the executor's own fp32 [batch][num_classes] dlogits buffer.
  * A caller that writes the loss gradient there (e.g. the fused cross-entropy backward) and passes
  * that pointer to dtc_rn18_backward saves the graph path's copy-in. */

@@ -138,6 +138,41 @@ def bn_train_bwd(dy, x, gamma, mean, invstd):
     return dx, dgamma, dbeta
 
 
+# ----------------------------------------------------------------------------- SyncBatchNorm (train)
+# nn.SyncBatchNorm (torch/nn/modules/_functions.py SyncBatchNorm.forward/backward in torch 1.7.1, the
+# conversion README.md:40 recommends): statistics over the union of every rank's batch. Restated as
+# the executor computes it (dtc_rn18_set_sync_bn): per-channel (sum, sumsq) SUM all-reduced, global
+# count; backward (sum dy, sum dy*xhat) SUM all-reduced; dgamma/dbeta are this rank's own sums.
+# `allreduce(a)` returns the elementwise sum of `a` over ranks (np.ndarray in, np.ndarray out).
+
+
+def sync_bn_train_fwd(x, gamma, beta, allreduce, running_mean=None, running_var=None, eps=1e-5, momentum=0.1):
+    x = np.asarray(x, np.float64)
+    s = allreduce(np.stack([x.sum(axis=0), (x * x).sum(axis=0), np.full(x.shape[1], float(x.shape[0]))]))
+    n = s[2][0]
+    mean = s[0] / n
+    var = s[1] / n - mean * mean
+    invstd = 1.0 / np.sqrt(var + eps)
+    y = (x - mean) * invstd * gamma + beta
+    rm = rv = None
+    if running_mean is not None:
+        rm = (1 - momentum) * running_mean + momentum * mean
+        rv = (1 - momentum) * running_var + momentum * var * n / max(n - 1, 1)
+    return y, mean, invstd, rm, rv
+
+
+def sync_bn_train_bwd(dy, x, gamma, mean, invstd, allreduce):
+    dy = np.asarray(dy, np.float64)
+    x = np.asarray(x, np.float64)
+    xhat = (x - mean) * invstd
+    dbeta = dy.sum(axis=0)
+    dgamma = (dy * xhat).sum(axis=0)
+    g = allreduce(np.stack([dbeta, dgamma, np.full(x.shape[1], float(x.shape[0]))]))
+    n = g[2][0]
+    dx = gamma * invstd * (dy - g[0] / n - xhat * g[1] / n)
+    return dx, dgamma, dbeta
+
+
 def relu(x):
     return np.maximum(x, 0)
 

@@ -106,3 +106,49 @@ def test_allreduce_probe_gloo():
     dtc = dtc_import.load()
     alg, bus = dtc.parallel.busbw(8 << 20, 1e-3, 8)
     assert abs(alg - 8.388608) < 1e-9 and abs(bus - alg * 1.75) < 1e-9
+
+
+def _syncbn_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import ops
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def allreduce(a):
+            t = torch.from_numpy(np.ascontiguousarray(a, np.float64))
+            dist.all_reduce(t)
+            return t.numpy()
+
+        rng = np.random.default_rng(7)
+        M, Cc = 48, 8  # ragged per-rank batches: rank r holds rows [lo, hi)
+        x = rng.standard_normal((M, Cc)) * 2 + 0.5
+        dy = rng.standard_normal((M, Cc))
+        gamma, beta = rng.standard_normal(Cc), rng.standard_normal(Cc)
+        rm0, rv0 = np.zeros(Cc), np.ones(Cc)
+        cuts = [0, 20, M]
+        lo, hi = cuts[rank], cuts[rank + 1]
+        y, mean, invstd, rm, rv = ops.sync_bn_train_fwd(x[lo:hi], gamma, beta, allreduce, rm0, rv0)
+        dx, dg, db = ops.sync_bn_train_bwd(dy[lo:hi], x[lo:hi], gamma, mean, invstd, allreduce)
+        # DDP's mean of the per-rank dgamma / dbeta (pre-divided by world, SUM all-reduced)
+        dgm = allreduce(np.stack([dg, db]) / world)
+        yf, meanf, invf, rmf, rvf = ops.bn_train_fwd(x, gamma, beta, rm0, rv0)
+        dxf, dgf, dbf = ops.bn_train_bwd(dy, x, gamma, meanf, invf)
+        out[rank] = max(np.abs(y - yf[lo:hi]).max(), np.abs(rm - rmf).max(), np.abs(rv - rvf).max(),
+                        np.abs(dx - dxf[lo:hi]).max(), np.abs(dgm[0] - dgf / world).max(),
+                        np.abs(dgm[1] - dbf / world).max())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sync_batchnorm_gloo():
+    """SyncBatchNorm semantics of the executor (dtc_rn18_set_sync_bn) restated in
+    the oracle and run over 2 gloo ranks with ragged shards (20 / 28 rows): each rank's output,
+    running statistics and input gradient equal plain BatchNorm over the concatenated batch, and
+    DDP's mean of the per-rank dgamma / dbeta equals the full-batch gradient / world."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_syncbn_worker, args=(2, _port(), out), nprocs=2, join=True)
+    assert set(out.keys()) == {0, 1}
+    for r, e in out.items():
+        assert e < 1e-12, (r, e)

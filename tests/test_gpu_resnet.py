@@ -579,3 +579,38 @@ def test_bucketed_allreduce_backward_one_rank(dtc, cuda, graphs):
     finally:
         comm.close()
         dtc._native.lib.dtc_set_option(b"graphs", 1)
+
+
+def test_sync_batchnorm_one_rank(dtc, cuda):
+    """SyncBatchNorm path (dtc_rn18_set_sync_bn) with a one-rank RCCL
+    communicator: every BN's fp64 sum slots go through an in-stream fp64 all-reduce (the identity
+    over one rank) and the executor runs eagerly; logits, gradients and running statistics must
+    equal the per-rank BatchNorm path (up to the order of the fp64 statistics atomics). The
+    two-rank statistics semantics are covered by tests/test_ddp_gloo.py::test_sync_batchnorm_gloo."""
+    comm = dtc.parallel.Comm(0, 1, dtc.parallel.Comm.unique_id(), cuda.index or 0)
+    try:
+        t = torch.arange(6, dtype=torch.float64, device=cuda)
+        comm.allreduce_sum_(t)
+        torch.cuda.synchronize()
+        assert t.cpu().tolist() == [0.0, 1.0, 2.0, 3.0, 4.0, 5.0]
+        g = torch.Generator().manual_seed(5)
+        x = torch.randn(32, 3, 32, 32, generator=g).to(cuda)
+        y = torch.randint(0, 100, (32,), generator=g).to(cuda)
+        res = []
+        for sync in (False, True):
+            torch.manual_seed(42)
+            model = dtc.ResNet18().to(cuda)
+            if sync:
+                model = dtc.SyncBatchNorm.convert_sync_batchnorm(model)
+                model.set_sync_bn(comm)
+            logits = model(x)
+            dtc.CrossEntropyLoss()(logits, y).backward()
+            torch.cuda.synchronize()
+            res.append((logits.detach().cpu().numpy(), model.flat.grads.detach().cpu().numpy().copy(),
+                        model.flat.bufs.detach().cpu().numpy().copy()))
+            model.set_sync_bn(None)
+        (l0, g0, b0), (l1, g1, b1) = res
+        assert np.isfinite(g1).all() and np.abs(g1).sum() > 0
+        assert rel_err(l1, l0) < 1e-3 and rel_err(g1, g0) < 1e-3 and rel_err(b1, b0) < 1e-5
+    finally:
+        comm.close()
