@@ -204,6 +204,7 @@ int bn_apply_dual_relu(const u16* x, const float* s, const float* h, const u16* 
 // (and num_batches_tracked once). Removes the separate finalize launch and its kernel boundary;
 // the slots are zeroed by a memset node at the start of the executor's forward.
 constexpr int FA_GROUP = 64;  // channels per workgroup
+constexpr int FA_UNROLL = 4;  // pixel rows in flight per thread
 
 __device__ __forceinline__ void fa_slot_sums(const double* __restrict__ st, int C, int cg, double* part, double& s,
                                              double& q) {
@@ -277,20 +278,37 @@ __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const u16* __restrict
     }
   }
   const int64_t m0 = (int64_t)blockIdx.x * rows, m1 = std::min<int64_t>(M, m0 + rows);
-  for (int64_t m = m0 + pr; m < m1; m += 32) {
-    const int64_t o = m * C + cg + q8;
-    float a[8], r[8], v[8];
-    unpack8(*(const uint4*)(x + o), a);
-    if constexpr (MODE != APPLY_RELU) unpack8(*(const uint4*)(x2 + o), r);
+  // FA_UNROLL rows per thread per trip: every load of the trip is issued before the first
+  // dependent use (memory-level parallelism); elementwise, so results are unchanged
+  for (int64_t mb = m0 + pr; mb < m1; mb += 32 * FA_UNROLL) {
+    uint4 xa[FA_UNROLL], xr[FA_UNROLL];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      v[k] = a[k] * sc[k] + sh[k];
-      // torch rounds each BN output to bf16 before the residual add (autocast)
-      if constexpr (MODE == APPLY_ADD_RELU) v[k] = round_bf(v[k]) + r[k];
-      if constexpr (MODE == APPLY_DUAL_RELU) v[k] = round_bf(v[k]) + round_bf(r[k] * sc2[k] + sh2[k]);
-      v[k] = fmaxf(v[k], 0.f);
+    for (int u = 0; u < FA_UNROLL; ++u) {
+      const int64_t m = mb + 32 * u;
+      if (m < m1) {
+        const int64_t o = m * C + cg + q8;
+        xa[u] = *(const uint4*)(x + o);
+        if constexpr (MODE != APPLY_RELU) xr[u] = *(const uint4*)(x2 + o);
+      }
     }
-    *(uint4*)(y + o) = pack8(v);
+#pragma unroll
+    for (int u = 0; u < FA_UNROLL; ++u) {
+      const int64_t m = mb + 32 * u;
+      if (m >= m1) break;
+      const int64_t o = m * C + cg + q8;
+      float a[8], r[8], v[8];
+      unpack8(xa[u], a);
+      if constexpr (MODE != APPLY_RELU) unpack8(xr[u], r);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[k] = a[k] * sc[k] + sh[k];
+        // torch rounds each BN output to bf16 before the residual add (autocast)
+        if constexpr (MODE == APPLY_ADD_RELU) v[k] = round_bf(v[k]) + r[k];
+        if constexpr (MODE == APPLY_DUAL_RELU) v[k] = round_bf(v[k]) + round_bf(r[k] * sc2[k] + sh2[k]);
+        v[k] = fmaxf(v[k], 0.f);
+      }
+      *(uint4*)(y + o) = pack8(v);
+    }
   }
 }
 
@@ -372,19 +390,35 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const u16* __rest
     }
   }
   const int64_t m0 = (int64_t)blockIdx.x * rows, m1 = std::min<int64_t>(M, m0 + rows);
-  for (int64_t m = m0 + pr; m < m1; m += 32) {
-    const int64_t o = m * C + cg + q8;
-    float d[8], a[8], v[8];
-    unpack8(*(const uint4*)(dz + o), d);
-    unpack8(*(const uint4*)(x1 + o), a);
+  for (int64_t mb = m0 + pr; mb < m1; mb += 32 * FA_UNROLL) {  // loads of a trip first (see bn_fin_apply)
+    uint4 vd[FA_UNROLL], va[FA_UNROLL], vb[FA_UNROLL];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = A1[k] * d[k] + B1[k] * a[k] + C1[k];
-    *(uint4*)(dx1 + o) = pack8(v);
-    if constexpr (DUAL) {
-      unpack8(*(const uint4*)(x2 + o), a);
+    for (int u = 0; u < FA_UNROLL; ++u) {
+      const int64_t m = mb + 32 * u;
+      if (m < m1) {
+        const int64_t o = m * C + cg + q8;
+        vd[u] = *(const uint4*)(dz + o);
+        va[u] = *(const uint4*)(x1 + o);
+        if constexpr (DUAL) vb[u] = *(const uint4*)(x2 + o);
+      }
+    }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = A2[k] * d[k] + B2[k] * a[k] + C2[k];
-      *(uint4*)(dx2 + o) = pack8(v);
+    for (int u = 0; u < FA_UNROLL; ++u) {
+      const int64_t m = mb + 32 * u;
+      if (m >= m1) break;
+      const int64_t o = m * C + cg + q8;
+      float d[8], a[8], v[8];
+      unpack8(vd[u], d);
+      unpack8(va[u], a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = A1[k] * d[k] + B1[k] * a[k] + C1[k];
+      *(uint4*)(dx1 + o) = pack8(v);
+      if constexpr (DUAL) {
+        unpack8(vb[u], a);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = A2[k] * d[k] + B2[k] * a[k] + C2[k];
+        *(uint4*)(dx2 + o) = pack8(v);
+      }
     }
   }
 }
