@@ -153,6 +153,58 @@ def bench_dp(args):
         "final_loss": round(losses[-1], 4)}), flush=True)
 
 
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy ~6.3 TB/s
+
+
+def hbm_probe(dtc, dev, B, S, nparam, reps=20):
+    """Achieved HBM GB/s of the two HBM-bound kernel classes the north star names, timed with
+    device events on the stream they are launched on (torch's current stream), after the timed
+    regions: (1) bn_bwd_reduce<mask> at the largest BN shape of the step (the stem / layer1 BNs:
+    B*S*S pixels x 64 channels; reads dy, y, x and writes dz: 8 B/element), the executor's
+    largest BN item per step; (2) the fused SGD-Nesterov + bf16-shadow kernel over a flat buffer of
+    the model's size (reads p, g, m; writes p, m, bf16 p: 22 B/parameter). Scratch tensors only."""
+    ops = dtc.ops
+    M, Cc = B * S * S, 64
+    g = torch.Generator(device=dev).manual_seed(7)
+    dy = torch.randn(M, Cc, device=dev, generator=g).bfloat16()
+    y = torch.randn(M, Cc, device=dev, generator=g).bfloat16()
+    x = torch.randn(M, Cc, device=dev, generator=g).bfloat16()
+    mean = torch.zeros(Cc, device=dev)
+    invstd = torch.ones(Cc, device=dev)
+    p = torch.randn(nparam, device=dev, generator=g)
+    gr = torch.randn(nparam, device=dev, generator=g) * 1e-3
+    mom = torch.zeros(nparam, device=dev)
+    pb = torch.empty(nparam, dtype=torch.bfloat16, device=dev)
+
+    def timeit(fn):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / reps
+
+    acc = ops.new_stats(Cc, dev)
+    dz = torch.empty_like(dy)
+    P, sp, call = dtc._native.ptr, dtc._native.stream_ptr, dtc._native.call
+    # the C-ABI directly with preallocated outputs (the slots accumulate across launches: only timing here)
+    t_bn = timeit(lambda: call("dtc_bn_bwd_reduce", P(dy), P(y), P(x), P(mean), P(invstd), P(acc), None, None, None,
+                               None, P(dz), M, Cc, sp()))
+    t_sgd = timeit(lambda: ops.sgd_nesterov_flat(p, gr, mom, pb, 1e-3, 1e-4, 0.9))
+    out = {}
+    for name, t, nbytes, unit in (("bn_bwd_reduce", t_bn, 8 * M * Cc, f"{M}x{Cc} bf16, 8 B/element"),
+                                  ("sgd_nesterov", t_sgd, 22 * nparam, f"{nparam} params, 22 B/param")):
+        gbps = nbytes / t / 1e9
+        out[name] = {"us": round(t * 1e6, 2), "bytes": nbytes, "achieved_GBps": round(gbps, 1),
+                     "peak_GBps": HBM_PEAK_GBPS, "frac": round(gbps / HBM_PEAK_GBPS, 4), "work": unit}
+    out["timing"] = "device events on torch's current stream (the launch stream), mean of %d launches" % reps
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -171,6 +223,7 @@ def main():
     ap.add_argument("--dp-devices", default="", help="dp mode: comma-separated replica devices (may repeat)")
     ap.add_argument("--no-allreduce-probe", action="store_true", help="skip the N>1 all-reduce busBW probe")
     ap.add_argument("--allreduce-probe", action="store_true", help="run the busBW probe at N=1 too (plumbing check)")
+    ap.add_argument("--no-hbm-probe", action="store_true", help="skip the BN / SGD HBM-roofline probe")
     ap.add_argument("--sync-bn", action="store_true",
                     help="SyncBatchNorm (off in the reference); at N=1 a one-rank communicator forces the sync path")
     ap.add_argument("--opt", action="append", default=[], help="native option NAME=VALUE (A/B runs)")
@@ -269,6 +322,13 @@ def main():
         except Exception as e:  # report, never hide; the throughput line stands on its own
             allreduce = {"error": repr(e)}
 
+    hbm = None
+    if rank == 0 and not args.no_hbm_probe:
+        try:
+            hbm = hbm_probe(dtc, dev, B, S, int(model.module.flat.params.numel()))
+        except Exception as e:  # report, never hide
+            hbm = {"error": repr(e)}
+
     if rank == 0:
         conv_ms = sum(ms)
         conv_flops = sum(fl)
@@ -313,6 +373,7 @@ def main():
                 "conv_calls_per_step": n_launch // max(1, args.steps),
                 "algorithmic_gflop_per_step": round(conv_flops / args.steps / 1e9, 3),
             },
+            "hbm_roofline": hbm,
             "step_flop_fraction_of_peak": round(FLOPS_PER_IMAGE * (S * S / 1024) * B / (elapsed / args.steps) / 1e12
                                                 / BF16_PEAK_TFLOPS, 4),
             "final_loss": round(losses[-1], 4) if losses else None,
