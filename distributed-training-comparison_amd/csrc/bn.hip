@@ -316,7 +316,9 @@ static void fa_grid(int64_t M, int C, int& nblk, int& rows) {
   const int groups = C / FA_GROUP;
   nblk = std::max(1, 1024 / groups);
   rows = (int)((M + nblk - 1) / nblk);
-  rows = std::max(32, (rows + 31) / 32 * 32);
+  // at least FA_UNROLL rows per thread: each workgroup's prologue folds 32 KB of fp64 slots, which
+  // dominated the small (layer3/4) launches at one row per thread
+  rows = std::max(32 * FA_UNROLL, (rows + 31) / 32 * 32);
   nblk = (int)((M + rows - 1) / rows);
 }
 
