@@ -38,3 +38,19 @@ def test_dp_flags_match_reference_defaults(dtc):
     assert dtc.trainer.load_config(["--device-ids", "0,0"], "dp").device_ids == [0, 0]
     with pytest.raises(ValueError):
         dtc.trainer.main([], "bogus")
+
+
+def test_sync_bn_flag_and_conversion(dtc):
+    """--sync-bn (ddp mode only, off by default as in the reference) and
+    SyncBatchNorm.convert_sync_batchnorm: marks the native ResNet in place (BN modules and
+    state_dict keys unchanged); anything else is refused rather than silently left unsynchronised."""
+    assert dtc.trainer.load_config([], "ddp").sync_bn is False
+    assert dtc.trainer.load_config(["--sync-bn"], "ddp").sync_bn is True
+    assert not hasattr(dtc.trainer.load_config([], "single"), "sync_bn")
+    m = dtc.ResNet18()
+    keys = list(m.state_dict().keys())
+    out = dtc.SyncBatchNorm.convert_sync_batchnorm(m)
+    assert out is m and m._sync_bn and list(m.state_dict().keys()) == keys
+    import torch.nn as tnn
+    with pytest.raises(NotImplementedError):
+        dtc.SyncBatchNorm.convert_sync_batchnorm(tnn.BatchNorm2d(4))
