@@ -66,36 +66,24 @@ def _committed_traffic():
         return None
 
 
-def cpu_baseline(seconds: float):
-    """Oracle (numpy restatement) training step on the host cores: a bounded sample."""
-    from oracle import resnet as R
+def cpu_baseline(seconds: float, steps: int = 50):
+    """BASELINE config 1 on the host cores: the reference's single-device fp32 step
+    (single/trainer.py:131-147) in stock torch CPU at batch 128 (oracle/torch_ref.py, pinned to the
+    reference-produced fixture by tests/test_oracle_golden.py), 3 warm-up steps, then the median of
+    up to `steps` steps bounded by `seconds` of CPU work. Threads = torch's intra-op pool
+    (OMP_NUM_THREADS on the box: the cores this job may use)."""
+    from oracle.torch_ref import time_cpu_step
 
-    try:  # the BLAS pool numpy actually uses (OMP_NUM_THREADS on the box), not the machine's CPU count
-        from threadpoolctl import threadpool_info
-
-        threads = max([p.get("num_threads", 1) for p in threadpool_info() if p.get("user_api") == "blas"] or [1])
-    except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
     torch.manual_seed(42)
     dtc = dtc_import.load()
     m = dtc.ResNet18()  # host-side construction only (identical init to the reference)
-    params = {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}
-    batch = 16
-    g = np.random.default_rng(0)
-    x = g.standard_normal((batch, 3, 32, 32)).astype(np.float32)
-    y = g.integers(0, 100, batch)
-    state = R.init_state(params)
-    t0 = time.perf_counter()
-    steps = 0
-    while True:
-        R.train_step(state, x, y, lr=0.1, bf16_mode=False)
-        steps += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(steps * batch / dt, 3), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"{steps} fp32 SGD steps of batch {batch} (32x32) through oracle/resnet.py (numpy), "
-                      f"{dt:.1f} s"}
+    r = time_cpu_step(m.state_dict(), batch=128, warmup=3, steps=steps, max_seconds=seconds)
+    return {"value": round(r["img_per_s"], 3), "unit": "images/sec", "cores": r["threads"], "kind": "port",
+            "impl": "torch-cpu", "batch": 128, "dtype": "fp32",
+            "sample": f"config 1: median of {r['steps']} steps (after 3 warm-ups) of the single-device fp32 "
+                      f"train step (zero_grad, forward, CrossEntropy, backward, SGD nesterov) at batch 128, "
+                      f"32x32, stock torch {torch.__version__} CPU on {r['threads']} threads; "
+                      f"median step {r['median_s'] * 1e3:.1f} ms, {r['seconds']:.1f} s sampled"}
 
 
 def bench_dp(args):
@@ -215,7 +203,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--no-barrier", action="store_true", help="drop the reference's per-step dist.barrier()")
     ap.add_argument("--no-item", action="store_true", help="drop the per-step loss.item() host sync")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=30.0, help="bound on the timed CPU-baseline steps")
+    ap.add_argument("--cpu-steps", type=int, default=50, help="CPU baseline: median over this many steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-live-roofline", action="store_true", help="skip the per-conv timing in the timed region")
     ap.add_argument("--mode", choices=("ddp", "dp"), default="ddp",
@@ -382,7 +371,7 @@ def main():
             out["allreduce"] = allreduce
         if world == 1 and not args.no_cpu_baseline:
             try:
-                out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+                out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_steps)
             except Exception as e:  # report, never hide
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)

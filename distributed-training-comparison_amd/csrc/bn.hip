@@ -616,4 +616,22 @@ int bn_bwd_apply(const u16* dz, const u16* x1, const float* coef1, u16* dx1, con
   return 0;
 }
 
+// ---------------------------------------------------------------- SyncBN slot compaction
+__global__ void bn_fold_slots_kernel(double* __restrict__ slots, int n2c) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n2c) return;
+  double a = 0.0;
+  for (int k = 0; k < DTC_STAT_SLOTS; ++k) a += slots[(size_t)k * n2c + j];
+  slots[j] = a;
+  for (int k = 1; k < DTC_STAT_SLOTS; ++k) slots[(size_t)k * n2c + j] = 0.0;
+}
+
+int bn_fold_slots(double* slots, int C, hipStream_t st) {
+  DTC_CHECK_ARG(slots && C > 0, "bn_fold_slots: bad args");
+  const int n2c = 2 * C;
+  hipLaunchKernelGGL(bn_fold_slots_kernel, dim3((n2c + 255) / 256), dim3(256), 0, st, slots, n2c);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // namespace dtc

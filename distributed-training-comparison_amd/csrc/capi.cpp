@@ -191,5 +191,25 @@ int dtc_comm_broadcast(dtc_comm* comm, void* buf, size_t count, int dtype, int r
   return comm_broadcast((Comm*)comm, buf, count, dtype, root, S(stream));
 }
 int dtc_comm_destroy(dtc_comm* comm) { return comm_destroy((Comm*)comm); }
+int dtc_comm_init_loopback(dtc_comm** out, int device, int world, float factor) {
+  GUARD(return comm_init_loopback((Comm**)out, device, world, factor);)
+}
+int dtc_comm_log_size(dtc_comm* comm) {
+  const auto* l = comm_log((Comm*)comm);
+  return l ? (int)l->size() : DTC_EINVAL;
+}
+int dtc_comm_log_entry(dtc_comm* comm, int idx, uint64_t* addr, uint64_t* count, int* is_async) {
+  const auto* l = comm_log((Comm*)comm);
+  DTC_CHECK_ARG(l && idx >= 0 && idx < (int)l->size(), "dtc_comm_log_entry: bad index");
+  if (addr) *addr = (*l)[idx].addr;
+  if (count) *count = (*l)[idx].count;
+  if (is_async) *is_async = (*l)[idx].async;
+  return 0;
+}
+int dtc_comm_log_clear(dtc_comm* comm) {
+  DTC_CHECK_ARG(comm != nullptr, "dtc_comm_log_clear: null comm");
+  comm_log_clear((Comm*)comm);
+  return 0;
+}
 
 }  // extern "C"

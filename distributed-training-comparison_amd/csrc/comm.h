@@ -2,9 +2,15 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdint.h>
+#include <vector>
 
 namespace dtc {
 struct Comm;
+struct CommLogEntry {
+  uint64_t addr, count;
+  int async;  // 1: a Reducer bucket (side stream), 0: an in-stream collective
+};
 size_t comm_unique_id_bytes();
 int comm_get_unique_id(void* out);
 int comm_init(Comm** out, int rank, int world, const void* uid, int device);
@@ -17,4 +23,8 @@ int comm_broadcast(Comm* c, void* buf, size_t count, int dtype, int root, hipStr
 int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute);
 int comm_join(Comm* c, hipStream_t compute);
 int comm_world(const Comm* c);
+// test communicator without RCCL: all-reduce = buf *= factor, logged; reports `world` ranks (comm.cpp)
+int comm_init_loopback(Comm** out, int device, int world, float factor);
+const std::vector<CommLogEntry>* comm_log(Comm* c);
+void comm_log_clear(Comm* c);
 }  // namespace dtc

@@ -139,6 +139,8 @@ int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, con
 int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
                      u16* dx2, int64_t M, int C, hipStream_t st);
 
+// slots [SLOTS][2][C] -> slot 0 holds the fixed-order sum over the slots, the others are zeroed
+int bn_fold_slots(double* slots, int C, hipStream_t st);
 // backward: dz = dy * [y > 0] (mask optional); accumulates sum(dz), sum(dz*xhat1) [, sum(dz*xhat2)]
 int bn_bwd_reduce(const u16* dy, const u16* ymask, const u16* x1, const float* mean1, const float* invstd1,
                   double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, u16* dz,
@@ -174,6 +176,9 @@ int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int
 int sgd_nesterov(float* p, const float* g, float* mom, u16* p_bf16, int64_t n, float lr, float wd, float mu,
                  const float* inv_scale, const int* found_inf, hipStream_t st);
 int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st);
+// x[i] *= f (loopback test communicator)
+int scale_f32(float* x, int64_t n, float f, hipStream_t st);
+int scale_f64(double* x, int64_t n, double f, hipStream_t st);
 int amp_check_finite(const float* g, int64_t n, int* found_inf, hipStream_t st);
 int amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, int* found_inf, float growth,
                      float backoff, int interval, hipStream_t st);

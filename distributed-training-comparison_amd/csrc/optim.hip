@@ -60,6 +60,27 @@ int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st) {
   return 0;
 }
 
+template <typename T>
+__global__ void scale_kernel(T* __restrict__ x, int64_t n, T f) {
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) x[i] *= f;
+}
+
+int scale_f32(float* x, int64_t n, float f, hipStream_t st) {
+  DTC_CHECK_ARG(x && n > 0, "scale_f32: bad args");
+  const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(scale_kernel<float>, dim3(blocks), dim3(256), 0, st, x, n, f);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+int scale_f64(double* x, int64_t n, double f, hipStream_t st) {
+  DTC_CHECK_ARG(x && n > 0, "scale_f64: bad args");
+  const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(scale_kernel<double>, dim3(blocks), dim3(256), 0, st, x, n, f);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 __global__ void amp_check_finite_kernel(const float* __restrict__ g, int64_t n, int* __restrict__ found) {
   bool bad = false;
   for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)

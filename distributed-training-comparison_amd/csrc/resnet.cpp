@@ -348,12 +348,15 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.ws_bytes = off;
 
   // gradient buckets at block granularity in backward order (head + layer4.1 first); a bucket
-  // closes once it holds >= bucket_cap_mb, the rest (down to the stem) forms the last bucket
+  // closes once it holds >= bucket_cap_mb, and whatever is open when layer2's backward ends closes
+  // there too: the last bucket -- issued after the stem, overlapping nothing -- is then only
+  // layer1 + the stem (0.6 MB, the unavoidable tail of SURVEY A.2) whatever the cap
   const int64_t cap = (int64_t)(bucket_cap_mb * 1024.0 * 1024.0 / 4.0);
   int64_t start = 0;
   for (int bi = (int)n.blocks.size() - 1; bi >= 0 && cap > 0; --bi) {
     const int64_t hi = n.blocks[bi].grad_hi;
-    if (hi - start >= cap) {
+    const bool tail_edge = bi == 2 && n.blocks.size() == 8;  // layer2.0: next come layer1 and the stem
+    if (hi - start >= cap || (tail_edge && hi > start)) {
       n.bucket_off.push_back(start);
       n.bucket_len.push_back(hi - start);
       n.bucket_after_block.push_back(bi);
@@ -439,10 +442,13 @@ static int bn_finalize_fwd(Net& n, BNL& b, int64_t count, bool train, hipStream_
 static bool bn_fused() { return option_get(OPT_BN_FUSED_FIN) != 0; }
 
 // SUM all-reduce of one BN's fp64 partial-sum slots ([DTC_STAT_SLOTS][2][C]) on the compute
-// stream: every apply kernel folds the slots, so after this each rank folds the global sums
-// (torch SyncBatchNorm's all-gather of per-rank mean/invstd/count, as one reduction).
+// stream: the slots are first folded into slot 0 (fixed order; the others zeroed), so the collective
+// carries 2*C doubles, not SLOTS*2*C; every apply kernel folds the slots, so after this each rank
+// folds the global sums (torch SyncBatchNorm's all-gather of per-rank mean/invstd/count, as one
+// reduction; every rank's batch is the same size -- checked by the Python DDP wrapper).
 static int sync_bn_sums(Net& n, size_t off, int C, hipStream_t st) {
-  return comm_allreduce(n.sync, n.ws + off, (size_t)DTC_STAT_SLOTS * 2 * C, 3, st);
+  DTC_TRY(bn_fold_slots(n.at<double>(off), C, st));
+  return comm_allreduce(n.sync, n.ws + off, (size_t)2 * C, 3, st);
 }
 
 static BnFwdArgs fwd_args(Net& n, BNL& b, int64_t count) {
@@ -816,10 +822,13 @@ extern "C" {
 int dtc_rn18_create(dtc_net** out, int batch, int height, int width, int num_classes, float bucket_cap_mb) {
   DTC_CHECK_ARG(out != nullptr, "dtc_rn18_create: null out");
   DTC_CHECK_ARG(batch > 0 && height >= 8 && width >= 8 && num_classes > 0, "dtc_rn18_create: bad shape");
-  // every kernel addresses an activation with 32-bit byte offsets (buffer descriptors): the largest,
-  // [batch, height, width, 64] bf16, must stay below 2 GiB (224x224: batch <= 333)
-  DTC_CHECK_ARG((int64_t)batch * height * width * 64 * 2 < (1ll << 31),
-                "dtc_rn18_create: activation too large (batch*height*width*128 bytes >= 2 GiB)");
+  // Kernels whose buffer descriptors take 32-bit byte offsets (conv_c64, conv_halo, wgrad_halo, the
+  // igemm fast wgrad loader) gate themselves on tensors < 2 GiB and the executor falls back to the
+  // 64-bit-addressed implicit-GEMM loaders above that (224x224 at batch > 333). What remains is the
+  // element index of the largest activation, [batch, height, width, 64]: it must fit an int32
+  // (224x224: batch <= 684; BASELINE config 5 is 512).
+  DTC_CHECK_ARG((int64_t)batch * height * width * 64 < (1ll << 31),
+                "dtc_rn18_create: activation too large (batch*height*width*64 elements >= 2^31)");
   dtc_net* h = new dtc_net();
   h->n.B = batch;
   h->n.H = height;

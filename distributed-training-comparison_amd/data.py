@@ -227,17 +227,28 @@ class DeviceLoader:
         gen = torch.Generator(device=self.device)
         gen.manual_seed(self.seed + self.epoch)
         B = self.batch_size
-        for k in range(len(self)):
-            idx = rows[k * B:(k + 1) * B]
-            n = idx.numel()
-            crop = flip = None
-            if self.train:
-                crop = torch.randint(0, 2 * self.pad + 1, (n, 2), dtype=torch.uint8, device=self.device,
-                                     generator=gen)
-                flip = torch.randint(0, 2, (n,), dtype=torch.uint8, device=self.device, generator=gen)
-            self.last_params = (idx, crop, flip)
-            yield self._ops.cifar_augment(self.images, idx, crop, flip, self.mean, self.std, self.pad,
-                                          targets=self.targets, status=self.status)
-        if int(self.status.item()):
-            self.status.zero_()
-            raise IndexError("DeviceLoader: a sampler index or crop offset was out of range this epoch")
+        finished = False
+        try:
+            for k in range(len(self)):
+                idx = rows[k * B:(k + 1) * B]
+                n = idx.numel()
+                crop = flip = None
+                if self.train:
+                    crop = torch.randint(0, 2 * self.pad + 1, (n, 2), dtype=torch.uint8, device=self.device,
+                                         generator=gen)
+                    flip = torch.randint(0, 2, (n,), dtype=torch.uint8, device=self.device, generator=gen)
+                self.last_params = (idx, crop, flip)
+                yield self._ops.cifar_augment(self.images, idx, crop, flip, self.mean, self.std, self.pad,
+                                              targets=self.targets, status=self.status)
+            finished = True
+        finally:
+            # checked however the epoch ends (also when the consumer breaks early, e.g. --max-steps),
+            # and reset, so a bad index is reported for the epoch it happened in, never a later one
+            if int(self.status.item()):
+                self.status.zero_()
+                msg = "DeviceLoader: a sampler index or crop offset was out of range this epoch"
+                if finished:
+                    raise IndexError(msg)
+                import warnings
+
+                warnings.warn(msg + " (epoch ended early)", RuntimeWarning)

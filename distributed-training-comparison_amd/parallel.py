@@ -40,6 +40,30 @@ class Comm:
         buf = C.create_string_buffer(unique_id, len(unique_id))
         call("dtc_comm_init", C.byref(self.handle), rank, world, buf, device)
 
+    @classmethod
+    def loopback(cls, device: int, factor: float = 2.0, world: int = 1) -> "Comm":
+        """Test communicator (include/dtc.h dtc_comm_init_loopback): no RCCL; every all-reduce
+        multiplies its buffer by `factor` on the stream the collective would use and is logged, so
+        a single GPU can check which ranges the Reducer reduces, how often and when. It reports
+        `world` ranks (factor == world: that many ranks holding identical data)."""
+        self = cls.__new__(cls)
+        self.rank, self.world, self.device = 0, world, device
+        self.handle = C.c_void_p()
+        call("dtc_comm_init_loopback", C.byref(self.handle), device, int(world), float(factor))
+        return self
+
+    def log(self) -> List[Tuple[int, int, bool]]:
+        """Loopback communicator: [(device address, element count, is_bucket)] in issue order."""
+        out = []
+        for i in range(lib.dtc_comm_log_size(self.handle)):
+            a, n, asy = C.c_uint64(), C.c_uint64(), C.c_int()
+            call("dtc_comm_log_entry", self.handle, i, C.byref(a), C.byref(n), C.byref(asy))
+            out.append((a.value, n.value, bool(asy.value)))
+        return out
+
+    def clear_log(self) -> None:
+        call("dtc_comm_log_clear", self.handle)
+
     @staticmethod
     def unique_id() -> bytes:
         n = lib.dtc_comm_unique_id_bytes()
@@ -154,6 +178,8 @@ class DistributedDataParallel(nn.Module):
         self.find_unused_parameters = find_unused_parameters
         self.world_size = dist.get_world_size(process_group)
         self.rank = dist.get_rank(process_group)
+        self.process_group = process_group
+        self._sync_checked = set()
         flat = module.flat  # raises unless the module already lives on a GPU
         device = flat.device.index if flat.device.index is not None else torch.cuda.current_device()
         if device_ids:
@@ -186,7 +212,22 @@ class DistributedDataParallel(nn.Module):
         self.module.sync_weights()
         return res
 
+    def _check_sync_bn_batch(self, x) -> None:
+        """SyncBN normalises with world x local count (the executor all-reduces compact sums, not
+        per-rank counts as torch's all_gather does): every rank's batch must be the same size --
+        checked once per input shape over the process group (drop_last samplers guarantee it)."""
+        n = int(x.shape[0])
+        if n in self._sync_checked:
+            return
+        sizes = [None] * self.world_size
+        dist.all_gather_object(sizes, n, group=self.process_group)
+        if len(set(sizes)) != 1:
+            raise NativeError(f"SyncBatchNorm: per-rank batch sizes differ {sizes}; use equal shards")
+        self._sync_checked.add(n)
+
     def forward(self, *inputs, **kwargs):
+        if self.sync_comm is not None and self.module.training and inputs:
+            self._check_sync_bn_batch(inputs[0])
         if self.broadcast_buffers and self.world_size > 1 and self.module.training:
             flat = self.module.flat
             self.comm.broadcast_(flat.bufs, 0)  # C2: rank-0 BN running statistics

@@ -147,7 +147,9 @@ class Trainer:
         self.val_loader = D.DeviceLoader(imgs, tg, bs, subset_idx=valid_idx, train=False, drop_last=False,
                                          device=self.device)
         timgs, ttg = D.synthetic_cifar_u8(n=hparams.synthetic_test, seed=hparams.seed + 1)
-        tsampler = D.DistributedSampler(range(len(ttg)), shuffle=False) if distributed else None
+        # DistributedSampler(test_dataset) with its default shuffle=True, exactly dataset.py:158: rank 0
+        # tests the same (shuffled) 1/W subset the reference's rank 0 does
+        tsampler = D.DistributedSampler(range(len(ttg))) if distributed else None
         self.test_loader = D.DeviceLoader(timgs, ttg, bs, sampler=tsampler, train=False, drop_last=False,
                                           mean=D.IMAGENET_MEAN, std=D.IMAGENET_STD, device=self.device)
 

@@ -158,6 +158,18 @@ int dtc_comm_init(dtc_comm** out, int rank, int world, const void* unique_id, in
 int dtc_comm_allreduce_sum(dtc_comm* comm, void* buf, size_t count, int dtype, void* stream);
 int dtc_comm_broadcast(dtc_comm* comm, void* buf, size_t count, int dtype, int root, void* stream);
 int dtc_comm_destroy(dtc_comm* comm);
+/* Test communicator (no RCCL): every all-reduce through it -- dtc_comm_allreduce_sum, the Reducer's
+ * bucket all-reduces inside dtc_rn18_backward and SyncBN's statistics all-reduces -- multiplies the
+ * buffer by `factor` on the stream the collective would run on (the side stream for buckets) and
+ * appends (address, count, is_async) to a host log; broadcast is the identity; the communicator
+ * reports `world` ranks. With factor == world it is `world` ranks holding identical data. Lets a
+ * one-GPU test prove that every gradient bucket is reduced exactly once and only after its producers,
+ * and that SyncBN's sums really go through the collective (a one-rank RCCL SUM is the identity and
+ * proves neither). fp32 / fp64 buffers only. */
+int dtc_comm_init_loopback(dtc_comm** out, int device, int world, float factor);
+int dtc_comm_log_size(dtc_comm* comm);
+int dtc_comm_log_entry(dtc_comm* comm, int idx, uint64_t* addr, uint64_t* count, int* is_async);
+int dtc_comm_log_clear(dtc_comm* comm);
 
 /* ------------------------------------------------------------------ ResNet-18 executor
  * The whole forward (ResNet.forward, net.py:107-116) and backward of ResNet18() (net.py:119-120)

@@ -26,7 +26,7 @@ BF = 1e-2     # bf16-valued tensors, teacher-forced
 F32 = 1e-4    # fp32 gradients from identical bf16 operands
 
 
-def _setup(dtc, cuda, batch, seed=0, capture=False):
+def _setup(dtc, cuda, batch, seed=0, capture=False, hw=32):
     torch.manual_seed(42)
     model = dtc.ResNet18()
     sd = {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
@@ -34,7 +34,7 @@ def _setup(dtc, cuda, batch, seed=0, capture=False):
     if capture:
         model.enable_capture()
     g = np.random.default_rng(seed)
-    x = g.standard_normal((batch, 3, 32, 32)).astype(np.float32)
+    x = g.standard_normal((batch, 3, hw, hw)).astype(np.float32)
     y = g.integers(0, 100, batch)
     return model, sd, x, y
 
@@ -64,31 +64,46 @@ def _bn_bwd(dz, x, g):
     return O.bf16(dx.reshape(x.shape)), dg, db
 
 
-@pytest.mark.parametrize("batch", [2, 8])
-def test_per_layer_teacher_forced(dtc, cuda, batch):
-    model, sd, x, y = _setup(dtc, cuda, batch, capture=True)
+def _teacher_forced(dtc, cuda, batch, hw=32, stages=(0, 1, 2, 3, 4), imgs=None, seed=0):
+    """Run one capture-enabled training forward/backward of the executor at (batch, hw x hw) and
+    check every layer of the listed stages (0 = stem + head, 1..4 = layer1..4) against the oracle
+    evaluated on THAT layer's executor inputs. `imgs` (index array) restricts the per-image ops
+    (conv forward / dgrad, the ReLU masks) to those images -- BN statistics and weight gradients,
+    which reduce over the whole batch, are always checked at full size, so every batch-dependent
+    kernel plan (split-K factors, wgrad splits, persistent-tile walks) is the one under test."""
+    model, sd, x, y = _setup(dtc, cuda, batch, seed=seed, capture=True, hw=hw)
     crit = dtc.CrossEntropyLoss()
     xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
     logits = model(xd)
     loss = crit(logits, yd)
     loss.backward()
     torch.cuda.synchronize()
-    exe = model.executor(batch, 32, 32)
+    exe = model.executor(batch, hw, hw)
     A = {k: _np(v) for k, v in exe.activations().items()}
     G = {k: _np(v) for k, v in exe.activations(captures=True).items()}
     P = {k: v for k, v in _split_state(sd)[0].items()}
     W = {k: O.bf16(O.kcrs_to_krsc(v)) for k, v in P.items() if v.ndim == 4}
     grads = {k: _np(p.grad) for k, p in model.named_parameters()}
+    del model, exe
+    torch.cuda.empty_cache()
+    sel = slice(None) if imgs is None else np.asarray(imgs)
     errs = {}
 
     def chk(name, got, ref, tol=BF):
         errs[name] = (rel_err(got, ref), tol)
 
+    def conv_f(inp, w, st, pad):
+        return O.conv2d_fwd(inp[sel], w, st, pad)
+
+    def conv_d(dy, w, shape_hw, st, pad):
+        return O.conv2d_dgrad(dy[sel], w, shape_hw, st, pad)
+
     # ---------------- forward, layer by layer
     xb = O.bf16(O.nchw_to_nhwc(x))
-    chk("stem.conv", A["stem.conv"], O.conv2d_fwd(xb, W["conv1.weight"], 1, 1))
-    a0, _, _ = _bn_fwd(A["stem.conv"], P["bn1.weight"], P["bn1.bias"])
-    chk("stem.out", A["stem.out"], O.relu(a0))
+    if 0 in stages:
+        chk("stem.conv", A["stem.conv"][sel], conv_f(xb, W["conv1.weight"], 1, 1))
+        a0, _, _ = _bn_fwd(A["stem.conv"], P["bn1.weight"], P["bn1.bias"])
+        chk("stem.out", A["stem.out"], O.relu(a0))
     inp = A["stem.out"]
     blocks = []
     for L in range(1, 5):
@@ -96,68 +111,142 @@ def test_per_layer_teacher_forced(dtc, cuda, batch):
             pre = f"layer{L}.{bi}"
             st = 2 if (L > 1 and bi == 0) else 1
             proj = f"{pre}.shortcut.0.weight" in P
-            chk(pre + ".conv1", A[pre + ".conv1"], O.conv2d_fwd(inp, W[pre + ".conv1.weight"], st, 1))
-            z1, _, _ = _bn_fwd(A[pre + ".conv1"], P[pre + ".bn1.weight"], P[pre + ".bn1.bias"])
-            chk(pre + ".relu1", A[pre + ".relu1"], O.relu(z1))
-            chk(pre + ".conv2", A[pre + ".conv2"], O.conv2d_fwd(A[pre + ".relu1"], W[pre + ".conv2.weight"], 1, 1))
-            z2, _, _ = _bn_fwd(A[pre + ".conv2"], P[pre + ".bn2.weight"], P[pre + ".bn2.bias"])
-            if proj:
-                chk(pre + ".shortcut", A[pre + ".shortcut"],
-                    O.conv2d_fwd(inp, W[pre + ".shortcut.0.weight"], st, 0))
-                zs, _, _ = _bn_fwd(A[pre + ".shortcut"], P[pre + ".shortcut.1.weight"], P[pre + ".shortcut.1.bias"])
-                chk(pre + ".out", A[pre + ".out"], O.relu(z2 + zs))
-            else:
-                chk(pre + ".out", A[pre + ".out"], O.relu(z2 + inp))
-            blocks.append((pre, st, proj, inp))
+            blocks.append((L, pre, st, proj, inp))
+            if L in stages:
+                chk(pre + ".conv1", A[pre + ".conv1"][sel], conv_f(inp, W[pre + ".conv1.weight"], st, 1))
+                z1, _, _ = _bn_fwd(A[pre + ".conv1"], P[pre + ".bn1.weight"], P[pre + ".bn1.bias"])
+                chk(pre + ".relu1", A[pre + ".relu1"], O.relu(z1))
+                chk(pre + ".conv2", A[pre + ".conv2"][sel], conv_f(A[pre + ".relu1"], W[pre + ".conv2.weight"], 1, 1))
+                z2, _, _ = _bn_fwd(A[pre + ".conv2"], P[pre + ".bn2.weight"], P[pre + ".bn2.bias"])
+                if proj:
+                    chk(pre + ".shortcut", A[pre + ".shortcut"][sel], conv_f(inp, W[pre + ".shortcut.0.weight"], st, 0))
+                    zs, _, _ = _bn_fwd(A[pre + ".shortcut"], P[pre + ".shortcut.1.weight"],
+                                       P[pre + ".shortcut.1.bias"])
+                    chk(pre + ".out", A[pre + ".out"], O.relu(z2 + zs))
+                else:
+                    chk(pre + ".out", A[pre + ".out"], O.relu(z2 + inp))
             inp = A[pre + ".out"]
     feat, lg = O.head_fwd(inp, P["linear.weight"], P["linear.bias"], bf16_mode=True)
-    chk("head.feat", A["head.feat_f32"].reshape(feat.shape), feat, 1e-5)
-    chk("logits", _np(logits), lg)
+    if 0 in stages:
+        chk("head.feat", A["head.feat_f32"].reshape(feat.shape), feat, 1e-5)
+        chk("logits", _np(logits), lg)
 
     # ---------------- backward, layer by layer (inputs = the executor's own intermediates)
     _, dl, _ = O.cross_entropy(_np(logits), y)
-    dw, db, dact = O.head_bwd(dl, A["head.feat_f32"].reshape(feat.shape), O.bf16(P["linear.weight"]), inp.shape[1:3])
-    chk("linear.weight.grad", grads["linear.weight"], dw, F32)
-    chk("linear.bias.grad", grads["linear.bias"], db, F32)
-    chk("grad.layer4.1.dy", G["grad.layer4.1.dy"], dact)
-    for pre, st, proj, inp in reversed(blocks):
+    if 0 in stages:
+        dw, db, dact = O.head_bwd(dl, A["head.feat_f32"].reshape(feat.shape), O.bf16(P["linear.weight"]),
+                                  inp.shape[1:3])
+        chk("linear.weight.grad", grads["linear.weight"], dw, F32)
+        chk("linear.bias.grad", grads["linear.bias"], db, F32)
+        chk("grad.layer4.1.dy", G["grad.layer4.1.dy"], dact)
+    for L, pre, st, proj, inp in reversed(blocks):
+        if L not in stages:
+            continue
         gp = "grad." + pre
-        np.testing.assert_array_equal(G[gp + ".dz"], np.where(A[pre + ".out"] > 0, G[gp + ".dy"], 0))
+        np.testing.assert_array_equal(G[gp + ".dz"][sel], np.where(A[pre + ".out"] > 0, G[gp + ".dy"], 0)[sel])
         dc2, dg2, db2 = _bn_bwd(G[gp + ".dz"], A[pre + ".conv2"], P[pre + ".bn2.weight"])
         chk(gp + ".dc2", G[gp + ".dc2"], dc2)
         chk(pre + ".bn2.weight.grad", grads[pre + ".bn2.weight"], dg2, 1e-3)
         chk(pre + ".bn2.bias.grad", grads[pre + ".bn2.bias"], db2, 1e-3)
         chk(pre + ".conv2.weight.grad", O.kcrs_to_krsc(grads[pre + ".conv2.weight"]),
             O.conv2d_wgrad(A[pre + ".relu1"], G[gp + ".dc2"], 3, 3, 1, 1), F32)
-        chk(gp + ".da1", G[gp + ".da1"], O.conv2d_dgrad(G[gp + ".dc2"], W[pre + ".conv2.weight"],
-                                                        A[pre + ".relu1"].shape[1:3], 1, 1))
-        np.testing.assert_array_equal(G[gp + ".dz1"], np.where(A[pre + ".relu1"] > 0, G[gp + ".da1"], 0))
+        chk(gp + ".da1", G[gp + ".da1"][sel], conv_d(G[gp + ".dc2"], W[pre + ".conv2.weight"],
+                                                     A[pre + ".relu1"].shape[1:3], 1, 1))
+        np.testing.assert_array_equal(G[gp + ".dz1"][sel], np.where(A[pre + ".relu1"] > 0, G[gp + ".da1"], 0)[sel])
         dc1, dg1, db1 = _bn_bwd(G[gp + ".dz1"], A[pre + ".conv1"], P[pre + ".bn1.weight"])
         chk(gp + ".dc1", G[gp + ".dc1"], dc1)
         chk(pre + ".bn1.weight.grad", grads[pre + ".bn1.weight"], dg1, 1e-3)
         chk(pre + ".conv1.weight.grad", O.kcrs_to_krsc(grads[pre + ".conv1.weight"]),
             O.conv2d_wgrad(inp, G[gp + ".dc1"], 3, 3, st, 1), F32)
-        dx = O.conv2d_dgrad(G[gp + ".dc1"], W[pre + ".conv1.weight"], inp.shape[1:3], st, 1)
+        dx = conv_d(G[gp + ".dc1"], W[pre + ".conv1.weight"], inp.shape[1:3], st, 1)
         if proj:
             ds, dgs, dbs = _bn_bwd(G[gp + ".dz"], A[pre + ".shortcut"], P[pre + ".shortcut.1.weight"])
             chk(gp + ".ds", G[gp + ".ds"], ds)
             chk(pre + ".shortcut.1.weight.grad", grads[pre + ".shortcut.1.weight"], dgs, 1e-3)
             chk(pre + ".shortcut.0.weight.grad", O.kcrs_to_krsc(grads[pre + ".shortcut.0.weight"]),
                 O.conv2d_wgrad(inp, G[gp + ".ds"], 1, 1, st, 0), F32)
-            chk(gp + ".dxs", G[gp + ".dxs"], O.conv2d_dgrad(G[gp + ".ds"], W[pre + ".shortcut.0.weight"],
-                                                            inp.shape[1:3], st, 0))
-            chk(gp + ".dx", G[gp + ".dx"], dx + G[gp + ".dxs"])
+            chk(gp + ".dxs", G[gp + ".dxs"][sel], conv_d(G[gp + ".ds"], W[pre + ".shortcut.0.weight"],
+                                                         inp.shape[1:3], st, 0))
+            chk(gp + ".dx", G[gp + ".dx"][sel], dx + G[gp + ".dxs"][sel])
         else:
-            chk(gp + ".dx", G[gp + ".dx"], dx + G[gp + ".dz"])
-    np.testing.assert_array_equal(G["grad.stem.dz"], np.where(A["stem.out"] > 0, G["grad.layer1.0.dx"], 0))
-    dc0, dg0, db0 = _bn_bwd(G["grad.stem.dz"], A["stem.conv"], P["bn1.weight"])
-    chk("grad.stem.dc", G["grad.stem.dc"], dc0)
-    chk("bn1.weight.grad", grads["bn1.weight"], dg0, 1e-3)
-    chk("conv1.weight.grad", O.kcrs_to_krsc(grads["conv1.weight"]), O.conv2d_wgrad(xb, G["grad.stem.dc"], 3, 3, 1, 1),
-        F32)
+            chk(gp + ".dx", G[gp + ".dx"][sel], dx + G[gp + ".dz"][sel])
+    if 0 in stages:
+        np.testing.assert_array_equal(G["grad.stem.dz"], np.where(A["stem.out"] > 0, G["grad.layer1.0.dx"], 0))
+        dc0, dg0, db0 = _bn_bwd(G["grad.stem.dz"], A["stem.conv"], P["bn1.weight"])
+        chk("grad.stem.dc", G["grad.stem.dc"], dc0)
+        chk("bn1.weight.grad", grads["bn1.weight"], dg0, 1e-3)
+        chk("conv1.weight.grad", O.kcrs_to_krsc(grads["conv1.weight"]),
+            O.conv2d_wgrad(xb, G["grad.stem.dc"], 3, 3, 1, 1), F32)
     bad = {k: v for k, v in errs.items() if v[0] > v[1]}
-    assert len(errs) > 90
+    worst = max(errs.items(), key=lambda kv: kv[1][0] / kv[1][1])
+    print(f"teacher-forced B={batch} {hw}x{hw} stages={stages}: {len(errs)} checks, worst {worst[0]} "
+          f"{worst[1][0]:.2e} (tol {worst[1][1]:.0e})")
     assert not bad, f"per-layer parity failures: {bad}"
+    return errs
+
+
+@pytest.mark.parametrize("batch", [2, 8])
+def test_per_layer_teacher_forced(dtc, cuda, batch):
+    errs = _teacher_forced(dtc, cuda, batch)
+    assert len(errs) > 90
+
+
+# BASELINE config 2 at its own size (B=256, 32x32): the launches bench.py times -- conv_c64's
+# multi-tile persistent walk, wgrad_halo at 256 splits on layer1, the halo layer2 tiles, split-K
+# layer3/4 fwd/dgrad/wgrad, the stride-2 parity classes -- against the oracle. Split by stage so each
+# test's numpy work stays well inside the per-test time limit; conv forward / dgrad compared on a
+# sample of 24 images spread over the batch (first, last, tile boundaries), everything that reduces
+# over the batch (BN, weight gradients) on all 256.
+_B256_IMGS = np.unique(np.concatenate([np.arange(4), np.arange(60, 68), np.arange(124, 132), np.arange(252, 256)]))
+
+
+@pytest.mark.parametrize("stages", [(0, 1), (2,), (3, 4)])
+def test_per_layer_teacher_forced_config2_b256(dtc, cuda, stages):
+    errs = _teacher_forced(dtc, cuda, 256, stages=stages, imgs=_B256_IMGS, seed=21)
+    assert len(errs) >= 20
+
+
+def test_per_layer_teacher_forced_224(dtc, cuda):
+    """BASELINE config 5's geometry (224x224, global pool; SURVEY §7 viii) at batch 2: every layer,
+    through the 64-bit-addressed implicit-GEMM path the 224x224 shapes take."""
+    errs = _teacher_forced(dtc, cuda, 2, hw=224, seed=22)
+    assert len(errs) > 90
+
+
+def test_config5_b512_224_step_properties(dtc, cuda):
+    """BASELINE config 5 at its full per-GPU size: batch 512 at 224x224 (activations > 2 GiB: the
+    largest is 512x224x224x64 bf16 = 3.3 GB). One AMP training step + SGD step must run and give a
+    finite loss near ln(100) for a fresh network, finite non-zero gradients in every parameter,
+    running statistics that moved, and a second step whose loss is finite too."""
+    torch.manual_seed(42)
+    model = dtc.ResNet18().to(cuda)
+    crit = dtc.CrossEntropyLoss()
+    opt = dtc.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    scaler = dtc.GradScaler()
+    g = torch.Generator(device=cuda).manual_seed(9)
+    x = torch.randn(512, 3, 224, 224, device=cuda, generator=g)
+    y = torch.randint(0, 100, (512,), device=cuda, generator=g)
+    rm0 = model.flat.bufs.clone()
+    losses = []
+    for _ in range(2):
+        opt.zero_grad()
+        with dtc.autocast():
+            loss = crit(model(x), y)
+        scaler.scale(loss).backward()
+        if not losses:
+            gr = model.flat.grads.clone()
+        scaler.step(opt)
+        scaler.update()
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    assert np.isfinite(losses).all() and 3.0 < losses[0] < 8.0, losses
+    assert bool(torch.isfinite(gr).all())  # the first step's (loss-scaled) gradients
+    lay = model.flat.layout
+    grn = gr.cpu().numpy()
+    for p in lay.params:
+        assert np.abs(grn[p.offset:p.offset + p.numel]).sum() > 0, p.name
+    assert float((model.flat.bufs - rm0).abs().sum()) > 0
+    assert int(model.state_dict()["bn1.num_batches_tracked"]) == 2
 
 
 @pytest.mark.parametrize("batch", [2, 8])
@@ -540,14 +629,67 @@ def test_dp_trainer_runs(dtc, cuda, tmp_path):
         assert all(k.startswith("module.") for k in sd)
 
 
+def _grads_with(model, crit, x, y, comm):
+    model._comm = comm
+    loss = crit(model(x), y)
+    loss.backward()
+    torch.cuda.synchronize()
+    return model.flat.grads.detach().cpu().numpy().copy()
+
+
 @pytest.mark.parametrize("graphs", [1, 0])
-def test_bucketed_allreduce_backward_one_rank(dtc, cuda, graphs):
-    """The N>1 DDP backward (ddp/trainer.py:157): the executor splits the backward at
-    bucket boundaries and issues each bucket's RCCL all-reduce on the communicator's side stream
-    (joined before the optimizer), captured into graph segments. Run here with a one-rank RCCL
-    communicator -- a SUM over one rank is the identity -- and a 1 MB bucket cap (many buckets /
-    segments): gradients must equal the no-communicator backward (up to the order of the fp64
-    BN-statistics atomics), on first use (capture) and on replay."""
+@pytest.mark.parametrize("cap_mb", [1.0, 5.0, 25.0])
+def test_reducer_reduces_every_bucket_once_after_its_producers(dtc, cuda, graphs, cap_mb):
+    """The N>1 DDP backward (ddp/trainer.py:157) on one GPU, made observable: a loopback
+    communicator (dtc_comm_init_loopback) replaces each bucket's ncclAllReduce with `bucket *= 2` on
+    the communicator's side stream and logs (address, count). Then, on capture AND on replay:
+      * the logged ranges are exactly the bucket plan, in backward-completion order, each once, and
+        together tile the flat gradient buffer [0, numel) with no gap or overlap;
+      * every bucket's gradients are exactly 2x the no-communicator gradients -- a bucket skipped
+        (1x), reduced twice (4x) or reduced before its producing kernels finished (they WRITE the
+        gradient, so the doubling would be overwritten: 1x) fails;
+      * with the DDP mean pre-scale of 1/2 (module._grad_scale, W=2) the result equals the local
+        gradient (the mean over two identical ranks).
+    The last bucket of the plan is only layer1 + the stem (the unavoidable exposed tail)."""
+    dtc._native.lib.dtc_set_option(b"graphs", graphs)
+    comm = dtc.parallel.Comm.loopback(cuda.index or 0, 2.0)
+    try:
+        torch.manual_seed(42)
+        model = dtc.ResNet18().to(cuda)
+        model.set_bucket_cap_mb(cap_mb)
+        buckets = model.buckets()
+        numel = model.flat.grads.numel()
+        assert buckets[0][0] == 0 and sum(n for _, n in buckets) == numel
+        assert all(o1 + n1 == o2 for (o1, n1), (o2, _) in zip(buckets, buckets[1:]))
+        assert buckets[-1][1] * 4 <= 2 * 2**20, buckets[-1]  # tail <= 2 MB (layer1 + stem: 0.57 MB)
+        crit = dtc.CrossEntropyLoss()
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(32, 3, 32, 32, generator=g).to(cuda)
+        y = torch.randint(0, 100, (32,), generator=g).to(cuda)
+        g0 = _grads_with(model, crit, x, y, None)
+        assert np.isfinite(g0).all() and np.abs(g0).sum() > 0
+        base = model.flat.grads.data_ptr()
+        for rep in range(2):  # first use (capture when graphs are on), then replay
+            comm.clear_log()
+            g1 = _grads_with(model, crit, x, y, comm)
+            log = comm.log()
+            assert all(is_bucket for _, _, is_bucket in log)
+            assert [((a - base) // 4, n) for a, n, _ in log] == buckets, (rep, log)
+            for off, n in buckets:
+                assert rel_err(g1[off:off + n], 2.0 * g0[off:off + n]) < 1e-3, (rep, off, n)
+        model._grad_scale = 0.5  # DDP over W=2 identical ranks: pre-divide by 2, SUM (x2) -> local grad
+        g2 = _grads_with(model, crit, x, y, comm)
+        assert rel_err(g2, g0) < 1e-3
+        model._comm, model._grad_scale = None, 1.0
+    finally:
+        comm.close()
+        dtc._native.lib.dtc_set_option(b"graphs", 1)
+
+
+@pytest.mark.parametrize("graphs", [1, 0])
+def test_bucketed_allreduce_backward_one_rank_rccl(dtc, cuda, graphs):
+    """The same backward through a real one-rank RCCL communicator (the production transport; a
+    one-rank SUM is the identity): gradients equal the no-communicator backward, capture and replay."""
     dtc._native.lib.dtc_set_option(b"graphs", graphs)
     comm = dtc.parallel.Comm(0, 1, dtc.parallel.Comm.unique_id(), cuda.index or 0)
     try:
@@ -559,26 +701,54 @@ def test_bucketed_allreduce_backward_one_rank(dtc, cuda, graphs):
         g = torch.Generator().manual_seed(3)
         x = torch.randn(32, 3, 32, 32, generator=g).to(cuda)
         y = torch.randint(0, 100, (32,), generator=g).to(cuda)
-
-        def grads(c):
-            model._comm = c
-            loss = crit(model(x), y)
-            loss.backward()
-            torch.cuda.synchronize()
-            return model.flat.grads.detach().cpu().numpy().copy()
-
-        g0 = grads(None)
-        g1 = grads(comm)
-        g2 = grads(comm)
-        assert np.isfinite(g0).all() and np.abs(g0).sum() > 0
+        g0 = _grads_with(model, crit, x, y, None)
+        g1 = _grads_with(model, crit, x, y, comm)
+        g2 = _grads_with(model, crit, x, y, comm)
         assert rel_err(g1, g0) < 1e-3 and rel_err(g2, g0) < 1e-3
-        # the last-completed (stem) and first-completed (linear) buckets both carry gradient
-        off, n = model.buckets()[-1]
-        assert np.abs(g1[off:off + n]).sum() > 0
         model._comm = None
     finally:
         comm.close()
         dtc._native.lib.dtc_set_option(b"graphs", 1)
+
+
+def test_sync_batchnorm_two_identical_ranks_loopback(dtc, cuda):
+    """SyncBatchNorm at W=2 on one GPU: a loopback communicator reporting 2 ranks doubles every BN
+    sum the executor all-reduces (= two ranks holding the same batch). Global statistics then equal
+    the local ones (sums x2, count x2), so logits, every gradient and the running statistics must equal
+    plain BN (dgamma/dbeta = (1/W) x the all-reduced sums = this rank's share, which DDP's mean then
+    averages -- torch SyncBN + DDP). A path that skipped a collective would halve that BN's mean / its
+    backward sums (sums x1, count x2) and fail. Every forward and backward BN all-reduce is logged:
+    20 BNs -> 20 forward + 20 backward in-stream collectives of 2*C fp64 values each (the compacted
+    [2][C] sums, not the 32 partial-sum slots).
+    """
+    comm = dtc.parallel.Comm.loopback(cuda.index or 0, 2.0, world=2)
+    try:
+        g = torch.Generator().manual_seed(5)
+        x = torch.randn(32, 3, 32, 32, generator=g).to(cuda)
+        y = torch.randint(0, 100, (32,), generator=g).to(cuda)
+        res = []
+        for sync in (False, True):
+            torch.manual_seed(42)
+            model = dtc.ResNet18().to(cuda)
+            if sync:
+                model = dtc.SyncBatchNorm.convert_sync_batchnorm(model)
+                model.set_sync_bn(comm)
+                comm.clear_log()
+            logits = model(x)
+            dtc.CrossEntropyLoss()(logits, y).backward()
+            torch.cuda.synchronize()
+            res.append((logits.detach().cpu().numpy(), model.flat.grads.detach().cpu().numpy().copy(),
+                        model.flat.bufs.detach().cpu().numpy().copy(), model))
+        (l0, g0, b0, m0), (l1, g1, b1, m1) = res
+        log = comm.log()
+        assert len(log) == 40 and not any(a for _, _, a in log)
+        chans = sorted(n for _, n, _ in log)
+        assert chans[0] == 2 * 64 and chans[-1] == 2 * 512
+        assert rel_err(l1, l0) < 1e-3 and rel_err(b1, b0) < 1e-5
+        assert rel_err(g1, g0) < 1e-3
+        m1.set_sync_bn(None)
+    finally:
+        comm.close()
 
 
 def test_sync_batchnorm_one_rank(dtc, cuda):

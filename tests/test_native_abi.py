@@ -65,9 +65,13 @@ def test_buckets_tile_the_gradient_buffer(dtc, cap_mb):
         assert off == pos and n > 0
         pos += n
     assert pos == lay.flat_numel
-    # every bucket but the last closes at a block boundary at or above the cap
+    # every bucket closes at a block boundary at or above the cap, except the one open when layer2's
+    # backward ends (closed there) and the last: layer1 + stem, the unavoidable tail
+    tail_start = min(p.offset for p in lay.params if p.name.startswith("layer1.") or p.name in
+                     ("conv1.weight", "bn1.weight", "bn1.bias"))
     for off, n in lay.buckets[:-1]:
-        assert n * 4 >= cap_mb * 2 ** 20
+        assert n * 4 >= cap_mb * 2 ** 20 or off + n == tail_start
+    assert lay.buckets[-1][0] == tail_start and lay.buckets[-1][1] * 4 < 0.6 * 2 ** 20
     # the first bucket starts with the head (linear.bias at offset 0): it is ready first
     names_at_0 = [p.name for p in lay.params if p.offset == 0]
     assert names_at_0 == ["linear.bias"]
@@ -88,3 +92,9 @@ def test_workspace_and_conv_plans(dtc):
     # 224x224 (BASELINE config 5) plans too
     dtc._native.call("dtc_rn18_create", C.byref(h), 8, 224, 224, 100, 25.0)
     lib.dtc_rn18_destroy(h)
+    # config 5 at its full per-GPU batch: 512 x 224 x 224 (activations > 2 GiB) plans and fits HBM
+    dtc._native.call("dtc_rn18_create", C.byref(h), 512, 224, 224, 100, 25.0)
+    ws = lib.dtc_rn18_workspace_bytes(h)
+    assert 30e9 < ws < 200e9, ws  # well inside 288 GB
+    lib.dtc_rn18_destroy(h)
+    assert lib.dtc_rn18_create(C.byref(h), 700, 224, 224, 100, 25.0) < 0  # int32 element-index guard

@@ -72,6 +72,39 @@ def test_oracle_fp32_matches_reference_forward_backward(model_sd):
         np.testing.assert_allclose(v[s["idx"]], s["val"], rtol=1e-5, atol=1e-7, err_msg=k)
 
 
+def test_torch_cpu_baseline_matches_reference(model_sd):
+    """oracle/torch_ref.py (bench.py's cpu_baseline, BASELINE config 1) is the reference's fp32
+    single step: loss, logits, every parameter gradient and the running statistics equal the
+    reference-produced fixture (same ATen CPU kernels, so to fp32 summation-order noise)."""
+    from oracle.torch_ref import TorchCPUStep
+
+    gold = _load("resnet18_b2.json")["fp32"]
+    m = TorchCPUStep({k: torch.from_numpy(v) for k, v in model_sd.items()})
+    g = np.random.default_rng(0)
+    x = torch.from_numpy(g.standard_normal((2, 3, 32, 32)).astype(np.float32))
+    y = torch.from_numpy(g.integers(0, 100, 2))
+    logits = m.forward(x)
+    loss = torch.nn.functional.cross_entropy(logits, y)
+    loss.backward()
+    assert abs(float(loss) - gold["loss"]) < 1e-5
+    np.testing.assert_allclose(logits.detach().numpy(), np.asarray(gold["logits"]), rtol=1e-4, atol=1e-5)
+    grads = m.grads()
+    for k, s in gold["grads"].items():
+        gk = grads[k].detach().numpy().astype(np.float64).ravel()
+        assert abs(np.linalg.norm(gk) - s["norm"]) <= 1e-4 * s["norm"] + 1e-7, k
+        np.testing.assert_allclose(gk[s["idx"]], s["val"], rtol=1e-3, atol=1e-6 * max(1.0, s["norm"]), err_msg=k)
+    for k, s in gold["running"].items():
+        v = m.buf[k].numpy().astype(np.float64).ravel()
+        np.testing.assert_allclose(v[s["idx"]], s["val"], rtol=1e-5, atol=1e-7, err_msg=k)
+    # and one optimizer step is torch SGD(nesterov) = the oracle's restatement
+    before = {k: v.detach().numpy().copy() for k, v in m.p.items()}
+    gnp = {k: v.detach().numpy().copy() for k, v in grads.items()}
+    m.opt.step()
+    for k in ("conv1.weight", "linear.bias", "layer4.1.conv2.weight"):
+        want, _ = O.sgd_nesterov(before[k], gnp[k], None, 0.1, 1e-4, 0.9, True)
+        np.testing.assert_allclose(m.p[k].detach().numpy(), want, rtol=1e-6, atol=1e-7, err_msg=k)
+
+
 def test_oracle_fp32_matches_reference_activations(model_sd):
     """Reference module outputs (forward hooks, NHWC) vs the oracle's per-layer activations."""
     gold = _load("resnet18_b2.json")["fp32"]["acts"]
