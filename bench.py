@@ -286,7 +286,7 @@ def main():
     ms, fl, cnt = (C.c_double * 3)(), (C.c_double * 3)(), (C.c_int * 3)()
     prof_elapsed = None
     if not args.no_live_roofline:
-        exe = model.module.executor(B, S, S)
+        exe = model.module.executor(B, S, S, "bf16")
         dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
         for i in range(2):
             step(args.warmup + args.steps + i)

@@ -100,6 +100,8 @@ _SIGS = {
     "dtc_rn18_num_buckets": (i32, [vp]),
     "dtc_rn18_bucket_info": (i32, [vp, i32, P64, P64]),
     "dtc_rn18_bind": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
+    "dtc_rn18_set_precision": (i32, [vp, i32]),
+    "dtc_rn18_precision": (i32, [vp]),
     "dtc_rn18_enable_capture": (i32, [vp]),
     "dtc_rn18_num_captures": (i32, [vp]),
     "dtc_rn18_capture_info": (i32, [vp, i32, C.POINTER(cstr), C.POINTER(sz), Pi32]),

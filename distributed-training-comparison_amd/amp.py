@@ -4,9 +4,9 @@ Reference: ``torch.cuda.amp.GradScaler()`` (src/ddp/main.py:25) used as
 ``scaler.scale(loss).backward(); scaler.step(optimizer); scaler.update()`` (trainer.py:157-159)
 inside ``torch.cuda.amp.autocast()`` (trainer.py:153).
 
-The native network always computes in bf16 with fp32 accumulation and fp32 master weights
-(the reference's fp16 autocast replaced by bf16, BASELINE.json north_star), so ``autocast`` is
-an API-compatible context manager only. GradScaler keeps torch's semantics exactly: the loss is
+Inside ``autocast`` the native network computes in bf16 with fp32 accumulation and fp32 master
+weights (the reference's fp16 autocast replaced by bf16, BASELINE.json north_star); outside it in
+fp32, like the reference without --amp. GradScaler keeps torch's semantics exactly: the loss is
 multiplied by ``scale``; before the step every gradient is checked for inf/NaN (after the DDP
 all-reduce, so all ranks agree); an overflowing step is skipped; ``scale`` backs off by 0.5 on
 overflow and grows by 2 after 2000 clean steps. ``found_inf`` and the scale never leave the GPU.
@@ -18,13 +18,21 @@ import contextlib
 import torch
 
 from . import ops
-from .nn import scaled_loss
+from .nn import is_autocast_enabled, scaled_loss, set_autocast_enabled
 
 
 @contextlib.contextmanager
 def autocast(enabled: bool = True, dtype=torch.bfloat16):
-    """API twin of torch.cuda.amp.autocast(); the native kernels are bf16 regardless."""
-    yield
+    """torch.cuda.amp.autocast() (trainer.py:153): inside it the native ResNet runs its bf16 executor
+    (bf16 activations, fp32 accumulation / statistics / master weights; the reference autocasts to
+    fp16, north_star asks for bf16); outside it, or with enabled=False, the fp32 executor -- the
+    reference's non-AMP path (trainer.py:160-165). Thread-local and nestable, as torch's."""
+    prev = is_autocast_enabled()
+    set_autocast_enabled(enabled)
+    try:
+        yield
+    finally:
+        set_autocast_enabled(prev)
 
 
 class GradScaler:

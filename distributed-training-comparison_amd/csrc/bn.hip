@@ -126,16 +126,17 @@ int bn_eval_coef(int C, const float* gamma, const float* beta, const float* runn
 // ------------------------------------------------------------------ forward apply
 enum { APPLY_PLAIN = 0, APPLY_RELU = 1, APPLY_ADD_RELU = 2, APPLY_DUAL_RELU = 3 };
 
-template <int MODE>
-__global__ void __launch_bounds__(256) bn_apply_kernel(const u16* __restrict__ x, const float* __restrict__ scale,
-                                                      const float* __restrict__ shift, const u16* __restrict__ x2,
+template <int MODE, typename T>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, const T* __restrict__ x2,
                                                       const float* __restrict__ scale2,
-                                                      const float* __restrict__ shift2, u16* __restrict__ y,
+                                                      const float* __restrict__ shift2, T* __restrict__ y,
                                                       int64_t nvec, int cvec) {
+  typedef Elt<T> E;
   for (int64_t v = blockIdx.x * (int64_t)256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
     const int c0 = (int)(v % cvec) * 8;
     float a[8], o[8];
-    unpack8(*(const uint4*)(x + v * 8), a);
+    E::unpack(E::ld(x + v * 8), a);
     const f32x4 s0 = *(const f32x4*)(scale + c0), s1 = *(const f32x4*)(scale + c0 + 4);
     const f32x4 h0 = *(const f32x4*)(shift + c0), h1 = *(const f32x4*)(shift + c0 + 4);
     const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
@@ -144,57 +145,61 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const u16* __restrict__ x
     for (int k = 0; k < 8; ++k) o[k] = a[k] * sc[k] + sh[k];
     if constexpr (MODE == APPLY_ADD_RELU) {
       float r[8];
-      unpack8(*(const uint4*)(x2 + v * 8), r);
-      // torch rounds the BN output to bf16 before `out += shortcut(x)` (autocast)
+      E::unpack(E::ld(x2 + v * 8), r);
+      // torch rounds the BN output to bf16 before `out += shortcut(x)` (autocast; identity in fp32)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = round_bf(o[k]) + r[k];
+      for (int k = 0; k < 8; ++k) o[k] = E::round(o[k]) + r[k];
     }
     if constexpr (MODE == APPLY_DUAL_RELU) {
       float r[8];
-      unpack8(*(const uint4*)(x2 + v * 8), r);
+      E::unpack(E::ld(x2 + v * 8), r);
       const f32x4 t0 = *(const f32x4*)(scale2 + c0), t1 = *(const f32x4*)(scale2 + c0 + 4);
       const f32x4 u0 = *(const f32x4*)(shift2 + c0), u1 = *(const f32x4*)(shift2 + c0 + 4);
       const float sc2[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
       const float sh2[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-      // torch rounds each BN output to bf16 before the residual add (autocast)
+      // torch rounds each BN output to bf16 before the residual add (autocast; identity in fp32)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = round_bf(o[k]) + round_bf(r[k] * sc2[k] + sh2[k]);
+      for (int k = 0; k < 8; ++k) o[k] = E::round(o[k]) + E::round(r[k] * sc2[k] + sh2[k]);
     }
     if constexpr (MODE != APPLY_PLAIN) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = fmaxf(o[k], 0.f);
     }
-    *(uint4*)(y + v * 8) = pack8(o);
+    E::st(y + v * 8, E::pack(o));
   }
 }
 
-template <int MODE>
-static int launch_apply(const u16* x, const float* s, const float* h, const u16* x2, const float* s2, const float* h2,
-                        u16* y, int64_t M, int C, hipStream_t st) {
+template <int MODE, typename T>
+static int launch_apply(const T* x, const float* s, const float* h, const T* x2, const float* s2, const float* h2,
+                        T* y, int64_t M, int C, hipStream_t st) {
   DTC_CHECK_ARG(x && s && h && y && C % 8 == 0 && M > 0, "bn_apply: bad args (C=%d)", C);
   const int64_t nvec = M * C / 8;
   const int blocks = (int)std::min<int64_t>(4096, (nvec + 255) / 256);
-  hipLaunchKernelGGL((bn_apply_kernel<MODE>), dim3(blocks), dim3(256), 0, st, x, s, h, x2, s2, h2, y, nvec, C / 8);
+  hipLaunchKernelGGL((bn_apply_kernel<MODE, T>), dim3(blocks), dim3(256), 0, st, x, s, h, x2, s2, h2, y, nvec, C / 8);
   DTC_LAUNCH_CHECK();
   return 0;
 }
 
-int bn_apply(const u16* x, const float* s, const float* h, u16* y, int64_t M, int C, hipStream_t st) {
-  return launch_apply<APPLY_PLAIN>(x, s, h, nullptr, nullptr, nullptr, y, M, C, st);
-}
-int bn_apply_relu(const u16* x, const float* s, const float* h, u16* y, int64_t M, int C, hipStream_t st) {
-  return launch_apply<APPLY_RELU>(x, s, h, nullptr, nullptr, nullptr, y, M, C, st);
-}
-int bn_apply_add_relu(const u16* x, const float* s, const float* h, const u16* res, u16* y, int64_t M, int C,
-                      hipStream_t st) {
-  DTC_CHECK_ARG(res != nullptr, "bn_apply_add_relu: residual required");
-  return launch_apply<APPLY_ADD_RELU>(x, s, h, res, nullptr, nullptr, y, M, C, st);
-}
-int bn_apply_dual_relu(const u16* x, const float* s, const float* h, const u16* x2, const float* s2, const float* h2,
-                       u16* y, int64_t M, int C, hipStream_t st) {
-  DTC_CHECK_ARG(x2 && s2 && h2, "bn_apply_dual_relu: second branch required");
-  return launch_apply<APPLY_DUAL_RELU>(x, s, h, x2, s2, h2, y, M, C, st);
-}
+#define DTC_BN_APPLY_DEFS(T)                                                                                      \
+  int bn_apply(const T* x, const float* s, const float* h, T* y, int64_t M, int C, hipStream_t st) {             \
+    return launch_apply<APPLY_PLAIN, T>(x, s, h, nullptr, nullptr, nullptr, y, M, C, st);                         \
+  }                                                                                                               \
+  int bn_apply_relu(const T* x, const float* s, const float* h, T* y, int64_t M, int C, hipStream_t st) {        \
+    return launch_apply<APPLY_RELU, T>(x, s, h, nullptr, nullptr, nullptr, y, M, C, st);                          \
+  }                                                                                                               \
+  int bn_apply_add_relu(const T* x, const float* s, const float* h, const T* res, T* y, int64_t M, int C,       \
+                        hipStream_t st) {                                                                         \
+    DTC_CHECK_ARG(res != nullptr, "bn_apply_add_relu: residual required");                                       \
+    return launch_apply<APPLY_ADD_RELU, T>(x, s, h, res, nullptr, nullptr, y, M, C, st);                          \
+  }                                                                                                               \
+  int bn_apply_dual_relu(const T* x, const float* s, const float* h, const T* x2, const float* s2, const float* h2, \
+                         T* y, int64_t M, int C, hipStream_t st) {                                               \
+    DTC_CHECK_ARG(x2 && s2 && h2, "bn_apply_dual_relu: second branch required");                                 \
+    return launch_apply<APPLY_DUAL_RELU, T>(x, s, h, x2, s2, h2, y, M, C, st);                                    \
+  }
+DTC_BN_APPLY_DEFS(u16)
+DTC_BN_APPLY_DEFS(float)
+#undef DTC_BN_APPLY_DEFS
 
 // ------------------------------------------------------------------ fused finalize + apply (forward)
 // The consumer computes the BN coefficients itself: workgroup (pixel block, 64-channel group)
@@ -257,10 +262,11 @@ __device__ __forceinline__ void fa_fwd_coef(const BnFwdArgs& A, int C, int cg, d
   __syncthreads();
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(256) bn_fin_apply_kernel(const u16* __restrict__ x, const BnFwdArgs a1,
-                                                          const u16* __restrict__ x2, const BnFwdArgs a2,
-                                                          u16* __restrict__ y, int64_t M, int C, int rows) {
+template <int MODE, typename T>
+__global__ void __launch_bounds__(256) bn_fin_apply_kernel(const T* __restrict__ x, const BnFwdArgs a1,
+                                                          const T* __restrict__ x2, const BnFwdArgs a2,
+                                                          T* __restrict__ y, int64_t M, int C, int rows) {
+  typedef Elt<T> E;
   __shared__ double part[4 * 2 * 64];
   __shared__ float coef[4][64];  // scale1, shift1, scale2, shift2
   const int cg = blockIdx.y * FA_GROUP;
@@ -281,14 +287,14 @@ __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const u16* __restrict
   // FA_UNROLL rows per thread per trip: every load of the trip is issued before the first
   // dependent use (memory-level parallelism); elementwise, so results are unchanged
   for (int64_t mb = m0 + pr; mb < m1; mb += 32 * FA_UNROLL) {
-    uint4 xa[FA_UNROLL], xr[FA_UNROLL];
+    typename E::V xa[FA_UNROLL], xr[FA_UNROLL];
 #pragma unroll
     for (int u = 0; u < FA_UNROLL; ++u) {
       const int64_t m = mb + 32 * u;
       if (m < m1) {
         const int64_t o = m * C + cg + q8;
-        xa[u] = *(const uint4*)(x + o);
-        if constexpr (MODE != APPLY_RELU) xr[u] = *(const uint4*)(x2 + o);
+        xa[u] = E::ld(x + o);
+        if constexpr (MODE != APPLY_RELU) xr[u] = E::ld(x2 + o);
       }
     }
 #pragma unroll
@@ -297,17 +303,17 @@ __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const u16* __restrict
       if (m >= m1) break;
       const int64_t o = m * C + cg + q8;
       float a[8], r[8], v[8];
-      unpack8(xa[u], a);
-      if constexpr (MODE != APPLY_RELU) unpack8(xr[u], r);
+      E::unpack(xa[u], a);
+      if constexpr (MODE != APPLY_RELU) E::unpack(xr[u], r);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         v[k] = a[k] * sc[k] + sh[k];
         // torch rounds each BN output to bf16 before the residual add (autocast)
-        if constexpr (MODE == APPLY_ADD_RELU) v[k] = round_bf(v[k]) + r[k];
-        if constexpr (MODE == APPLY_DUAL_RELU) v[k] = round_bf(v[k]) + round_bf(r[k] * sc2[k] + sh2[k]);
+        if constexpr (MODE == APPLY_ADD_RELU) v[k] = E::round(v[k]) + r[k];
+        if constexpr (MODE == APPLY_DUAL_RELU) v[k] = E::round(v[k]) + E::round(r[k] * sc2[k] + sh2[k]);
         v[k] = fmaxf(v[k], 0.f);
       }
-      *(uint4*)(y + o) = pack8(v);
+      E::st(y + o, E::pack(v));
     }
   }
 }
@@ -322,8 +328,9 @@ static void fa_grid(int64_t M, int C, int& nblk, int& rows) {
   nblk = (int)((M + rows - 1) / rows);
 }
 
-int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, const BnFwdArgs* a2, u16* y, int64_t M,
-                 int C, hipStream_t st) {
+template <typename T>
+static int fin_apply(int mode, const T* x, const BnFwdArgs& a1, const T* x2, const BnFwdArgs* a2, T* y, int64_t M,
+                     int C, hipStream_t st) {
   DTC_CHECK_ARG(x && y && a1.stats && a1.gamma && a1.beta && a1.mean && a1.invstd && C % FA_GROUP == 0 && M > 0,
                 "bn_fin_apply: bad args (C=%d)", C);
   int nblk, rows;
@@ -332,19 +339,28 @@ int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, con
   const BnFwdArgs none{};
   switch (mode) {
     case APPLY_RELU:
-      hipLaunchKernelGGL(bn_fin_apply_kernel<APPLY_RELU>, grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows);
+      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows);
       break;
     case APPLY_ADD_RELU:
       DTC_CHECK_ARG(x2 != nullptr, "bn_fin_apply: residual required");
-      hipLaunchKernelGGL(bn_fin_apply_kernel<APPLY_ADD_RELU>, grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows);
+      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_ADD_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows);
       break;
     default:
       DTC_CHECK_ARG(x2 && a2 && a2->stats, "bn_fin_apply: second branch required");
-      hipLaunchKernelGGL(bn_fin_apply_kernel<APPLY_DUAL_RELU>, grid, dim3(256), 0, st, x, a1, x2, *a2, y, M, C, rows);
+      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_DUAL_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, *a2, y, M, C, rows);
       break;
   }
   DTC_LAUNCH_CHECK();
   return 0;
+}
+
+int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, const BnFwdArgs* a2, u16* y, int64_t M,
+                 int C, hipStream_t st) {
+  return fin_apply<u16>(mode, x, a1, x2, a2, y, M, C, st);
+}
+int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2, const BnFwdArgs* a2, float* y,
+                 int64_t M, int C, hipStream_t st) {
+  return fin_apply<float>(mode, x, a1, x2, a2, y, M, C, st);
 }
 
 // ------------------------------------------------------------------ fused finalize + apply (backward)
@@ -372,11 +388,12 @@ __device__ __forceinline__ void fa_bwd_coef(const BnBwdArgs& A, int C, int cg, d
   __syncthreads();
 }
 
-template <bool DUAL>
-__global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const u16* __restrict__ dz, const u16* __restrict__ x1,
-                                                              const BnBwdArgs a1, u16* __restrict__ dx1,
-                                                              const u16* __restrict__ x2, const BnBwdArgs a2,
-                                                              u16* __restrict__ dx2, int64_t M, int C, int rows) {
+template <bool DUAL, typename T>
+__global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restrict__ dz, const T* __restrict__ x1,
+                                                              const BnBwdArgs a1, T* __restrict__ dx1,
+                                                              const T* __restrict__ x2, const BnBwdArgs a2,
+                                                              T* __restrict__ dx2, int64_t M, int C, int rows) {
+  typedef Elt<T> E;
   __shared__ double part[4 * 2 * 64];
   __shared__ float coef[6][64];
   const int cg = blockIdx.y * FA_GROUP;
@@ -393,15 +410,15 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const u16* __rest
   }
   const int64_t m0 = (int64_t)blockIdx.x * rows, m1 = std::min<int64_t>(M, m0 + rows);
   for (int64_t mb = m0 + pr; mb < m1; mb += 32 * FA_UNROLL) {  // loads of a trip first (see bn_fin_apply)
-    uint4 vd[FA_UNROLL], va[FA_UNROLL], vb[FA_UNROLL];
+    typename E::V vd[FA_UNROLL], va[FA_UNROLL], vb[FA_UNROLL];
 #pragma unroll
     for (int u = 0; u < FA_UNROLL; ++u) {
       const int64_t m = mb + 32 * u;
       if (m < m1) {
         const int64_t o = m * C + cg + q8;
-        vd[u] = *(const uint4*)(dz + o);
-        va[u] = *(const uint4*)(x1 + o);
-        if constexpr (DUAL) vb[u] = *(const uint4*)(x2 + o);
+        vd[u] = E::ld(dz + o);
+        va[u] = E::ld(x1 + o);
+        if constexpr (DUAL) vb[u] = E::ld(x2 + o);
       }
     }
 #pragma unroll
@@ -410,23 +427,24 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const u16* __rest
       if (m >= m1) break;
       const int64_t o = m * C + cg + q8;
       float d[8], a[8], v[8];
-      unpack8(vd[u], d);
-      unpack8(va[u], a);
+      E::unpack(vd[u], d);
+      E::unpack(va[u], a);
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = A1[k] * d[k] + B1[k] * a[k] + C1[k];
-      *(uint4*)(dx1 + o) = pack8(v);
+      E::st(dx1 + o, E::pack(v));
       if constexpr (DUAL) {
-        unpack8(vb[u], a);
+        E::unpack(vb[u], a);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = A2[k] * d[k] + B2[k] * a[k] + C2[k];
-        *(uint4*)(dx2 + o) = pack8(v);
+        E::st(dx2 + o, E::pack(v));
       }
     }
   }
 }
 
-int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
-                     u16* dx2, int64_t M, int C, hipStream_t st) {
+template <typename T>
+static int bwd_fin_apply(const T* dz, const T* x1, const BnBwdArgs& a1, T* dx1, const T* x2, const BnBwdArgs* a2,
+                         T* dx2, int64_t M, int C, hipStream_t st) {
   DTC_CHECK_ARG(dz && x1 && dx1 && a1.acc && a1.gamma && a1.mean && a1.invstd && C % FA_GROUP == 0 && M > 0,
                 "bn_bwd_fin_apply: bad args (C=%d)", C);
   int nblk, rows;
@@ -434,24 +452,34 @@ int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1
   const dim3 grid(nblk, C / FA_GROUP);
   if (x2) {
     DTC_CHECK_ARG(a2 && a2->acc && dx2, "bn_bwd_fin_apply: dual branch args");
-    hipLaunchKernelGGL(bn_bwd_fin_apply_kernel<true>, grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, *a2, dx2, M, C,
+    hipLaunchKernelGGL((bn_bwd_fin_apply_kernel<true, T>), grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, *a2, dx2, M, C,
                        rows);
   } else {
     const BnBwdArgs none{};
-    hipLaunchKernelGGL(bn_bwd_fin_apply_kernel<false>, grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, none, dx2, M, C,
+    hipLaunchKernelGGL((bn_bwd_fin_apply_kernel<false, T>), grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, none, dx2, M, C,
                        rows);
   }
   DTC_LAUNCH_CHECK();
   return 0;
 }
 
+int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
+                     u16* dx2, int64_t M, int C, hipStream_t st) {
+  return bwd_fin_apply<u16>(dz, x1, a1, dx1, x2, a2, dx2, M, C, st);
+}
+int bn_bwd_fin_apply(const float* dz, const float* x1, const BnBwdArgs& a1, float* dx1, const float* x2,
+                     const BnBwdArgs* a2, float* dx2, int64_t M, int C, hipStream_t st) {
+  return bwd_fin_apply<float>(dz, x1, a1, dx1, x2, a2, dx2, M, C, st);
+}
+
 // ------------------------------------------------------------------ backward
-template <bool MASK, bool DUAL>
+template <bool MASK, bool DUAL, typename T>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
-    const u16* __restrict__ dy, const u16* __restrict__ ym, const u16* __restrict__ x1,
+    const T* __restrict__ dy, const T* __restrict__ ym, const T* __restrict__ x1,
     const float* __restrict__ mean1, const float* __restrict__ invstd1, double* __restrict__ acc1,
-    const u16* __restrict__ x2, const float* __restrict__ mean2, const float* __restrict__ invstd2,
-    double* __restrict__ acc2, u16* __restrict__ dz, int64_t M, int C, int rows_per_block) {
+    const T* __restrict__ x2, const float* __restrict__ mean2, const float* __restrict__ invstd2,
+    double* __restrict__ acc2, T* __restrict__ dz, int64_t M, int C, int rows_per_block) {
+  typedef Elt<T> E;
   __shared__ float red[256 * 24];
   const int tpr = C >> 3, rpp = 256 / tpr;
   const int t = threadIdx.x, g = t % tpr, rr = t / tpr;
@@ -472,15 +500,15 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
   for (int64_t m = m_begin + rr; m < m_end; m += rpp) {
     const int64_t o = m * C + c0;
     float d[8], a[8];
-    unpack8(*(const uint4*)(dy + o), d);
+    E::unpack(E::ld(dy + o), d);
     if constexpr (MASK) {
       float yv[8];
-      unpack8(*(const uint4*)(ym + o), yv);
+      E::unpack(E::ld(ym + o), yv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
-      *(uint4*)(dz + o) = pack8(d);  // exact: masking a bf16 value is exact
+      E::st(dz + o, E::pack(d));  // exact: masking is exact
     }
-    unpack8(*(const uint4*)(x1 + o), a);
+    E::unpack(E::ld(x1 + o), a);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       sd[k] += d[k];
@@ -488,7 +516,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     }
     if constexpr (DUAL) {
       float b[8];
-      unpack8(*(const uint4*)(x2 + o), b);
+      E::unpack(E::ld(x2 + o), b);
 #pragma unroll
       for (int k = 0; k < 8; ++k) s2[k] += d[k] * ((b[k] - m2[k]) * i2[k]);
     }
@@ -519,9 +547,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
   }
 }
 
-int bn_bwd_reduce(const u16* dy, const u16* ymask, const u16* x1, const float* mean1, const float* invstd1,
-                  double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, u16* dz,
-                  int64_t M, int C, hipStream_t st) {
+template <typename T>
+static int bwd_reduce(const T* dy, const T* ymask, const T* x1, const float* mean1, const float* invstd1, double* acc1,
+                      const T* x2, const float* mean2, const float* invstd2, double* acc2, T* dz, int64_t M, int C,
+                      hipStream_t st) {
   DTC_CHECK_ARG(dy && x1 && mean1 && invstd1 && acc1 && C % 8 == 0 && C <= 2048 && M > 0, "bn_bwd_reduce: bad args");
   DTC_CHECK_ARG(!ymask || dz, "bn_bwd_reduce: masked reduce needs a dz output");
   const int tpr = C / 8, rpp = 256 / tpr;
@@ -533,19 +562,30 @@ int bn_bwd_reduce(const u16* dy, const u16* ymask, const u16* x1, const float* m
   const bool dual = x2 != nullptr;
   if (dual) DTC_CHECK_ARG(mean2 && invstd2 && acc2, "bn_bwd_reduce: dual branch args");
   if (ymask && dual)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, true>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1, invstd1,
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, true, T>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1, invstd1,
                        acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
   else if (ymask)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, false>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, false, T>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
                        invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
   else if (dual)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, true>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, true, T>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
                        invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
   else
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false, T>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
                        invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
   DTC_LAUNCH_CHECK();
   return 0;
+}
+
+int bn_bwd_reduce(const u16* dy, const u16* ymask, const u16* x1, const float* mean1, const float* invstd1,
+                  double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, u16* dz,
+                  int64_t M, int C, hipStream_t st) {
+  return bwd_reduce<u16>(dy, ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, st);
+}
+int bn_bwd_reduce(const float* dy, const float* ymask, const float* x1, const float* mean1, const float* invstd1,
+                  double* acc1, const float* x2, const float* mean2, const float* invstd2, double* acc2, float* dz,
+                  int64_t M, int C, hipStream_t st) {
+  return bwd_reduce<float>(dy, ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, st);
 }
 
 __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
@@ -576,44 +616,55 @@ int bn_bwd_finalize(double* acc, int C, int64_t count, const float* gamma, const
   return 0;
 }
 
-template <bool DUAL>
-__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const u16* __restrict__ dz, const u16* __restrict__ x1,
-                                                          const float* __restrict__ coef1, u16* __restrict__ dx1,
-                                                          const u16* __restrict__ x2, const float* __restrict__ coef2,
-                                                          u16* __restrict__ dx2, int64_t nvec, int C) {
+template <bool DUAL, typename T>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__ dz, const T* __restrict__ x1,
+                                                          const float* __restrict__ coef1, T* __restrict__ dx1,
+                                                          const T* __restrict__ x2, const float* __restrict__ coef2,
+                                                          T* __restrict__ dx2, int64_t nvec, int C) {
+  typedef Elt<T> E;
   const int cvec = C >> 3;
   for (int64_t v = blockIdx.x * (int64_t)256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
     const int c0 = (int)(v % cvec) * 8;
     float d[8], a[8], o[8];
-    unpack8(*(const uint4*)(dz + v * 8), d);
-    unpack8(*(const uint4*)(x1 + v * 8), a);
+    E::unpack(E::ld(dz + v * 8), d);
+    E::unpack(E::ld(x1 + v * 8), a);
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = coef1[c0 + k] * d[k] + coef1[C + c0 + k] * a[k] + coef1[2 * C + c0 + k];
-    *(uint4*)(dx1 + v * 8) = pack8(o);
+    E::st(dx1 + v * 8, E::pack(o));
     if constexpr (DUAL) {
-      unpack8(*(const uint4*)(x2 + v * 8), a);
+      E::unpack(E::ld(x2 + v * 8), a);
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = coef2[c0 + k] * d[k] + coef2[C + c0 + k] * a[k] + coef2[2 * C + c0 + k];
-      *(uint4*)(dx2 + v * 8) = pack8(o);
+      E::st(dx2 + v * 8, E::pack(o));
     }
   }
 }
 
-int bn_bwd_apply(const u16* dz, const u16* x1, const float* coef1, u16* dx1, const u16* x2, const float* coef2,
-                 u16* dx2, int64_t M, int C, hipStream_t st) {
+template <typename T>
+static int bwd_apply(const T* dz, const T* x1, const float* coef1, T* dx1, const T* x2, const float* coef2, T* dx2,
+                     int64_t M, int C, hipStream_t st) {
   DTC_CHECK_ARG(dz && x1 && coef1 && dx1 && C % 8 == 0 && M > 0, "bn_bwd_apply: bad args");
   const int64_t nvec = M * C / 8;
   const int blocks = (int)std::min<int64_t>(4096, (nvec + 255) / 256);
   if (x2) {
     DTC_CHECK_ARG(coef2 && dx2, "bn_bwd_apply: dual branch args");
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(blocks), dim3(256), 0, st, dz, x1, coef1, dx1, x2, coef2, dx2,
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, T>), dim3(blocks), dim3(256), 0, st, dz, x1, coef1, dx1, x2, coef2, dx2,
                        nvec, C);
   } else {
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(blocks), dim3(256), 0, st, dz, x1, coef1, dx1, x2, coef2,
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, T>), dim3(blocks), dim3(256), 0, st, dz, x1, coef1, dx1, x2, coef2,
                        dx2, nvec, C);
   }
   DTC_LAUNCH_CHECK();
   return 0;
+}
+
+int bn_bwd_apply(const u16* dz, const u16* x1, const float* coef1, u16* dx1, const u16* x2, const float* coef2,
+                 u16* dx2, int64_t M, int C, hipStream_t st) {
+  return bwd_apply<u16>(dz, x1, coef1, dx1, x2, coef2, dx2, M, C, st);
+}
+int bn_bwd_apply(const float* dz, const float* x1, const float* coef1, float* dx1, const float* x2, const float* coef2,
+                 float* dx2, int64_t M, int C, hipStream_t st) {
+  return bwd_apply<float>(dz, x1, coef1, dx1, x2, coef2, dx2, M, C, st);
 }
 
 // ---------------------------------------------------------------- SyncBN slot compaction

@@ -66,6 +66,47 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return v;
 }
 
+// ---------------------------------------------------------------- activation element traits
+// The executor runs activations either as bf16 (AMP: autocast rounding points) or as fp32 (the
+// reference without --amp, ddp/trainer.py:160-165). Elementwise kernels are written once over
+// 8-element vectors: V = the raw 8-element register image (16 B of bf16 or 32 B of fp32),
+// round() = the autocast rounding of an intermediate (identity in fp32 mode).
+template <typename T>
+struct Elt;
+template <>
+struct Elt<u16> {
+  typedef uint4 V;
+  static __device__ __forceinline__ V ld(const u16* p) { return *(const uint4*)p; }
+  static __device__ __forceinline__ void st(u16* p, const V& v) { *(uint4*)p = v; }
+  static __device__ __forceinline__ void unpack(const V& v, float* f) { unpack8(v, f); }
+  static __device__ __forceinline__ V pack(const float* f) { return pack8(f); }
+  static __device__ __forceinline__ float round(float x) { return round_bf(x); }
+  static __device__ __forceinline__ float cvt(u16 v) { return bf2f(v); }
+  static __device__ __forceinline__ u16 from(float f) { return f2bf(f); }
+};
+struct F32x8 {
+  f32x4 a, b;
+};
+template <>
+struct Elt<float> {
+  typedef F32x8 V;
+  static __device__ __forceinline__ V ld(const float* p) { return V{*(const f32x4*)p, *(const f32x4*)(p + 4)}; }
+  static __device__ __forceinline__ void st(float* p, const V& v) {
+    *(f32x4*)p = v.a;
+    *(f32x4*)(p + 4) = v.b;
+  }
+  static __device__ __forceinline__ void unpack(const V& v, float* f) {
+    f[0] = v.a[0]; f[1] = v.a[1]; f[2] = v.a[2]; f[3] = v.a[3];
+    f[4] = v.b[0]; f[5] = v.b[1]; f[6] = v.b[2]; f[7] = v.b[3];
+  }
+  static __device__ __forceinline__ V pack(const float* f) {
+    return V{f32x4{f[0], f[1], f[2], f[3]}, f32x4{f[4], f[5], f[6], f[7]}};
+  }
+  static __device__ __forceinline__ float round(float x) { return x; }
+  static __device__ __forceinline__ float cvt(float v) { return v; }
+  static __device__ __forceinline__ float from(float f) { return f; }
+};
+
 // ---------------------------------------------------------------- fast unsigned division
 // q = (umulhi(n, m) + n) >> s, exact for n < 2^31 (pixel indices here are < 2^31).
 struct FastDiv {

@@ -82,22 +82,24 @@ int stem_pack_weight(const u16* w27, u16* w64, int K, hipStream_t st) {
 // channel quarter `wave` and its lanes classes j0 + lane: an independent 8-wide FMA chain per
 // lane (no cross-lane reduction per class), the four quarter sums then added in LDS. Both
 // reductions have a fixed order: deterministic.
-__global__ void __launch_bounds__(256) head_fwd_kernel(const u16* __restrict__ act, int HW, int C,
-                                                      const u16* __restrict__ wfc, const float* __restrict__ bfc,
+template <typename T>
+__global__ void __launch_bounds__(256) head_fwd_kernel(const T* __restrict__ act, int HW, int C,
+                                                      const T* __restrict__ wfc, const float* __restrict__ bfc,
                                                       int ncls, float* __restrict__ feat, float* __restrict__ logits) {
+  typedef Elt<T> E;
   extern __shared__ float hsm[];  // [C] feat, then [256 / (C/8)][C] pool partials
   const int n = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int tpr = C >> 3, groups = max(1, 256 / tpr);
   float* fs = hsm;
   float* part = hsm + C;
-  const u16* a = act + (int64_t)n * HW * C;
+  const T* a = act + (int64_t)n * HW * C;
   for (int c8 = t % tpr; c8 < tpr; c8 += 256) {  // (tpr > 256: threads loop over channel groups)
     const int g = t / tpr;
     if (g >= groups) break;
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int p = g; p < HW; p += groups) {
       float v[8];
-      unpack8(*(const uint4*)(a + (int64_t)p * C + c8 * 8), v);
+      E::unpack(E::ld(a + (int64_t)p * C + c8 * 8), v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) s[k] += v[k];
     }
@@ -108,7 +110,7 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const u16* __restrict__ a
   for (int c = t; c < C; c += 256) {
     float s = 0.f;
     for (int g = 0; g < groups; ++g) s += part[g * C + c];
-    const float f = round_bf(s / (float)HW);
+    const float f = E::round(s / (float)HW);
     fs[c] = f;
     feat[(int64_t)n * C + c] = f;
   }
@@ -119,10 +121,10 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const u16* __restrict__ a
     const int j = j0 + lane;
     float acc = 0.f;
     if (j < ncls) {
-      const u16* w = wfc + (int64_t)j * C + cb;
+      const T* w = wfc + (int64_t)j * C + cb;
       for (int c8 = 0; c8 < q8; ++c8) {
         float wv[8];
-        unpack8(*(const uint4*)(w + c8 * 8), wv);
+        E::unpack(E::ld(w + c8 * 8), wv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc += fs[cb + c8 * 8 + k] * wv[k];
       }
@@ -131,22 +133,31 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const u16* __restrict__ a
     __syncthreads();
     if (t < 64 && j0 + t < ncls) {
       const float s = part[t] + part[64 + t] + part[128 + t] + part[192 + t];
-      logits[(int64_t)n * ncls + j0 + t] = round_bf(s + round_bf(bfc[j0 + t]));
+      logits[(int64_t)n * ncls + j0 + t] = E::round(s + E::round(bfc[j0 + t]));
     }
     __syncthreads();
   }
 }
 
-int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
-             float* logits, hipStream_t st) {
+template <typename T>
+static int head_fwd_t(const T* act, int N, int HW, int C, const T* wfc, const float* bfc, int ncls, float* feat,
+                      float* logits, hipStream_t st) {
   DTC_CHECK_ARG(act && wfc && bfc && feat && logits && N > 0 && HW > 0 && C > 0 && C % 32 == 0 && C <= 2048 &&
                     ncls > 0,
                 "head_fwd: bad args");
   const int groups = std::max(1, 256 / (C / 8));
   const size_t lds = (size_t)(C + std::max(groups * C, 256)) * sizeof(float);
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(N), dim3(256), lds, st, act, HW, C, wfc, bfc, ncls, feat, logits);
+  hipLaunchKernelGGL(head_fwd_kernel<T>, dim3(N), dim3(256), lds, st, act, HW, C, wfc, bfc, ncls, feat, logits);
   DTC_LAUNCH_CHECK();
   return 0;
+}
+int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
+             float* logits, hipStream_t st) {
+  return head_fwd_t<u16>(act, N, HW, C, wfc, bfc, ncls, feat, logits, st);
+}
+int head_fwd(const float* act, int N, int HW, int C, const float* wfc, const float* bfc, int ncls, float* feat,
+             float* logits, hipStream_t st) {
+  return head_fwd_t<float>(act, N, HW, C, wfc, bfc, ncls, feat, logits, st);
 }
 
 // per-row log-sum-exp: one wave per row
@@ -279,24 +290,27 @@ size_t head_bwd_workspace(int N, int C, int ncls) {
 }
 
 // dact[n][p][c] = (sum_j dl[n][j] * W[j][c]) / HW
-__global__ void __launch_bounds__(256) head_bwd_x_kernel(const float* __restrict__ dl, const u16* __restrict__ wfc,
-                                                        int HW, int C, int ncls, u16* __restrict__ dact) {
+template <typename T>
+__global__ void __launch_bounds__(256) head_bwd_x_kernel(const float* __restrict__ dl, const T* __restrict__ wfc,
+                                                        int HW, int C, int ncls, T* __restrict__ dact) {
+  typedef Elt<T> E;
   extern __shared__ float row[];
   const int n = blockIdx.x, t = threadIdx.x;
   for (int j = t; j < ncls; j += 256) row[j] = dl[(int64_t)n * ncls + j];
   __syncthreads();
   const float inv = 1.f / (float)HW;
-  u16* o = dact + (int64_t)n * HW * C;
+  T* o = dact + (int64_t)n * HW * C;
   for (int c = t; c < C; c += 256) {
     float s = 0.f;
-    for (int j = 0; j < ncls; ++j) s += row[j] * bf2f(wfc[(int64_t)j * C + c]);
-    const u16 v = f2bf(s * inv);
+    for (int j = 0; j < ncls; ++j) s += row[j] * E::cvt(wfc[(int64_t)j * C + c]);
+    const T v = E::from(s * inv);
     for (int p = 0; p < HW; ++p) o[(int64_t)p * C + c] = v;
   }
 }
 
-int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int HW, int C, int ncls, float scale,
-             float* dw, float* db, u16* dact, float* ws, size_t ws_bytes, hipStream_t st) {
+template <typename T>
+static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int N, int HW, int C, int ncls,
+                      float scale, float* dw, float* db, T* dact, float* ws, size_t ws_bytes, hipStream_t st) {
   DTC_CHECK_ARG(dlogits && feat && wfc && dw && db && dact && N > 0 && HW > 0 && C > 0 && ncls > 0,
                 "head_bwd: bad args");
   DTC_CHECK_ARG(ws && ws_bytes >= head_bwd_workspace(N, C, ncls), "head_bwd: workspace too small");
@@ -307,10 +321,18 @@ int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int
   hipLaunchKernelGGL(head_bwd_w_reduce_kernel, dim3((int)(((int64_t)ncls * C + 255) / 256)), dim3(256), 0, st, ws,
                      splits, dlogits, N, C, ncls, scale, dw, db);
   DTC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(head_bwd_x_kernel, dim3(N), dim3(256), ncls * sizeof(float), st, dlogits, wfc, HW, C, ncls,
+  hipLaunchKernelGGL(head_bwd_x_kernel<T>, dim3(N), dim3(256), ncls * sizeof(float), st, dlogits, wfc, HW, C, ncls,
                      dact);
   DTC_LAUNCH_CHECK();
   return 0;
+}
+int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int HW, int C, int ncls, float scale,
+             float* dw, float* db, u16* dact, float* ws, size_t ws_bytes, hipStream_t st) {
+  return head_bwd_t<u16>(dlogits, feat, wfc, N, HW, C, ncls, scale, dw, db, dact, ws, ws_bytes, st);
+}
+int head_bwd(const float* dlogits, const float* feat, const float* wfc, int N, int HW, int C, int ncls, float scale,
+             float* dw, float* db, float* dact, float* ws, size_t ws_bytes, hipStream_t st) {
+  return head_bwd_t<float>(dlogits, feat, wfc, N, HW, C, ncls, scale, dw, db, dact, ws, ws_bytes, st);
 }
 
 }  // namespace dtc

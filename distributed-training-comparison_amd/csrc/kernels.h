@@ -89,6 +89,16 @@ int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const 
 // per slot i of ts[n][DTC_PROF_SLOT_U64]: acc[i] += (max end - min start, 1) if stamped; cells reset
 int prof_accumulate(u64* ts, int n, u64* acc, hipStream_t st);
 
+// fp32 mode (conv_f32.hip): fp32 in / fp32 out implicit GEMM on v_mfma_f32_16x16x4_f32.
+// FWD: out = y (+ BN stats into `stats`); DGRAD: out = dx (+ res); WGRAD: dw[k][0:dw_cols] (row stride
+// dw_ld; 0 = R*S*C) = scale * sum over pixels, via split-K slabs in `slab`. C and K multiples of 16.
+int conv_f32(const ConvShape& s, int mode, const float* a, const float* b, float* out, const float* res,
+             double* stats, float* dw, int dw_cols, int dw_ld, float scale, float* slab, size_t slab_bytes,
+             hipStream_t st, u64* ts = nullptr);
+size_t f32_conv_workspace(const ConvShape& s, int mode);  // fp32 slab bytes the pass wants
+int f32_stem_im2col(const float* x, float* cols, int N, int H, int W, hipStream_t st);  // [N*H*W][32]
+int f32_stem_pack_weight(const float* w27, float* w32, int K, hipStream_t st);          // [K][27] -> [K][32]
+
 // ------------------------------------------------------------------ batch norm (NHWC, C channels, M pixels)
 // forward finalize: mean/invstd/scale/shift from stats; running-stat update; stats re-zeroed.
 int bn_fwd_finalize(double* stats, int C, int64_t count, const float* gamma, const float* beta,
@@ -107,6 +117,13 @@ int bn_apply_dual_relu(const u16* x, const float* scale, const float* shift, con
                        const float* shift2, u16* y, int64_t M, int C, hipStream_t st);
 // y = x*scale + shift (no activation; eval helpers / tests)
 int bn_apply(const u16* x, const float* scale, const float* shift, u16* y, int64_t M, int C, hipStream_t st);
+// fp32-activation versions of the four (fp32 mode: the reference without --amp)
+int bn_apply_relu(const float* x, const float* scale, const float* shift, float* y, int64_t M, int C, hipStream_t st);
+int bn_apply_add_relu(const float* x, const float* scale, const float* shift, const float* res, float* y, int64_t M,
+                      int C, hipStream_t st);
+int bn_apply_dual_relu(const float* x, const float* scale, const float* shift, const float* x2, const float* scale2,
+                       const float* shift2, float* y, int64_t M, int C, hipStream_t st);
+int bn_apply(const float* x, const float* scale, const float* shift, float* y, int64_t M, int C, hipStream_t st);
 
 // Fused finalize + apply: the coefficients are computed by the consumer from the fp64 slots
 // (bn.hip); the first pixel block writes the saved / running statistics (forward) or dgamma /
@@ -138,6 +155,10 @@ int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, con
                  int C, hipStream_t st);
 int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
                      u16* dx2, int64_t M, int C, hipStream_t st);
+int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2, const BnFwdArgs* a2, float* y,
+                 int64_t M, int C, hipStream_t st);
+int bn_bwd_fin_apply(const float* dz, const float* x1, const BnBwdArgs& a1, float* dx1, const float* x2,
+                     const BnBwdArgs* a2, float* dx2, int64_t M, int C, hipStream_t st);
 
 // slots [SLOTS][2][C] -> slot 0 holds the fixed-order sum over the slots, the others are zeroed
 int bn_fold_slots(double* slots, int C, hipStream_t st);
@@ -145,12 +166,17 @@ int bn_fold_slots(double* slots, int C, hipStream_t st);
 int bn_bwd_reduce(const u16* dy, const u16* ymask, const u16* x1, const float* mean1, const float* invstd1,
                   double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, u16* dz,
                   int64_t M, int C, hipStream_t st);
+int bn_bwd_reduce(const float* dy, const float* ymask, const float* x1, const float* mean1, const float* invstd1,
+                  double* acc1, const float* x2, const float* mean2, const float* invstd2, double* acc2, float* dz,
+                  int64_t M, int C, hipStream_t st);
 // dgamma/dbeta (scaled by gscale) into the flat grad buffer; apply coefficients coef[3][C]; acc re-zeroed.
 int bn_bwd_finalize(double* acc, int C, int64_t count, const float* gamma, const float* mean,
                     const float* invstd, float gscale, float* dgamma, float* dbeta, float* coef, hipStream_t st);
 // dx1 = A1*dz + B1*x1 + C1 [; dx2 = A2*dz + B2*x2 + C2]
 int bn_bwd_apply(const u16* dz, const u16* x1, const float* coef1, u16* dx1, const u16* x2, const float* coef2,
                  u16* dx2, int64_t M, int C, hipStream_t st);
+int bn_bwd_apply(const float* dz, const float* x1, const float* coef1, float* dx1, const float* x2, const float* coef2,
+                 float* dx2, int64_t M, int C, hipStream_t st);
 
 // ------------------------------------------------------------------ stem / head / loss
 // x fp32 NCHW [N][3][H][W] -> im2col bf16 [N*H*W][64] (3x3 pad 1 taps, (r,s,c) order, zero padded)
@@ -168,6 +194,11 @@ int xent_bwd(const float* logits, const int64_t* labels, const float* lse, const
              float* dlogits, hipStream_t st);
 // dW = scale*dlogits^T feat ; db = scale*sum dlogits ; dact[n][hw][c] = (dlogits . W)[c] / HW
 size_t head_bwd_workspace(int N, int C, int ncls);
+// fp32 mode: fp32 activations and fp32 Linear weights, no autocast rounding
+int head_fwd(const float* act, int N, int HW, int C, const float* wfc, const float* bfc, int ncls, float* feat,
+             float* logits, hipStream_t st);
+int head_bwd(const float* dlogits, const float* feat, const float* wfc, int N, int HW, int C, int ncls, float scale,
+             float* dw, float* db, float* dact, float* ws, size_t ws_bytes, hipStream_t st);
 int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int HW, int C, int ncls, float scale,
              float* dw, float* db, u16* dact, float* ws, size_t ws_bytes, hipStream_t st);
 

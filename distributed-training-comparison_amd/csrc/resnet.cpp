@@ -61,6 +61,10 @@ struct BlockL {
 
 struct Net {
   int B = 0, H = 0, W = 0, ncls = 100;
+  // fp32 mode (dtc_rn18_set_precision): fp32 activations, f32-MFMA convs, fp32 BN / head -- the
+  // reference without --amp (ddp/trainer.py:160-165). Default: bf16 activations (autocast).
+  bool f32 = false;
+  size_t esz() const { return f32 ? 4 : 2; }
   std::vector<ParamEntry> params;
   int64_t flat_numel = 0;
   int64_t bufs_numel = 0;
@@ -246,6 +250,9 @@ static int build(Net& n) {
   return 0;
 }
 
+// fp32 stem: a 1x1 "conv" over the 32-column fp32 im2col image (27 taps + 5 zero columns)
+static ConvShape f32_stem_shape(const Net& n) { return ConvShape{n.B, n.H, n.W, 32, 64, 1, 1, 1, 0}; }
+
 static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.acts.clear();
   n.caps.clear();
@@ -260,14 +267,15 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   };
   const int64_t B = n.B;
   const int64_t M0 = B * n.H * n.W;
-  n.X0 = take(M0 * 64 * 2);
+  const size_t E = n.esz();
+  n.X0 = take(M0 * 64 * 2);  // im2col: [M0][64] bf16 or [M0][32] fp32
   n.WSTEM = take(64 * 64 * 2);
-  n.C0 = take(M0 * 64 * 2);
-  n.A0 = take(M0 * 64 * 2);
+  n.C0 = take(M0 * 64 * E);
+  n.A0 = take(M0 * 64 * E);
   int64_t gmax = M0 * 64;
   for (auto& b : n.blocks) {
     const int64_t M = B * b.Hout * b.Wout;
-    const size_t bytes = M * b.Cout * 2;
+    const size_t bytes = M * b.Cout * E;
     b.C1 = take(bytes);
     b.A1 = take(bytes);
     b.C2 = take(bytes);
@@ -293,14 +301,14 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.HEADWS_bytes = head_bwd_workspace((int)B, 512, n.ncls);
   n.HEADWS = take(n.HEADWS_bytes);
   n.acts.push_back({"head.feat_f32", n.FEAT, (int)B, 1, 1, 512});
-  for (int i = 0; i < 6; ++i) n.G[i] = take(gmax * 2);
+  for (int i = 0; i < 6; ++i) n.G[i] = take(gmax * E);
   for (auto& b : n.blocks) {  // per-block, so a pending side-stream wgrad never sees them overwritten
-    const size_t bytes = (size_t)B * b.Hout * b.Wout * b.Cout * 2;
+    const size_t bytes = (size_t)B * b.Hout * b.Wout * b.Cout * E;
     b.DC2 = take(bytes);
     b.DC1 = take(bytes);
     if (b.proj) b.DSC = take(bytes);
   }
-  n.DC0 = take(M0 * 64 * 2);
+  n.DC0 = take(M0 * 64 * E);
   // BN per-layer state
   n.stats_lo = off;  // forward statistics of every BN, then backward sums: each zeroed by one memset node
   for (BNL* b : n.bns) b->stats = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
@@ -317,9 +325,10 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   // split-K slabs: max over every conv pass
   size_t slab = (size_t)64 * 64 * 4;
   auto consider = [&](const ConvShape& s) {
-    for (int m = 0; m < 3; ++m) slab = std::max(slab, plan_conv(s, m).slab_bytes);
+    for (int m = 0; m < 3; ++m)
+      slab = std::max(slab, n.f32 ? f32_conv_workspace(s, m) : plan_conv(s, m).slab_bytes);
   };
-  consider(n.stem.s);
+  consider(n.f32 ? f32_stem_shape(n) : n.stem.s);
   for (auto& b : n.blocks) {
     consider(b.c1.s);
     consider(b.c2.s);
@@ -330,7 +339,7 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.SLABW = take(slab);
   if (n.capture) {
     auto cap = [&](const std::string& nm, int h, int w, int c) {
-      n.caps.push_back({nm, take((size_t)B * h * w * c * 2), (int)B, h, w, c});
+      n.caps.push_back({nm, take((size_t)B * h * w * c * E), (int)B, h, w, c});
     };
     for (size_t i = 0; i < n.blocks.size(); ++i) {
       const BlockL& b = n.blocks[i];
@@ -487,8 +496,12 @@ static int bn_act(Net& n, int mode, BNL& b, const u16* x, BNL* b2, const u16* x2
   return bn_apply_dual_relu(x, s1, h1, x2, n.at<float>(b2->scale), n.at<float>(b2->shift), y, M, b.C, st);
 }
 
+static ConvShape f32_stem_shape(const Net& n);
+static int forward_body_f32(Net& n, float* logits, bool train, hipStream_t st);
+
 // everything after the input im2col (reads only executor-owned memory: capturable)
 static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
+  if (n.f32) return forward_body_f32(n, logits, train, st);
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
   u16* X0 = n.at<u16>(n.X0);
   n.prof_next = train ? 0 : Net::PROF_SLOTS;  // eval passes are not timed
@@ -524,8 +537,177 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
                   logits, st);
 }
 
+// ------------------------------------------------------------------ fp32 mode (no autocast)
+// Same structure as forward_body / backward_body with fp32 activations: f32-MFMA convs
+// (conv_f32.hip, BN statistics in the forward epilogue), the fused BN apply kernels on fp32
+// tensors (no autocast rounding points), a separate masked BN-backward reduction after each dgrad,
+// fp32 head with the fp32 master Linear weights.
+static int bn_act_f32(Net& n, int mode, BNL& b, const float* x, BNL* b2, const float* x2, float* y, int64_t M,
+                      bool train, hipStream_t st) {
+  if (train && n.sync) {
+    DTC_TRY(sync_bn_sums(n, b.stats, b.C, st));
+    if (b2) DTC_TRY(sync_bn_sums(n, b2->stats, b2->C, st));
+  }
+  const int64_t cnt = train && n.sync ? M * n.sync_world : M;
+  if (train) {
+    const BnFwdArgs a1 = fwd_args(n, b, cnt);
+    const BnFwdArgs a2 = b2 ? fwd_args(n, *b2, cnt) : BnFwdArgs{};
+    return bn_fin_apply(mode, x, a1, x2, b2 ? &a2 : nullptr, y, M, b.C, st);
+  }
+  DTC_TRY(bn_finalize_fwd(n, b, cnt, false, st));
+  if (b2) DTC_TRY(bn_finalize_fwd(n, *b2, cnt, false, st));
+  const float* s1 = n.at<float>(b.scale);
+  const float* h1 = n.at<float>(b.shift);
+  if (mode == 1) return bn_apply_relu(x, s1, h1, y, M, b.C, st);
+  if (mode == 2) return bn_apply_add_relu(x, s1, h1, x2, y, M, b.C, st);
+  return bn_apply_dual_relu(x, s1, h1, x2, n.at<float>(b2->scale), n.at<float>(b2->shift), y, M, b.C, st);
+}
+
+static int forward_body_f32(Net& n, float* logits, bool train, hipStream_t st) {
+  const int64_t M0 = (int64_t)n.B * n.H * n.W;
+  float* slab = n.at<float>(n.SLAB);
+  n.prof_next = train ? 0 : Net::PROF_SLOTS;
+  DTC_TRY(f32_stem_pack_weight(n.pf(n.stem.pidx), n.at<float>(n.WSTEM), 64, st));
+  if (train) DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.acc_lo - n.stats_lo, st));
+  PROF(0, 2.0 * M0 * 64 * 27,
+       conv_f32(f32_stem_shape(n), CONV_FWD, n.at<float>(n.X0), n.at<float>(n.WSTEM), n.at<float>(n.C0), nullptr,
+                train ? n.at<double>(n.bn0.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
+  DTC_TRY(bn_act_f32(n, 1, n.bn0, n.at<float>(n.C0), nullptr, nullptr, n.at<float>(n.A0), M0, train, st));
+  const float* in = n.at<float>(n.A0);
+  for (auto& b : n.blocks) {
+    const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
+    PROF(0, conv_flops(b.c1.s),
+         conv_f32(b.c1.s, CONV_FWD, in, n.pf(b.c1.pidx), n.at<float>(b.C1), nullptr,
+                  train ? n.at<double>(b.b1.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
+    DTC_TRY(bn_act_f32(n, 1, b.b1, n.at<float>(b.C1), nullptr, nullptr, n.at<float>(b.A1), M, train, st));
+    PROF(0, conv_flops(b.c2.s),
+         conv_f32(b.c2.s, CONV_FWD, n.at<float>(b.A1), n.pf(b.c2.pidx), n.at<float>(b.C2), nullptr,
+                  train ? n.at<double>(b.b2.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
+    if (b.proj) {
+      PROF(0, conv_flops(b.sc.s),
+           conv_f32(b.sc.s, CONV_FWD, in, n.pf(b.sc.pidx), n.at<float>(b.S), nullptr,
+                    train ? n.at<double>(b.bsc.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
+      DTC_TRY(bn_act_f32(n, 3, b.b2, n.at<float>(b.C2), &b.bsc, n.at<float>(b.S), n.at<float>(b.OUT), M, train, st));
+    } else {
+      DTC_TRY(bn_act_f32(n, 2, b.b2, n.at<float>(b.C2), nullptr, in, n.at<float>(b.OUT), M, train, st));
+    }
+    in = n.at<float>(b.OUT);
+  }
+  const BlockL& last = n.blocks.back();
+  return head_fwd(in, n.B, last.Hout * last.Wout, 512, n.pf(n.fc_w), n.pf(n.fc_b), n.ncls, n.at<float>(n.FEAT),
+                  logits, st);
+}
+
+struct BwdCtx;
+static int maybe_bucket(Net& n, int after_block, const BwdCtx& cx, hipStream_t st);
+static int cap(Net& n, const std::string& name, const void* src, hipStream_t st);
+static BnBwdArgs bwd_args(Net& n, BNL& b, int64_t count, float gs);
+
+static int backward_body_f32(Net& n, const float* dlogits, float gs, const BwdCtx& cx, hipStream_t st) {
+  n.prof_next = Net::PROF_BWD0;
+  n.ev_next = 0;
+  float* G[6];
+  for (int i = 0; i < 6; ++i) G[i] = n.at<float>(n.G[i]);
+  float* slab = n.at<float>(n.SLAB);
+  const BlockL& last = n.blocks.back();
+  DTC_HIP(hipMemsetAsync(n.ws + n.acc_lo, 0, n.stats_hi - n.acc_lo, st));
+  DTC_TRY(head_bwd(dlogits, n.at<float>(n.FEAT), n.pf(n.fc_w), n.B, last.Hout * last.Wout, 512, n.ncls, gs,
+                   n.gf(n.fc_w), n.gf(n.fc_b), G[0], n.at<float>(n.HEADWS), n.HEADWS_bytes, st));
+  for (int bi = (int)n.blocks.size() - 1; bi >= 0; --bi) {
+    BlockL& b = n.blocks[bi];
+    const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
+    const float* in = bi > 0 ? n.at<float>(n.blocks[bi - 1].OUT) : n.at<float>(n.A0);
+    float* dc2 = n.at<float>(b.DC2);
+    float* dc1 = n.at<float>(b.DC1);
+    float* dsc = b.proj ? n.at<float>(b.DSC) : nullptr;
+    const std::string cp = n.capture ? "grad.layer" + std::to_string(bi / 2 + 1) + "." + std::to_string(bi % 2) : "";
+    DTC_TRY(cap(n, cp + ".dy", G[0], st));
+    // out = relu(bn2(c2) + shortcut): dz = dy * [out > 0] and the BN-backward sums of bn2 (+ bn_sc)
+    DTC_TRY(bn_bwd_reduce(G[0], n.at<float>(b.OUT), n.at<float>(b.C2), n.at<float>(b.b2.mean),
+                          n.at<float>(b.b2.invstd), n.at<double>(b.b2.acc), b.proj ? n.at<float>(b.S) : nullptr,
+                          b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
+                          b.proj ? n.at<double>(b.bsc.acc) : nullptr, G[1], M, b.Cout, st));
+    float* dz2 = G[1];
+    {
+      if (n.sync) {
+        DTC_TRY(sync_bn_sums(n, b.b2.acc, b.b2.C, st));
+        if (b.proj) DTC_TRY(sync_bn_sums(n, b.bsc.acc, b.bsc.C, st));
+      }
+      const float g2 = n.sync ? gs / (float)n.sync_world : gs;
+      const int64_t cnt = n.sync ? M * n.sync_world : M;
+      const BnBwdArgs a1 = bwd_args(n, b.b2, cnt, g2);
+      const BnBwdArgs a2 = b.proj ? bwd_args(n, b.bsc, cnt, g2) : BnBwdArgs{};
+      DTC_TRY(bn_bwd_fin_apply(dz2, n.at<float>(b.C2), a1, dc2, b.proj ? n.at<float>(b.S) : nullptr,
+                               b.proj ? &a2 : nullptr, dsc, M, b.Cout, st));
+    }
+    DTC_TRY(cap(n, cp + ".dz", dz2, st));
+    DTC_TRY(cap(n, cp + ".dc2", dc2, st));
+    if (b.proj) DTC_TRY(cap(n, cp + ".ds", dsc, st));
+    PROF(2, conv_flops(b.c2.s),
+         conv_f32(b.c2.s, CONV_WGRAD, n.at<float>(b.A1), dc2, nullptr, nullptr, nullptr, n.gf(b.c2.pidx), 0, 0, gs,
+                  slab, n.slab_bytes, st, ts));
+    PROF(1, conv_flops(b.c2.s),
+         conv_f32(b.c2.s, CONV_DGRAD, dc2, n.pf(b.c2.pidx), G[4], nullptr, nullptr, nullptr, 0, 0, 0.f, slab,
+                  n.slab_bytes, st, ts));
+    DTC_TRY(cap(n, cp + ".da1", G[4], st));
+    // a1 = relu(bn1(c1)): dz1 = da1 * [a1 > 0] (in place) and bn1's sums
+    DTC_TRY(bn_bwd_reduce(G[4], n.at<float>(b.A1), n.at<float>(b.C1), n.at<float>(b.b1.mean),
+                          n.at<float>(b.b1.invstd), n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, G[4],
+                          M, b.Cout, st));
+    DTC_TRY(cap(n, cp + ".dz1", G[4], st));
+    {
+      if (n.sync) DTC_TRY(sync_bn_sums(n, b.b1.acc, b.b1.C, st));
+      const float g1 = n.sync ? gs / (float)n.sync_world : gs;
+      const BnBwdArgs a1 = bwd_args(n, b.b1, n.sync ? M * n.sync_world : M, g1);
+      DTC_TRY(bn_bwd_fin_apply(G[4], n.at<float>(b.C1), a1, dc1, (const float*)nullptr, nullptr, nullptr, M, b.Cout,
+                               st));
+    }
+    DTC_TRY(cap(n, cp + ".dc1", dc1, st));
+    PROF(2, conv_flops(b.c1.s),
+         conv_f32(b.c1.s, CONV_WGRAD, in, dc1, nullptr, nullptr, nullptr, n.gf(b.c1.pidx), 0, 0, gs, slab,
+                  n.slab_bytes, st, ts));
+    if (b.proj) {
+      PROF(2, conv_flops(b.sc.s),
+           conv_f32(b.sc.s, CONV_WGRAD, in, dsc, nullptr, nullptr, nullptr, n.gf(b.sc.pidx), 0, 0, gs, slab,
+                    n.slab_bytes, st, ts));
+      PROF(1, conv_flops(b.sc.s),
+           conv_f32(b.sc.s, CONV_DGRAD, dsc, n.pf(b.sc.pidx), G[5], nullptr, nullptr, nullptr, 0, 0, 0.f, slab,
+                    n.slab_bytes, st, ts));
+      DTC_TRY(cap(n, cp + ".dxs", G[5], st));
+      PROF(1, conv_flops(b.c1.s),
+           conv_f32(b.c1.s, CONV_DGRAD, dc1, n.pf(b.c1.pidx), G[0], G[5], nullptr, nullptr, 0, 0, 0.f, slab,
+                    n.slab_bytes, st, ts));
+    } else {  // dx = dgrad + dz2 (the identity shortcut's gradient)
+      PROF(1, conv_flops(b.c1.s),
+           conv_f32(b.c1.s, CONV_DGRAD, dc1, n.pf(b.c1.pidx), G[0], dz2, nullptr, nullptr, 0, 0, 0.f, slab,
+                    n.slab_bytes, st, ts));
+    }
+    DTC_TRY(cap(n, cp + ".dx", G[0], st));
+    DTC_TRY(maybe_bucket(n, bi, cx, st));
+  }
+  const int64_t M0 = (int64_t)n.B * n.H * n.W;
+  float* dc0 = n.at<float>(n.DC0);
+  DTC_TRY(bn_bwd_reduce(G[0], n.at<float>(n.A0), n.at<float>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
+                        n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, G[1], M0, 64, st));
+  {
+    if (n.sync) DTC_TRY(sync_bn_sums(n, n.bn0.acc, n.bn0.C, st));
+    const float g0 = n.sync ? gs / (float)n.sync_world : gs;
+    const BnBwdArgs a0 = bwd_args(n, n.bn0, n.sync ? M0 * n.sync_world : M0, g0);
+    DTC_TRY(bn_bwd_fin_apply(G[1], n.at<float>(n.C0), a0, dc0, (const float*)nullptr, nullptr, nullptr, M0, 64, st));
+  }
+  DTC_TRY(cap(n, "grad.stem.dz", G[1], st));
+  DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
+  PROF(2, 2.0 * M0 * 64 * 27,
+       conv_f32(f32_stem_shape(n), CONV_WGRAD, n.at<float>(n.X0), dc0, nullptr, nullptr, nullptr, n.gf(n.stem.pidx),
+                27, 27, gs, slab, n.slab_bytes, st, ts));
+  DTC_TRY(maybe_bucket(n, -1, cx, st));
+  if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
+  return 0;
+}
+
 static int forward(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
-  DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
+  if (n.f32) DTC_TRY(f32_stem_im2col(x, n.at<float>(n.X0), n.B, n.H, n.W, st));
+  else DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
   if (!graphs_on(n)) return forward_body(n, logits, train, st);
   hipGraphExec_t& ex = n.fwd_exec[train ? 1 : 0];
   if (!ex) {
@@ -569,7 +751,7 @@ static int cap(Net& n, const std::string& name, const void* src, hipStream_t st)
   if (!n.capture) return 0;
   for (const auto& a : n.caps)
     if (a.name == name) {
-      DTC_HIP(hipMemcpyAsync(n.ws + a.off, src, (size_t)a.n * a.h * a.w * a.c * 2, hipMemcpyDeviceToDevice, st));
+      DTC_HIP(hipMemcpyAsync(n.ws + a.off, src, (size_t)a.n * a.h * a.w * a.c * n.esz(), hipMemcpyDeviceToDevice, st));
       return 0;
     }
   return set_error(DTC_EINVAL, "capture slot %s missing", name.c_str());
@@ -666,6 +848,7 @@ static BnbArgs bnb_of(Net& n, size_t y, size_t x1, BNL& b1, size_t x2 = 0, BNL* 
 }
 
 static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& cx, hipStream_t st) {
+  if (n.f32) return backward_body_f32(n, dlogits, gs, cx, st);
   n.prof_next = Net::PROF_BWD0;
   n.ev_next = 0;
   u16* G[6];
@@ -931,6 +1114,15 @@ int dtc_rn18_enable_capture(dtc_net* net) {
   plan_workspace(net->n, net->bucket_cap_mb);
   return 0;
 }
+
+int dtc_rn18_set_precision(dtc_net* net, int fp32) {
+  DTC_CHECK_ARG(net && net->n.ws == nullptr, "dtc_rn18_set_precision: call before dtc_rn18_bind");
+  net->n.f32 = fp32 != 0;
+  plan_workspace(net->n, net->bucket_cap_mb);
+  return 0;
+}
+
+int dtc_rn18_precision(const dtc_net* net) { return net ? (net->n.f32 ? 1 : 0) : DTC_EINVAL; }
 
 int dtc_rn18_num_captures(const dtc_net* net) { return net ? (int)net->n.caps.size() : DTC_EINVAL; }
 

@@ -16,6 +16,7 @@ Mirror of the reference's operator boundary (src/ddp/net.py, trainer.py:40):
 from __future__ import annotations
 
 import ctypes as C
+import threading
 import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
@@ -25,6 +26,25 @@ import torch.nn as nn
 
 from . import ops
 from ._native import NativeError, call, lib, ptr, require_cuda, stream_ptr
+
+
+# ----------------------------------------------------------------------------- autocast state
+# torch semantics: inside `autocast()` (trainer.py:153, the --amp path) the network computes in reduced
+# precision (bf16 here, fp16 in the reference), outside it in fp32 (trainer.py:160-165 without --amp).
+# amp.autocast flips this thread-local flag; ResNet.forward picks the executor precision from it
+# unless the module's `precision` attribute forces one ("bf16" / "fp32").
+_AUTOCAST = threading.local()
+
+
+def is_autocast_enabled() -> bool:
+    return bool(getattr(_AUTOCAST, "enabled", False))
+
+
+def set_autocast_enabled(enabled: bool) -> None:
+    _AUTOCAST.enabled = bool(enabled)
+
+
+PRECISIONS = ("bf16", "fp32")
 
 
 # ----------------------------------------------------------------------------- layout
@@ -100,9 +120,14 @@ class Executor:
     """One native executor (plan + workspace) for a fixed (batch, height, width)."""
 
     def __init__(self, flat: FlatState, batch: int, height: int, width: int, num_classes: int, bucket_cap_mb: float,
-                 capture: bool = False):
+                 capture: bool = False, precision: str = "bf16"):
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {PRECISIONS}, not {precision!r}")
         self.handle = C.c_void_p()
         call("dtc_rn18_create", C.byref(self.handle), batch, height, width, num_classes, float(bucket_cap_mb))
+        self.precision = precision
+        if precision == "fp32":
+            call("dtc_rn18_set_precision", self.handle, 1)
         if capture:
             call("dtc_rn18_enable_capture", self.handle)
         nbytes = lib.dtc_rn18_workspace_bytes(self.handle)
@@ -151,7 +176,7 @@ class Executor:
             shp = (C.c_int * 4)()
             call(info, self.handle, i, C.byref(name), C.byref(off), shp)
             nm = name.value.decode()
-            dt = torch.float32 if nm.endswith("_f32") else torch.bfloat16
+            dt = torch.float32 if (nm.endswith("_f32") or self.precision == "fp32") else torch.bfloat16
             numel = shp[0] * shp[1] * shp[2] * shp[3]
             nbytes = numel * (4 if dt == torch.float32 else 2)
             o = base + off.value
@@ -333,6 +358,8 @@ class ResNet(nn.Module):
         self._capture = False
         self._sync_bn = False  # SyncBatchNorm.convert_sync_batchnorm marks the module
         self._sync_comm = None  # communicator the executors all-reduce BN sums over
+        # None: follow autocast (bf16 inside, fp32 outside, as torch); "bf16" / "fp32": force
+        self.precision: Optional[str] = None
 
     def _make_layer(self, block, planes, num_blocks, stride):
         strides = [stride] + [1] * (num_blocks - 1)
@@ -425,12 +452,22 @@ class ResNet(nn.Module):
         self._bucket_cap_mb = float(mb)
         self._executors.clear()
 
-    def executor(self, batch: int, height: int, width: int) -> Executor:
-        key = (batch, height, width)
+    def compute_precision(self) -> str:
+        """The precision the next forward runs in: `self.precision` when set ("bf16" / "fp32"),
+        else torch's rule -- bf16 inside `autocast()`, fp32 outside (trainer.py:152-165)."""
+        if self.precision is not None:
+            if self.precision not in PRECISIONS:
+                raise ValueError(f"precision must be None or one of {PRECISIONS}, not {self.precision!r}")
+            return self.precision
+        return "bf16" if is_autocast_enabled() else "fp32"
+
+    def executor(self, batch: int, height: int, width: int, precision: Optional[str] = None) -> Executor:
+        precision = precision or self.compute_precision()
+        key = (batch, height, width, precision)
         exe = self._executors.get(key)
         if exe is None:
             exe = Executor(self.flat, batch, height, width, self.num_classes, self._bucket_cap_mb,
-                           capture=self._capture)
+                           capture=self._capture, precision=precision)
             if self._sync_comm is not None:
                 call("dtc_rn18_set_sync_bn", exe.handle, self._sync_comm.handle)
             self._executors[key] = exe

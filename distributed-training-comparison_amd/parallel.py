@@ -255,14 +255,15 @@ class _Replica:
             self.flat = FlatState(model.flat.layout, device)
         self._executors = {}
 
-    def executor(self, batch: int, height: int, width: int):
+    def executor(self, batch: int, height: int, width: int, precision: str):
         from .nn import Executor
 
-        key = (batch, height, width)
+        key = (batch, height, width, precision)
         exe = self._executors.get(key)
         if exe is None:
             with torch.cuda.device(self.device):
-                exe = Executor(self.flat, batch, height, width, self.model.num_classes, self.model._bucket_cap_mb)
+                exe = Executor(self.flat, batch, height, width, self.model.num_classes, self.model._bucket_cap_mb,
+                               precision=precision)
             self._executors[key] = exe
         return exe
 
@@ -286,16 +287,17 @@ class _DPFn(torch.autograd.Function):
         model = dp.module
         chunks = x.chunk(len(dp.device_ids))  # torch.nn.parallel.scatter's split of dim 0
         train = model.training
+        prec = model.compute_precision()  # autocast is thread-local: decided once, here
         runs = []
         for i, c in enumerate(chunks):
             dev = dp.devices[i]
             with torch.cuda.device(dev):
                 if i == 0:
-                    exe = model.executor(c.shape[0], c.shape[2], c.shape[3])
+                    exe = model.executor(c.shape[0], c.shape[2], c.shape[3], prec)
                 else:
                     rep = dp._replica(i)
                     rep.pull(model.flat)
-                    exe = rep.executor(c.shape[0], c.shape[2], c.shape[3])
+                    exe = rep.executor(c.shape[0], c.shape[2], c.shape[3], prec)
                 xi = c.to(dev, non_blocking=True).contiguous()
                 logits = torch.empty(c.shape[0], model.num_classes, dtype=torch.float32, device=dev)
                 gen = exe.forward(xi, logits, train)

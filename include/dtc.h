@@ -193,6 +193,13 @@ int64_t dtc_rn18_bufs_numel(const dtc_net* net);
 size_t dtc_rn18_workspace_bytes(const dtc_net* net);
 int dtc_rn18_num_buckets(const dtc_net* net);
 int dtc_rn18_bucket_info(const dtc_net* net, int idx, int64_t* offset, int64_t* numel);
+/* Precision of the executor (call before dtc_rn18_bind; re-plans the workspace): 0 = bf16 activations
+ * with fp32 accumulation and master weights (the reference under --amp, autocast, trainer.py:152-159),
+ * 1 = fp32 throughout (the reference without --amp, ddp/trainer.py:160-165): fp32 activations in the
+ * workspace, f32-input MFMA convolutions, BN / pool / Linear on fp32 tensors with the fp32 master
+ * weights (no bf16 shadow), no autocast rounding points. */
+int dtc_rn18_set_precision(dtc_net* net, int fp32);
+int dtc_rn18_precision(const dtc_net* net);
 /* Attach caller-owned device memory. Zeroes the workspace statistics areas (enqueued on stream). */
 int dtc_rn18_bind(dtc_net* net, void* workspace, float* params, float* grads, uint16_t* params_bf16, float* bufs,
                   int64_t* num_batches_tracked, void* stream);

@@ -1,0 +1,119 @@
+"""fp32 mode: the reference WITHOUT --amp (ddp/trainer.py:160-165, single/trainer.py:144-145) trains
+plain fp32; north_star holds per-layer activations and gradients to 1e-5 relative there. The native
+executor runs that path (outside `autocast`) on f32-input MFMA convolutions (conv_f32.hip) and fp32
+BN / head kernels; every check here is against the fp32 oracle (float64 arithmetic on the
+executor's own fp32 inputs)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import resnet as R
+from tests.conftest import rel_err
+from tests.test_gpu_resnet import _np, _setup, _split_state, _teacher_forced
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("batch", [2, 8])
+def test_fp32_per_layer_teacher_forced(dtc, cuda, batch):
+    """Every layer's forward output and backward intermediate, and every parameter gradient, of
+    the fp32 executor within 1e-5 of the oracle on that layer's inputs (129 checks)."""
+    errs = _teacher_forced(dtc, cuda, batch, precision="fp32")
+    assert len(errs) > 90
+
+
+def test_fp32_per_layer_teacher_forced_b64_224(dtc, cuda):
+    """fp32 at a split-K-heavy shape (batch 64: wgrad splits, many tiles) on layers 3-4 + head, and at
+    224x224 batch 1 on every layer (large images: multi-tile rows, int64 offsets)."""
+    _teacher_forced(dtc, cuda, 64, stages=(0, 3, 4), imgs=np.arange(0, 64, 7), seed=31, precision="fp32")
+    _teacher_forced(dtc, cuda, 1, hw=224, seed=32, precision="fp32")
+
+
+def test_fp32_end_to_end_matches_oracle(dtc, cuda):
+    """Free-running fp32 forward + backward vs the fp32 oracle (no rounding points anywhere): unlike
+    bf16, fp32 stays close end to end -- logits and loss to 1e-5, every activation to 1e-4, every
+    parameter gradient to 1e-3 (measured drift is fp32 summation order only), running statistics
+    to 1e-5."""
+    model, sd, x, y = _setup(dtc, cuda, 8, seed=4)
+    model.precision = "fp32"
+    crit = dtc.CrossEntropyLoss()
+    logits = model(torch.from_numpy(x).to(cuda))
+    loss = crit(logits, torch.from_numpy(y).to(cuda))
+    loss.backward()
+    torch.cuda.synchronize()
+    params, bufs = _split_state(sd)
+    ref = R.forward_backward(params, bufs, x, y, bf16_mode=False, train=True, want_acts=True)
+    assert rel_err(_np(logits), ref["logits"]) < 1e-5
+    assert abs(float(loss) - ref["loss"]) < 1e-5 * max(1.0, abs(ref["loss"]))
+    acts = model.executor(8, 32, 32, "fp32").activations()
+    for k, v in ref["acts"].items():
+        assert rel_err(_np(acts[k]).reshape(v.shape), v) < 1e-4, k
+    for k, p in model.named_parameters():
+        assert rel_err(_np(p.grad), ref["grads"][k]) < 1e-3, k
+    sd2 = model.state_dict()
+    for k, v in ref["buffers"].items():
+        assert rel_err(sd2[k].cpu().numpy(), v) < 1e-5, k
+
+
+def test_autocast_selects_executor_precision(dtc, cuda):
+    """torch semantics at the boundary: inside dtc.autocast() the bf16 executor, outside it fp32
+    (what the reference's trainer does with and without --amp); `precision` forces one."""
+    torch.manual_seed(42)
+    model = dtc.ResNet18().to(cuda)
+    x = torch.randn(4, 3, 32, 32, device=cuda)
+    with torch.no_grad():
+        lo32 = model(x)
+        with dtc.autocast():
+            lo16 = model(x)
+            with dtc.autocast(enabled=False):
+                lo32b = model(x)
+    keys = sorted(model._executors)
+    assert [k[3] for k in keys] == ["bf16", "fp32"]
+    assert torch.equal(lo32, lo32b)
+    assert 1e-6 < rel_err(_np(lo16), _np(lo32)) < 3e-2  # same network, bf16 rounding only
+    model.precision = "bf16"
+    with torch.no_grad():
+        assert torch.equal(model(x), lo16)
+
+
+@pytest.mark.parametrize("graphs", [1, 0])
+def test_fp32_sgd_steps_graph_and_eager(dtc, cuda, graphs):
+    """Three fp32 training steps (forward, backward, fused SGD) with graph replay and eagerly: the
+    same numbers (graph replay changes nothing but launch overhead), finite decreasing-ish loss."""
+    dtc._native.lib.dtc_set_option(b"graphs", graphs)
+    try:
+        torch.manual_seed(42)
+        model = dtc.ResNet18().to(cuda)
+        crit = dtc.CrossEntropyLoss()
+        opt = dtc.SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4, nesterov=True)
+        g = torch.Generator().manual_seed(8)
+        x = torch.randn(16, 3, 32, 32, generator=g).to(cuda)
+        y = torch.randint(0, 100, (16,), generator=g).to(cuda)
+        losses = []
+        for _ in range(3):
+            opt.zero_grad()
+            loss = crit(model(x), y)
+            loss.backward()
+            opt.step()
+            losses.append(float(loss))
+        assert np.isfinite(losses).all() and losses[-1] < losses[0]
+        test_fp32_sgd_steps_graph_and_eager.results[graphs] = (losses, _np(model.flat.params))
+    finally:
+        dtc._native.lib.dtc_set_option(b"graphs", 1)
+    res = test_fp32_sgd_steps_graph_and_eager.results
+    if len(res) == 2:
+        np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-6)
+        assert rel_err(res[0][1], res[1][1]) < 1e-7
+
+
+test_fp32_sgd_steps_graph_and_eager.results = {}
+
+
+def test_trainer_without_amp_trains_fp32(dtc, cuda, tmp_path):
+    """`train.py single` without --amp (single/trainer.py:144-145): the loop runs the fp32 executor
+    (no GradScaler), like the reference."""
+    t = dtc.trainer.main(["--epoch", "1", "--batch-size", "32", "--max-steps", "3", "--workers", "0",
+                          "--synthetic-train", "320", "--synthetic-test", "64", "--eval-step", "1",
+                          "--ckpt-path", str(tmp_path)], "single")
+    precs = {k[3] for k in t.model._executors}
+    assert precs == {"fp32"}, precs

@@ -26,6 +26,16 @@ BF = 1e-2     # bf16-valued tensors, teacher-forced
 F32 = 1e-4    # fp32 gradients from identical bf16 operands
 
 
+@pytest.fixture(autouse=True)
+def _autocast_bf16(dtc):
+    """Every test here is about the AMP (bf16) executor: run it with autocast on, as the reference's
+    --amp loop does (trainer.py:153). The fp32 executor has its own tests (test_gpu_fp32.py)."""
+    prev = dtc.nn.is_autocast_enabled()
+    dtc.nn.set_autocast_enabled(True)
+    yield
+    dtc.nn.set_autocast_enabled(prev)
+
+
 def _setup(dtc, cuda, batch, seed=0, capture=False, hw=32):
     torch.manual_seed(42)
     model = dtc.ResNet18()
@@ -50,39 +60,50 @@ def _np(t):
     return t.detach().float().cpu().numpy()
 
 
-def _bn_fwd(x, g, b):
-    """Oracle BN (train) on an NHWC bf16-valued tensor -> bf16-rounded output, mean, invstd."""
+def _f32(a):
+    return np.asarray(a, np.float32)
+
+
+def _bn_fwd(x, g, b, rnd=O.bf16):
+    """Oracle BN (train) on an NHWC tensor -> output rounded like the executor's (bf16 under
+    autocast, fp32 otherwise), mean, invstd."""
     C = x.shape[-1]
     y, mean, invstd, _, _ = O.bn_train_fwd(x.reshape(-1, C), g, b)
-    return O.bf16(y.reshape(x.shape)), mean, invstd
+    return rnd(y.reshape(x.shape)), mean, invstd
 
 
-def _bn_bwd(dz, x, g):
+def _bn_bwd(dz, x, g, rnd=O.bf16):
     C = x.shape[-1]
     _, mean, invstd, _, _ = O.bn_train_fwd(x.reshape(-1, C), g, np.zeros(C))
     dx, dg, db = O.bn_train_bwd(dz.reshape(-1, C), x.reshape(-1, C), g, mean, invstd)
-    return O.bf16(dx.reshape(x.shape)), dg, db
+    return rnd(dx.reshape(x.shape)), dg, db
 
 
-def _teacher_forced(dtc, cuda, batch, hw=32, stages=(0, 1, 2, 3, 4), imgs=None, seed=0):
+def _teacher_forced(dtc, cuda, batch, hw=32, stages=(0, 1, 2, 3, 4), imgs=None, seed=0, precision="bf16"):
     """Run one capture-enabled training forward/backward of the executor at (batch, hw x hw) and
     check every layer of the listed stages (0 = stem + head, 1..4 = layer1..4) against the oracle
     evaluated on THAT layer's executor inputs. `imgs` (index array) restricts the per-image ops
     (conv forward / dgrad, the ReLU masks) to those images -- BN statistics and weight gradients,
     which reduce over the whole batch, are always checked at full size, so every batch-dependent
-    kernel plan (split-K factors, wgrad splits, persistent-tile walks) is the one under test."""
+    kernel plan (split-K factors, wgrad splits, persistent-tile walks) is the one under test.
+    precision "bf16": the AMP executor at the north_star's 1e-2 (bf16 outputs; fp32 weight gradients
+    from identical bf16 operands 1e-4); "fp32": the non-AMP executor at the north_star's 1e-5
+    everywhere, against the fp32 (unrounded) oracle."""
     model, sd, x, y = _setup(dtc, cuda, batch, seed=seed, capture=True, hw=hw)
+    model.precision = precision
+    bf = precision == "bf16"
+    rnd = O.bf16 if bf else _f32
     crit = dtc.CrossEntropyLoss()
     xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
     logits = model(xd)
     loss = crit(logits, yd)
     loss.backward()
     torch.cuda.synchronize()
-    exe = model.executor(batch, hw, hw)
+    exe = model.executor(batch, hw, hw, precision)
     A = {k: _np(v) for k, v in exe.activations().items()}
     G = {k: _np(v) for k, v in exe.activations(captures=True).items()}
     P = {k: v for k, v in _split_state(sd)[0].items()}
-    W = {k: O.bf16(O.kcrs_to_krsc(v)) for k, v in P.items() if v.ndim == 4}
+    W = {k: rnd(O.kcrs_to_krsc(v)) for k, v in P.items() if v.ndim == 4}
     grads = {k: _np(p.grad) for k, p in model.named_parameters()}
     del model, exe
     torch.cuda.empty_cache()
@@ -90,7 +111,7 @@ def _teacher_forced(dtc, cuda, batch, hw=32, stages=(0, 1, 2, 3, 4), imgs=None, 
     errs = {}
 
     def chk(name, got, ref, tol=BF):
-        errs[name] = (rel_err(got, ref), tol)
+        errs[name] = (rel_err(got, ref), tol if bf else 1e-5)  # fp32 mode: 1e-5 for everything
 
     def conv_f(inp, w, st, pad):
         return O.conv2d_fwd(inp[sel], w, st, pad)
@@ -99,10 +120,10 @@ def _teacher_forced(dtc, cuda, batch, hw=32, stages=(0, 1, 2, 3, 4), imgs=None, 
         return O.conv2d_dgrad(dy[sel], w, shape_hw, st, pad)
 
     # ---------------- forward, layer by layer
-    xb = O.bf16(O.nchw_to_nhwc(x))
+    xb = rnd(O.nchw_to_nhwc(x))
     if 0 in stages:
         chk("stem.conv", A["stem.conv"][sel], conv_f(xb, W["conv1.weight"], 1, 1))
-        a0, _, _ = _bn_fwd(A["stem.conv"], P["bn1.weight"], P["bn1.bias"])
+        a0, _, _ = _bn_fwd(A["stem.conv"], P["bn1.weight"], P["bn1.bias"], rnd)
         chk("stem.out", A["stem.out"], O.relu(a0))
     inp = A["stem.out"]
     blocks = []
@@ -114,19 +135,19 @@ def _teacher_forced(dtc, cuda, batch, hw=32, stages=(0, 1, 2, 3, 4), imgs=None, 
             blocks.append((L, pre, st, proj, inp))
             if L in stages:
                 chk(pre + ".conv1", A[pre + ".conv1"][sel], conv_f(inp, W[pre + ".conv1.weight"], st, 1))
-                z1, _, _ = _bn_fwd(A[pre + ".conv1"], P[pre + ".bn1.weight"], P[pre + ".bn1.bias"])
+                z1, _, _ = _bn_fwd(A[pre + ".conv1"], P[pre + ".bn1.weight"], P[pre + ".bn1.bias"], rnd)
                 chk(pre + ".relu1", A[pre + ".relu1"], O.relu(z1))
                 chk(pre + ".conv2", A[pre + ".conv2"][sel], conv_f(A[pre + ".relu1"], W[pre + ".conv2.weight"], 1, 1))
-                z2, _, _ = _bn_fwd(A[pre + ".conv2"], P[pre + ".bn2.weight"], P[pre + ".bn2.bias"])
+                z2, _, _ = _bn_fwd(A[pre + ".conv2"], P[pre + ".bn2.weight"], P[pre + ".bn2.bias"], rnd)
                 if proj:
                     chk(pre + ".shortcut", A[pre + ".shortcut"][sel], conv_f(inp, W[pre + ".shortcut.0.weight"], st, 0))
                     zs, _, _ = _bn_fwd(A[pre + ".shortcut"], P[pre + ".shortcut.1.weight"],
-                                       P[pre + ".shortcut.1.bias"])
+                                       P[pre + ".shortcut.1.bias"], rnd)
                     chk(pre + ".out", A[pre + ".out"], O.relu(z2 + zs))
                 else:
                     chk(pre + ".out", A[pre + ".out"], O.relu(z2 + inp))
             inp = A[pre + ".out"]
-    feat, lg = O.head_fwd(inp, P["linear.weight"], P["linear.bias"], bf16_mode=True)
+    feat, lg = O.head_fwd(inp, P["linear.weight"], P["linear.bias"], bf16_mode=bf)
     if 0 in stages:
         chk("head.feat", A["head.feat_f32"].reshape(feat.shape), feat, 1e-5)
         chk("logits", _np(logits), lg)
@@ -134,7 +155,7 @@ def _teacher_forced(dtc, cuda, batch, hw=32, stages=(0, 1, 2, 3, 4), imgs=None, 
     # ---------------- backward, layer by layer (inputs = the executor's own intermediates)
     _, dl, _ = O.cross_entropy(_np(logits), y)
     if 0 in stages:
-        dw, db, dact = O.head_bwd(dl, A["head.feat_f32"].reshape(feat.shape), O.bf16(P["linear.weight"]),
+        dw, db, dact = O.head_bwd(dl, A["head.feat_f32"].reshape(feat.shape), rnd(P["linear.weight"]),
                                   inp.shape[1:3])
         chk("linear.weight.grad", grads["linear.weight"], dw, F32)
         chk("linear.bias.grad", grads["linear.bias"], db, F32)
@@ -144,7 +165,7 @@ def _teacher_forced(dtc, cuda, batch, hw=32, stages=(0, 1, 2, 3, 4), imgs=None, 
             continue
         gp = "grad." + pre
         np.testing.assert_array_equal(G[gp + ".dz"][sel], np.where(A[pre + ".out"] > 0, G[gp + ".dy"], 0)[sel])
-        dc2, dg2, db2 = _bn_bwd(G[gp + ".dz"], A[pre + ".conv2"], P[pre + ".bn2.weight"])
+        dc2, dg2, db2 = _bn_bwd(G[gp + ".dz"], A[pre + ".conv2"], P[pre + ".bn2.weight"], rnd)
         chk(gp + ".dc2", G[gp + ".dc2"], dc2)
         chk(pre + ".bn2.weight.grad", grads[pre + ".bn2.weight"], dg2, 1e-3)
         chk(pre + ".bn2.bias.grad", grads[pre + ".bn2.bias"], db2, 1e-3)
@@ -153,14 +174,14 @@ def _teacher_forced(dtc, cuda, batch, hw=32, stages=(0, 1, 2, 3, 4), imgs=None, 
         chk(gp + ".da1", G[gp + ".da1"][sel], conv_d(G[gp + ".dc2"], W[pre + ".conv2.weight"],
                                                      A[pre + ".relu1"].shape[1:3], 1, 1))
         np.testing.assert_array_equal(G[gp + ".dz1"][sel], np.where(A[pre + ".relu1"] > 0, G[gp + ".da1"], 0)[sel])
-        dc1, dg1, db1 = _bn_bwd(G[gp + ".dz1"], A[pre + ".conv1"], P[pre + ".bn1.weight"])
+        dc1, dg1, db1 = _bn_bwd(G[gp + ".dz1"], A[pre + ".conv1"], P[pre + ".bn1.weight"], rnd)
         chk(gp + ".dc1", G[gp + ".dc1"], dc1)
         chk(pre + ".bn1.weight.grad", grads[pre + ".bn1.weight"], dg1, 1e-3)
         chk(pre + ".conv1.weight.grad", O.kcrs_to_krsc(grads[pre + ".conv1.weight"]),
             O.conv2d_wgrad(inp, G[gp + ".dc1"], 3, 3, st, 1), F32)
         dx = conv_d(G[gp + ".dc1"], W[pre + ".conv1.weight"], inp.shape[1:3], st, 1)
         if proj:
-            ds, dgs, dbs = _bn_bwd(G[gp + ".dz"], A[pre + ".shortcut"], P[pre + ".shortcut.1.weight"])
+            ds, dgs, dbs = _bn_bwd(G[gp + ".dz"], A[pre + ".shortcut"], P[pre + ".shortcut.1.weight"], rnd)
             chk(gp + ".ds", G[gp + ".ds"], ds)
             chk(pre + ".shortcut.1.weight.grad", grads[pre + ".shortcut.1.weight"], dgs, 1e-3)
             chk(pre + ".shortcut.0.weight.grad", O.kcrs_to_krsc(grads[pre + ".shortcut.0.weight"]),
@@ -172,14 +193,14 @@ def _teacher_forced(dtc, cuda, batch, hw=32, stages=(0, 1, 2, 3, 4), imgs=None, 
             chk(gp + ".dx", G[gp + ".dx"][sel], dx + G[gp + ".dz"][sel])
     if 0 in stages:
         np.testing.assert_array_equal(G["grad.stem.dz"], np.where(A["stem.out"] > 0, G["grad.layer1.0.dx"], 0))
-        dc0, dg0, db0 = _bn_bwd(G["grad.stem.dz"], A["stem.conv"], P["bn1.weight"])
+        dc0, dg0, db0 = _bn_bwd(G["grad.stem.dz"], A["stem.conv"], P["bn1.weight"], rnd)
         chk("grad.stem.dc", G["grad.stem.dc"], dc0)
         chk("bn1.weight.grad", grads["bn1.weight"], dg0, 1e-3)
         chk("conv1.weight.grad", O.kcrs_to_krsc(grads["conv1.weight"]),
             O.conv2d_wgrad(xb, G["grad.stem.dc"], 3, 3, 1, 1), F32)
     bad = {k: v for k, v in errs.items() if v[0] > v[1]}
     worst = max(errs.items(), key=lambda kv: kv[1][0] / kv[1][1])
-    print(f"teacher-forced B={batch} {hw}x{hw} stages={stages}: {len(errs)} checks, worst {worst[0]} "
+    print(f"teacher-forced {precision} B={batch} {hw}x{hw} stages={stages}: {len(errs)} checks, worst {worst[0]} "
           f"{worst[1][0]:.2e} (tol {worst[1][1]:.0e})")
     assert not bad, f"per-layer parity failures: {bad}"
     return errs
@@ -484,8 +505,25 @@ def test_loss_curve_200_steps(dtc, cuda):
     se = np.sqrt(mo.var(ddof=1) / n + mr.var(ddof=1) / n) / mr.mean()
     tol = max(1e-2, 3.0 * se)
     rel = (mo.mean() - mr.mean()) / mr.mean()
-    print(f"ensemble n={n}: ours {mo.mean():.4f} ref {mr.mean():.4f} rel {rel:+.4f} (se {se:.4f}, tol {tol:.4f})")
-    assert abs(rel) < tol
+    # per-step ensemble means: the 1% bound held step by step over the steps where the reference's own
+    # 1-ulp ensemble is still tight enough to resolve 1% (3 standard errors of the step's ensemble-mean
+    # difference < 1%); past that the trajectories have decorrelated and only the statistic above applies
+    O_ = np.stack(ours)
+    R_ = np.stack(ref_curves)
+    step_rel = (O_.mean(0) - R_.mean(0)) / R_.mean(0)
+    step_se = np.sqrt(O_.var(0, ddof=1) / n + R_.var(0, ddof=1) / n) / R_.mean(0)
+    resolvable = 3.0 * step_se < 1e-2
+    K = int(np.argmin(resolvable)) if not resolvable.all() else len(resolvable)
+    worst_k = float(np.abs(step_rel[:K]).max()) if K else 0.0
+    report = (f"loss-curve parity (n={n} ensembles x {O_.shape[1]} steps): 200-step mean ours {mo.mean():.4f} "
+              f"ref {mr.mean():.4f} rel {rel:+.4f} (se {se:.4f}; bound max(1%, 3se) = {tol:.4f}); per-step "
+              f"ensemble mean over the first {K} resolvable steps: max |rel| {worst_k:.4f} (bound 0.01)")
+    print(report)
+    import warnings
+
+    warnings.warn(report, UserWarning)  # lands in the pytest warnings summary of the GPU test log
+    assert K >= 5 and worst_k < 1e-2, report
+    assert abs(rel) < tol, report
 
 
 def test_native_loss_backward_matches_autograd(dtc, cuda):
@@ -744,7 +782,9 @@ def test_sync_batchnorm_two_identical_ranks_loopback(dtc, cuda):
         assert len(log) == 40 and not any(a for _, _, a in log)
         chans = sorted(n for _, n, _ in log)
         assert chans[0] == 2 * 64 and chans[-1] == 2 * 512
-        assert rel_err(l1, l0) < 1e-3 and rel_err(b1, b0) < 1e-5
+        # running_var's unbiased factor uses the GLOBAL count (2M/(2M-1) vs M/(M-1): up to 1e-4 on
+        # layer4 at M=512), as torch SyncBatchNorm does; running_mean is unaffected
+        assert rel_err(l1, l0) < 1e-3 and rel_err(b1, b0) < 2e-4
         assert rel_err(g1, g0) < 1e-3
         m1.set_sync_bn(None)
     finally:
