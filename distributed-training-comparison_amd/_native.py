@@ -74,6 +74,7 @@ _SIGS = {
     "dtc_xent_bwd": (i32, [vp, vp, vp, vp, i32, i32, vp, vp]),
     "dtc_sgd_nesterov_flat": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, vp, vp, vp]),
     "dtc_cast_f32_bf16": (i32, [vp, vp, i64, vp]),
+    "dtc_amp_scale": (i32, [vp, vp, vp, i64, vp]),
     "dtc_amp_check_finite": (i32, [vp, i64, vp, vp]),
     "dtc_amp_update_scale": (i32, [vp, vp, vp, vp, f32, f32, i32, vp]),
     "dtc_cifar_augment": (i32, [vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, C.POINTER(f32), C.POINTER(f32), vp, vp,
@@ -88,6 +89,12 @@ _SIGS = {
     "dtc_comm_log_size": (i32, [vp]),
     "dtc_comm_log_entry": (i32, [vp, i32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(i32)]),
     "dtc_comm_log_clear": (i32, [vp]),
+    "dtc_dp_create": (i32, [C.POINTER(vp), i32, C.POINTER(i32)]),
+    "dtc_dp_destroy": (i32, [vp]),
+    "dtc_dp_is_local": (i32, [vp]),
+    "dtc_dp_broadcast": (i32, [vp, C.POINTER(vp), sz, i32, C.POINTER(vp)]),
+    "dtc_dp_reduce_add": (i32, [vp, C.POINTER(vp), sz, C.POINTER(vp)]),
+    "dtc_copy_peer": (i32, [vp, i32, vp, i32, sz, vp]),
     "dtc_rn18_create": (i32, [C.POINTER(vp), i32, i32, i32, i32, f32]),
     "dtc_rn18_destroy": (i32, [vp]),
     "dtc_rn18_num_params": (i32, [vp]),

@@ -164,6 +164,9 @@ int dtc_sgd_nesterov_flat(float* p, const float* g, float* mom, uint16_t* pb, in
 int dtc_cast_f32_bf16(const float* src, uint16_t* dst, int64_t n, void* stream) {
   return cast_f32_bf16(src, dst, n, S(stream));
 }
+int dtc_amp_scale(const float* x, const float* scale, float* out, int64_t n, void* stream) {
+  return amp_scale(x, scale, out, n, S(stream));
+}
 int dtc_amp_check_finite(const float* g, int64_t n, int* found_inf, void* stream) {
   return amp_check_finite(g, n, found_inf, S(stream));
 }
@@ -205,6 +208,18 @@ int dtc_comm_log_entry(dtc_comm* comm, int idx, uint64_t* addr, uint64_t* count,
   if (count) *count = (*l)[idx].count;
   if (is_async) *is_async = (*l)[idx].async;
   return 0;
+}
+int dtc_dp_create(dtc_dp** out, int n, const int* devices) { GUARD(return dp_create((DPGroup**)out, n, devices);) }
+int dtc_dp_destroy(dtc_dp* g) { return dp_destroy((DPGroup*)g); }
+int dtc_dp_is_local(const dtc_dp* g) { return dp_local((const DPGroup*)g); }
+int dtc_dp_broadcast(dtc_dp* g, void* const* bufs, size_t count, int dtype, void* const* streams) {
+  GUARD(return dp_broadcast((DPGroup*)g, bufs, count, dtype, streams);)
+}
+int dtc_dp_reduce_add(dtc_dp* g, float* const* bufs, size_t count, void* const* streams) {
+  GUARD(return dp_reduce_add((DPGroup*)g, bufs, count, streams);)
+}
+int dtc_copy_peer(void* dst, int dst_device, const void* src, int src_device, size_t bytes, void* stream) {
+  return copy_peer(dst, dst_device, src, src_device, bytes, S(stream));
 }
 int dtc_comm_log_clear(dtc_comm* comm) {
   DTC_CHECK_ARG(comm != nullptr, "dtc_comm_log_clear: null comm");

@@ -163,3 +163,115 @@ int comm_join(Comm* c, hipStream_t compute) {
 int comm_world(const Comm* c) { return c ? c->world : 1; }
 
 }  // namespace dtc
+
+// ---------------------------------------------------------------- DataParallel group (config 4)
+// nn.DataParallel (reference src/dp/trainer.py:27) is ONE process driving every GPU: torch
+// replicates the module with broadcast_coalesced and sums the replicas' gradients with
+// reduce_add_coalesced (NCCL) every step. Here: one RCCL communicator per
+// device from ncclCommInitAll (single-process multi-rank), and the flat parameter / gradient
+// buffers move as ONE broadcast / ONE reduce each, grouped across devices. A group whose replicas
+// all share one device (the one-GPU test form, device_ids=[0, 0]) cannot hold one RCCL rank per
+// replica; it runs the same collectives as on-device copies and a fixed-order HIP reduce-add.
+namespace dtc {
+
+struct DPGroup {
+  int n = 0;
+  std::vector<int> devs;
+  bool local = false;  // every replica on one device
+  std::vector<ncclComm_t> comms;
+};
+
+static size_t dtype_bytes(int dtype) { return dtype == 1 ? 2 : (dtype == 2 || dtype == 3) ? 8 : 4; }
+
+struct DeviceGuard {
+  int prev = 0;
+  DeviceGuard() { (void)hipGetDevice(&prev); }
+  ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+int dp_create(DPGroup** out, int n, const int* devs) {
+  DTC_CHECK_ARG(out && devs && n >= 1 && n <= 64, "dp_create: bad args");
+  DPGroup* g = new DPGroup();
+  g->n = n;
+  g->devs.assign(devs, devs + n);
+  bool all_same = true, distinct = true;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      if (devs[i] != devs[j]) all_same = false;
+      if (i != j && devs[i] == devs[j]) distinct = false;
+    }
+  if (!all_same && !distinct) {
+    delete g;
+    return set_error(DTC_EINVAL, "dp_create: device ids must be all distinct or all equal");
+  }
+  g->local = all_same;
+  if (!g->local) {
+    DeviceGuard guard;
+    g->comms.resize(n);
+    ncclResult_t r = ncclCommInitAll(g->comms.data(), n, devs);
+    if (r != ncclSuccess) {
+      delete g;
+      return set_error(1000 + (int)r, "ncclCommInitAll failed: %s", ncclGetErrorString(r));
+    }
+  }
+  *out = g;
+  return 0;
+}
+
+int dp_destroy(DPGroup* g) {
+  if (!g) return 0;
+  for (auto& c : g->comms)
+    if (c) ncclCommDestroy(c);
+  delete g;
+  return 0;
+}
+
+int dp_local(const DPGroup* g) { return g ? (g->local ? 1 : 0) : DTC_EINVAL; }
+
+// bufs[i] lives on devs[i]; bufs[0] is the root (the module on device_ids[0])
+int dp_broadcast(DPGroup* g, void* const* bufs, size_t count, int dtype, void* const* streams) {
+  DTC_CHECK_ARG(g && bufs && streams, "dp_broadcast: bad args");
+  if (count == 0 || g->n == 1) return 0;
+  if (g->local) {
+    for (int i = 1; i < g->n; ++i)
+      DTC_HIP(hipMemcpyAsync(bufs[i], bufs[0], count * dtype_bytes(dtype), hipMemcpyDeviceToDevice,
+                             (hipStream_t)streams[0]));
+    return 0;
+  }
+  DeviceGuard guard;
+  DTC_NCCL(ncclGroupStart());
+  for (int i = 0; i < g->n; ++i) {
+    DTC_HIP(hipSetDevice(g->devs[i]));
+    DTC_NCCL(ncclBroadcast(bufs[i], bufs[i], count, to_nccl(dtype), 0, g->comms[i], (hipStream_t)streams[i]));
+  }
+  DTC_NCCL(ncclGroupEnd());
+  return 0;
+}
+
+// bufs[0] += sum_{i>0} bufs[i] (fp32), i.e. torch's reduce_add onto device_ids[0]
+int dp_reduce_add(DPGroup* g, float* const* bufs, size_t count, void* const* streams) {
+  DTC_CHECK_ARG(g && bufs && streams, "dp_reduce_add: bad args");
+  if (count == 0 || g->n == 1) return 0;
+  if (g->local) {
+    for (int i = 1; i < g->n; ++i) DTC_TRY(add_f32(bufs[0], bufs[i], (int64_t)count, (hipStream_t)streams[0]));
+    return 0;
+  }
+  DeviceGuard guard;
+  DTC_NCCL(ncclGroupStart());
+  for (int i = 0; i < g->n; ++i) {
+    DTC_HIP(hipSetDevice(g->devs[i]));
+    DTC_NCCL(ncclReduce(bufs[i], bufs[i], count, ncclFloat32, ncclSum, 0, g->comms[i], (hipStream_t)streams[i]));
+  }
+  DTC_NCCL(ncclGroupEnd());
+  return 0;
+}
+
+int copy_peer(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes, hipStream_t st) {
+  DTC_CHECK_ARG(dst && src, "copy_peer: null pointer");
+  if (bytes == 0) return 0;
+  if (dst_dev == src_dev) DTC_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+  else DTC_HIP(hipMemcpyPeerAsync(dst, dst_dev, src, src_dev, bytes, st));
+  return 0;
+}
+
+}  // namespace dtc

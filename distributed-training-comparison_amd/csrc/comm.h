@@ -27,4 +27,12 @@ int comm_world(const Comm* c);
 int comm_init_loopback(Comm** out, int device, int world, float factor);
 const std::vector<CommLogEntry>* comm_log(Comm* c);
 void comm_log_clear(Comm* c);
+// DataParallel group (single process, one replica per device; see comm.cpp)
+struct DPGroup;
+int dp_create(DPGroup** out, int n, const int* devs);
+int dp_destroy(DPGroup* g);
+int dp_local(const DPGroup* g);
+int dp_broadcast(DPGroup* g, void* const* bufs, size_t count, int dtype, void* const* streams);
+int dp_reduce_add(DPGroup* g, float* const* bufs, size_t count, void* const* streams);
+int copy_peer(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes, hipStream_t st);
 }  // namespace dtc

@@ -210,7 +210,10 @@ int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st);
 // x[i] *= f (loopback test communicator)
 int scale_f32(float* x, int64_t n, float f, hipStream_t st);
 int scale_f64(double* x, int64_t n, double f, hipStream_t st);
+// dst[i] += src[i] (DataParallel reduce-add of replicas sharing a device)
+int add_f32(float* dst, const float* src, int64_t n, hipStream_t st);
 int amp_check_finite(const float* g, int64_t n, int* found_inf, hipStream_t st);
+int amp_scale(const float* x, const float* scale, float* out, int64_t n, hipStream_t st);  // out = x * (*scale)
 int amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, int* found_inf, float growth,
                      float backoff, int interval, hipStream_t st);
 

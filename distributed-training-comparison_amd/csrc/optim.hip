@@ -81,6 +81,37 @@ int scale_f64(double* x, int64_t n, double f, hipStream_t st) {
   return 0;
 }
 
+__global__ void amp_scale_kernel(const float* __restrict__ x, const float* __restrict__ scale, float* __restrict__ out,
+                                 int64_t n) {
+  const float s = *scale;
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) out[i] = x[i] * s;
+}
+
+int amp_scale(const float* x, const float* scale, float* out, int64_t n, hipStream_t st) {
+  DTC_CHECK_ARG(x && scale && out && n > 0, "amp_scale: bad args");
+  const int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(amp_scale_kernel, dim3(blocks), dim3(256), 0, st, x, scale, out, n);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void add_f32_kernel(float* __restrict__ d, const float* __restrict__ s, int64_t n4) {
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    f32x4 a = ((f32x4*)d)[i];
+    a += ((const f32x4*)s)[i];
+    ((f32x4*)d)[i] = a;
+  }
+}
+
+int add_f32(float* dst, const float* src, int64_t n, hipStream_t st) {
+  DTC_CHECK_ARG(dst && src && n > 0 && n % 4 == 0 && ((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0,
+                "add_f32: bad args (n %% 4 and 16-byte alignment required)");
+  const int blocks = (int)std::min<int64_t>(2048, (n / 4 + 255) / 256);
+  hipLaunchKernelGGL(add_f32_kernel, dim3(blocks), dim3(256), 0, st, dst, src, n / 4);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 __global__ void amp_check_finite_kernel(const float* __restrict__ g, int64_t n, int* __restrict__ found) {
   bool bad = false;
   for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)

@@ -237,18 +237,32 @@ class NativeLoss(torch.Tensor):
 
     __torch_function__ = torch._C._disabled_torch_function_impl
 
+    @property
+    def _dtc_graph(self):
+        """The autograd form of this loss (built on first use: the fast path never needs it)."""
+        g = self.__dict__.get("_dtc_graph_t")
+        if g is None:
+            g = self._dtc_graph_fn()
+            self.__dict__["_dtc_graph_t"] = g
+        return g
+
     def backward(self, gradient=None, retain_graph=None, create_graph=False, inputs=None):
         fast = self._dtc_fast
         if fast is None or gradient is not None or create_graph or inputs is not None or not _FAST_BACKWARD[0]:
             return self._dtc_graph.backward(gradient, retain_graph, create_graph, inputs)
         node, logits, labels, lse, gscale = fast
-        model, exe = node.model, node.exe
-        if exe.generation != node.gen:
-            raise NativeError("ResNet backward: the executor ran another forward since this graph was built "
-                              "(one forward per backward is supported)")
-        dl = ops.xent_bwd(logits, labels, lse, gscale, out=exe.dlogits_buffer())
-        exe.backward(dl, model._grad_scale, model._comm)
-        model._ensure_grads()
+        if isinstance(node, _NetFn._backward_cls):
+            model, exe = node.model, node.exe
+            if exe.generation != node.gen:
+                raise NativeError("ResNet backward: the executor ran another forward since this graph was built "
+                                  "(one forward per backward is supported)")
+            dl = ops.xent_bwd(logits, labels, lse, gscale, out=exe.dlogits_buffer())
+            exe.backward(dl, model._grad_scale, model._comm)
+            model._ensure_grads()
+        else:  # DataParallel's gathered logits: xent backward, then the replicas' backward + reduce-add
+            from .parallel import _DPFn
+
+            _DPFn.backward(node, ops.xent_bwd(logits, labels, lse, gscale))
         if not retain_graph:
             self._dtc_fast = None
         return None
@@ -271,9 +285,11 @@ class NativeLoss(torch.Tensor):
 _FAST_BACKWARD = [True]  # tests flip this to compare against the autograd-engine path
 
 
-def _wrap_loss(graph: torch.Tensor, fast, host_copy: bool = False) -> torch.Tensor:
-    out = torch.Tensor._make_subclass(NativeLoss, graph.detach(), False)
-    out._dtc_graph = graph
+def _wrap_loss(value: torch.Tensor, graph_fn, fast, host_copy: bool = False) -> torch.Tensor:
+    """NativeLoss holding `value` (no autograd history of its own); graph_fn() builds the autograd
+    form on demand (the fallback backward path)."""
+    out = torch.Tensor._make_subclass(NativeLoss, value.detach(), False)
+    out._dtc_graph_fn = graph_fn
     out._dtc_fast = fast
     if host_copy:
         h = torch.empty((), dtype=graph.dtype, pin_memory=True)
@@ -287,9 +303,10 @@ def _wrap_loss(graph: torch.Tensor, fast, host_copy: bool = False) -> torch.Tens
 def scaled_loss(loss: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
     """loss * scale (GradScaler.scale); keeps the direct backward chain of a NativeLoss."""
     if isinstance(loss, NativeLoss):
-        g = loss._dtc_graph * scale
         f = loss._dtc_fast
-        return _wrap_loss(g, None if f is None else (f[0], f[1], f[2], f[3], scale))
+        # the value on the native kernel (GradScaler K9: no torch elementwise launch in the step)
+        return _wrap_loss(ops.amp_scale(loss.detach(), scale), lambda: loss._dtc_graph * scale,
+                          None if f is None else (f[0], f[1], f[2], f[3], scale))
     return loss * scale
 
 
@@ -304,8 +321,11 @@ class CrossEntropyLoss(nn.Module):
         labels = labels.long().contiguous()
         loss = _XentFn.apply(logits, labels)
         node = logits.grad_fn
-        if torch.is_grad_enabled() and isinstance(node, _NetFn._backward_cls):
-            return _wrap_loss(loss, (node, logits, labels, loss.grad_fn.lse, None), host_copy=True)
+        if torch.is_grad_enabled() and node is not None:
+            from .parallel import _DPFn
+
+            if isinstance(node, (_NetFn._backward_cls, _DPFn._backward_cls)):
+                return _wrap_loss(loss, lambda: loss, (node, logits, labels, loss.grad_fn.lse, None), host_copy=True)
         return loss
 
 

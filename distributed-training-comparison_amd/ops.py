@@ -221,6 +221,13 @@ def amp_check_finite(g, found_inf):
     call("dtc_amp_check_finite", ptr(g), g.numel(), ptr(found_inf), stream_ptr())
 
 
+def amp_scale(x, scale):
+    """GradScaler.scale(x) (main.py:25, trainer.py:157) on the native kernel: x * scale, device-side."""
+    out = torch.empty_like(x)
+    call("dtc_amp_scale", ptr(x), ptr(scale), ptr(out), x.numel(), stream_ptr())
+    return out
+
+
 def amp_update_scale(scale, inv_scale, tracker, found_inf, growth, backoff, interval):
     call("dtc_amp_update_scale", ptr(scale), ptr(inv_scale), ptr(tracker), ptr(found_inf), float(growth),
          float(backoff), int(interval), stream_ptr())

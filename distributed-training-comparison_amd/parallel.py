@@ -242,6 +242,61 @@ DDP = DistributedDataParallel
 
 
 # ----------------------------------------------------------------------------- DataParallel
+class DPGroup:
+    """Native DataParallel group over `device_ids` (include/dtc.h dtc_dp_*): one grouped RCCL
+    broadcast / reduce per call over distinct devices (ncclCommInitAll, one process), or on-device
+    copies + a HIP reduce-add kernel when every replica shares one device."""
+
+    def __init__(self, device_ids):
+        self.device_ids = list(device_ids)
+        n = len(self.device_ids)
+        arr = (C.c_int * n)(*self.device_ids)
+        self.handle = C.c_void_p()
+        call("dtc_dp_create", C.byref(self.handle), n, arr)
+        self.local = bool(lib.dtc_dp_is_local(self.handle))
+
+    def _streams(self):
+        return (C.c_void_p * len(self.device_ids))(*[stream_ptr(torch.cuda.current_stream(d))
+                                                     for d in self.device_ids])
+
+    def broadcast(self, tensors) -> None:
+        """tensors[i] on device_ids[i]; tensors[0] (the module's) is the source (C5)."""
+        n = tensors[0].numel()
+        bufs = (C.c_void_p * len(tensors))(*[ptr(t) for t in tensors])
+        call("dtc_dp_broadcast", self.handle, bufs, n, _DTYPES[tensors[0].dtype], self._streams())
+
+    def reduce_add(self, tensors) -> None:
+        """tensors[0] += sum of the others (fp32), onto device_ids[0] (C7)."""
+        n = tensors[0].numel()
+        bufs = (C.c_void_p * len(tensors))(*[ptr(t) for t in tensors])
+        call("dtc_dp_reduce_add", self.handle, bufs, n, self._streams())
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib.dtc_dp_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass
+
+
+def _copy_peer(dst: torch.Tensor, src: torch.Tensor, stream) -> None:
+    call("dtc_copy_peer", ptr(dst), dst.device.index, ptr(src), src.device.index, src.numel() * src.element_size(),
+         stream_ptr(stream))
+
+
+def _order_after(dst_dev: torch.device, src_dev: torch.device) -> None:
+    """Make dst_dev's current stream wait for everything issued so far on src_dev's current stream."""
+    if dst_dev == src_dev:
+        return
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(src_dev))
+    torch.cuda.current_stream(dst_dev).wait_event(ev)
+
+
 class _Replica:
     """A non-primary replica of a native ResNet: its own flat parameter / gradient / buffer
     copies and executors on one device. Parameters and buffers are refreshed from the primary
@@ -254,6 +309,7 @@ class _Replica:
         with torch.cuda.device(device):
             self.flat = FlatState(model.flat.layout, device)
         self._executors = {}
+        self._io = {}
 
     def executor(self, batch: int, height: int, width: int, precision: str):
         from .nn import Executor
@@ -267,59 +323,87 @@ class _Replica:
             self._executors[key] = exe
         return exe
 
-    def pull(self, primary) -> None:
-        """Broadcast (replicate) of the primary's fp32 parameters, their bf16 shadow and the BN
-        buffers into this replica (device-to-device copies over xGMI for a peer GPU)."""
-        with torch.cuda.device(self.device):
-            self.flat.params.copy_(primary.params, non_blocking=True)
-            self.flat.params_bf16.copy_(primary.params_bf16, non_blocking=True)
-            self.flat.bufs.copy_(primary.bufs, non_blocking=True)
-            self.flat.nbt.copy_(primary.nbt, non_blocking=True)
+    def io(self, name: str, shape, dtype=torch.float32) -> torch.Tensor:
+        """Cached per-replica staging buffer (input chunk, logits, dlogits) on this replica's device."""
+        t = self._io.get(name)
+        if t is None or tuple(t.shape) != tuple(shape):
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+            self._io[name] = t
+        return t
 
 
 class _DPFn(torch.autograd.Function):
     """scatter -> replicate -> parallel_apply -> gather (forward) and its reverse (backward:
     gather's backward scatters dlogits, replicate's backward reduce-adds the replicas' gradients
-    into the primary's flat gradient buffer on device_ids[0])."""
+    into the primary's flat gradient buffer on device_ids[0]). Every byte moves through the native
+    library: replicate / reduce-add as grouped RCCL collectives (or on-device copies + a HIP add
+    kernel for replicas sharing a device), scatter / gather as peer copies, or as plain views into
+    the caller's tensors where a replica shares device_ids[0] (no copy at all)."""
 
     @staticmethod
     def forward(ctx, x, anchor, dp):
         model = dp.module
-        chunks = x.chunk(len(dp.device_ids))  # torch.nn.parallel.scatter's split of dim 0
+        dev0 = dp.devices[0]
+        sizes = [c.shape[0] for c in x.chunk(len(dp.device_ids))]  # torch.nn.parallel.scatter's split
+        offs = [sum(sizes[:i]) for i in range(len(sizes))]
         train = model.training
         prec = model.compute_precision()  # autocast is thread-local: decided once, here
+        reps = [None] + [dp._replica(i) for i in range(1, len(sizes))]
+        # C5 replicate: fp32 master parameters, their bf16 shadow, BN buffers -- one call each
+        flats = [model.flat] + [r.flat for r in reps[1:]]
+        for i in range(1, len(flats)):
+            _order_after(dp.devices[i], dev0)  # the replicas receive after the module's last update
+        dp.group.broadcast([f.params for f in flats])
+        dp.group.broadcast([f.params_bf16 for f in flats])
+        dp.group.broadcast([f.bufs for f in flats])
+        dp.group.broadcast([f.nbt for f in flats])
+        out = torch.empty(x.shape[0], model.num_classes, dtype=torch.float32, device=dev0)
         runs = []
-        for i, c in enumerate(chunks):
+        for i, n in enumerate(sizes):
             dev = dp.devices[i]
+            xi = x[offs[i]:offs[i] + n]
             with torch.cuda.device(dev):
-                if i == 0:
-                    exe = model.executor(c.shape[0], c.shape[2], c.shape[3], prec)
+                exe = (model if i == 0 else reps[i]).executor(n, x.shape[2], x.shape[3], prec)
+                if dev == dev0:  # the chunk and the logits slice are views: no copies (C6 on one device)
+                    lo = out[offs[i]:offs[i] + n]
                 else:
-                    rep = dp._replica(i)
-                    rep.pull(model.flat)
-                    exe = rep.executor(c.shape[0], c.shape[2], c.shape[3], prec)
-                xi = c.to(dev, non_blocking=True).contiguous()
-                logits = torch.empty(c.shape[0], model.num_classes, dtype=torch.float32, device=dev)
-                gen = exe.forward(xi, logits, train)
-                runs.append((exe, gen, logits, xi))
-        ctx.dp, ctx.runs = dp, [(r[0], r[1]) for r in runs]
-        ctx.sizes = [c.shape[0] for c in chunks]
-        return torch.cat([r[2].to(dp.devices[0], non_blocking=True) for r in runs])  # gather (C7)
+                    xd = reps[i].io("x", xi.shape)
+                    _order_after(dev, dev0)
+                    _copy_peer(xd, xi, torch.cuda.current_stream(dev))
+                    xi = xd
+                    lo = reps[i].io("logits", (n, model.num_classes))
+                gen = exe.forward(xi, lo, train)
+                runs.append((exe, gen, lo))
+        for i, (_, _, lo) in enumerate(runs):  # C6 gather onto device_ids[0]
+            if dp.devices[i] != dev0:
+                _order_after(dev0, dp.devices[i])
+                _copy_peer(out[offs[i]:offs[i] + sizes[i]], lo, torch.cuda.current_stream(dev0))
+        ctx.dp, ctx.runs, ctx.sizes, ctx.offs = dp, [(r[0], r[1]) for r in runs], sizes, offs
+        return out
 
     @staticmethod
     def backward(ctx, dlogits):
         dp = ctx.dp
         model = dp.module
-        parts = dlogits.contiguous().float().split(ctx.sizes)
-        for i, ((exe, gen), d) in enumerate(zip(ctx.runs, parts)):
+        dev0 = dp.devices[0]
+        dl = dlogits.contiguous().float()
+        for i, (exe, gen) in enumerate(ctx.runs):
             if exe.generation != gen:
                 raise NativeError("DataParallel backward: a replica ran another forward since this graph was built")
             dev = dp.devices[i]
+            d = dl[ctx.offs[i]:ctx.offs[i] + ctx.sizes[i]]
             with torch.cuda.device(dev):
-                exe.backward(d.to(dev, non_blocking=True).contiguous(), 1.0, None)
-        g0 = model.flat.grads
-        for i in range(1, len(ctx.runs)):  # ReduceAddCoalesced onto device_ids[0] (C6)
-            g0.add_(dp._replica(i).flat.grads.to(g0.device, non_blocking=True))
+                if dev != dev0:  # gather's backward: the replica's slice of dlogits
+                    dd = dp._replica(i).io("dlogits", d.shape)
+                    _order_after(dev, dev0)
+                    _copy_peer(dd, d, torch.cuda.current_stream(dev))
+                    d = dd
+                exe.backward(d, 1.0, None)
+        # C7 ReduceAddCoalesced onto device_ids[0]: one call over the flat gradient buffers
+        flats = [model.flat] + [dp._replica(i).flat for i in range(1, len(ctx.runs))]
+        for i in range(1, len(flats)):
+            _order_after(dev0, dp.devices[i])
+        dp.group.reduce_add([f.grads for f in flats])
         model._ensure_grads()
         return None, None, None
 
@@ -333,7 +417,8 @@ class DataParallel(nn.Module):
     replicas' native backwards on their logits-gradient slices and sums their gradients into the
     module's. BatchNorm statistics are per replica, and only replica 0 -- the module itself --
     keeps its running-statistics update, exactly as torch's replicate() leaves them.
-    A device id may repeat (replicas sharing one GPU) -- the single-GPU test of this path."""
+    Replicas on distinct devices exchange through RCCL; device ids that are all equal (replicas
+    sharing one GPU) are the single-GPU test form of the same path."""
 
     def __init__(self, module, device_ids=None, output_device=None, dim=0):
         super().__init__()
@@ -354,6 +439,7 @@ class DataParallel(nn.Module):
         module._grad_scale = 1.0
         module._comm = None
         self._replicas = {}
+        self.group = DPGroup(self.device_ids) if len(self.device_ids) > 1 else None
 
     def _replica(self, i: int) -> _Replica:
         rep = self._replicas.get(i)
@@ -375,6 +461,8 @@ class DataParallel(nn.Module):
         require_cuda(x)
         if x.dim() != 4 or x.shape[1] != 3:
             raise ValueError(f"expected [N,3,H,W] input, got {tuple(x.shape)}")
-        if x.dtype != torch.float32:
-            x = x.float()
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.float().contiguous()
+        if x.device != self.devices[0]:
+            raise NativeError(f"DataParallel input must be on device_ids[0] ({self.devices[0]}), not {x.device}")
         return _DPFn.apply(x, self.module._anchor, self)

@@ -127,6 +127,8 @@ int dtc_sgd_nesterov_flat(float* p, const float* g, float* momentum_buf, uint16_
                           void* stream);
 int dtc_cast_f32_bf16(const float* src, uint16_t* dst, int64_t n, void* stream);
 int dtc_amp_check_finite(const float* g, int64_t n, int* found_inf, void* stream);
+/* GradScaler.scale(loss): out = x * (*scale) with the scale device-resident (no host sync) */
+int dtc_amp_scale(const float* x, const float* scale, float* out, int64_t n, void* stream);
 int dtc_amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, int* found_inf, float growth_factor,
                          float backoff_factor, int growth_interval, void* stream);
 
@@ -170,6 +172,25 @@ int dtc_comm_init_loopback(dtc_comm** out, int device, int world, float factor);
 int dtc_comm_log_size(dtc_comm* comm);
 int dtc_comm_log_entry(dtc_comm* comm, int idx, uint64_t* addr, uint64_t* count, int* is_async);
 int dtc_comm_log_clear(dtc_comm* comm);
+
+/* ------------------------------------------------------------------ DataParallel group
+ * Replaces the per-step traffic of nn.DataParallel (reference src/dp/trainer.py:27):
+ * replicate = broadcast of the module's flat buffers from device_ids[0] to every replica (C5),
+ * backward = reduce-add of the replicas' flat gradient buffers onto device_ids[0] (C7), input scatter
+ * / logits gather as peer copies (C6). One process drives all devices: distinct devices get one RCCL
+ * rank each (ncclCommInitAll) and every call is one grouped RCCL collective over all replicas;
+ * replicas that all share ONE device (device_ids=[0, 0], the single-GPU test form) run the same
+ * calls as on-device copies and a fixed-order HIP reduce-add kernel. bufs[i] / streams[i] belong to
+ * replica i (its device), bufs[0] is the root. dtype as for dtc_comm_*. */
+typedef struct dtc_dp dtc_dp;
+int dtc_dp_create(dtc_dp** out, int n, const int* devices);
+int dtc_dp_destroy(dtc_dp* group);
+int dtc_dp_is_local(const dtc_dp* group);
+int dtc_dp_broadcast(dtc_dp* group, void* const* bufs, size_t count, int dtype, void* const* streams);
+int dtc_dp_reduce_add(dtc_dp* group, float* const* bufs, size_t count, void* const* streams);
+/* dst (on dst_device) <- src (on src_device), `bytes`, ordered on `stream` (hipMemcpyPeerAsync; a plain
+ * device-to-device copy when the devices are equal) */
+int dtc_copy_peer(void* dst, int dst_device, const void* src, int src_device, size_t bytes, void* stream);
 
 /* ------------------------------------------------------------------ ResNet-18 executor
  * The whole forward (ResNet.forward, net.py:107-116) and backward of ResNet18() (net.py:119-120)
