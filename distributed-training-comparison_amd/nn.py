@@ -292,8 +292,8 @@ def _wrap_loss(value: torch.Tensor, graph_fn, fast, host_copy: bool = False) -> 
     out._dtc_graph_fn = graph_fn
     out._dtc_fast = fast
     if host_copy:
-        h = torch.empty((), dtype=graph.dtype, pin_memory=True)
-        h.copy_(graph.detach(), non_blocking=True)
+        h = torch.empty((), dtype=value.dtype, pin_memory=True)
+        h.copy_(value.detach(), non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         out._dtc_host = (h, ev)

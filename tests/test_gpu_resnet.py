@@ -712,6 +712,14 @@ def test_data_parallel_step_launches_only_native_kernels(dtc, cuda):
     assert not foreign, foreign
 
 
+def _grads_with(model, crit, x, y, comm):
+    model._comm = comm
+    loss = crit(model(x), y)
+    loss.backward()
+    torch.cuda.synchronize()
+    return model.flat.grads.detach().cpu().numpy().copy()
+
+
 @pytest.mark.parametrize("graphs", [1, 0])
 @pytest.mark.parametrize("cap_mb", [1.0, 5.0, 25.0])
 def test_reducer_reduces_every_bucket_once_after_its_producers(dtc, cuda, graphs, cap_mb):
