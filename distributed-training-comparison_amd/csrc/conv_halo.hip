@@ -70,7 +70,7 @@ struct HConvParams {
   u64* ts;
 };
 
-template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP>
+template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP, int WS>
 __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) {
   constexpr int FM = BM / (WR * 16);
   constexpr int FN = BN / (WC * 16);
@@ -78,8 +78,8 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   constexpr int HBYTES = HCAP * 128;
   constexpr int NIW = BM / 32;       // weight DMA instructions per wave per step
   constexpr int NHI = HCAP / 32;     // max halo DMA instructions per wave
-  static_assert(WR * WC == 4 && HCAP % 32 == 0, "shape");
-  __shared__ __attribute__((aligned(1024))) char smem[NHB * HBYTES + 2 * WBYTES];
+  static_assert(WR * WC == 4 && HCAP % 32 == 0 && (WS == 2 || WS == 3), "shape");
+  __shared__ __attribute__((aligned(1024))) char smem[NHB * HBYTES + WS * WBYTES];
   char* const wbase = smem + NHB * HBYTES;
 
   stamp_start(p.ts);
@@ -230,10 +230,21 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     }
   };
 
-  // ---- main loop: chunk pairs x 9 unrolled taps; step (c, tap) reads weight buffer (c + tap) & 1
-  // (9 is odd) and, for NHB == 2, halo buffer c & 1 -- both static after the unrolling
+  // ---- main loop: chunk pairs x 9 unrolled taps. Weights: a WS-slot ring; step (c, tap) reads slot
+  // (c + tap) & 1 (WS = 2; 9 is odd) or tap % 3 (WS = 3; 9 = 3 x 3) -- static after the unrolling.
+  // WS = 2: the next step's weights are issued right before this step's MFMAs and waited for with
+  // vmcnt(0) at the next step. WS = 3: two steps of weights in flight; a step waits only until its
+  // own weights (and any older halo DMA) landed: vmcnt(NIW) leaves the next step's NIW weight DMAs
+  // outstanding, vmcnt(0) where nothing younger exists (the last step) or where the NHB = 1 halo
+  // reload is the youngest DMA (a chunk's first step).
+  // Halo: NHB = 2 double-buffers it (the next chunk's halo arrives in slices during the current
+  // chunk's first eight taps; buffer c & 1), NHB = 1 reloads it at chunk boundaries.
+  const int nsteps = p.nchunk * 9;
   stage_h(smem, c0, 0, NHI);
   stage_w(wbase, c0, 0);
+  if constexpr (WS == 3) {
+    if (nsteps > 1) stage_w(wbase + WBYTES, c0, 1);
+  }
   for (int cc = 0; cc < p.nchunk; cc += 2) {
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -242,19 +253,30 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
       const char* hbuf = smem + (NHB == 2 ? half * HBYTES : 0);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        const int par = (half + tap) & 1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int step = c * 9 + tap;
+        if constexpr (WS == 3) {
+          if (step + 1 < nsteps && !(NHB == 1 && tap == 0 && c > 0)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIW) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (tap < 8) stage_w(wbase + (par ^ 1) * WBYTES, c0 + c, tap + 1);
-        else if (c + 1 < p.nchunk) stage_w(wbase + (par ^ 1) * WBYTES, c0 + c + 1, 0);
+        if constexpr (WS == 3) {  // weights of step + 2 into the slot step - 1 used
+          if (tap + 2 <= 8) stage_w(wbase + ((tap + 2) % 3) * WBYTES, c0 + c, tap + 2);
+          else if (c + 1 < p.nchunk) stage_w(wbase + ((tap + 2) % 3) * WBYTES, c0 + c + 1, tap + 2 - 9);
+        } else {
+          const int par = (half + tap) & 1;
+          if (tap < 8) stage_w(wbase + (par ^ 1) * WBYTES, c0 + c, tap + 1);
+          else if (c + 1 < p.nchunk) stage_w(wbase + (par ^ 1) * WBYTES, c0 + c + 1, 0);
+        }
         if constexpr (NHB == 2) {
           if (c + 1 < p.nchunk && tap < 8) {  // next chunk's halo, slice `tap` of 8
             const int q_lo = (tap * p.nhi) >> 3, q_hi = ((tap + 1) * p.nhi) >> 3;
             stage_h(smem + (half ^ 1) * HBYTES, c0 + c + 1, q_lo, q_hi);
           }
         }
-        compute(hbuf, wbase + par * WBYTES, tap);
+        compute(hbuf, wbase + (WS == 3 ? (tap % 3) : ((half + tap) & 1)) * WBYTES, tap);
         if (NHB == 1 && tap == 8 && c + 1 < p.nchunk) {  // every wave is done with the halo: refill it
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
@@ -510,20 +532,26 @@ size_t conv_halo_slab_bytes(const ConvShape& s, int mode) {
   return (size_t)hp.split * s.N * s.H * s.W * cout * 4;
 }
 
-template <int MODE>
-static int launch_halo(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
+template <int MODE, int WS>
+static int launch_halo_ws(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
   switch (cfg) {
-    case 0: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 256, 1, 4, 1, 416>), grid, dim3(256), 0, st, p); break;
-    case 1: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 2, 288>), grid, dim3(256), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 1, 288>), grid, dim3(256), 0, st, p); break;
-    case 3: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 256, 2, 2, 1, 416>), grid, dim3(256), 0, st, p); break;
-    case 4: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 1, 288>), grid, dim3(256), 0, st, p); break;
-    case 5: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 2, 288>), grid, dim3(256), 0, st, p); break;
-    case 6: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 2, 224>), grid, dim3(256), 0, st, p); break;
-    default: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 64, 2, 2, 2, 160>), grid, dim3(256), 0, st, p); break;
+    case 0: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 256, 1, 4, 1, 416, WS>), grid, dim3(256), 0, st, p); break;
+    case 1: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 2, 288, WS>), grid, dim3(256), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 1, 288, WS>), grid, dim3(256), 0, st, p); break;
+    case 3: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 256, 2, 2, 1, 416, WS>), grid, dim3(256), 0, st, p); break;
+    case 4: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 1, 288, WS>), grid, dim3(256), 0, st, p); break;
+    case 5: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 2, 288, WS>), grid, dim3(256), 0, st, p); break;
+    case 6: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 2, 224, WS>), grid, dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 64, 2, 2, 2, 160, WS>), grid, dim3(256), 0, st, p); break;
   }
   DTC_LAUNCH_CHECK();
   return 0;
+}
+
+template <int MODE>
+static int launch_halo(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
+  if (option_get(OPT_HALO_WSTAGES) >= 3) return launch_halo_ws<MODE, 3>(p, cfg, grid, st);
+  return launch_halo_ws<MODE, 2>(p, cfg, grid, st);
 }
 
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,

@@ -28,6 +28,8 @@ enum {
                           // kernels: 1 conv_c64, 2 conv_halo, 4 split-K reduce (others: separate pass).
                           // Default 0: measured neutral (c64, split-K) to -1% (halo) at B=256 -- the
                           // epilogue's strided 8-B y/x loads cost what the separate pass costs.
+  OPT_WGRAD_STAGES = 13,   // LDS ring depth of wgrad_halo (2: one step of DMA in flight; 4: three)
+  OPT_HALO_WSTAGES = 14,   // weight ring depth of conv_halo (2 or 3)
   OPT_COUNT
 };
 int option_get(int id);

@@ -35,9 +35,14 @@ struct HaloParams {
   u64* ts;
 };
 
-constexpr int HALO_ROWS = 192;                 // LDS rows reserved for the halo (3 DMA rounds)
-constexpr int HALO_BYTES = HALO_ROWS * 128;    // 24 KiB
-constexpr int HSTAGE = HALO_BYTES + 64 * 128;  // + dy tile (64 pixels x 64 channels)
+// LDS per pipeline stage: the halo (NR DMA rounds of 64 rows of 128 B) + the dy tile (64 pixels x 64
+// channels). NS stages form a ring; NS - 1 of them are in flight while one is computed.
+template <int NR>
+struct WgStage {
+  static constexpr int HALO_ROWS = 64 * NR;
+  static constexpr int HALO_BYTES = HALO_ROWS * 128;
+  static constexpr int BYTES = HALO_BYTES + 64 * 128;
+};
 
 // Tr-image fragment from the halo: lane holds column (channel) cin + lane&15, reduction rows =
 // the pixels whose halo rows are ra (4 pixels) and rb (next 4), already shifted by the tap.
@@ -51,8 +56,13 @@ __device__ __forceinline__ bf16x8 frag_halo(const char* halo, int cin, int ra, i
   return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// NS: pipeline stages in the LDS ring (2: wait for the next step's DMA at every step; 4: three
+// steps of DMA in flight, a counted s_waitcnt per step). NR: halo DMA rounds per step (2 or 3).
+template <int NS, int NR>
 __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * HSTAGE];
+  typedef WgStage<NR> SG;
+  constexpr int PER = NR + 1;  // LDS-DMA instructions per wave per stage (halo rounds + dy tile)
+  __shared__ __attribute__((aligned(1024))) char smem[NS * SG::BYTES];
   stamp_start(p.ts);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ktiles = p.K >> 6;
@@ -63,11 +73,10 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   const int W2 = p.W + 2;
 
   // ---- halo DMA: round j covers LDS rows j*64 + wave*8 + lane/8, 16-B chunk lane%8
-  const int nrounds = (p.nh + 63) >> 6;
-  int hrel[3], hrow_in[3];
-  bool hcol[3];
+  int hrel[NR], hrow_in[NR];
+  bool hcol[NR];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
+  for (int j = 0; j < NR; ++j) {
     const int hrow = j * 64 + wave * 8 + (lane >> 3);
     const int ii = hrow / p.hb, rem = hrow - ii * p.hb;
     const int hr = rem / W2, wc = rem - hr * W2;
@@ -86,13 +95,11 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     const int p0 = (int)fdiv((uint32_t)(m0 - n0 * (int)p.fd_hw.d), p.fd_w);
     const int base = ((n0 * p.H + p0) * p.W) * p.C * 2;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      if (j < nrounds) {
-        const bool ok = hcol[j] && (unsigned)(p0 + hrow_in[j]) < (unsigned)p.H;
-        buf_lds16(p.x, p.x_bytes, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)(base + hrel[j]) : 0x80000000u);
-      }
+    for (int j = 0; j < NR; ++j) {
+      const bool ok = hcol[j] && (unsigned)(p0 + hrow_in[j]) < (unsigned)p.H;
+      buf_lds16(p.x, p.x_bytes, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)(base + hrel[j]) : 0x80000000u);
     }
-    glds16(p.dy + (size_t)(m0 + trow) * p.K + dcol, sb + HALO_BYTES + wave * 1024);
+    glds16(p.dy + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + wave * 1024);
   };
 
   // ---- per-lane halo rows of the pixels this lane reads: t = ks*32 + 8*(lane>>4) + (lane&15)/4 (+4)
@@ -116,7 +123,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
 
   // Per-lane LDS byte offsets (within a stage) of every fragment half a step reads, computed once:
   // A = the x halo read transposed at each tap's shift, B = the dy tile read transposed. The step
-  // loop is unrolled by two so the stage base is a constant the ds_read offset field absorbs: the
+  // loop is unrolled by NS so each stage base is a constant the ds_read offset field absorbs: the
   // MFMA stream carries no address arithmetic.
   uint32_t aoff[2][9][2], boff[2][2][2];
 #pragma unroll
@@ -143,7 +150,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       for (int h = 0; h < 2; ++h) {
         const int kr = ks * 32 + g * 8 + q + 4 * h;
         const int f = (((kr >> 1) & 1) << 2) | (((kr >> 3) & 1) << 3);
-        boff[ks][j][h] = (uint32_t)(HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
+        boff[ks][j][h] = (uint32_t)(SG::HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
       }
     }
   }
@@ -168,20 +175,28 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     }
   };
 
-  // 2-stage LDS ring (as igemm_kernel): wait own DMAs, barrier, refill the other buffer, compute.
+  // NS-stage LDS ring. Step k: wait until this wave's DMAs of stage k landed (the DMAs of the
+  // NS - 2 younger stages may stay outstanding: a counted vmcnt; near the tail vmcnt(0)), barrier
+  // (every wave's DMAs of stage k landed, and every wave finished computing stage k - 1, whose slot
+  // is refilled next), issue stage k + NS - 1, compute stage k. A raw s_barrier is used:
+  // __syncthreads() would also drain vmcnt to 0.
   if (st_begin < st_end) {
-    stage(smem, st_begin);
     const int nk = st_end - st_begin;
-    auto one = [&](int it, char* cur, char* nxt) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (it + 1 < nk) stage(nxt, st_begin + it + 1);
-      compute(cur);
-    };
-    for (int it = 0; it < nk; it += 2) {
-      one(it, smem, smem + HSTAGE);
-      if (it + 1 < nk) one(it + 1, smem + HSTAGE, smem);
+#pragma unroll
+    for (int i = 0; i < NS - 1; ++i)
+      if (i < nk) stage(smem + i * SG::BYTES, st_begin + i);
+    for (int it = 0; it < nk; it += NS) {
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        const int k = it + u;
+        if (k >= nk) break;
+        if (NS > 2 && k + NS - 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PER) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (k + NS - 1 < nk) stage(smem + ((u + NS - 1) % NS) * SG::BYTES, st_begin + k + NS - 1);
+        compute(smem + u * SG::BYTES);
+      }
     }
   }
 
@@ -217,7 +232,7 @@ static bool halo_geometry(const ConvShape& s, int& rs, int& imgs) {
   }
   const int nh = imgs * (rs + 2) * (s.W + 2);
   // whole 64-pixel steps only (multi-image steps need N a multiple of the images per step)
-  return nh <= HALO_ROWS && ((int64_t)s.N * hw) % 64 == 0 && (uint64_t)s.N * hw * s.C * 2 < (1ull << 31);
+  return nh <= 192 && ((int64_t)s.N * hw) % 64 == 0 && (uint64_t)s.N * hw * s.C * 2 < (1ull << 31);
 }
 
 int wgrad_halo_splits(const ConvShape& s) {
@@ -250,7 +265,15 @@ int conv_wgrad_halo(const ConvShape& s, const u16* x, const u16* dy, float* slab
   p.ts = ts;
   const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
   dim3 grid((s.C / 64) * (s.K / 64), used);
-  hipLaunchKernelGGL(wgrad_halo_kernel, grid, dim3(512), 0, st, p);
+  const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
+  const bool deep = option_get(OPT_WGRAD_STAGES) >= 4;
+  if (nr <= 2) {
+    if (deep) hipLaunchKernelGGL((wgrad_halo_kernel<4, 2>), grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_halo_kernel<2, 2>), grid, dim3(512), 0, st, p);
+  } else {
+    if (deep) hipLaunchKernelGGL((wgrad_halo_kernel<4, 3>), grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_halo_kernel<2, 3>), grid, dim3(512), 0, st, p);
+  }
   DTC_LAUNCH_CHECK();
   *used_splits = used;
   return 0;
