@@ -129,6 +129,7 @@ def bench_dp(args):
     for d in set(dev_ids):
         torch.cuda.synchronize(d)
     elapsed = time.perf_counter() - t0
+    shared = len(set(dev_ids)) < len(dev_ids)
     print(json.dumps({
         "metric": f"images/sec ResNet-18 CIFAR-100 DataParallel (global batch {B}, one process)",
         "value": round(B * args.steps / elapsed, 2), "unit": "images/sec", "n_gpus": len(set(dev_ids)),
@@ -137,7 +138,11 @@ def bench_dp(args):
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic, resident in HBM",
         "config": {"workload": f"ResNet-18 DataParallel step, global batch {B}, {S}x{S}", "model": "ResNet18",
                    "global_batch": B, "seq_len": None, "parallelism": f"dp-single-process x{len(dev_ids)}",
-                   "device_ids": dev_ids},
+                   "device_ids": dev_ids,
+                   "transport": "replicas share one device: on-device copies + HIP reduce-add (dtc_dp_*)" if shared
+                   else "grouped RCCL broadcast / reduce over distinct devices (dtc_dp_*, ncclCommInitAll)"},
+        "note": (f"device_ids {dev_ids}: {len(dev_ids)} replicas on ONE GPU -- the single-GPU form of the "
+                 "DataParallel path, NOT BASELINE config 4 (8 GPUs)") if shared else None,
         "final_loss": round(losses[-1], 4)}), flush=True)
 
 
@@ -343,7 +348,8 @@ def main():
                        "model": "ResNet18 (CIFAR, src/ddp/net.py)", "global_batch": B * world, "seq_len": None,
                        "parallelism": f"dp{world}", "per_gpu_batch": B, "image_size": S,
                        "step_barrier": not args.no_barrier, "loss_item": not args.no_item,
-                       "sync_bn": bool(args.sync_bn)},
+                       "sync_bn": bool(args.sync_bn),
+                       "buckets_mb": [round(n * 4 / 2**20, 2) for _, n in model.buckets]},
             "roofline": {
                 "bound": "mfma",
                 "achieved": round(achieved, 2) if achieved else None,

@@ -30,6 +30,8 @@ enum {
                           // epilogue's strided 8-B y/x loads cost what the separate pass costs.
   OPT_WGRAD_STAGES = 13,   // LDS ring depth of wgrad_halo (2: one step of DMA in flight; 4: three)
   OPT_HALO_WSTAGES = 14,   // weight ring depth of conv_halo (2 or 3)
+  OPT_WGRAD_DIAG = 15,     // diagnostics only: 1 = wgrad_halo skips its slab stores (WRONG results)
+  OPT_WGRAD_PF = 16,       // wgrad_halo LDS fragment prefetch window (0 = compiler-scheduled, 5, 8)
   OPT_COUNT
 };
 int option_get(int id);

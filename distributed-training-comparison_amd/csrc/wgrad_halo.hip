@@ -32,6 +32,8 @@ struct HaloParams {
   int steps_per_split, nsteps;
   int rs, hb, nh;  // output rows per image per step, halo rows per image block, halo rows per step
   int spi;         // pixels per image block of a step (rs * W)
+  int nostore;     // diagnostics only (option wgrad_diag = 1): skip the slab stores (wrong results)
+  int diag;        // diagnostics only: 2 = no halo DMA after the first stage, 3 = no dy DMA after it
   u64* ts;
 };
 
@@ -58,7 +60,11 @@ __device__ __forceinline__ bf16x8 frag_halo(const char* halo, int cin, int ra, i
 
 // NS: pipeline stages in the LDS ring (2: wait for the next step's DMA at every step; 4: three
 // steps of DMA in flight, a counted s_waitcnt per step). NR: halo DMA rounds per step (2 or 3).
-template <int NS, int NR>
+// PF: 0 = fragments read next to their MFMAs (compiler-scheduled), > 0 = explicit LDS prefetch
+// window: the step's 22 operand fragments (per k-step: 2 dy, 9 halo) are read PF fragments ahead
+// of the MFMAs that consume them, one fragment (two ds_read_b64_tr_b16) issued per consumed halo
+// fragment, so an LDS read's latency hides behind the MFMAs of the PF fragments before it.
+template <int NS, int NR, int PF>
 __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   typedef WgStage<NR> SG;
   constexpr int PER = NR + 1;  // LDS-DMA instructions per wave per stage (halo rounds + dy tile)
@@ -94,12 +100,15 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     const int n0 = (int)fdiv((uint32_t)m0, p.fd_hw);
     const int p0 = (int)fdiv((uint32_t)(m0 - n0 * (int)p.fd_hw.d), p.fd_w);
     const int base = ((n0 * p.H + p0) * p.W) * p.C * 2;
+    const bool first = step == st_begin;
+    if (p.diag != 2 || first) {
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const bool ok = hcol[j] && (unsigned)(p0 + hrow_in[j]) < (unsigned)p.H;
-      buf_lds16(p.x, p.x_bytes, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)(base + hrel[j]) : 0x80000000u);
+      for (int j = 0; j < NR; ++j) {
+        const bool ok = hcol[j] && (unsigned)(p0 + hrow_in[j]) < (unsigned)p.H;
+        buf_lds16(p.x, p.x_bytes, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)(base + hrel[j]) : 0x80000000u);
+      }
     }
-    glds16(p.dy + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + wave * 1024);
+    if (p.diag != 3 || first) glds16(p.dy + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + wave * 1024);
   };
 
   // ---- per-lane halo rows of the pixels this lane reads: t = ks*32 + 8*(lane>>4) + (lane&15)/4 (+4)
@@ -161,16 +170,44 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
   };
   auto compute = [&](const char* sb) {
+    if constexpr (PF == 0) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 bfr[2];
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 bfr[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
+        for (int j = 0; j < 2; ++j) bfr[j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
 #pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        const bf16x8 af = tr8(sb, aoff[ks][i][0], aoff[ks][i][1]);
+        for (int i = 0; i < 9; ++i) {
+          const bf16x8 af = tr8(sb, aoff[ks][i][0], aoff[ks][i][1]);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    } else {
+      constexpr int NF = 22;  // fragment q: k-step q / 11; slot q % 11: 0, 1 = dy (B), 2..10 = halo (A)
+      bf16x8 f[NF];
+      auto ld = [&](int q) {
+        const int ks = q / 11, r = q % 11;
+        f[q] = r < 2 ? tr8(sb, boff[ks][r][0], boff[ks][r][1]) : tr8(sb, aoff[ks][r - 2][0], aoff[ks][r - 2][1]);
+      };
+#pragma unroll
+      for (int q = 0; q < PF; ++q) ld(q);
+      int next = PF;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+          const int q = ks * 11 + 2 + i;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[q], f[ks * 11 + j], acc[i][j], 0, 0, 0);
+          if (next < NF) {
+            ld(next);
+            ++next;
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // the two MFMAs,
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // then this slot's two LDS reads
+        }
       }
     }
   };
@@ -201,6 +238,10 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   }
 
   // ---- epilogue: slab[split][k][tap*C + c0 + c] (4 consecutive c per lane: one 16-B store)
+  if (p.nostore) {
+    stamp_end(p.ts);
+    return;
+  }
   const int RSC = 9 * p.C;
   float* slab = p.slab + (size_t)split * p.K * RSC;
 #pragma unroll
@@ -263,17 +304,24 @@ int conv_wgrad_halo(const ConvShape& s, const u16* x, const u16* dy, float* slab
   p.nh = imgs * p.hb;
   p.spi = rs * s.W;
   p.ts = ts;
+  p.nostore = option_get(OPT_WGRAD_DIAG) == 1;
+  p.diag = option_get(OPT_WGRAD_DIAG);
   const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
   dim3 grid((s.C / 64) * (s.K / 64), used);
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
   const bool deep = option_get(OPT_WGRAD_STAGES) >= 4;
+  const int pf = option_get(OPT_WGRAD_PF);
+#define DTC_WH(NS_, NR_, PF_) hipLaunchKernelGGL((wgrad_halo_kernel<NS_, NR_, PF_>), grid, dim3(512), 0, st, p)
   if (nr <= 2) {
-    if (deep) hipLaunchKernelGGL((wgrad_halo_kernel<4, 2>), grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((wgrad_halo_kernel<2, 2>), grid, dim3(512), 0, st, p);
+    if (pf >= 8) { if (deep) DTC_WH(4, 2, 8); else DTC_WH(2, 2, 8); }
+    else if (pf > 0) { if (deep) DTC_WH(4, 2, 5); else DTC_WH(2, 2, 5); }
+    else { if (deep) DTC_WH(4, 2, 0); else DTC_WH(2, 2, 0); }
   } else {
-    if (deep) hipLaunchKernelGGL((wgrad_halo_kernel<4, 3>), grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((wgrad_halo_kernel<2, 3>), grid, dim3(512), 0, st, p);
+    if (pf >= 8) { if (deep) DTC_WH(4, 3, 8); else DTC_WH(2, 3, 8); }
+    else if (pf > 0) { if (deep) DTC_WH(4, 3, 5); else DTC_WH(2, 3, 5); }
+    else { if (deep) DTC_WH(4, 3, 0); else DTC_WH(2, 3, 0); }
   }
+#undef DTC_WH
   DTC_LAUNCH_CHECK();
   *used_splits = used;
   return 0;

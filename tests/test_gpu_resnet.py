@@ -681,6 +681,8 @@ def _native_kernels_only(dtc, cuda, fn):
         fn()
         torch.cuda.synchronize()
     names = {e.name for e in prof.events() if e.device_type.name == "CUDA"}
+    native = sorted(n for n in names if "dtc::" in n)
+    assert len(native) >= 20, f"profiler saw too few native kernels to judge: {sorted(names)}"
     return sorted(n for n in names if "dtc::" not in n and not n.startswith(("Memcpy", "Memset", "hipMemcpy",
                                                                              "hipMemset", "__amd_rocclr")))
 
