@@ -12,11 +12,11 @@
 #include <cstring>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {0}, {1}, {1}, {0}, {0}, {2}, {3}, {0}, {0}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {0}, {1}, {1}, {0}, {0}, {2}, {3}, {0}, {0}, {1}, {4}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
                                              "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
                                              "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse",
-                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf"};
+                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch"};
 static std::atomic<int> g_epoch{0};
 int option_get(int id) { return g_opts[id].load(std::memory_order_relaxed); }
 int option_epoch() { return g_epoch.load(std::memory_order_relaxed); }
@@ -101,6 +101,19 @@ int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* 
                      size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && dy && dw && ws, "dtc_conv2d_wgrad: null argument (workspace is required)");
   GUARD(return conv_wgrad(shape_of(d), x, dy, dw, 0, 0, scale, (float*)ws, ws_bytes, S(stream));)
+}
+
+size_t dtc_conv2d_wgrad_batch_workspace_size(const dtc_conv_desc* d, int n) {
+  if (!d || n < 1 || n > DTC_WG_BATCH) return 0;
+  const ConvShape s = shape_of(d);
+  return wgrad_halo_splits(s, n) > 0 ? conv_wgrad_batch_slab_bytes(s, n) : 0;
+}
+
+int dtc_conv2d_wgrad_batch(const dtc_conv_desc* d, int n, const uint16_t* const* x, const uint16_t* const* dy,
+                           float* const* dw, float scale, void* ws, size_t ws_bytes, void* stream) {
+  DTC_CHECK_ARG(d && x && dy && dw && ws && n >= 1 && n <= DTC_WG_BATCH, "dtc_conv2d_wgrad_batch: bad argument");
+  for (int i = 0; i < n; ++i) DTC_CHECK_ARG(x[i] && dy[i] && dw[i], "dtc_conv2d_wgrad_batch: null problem %d", i);
+  GUARD(return conv_wgrad_batch(shape_of(d), n, x, dy, dw, scale, (float*)ws, ws_bytes, S(stream));)
 }
 
 int dtc_bn_fwd_finalize(double* stats, int c, int64_t count, const float* gamma, const float* beta,

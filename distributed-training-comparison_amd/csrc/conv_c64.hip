@@ -58,7 +58,7 @@ __device__ __forceinline__ bf16x8 lds_frag(uint32_t addr) {
 // instead of running after them on the wave's single SIMD (one wave per SIMD: nothing else would
 // hide it). Per-lane B-fragment LDS offsets for all nine taps and both k-steps, and the
 // tile-invariant part of the halo DMA addressing, are computed once per workgroup.
-template <int MODE>
+template <int MODE, bool PF>
 __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   constexpr int FM = 4, FN = 4;  // wave tile: 64 channels x 64 pixels
   constexpr bool FWD = MODE == 0, RES = MODE == 2 || MODE == 4, BNB = MODE >= 3;
@@ -247,25 +247,55 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[FM], bfr[FN];
+    if constexpr (PF) {
+      // 18 (tap, k-step) groups of FM + FN fragment reads and FM x FN MFMAs. The reads of group g + 1
+      // go out before the MFMAs of group g (two register sets; scheduling fences keep the compiler
+      // from sinking them back next to their uses), so with one wave per SIMD an LDS read's latency
+      // hides behind the 16 MFMAs before it instead of stalling the SIMD once per group.
+      bf16x8 af[2][FM], bfr[2][FN];
+      auto load = [&](int g, int b) {
+        const int t = g >> 1, ks = g & 1;
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          af[i] = FWD ? frag_row(smem + t * 8192, i * 16, ks, lane) : frag_tr(smem + t * 8192, i * 16, ks, lane);
+          af[b][i] = FWD ? frag_row(smem + t * 8192, i * 16, ks, lane) : frag_tr(smem + t * 8192, i * 16, ks, lane);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[j] = lds_frag(hb + boff[t][ks][j]);
+        for (int j = 0; j < FN; ++j) bfr[b][j] = lds_frag(hb + boff[t][ks][j]);
+      };
+      load(0, 0);
+#pragma unroll
+      for (int g = 0; g < 18; ++g) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + 1 < 18) load(g + 1, (g + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[g & 1][i], bfr[g & 1][j], acc[i][j], 0, 0, 0);
+        // the previous tile's epilogue, one pixel-column group after each odd tap's second k-step
+        if ((g & 3) == 3) epilogue_col(accp, tilep, k > 0, g >> 2);
       }
-      // the previous tile's epilogue, one pixel-column group after each odd tap (placed between
-      // MFMA groups so the scheduler spreads it over the MFMA issue gaps)
-      if (t & 1) epilogue_col(accp, tilep, k > 0, t >> 1);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          bf16x8 af[FM], bfr[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            af[i] = FWD ? frag_row(smem + t * 8192, i * 16, ks, lane) : frag_tr(smem + t * 8192, i * 16, ks, lane);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bfr[j] = lds_frag(hb + boff[t][ks][j]);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        // the previous tile's epilogue, one pixel-column group after each odd tap (placed between
+        // MFMA groups so the scheduler spreads it over the MFMA issue gaps)
+        if (t & 1) epilogue_col(accp, tilep, k > 0, t >> 1);
+      }
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -361,16 +391,19 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   const int grid = std::min(p.ntiles, 256);
   const bool in_kernel = fuse && bnb->x2 == nullptr;  // one BN per epilogue (layer1 has no projection)
   if (in_kernel) p.bnb = *bnb;
-  if (mode == CONV_FWD)
-    hipLaunchKernelGGL(conv_c64_kernel<0>, dim3(grid), dim3(256), 0, st, p);
-  else if (in_kernel && res == nullptr)
-    hipLaunchKernelGGL(conv_c64_kernel<3>, dim3(grid), dim3(256), 0, st, p);
-  else if (in_kernel)
-    hipLaunchKernelGGL(conv_c64_kernel<4>, dim3(grid), dim3(256), 0, st, p);
-  else if (res == nullptr)
-    hipLaunchKernelGGL(conv_c64_kernel<1>, dim3(grid), dim3(256), 0, st, p);
-  else
-    hipLaunchKernelGGL(conv_c64_kernel<2>, dim3(grid), dim3(256), 0, st, p);
+  const int kmode = mode == CONV_FWD ? 0 : in_kernel ? (res == nullptr ? 3 : 4) : (res == nullptr ? 1 : 2);
+  const bool pf = option_get(OPT_C64_PF) != 0;
+#define DTC_C64(M_)                                                                          \
+  if (pf) hipLaunchKernelGGL((conv_c64_kernel<M_, true>), dim3(grid), dim3(256), 0, st, p); \
+  else hipLaunchKernelGGL((conv_c64_kernel<M_, false>), dim3(grid), dim3(256), 0, st, p)
+  switch (kmode) {
+    case 0: DTC_C64(0); break;
+    case 1: DTC_C64(1); break;
+    case 2: DTC_C64(2); break;
+    case 3: DTC_C64(3); break;
+    default: DTC_C64(4); break;
+  }
+#undef DTC_C64
   DTC_LAUNCH_CHECK();
   if (fuse && !in_kernel)
     return bn_bwd_reduce(out, bnb->ym, bnb->x1, bnb->mean1, bnb->invstd1, bnb->acc1, bnb->x2, bnb->mean2,

@@ -608,10 +608,16 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 // grad[k][c] (row stride ld_out, first ncols columns) = scale * sum_s slab[s][k][c] (row stride ld_in).
 // A workgroup owns 256/SG output float4s; SG lanes per output stride over the splits (independent
 // loads in flight), then combine through LDS in a fixed order (deterministic).
+struct WgOuts {
+  float* dw[DTC_WG_BATCH];
+};
 template <int SG>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K,
                                                            int ld_in, int ncols, int ld_out, float scale,
-                                                           float* __restrict__ grad, u64* ts) {
+                                                           const WgOuts outs, size_t prob_stride, u64* ts) {
+  // batched launches: blockIdx.y = problem (its own slab region and output)
+  slab += blockIdx.y * prob_stride;
+  float* __restrict__ grad = outs.dw[blockIdx.y];
   constexpr int OPB = 256 / SG;  // outputs (float4) per block
   __shared__ f32x4 red[256];
   const size_t plane = (size_t)K * ld_in;
@@ -833,6 +839,26 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
   return bnb_after(bnb, dx, p.M, s.C, st);
 }
 
+static int launch_wgrad_reduce(const float* slab, int splits, int K, int RSC, int ncols, int ldo, float scale,
+                               const WgOuts& outs, int nprob, size_t prob_stride, hipStream_t st, u64* ts) {
+  const size_t nv = (size_t)K * RSC / 4;
+  int sg = 1;
+  while (sg < 16 && sg * 2 <= splits && (nv * sg * nprob) / 256 < 1024) sg *= 2;
+  const dim3 grid((unsigned)((nv + (256 / sg) - 1) / (256 / sg)), nprob);
+#define DTC_WR(SG_) \
+  hipLaunchKernelGGL(wgrad_reduce_kernel<SG_>, grid, dim3(256), 0, st, slab, splits, K, RSC, ncols, ldo, scale, outs, prob_stride, ts)
+  switch (sg) {
+    case 1: DTC_WR(1); break;
+    case 2: DTC_WR(2); break;
+    case 4: DTC_WR(4); break;
+    case 8: DTC_WR(8); break;
+    default: DTC_WR(16); break;
+  }
+#undef DTC_WR
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
                float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
   IGemmParams p{};
@@ -854,7 +880,7 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
   }
   int splits = pl.splits;
   if (pl.bm == 576 && slab_bytes >= pl.slab_bytes) {
-    DTC_TRY(conv_wgrad_halo(s, x, dy, slab, pl.splits, &splits, st, ts));
+    DTC_TRY(conv_wgrad_halo(s, 1, &x, &dy, slab, pl.splits, &splits, st, ts));
   } else {
     if (pl.bm == 576) pl = ConvPlan{64, 64, 1, ceil_div(p.M, 64), 0};  // workspace too small for the halo plan
     p.num_kt = pl.num_kt;
@@ -868,19 +894,26 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
   }
   const int ncols = dw_cols > 0 ? dw_cols : p.RSC;
   const int ldo = dw_ld > 0 ? dw_ld : p.RSC;
-  const size_t nv = (size_t)s.K * p.RSC / 4;
-  int sg = 1;
-  while (sg < 16 && sg * 2 <= splits && (nv * sg) / 256 < 1024) sg *= 2;
-  const int blocks = (int)((nv + (256 / sg) - 1) / (256 / sg));
-  switch (sg) {
-    case 1: hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw, ts); break;
-    case 2: hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw, ts); break;
-    case 4: hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw, ts); break;
-    case 8: hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw, ts); break;
-    default: hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(blocks), dim3(256), 0, st, slab, splits, s.K, p.RSC, ncols, ldo, scale, dw, ts); break;
-  }
-  DTC_LAUNCH_CHECK();
-  return 0;
+  WgOuts outs{};
+  outs.dw[0] = dw;
+  return launch_wgrad_reduce(slab, splits, s.K, p.RSC, ncols, ldo, scale, outs, 1, 0, st, ts);
+}
+
+size_t conv_wgrad_batch_slab_bytes(const ConvShape& s, int nprob) {
+  return (size_t)nprob * wgrad_halo_splits(s, nprob) * s.K * s.R * s.S * s.C * 4;
+}
+
+int conv_wgrad_batch(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* const* dw,
+                     float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
+  const int hs = wgrad_halo_splits(s, nprob);
+  if (hs <= 0 || slab == nullptr || slab_bytes < conv_wgrad_batch_slab_bytes(s, nprob))
+    return set_error(DTC_EINVAL, "conv_wgrad_batch: no halo plan for %d problems or slab too small", nprob);
+  int splits = hs;
+  DTC_TRY(conv_wgrad_halo(s, nprob, x, dy, slab, hs, &splits, st, ts));
+  const int RSC = s.R * s.S * s.C;
+  WgOuts outs{};
+  for (int i = 0; i < nprob; ++i) outs.dw[i] = dw[i];
+  return launch_wgrad_reduce(slab, splits, s.K, RSC, RSC, RSC, scale, outs, nprob, (size_t)splits * s.K * RSC, st, ts);
 }
 
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,

@@ -32,6 +32,8 @@ enum {
   OPT_HALO_WSTAGES = 14,   // weight ring depth of conv_halo (2 or 3)
   OPT_WGRAD_DIAG = 15,     // diagnostics only: 1 = wgrad_halo skips its slab stores (WRONG results)
   OPT_WGRAD_PF = 16,       // wgrad_halo LDS fragment prefetch window (0 = compiler-scheduled, 5, 8)
+  OPT_C64_PF = 17,         // conv_c64: 1 = next (tap, k-step) fragments read before this group's MFMAs
+  OPT_WGRAD_BATCH = 18,    // executor: up to this many 3x3 stride-1 weight gradients of a bucket per launch
   OPT_COUNT
 };
 int option_get(int id);
@@ -68,10 +70,18 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
                float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 // Halo-tiled WGRAD for 3x3 / stride 1 / pad 1 (wgrad_halo.hip): split count it would use for s
-// (0 = not applicable / disabled), and the launch writing slab[used][K][9C] (reduce separately).
-int wgrad_halo_splits(const ConvShape& s);
-int conv_wgrad_halo(const ConvShape& s, const u16* x, const u16* dy, float* slab, int splits, int* used_splits,
-                    hipStream_t st, u64* ts);
+// batched nprob at a time (0 = not applicable / disabled), and the launch writing
+// slab[nprob][used][K][9C] (reduce separately).
+constexpr int DTC_WG_BATCH = 4;
+int wgrad_halo_splits(const ConvShape& s, int nprob = 1);
+int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* slab, int splits,
+                    int* used_splits, hipStream_t st, u64* ts);
+// nprob (<= DTC_WG_BATCH) independent weight gradients of one 3x3 stride-1 geometry in one halo
+// launch + one reduce launch: dw[i] = scale * wgrad(x[i], dy[i]). Returns DTC_EINVAL when the
+// geometry has no halo plan or the slab is too small (callers then issue them one by one).
+size_t conv_wgrad_batch_slab_bytes(const ConvShape& s, int nprob);
+int conv_wgrad_batch(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* const* dw,
+                     float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 // Halo-tiled 3x3 / stride 1 FWD and DGRAD (conv_halo.hip): configuration for the pass (-1: not
 // applicable), and the launch (FWD: stats optional; DGRAD: res optional).
 // Persistent 64-channel 3x3 stride-1 FWD / DGRAD (conv_c64.hip).

@@ -333,6 +333,11 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
     consider(b.c1.s);
     consider(b.c2.s);
     if (b.proj) consider(b.sc.s);
+    if (!n.f32)
+      for (int np = 2; np <= DTC_WG_BATCH; ++np) {
+        slab = std::max(slab, conv_wgrad_batch_slab_bytes(b.c1.s, np));
+        slab = std::max(slab, conv_wgrad_batch_slab_bytes(b.c2.s, np));
+      }
   }
   n.slab_bytes = slab;
   n.SLAB = take(slab);
@@ -847,6 +852,57 @@ static BnbArgs bnb_of(Net& n, size_t y, size_t x1, BNL& b1, size_t x2 = 0, BNL* 
   return a;
 }
 
+// Deferred 3x3 stride-1 weight gradients (option wgrad_batch): every wgrad of the halo geometry is
+// queued and issued together with the others of its geometry -- at most wgrad_batch per launch --
+// when the geometry changes, before a DDP bucket that needs them is all-reduced, and at the end of
+// backward. The inputs stay valid while queued (per-block conv-output gradient buffers, forward
+// activations). One batched launch of P problems writes the split-K slab of ONE (conv_wgrad_batch).
+struct WgQueue {
+  ConvShape s{};
+  int count = 0;
+  const u16* x[DTC_WG_BATCH] = {};
+  const u16* dy[DTC_WG_BATCH] = {};
+  float* dw[DTC_WG_BATCH] = {};
+};
+static int wgrad_batch_max() { return std::min(std::max(option_get(OPT_WGRAD_BATCH), 1), DTC_WG_BATCH); }
+static bool same_shape(const ConvShape& a, const ConvShape& b) {
+  return a.N == b.N && a.H == b.H && a.W == b.W && a.C == b.C && a.K == b.K && a.R == b.R && a.S == b.S &&
+         a.stride == b.stride && a.pad == b.pad;
+}
+static int wg_flush(Net& n, WgQueue& q, float gs, float* slabw, hipStream_t sd) {
+  if (q.count == 0) return 0;
+  const int np = q.count;
+  q.count = 0;
+  if (np == 1) {
+    PROF(2, conv_flops(q.s), conv_wgrad(q.s, q.x[0], q.dy[0], q.dw[0], 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+    return 0;
+  }
+  PROF(2, conv_flops(q.s) * np, conv_wgrad_batch(q.s, np, q.x, q.dy, q.dw, gs, slabw, n.slab_bytes, sd, ts));
+  return 0;
+}
+static int wg_issue(Net& n, WgQueue& q, const ConvShape& s, const u16* x, const u16* dy, float* dw, float gs,
+                    float* slabw, hipStream_t sd) {
+  const int bmax = wgrad_batch_max();
+  if (bmax <= 1 || wgrad_halo_splits(s, 2) <= 0) {
+    PROF(2, conv_flops(s), conv_wgrad(s, x, dy, dw, 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+    return 0;
+  }
+  if (q.count > 0 && !same_shape(q.s, s)) DTC_TRY(wg_flush(n, q, gs, slabw, sd));
+  q.s = s;
+  q.x[q.count] = x;
+  q.dy[q.count] = dy;
+  q.dw[q.count] = dw;
+  if (++q.count >= bmax) DTC_TRY(wg_flush(n, q, gs, slabw, sd));
+  return 0;
+}
+// (the plan's bucket points, with or without a communicator: the batches -- and so the split-K
+// summation order -- are the same whether or not the gradients are all-reduced)
+static bool bucket_fires(const Net& n, int after_block) {
+  for (int a : n.bucket_after_block)
+    if (a == after_block) return true;
+  return false;
+}
+
 static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& cx, hipStream_t st) {
   if (n.f32) return backward_body_f32(n, dlogits, gs, cx, st);
   n.prof_next = Net::PROF_BWD0;
@@ -864,6 +920,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   // (captures keep the unfused order: they record dy and dz separately)
   const bool fuse = !n.capture;
   bool dz_ready = false;  // G[0] already holds the next BN's dz (the previous dgrad's fused epilogue)
+  WgQueue wq;
   for (int bi = (int)n.blocks.size() - 1; bi >= 0; --bi) {
     BlockL& b = n.blocks[bi];
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
@@ -889,7 +946,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
     if (b.proj) DTC_TRY(cap(n, cp + ".ds", dsc, st));
     // conv2: dW2 (side stream) and da1
     DTC_TRY(fork_side(n, st, &sd));
-    PROF(2, conv_flops(b.c2.s), conv_wgrad(b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+    DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd));
     // a1 = relu(bn1(c1)): da1 -> dz1 (fused into the dgrad, or a separate reduction)
     {
       const BnbArgs bz = bnb_of(n, b.A1, b.C1, b.b1);
@@ -907,7 +964,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
     DTC_TRY(cap(n, cp + ".dc1", dc1, st));
     // conv1 (+ shortcut): weight grads (side stream), then the block-input gradient with the residual fused
     DTC_TRY(fork_side(n, st, &sd));
-    PROF(2, conv_flops(b.c1.s), conv_wgrad(b.c1.s, in, dc1, n.gf(b.c1.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+    DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd));
     // the block input's gradient feeds the previous block's bn2 (+ its projection BN) or the stem BN
     BnbArgs bp;
     if (bi > 0) {
@@ -927,6 +984,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
     dz_ready = fuse;
     if (b.proj) DTC_TRY(cap(n, cp + ".dxs", G[5], st));
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
+    if (bucket_fires(n, bi)) DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
     DTC_TRY(maybe_bucket(n, bi, cx, st));
   }
   // stem: a0 = relu(bn1(conv1(x)))
@@ -942,6 +1000,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   DTC_TRY(bn_bwd_coef_apply(n, n.bn0, dz0, n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st));
   DTC_TRY(cap(n, "grad.stem.dz", dz0, st));
   DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
+  DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
   DTC_TRY(join_side(n, st));  // the stem wgrad is the last kernel: run it on the main stream
   PROF(2, 2.0 * M0 * 64 * 27,
        conv_wgrad(n.stem.s, n.at<u16>(n.X0), dc0, n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st, ts));

@@ -16,6 +16,10 @@
 // 8 waves: 4 along the 576 rows (9 fragments each) x 2 along the 64 output channels.
 // Pixel steps are split across workgroups; each writes an fp32 slab [split][K][RSC] that the
 // shared deterministic wgrad_reduce kernel (igemm.hip) sums and scales.
+// Batched launches (blockIdx.z = problem): up to DTC_WG_BATCH independent weight gradients of one
+// geometry (the executor defers the 3x3 wgrads of a bucket and issues them together). The chip is
+// filled by problems x splits workgroups, so each problem needs 1/P of the splits: the fp32 slab
+// written and re-read per conv -- the cost that bounds this kernel beside the MFMAs -- drops P-fold.
 #include "common.h"
 #include "kernels.h"
 #include "tile_common.h"
@@ -23,9 +27,10 @@
 namespace dtc {
 
 struct HaloParams {
-  const u16* x;    // NHWC [N][H][W][C]
-  const u16* dy;   // NPQK [N][H][W][K] (stride 1, pad 1: P = H, Q = W)
-  float* slab;     // [splits][K][9*C]
+  const u16* xs[DTC_WG_BATCH];   // per problem: NHWC [N][H][W][C]
+  const u16* dys[DTC_WG_BATCH];  // per problem: NPQK [N][H][W][K] (stride 1, pad 1: P = H, Q = W)
+  float* slab;     // [problem][splits][K][9*C]
+  size_t slab_stride;  // floats per problem
   int N, H, W, C, K;
   uint32_t x_bytes;
   FastDiv fd_hw, fd_w;
@@ -36,6 +41,13 @@ struct HaloParams {
   int diag;        // diagnostics only: 2 = no halo DMA after the first stage, 3 = no dy DMA after it
   u64* ts;
 };
+
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* ptr) {
+  const uint64_t v = (uint64_t)(uintptr_t)ptr;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
 
 // LDS per pipeline stage: the halo (NR DMA rounds of 64 rows of 128 B) + the dy tile (64 pixels x 64
 // channels). NS stages form a ring; NS - 1 of them are in flight while one is computed.
@@ -74,6 +86,11 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   const int ktiles = p.K >> 6;
   const int c0 = (blockIdx.x / ktiles) * 64, k0 = (blockIdx.x % ktiles) * 64;
   const int split = blockIdx.y;
+  // problem pointers as scalar selects (a dynamically indexed kernarg array would land in VGPRs, and
+  // the LDS-DMA buffer descriptor must be scalar)
+  const unsigned z = blockIdx.z;
+  const u16* const px = uniform_ptr(z == 0 ? p.xs[0] : z == 1 ? p.xs[1] : z == 2 ? p.xs[2] : p.xs[3]);
+  const u16* const pdy = uniform_ptr(z == 0 ? p.dys[0] : z == 1 ? p.dys[1] : z == 2 ? p.dys[2] : p.dys[3]);
   const int st_begin = split * p.steps_per_split;
   const int st_end = min(p.nsteps, st_begin + p.steps_per_split);
   const int W2 = p.W + 2;
@@ -105,10 +122,10 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
 #pragma unroll
       for (int j = 0; j < NR; ++j) {
         const bool ok = hcol[j] && (unsigned)(p0 + hrow_in[j]) < (unsigned)p.H;
-        buf_lds16(p.x, p.x_bytes, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)(base + hrel[j]) : 0x80000000u);
+        buf_lds16(px, p.x_bytes, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)(base + hrel[j]) : 0x80000000u);
       }
     }
-    if (p.diag != 3 || first) glds16(p.dy + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + wave * 1024);
+    if (p.diag != 3 || first) glds16(pdy + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + wave * 1024);
   };
 
   // ---- per-lane halo rows of the pixels this lane reads: t = ks*32 + 8*(lane>>4) + (lane&15)/4 (+4)
@@ -243,7 +260,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     return;
   }
   const int RSC = 9 * p.C;
-  float* slab = p.slab + (size_t)split * p.K * RSC;
+  float* slab = p.slab + blockIdx.z * p.slab_stride + (size_t)split * p.K * RSC;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int row = wm * 144 + i * 16 + 4 * (lane >> 4);
@@ -276,23 +293,28 @@ static bool halo_geometry(const ConvShape& s, int& rs, int& imgs) {
   return nh <= 192 && ((int64_t)s.N * hw) % 64 == 0 && (uint64_t)s.N * hw * s.C * 2 < (1ull << 31);
 }
 
-int wgrad_halo_splits(const ConvShape& s) {
+int wgrad_halo_splits(const ConvShape& s, int nprob) {
   const int target = option_get(OPT_WGRAD_HALO);
   int rs = 0, imgs = 0;
-  if (target <= 0 || !halo_geometry(s, rs, imgs)) return 0;
+  if (target <= 0 || nprob < 1 || nprob > DTC_WG_BATCH || !halo_geometry(s, rs, imgs)) return 0;
   const int tiles = (s.C / 64) * (s.K / 64);
   const int nsteps = s.N * s.H * s.W / 64;
-  int splits = std::max(1, target / tiles);
+  int splits = std::max(1, target / (tiles * nprob));
   splits = std::min(splits, std::max(1, nsteps / 4));  // >= 4 pixel steps per workgroup
   return splits;
 }
 
-int conv_wgrad_halo(const ConvShape& s, const u16* x, const u16* dy, float* slab, int splits, int* used_splits,
-                    hipStream_t st, u64* ts) {
+int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* slab, int splits,
+                    int* used_splits, hipStream_t st, u64* ts) {
   int rs = 0, imgs = 0;
-  DTC_CHECK_ARG(halo_geometry(s, rs, imgs) && splits > 0, "wgrad_halo: unsupported geometry");
+  DTC_CHECK_ARG(halo_geometry(s, rs, imgs) && splits > 0 && nprob >= 1 && nprob <= DTC_WG_BATCH,
+                "wgrad_halo: unsupported geometry");
   HaloParams p{};
-  p.x = x; p.dy = dy; p.slab = slab;
+  for (int i = 0; i < nprob; ++i) {
+    p.xs[i] = x[i];
+    p.dys[i] = dy[i];
+  }
+  p.slab = slab;
   p.N = s.N; p.H = s.H; p.W = s.W; p.C = s.C; p.K = s.K;
   p.x_bytes = (uint32_t)((uint64_t)s.N * s.H * s.W * s.C * 2);
   p.fd_hw = make_fastdiv(s.H * s.W);
@@ -307,7 +329,8 @@ int conv_wgrad_halo(const ConvShape& s, const u16* x, const u16* dy, float* slab
   p.nostore = option_get(OPT_WGRAD_DIAG) == 1;
   p.diag = option_get(OPT_WGRAD_DIAG);
   const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
-  dim3 grid((s.C / 64) * (s.K / 64), used);
+  p.slab_stride = (size_t)used * s.K * 9 * s.C;
+  dim3 grid((s.C / 64) * (s.K / 64), used, nprob);
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
   const bool deep = option_get(OPT_WGRAD_STAGES) >= 4;
   const int pf = option_get(OPT_WGRAD_PF);

@@ -87,6 +87,25 @@ def conv2d_wgrad(x, dy, r, s, stride, pad, scale=1.0):
     return dw
 
 
+def conv2d_wgrad_batch(xs, dys, scale=1.0):
+    """n (<= 4) same-shape 3x3 stride-1 weight gradients in one launch (dtc_conv2d_wgrad_batch):
+    xs[i] [N,H,W,C] bf16, dys[i] [N,H,W,K] bf16 -> list of dw [K,3,3,C] fp32 (scaled)."""
+    require_cuda(*xs, *dys)
+    n = len(xs)
+    N, H, W, Cc = xs[0].shape
+    K = dys[0].shape[3]
+    d = conv_desc(N, H, W, Cc, K, 3, 3, 1, 1)
+    nb = lib.dtc_conv2d_wgrad_batch_workspace_size(d, n)
+    if nb == 0:
+        raise ValueError(f"conv2d_wgrad_batch: no batched halo plan for {(N, H, W, Cc, K)} x {n}")
+    ws = torch.empty(nb // 4 + 64, dtype=torch.float32, device=xs[0].device)
+    dws = [torch.empty(K, 3, 3, Cc, dtype=torch.float32, device=xs[0].device) for _ in range(n)]
+    arr = C.c_void_p * n
+    call("dtc_conv2d_wgrad_batch", d, n, arr(*[ptr(t) for t in xs]), arr(*[ptr(t) for t in dys]),
+         arr(*[ptr(t) for t in dws]), float(scale), ptr(ws), nb, stream_ptr())
+    return dws
+
+
 def new_stats(c, device):
     return torch.zeros(STAT_SLOTS, 2, c, dtype=torch.float64, device=device)
 

@@ -76,6 +76,15 @@ int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16
 /* dw[k][r][s][c] (fp32) = scale * sum over pixels of dy (x) im2col(x): the weight gradient */
 int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* dw, float scale,
                      void* ws, size_t ws_bytes, void* stream);
+/* n (1..4) independent weight gradients of one 3x3 / stride-1 / pad-1 geometry (64-multiple
+ * channels) in one halo launch + one reduce launch: dw[i] = scale * wgrad(x[i], dy[i]). The chip is
+ * filled by n x splits workgroups, so each gradient's fp32 split-K slab is 1/n the size of a single
+ * dtc_conv2d_wgrad's. Replaces the weight-gradient halves of n `nn.Conv2d` backward passes
+ * (net.py:18-24, 29-35) that autograd would run one by one. Workspace: ..._batch_workspace_size
+ * (0 = no halo plan for this geometry: use dtc_conv2d_wgrad per problem). */
+size_t dtc_conv2d_wgrad_batch_workspace_size(const dtc_conv_desc* d, int n);
+int dtc_conv2d_wgrad_batch(const dtc_conv_desc* d, int n, const uint16_t* const* x, const uint16_t* const* dy,
+                           float* const* dw, float scale, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------ batch norm (training)
  * Replaces nn.BatchNorm2d train-mode forward/backward (net.py:21,25,37,92) with the F.relu and

@@ -296,6 +296,38 @@ def test_conv_wgrad_halo(dtc, cuda, case):
     assert rel_err(generic, ref) < 1e-5
 
 
+@pytest.mark.parametrize("case", [
+    (4, 32, 32, 64, 64, 4),    # layer1 geometry, the executor's four-conv batch (64 splits each)
+    (4, 32, 32, 64, 64, 2),
+    (8, 16, 16, 128, 128, 3),  # 2x2 output tiles, three problems
+    (12, 4, 4, 512, 512, 4),   # multi-image halo, one split per problem
+    (3, 8, 8, 64, 128, 2),     # ragged split of 3 steps
+])
+def test_conv_wgrad_batch(dtc, cuda, case):
+    """dtc_conv2d_wgrad_batch: n independent weight gradients in one halo launch (blockIdx.z =
+    problem, 1/n of the splits each) + one reduce launch == the oracle per problem, and == the
+    one-by-one dtc_conv2d_wgrad to fp32 summation order (different split counts)."""
+    N, H, W, C, K, n = case
+    g = np.random.default_rng(11)
+    xs = [_rand_bf16((N, H, W, C), g) for _ in range(n)]
+    dys = [_rand_bf16((N, H, W, K), g) for _ in range(n)]
+    xd = [_to_dev_bf16(a, cuda) for a in xs]
+    dyd = [_to_dev_bf16(a, cuda) for a in dys]
+    got = dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.25)
+    assert len(got) == n
+    for i in range(n):
+        ref = 0.25 * O.conv2d_wgrad(xs[i], dys[i], 3, 3, 1, 1)
+        one = dtc.ops.conv2d_wgrad(xd[i], dyd[i], 3, 3, 1, 1, scale=0.25).cpu().numpy()
+        assert rel_err(got[i].cpu().numpy(), ref) < 1e-5, i
+        assert rel_err(got[i].cpu().numpy(), one) < 1e-6, i
+
+
+def test_conv_wgrad_batch_rejects_non_halo(dtc, cuda):
+    """No batched plan for a stride-2 geometry: workspace size 0 and a clean error, no launch."""
+    d = dtc.ops.conv_desc(8, 16, 16, 64, 128, 3, 3, 2, 1)
+    assert dtc._native.lib.dtc_conv2d_wgrad_batch_workspace_size(d, 2) == 0
+
+
 HALO_CASES = [
     # (N, H, W, C, K): 3x3 stride-1 convs for every halo configuration (conv_halo.hip)
     (2, 32, 32, 64, 64),

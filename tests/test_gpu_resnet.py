@@ -408,6 +408,41 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
         assert rel_err(ba[k], bb[k]) < 1e-4, k
 
 
+def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5):
+    dtc._native.lib.dtc_set_option(b"graphs", int(graphs))
+    try:
+        model, _, x, y = _setup(dtc, cuda, batch, seed=seed)
+        crit = dtc.CrossEntropyLoss()
+        xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
+        out = []
+        for _ in range(reps):  # graphs: capture, then replay
+            loss = crit(model(xd), yd)
+            loss.backward()
+            out.append(_np(model.flat.grads).copy())
+        return out
+    finally:
+        dtc._native.lib.dtc_set_option(b"graphs", 1)
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_wgrad_batch_matches_unbatched(dtc, cuda, graphs):
+    """Deferred, batched 3x3 weight gradients (option wgrad_batch=4, default: one halo launch per
+    geometry within a DDP bucket, 1/P of the split-K slab each) vs one launch per conv, on the same
+    parameters and batch (capture and replay): only the fp32 split-K summation order differs."""
+    ga = _grads_repeated(dtc, cuda, graphs)
+    dtc._native.lib.dtc_set_option(b"wgrad_batch", 1)
+    try:
+        gb = _grads_repeated(dtc, cuda, graphs)
+    finally:
+        dtc._native.lib.dtc_set_option(b"wgrad_batch", 4)
+    lay = dtc.nn.Layout(100, 25.0)
+    for rep in range(2):
+        for pe in lay.params:
+            a = ga[rep][pe.offset:pe.offset + pe.numel]
+            b = gb[rep][pe.offset:pe.offset + pe.numel]
+            assert rel_err(a, b) < 1e-5, (rep, pe.name, rel_err(a, b))
+
+
 def test_graph_recapture_on_option_change(dtc, cuda):
     """Options are baked into captured launches: changing one re-captures (results unchanged)."""
     model, _, x, y = _setup(dtc, cuda, 4, seed=6)
