@@ -207,6 +207,7 @@ def main():
     ap.add_argument("--size", type=int, default=32)
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--no-barrier", action="store_true", help="drop the reference's per-step dist.barrier()")
+    ap.add_argument("--torch-barrier", action="store_true", help="per-step barrier via torch.distributed (A/B)")
     ap.add_argument("--no-item", action="store_true", help="drop the per-step loss.item() host sync")
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="bound on the timed CPU-baseline steps")
     ap.add_argument("--cpu-steps", type=int, default=50, help="CPU baseline: median over this many steps")
@@ -260,7 +261,10 @@ def main():
             logit = model(img)
             loss = crit(logit, label)
         if not args.no_barrier:
-            dist.barrier()
+            if args.torch_barrier:
+                dist.barrier()
+            else:
+                dtc.barrier()  # the reference's dist.barrier() (trainer.py:156) on the native communicator
         scaler.scale(loss).backward()
         scaler.step(opt)
         scaler.update()
@@ -292,6 +296,10 @@ def main():
     prof_elapsed = None
     if not args.no_live_roofline:
         exe = model.module.executor(B, S, S, "bf16")
+        # kernel efficiency: the weight gradients back on the compute stream, so every conv launch
+        # has the chip to itself (region 1 overlaps them with the dgrad / BN chain on a side stream)
+        bwd_streams = int(dtc._native.lib.dtc_get_option(b"bwd_streams"))
+        dtc._native.call("dtc_set_option", b"bwd_streams", 0)
         dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
         for i in range(2):
             step(args.warmup + args.steps + i)
@@ -299,6 +307,7 @@ def main():
         dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
         prof_elapsed = timed(args.steps, args.warmup + args.steps + 2)
         dtc._native.call("dtc_rn18_profile_end", exe.handle, ms, fl, cnt)
+        dtc._native.call("dtc_set_option", b"bwd_streams", bwd_streams)
 
     # C4 all-reduce bus bandwidth on the Reducer's own RCCL communicator: the full gradient
     # (11,220,132 fp32) and the bucket-size sweep of BASELINE config 5 (N > 1 only: one rank has
@@ -360,7 +369,9 @@ def main():
                 "kernel": "implicit-GEMM conv (fwd+dgrad+wgrad incl. split-K reduce), all launches in the timed "
                           "region; per-call duration = last workgroup end - first workgroup start (s_memrealtime, "
                           "stamped by the kernels on the compute stream); measured over a second timed region of "
-                          "the same K steps with the stamps armed (region_ms_per_step), value from the first",
+                          "the same K steps with the stamps armed (region_ms_per_step) and the weight gradients on "
+                          "the compute stream (bwd_streams=0: each launch has the chip to itself), value from the "
+                          "first (weight gradients overlapped on a side stream)",
                 "traffic_unit": "HBM bytes per conv call (PMC, profiles/*conv_traffic.json)",
                 "conv_ms_per_step": round(conv_ms / args.steps, 4),
                 "region_ms_per_step": round(prof_elapsed / args.steps * 1e3, 4) if prof_elapsed else None,

@@ -15,7 +15,7 @@ from . import data, ops  # noqa: F401
 from .amp import GradScaler, autocast  # noqa: F401
 from .nn import BasicBlock, CrossEntropyLoss, ResNet, ResNet18, SyncBatchNorm  # noqa: F401
 from .optim import SGD  # noqa: F401
-from .parallel import DDP, Comm, DataParallel, DistributedDataParallel  # noqa: F401
+from .parallel import DDP, Comm, DataParallel, DistributedDataParallel, barrier  # noqa: F401
 from . import parallel  # noqa: F401
 from . import trainer  # noqa: F401
 

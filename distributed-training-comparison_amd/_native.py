@@ -87,6 +87,7 @@ _SIGS = {
     "dtc_comm_allreduce_sum": (i32, [vp, vp, sz, i32, vp]),
     "dtc_comm_broadcast": (i32, [vp, vp, sz, i32, i32, vp]),
     "dtc_comm_destroy": (i32, [vp]),
+    "dtc_barrier": (i32, [vp, vp]),
     "dtc_comm_init_loopback": (i32, [C.POINTER(vp), i32, i32, C.c_float]),
     "dtc_comm_log_size": (i32, [vp]),
     "dtc_comm_log_entry": (i32, [vp, i32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(i32)]),

@@ -262,10 +262,13 @@ __device__ __forceinline__ void fa_fwd_coef(const BnFwdArgs& A, int C, int cg, d
   __syncthreads();
 }
 
+// mask (optional): the ReLU mask of y, one bit per element (byte o/8 of element offset o, bit k =
+// channel c0 + k): the backward reads it instead of y (0.125 B instead of 2 B per element).
 template <int MODE, typename T>
 __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const T* __restrict__ x, const BnFwdArgs a1,
                                                           const T* __restrict__ x2, const BnFwdArgs a2,
-                                                          T* __restrict__ y, int64_t M, int C, int rows) {
+                                                          T* __restrict__ y, int64_t M, int C, int rows,
+                                                          uint8_t* __restrict__ mask) {
   typedef Elt<T> E;
   __shared__ double part[4 * 2 * 64];
   __shared__ float coef[4][64];  // scale1, shift1, scale2, shift2
@@ -313,7 +316,9 @@ __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const T* __restrict__
         if constexpr (MODE == APPLY_DUAL_RELU) v[k] = E::round(v[k]) + E::round(r[k] * sc2[k] + sh2[k]);
         v[k] = fmaxf(v[k], 0.f);
       }
-      E::st(y + o, E::pack(v));
+      const typename E::V pk = E::pack(v);
+      E::st(y + o, pk);
+      if (mask != nullptr) mask[o >> 3] = (uint8_t)E::mask8(pk);
     }
   }
 }
@@ -330,7 +335,7 @@ static void fa_grid(int64_t M, int C, int& nblk, int& rows) {
 
 template <typename T>
 static int fin_apply(int mode, const T* x, const BnFwdArgs& a1, const T* x2, const BnFwdArgs* a2, T* y, int64_t M,
-                     int C, hipStream_t st) {
+                     int C, hipStream_t st, uint8_t* mask) {
   DTC_CHECK_ARG(x && y && a1.stats && a1.gamma && a1.beta && a1.mean && a1.invstd && C % FA_GROUP == 0 && M > 0,
                 "bn_fin_apply: bad args (C=%d)", C);
   int nblk, rows;
@@ -339,15 +344,15 @@ static int fin_apply(int mode, const T* x, const BnFwdArgs& a1, const T* x2, con
   const BnFwdArgs none{};
   switch (mode) {
     case APPLY_RELU:
-      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows);
+      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows, mask);
       break;
     case APPLY_ADD_RELU:
       DTC_CHECK_ARG(x2 != nullptr, "bn_fin_apply: residual required");
-      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_ADD_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows);
+      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_ADD_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows, mask);
       break;
     default:
       DTC_CHECK_ARG(x2 && a2 && a2->stats, "bn_fin_apply: second branch required");
-      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_DUAL_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, *a2, y, M, C, rows);
+      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_DUAL_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, *a2, y, M, C, rows, mask);
       break;
   }
   DTC_LAUNCH_CHECK();
@@ -355,12 +360,12 @@ static int fin_apply(int mode, const T* x, const BnFwdArgs& a1, const T* x2, con
 }
 
 int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, const BnFwdArgs* a2, u16* y, int64_t M,
-                 int C, hipStream_t st) {
-  return fin_apply<u16>(mode, x, a1, x2, a2, y, M, C, st);
+                 int C, hipStream_t st, uint8_t* mask) {
+  return fin_apply<u16>(mode, x, a1, x2, a2, y, M, C, st, mask);
 }
 int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2, const BnFwdArgs* a2, float* y,
                  int64_t M, int C, hipStream_t st) {
-  return fin_apply<float>(mode, x, a1, x2, a2, y, M, C, st);
+  return fin_apply<float>(mode, x, a1, x2, a2, y, M, C, st, nullptr);
 }
 
 // ------------------------------------------------------------------ fused finalize + apply (backward)
@@ -388,11 +393,15 @@ __device__ __forceinline__ void fa_bwd_coef(const BnBwdArgs& A, int C, int cg, d
   __syncthreads();
 }
 
-template <bool DUAL, typename T>
+// MB: dz is formed here from the raw gradient (`dz` = dy) and the forward's ReLU mask bits
+// (dz = dy * [y > 0]; exact), and optionally stored to dzo (may alias dy: each element is read and
+// written by the same lane) for a consumer that needs it (the identity shortcut's residual).
+template <bool DUAL, bool MB, typename T>
 __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restrict__ dz, const T* __restrict__ x1,
                                                               const BnBwdArgs a1, T* __restrict__ dx1,
                                                               const T* __restrict__ x2, const BnBwdArgs a2,
-                                                              T* __restrict__ dx2, int64_t M, int C, int rows) {
+                                                              T* __restrict__ dx2, int64_t M, int C, int rows,
+                                                              const uint8_t* __restrict__ mbits, T* dzo) {
   typedef Elt<T> E;
   __shared__ double part[4 * 2 * 64];
   __shared__ float coef[6][64];
@@ -411,6 +420,7 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restri
   const int64_t m0 = (int64_t)blockIdx.x * rows, m1 = std::min<int64_t>(M, m0 + rows);
   for (int64_t mb = m0 + pr; mb < m1; mb += 32 * FA_UNROLL) {  // loads of a trip first (see bn_fin_apply)
     typename E::V vd[FA_UNROLL], va[FA_UNROLL], vb[FA_UNROLL];
+    uint32_t mk[FA_UNROLL];
 #pragma unroll
     for (int u = 0; u < FA_UNROLL; ++u) {
       const int64_t m = mb + 32 * u;
@@ -419,6 +429,7 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restri
         vd[u] = E::ld(dz + o);
         va[u] = E::ld(x1 + o);
         if constexpr (DUAL) vb[u] = E::ld(x2 + o);
+        if constexpr (MB) mk[u] = mbits[o >> 3];
       }
     }
 #pragma unroll
@@ -428,6 +439,11 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restri
       const int64_t o = m * C + cg + q8;
       float d[8], a[8], v[8];
       E::unpack(vd[u], d);
+      if constexpr (MB) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = (mk[u] >> k) & 1u ? d[k] : 0.f;
+        if (dzo != nullptr) E::st(dzo + o, E::pack(d));  // exact: masking is exact
+      }
       E::unpack(va[u], a);
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = A1[k] * d[k] + B1[k] * a[k] + C1[k];
@@ -444,23 +460,31 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restri
 
 template <typename T>
 static int bwd_fin_apply(const T* dz, const T* x1, const BnBwdArgs& a1, T* dx1, const T* x2, const BnBwdArgs* a2,
-                         T* dx2, int64_t M, int C, hipStream_t st) {
+                         T* dx2, int64_t M, int C, hipStream_t st, const uint8_t* mbits = nullptr, T* dzo = nullptr) {
   DTC_CHECK_ARG(dz && x1 && dx1 && a1.acc && a1.gamma && a1.mean && a1.invstd && C % FA_GROUP == 0 && M > 0,
                 "bn_bwd_fin_apply: bad args (C=%d)", C);
+  DTC_CHECK_ARG(mbits || !dzo, "bn_bwd_fin_apply: a dz output needs the mask bits");
   int nblk, rows;
   fa_grid(M, C, nblk, rows);
   const dim3 grid(nblk, C / FA_GROUP);
-  if (x2) {
-    DTC_CHECK_ARG(a2 && a2->acc && dx2, "bn_bwd_fin_apply: dual branch args");
-    hipLaunchKernelGGL((bn_bwd_fin_apply_kernel<true, T>), grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, *a2, dx2, M, C,
-                       rows);
-  } else {
-    const BnBwdArgs none{};
-    hipLaunchKernelGGL((bn_bwd_fin_apply_kernel<false, T>), grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, none, dx2, M, C,
-                       rows);
-  }
+  const BnBwdArgs none{};
+  if (x2) DTC_CHECK_ARG(a2 && a2->acc && dx2, "bn_bwd_fin_apply: dual branch args");
+#define DTC_BFA(D_, M_) \
+  hipLaunchKernelGGL((bn_bwd_fin_apply_kernel<D_, M_, T>), grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, D_ ? *a2 : none, \
+                     dx2, M, C, rows, mbits, dzo)
+  if (x2 && mbits) DTC_BFA(true, true);
+  else if (x2) DTC_BFA(true, false);
+  else if (mbits) DTC_BFA(false, true);
+  else DTC_BFA(false, false);
+#undef DTC_BFA
   DTC_LAUNCH_CHECK();
   return 0;
+}
+
+int bn_bwd_fin_apply_mask(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
+                          const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st) {
+  DTC_CHECK_ARG(mbits != nullptr, "bn_bwd_fin_apply_mask: mask bits required");
+  return bwd_fin_apply<u16>(dy, x1, a1, dx1, x2, a2, dx2, M, C, st, mbits, dzo);
 }
 
 int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
@@ -473,12 +497,15 @@ int bn_bwd_fin_apply(const float* dz, const float* x1, const BnBwdArgs& a1, floa
 }
 
 // ------------------------------------------------------------------ backward
-template <bool MASK, bool DUAL, typename T>
+// MASK: dz = dy * [ym > 0], stored. MB: dz = dy * mask bit (the forward's ReLU mask), not stored
+// (bn_bwd_fin_apply_mask forms it again from the same bits): 4.125 B per element instead of 8.
+template <bool MASK, bool DUAL, typename T, bool MB = false>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const T* __restrict__ dy, const T* __restrict__ ym, const T* __restrict__ x1,
     const float* __restrict__ mean1, const float* __restrict__ invstd1, double* __restrict__ acc1,
     const T* __restrict__ x2, const float* __restrict__ mean2, const float* __restrict__ invstd2,
-    double* __restrict__ acc2, T* __restrict__ dz, int64_t M, int C, int rows_per_block) {
+    double* __restrict__ acc2, T* __restrict__ dz, int64_t M, int C, int rows_per_block,
+    const uint8_t* __restrict__ mbits = nullptr) {
   typedef Elt<T> E;
   __shared__ float red[256 * 24];
   const int tpr = C >> 3, rpp = 256 / tpr;
@@ -501,6 +528,11 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const int64_t o = m * C + c0;
     float d[8], a[8];
     E::unpack(E::ld(dy + o), d);
+    if constexpr (MB) {
+      const uint32_t mk = mbits[o >> 3];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = (mk >> k) & 1u ? d[k] : 0.f;
+    }
     if constexpr (MASK) {
       float yv[8];
       E::unpack(E::ld(ym + o), yv);
@@ -573,6 +605,49 @@ static int bwd_reduce(const T* dy, const T* ymask, const T* x1, const float* mea
   else
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false, T>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
                        invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+int bn_bwd_reduce_mask(const u16* dy, const uint8_t* mbits, const u16* x1, const float* mean1, const float* invstd1,
+                       double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, int64_t M,
+                       int C, hipStream_t st) {
+  DTC_CHECK_ARG(dy && mbits && x1 && mean1 && invstd1 && acc1 && C % 8 == 0 && C <= 2048 && M > 0,
+                "bn_bwd_reduce_mask: bad args");
+  const int tpr = C / 8, rpp = 256 / tpr;
+  int64_t rpb = std::max<int64_t>({(int64_t)rpp, (M + 1023) / 1024,
+                                   std::min<int64_t>((16384 + C - 1) / C, (M + 255) / 256)});
+  rpb = ((rpb + rpp - 1) / rpp) * rpp;
+  const int blocks = ceil_div_i(M, rpb);
+  if (x2) {
+    DTC_CHECK_ARG(mean2 && invstd2 && acc2, "bn_bwd_reduce_mask: dual branch args");
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, true, u16, true>), dim3(blocks), dim3(256), 0, st, dy, nullptr, x1,
+                       mean1, invstd1, acc1, x2, mean2, invstd2, acc2, nullptr, M, C, (int)rpb, mbits);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false, u16, true>), dim3(blocks), dim3(256), 0, st, dy, nullptr, x1,
+                       mean1, invstd1, acc1, x2, mean2, invstd2, acc2, nullptr, M, C, (int)rpb, mbits);
+  }
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void __launch_bounds__(256) bn_mask_apply_kernel(const u16* __restrict__ dy, const uint8_t* __restrict__ mbits,
+                                                            u16* __restrict__ dz, int64_t nvec) {
+  for (int64_t v = blockIdx.x * (int64_t)256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    float d[8];
+    unpack8(*(const uint4*)(dy + v * 8), d);
+    const uint32_t mk = mbits[v];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = (mk >> k) & 1u ? d[k] : 0.f;
+    *(uint4*)(dz + v * 8) = pack8(d);
+  }
+}
+
+int bn_mask_apply(const u16* dy, const uint8_t* mbits, u16* dz, int64_t M, int C, hipStream_t st) {
+  DTC_CHECK_ARG(dy && mbits && dz && C % 8 == 0 && M > 0, "bn_mask_apply: bad args");
+  const int64_t nvec = M * C / 8;
+  hipLaunchKernelGGL(bn_mask_apply_kernel, dim3((unsigned)std::min<int64_t>(4096, (nvec + 255) / 256)), dim3(256), 0, st,
+                     dy, mbits, dz, nvec);
   DTC_LAUNCH_CHECK();
   return 0;
 }

@@ -12,11 +12,11 @@
 #include <cstring>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {0}, {1}, {1}, {0}, {0}, {2}, {3}, {0}, {0}, {1}, {4}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {2}, {3}, {0}, {0}, {1}, {4}, {1}, {1}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
                                              "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
                                              "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse",
-                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch"};
+                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin"};
 static std::atomic<int> g_epoch{0};
 int option_get(int id) { return g_opts[id].load(std::memory_order_relaxed); }
 int option_epoch() { return g_epoch.load(std::memory_order_relaxed); }
@@ -208,6 +208,7 @@ int dtc_comm_broadcast(dtc_comm* comm, void* buf, size_t count, int dtype, int r
   return comm_broadcast((Comm*)comm, buf, count, dtype, root, S(stream));
 }
 int dtc_comm_destroy(dtc_comm* comm) { return comm_destroy((Comm*)comm); }
+int dtc_barrier(dtc_comm* comm, void* stream) { GUARD(return comm_barrier((Comm*)comm, S(stream));) }
 int dtc_comm_init_loopback(dtc_comm** out, int device, int world, float factor) {
   GUARD(return comm_init_loopback((Comm**)out, device, world, factor);)
 }

@@ -38,6 +38,7 @@ struct Comm {
   bool loopback = false;
   float factor = 1.f;
   std::vector<CommLogEntry> log;
+  float* token = nullptr;  // barrier: one float all-reduced on the side stream
 };
 
 static ncclDataType_t to_nccl(int dtype) {
@@ -110,9 +111,51 @@ static int loopback_reduce(Comm* c, void* buf, size_t count, int dtype, hipStrea
                     : scale_f64(reinterpret_cast<double*>(buf), (int64_t)count, (double)c->factor, st);
 }
 
+// Host-side wait that polls instead of sleeping in the driver: after the reference's per-step
+// barrier the GPU queue is empty, so every microsecond of wake-up latency is GPU idle time.
+static int spin_wait(hipEvent_t ev) {
+  if (option_get(OPT_BARRIER_SPIN) == 0) {
+    DTC_HIP(hipEventSynchronize(ev));
+    return 0;
+  }
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorNotReady) return set_error((int)e, "barrier: hipEventQuery: %s", hipGetErrorString(e));
+  }
+}
+
+// dist.barrier() (reference ddp/trainer.py:156): every rank's host returns only after
+// all ranks reached it AND this rank's work queued on `st` before it has finished (what torch's
+// NCCL barrier does: an all-reduce of one element, then a stream synchronize). One float is SUM
+// all-reduced on the communicator's side stream (after `st`, so every collective of this
+// communicator stays on one stream), the host polls its completion event. Without an RCCL
+// communicator (comm == NULL or a loopback test communicator) it is the stream drain (the Python
+// barrier() passes NULL at world 1: a one-rank all-reduce would only add a launch).
+int comm_barrier(Comm* c, hipStream_t st) {
+  static thread_local hipEvent_t local_ev = nullptr;
+  if (c == nullptr || c->loopback || c->nccl == nullptr) {
+    if (!local_ev) DTC_HIP(hipEventCreateWithFlags(&local_ev, hipEventDisableTiming));
+    DTC_HIP(hipEventRecord(local_ev, st));
+    return spin_wait(local_ev);
+  }
+  if (!c->token) {
+    DTC_HIP(hipMalloc(&c->token, sizeof(float)));
+    DTC_HIP(hipMemsetAsync(c->token, 0, sizeof(float), st));
+  }
+  hipEvent_t ev = c->fork[c->next_fork];
+  c->next_fork = (c->next_fork + 1) % (int)c->fork.size();
+  DTC_HIP(hipEventRecord(ev, st));
+  DTC_HIP(hipStreamWaitEvent(c->side, ev, 0));
+  DTC_NCCL(ncclAllReduce(c->token, c->token, 1, ncclFloat32, ncclSum, c->nccl, c->side));
+  DTC_HIP(hipEventRecord(c->done, c->side));
+  return spin_wait(c->done);  // anything issued after the return is ordered after it in real time
+}
+
 int comm_destroy(Comm* c) {
   if (!c) return 0;
   if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->token) (void)hipFree(c->token);
   if (c->nccl) ncclCommDestroy(c->nccl);
   for (auto& e : c->fork)
     if (e) (void)hipEventDestroy(e);

@@ -23,6 +23,8 @@ int comm_broadcast(Comm* c, void* buf, size_t count, int dtype, int root, hipStr
 int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute);
 int comm_join(Comm* c, hipStream_t compute);
 int comm_world(const Comm* c);
+// dist.barrier(): all ranks + this rank's queued work on `st`; the host polls (comm.cpp)
+int comm_barrier(Comm* c, hipStream_t st);
 // test communicator without RCCL: all-reduce = buf *= factor, logged; reports `world` ranks (comm.cpp)
 int comm_init_loopback(Comm** out, int device, int world, float factor);
 const std::vector<CommLogEntry>* comm_log(Comm* c);

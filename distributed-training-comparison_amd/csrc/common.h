@@ -83,6 +83,14 @@ struct Elt<u16> {
   static __device__ __forceinline__ float round(float x) { return round_bf(x); }
   static __device__ __forceinline__ float cvt(u16 v) { return bf2f(v); }
   static __device__ __forceinline__ u16 from(float f) { return f2bf(f); }
+  // ReLU mask of 8 packed outputs (>= 0 after the ReLU): bit k = element k > 0
+  static __device__ __forceinline__ uint32_t mask8(const V& v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t b = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) b |= (((w[k] & 0x7fffu) != 0u) ? 1u : 0u) << (2 * k) | (((w[k] & 0x7fff0000u) != 0u) ? 2u : 0u) << (2 * k);
+    return b;
+  }
 };
 struct F32x8 {
   f32x4 a, b;
@@ -105,6 +113,12 @@ struct Elt<float> {
   static __device__ __forceinline__ float round(float x) { return x; }
   static __device__ __forceinline__ float cvt(float v) { return v; }
   static __device__ __forceinline__ float from(float f) { return f; }
+  static __device__ __forceinline__ uint32_t mask8(const V& v) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) b |= (v.a[k] > 0.f ? 1u : 0u) << k | (v.b[k] > 0.f ? 1u : 0u) << (k + 4);
+    return b;
+  }
 };
 
 // ---------------------------------------------------------------- fast unsigned division

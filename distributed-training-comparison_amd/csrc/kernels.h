@@ -19,8 +19,9 @@ enum {
   OPT_WGRAD_HALO = 5,  // target workgroup count of the halo WGRAD kernel (0 = generic loader only)
   OPT_HALO_CONV = 6,   // halo FWD/DGRAD for 3x3 s1: 0 off, 1 auto, 2+k force configuration k (tuning)
   OPT_HALO_SPLIT = 7,  // halo FWD/DGRAD split-K over reduction chunks: 0 auto, k forced
-  OPT_BWD_STREAMS = 8,  // 1: weight gradients on a side stream, overlapped with the dgrad/BN chain
-                        // (off by default: measured 5% slower at B=256, both chains fill the CUs)
+  OPT_BWD_STREAMS = 8,  // 1 (default): weight gradients on a side stream, overlapped with the
+                        // dgrad/BN chain (the MFMA-bound wgrads beside the HBM-bound BN kernels:
+                        // +2% at B=256 once the wgrads were batched; 5% slower before)
   OPT_CONV_C64 = 9,     // persistent 64->64 channel 3x3 conv (conv_c64.hip) for layer1 FWD/DGRAD
   OPT_BN_FUSED_FIN = 10,  // 1: BN coefficients computed by the apply kernels (no finalize launches)
   OPT_HALO_NHB2 = 11,     // 1: prefer the double-buffered-halo conv_halo tiles where they fit 2 WG/CU
@@ -34,6 +35,8 @@ enum {
   OPT_WGRAD_PF = 16,       // wgrad_halo LDS fragment prefetch window (0 = compiler-scheduled, 5, 8)
   OPT_C64_PF = 17,         // conv_c64: 1 = next (tap, k-step) fragments read before this group's MFMAs
   OPT_WGRAD_BATCH = 18,    // executor: up to this many 3x3 stride-1 weight gradients of a bucket per launch
+  OPT_BN_MASK = 19,        // executor: 1 = ReLU mask bits from the forward BN apply drive the BN backward
+  OPT_BARRIER_SPIN = 20,   // dtc_barrier host wait: 1 = poll the completion event, 0 = hipEventSynchronize
   OPT_COUNT
 };
 int option_get(int id);
@@ -165,8 +168,18 @@ struct BnBwdArgs {
   float* dbeta = nullptr;
 };
 // mode: 1 relu, 2 add residual x2 + relu, 3 dual BN (x2 normalised by a2) + relu
+// mask (optional): ReLU mask bits of y (byte o/8 for element offset o) for the mask-bit backward
 int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, const BnFwdArgs* a2, u16* y, int64_t M,
-                 int C, hipStream_t st);
+                 int C, hipStream_t st, uint8_t* mask = nullptr);
+// Mask-bit BN backward (the executor's default): dz = dy * mask bit is formed where it is used, never
+// stored by the reduction. Reduce: sums only (dy, bits, x read: 4.125 B/element); apply: dx (and
+// dzo = dz if non-null, may alias dy) from dy, bits, x. bn_mask_apply: dz alone (parity captures).
+int bn_bwd_reduce_mask(const u16* dy, const uint8_t* mbits, const u16* x1, const float* mean1, const float* invstd1,
+                       double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, int64_t M,
+                       int C, hipStream_t st);
+int bn_bwd_fin_apply_mask(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
+                          const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st);
+int bn_mask_apply(const u16* dy, const uint8_t* mbits, u16* dz, int64_t M, int C, hipStream_t st);
 int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
                      u16* dx2, int64_t M, int C, hipStream_t st);
 int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2, const BnFwdArgs* a2, float* y,

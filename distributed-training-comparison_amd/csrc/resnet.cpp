@@ -55,6 +55,7 @@ struct BlockL {
   bool proj = false;
   int Cin = 0, Cout = 0, Hin = 0, Win = 0, Hout = 0, Wout = 0;
   size_t C1 = 0, A1 = 0, C2 = 0, S = 0, OUT = 0;  // activation buffers (workspace byte offsets)
+  size_t MA1 = 0, MOUT = 0;  // ReLU mask bits of A1 / OUT (bf16 executor, option bn_mask)
   size_t DC2 = 0, DC1 = 0, DSC = 0;  // backward: conv-output gradients read by the (side-stream) wgrads
   int64_t grad_hi = 0;  // end of this block's flat region: after its backward, [0, grad_hi) is complete
 };
@@ -76,6 +77,7 @@ struct Net {
   // workspace
   size_t ws_bytes = 0;
   size_t X0 = 0, WSTEM = 0, C0 = 0, A0 = 0, FEAT = 0, G[6] = {0, 0, 0, 0, 0, 0}, SLAB = 0;
+  size_t MA0 = 0;  // ReLU mask bits of A0
   size_t HEADWS = 0, HEADWS_bytes = 0;
   size_t DC0 = 0, SLABW = 0;  // stem conv-output gradient; split-K slab of the side-stream wgrads
   // backward weight gradients run on a side stream (option bwd_streams), overlapped with the
@@ -272,6 +274,7 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.WSTEM = take(64 * 64 * 2);
   n.C0 = take(M0 * 64 * E);
   n.A0 = take(M0 * 64 * E);
+  n.MA0 = take(M0 * 64 / 8);
   int64_t gmax = M0 * 64;
   for (auto& b : n.blocks) {
     const int64_t M = B * b.Hout * b.Wout;
@@ -281,6 +284,8 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
     b.C2 = take(bytes);
     if (b.proj) b.S = take(bytes);
     b.OUT = take(bytes);
+    b.MA1 = take(M * b.Cout / 8);
+    b.MOUT = take(M * b.Cout / 8);
     gmax = std::max<int64_t>(gmax, std::max<int64_t>(M * b.Cout, B * b.Hin * b.Win * b.Cin));
   }
   n.acts.push_back({"stem.im2col", n.X0, (int)B, n.H, n.W, 64});
@@ -454,6 +459,12 @@ static int bn_finalize_fwd(Net& n, BNL& b, int64_t count, bool train, hipStream_
 }
 
 static bool bn_fused() { return option_get(OPT_BN_FUSED_FIN) != 0; }
+// Mask-bit BN backward (option bn_mask, default on): the training forward's fused BN apply also
+// writes the ReLU mask of its output as bits, and the backward forms dz = dy * bit where it needs it
+// instead of reading the bf16 output (2 B) and storing / re-reading dz (4 B) per element.
+static bool bn_mask_on(const Net& n) {
+  return !n.f32 && option_get(OPT_BN_MASK) != 0 && bn_fused() && option_get(OPT_BNB_FUSE) == 0;
+}
 
 // SUM all-reduce of one BN's fp64 partial-sum slots ([DTC_STAT_SLOTS][2][C]) on the compute
 // stream: the slots are first folded into slot 0 (fixed order; the others zeroed), so the collective
@@ -481,7 +492,7 @@ static BnFwdArgs fwd_args(Net& n, BNL& b, int64_t count) {
 
 // BN (+ residual / second BN) + ReLU after the producing conv(s): y = relu(bn(x) [+ x2 | + bn2(x2)])
 static int bn_act(Net& n, int mode, BNL& b, const u16* x, BNL* b2, const u16* x2, u16* y, int64_t M, bool train,
-                  hipStream_t st) {
+                  hipStream_t st, size_t mask_off = 0) {
   if (train && n.sync) {  // SyncBN: global per-channel (sum, sumsq) slots, global element count
     DTC_TRY(sync_bn_sums(n, b.stats, b.C, st));
     if (b2) DTC_TRY(sync_bn_sums(n, b2->stats, b2->C, st));
@@ -490,7 +501,8 @@ static int bn_act(Net& n, int mode, BNL& b, const u16* x, BNL* b2, const u16* x2
   if (train && bn_fused()) {
     const BnFwdArgs a1 = fwd_args(n, b, cnt);
     const BnFwdArgs a2 = b2 ? fwd_args(n, *b2, cnt) : BnFwdArgs{};
-    return bn_fin_apply(mode, x, a1, x2, b2 ? &a2 : nullptr, y, M, b.C, st);
+    uint8_t* mask = bn_mask_on(n) && mask_off ? n.at<uint8_t>(mask_off) : nullptr;
+    return bn_fin_apply(mode, x, a1, x2, b2 ? &a2 : nullptr, y, M, b.C, st, mask);
   }
   DTC_TRY(bn_finalize_fwd(n, b, cnt, train, st));
   if (b2) DTC_TRY(bn_finalize_fwd(n, *b2, cnt, train, st));
@@ -515,7 +527,7 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   PROF(0, 2.0 * M0 * 64 * 27,
        conv_fwd(n.stem.s, X0, n.at<u16>(n.WSTEM), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
                 n.at<float>(n.SLAB), n.slab_bytes, st, ts));
-  DTC_TRY(bn_act(n, 1, n.bn0, n.at<u16>(n.C0), nullptr, nullptr, n.at<u16>(n.A0), M0, train, st));
+  DTC_TRY(bn_act(n, 1, n.bn0, n.at<u16>(n.C0), nullptr, nullptr, n.at<u16>(n.A0), M0, train, st, n.MA0));
   const u16* in = n.at<u16>(n.A0);
   for (auto& b : n.blocks) {
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
@@ -523,7 +535,7 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
     PROF(0, conv_flops(b.c1.s),
          conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
                   n.slab_bytes, st, ts));
-    DTC_TRY(bn_act(n, 1, b.b1, n.at<u16>(b.C1), nullptr, nullptr, n.at<u16>(b.A1), M, train, st));
+    DTC_TRY(bn_act(n, 1, b.b1, n.at<u16>(b.C1), nullptr, nullptr, n.at<u16>(b.A1), M, train, st, b.MA1));
     PROF(0, conv_flops(b.c2.s),
          conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
                   train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st, ts));
@@ -531,9 +543,9 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
       PROF(0, conv_flops(b.sc.s),
            conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr,
                     slab, n.slab_bytes, st, ts));
-      DTC_TRY(bn_act(n, 3, b.b2, n.at<u16>(b.C2), &b.bsc, n.at<u16>(b.S), n.at<u16>(b.OUT), M, train, st));
+      DTC_TRY(bn_act(n, 3, b.b2, n.at<u16>(b.C2), &b.bsc, n.at<u16>(b.S), n.at<u16>(b.OUT), M, train, st, b.MOUT));
     } else {
-      DTC_TRY(bn_act(n, 2, b.b2, n.at<u16>(b.C2), nullptr, in, n.at<u16>(b.OUT), M, train, st));
+      DTC_TRY(bn_act(n, 2, b.b2, n.at<u16>(b.C2), nullptr, in, n.at<u16>(b.OUT), M, train, st, b.MOUT));
     }
     in = n.at<u16>(b.OUT);
   }
@@ -778,7 +790,8 @@ static BnBwdArgs bwd_args(Net& n, BNL& b, int64_t count, float gs) {
 // dx1 = BN-backward apply of b1 on (dz, x1) [; dx2 of b2 on (dz, x2)], coefficients from the sums
 // bn_bwd_reduce accumulated; dgamma / dbeta into the flat gradient buffer.
 static int bn_bwd_coef_apply(Net& n, BNL& b1, const u16* dz, const u16* x1, u16* dx1, BNL* b2, const u16* x2, u16* dx2,
-                             int64_t M, float gs, hipStream_t st) {
+                             int64_t M, float gs, hipStream_t st, const uint8_t* mbits = nullptr,
+                             u16* dzo = nullptr) {
   if (n.sync) {  // SyncBN backward: global sum(dz), sum(dz*xhat); dgamma/dbeta stay this rank's share
     DTC_TRY(sync_bn_sums(n, b1.acc, b1.C, st));
     if (b2) DTC_TRY(sync_bn_sums(n, b2->acc, b2->C, st));
@@ -788,8 +801,10 @@ static int bn_bwd_coef_apply(Net& n, BNL& b1, const u16* dz, const u16* x1, u16*
   if (bn_fused()) {
     const BnBwdArgs a1 = bwd_args(n, b1, cnt, gs);
     const BnBwdArgs a2 = b2 ? bwd_args(n, *b2, cnt, gs) : BnBwdArgs{};
+    if (mbits) return bn_bwd_fin_apply_mask(dz, mbits, dzo, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st);
     return bn_bwd_fin_apply(dz, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st);
   }
+  DTC_CHECK_ARG(mbits == nullptr, "mask-bit BN backward needs the fused finalize");
   DTC_TRY(bn_bwd_finalize(n.at<double>(b1.acc), b1.C, cnt, n.pf(b1.gidx), n.at<float>(b1.mean), n.at<float>(b1.invstd),
                           gs, n.gf(b1.gidx), n.gf(b1.bidx), n.at<float>(b1.coef), st));
   if (b2)
@@ -903,8 +918,97 @@ static bool bucket_fires(const Net& n, int after_block) {
   return false;
 }
 
+// Backward with the mask-bit BN path (bn_mask_on): G[0] carries the RAW gradient of a block output
+// (never masked in place by a reduction), each BN reduction reads (dy, mask bits, x) and stores
+// nothing, and each BN apply forms dz = dy * bit again. The identity shortcut needs dz itself (the
+// residual of conv1's dgrad): bn2's apply writes it over dy in place (same lane reads then writes).
+// Parity captures (n.capture) materialise dz with bn_mask_apply into their slots.
+static int cap_masked(Net& n, const std::string& name, const u16* dy, size_t mask_off, int64_t M, int C, hipStream_t st) {
+  if (!n.capture) return 0;
+  for (const auto& a : n.caps)
+    if (a.name == name) return bn_mask_apply(dy, n.at<uint8_t>(mask_off), (u16*)(n.ws + a.off), M, C, st);
+  return set_error(DTC_EINVAL, "capture slot %s missing", name.c_str());
+}
+
+static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdCtx& cx, hipStream_t st) {
+  n.prof_next = Net::PROF_BWD0;
+  n.ev_next = 0;
+  u16* G[6];
+  for (int i = 0; i < 6; ++i) G[i] = n.at<u16>(n.G[i]);
+  float* slab = n.at<float>(n.SLAB);
+  float* slabw = n.at<float>(n.SLABW);
+  hipStream_t sd = st;  // weight-gradient stream
+  const BlockL& last = n.blocks.back();
+  DTC_HIP(hipMemsetAsync(n.ws + n.acc_lo, 0, n.stats_hi - n.acc_lo, st));
+  DTC_TRY(head_bwd(dlogits, n.at<float>(n.FEAT), n.wbf(n.fc_w), n.B, last.Hout * last.Wout, 512, n.ncls, gs,
+                   n.gf(n.fc_w), n.gf(n.fc_b), G[0], n.at<float>(n.HEADWS), n.HEADWS_bytes, st));
+  WgQueue wq;
+  for (int bi = (int)n.blocks.size() - 1; bi >= 0; --bi) {
+    BlockL& b = n.blocks[bi];
+    const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
+    const u16* in = bi > 0 ? n.at<u16>(n.blocks[bi - 1].OUT) : n.at<u16>(n.A0);
+    u16* dc2 = n.at<u16>(b.DC2);
+    u16* dc1 = n.at<u16>(b.DC1);
+    u16* dsc = b.proj ? n.at<u16>(b.DSC) : nullptr;
+    const uint8_t* mout = n.at<uint8_t>(b.MOUT);
+    const uint8_t* ma1 = n.at<uint8_t>(b.MA1);
+    const std::string cp = n.capture ? "grad.layer" + std::to_string(bi / 2 + 1) + "." + std::to_string(bi % 2) : "";
+    DTC_TRY(cap(n, cp + ".dy", G[0], st));
+    DTC_TRY(cap_masked(n, cp + ".dz", G[0], b.MOUT, M, b.Cout, st));
+    // out = relu(bn2(c2) + shortcut): sums of dz = dy * [out > 0] (and of the projection BN)
+    DTC_TRY(bn_bwd_reduce_mask(G[0], mout, n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
+                               n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
+                               b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
+                               b.proj ? n.at<double>(b.bsc.acc) : nullptr, M, b.Cout, st));
+    // dc2 (and dsc); an identity block also needs dz itself as conv1's dgrad residual: in place in G[0]
+    DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[0], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
+                              b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st, mout, b.proj ? nullptr : G[0]));
+    DTC_TRY(cap(n, cp + ".dc2", dc2, st));
+    if (b.proj) DTC_TRY(cap(n, cp + ".ds", dsc, st));
+    DTC_TRY(fork_side(n, st, &sd));
+    DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd));
+    PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts));
+    DTC_TRY(cap(n, cp + ".da1", G[4], st));
+    DTC_TRY(cap_masked(n, cp + ".dz1", G[4], b.MA1, M, b.Cout, st));
+    DTC_TRY(bn_bwd_reduce_mask(G[4], ma1, n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
+                               n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, M, b.Cout, st));
+    DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st, ma1));
+    DTC_TRY(cap(n, cp + ".dc1", dc1, st));
+    DTC_TRY(fork_side(n, st, &sd));
+    DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd));
+    if (b.proj) {
+      PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+      PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts));
+      DTC_TRY(cap(n, cp + ".dxs", G[5], st));
+    } else {  // residual = dz of this block's output (G[0], written by bn2's apply); dx over it in place
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[0], slab, n.slab_bytes, st, ts));
+    }
+    DTC_TRY(cap(n, cp + ".dx", G[0], st));
+    if (bucket_fires(n, bi)) DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
+    DTC_TRY(maybe_bucket(n, bi, cx, st));
+  }
+  // stem: a0 = relu(bn1(conv1(x)))
+  const int64_t M0 = (int64_t)n.B * n.H * n.W;
+  u16* dc0 = n.at<u16>(n.DC0);
+  const uint8_t* m0 = n.at<uint8_t>(n.MA0);
+  DTC_TRY(bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
+                             n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st));
+  DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[0], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st, m0));
+  DTC_TRY(cap_masked(n, "grad.stem.dz", G[0], n.MA0, M0, 64, st));
+  DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
+  DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
+  DTC_TRY(join_side(n, st));  // the stem wgrad is the last kernel: run it on the main stream
+  PROF(2, 2.0 * M0 * 64 * 27,
+       conv_wgrad(n.stem.s, n.at<u16>(n.X0), dc0, n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st, ts));
+  DTC_TRY(maybe_bucket(n, -1, cx, st));
+  if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
+  return 0;
+}
+
 static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& cx, hipStream_t st) {
   if (n.f32) return backward_body_f32(n, dlogits, gs, cx, st);
+  if (bn_mask_on(n)) return backward_body_mask(n, dlogits, gs, cx, st);
   n.prof_next = Net::PROF_BWD0;
   n.ev_next = 0;
   u16* G[6];

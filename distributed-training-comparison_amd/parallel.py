@@ -98,6 +98,27 @@ class Comm:
             pass
 
 
+_WORLD_COMM = [None]  # the default group's native communicator (set by DistributedDataParallel)
+
+
+def barrier(group=None) -> None:
+    """``torch.distributed.barrier()`` (reference ddp/trainer.py:156) on the native
+    communicator (include/dtc.h ``dtc_barrier``): returns once every rank reached it and this rank's
+    queued GPU work has finished -- torch's NCCL barrier does the same with a one-element all-reduce
+    and a stream synchronize, plus a device fill kernel for its token. Here the token is the
+    communicator's own, the all-reduce runs on the Reducer's side stream (one stream per
+    communicator) and the host polls the completion event instead of a sleeping wait (the GPU
+    queue is empty until the host returns). Before a DistributedDataParallel exists, or for
+    another group, it is ``torch.distributed.barrier``."""
+    comm = _WORLD_COMM[0]
+    if group is None and comm is not None and comm.handle:
+        call("dtc_barrier", comm.handle if comm.world > 1 else None, stream_ptr())
+    elif dist.is_available() and dist.is_initialized():
+        dist.barrier(group)
+    else:
+        call("dtc_barrier", None, stream_ptr())
+
+
 def bucket_plan(layout) -> List[Tuple[int, int]]:
     """[(offset, numel)] of the gradient buckets, in the order backward completes them."""
     return list(layout.buckets)
@@ -189,6 +210,8 @@ class DistributedDataParallel(nn.Module):
                 raise NativeError(f"device_ids={device_ids} but the module lives on cuda:{device}")
         with torch.cuda.device(device):
             self.comm = Comm.from_process_group(device, process_group)
+            if process_group is None:
+                _WORLD_COMM[0] = self.comm  # barrier() of the default group runs on it
             module.set_bucket_cap_mb(float(bucket_cap_mb))
             # a one-rank all-reduce is the identity: no side-stream fork/join inside the backward
             module._comm = self.comm if self.world_size > 1 else None

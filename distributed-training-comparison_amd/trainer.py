@@ -23,7 +23,7 @@ from . import data as D
 from .amp import GradScaler, autocast
 from .nn import CrossEntropyLoss, ResNet18, SyncBatchNorm
 from .optim import SGD
-from .parallel import DDP, DataParallel
+from .parallel import DDP, DataParallel, barrier
 
 
 def load_config(argv=None, mode: str = "ddp"):
@@ -198,7 +198,7 @@ class Trainer:
                     logit = self.model(img)
                     loss = self.criterion(logit, label)
                 if self.distributed:
-                    dist.barrier()                                                        # trainer.py:156
+                    barrier()  # dist.barrier() on the native communicator            # trainer.py:156
                 self.scaler.scale(loss).backward()
                 self.scaler.step(self.optimizer)
                 self.scaler.update()
@@ -206,7 +206,7 @@ class Trainer:
                 logit = self.model(img)
                 loss = self.criterion(logit, label)
                 if self.distributed:
-                    dist.barrier()
+                    barrier()                                                             # trainer.py:163
                 loss.backward()
                 self.optimizer.step()
             train_loss.update(loss.item())

@@ -169,6 +169,13 @@ int dtc_comm_init(dtc_comm** out, int rank, int world, const void* unique_id, in
 int dtc_comm_allreduce_sum(dtc_comm* comm, void* buf, size_t count, int dtype, void* stream);
 int dtc_comm_broadcast(dtc_comm* comm, void* buf, size_t count, int dtype, int root, void* stream);
 int dtc_comm_destroy(dtc_comm* comm);
+/* torch.distributed.barrier() (reference ddp/trainer.py:156, dp/single variants have none): returns
+ * once every rank called it and this rank's work enqueued on `stream` before the call has finished
+ * (torch's NCCL barrier = a one-element all-reduce + a stream synchronize). One float is SUM
+ * all-reduced on the communicator's side stream; the host polls the completion event (no sleeping
+ * driver wait: the GPU is idle until the host returns). comm == NULL or a loopback communicator:
+ * the stream drain alone. */
+int dtc_barrier(dtc_comm* comm, void* stream);
 /* Test communicator (no RCCL): every all-reduce through it -- dtc_comm_allreduce_sum, the Reducer's
  * bucket all-reduces inside dtc_rn18_backward and SyncBN's statistics all-reduces -- multiplies the
  * buffer by `factor` on the stream the collective would run on (the side stream for buckets) and

@@ -376,15 +376,15 @@ def test_graph_replay_matches_eager(dtc, cuda):
 
 @pytest.mark.parametrize("graphs", [True, False])
 def test_side_stream_wgrad_matches_serial(dtc, cuda, graphs):
-    """Weight gradients on the side stream (option bwd_streams=1; off by default), forked/joined by
+    """Weight gradients on the side stream (option bwd_streams=1, the default), forked/joined by
     events inside the (captured) backward, vs everything on one stream: the same kernels on the
     same operands, so results agree up to the order of the fp64 BN-statistics atomics."""
-    lb, gb, pb, _ = _train_steps(dtc, cuda, 3, graphs=graphs)
-    dtc._native.lib.dtc_set_option(b"bwd_streams", 1)
+    la, ga, pa, _ = _train_steps(dtc, cuda, 3, graphs=graphs)
+    dtc._native.lib.dtc_set_option(b"bwd_streams", 0)
     try:
-        la, ga, pa, _ = _train_steps(dtc, cuda, 3, graphs=graphs)
+        lb, gb, pb, _ = _train_steps(dtc, cuda, 3, graphs=graphs)
     finally:
-        dtc._native.lib.dtc_set_option(b"bwd_streams", 0)
+        dtc._native.lib.dtc_set_option(b"bwd_streams", 1)
     np.testing.assert_allclose(la, lb, rtol=1e-4)
     assert rel_err(ga, gb) < 1e-3
     assert rel_err(pa, pb) < 1e-5
@@ -441,6 +441,28 @@ def test_wgrad_batch_matches_unbatched(dtc, cuda, graphs):
             a = ga[rep][pe.offset:pe.offset + pe.numel]
             b = gb[rep][pe.offset:pe.offset + pe.numel]
             assert rel_err(a, b) < 1e-5, (rep, pe.name, rel_err(a, b))
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
+    """Mask-bit BN backward (option bn_mask=1, default: the forward BN apply writes the ReLU mask as
+    bits, the reduction stores no dz, the apply forms dz from dy and the bits) vs masking with the
+    bf16 outputs and a stored dz: masking is exact and the sums run in the same order, so gradients
+    agree to the fp64 slot-atomic order (capture and replay), and so do three training steps."""
+    ga = _grads_repeated(dtc, cuda, graphs)
+    la, _, pa, ba = _train_steps(dtc, cuda, 3, graphs=graphs)
+    dtc._native.lib.dtc_set_option(b"bn_mask", 0)
+    try:
+        gb = _grads_repeated(dtc, cuda, graphs)
+        lb, _, pb, bb = _train_steps(dtc, cuda, 3, graphs=graphs)
+    finally:
+        dtc._native.lib.dtc_set_option(b"bn_mask", 1)
+    for rep in range(2):
+        assert rel_err(ga[rep], gb[rep]) < 1e-6, rep
+    np.testing.assert_allclose(la, lb, rtol=1e-4)
+    assert rel_err(pa, pb) < 1e-5
+    for k in ba:
+        assert rel_err(ba[k], bb[k]) < 1e-4, k
 
 
 def test_graph_recapture_on_option_change(dtc, cuda):
@@ -596,6 +618,31 @@ def test_native_loss_backward_matches_autograd(dtc, cuda):
     # arithmetic on the loss leaves the fast path: a plain autograd tensor
     loss = crit(model(xd), yd)
     assert type(loss * 2.0) is torch.Tensor
+
+
+def test_native_barrier_waits_for_queued_work(dtc, cuda):
+    """dtc.barrier() (dtc_barrier; the reference's per-step dist.barrier(), trainer.py:156) returns only
+    after the work queued on the current stream before it finished -- torch's NCCL barrier semantics
+    -- with no communicator (world 1) and through a one-rank RCCL communicator registered as the
+    default group's."""
+    s = torch.cuda.current_stream()
+    torch.cuda._sleep(50_000_000)  # a long spin kernel (~20+ ms)
+    assert not s.query()
+    dtc.barrier()
+    assert s.query()
+    comm = dtc.parallel.Comm(0, 1, dtc.parallel.Comm.unique_id(), cuda.index or 0)
+    prev = dtc.parallel._WORLD_COMM[0]
+    dtc.parallel._WORLD_COMM[0] = comm
+    try:
+        torch.cuda._sleep(50_000_000)
+        assert not s.query()
+        dtc.barrier()
+        assert s.query()
+        dtc._native.call("dtc_barrier", comm.handle, dtc._native.stream_ptr())  # the RCCL form itself
+        assert s.query()
+    finally:
+        dtc.parallel._WORLD_COMM[0] = prev
+        comm.close()
 
 
 def test_native_loss_item_and_dlogits_buffer(dtc, cuda):
