@@ -152,10 +152,11 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy
 def hbm_probe(dtc, dev, B, S, nparam, reps=20):
     """Achieved HBM GB/s of the two HBM-bound kernel classes the north star names, timed with
     device events on the stream they are launched on (torch's current stream), after the timed
-    regions: (1) bn_bwd_reduce<mask> at the largest BN shape of the step (the stem / layer1 BNs:
-    B*S*S pixels x 64 channels; reads dy, y, x and writes dz: 8 B/element), the executor's
-    largest BN item per step; (2) the fused SGD-Nesterov + bf16-shadow kernel over a flat buffer of
-    the model's size (reads p, g, m; writes p, m, bf16 p: 22 B/parameter). Scratch tensors only."""
+    regions: (1) the stand-alone dtc_bn_bwd_reduce (bf16-output mask, dz stored: 8 B/element) at the
+    largest BN shape of the step (B*S*S pixels x 64 channels) -- an isolated bandwidth reference; the
+    executor's own BN kernels (mask-bit path) are timed in the step itself (`bn_in_step`); (2) the
+    fused SGD-Nesterov + bf16-shadow kernel over a flat buffer of the model's size (reads p, g, m;
+    writes p, m, bf16 p: 22 B/parameter), which the in-step timing does not cover. Scratch tensors."""
     ops = dtc.ops
     M, Cc = B * S * S, 64
     g = torch.Generator(device=dev).manual_seed(7)
@@ -292,7 +293,7 @@ def main():
     # kernel per step folds into totals; arming re-captures the step graphs, so two untimed steps
     # follow the arming and the totals are re-zeroed before the region.
     import ctypes as C
-    ms, fl, cnt = (C.c_double * 3)(), (C.c_double * 3)(), (C.c_int * 3)()
+    ms4, fl4, cnt4 = (C.c_double * 4)(), (C.c_double * 4)(), (C.c_int * 4)()
     prof_elapsed = None
     if not args.no_live_roofline:
         exe = model.module.executor(B, S, S, "bf16")
@@ -306,8 +307,9 @@ def main():
         torch.cuda.synchronize()
         dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
         prof_elapsed = timed(args.steps, args.warmup + args.steps + 2)
-        dtc._native.call("dtc_rn18_profile_end", exe.handle, ms, fl, cnt)
+        dtc._native.call("dtc_rn18_profile_end_ex", exe.handle, 4, ms4, fl4, cnt4)
         dtc._native.call("dtc_set_option", b"bwd_streams", bwd_streams)
+    ms, fl, cnt = list(ms4)[:3], list(fl4)[:3], list(cnt4)[:3]  # the conv passes (kinds 0-2)
 
     # C4 all-reduce bus bandwidth on the Reducer's own RCCL communicator: the full gradient
     # (11,220,132 fp32) and the bucket-size sweep of BASELINE config 5 (N > 1 only: one rank has
@@ -380,6 +382,16 @@ def main():
                 "algorithmic_gflop_per_step": round(conv_flops / args.steps / 1e9, 3),
             },
             "hbm_roofline": hbm,
+            # the whole in-step BN family (kind 3: forward finalize+apply, backward reduce, backward
+            # finalize+apply of all 20 BNs), measured live in region 2 like the convs: algorithmic bytes
+            # (each tensor read / written once) / summed kernel durations
+            "bn_in_step": ({"ms_per_step": round(ms4[3] / args.steps, 4),
+                            "bytes_per_step": round(fl4[3] / args.steps),
+                            "calls_per_step": cnt4[3] // max(1, args.steps),
+                            "achieved_GBps": round(fl4[3] / (ms4[3] * 1e-3) / 1e9, 1) if ms4[3] > 0 else None,
+                            "peak_GBps": HBM_PEAK_GBPS,
+                            "frac": round(fl4[3] / (ms4[3] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if ms4[3] > 0 else None}
+                           if not args.no_live_roofline else None),
             "step_flop_fraction_of_peak": round(FLOPS_PER_IMAGE * (S * S / 1024) * B / (elapsed / args.steps) / 1e12
                                                 / BF16_PEAK_TFLOPS, 4),
             "final_loss": round(losses[-1], 4) if losses else None,

@@ -69,6 +69,9 @@ _SIGS = {
     "dtc_bn_bwd_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
     "dtc_stem_im2col": (i32, [vp, vp, i32, i32, i32, vp]),
     "dtc_stem_pack_weight": (i32, [vp, vp, i32, vp]),
+    "dtc_stem_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
+    "dtc_stem_wgrad_workspace_size": (sz, [i32, i32, i32]),
+    "dtc_stem_wgrad": (i32, [vp, vp, vp, f32, i32, i32, i32, vp, sz, vp]),
     "dtc_head_fwd": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp]),
     "dtc_head_bwd_workspace_size": (sz, [i32, i32, i32]),
     "dtc_head_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, sz, vp]),
@@ -119,6 +122,7 @@ _SIGS = {
     "dtc_rn18_activation_info": (i32, [vp, i32, C.POINTER(cstr), C.POINTER(sz), Pi32]),
     "dtc_rn18_profile_begin": (i32, [vp, i32]),
     "dtc_rn18_profile_end": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), Pi32]),
+    "dtc_rn18_profile_end_ex": (i32, [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double), Pi32]),
     "dtc_rn18_forward": (i32, [vp, vp, vp, i32, vp]),
     "dtc_rn18_backward": (i32, [vp, vp, f32, vp, vp]),
     "dtc_rn18_set_sync_bn": (i32, [vp, vp]),

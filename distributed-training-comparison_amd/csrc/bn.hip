@@ -12,6 +12,7 @@
 // are reduced per workgroup through LDS and then added into fp64 slots.
 #include "common.h"
 #include "kernels.h"
+#include "tile_common.h"
 
 namespace dtc {
 
@@ -268,10 +269,11 @@ template <int MODE, typename T>
 __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const T* __restrict__ x, const BnFwdArgs a1,
                                                           const T* __restrict__ x2, const BnFwdArgs a2,
                                                           T* __restrict__ y, int64_t M, int C, int rows,
-                                                          uint8_t* __restrict__ mask) {
+                                                          uint8_t* __restrict__ mask, u64* ts) {
   typedef Elt<T> E;
   __shared__ double part[4 * 2 * 64];
   __shared__ float coef[4][64];  // scale1, shift1, scale2, shift2
+  stamp_start(ts);
   const int cg = blockIdx.y * FA_GROUP;
   fa_fwd_coef(a1, C, cg, part, coef[0], coef[1]);
   if constexpr (MODE == APPLY_DUAL_RELU) fa_fwd_coef(a2, C, cg, part, coef[2], coef[3]);
@@ -321,6 +323,7 @@ __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const T* __restrict__
       if (mask != nullptr) mask[o >> 3] = (uint8_t)E::mask8(pk);
     }
   }
+  stamp_end(ts);
 }
 
 static void fa_grid(int64_t M, int C, int& nblk, int& rows) {
@@ -335,7 +338,7 @@ static void fa_grid(int64_t M, int C, int& nblk, int& rows) {
 
 template <typename T>
 static int fin_apply(int mode, const T* x, const BnFwdArgs& a1, const T* x2, const BnFwdArgs* a2, T* y, int64_t M,
-                     int C, hipStream_t st, uint8_t* mask) {
+                     int C, hipStream_t st, uint8_t* mask, u64* ts) {
   DTC_CHECK_ARG(x && y && a1.stats && a1.gamma && a1.beta && a1.mean && a1.invstd && C % FA_GROUP == 0 && M > 0,
                 "bn_fin_apply: bad args (C=%d)", C);
   int nblk, rows;
@@ -344,15 +347,15 @@ static int fin_apply(int mode, const T* x, const BnFwdArgs& a1, const T* x2, con
   const BnFwdArgs none{};
   switch (mode) {
     case APPLY_RELU:
-      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows, mask);
+      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows, mask, ts);
       break;
     case APPLY_ADD_RELU:
       DTC_CHECK_ARG(x2 != nullptr, "bn_fin_apply: residual required");
-      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_ADD_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows, mask);
+      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_ADD_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows, mask, ts);
       break;
     default:
       DTC_CHECK_ARG(x2 && a2 && a2->stats, "bn_fin_apply: second branch required");
-      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_DUAL_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, *a2, y, M, C, rows, mask);
+      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_DUAL_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, *a2, y, M, C, rows, mask, ts);
       break;
   }
   DTC_LAUNCH_CHECK();
@@ -360,12 +363,12 @@ static int fin_apply(int mode, const T* x, const BnFwdArgs& a1, const T* x2, con
 }
 
 int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, const BnFwdArgs* a2, u16* y, int64_t M,
-                 int C, hipStream_t st, uint8_t* mask) {
-  return fin_apply<u16>(mode, x, a1, x2, a2, y, M, C, st, mask);
+                 int C, hipStream_t st, uint8_t* mask, u64* ts) {
+  return fin_apply<u16>(mode, x, a1, x2, a2, y, M, C, st, mask, ts);
 }
 int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2, const BnFwdArgs* a2, float* y,
                  int64_t M, int C, hipStream_t st) {
-  return fin_apply<float>(mode, x, a1, x2, a2, y, M, C, st, nullptr);
+  return fin_apply<float>(mode, x, a1, x2, a2, y, M, C, st, nullptr, nullptr);
 }
 
 // ------------------------------------------------------------------ fused finalize + apply (backward)
@@ -401,10 +404,11 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restri
                                                               const BnBwdArgs a1, T* __restrict__ dx1,
                                                               const T* __restrict__ x2, const BnBwdArgs a2,
                                                               T* __restrict__ dx2, int64_t M, int C, int rows,
-                                                              const uint8_t* __restrict__ mbits, T* dzo) {
+                                                              const uint8_t* __restrict__ mbits, T* dzo, u64* ts) {
   typedef Elt<T> E;
   __shared__ double part[4 * 2 * 64];
   __shared__ float coef[6][64];
+  stamp_start(ts);
   const int cg = blockIdx.y * FA_GROUP;
   fa_bwd_coef(a1, C, cg, part, coef[0], coef[1], coef[2]);
   if constexpr (DUAL) fa_bwd_coef(a2, C, cg, part, coef[3], coef[4], coef[5]);
@@ -456,11 +460,13 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restri
       }
     }
   }
+  stamp_end(ts);
 }
 
 template <typename T>
 static int bwd_fin_apply(const T* dz, const T* x1, const BnBwdArgs& a1, T* dx1, const T* x2, const BnBwdArgs* a2,
-                         T* dx2, int64_t M, int C, hipStream_t st, const uint8_t* mbits = nullptr, T* dzo = nullptr) {
+                         T* dx2, int64_t M, int C, hipStream_t st, const uint8_t* mbits = nullptr, T* dzo = nullptr,
+                         u64* ts = nullptr) {
   DTC_CHECK_ARG(dz && x1 && dx1 && a1.acc && a1.gamma && a1.mean && a1.invstd && C % FA_GROUP == 0 && M > 0,
                 "bn_bwd_fin_apply: bad args (C=%d)", C);
   DTC_CHECK_ARG(mbits || !dzo, "bn_bwd_fin_apply: a dz output needs the mask bits");
@@ -471,7 +477,7 @@ static int bwd_fin_apply(const T* dz, const T* x1, const BnBwdArgs& a1, T* dx1, 
   if (x2) DTC_CHECK_ARG(a2 && a2->acc && dx2, "bn_bwd_fin_apply: dual branch args");
 #define DTC_BFA(D_, M_) \
   hipLaunchKernelGGL((bn_bwd_fin_apply_kernel<D_, M_, T>), grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, D_ ? *a2 : none, \
-                     dx2, M, C, rows, mbits, dzo)
+                     dx2, M, C, rows, mbits, dzo, ts)
   if (x2 && mbits) DTC_BFA(true, true);
   else if (x2) DTC_BFA(true, false);
   else if (mbits) DTC_BFA(false, true);
@@ -482,9 +488,9 @@ static int bwd_fin_apply(const T* dz, const T* x1, const BnBwdArgs& a1, T* dx1, 
 }
 
 int bn_bwd_fin_apply_mask(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
-                          const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st) {
+                          const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(mbits != nullptr, "bn_bwd_fin_apply_mask: mask bits required");
-  return bwd_fin_apply<u16>(dy, x1, a1, dx1, x2, a2, dx2, M, C, st, mbits, dzo);
+  return bwd_fin_apply<u16>(dy, x1, a1, dx1, x2, a2, dx2, M, C, st, mbits, dzo, ts);
 }
 
 int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
@@ -505,9 +511,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const float* __restrict__ mean1, const float* __restrict__ invstd1, double* __restrict__ acc1,
     const T* __restrict__ x2, const float* __restrict__ mean2, const float* __restrict__ invstd2,
     double* __restrict__ acc2, T* __restrict__ dz, int64_t M, int C, int rows_per_block,
-    const uint8_t* __restrict__ mbits = nullptr) {
+    const uint8_t* __restrict__ mbits = nullptr, u64* ts = nullptr) {
   typedef Elt<T> E;
   __shared__ float red[256 * 24];
+  stamp_start(ts);
   const int tpr = C >> 3, rpp = 256 / tpr;
   const int t = threadIdx.x, g = t % tpr, rr = t / tpr;
   const int c0 = g * 8;
@@ -577,6 +584,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
       unsafeAtomicAdd(acc2 + slot + C + c, (double)e);
     }
   }
+  stamp_end(ts);
 }
 
 template <typename T>
@@ -611,7 +619,7 @@ static int bwd_reduce(const T* dy, const T* ymask, const T* x1, const float* mea
 
 int bn_bwd_reduce_mask(const u16* dy, const uint8_t* mbits, const u16* x1, const float* mean1, const float* invstd1,
                        double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, int64_t M,
-                       int C, hipStream_t st) {
+                       int C, hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(dy && mbits && x1 && mean1 && invstd1 && acc1 && C % 8 == 0 && C <= 2048 && M > 0,
                 "bn_bwd_reduce_mask: bad args");
   const int tpr = C / 8, rpp = 256 / tpr;
@@ -622,10 +630,10 @@ int bn_bwd_reduce_mask(const u16* dy, const uint8_t* mbits, const u16* x1, const
   if (x2) {
     DTC_CHECK_ARG(mean2 && invstd2 && acc2, "bn_bwd_reduce_mask: dual branch args");
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, true, u16, true>), dim3(blocks), dim3(256), 0, st, dy, nullptr, x1,
-                       mean1, invstd1, acc1, x2, mean2, invstd2, acc2, nullptr, M, C, (int)rpb, mbits);
+                       mean1, invstd1, acc1, x2, mean2, invstd2, acc2, nullptr, M, C, (int)rpb, mbits, ts);
   } else {
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false, u16, true>), dim3(blocks), dim3(256), 0, st, dy, nullptr, x1,
-                       mean1, invstd1, acc1, x2, mean2, invstd2, acc2, nullptr, M, C, (int)rpb, mbits);
+                       mean1, invstd1, acc1, x2, mean2, invstd2, acc2, nullptr, M, C, (int)rpb, mbits, ts);
   }
   DTC_LAUNCH_CHECK();
   return 0;

@@ -12,11 +12,11 @@
 #include <cstring>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {2}, {3}, {0}, {0}, {1}, {4}, {1}, {1}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {2}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
                                              "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
                                              "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse",
-                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin"};
+                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct"};
 static std::atomic<int> g_epoch{0};
 int option_get(int id) { return g_opts[id].load(std::memory_order_relaxed); }
 int option_epoch() { return g_epoch.load(std::memory_order_relaxed); }
@@ -153,6 +153,17 @@ int dtc_stem_im2col(const float* x, uint16_t* cols, int n, int h, int w, void* s
 }
 int dtc_stem_pack_weight(const uint16_t* w27, uint16_t* w64, int k, void* stream) {
   return stem_pack_weight(w27, w64, k, S(stream));
+}
+int dtc_stem_fwd(const float* x_nchw, const uint16_t* w27, uint16_t* y, double* stats, int n, int h, int w,
+                 void* stream) {
+  GUARD(return stem_fwd(x_nchw, w27, y, stats, n, h, w, S(stream));)
+}
+size_t dtc_stem_wgrad_workspace_size(int n, int h, int w) {
+  return n > 0 && h > 0 && w > 0 ? stem_wgrad_slab_bytes((int64_t)n * h * w) : 0;
+}
+int dtc_stem_wgrad(const float* x_nchw, const uint16_t* dy, float* dw27, float scale, int n, int h, int w, void* ws,
+                   size_t ws_bytes, void* stream) {
+  GUARD(return stem_wgrad(x_nchw, dy, dw27, scale, n, h, w, (float*)ws, ws_bytes, S(stream));)
 }
 int dtc_head_fwd(const uint16_t* act, int n, int hw, int c, const uint16_t* wfc, const float* bfc, int ncls,
                  float* feat, float* logits, void* stream) {

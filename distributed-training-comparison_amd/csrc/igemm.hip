@@ -899,6 +899,14 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
   return launch_wgrad_reduce(slab, splits, s.K, p.RSC, ncols, ldo, scale, outs, 1, 0, st, ts);
 }
 
+int wgrad_reduce_to(const float* slab, int splits, int K, int RSC, int ncols, int ldo, float scale, float* dw,
+                    hipStream_t st, u64* ts) {
+  DTC_CHECK_ARG(slab && dw && splits > 0 && K > 0 && RSC % 4 == 0 && ncols <= RSC, "wgrad_reduce_to: bad args");
+  WgOuts outs{};
+  outs.dw[0] = dw;
+  return launch_wgrad_reduce(slab, splits, K, RSC, ncols, ldo, scale, outs, 1, 0, st, ts);
+}
+
 size_t conv_wgrad_batch_slab_bytes(const ConvShape& s, int nprob) {
   return (size_t)nprob * wgrad_halo_splits(s, nprob) * s.K * s.R * s.S * s.C * 4;
 }

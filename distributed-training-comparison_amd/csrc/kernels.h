@@ -37,6 +37,8 @@ enum {
   OPT_WGRAD_BATCH = 18,    // executor: up to this many 3x3 stride-1 weight gradients of a bucket per launch
   OPT_BN_MASK = 19,        // executor: 1 = ReLU mask bits from the forward BN apply drive the BN backward
   OPT_BARRIER_SPIN = 20,   // dtc_barrier host wait: 1 = poll the completion event, 0 = hipEventSynchronize
+  OPT_WGRAD_KERNEL = 21,   // wgrad_halo: 0 = 8 waves (144 x 32 per wave), 1 = 4 waves (144 x 64, one per SIMD)
+  OPT_STEM_DIRECT = 22,    // executor (at plan time): 1 = direct stem conv (stem.hip), 0 = im2col + GEMM
   OPT_COUNT
 };
 int option_get(int id);
@@ -170,15 +172,16 @@ struct BnBwdArgs {
 // mode: 1 relu, 2 add residual x2 + relu, 3 dual BN (x2 normalised by a2) + relu
 // mask (optional): ReLU mask bits of y (byte o/8 for element offset o) for the mask-bit backward
 int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, const BnFwdArgs* a2, u16* y, int64_t M,
-                 int C, hipStream_t st, uint8_t* mask = nullptr);
+                 int C, hipStream_t st, uint8_t* mask = nullptr, u64* ts = nullptr);
 // Mask-bit BN backward (the executor's default): dz = dy * mask bit is formed where it is used, never
 // stored by the reduction. Reduce: sums only (dy, bits, x read: 4.125 B/element); apply: dx (and
 // dzo = dz if non-null, may alias dy) from dy, bits, x. bn_mask_apply: dz alone (parity captures).
 int bn_bwd_reduce_mask(const u16* dy, const uint8_t* mbits, const u16* x1, const float* mean1, const float* invstd1,
                        double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, int64_t M,
-                       int C, hipStream_t st);
+                       int C, hipStream_t st, u64* ts = nullptr);
 int bn_bwd_fin_apply_mask(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
-                          const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st);
+                          const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st,
+                          u64* ts = nullptr);
 int bn_mask_apply(const u16* dy, const uint8_t* mbits, u16* dz, int64_t M, int C, hipStream_t st);
 int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
                      u16* dx2, int64_t M, int C, hipStream_t st);
@@ -210,6 +213,17 @@ int bn_bwd_apply(const float* dz, const float* x1, const float* coef1, float* dx
 int stem_im2col(const float* x, u16* cols, int N, int H, int W, hipStream_t st);
 // w bf16 [64][27] -> [64][64] zero padded
 int stem_pack_weight(const u16* w27, u16* w64, int K, hipStream_t st);
+// Direct stem conv (stem.hip): im2col gathered into LDS per 256-pixel tile, one K=32 MFMA k-step.
+// fwd: y [N*H*W][64] bf16 (+ BN statistics of the bf16 output into stats[SLOTS][2][64] if non-null)
+// from fp32 NCHW x and the bf16 [64][27] weight; wgrad: dw27 [64][27] fp32 = scale * sum.
+int stem_fwd(const float* x, const u16* w27, u16* y, double* stats, int N, int H, int W, hipStream_t st,
+             u64* ts = nullptr);
+size_t stem_wgrad_slab_bytes(int64_t M);
+int stem_wgrad(const float* x, const u16* dy, float* dw27, float scale, int N, int H, int W, float* slab,
+               size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
+// grad[k][0:ncols] (row stride ldo) = scale * sum_s slab[s][k][0:RSC] (igemm.hip's deterministic reduce)
+int wgrad_reduce_to(const float* slab, int splits, int K, int RSC, int ncols, int ldo, float scale, float* dw,
+                    hipStream_t st, u64* ts = nullptr);
 // feat[n][c] = bf16round(mean_hw act); logits[n][j] = feat . W[j] + b[j]
 int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st);

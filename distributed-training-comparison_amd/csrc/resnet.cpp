@@ -78,6 +78,8 @@ struct Net {
   size_t ws_bytes = 0;
   size_t X0 = 0, WSTEM = 0, C0 = 0, A0 = 0, FEAT = 0, G[6] = {0, 0, 0, 0, 0, 0}, SLAB = 0;
   size_t MA0 = 0;  // ReLU mask bits of A0
+  size_t XIN = 0;  // executor-owned copy of the fp32 NCHW input (direct stem conv, bf16 mode)
+  bool stem_direct = false;  // planned with option stem_direct (bf16): stem.hip instead of im2col + GEMM
   size_t HEADWS = 0, HEADWS_bytes = 0;
   size_t DC0 = 0, SLABW = 0;  // stem conv-output gradient; split-K slab of the side-stream wgrads
   // backward weight gradients run on a side stream (option bwd_streams), overlapped with the
@@ -94,7 +96,7 @@ struct Net {
   // live conv timing (bench roofline): each conv call stamps min(start)/max(end) of its workgroups
   // (s_memrealtime) into its own slot; one kernel per step folds the slots into running totals.
   // Graph-safe: the slot pointers are baked at capture, nothing happens on the host per call.
-  static constexpr int PROF_SLOTS = 128, PROF_BWD0 = 32;  // forward calls use [0,32), backward [32,128)
+  static constexpr int PROF_SLOTS = 256, PROF_BWD0 = 96;  // forward calls use [0,96), backward [96,256)
   bool profiling = false;
   u64* prof_ts = nullptr;   // [PROF_SLOTS][DTC_PROF_SLOT_U64] device
   u64* prof_acc = nullptr;  // [PROF_SLOTS][2] device: (sum ticks, calls)
@@ -270,7 +272,9 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   const int64_t B = n.B;
   const int64_t M0 = B * n.H * n.W;
   const size_t E = n.esz();
-  n.X0 = take(M0 * 64 * 2);  // im2col: [M0][64] bf16 or [M0][32] fp32
+  n.stem_direct = !n.f32 && option_get(OPT_STEM_DIRECT) != 0;
+  n.XIN = n.stem_direct ? take(M0 * 3 * 4) : 0;
+  n.X0 = n.stem_direct ? 0 : take(M0 * 64 * 2);  // im2col: [M0][64] bf16 or [M0][32] fp32
   n.WSTEM = take(64 * 64 * 2);
   n.C0 = take(M0 * 64 * E);
   n.A0 = take(M0 * 64 * E);
@@ -288,7 +292,7 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
     b.MOUT = take(M * b.Cout / 8);
     gmax = std::max<int64_t>(gmax, std::max<int64_t>(M * b.Cout, B * b.Hin * b.Win * b.Cin));
   }
-  n.acts.push_back({"stem.im2col", n.X0, (int)B, n.H, n.W, 64});
+  if (!n.stem_direct) n.acts.push_back({"stem.im2col", n.X0, (int)B, n.H, n.W, 64});
   n.acts.push_back({"stem.conv", n.C0, (int)B, n.H, n.W, 64});
   n.acts.push_back({"stem.out", n.A0, (int)B, n.H, n.W, 64});
   for (size_t i = 0; i < n.blocks.size(); ++i) {
@@ -344,6 +348,7 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
         slab = std::max(slab, conv_wgrad_batch_slab_bytes(b.c2.s, np));
       }
   }
+  if (n.stem_direct) slab = std::max(slab, stem_wgrad_slab_bytes(M0));
   n.slab_bytes = slab;
   n.SLAB = take(slab);
   n.SLABW = take(slab);
@@ -392,6 +397,8 @@ static double conv_flops(const ConvShape& s) {
   const int P = (s.H + 2 * s.pad - s.R) / s.stride + 1, Q = (s.W + 2 * s.pad - s.S) / s.stride + 1;
   return 2.0 * s.N * P * Q * (double)s.K * s.R * s.S * s.C;
 }
+// kinds: 0 conv forward, 1 conv dgrad, 2 conv wgrad (work = algorithmic FLOPs), 3 BN family (work =
+// algorithmic HBM bytes: the tensors each BN kernel must read / write once)
 static u64* prof_slot(Net& n, int kind, double flops) {
   if (!n.profiling || n.prof_next >= Net::PROF_SLOTS) return nullptr;
   const int i = n.prof_next++;
@@ -502,7 +509,8 @@ static int bn_act(Net& n, int mode, BNL& b, const u16* x, BNL* b2, const u16* x2
     const BnFwdArgs a1 = fwd_args(n, b, cnt);
     const BnFwdArgs a2 = b2 ? fwd_args(n, *b2, cnt) : BnFwdArgs{};
     uint8_t* mask = bn_mask_on(n) && mask_off ? n.at<uint8_t>(mask_off) : nullptr;
-    return bn_fin_apply(mode, x, a1, x2, b2 ? &a2 : nullptr, y, M, b.C, st, mask);
+    u64* ts = prof_slot(n, 3, (double)M * b.C * (4.0 + (mode != 1 ? 2.0 : 0.0) + (mask ? 0.125 : 0.0)));
+    return bn_fin_apply(mode, x, a1, x2, b2 ? &a2 : nullptr, y, M, b.C, st, mask, ts);
   }
   DTC_TRY(bn_finalize_fwd(n, b, cnt, train, st));
   if (b2) DTC_TRY(bn_finalize_fwd(n, *b2, cnt, train, st));
@@ -520,13 +528,18 @@ static int forward_body_f32(Net& n, float* logits, bool train, hipStream_t st);
 static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   if (n.f32) return forward_body_f32(n, logits, train, st);
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
-  u16* X0 = n.at<u16>(n.X0);
   n.prof_next = train ? 0 : Net::PROF_SLOTS;  // eval passes are not timed
-  DTC_TRY(stem_pack_weight(n.wbf(n.stem.pidx), n.at<u16>(n.WSTEM), 64, st));
   if (train) DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.acc_lo - n.stats_lo, st));
-  PROF(0, 2.0 * M0 * 64 * 27,
-       conv_fwd(n.stem.s, X0, n.at<u16>(n.WSTEM), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
-                n.at<float>(n.SLAB), n.slab_bytes, st, ts));
+  if (n.stem_direct) {  // stem.hip: taps gathered per tile from the fp32 input, one K=32 k-step
+    PROF(0, 2.0 * M0 * 64 * 27,
+         stem_fwd(n.at<float>(n.XIN), n.wbf(n.stem.pidx), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
+                  n.B, n.H, n.W, st, ts));
+  } else {
+    DTC_TRY(stem_pack_weight(n.wbf(n.stem.pidx), n.at<u16>(n.WSTEM), 64, st));
+    PROF(0, 2.0 * M0 * 64 * 27,
+         conv_fwd(n.stem.s, n.at<u16>(n.X0), n.at<u16>(n.WSTEM), n.at<u16>(n.C0),
+                  train ? n.at<double>(n.bn0.stats) : nullptr, n.at<float>(n.SLAB), n.slab_bytes, st, ts));
+  }
   DTC_TRY(bn_act(n, 1, n.bn0, n.at<u16>(n.C0), nullptr, nullptr, n.at<u16>(n.A0), M0, train, st, n.MA0));
   const u16* in = n.at<u16>(n.A0);
   for (auto& b : n.blocks) {
@@ -724,6 +737,8 @@ static int backward_body_f32(Net& n, const float* dlogits, float gs, const BwdCt
 
 static int forward(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
   if (n.f32) DTC_TRY(f32_stem_im2col(x, n.at<float>(n.X0), n.B, n.H, n.W, st));
+  else if (n.stem_direct)  // the graph reads only executor memory: a plain copy of the 12 B/pixel input
+    DTC_HIP(hipMemcpyAsync(n.at<float>(n.XIN), x, (size_t)n.B * 3 * n.H * n.W * 4, hipMemcpyDeviceToDevice, st));
   else DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
   if (!graphs_on(n)) return forward_body(n, logits, train, st);
   hipGraphExec_t& ex = n.fwd_exec[train ? 1 : 0];
@@ -801,7 +816,10 @@ static int bn_bwd_coef_apply(Net& n, BNL& b1, const u16* dz, const u16* x1, u16*
   if (bn_fused()) {
     const BnBwdArgs a1 = bwd_args(n, b1, cnt, gs);
     const BnBwdArgs a2 = b2 ? bwd_args(n, *b2, cnt, gs) : BnBwdArgs{};
-    if (mbits) return bn_bwd_fin_apply_mask(dz, mbits, dzo, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st);
+    if (mbits) {
+      u64* ts = prof_slot(n, 3, (double)M * b1.C * (6.125 + (x2 ? 4.0 : 0.0) + (dzo ? 2.0 : 0.0)));
+      return bn_bwd_fin_apply_mask(dz, mbits, dzo, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st, ts);
+    }
     return bn_bwd_fin_apply(dz, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st);
   }
   DTC_CHECK_ARG(mbits == nullptr, "mask-bit BN backward needs the fused finalize");
@@ -956,10 +974,11 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     DTC_TRY(cap(n, cp + ".dy", G[0], st));
     DTC_TRY(cap_masked(n, cp + ".dz", G[0], b.MOUT, M, b.Cout, st));
     // out = relu(bn2(c2) + shortcut): sums of dz = dy * [out > 0] (and of the projection BN)
-    DTC_TRY(bn_bwd_reduce_mask(G[0], mout, n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
-                               n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
-                               b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
-                               b.proj ? n.at<double>(b.bsc.acc) : nullptr, M, b.Cout, st));
+    PROF(3, (double)M * b.Cout * (b.proj ? 6.125 : 4.125),
+         bn_bwd_reduce_mask(G[0], mout, n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
+                            n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
+                            b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
+                            b.proj ? n.at<double>(b.bsc.acc) : nullptr, M, b.Cout, st, ts));
     // dc2 (and dsc); an identity block also needs dz itself as conv1's dgrad residual: in place in G[0]
     DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[0], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
                               b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st, mout, b.proj ? nullptr : G[0]));
@@ -970,8 +989,9 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts));
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
     DTC_TRY(cap_masked(n, cp + ".dz1", G[4], b.MA1, M, b.Cout, st));
-    DTC_TRY(bn_bwd_reduce_mask(G[4], ma1, n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
-                               n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, M, b.Cout, st));
+    PROF(3, (double)M * b.Cout * 4.125,
+         bn_bwd_reduce_mask(G[4], ma1, n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
+                            n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, M, b.Cout, st, ts));
     DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st, ma1));
     DTC_TRY(cap(n, cp + ".dc1", dc1, st));
     DTC_TRY(fork_side(n, st, &sd));
@@ -992,15 +1012,17 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
   u16* dc0 = n.at<u16>(n.DC0);
   const uint8_t* m0 = n.at<uint8_t>(n.MA0);
-  DTC_TRY(bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
-                             n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st));
+  PROF(3, (double)M0 * 64 * 4.125,
+       bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
+                          n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
   DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[0], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st, m0));
   DTC_TRY(cap_masked(n, "grad.stem.dz", G[0], n.MA0, M0, 64, st));
   DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
   DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
   DTC_TRY(join_side(n, st));  // the stem wgrad is the last kernel: run it on the main stream
   PROF(2, 2.0 * M0 * 64 * 27,
-       conv_wgrad(n.stem.s, n.at<u16>(n.X0), dc0, n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st, ts));
+       n.stem_direct ? stem_wgrad(n.at<float>(n.XIN), dc0, n.gf(n.stem.pidx), gs, n.B, n.H, n.W, slab, n.slab_bytes, st, ts)
+                     : conv_wgrad(n.stem.s, n.at<u16>(n.X0), dc0, n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st, ts));
   DTC_TRY(maybe_bucket(n, -1, cx, st));
   if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
   return 0;
@@ -1107,7 +1129,8 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
   DTC_TRY(join_side(n, st));  // the stem wgrad is the last kernel: run it on the main stream
   PROF(2, 2.0 * M0 * 64 * 27,
-       conv_wgrad(n.stem.s, n.at<u16>(n.X0), dc0, n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st, ts));
+       n.stem_direct ? stem_wgrad(n.at<float>(n.XIN), dc0, n.gf(n.stem.pidx), gs, n.B, n.H, n.W, slab, n.slab_bytes, st, ts)
+                     : conv_wgrad(n.stem.s, n.at<u16>(n.X0), dc0, n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st, ts));
   DTC_TRY(maybe_bucket(n, -1, cx, st));
   if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
   return 0;
@@ -1343,9 +1366,14 @@ int dtc_rn18_profile_begin(dtc_net* net, int capacity) {
 }
 
 int dtc_rn18_profile_end(dtc_net* net, double* ms_by_kind, double* flops_by_kind, int* count_by_kind) {
-  DTC_CHECK_ARG(net != nullptr, "dtc_rn18_profile_end: null net");
+  return dtc_rn18_profile_end_ex(net, 3, ms_by_kind, flops_by_kind, count_by_kind);
+}
+
+int dtc_rn18_profile_end_ex(dtc_net* net, int nkinds, double* ms_by_kind, double* work_by_kind, int* count_by_kind) {
+  DTC_CHECK_ARG(net != nullptr && nkinds >= 1 && nkinds <= 4, "dtc_rn18_profile_end_ex: bad args");
+  double* flops_by_kind = work_by_kind;
   Net& n = net->n;
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < nkinds; ++k) {
     if (ms_by_kind) ms_by_kind[k] = 0;
     if (flops_by_kind) flops_by_kind[k] = 0;
     if (count_by_kind) count_by_kind[k] = 0;
@@ -1358,6 +1386,7 @@ int dtc_rn18_profile_end(dtc_net* net, double* ms_by_kind, double* flops_by_kind
     const u64 calls = acc[2 * i + 1];
     if (calls == 0) continue;
     const int k = n.prof_kind[i];
+    if (k >= nkinds) continue;
     if (ms_by_kind) ms_by_kind[k] += (double)acc[2 * i] / (double)n.prof_khz;
     if (flops_by_kind) flops_by_kind[k] += n.prof_flops[i] * (double)calls;
     if (count_by_kind) count_by_kind[k] += (int)calls;

@@ -274,6 +274,194 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   stamp_end(p.ts);
 }
 
+// ---------------------------------------------------------------- one wave per SIMD
+// The same GEMM with 4 waves, each owning 144 GEMM rows (9 A fragments) x ALL 64 output channels
+// (4 B fragments): 13 fragment reads per 36 MFMAs per k-step (0.36 per MFMA, vs 0.61 with 8 waves
+// of 144 x 32), so LDS reads (and their latency) per MFMA drop by 40%; the accumulators (144
+// registers) live in AGPRs. With one wave per SIMD nothing else hides an LDS read's latency, so the
+// step's 26 fragments (k-step 0: B0..B3, A0..A8; k-step 1 likewise) are read D fragments ahead of
+// the MFMA group that consumes them, in one unrolled stream: at most ~2D tr reads in flight (the
+// lgkmcnt field counts 15), each read's latency behind the MFMAs of the fragments before it.
+// NS-stage LDS ring as wgrad_halo_kernel; each wave issues 2*NR halo + 2 dy DMA instructions per
+// stage (two 32-row halves of every 64-row round).
+template <int NS, int NR, int D>
+__global__ void __launch_bounds__(256, 1) wgrad_halo4_kernel(const HaloParams p) {
+  typedef WgStage<NR> SG;
+  constexpr int HI = 2 * NR;  // halo DMA instructions per wave per stage
+  constexpr int PER = HI + 2;  // + dy
+  static_assert((NS - 2) * PER < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * SG::BYTES];
+  stamp_start(p.ts);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ktiles = p.K >> 6;
+  const int c0 = (blockIdx.x / ktiles) * 64, k0 = (blockIdx.x % ktiles) * 64;
+  const int split = blockIdx.y;
+  const unsigned z = blockIdx.z;
+  const u16* const px = uniform_ptr(z == 0 ? p.xs[0] : z == 1 ? p.xs[1] : z == 2 ? p.xs[2] : p.xs[3]);
+  const u16* const pdy = uniform_ptr(z == 0 ? p.dys[0] : z == 1 ? p.dys[1] : z == 2 ? p.dys[2] : p.dys[3]);
+  const int st_begin = split * p.steps_per_split;
+  const int st_end = min(p.nsteps, st_begin + p.steps_per_split);
+  const int W2 = p.W + 2;
+
+  // ---- halo DMA: instruction u covers LDS rows (u/2)*64 + ((u%2)*4 + wave)*8 + lane/8, chunk lane%8
+  int hrel[HI], hrow_in[HI];
+  bool hcol[HI];
+#pragma unroll
+  for (int u = 0; u < HI; ++u) {
+    const int hrow = (u >> 1) * 64 + ((u & 1) * 4 + wave) * 8 + (lane >> 3);
+    const int ii = hrow / p.hb, rem = hrow - ii * p.hb;
+    const int hr = rem / W2, wc = rem - hr * W2;
+    const int src_chunk = (lane & 7) ^ trswz(hrow);
+    hcol[u] = hrow < p.nh && wc >= 1 && wc <= p.W;
+    hrow_in[u] = hr - 1;
+    hrel[u] = (((ii * p.H + hr - 1) * p.W + wc - 1) * p.C + c0 + src_chunk * 8) * 2;
+  }
+  // ---- dy DMA: instruction v covers rows (v*4 + wave)*8 + lane/8 of the 64-pixel step
+  int trow[2], dcol[2];
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    trow[v] = (v * 4 + wave) * 8 + (lane >> 3);
+    dcol[v] = k0 + (((lane & 7) ^ trswz(trow[v])) * 8);
+  }
+  auto stage = [&](char* sb, int step) {
+    const int m0 = step * 64;
+    const int n0 = (int)fdiv((uint32_t)m0, p.fd_hw);
+    const int p0 = (int)fdiv((uint32_t)(m0 - n0 * (int)p.fd_hw.d), p.fd_w);
+    const int base = ((n0 * p.H + p0) * p.W) * p.C * 2;
+#pragma unroll
+    for (int u = 0; u < HI; ++u) {
+      const bool ok = hcol[u] && (unsigned)(p0 + hrow_in[u]) < (unsigned)p.H;
+      buf_lds16(px, p.x_bytes, sb + ((u >> 1) * 64 + ((u & 1) * 4 + wave) * 8) * 128,
+                ok ? (uint32_t)(base + hrel[u]) : 0x80000000u);
+    }
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+      glds16(pdy + (size_t)(m0 + trow[v]) * p.K + dcol[v], sb + SG::HALO_BYTES + (v * 4 + wave) * 1024);
+  };
+
+  // ---- per-lane LDS byte offsets of every fragment half (as wgrad_halo_kernel, wm = wave, wn = 0)
+  int hm[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int t = ks * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2) + 4 * h;
+      const int ii = t / p.spi, rem = t - ii * p.spi;
+      const int pr = rem / p.W, q = rem - pr * p.W;
+      hm[ks][h] = ii * p.hb + pr * W2 + q;
+    }
+  uint32_t aoff[2][9][2], boff[2][4][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int row = wave * 144 + i * 16;
+      const int tap = row >> 6, cin = row & 63;
+      const int toff = (tap / 3) * W2 + (tap % 3);
+      const int unit = (cin >> 2) + (lane & 3);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ra = hm[ks][h] + toff;
+        const int f = (((ra >> 1) & 1) << 2) | (((ra >> 3) & 1) << 3);
+        aoff[ks][i][h] = (uint32_t)(ra * 128 + ((unit ^ f) << 3));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int li = lane & 15, q = li >> 2, pp = li & 3, g = lane >> 4;
+      const int unit = ((j * 16) >> 2) + pp;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int kr = ks * 32 + g * 8 + q + 4 * h;
+        const int f = (((kr >> 1) & 1) << 2) | (((kr >> 3) & 1) << 3);
+        boff[ks][j][h] = (uint32_t)(SG::HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
+      }
+    }
+  }
+  typedef __attribute__((address_space(3))) bf16x4_t lds_v4;
+  auto tr8 = [&](const char* sb, uint32_t o0, uint32_t o1) {
+    const bf16x4_t t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(sb + o0));
+    const bf16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(sb + o1));
+    return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+
+  f32x4 acc[9][4];
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment q of a step: k-step q / 13; r = q % 13: 0..3 = B (dy) fragment r, 4..12 = A (halo) r - 4
+  auto compute = [&](const char* sb, bf16x8 fz) {
+    constexpr int NF = 26;
+    bf16x8 f[NF];
+    auto ld = [&](int q) {
+      const int ks = q / 13, r = q % 13;
+      if (p.diag == 4) {  // diagnostics: no LDS reads in the loop (fragments read once per step)
+        f[q] = fz;
+        return;
+      }
+      f[q] = r < 4 ? tr8(sb, boff[ks][r][0], boff[ks][r][1]) : tr8(sb, aoff[ks][r - 4][0], aoff[ks][r - 4][1]);
+    };
+    int cur = 0;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const int q = ks * 13 + 4 + i;  // the A fragment this group consumes
+        const int target = q + 1 + D < NF ? q + 1 + D : NF;
+#pragma unroll
+        for (; cur < target; ++cur) ld(cur);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[q], f[ks * 13 + j], acc[i][j], 0, 0, 0);
+        // pin the order: the scheduler would otherwise sink each read next to its first use
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  if (st_begin < st_end) {
+    const int nk = st_end - st_begin;
+#pragma unroll
+    for (int i = 0; i < NS - 1; ++i)
+      if (i < nk) stage(smem + i * SG::BYTES, st_begin + i);
+    for (int it = 0; it < nk; it += NS) {
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        const int k = it + u;
+        if (k >= nk) break;
+        if (k + NS - 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PER) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // diagnostics (option wgrad_diag, WRONG results): 5 = no DMA after the prologue
+        if (k + NS - 1 < nk && p.diag != 5) stage(smem + ((u + NS - 1) % NS) * SG::BYTES, st_begin + k + NS - 1);
+        const bf16x8 fz = p.diag == 4 ? tr8(smem + u * SG::BYTES, aoff[0][0][0], aoff[0][0][1]) : bf16x8{};
+        compute(smem + u * SG::BYTES, fz);
+      }
+    }
+  }
+
+  if (p.nostore) {
+    stamp_end(p.ts);
+    return;
+  }
+  const int RSC = 9 * p.C;
+  float* slab = p.slab + blockIdx.z * p.slab_stride + (size_t)split * p.K * RSC;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int row = wave * 144 + i * 16 + 4 * (lane >> 4);
+    const int rsc = (row >> 6) * p.C + c0 + (row & 63);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kout = k0 + j * 16 + (lane & 15);
+      *(f32x4*)(slab + (size_t)kout * RSC + rsc) = acc[i][j];
+    }
+  }
+  stamp_end(p.ts);
+}
+
 // ---------------------------------------------------------------- host side
 static bool halo_geometry(const ConvShape& s, int& rs, int& imgs) {
   if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.C % 64 == 0 && s.K % 64 == 0)) return false;
@@ -334,6 +522,15 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
   const bool deep = option_get(OPT_WGRAD_STAGES) >= 4;
   const int pf = option_get(OPT_WGRAD_PF);
+  if (option_get(OPT_WGRAD_KERNEL) != 0) {  // one wave per SIMD (wgrad_halo4_kernel), 4-stage ring
+#define DTC_WH4(NR_, D_) hipLaunchKernelGGL((wgrad_halo4_kernel<4, NR_, D_>), grid, dim3(256), 0, st, p)
+    if (nr <= 2) { if (pf >= 6) DTC_WH4(2, 6); else DTC_WH4(2, 4); }
+    else { if (pf >= 6) DTC_WH4(3, 6); else DTC_WH4(3, 4); }
+#undef DTC_WH4
+    DTC_LAUNCH_CHECK();
+    *used_splits = used;
+    return 0;
+  }
 #define DTC_WH(NS_, NR_, PF_) hipLaunchKernelGGL((wgrad_halo_kernel<NS_, NR_, PF_>), grid, dim3(512), 0, st, p)
   if (nr <= 2) {
     if (pf >= 8) { if (deep) DTC_WH(4, 2, 8); else DTC_WH(2, 2, 8); }

@@ -181,6 +181,24 @@ def stem_im2col(x):
     return cols
 
 
+def stem_fwd(x, w27, stats=None):
+    """Direct stem conv (dtc_stem_fwd): x [N,3,H,W] fp32, w27 [64,27] bf16 (KRSC) -> y [N,H,W,64] bf16."""
+    n, _, h, w = x.shape
+    y = torch.empty(n, h, w, 64, dtype=torch.bfloat16, device=x.device)
+    call("dtc_stem_fwd", ptr(x), ptr(w27), ptr(y), ptr(stats), n, h, w, stream_ptr())
+    return y
+
+
+def stem_wgrad(x, dy, scale=1.0):
+    """Direct stem weight gradient (dtc_stem_wgrad): x [N,3,H,W] fp32, dy [N,H,W,64] bf16 -> [64,27] fp32."""
+    n, _, h, w = x.shape
+    nb = lib.dtc_stem_wgrad_workspace_size(n, h, w)
+    ws = torch.empty(nb // 4 + 64, dtype=torch.float32, device=x.device)
+    dw = torch.empty(64, 27, dtype=torch.float32, device=x.device)
+    call("dtc_stem_wgrad", ptr(x), ptr(dy), ptr(dw), float(scale), n, h, w, ptr(ws), nb, stream_ptr())
+    return dw
+
+
 def stem_pack_weight(w27):
     k = w27.shape[0]
     w64 = torch.empty(k, 64, dtype=torch.bfloat16, device=w27.device)

@@ -116,6 +116,16 @@ int dtc_bn_bwd_apply(const uint16_t* dz, const uint16_t* x1, const float* coef1,
  * loss: nn.CrossEntropyLoss() (trainer.py:40, 155), mean reduction. */
 int dtc_stem_im2col(const float* x_nchw, uint16_t* cols, int n, int h, int w, void* stream);
 int dtc_stem_pack_weight(const uint16_t* w27, uint16_t* w64, int k, void* stream);
+/* Direct stem conv (the executor's default): y [n*h*w][64] bf16 = conv1(x) from fp32 NCHW x and the
+ * bf16 KRSC weight [64][27], the 27 taps gathered per 256-pixel tile into LDS (no im2col matrix in
+ * HBM); stats (optional, [32][2][64] fp64, accumulated) = BN batch sums of the bf16 outputs. The
+ * weight gradient dw27 [64][27] fp32 = scale * sum_pixels dy (x) taps(x), workspace from
+ * dtc_stem_wgrad_workspace_size. */
+int dtc_stem_fwd(const float* x_nchw, const uint16_t* w27, uint16_t* y, double* stats, int n, int h, int w,
+                 void* stream);
+size_t dtc_stem_wgrad_workspace_size(int n, int h, int w);
+int dtc_stem_wgrad(const float* x_nchw, const uint16_t* dy, float* dw27, float scale, int n, int h, int w, void* ws,
+                   size_t ws_bytes, void* stream);
 int dtc_head_fwd(const uint16_t* act, int n, int hw, int c, const uint16_t* wfc, const float* bfc, int ncls,
                  float* feat, float* logits, void* stream);
 size_t dtc_head_bwd_workspace_size(int n, int c, int ncls);
@@ -286,6 +296,10 @@ int dtc_rn18_capture_info(const dtc_net* net, int idx, const char** name, size_t
  * (index 0 = forward, 1 = dgrad, 2 = wgrad: ms, algorithmic FLOPs, calls) and disarms. */
 int dtc_rn18_profile_begin(dtc_net* net, int capacity);
 int dtc_rn18_profile_end(dtc_net* net, double* ms_by_kind, double* flops_by_kind, int* count_by_kind);
+/* The same with nkinds (1..4) entries per array; kind 3 = the BatchNorm family of the mask-bit path
+ * (forward finalize+apply, backward reduce, backward finalize+apply), work = algorithmic HBM bytes
+ * (every tensor the kernel must touch, read or written once: the in-step BN HBM roofline). */
+int dtc_rn18_profile_end_ex(dtc_net* net, int nkinds, double* ms_by_kind, double* work_by_kind, int* count_by_kind);
 
 #ifdef __cplusplus
 }

@@ -233,6 +233,31 @@ def test_stem_im2col(dtc, cuda):
     assert not cols[..., 27:].any()
 
 
+@pytest.mark.parametrize("shape", [(2, 6, 5), (4, 32, 32), (3, 7, 9)])
+def test_stem_direct_fwd_wgrad(dtc, cuda, shape):
+    """Direct stem conv (stem.hip: taps gathered per 256-pixel tile, one K=32 MFMA k-step) vs the
+    oracle conv on the same bf16 operands (conv1 = nn.Conv2d(3, 64, 3, 1, 1), net.py:91): forward
+    (bf16 output), its BN batch sums, and the fp32 weight gradient; ragged last tiles included."""
+    n, h, w = shape
+    g = np.random.default_rng(12)
+    x = g.standard_normal((n, 3, h, w)).astype(np.float32)
+    w27 = _rand_bf16((64, 3, 3, 3), g, scale=0.2)
+    dy = _rand_bf16((n, h, w, 64), g)
+    xd = torch.from_numpy(x).to(cuda)
+    xb = O.bf16(O.nchw_to_nhwc(x))  # the kernel rounds the gathered taps to bf16
+    stats = dtc.ops.new_stats(64, cuda)
+    y = dtc.ops.stem_fwd(xd, _to_dev_bf16(w27.reshape(64, 27), cuda), stats).float().cpu().numpy()
+    ref = O.conv2d_fwd(xb, w27, 1, 1)
+    assert rel_err(y, O.bf16(ref)) < 1e-2
+    st = stats.sum(0).cpu().numpy()
+    yb = y.reshape(-1, 64).astype(np.float64)
+    np.testing.assert_allclose(st[0], yb.sum(0), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(st[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
+    dw = dtc.ops.stem_wgrad(xd, _to_dev_bf16(dy, cuda), scale=0.5).cpu().numpy()
+    ref_w = 0.5 * O.conv2d_wgrad(xb, dy, 3, 3, 1, 1).reshape(64, 27)
+    assert rel_err(dw, ref_w) < 1e-5
+
+
 def test_sgd_and_amp(dtc, cuda):
     n = 4096
     g = np.random.default_rng(9)

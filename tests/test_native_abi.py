@@ -83,7 +83,7 @@ def test_workspace_and_conv_plans(dtc):
     dtc._native.call("dtc_rn18_create", C.byref(h), 256, 32, 32, 100, 25.0)
     ws = lib.dtc_rn18_workspace_bytes(h)
     assert 0.3e9 < ws < 3e9, ws
-    assert lib.dtc_rn18_num_activations(h) == 3 + 8 * 4 + 3 + 1
+    assert lib.dtc_rn18_num_activations(h) == 2 + 8 * 4 + 3 + 1  # direct stem: no im2col image
     lib.dtc_rn18_destroy(h)
     d = dtc._native.ConvDesc(256, 4, 4, 512, 512, 3, 3, 1, 1)
     assert lib.dtc_conv2d_workspace_size(d, 2) > 0  # wgrad always wants split-K slabs
