@@ -62,8 +62,6 @@ template <int MODE, bool PF>
 __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   constexpr int FM = 4, FN = 4;  // wave tile: 64 channels x 64 pixels
   constexpr bool FWD = MODE == 0, RES = MODE == 2 || MODE == 4, BNB = MODE >= 3;
-  // VMEM ops one tile's epilogue leaves in flight per wave: stores (+ residual loads) (+ y, x loads)
-  constexpr int EPI_VM = 16 + (RES ? 16 : 0) + (BNB ? 32 : 0);
   __shared__ __attribute__((aligned(1024))) char smem[C64_WBYTES + 2 * C64_HBYTES];
   char* const halo = smem + C64_WBYTES;
   stamp_start(p.ts);
@@ -157,21 +155,43 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     }
   }
 
-  // epilogue of one finished tile: exactly FM*FN buffer stores per wave (+ as many residual loads);
-  // lanes of pixels past M, or of no tile (have == false), are dropped by the descriptor bound
-  auto epilogue_col = [&](const f32x4 (&a)[FM][FN], int tile, bool have, int j) {
-    typedef int i32x2 __attribute__((ext_vector_type(2)));
-    const int px0 = tile * 256;  // tiles are 256 consecutive pixels
-    const int pix = px0 + bcol0 + j * 16 + fpx;
+  // DGRAD residual of one tile, loaded one tile AHEAD of its use: issued right after the tile's
+  // halo wait, before the next halo DMA, so it has landed by the next iteration's halo wait and the
+  // epilogue (interleaved with the following tile's MFMAs) never waits on it. Loading it inside the
+  // epilogue stalled the wave's only SIMD on a full HBM latency per pixel-column group (and on the
+  // younger halo DMA: vmcnt retires in order): 74 -> 26 us per layer1 dgrad at B=256. The fused
+  // BN-backward operands (y, x; option bnb_fuse) are still loaded in the epilogue: prefetching them
+  // too would need 96 more VGPRs than the wave has.
+  typedef int i32x2 __attribute__((ext_vector_type(2)));
+  struct EpiOps {
+    i32x2 r[FN][FM];
+  };
+  // VMEM ops the previous tile's epilogue leaves in flight per wave at the halo wait: stores (+ y, x)
+  constexpr int EPI_VM = 16 + (BNB ? 32 : 0);
+  auto epi_off = [&](int tile, int j, int i) {
+    const int pix = tile * 256 + bcol0 + j * 16 + fpx;  // tiles are 256 consecutive pixels
+    return pix < M ? (uint32_t)((pix * 64 + i * 16 + rq) * 2) : 0x80000000u;
+  };
+  auto prefetch = [&](EpiOps& o, int tile) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const uint32_t off = epi_off(tile, j, i);
+        o.r[j][i] = __builtin_amdgcn_raw_buffer_load_b64(rrsrc, off, 0, 0);
+      }
+  };
+
+  // epilogue of one finished tile: exactly FM*FN buffer stores per wave; lanes of pixels past M, or
+  // of no tile (have == false), are dropped by the descriptor bound
+  auto epilogue_col = [&](const f32x4 (&a)[FM][FN], const EpiOps& o, int tile, bool have, int j) {
+    const int pix = tile * 256 + bcol0 + j * 16 + fpx;
     const bool ok = have && pix < M;
     uint32_t off[FM];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) off[i] = ok ? (uint32_t)((pix * 64 + i * 16 + rq) * 2) : 0x80000000u;
-    // DGRAD operands of all FM fragments issued before any is used (one latency per column group)
-    i32x2 rr[FM], yy[FM], xx[FM];
+    i32x2 yy[FM], xx[FM];
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      if constexpr (RES) rr[i] = __builtin_amdgcn_raw_buffer_load_b64(rrsrc, off[i], 0, 0);
+      off[i] = ok ? epi_off(tile, j, i) : 0x80000000u;
       if constexpr (BNB) {  // out-of-range lanes read zeros (descriptor bound): masked to 0, no sums
         yy[i] = __builtin_amdgcn_raw_buffer_load_b64(yrsrc, off[i], 0, 0);
         xx[i] = __builtin_amdgcn_raw_buffer_load_b64(xrsrc, off[i], 0, 0);
@@ -192,8 +212,9 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = a[i][j][t];
         if constexpr (RES) {
-          v[0] += bf_lo((uint32_t)rr[i].x); v[1] += bf_hi((uint32_t)rr[i].x);
-          v[2] += bf_lo((uint32_t)rr[i].y); v[3] += bf_hi((uint32_t)rr[i].y);
+          const i32x2 rr = o.r[j][i];
+          v[0] += bf_lo((uint32_t)rr.x); v[1] += bf_hi((uint32_t)rr.x);
+          v[2] += bf_lo((uint32_t)rr.y); v[3] += bf_hi((uint32_t)rr.y);
         }
         if constexpr (BNB) {
           const float yv[4] = {bf_lo((uint32_t)yy[i].x), bf_hi((uint32_t)yy[i].x), bf_lo((uint32_t)yy[i].y),
@@ -214,9 +235,9 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
       __builtin_amdgcn_raw_buffer_store_b64(wv, orsrc, off[i], 0, 0);
     }
   };
-  auto epilogue = [&](const f32x4 (&a)[FM][FN], int tile, bool have) {
+  auto epilogue = [&](const f32x4 (&a)[FM][FN], const EpiOps& o, int tile, bool have) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j) epilogue_col(a, tile, have, j);
+    for (int j = 0; j < FN; ++j) epilogue_col(a, o, tile, have, j);
   };
 
   f32x4 accp[FM][FN];
@@ -224,21 +245,21 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) accp[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  EpiOps opp{}, opc{};  // residual of the previous / current tile (modes 2, 4)
   int tilep = 0;
   int k = 0;
   int tile = blockIdx.x;
   if (tile < p.ntiles) stage_halo(halo, tile);
   for (; tile < p.ntiles; tile += gridDim.x, ++k) {
-    // this tile's halo has landed; the previous iteration's epilogue VMEM ops (FM*FN stores, plus
-    // FM*FN residual loads) were issued after it and may still be in flight
+    // this tile's halo (and the residual issued before it) have landed; the previous iteration's
+    // epilogue VMEM ops (FM*FN stores, + the BN-backward y/x loads) were issued after it
     if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (EPI_VM >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
     else if constexpr (EPI_VM == 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-    else if constexpr (EPI_VM == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const uint32_t hb = halo_lds + (uint32_t)((k & 1) * C64_HBYTES);
+    if constexpr (RES) prefetch(opc, tile);
     const int tn = tile + gridDim.x;
     if (tn < p.ntiles) stage_halo(halo + ((k + 1) & 1) * C64_HBYTES, tn);
 
@@ -273,7 +294,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[g & 1][i], bfr[g & 1][j], acc[i][j], 0, 0, 0);
         // the previous tile's epilogue, one pixel-column group after each odd tap's second k-step
-        if ((g & 3) == 3) epilogue_col(accp, tilep, k > 0, g >> 2);
+        if ((g & 3) == 3) epilogue_col(accp, opp, tilep, k > 0, g >> 2);
       }
     } else {
 #pragma unroll
@@ -294,7 +315,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
         }
         // the previous tile's epilogue, one pixel-column group after each odd tap (placed between
         // MFMA groups so the scheduler spreads it over the MFMA issue gaps)
-        if (t & 1) epilogue_col(accp, tilep, k > 0, t >> 1);
+        if (t & 1) epilogue_col(accp, opp, tilep, k > 0, t >> 1);
       }
     }
 #pragma unroll
@@ -302,8 +323,9 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) accp[i][j] = acc[i][j];
     tilep = tile;
+    if constexpr (RES) opp = opc;
   }
-  if (k > 0) epilogue(accp, tilep, true);
+  if (k > 0) epilogue(accp, opp, tilep, true);
 
   if constexpr (FWD || BNB) {
     double* const sacc = BNB ? p.bnb.acc1 : p.stats;

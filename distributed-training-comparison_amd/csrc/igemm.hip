@@ -880,7 +880,9 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
   }
   int splits = pl.splits;
   if (pl.bm == 576 && slab_bytes >= pl.slab_bytes) {
-    DTC_TRY(conv_wgrad_halo(s, 1, &x, &dy, slab, pl.splits, &splits, st, ts));
+    const bool whole = (dw_cols <= 0 || dw_cols == p.RSC) && (dw_ld <= 0 || dw_ld == p.RSC);
+    DTC_TRY(conv_wgrad_halo(s, 1, &x, &dy, slab, pl.splits, &splits, st, ts, whole ? &dw : nullptr, scale));
+    if (splits == 0) return 0;  // one split: the halo kernel wrote dw itself
   } else {
     if (pl.bm == 576) pl = ConvPlan{64, 64, 1, ceil_div(p.M, 64), 0};  // workspace too small for the halo plan
     p.num_kt = pl.num_kt;
@@ -917,7 +919,8 @@ int conv_wgrad_batch(const ConvShape& s, int nprob, const u16* const* x, const u
   if (hs <= 0 || slab == nullptr || slab_bytes < conv_wgrad_batch_slab_bytes(s, nprob))
     return set_error(DTC_EINVAL, "conv_wgrad_batch: no halo plan for %d problems or slab too small", nprob);
   int splits = hs;
-  DTC_TRY(conv_wgrad_halo(s, nprob, x, dy, slab, hs, &splits, st, ts));
+  DTC_TRY(conv_wgrad_halo(s, nprob, x, dy, slab, hs, &splits, st, ts, dw, scale));
+  if (splits == 0) return 0;  // one split: the halo kernel wrote dw itself
   const int RSC = s.R * s.S * s.C;
   WgOuts outs{};
   for (int i = 0; i < nprob; ++i) outs.dw[i] = dw[i];

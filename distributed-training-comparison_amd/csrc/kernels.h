@@ -39,6 +39,8 @@ enum {
   OPT_BARRIER_SPIN = 20,   // dtc_barrier host wait: 1 = poll the completion event, 0 = hipEventSynchronize
   OPT_WGRAD_KERNEL = 21,   // wgrad_halo: 0 = 8 waves (144 x 32 per wave), 1 = 4 waves (144 x 64, one per SIMD)
   OPT_STEM_DIRECT = 22,    // executor (at plan time): 1 = direct stem conv (stem.hip), 0 = im2col + GEMM
+  OPT_WGRAD_XCD = 23,      // wgrad_halo: 1 = the tiles of one (problem, split) are dispatched to one XCD
+  OPT_WGRAD_DIRECT = 24,   // wgrad_halo: 1 = a one-split launch writes the scaled dw itself (no reduce)
   OPT_COUNT
 };
 int option_get(int id);
@@ -79,8 +81,10 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
 // slab[nprob][used][K][9C] (reduce separately).
 constexpr int DTC_WG_BATCH = 4;
 int wgrad_halo_splits(const ConvShape& s, int nprob = 1);
+// dw (optional): when the launch uses ONE split its epilogue writes dw[i] = scale * sum directly (no
+// slab, no reduce; *used_splits = 0 tells the caller), else slab[nprob][used][K][9C] as above.
 int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* slab, int splits,
-                    int* used_splits, hipStream_t st, u64* ts);
+                    int* used_splits, hipStream_t st, u64* ts, float* const* dw = nullptr, float scale = 1.f);
 // nprob (<= DTC_WG_BATCH) independent weight gradients of one 3x3 stride-1 geometry in one halo
 // launch + one reduce launch: dw[i] = scale * wgrad(x[i], dy[i]). Returns DTC_EINVAL when the
 // geometry has no halo plan or the slab is too small (callers then issue them one by one).

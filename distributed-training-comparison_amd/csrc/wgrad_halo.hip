@@ -30,6 +30,9 @@ struct HaloParams {
   const u16* xs[DTC_WG_BATCH];   // per problem: NHWC [N][H][W][C]
   const u16* dys[DTC_WG_BATCH];  // per problem: NPQK [N][H][W][K] (stride 1, pad 1: P = H, Q = W)
   float* slab;     // [problem][splits][K][9*C]
+  float* dws[DTC_WG_BATCH];  // direct: per problem dw [K][9*C] (one split: no slab, no reduce)
+  float scale;     // direct: dw = scale * sum
+  int direct;
   size_t slab_stride;  // floats per problem
   int N, H, W, C, K;
   uint32_t x_bytes;
@@ -39,8 +42,32 @@ struct HaloParams {
   int spi;         // pixels per image block of a step (rs * W)
   int nostore;     // diagnostics only (option wgrad_diag = 1): skip the slab stores (wrong results)
   int diag;        // diagnostics only: 2 = no halo DMA after the first stage, 3 = no dy DMA after it
+  int xcd;         // 1: XCD-grouped decode of the workgroup id (wg_coords)
   u64* ts;
 };
+
+// (output tile, split, problem) of this workgroup. Workgroups are dispatched to the 8 XCDs round-robin
+// by linear id, so with the plain grid decode the tiles of one (problem, split) -- which read the same
+// x halo (tiles of one input-channel slice) and the same dy rows (tiles of one output-channel slice) --
+// land on different XCDs and each XCD's L2 fetches those operands again. With xcd = 1 the linear id is
+// renumbered so every XCD owns a contiguous range of (problem, split, tile) triples: the tiles of a
+// (problem, split) run on one XCD at the same time and share its L2.
+__device__ __forceinline__ void wg_coords(const HaloParams& p, int& tile, int& split, unsigned& z) {
+  if (!p.xcd) {
+    tile = blockIdx.x;
+    split = blockIdx.y;
+    z = blockIdx.z;
+    return;
+  }
+  const unsigned T = gridDim.x * gridDim.y * gridDim.z;
+  const unsigned L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const unsigned r = L & 7, q = T >> 3, rem = T & 7;
+  const unsigned Lp = r * q + min(r, rem) + (L >> 3);
+  tile = (int)(Lp % gridDim.x);
+  const unsigned g = Lp / gridDim.x;
+  split = (int)(g % gridDim.y);
+  z = g / gridDim.y;
+}
 
 template <typename T>
 __device__ __forceinline__ T* uniform_ptr(T* ptr) {
@@ -84,11 +111,12 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   stamp_start(p.ts);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ktiles = p.K >> 6;
-  const int c0 = (blockIdx.x / ktiles) * 64, k0 = (blockIdx.x % ktiles) * 64;
-  const int split = blockIdx.y;
+  int tile, split;
+  unsigned z;
+  wg_coords(p, tile, split, z);
+  const int c0 = (tile / ktiles) * 64, k0 = (tile % ktiles) * 64;
   // problem pointers as scalar selects (a dynamically indexed kernarg array would land in VGPRs, and
   // the LDS-DMA buffer descriptor must be scalar)
-  const unsigned z = blockIdx.z;
   const u16* const px = uniform_ptr(z == 0 ? p.xs[0] : z == 1 ? p.xs[1] : z == 2 ? p.xs[2] : p.xs[3]);
   const u16* const pdy = uniform_ptr(z == 0 ? p.dys[0] : z == 1 ? p.dys[1] : z == 2 ? p.dys[2] : p.dys[3]);
   const int st_begin = split * p.steps_per_split;
@@ -260,7 +288,10 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     return;
   }
   const int RSC = 9 * p.C;
-  float* slab = p.slab + blockIdx.z * p.slab_stride + (size_t)split * p.K * RSC;
+  // one split: the final weight gradient itself (scale * sum, exactly what wgrad_reduce would write)
+  float* const slab = p.direct ? uniform_ptr(z == 0 ? p.dws[0] : z == 1 ? p.dws[1] : z == 2 ? p.dws[2] : p.dws[3])
+                               : p.slab + z * p.slab_stride + (size_t)split * p.K * RSC;
+  const float osc = p.direct ? p.scale : 1.f;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int row = wm * 144 + i * 16 + 4 * (lane >> 4);
@@ -268,7 +299,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int kout = k0 + wn * 32 + j * 16 + (lane & 15);
-      *(f32x4*)(slab + (size_t)kout * RSC + rsc) = acc[i][j];
+      *(f32x4*)(slab + (size_t)kout * RSC + rsc) = acc[i][j] * osc;
     }
   }
   stamp_end(p.ts);
@@ -294,9 +325,10 @@ __global__ void __launch_bounds__(256, 1) wgrad_halo4_kernel(const HaloParams p)
   stamp_start(p.ts);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ktiles = p.K >> 6;
-  const int c0 = (blockIdx.x / ktiles) * 64, k0 = (blockIdx.x % ktiles) * 64;
-  const int split = blockIdx.y;
-  const unsigned z = blockIdx.z;
+  int tile, split;
+  unsigned z;
+  wg_coords(p, tile, split, z);
+  const int c0 = (tile / ktiles) * 64, k0 = (tile % ktiles) * 64;
   const u16* const px = uniform_ptr(z == 0 ? p.xs[0] : z == 1 ? p.xs[1] : z == 2 ? p.xs[2] : p.xs[3]);
   const u16* const pdy = uniform_ptr(z == 0 ? p.dys[0] : z == 1 ? p.dys[1] : z == 2 ? p.dys[2] : p.dys[3]);
   const int st_begin = split * p.steps_per_split;
@@ -448,7 +480,10 @@ __global__ void __launch_bounds__(256, 1) wgrad_halo4_kernel(const HaloParams p)
     return;
   }
   const int RSC = 9 * p.C;
-  float* slab = p.slab + blockIdx.z * p.slab_stride + (size_t)split * p.K * RSC;
+  // one split: the final weight gradient itself (scale * sum, exactly what wgrad_reduce would write)
+  float* const slab = p.direct ? uniform_ptr(z == 0 ? p.dws[0] : z == 1 ? p.dws[1] : z == 2 ? p.dws[2] : p.dws[3])
+                               : p.slab + z * p.slab_stride + (size_t)split * p.K * RSC;
+  const float osc = p.direct ? p.scale : 1.f;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int row = wave * 144 + i * 16 + 4 * (lane >> 4);
@@ -456,7 +491,7 @@ __global__ void __launch_bounds__(256, 1) wgrad_halo4_kernel(const HaloParams p)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int kout = k0 + j * 16 + (lane & 15);
-      *(f32x4*)(slab + (size_t)kout * RSC + rsc) = acc[i][j];
+      *(f32x4*)(slab + (size_t)kout * RSC + rsc) = acc[i][j] * osc;
     }
   }
   stamp_end(p.ts);
@@ -493,7 +528,7 @@ int wgrad_halo_splits(const ConvShape& s, int nprob) {
 }
 
 int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* slab, int splits,
-                    int* used_splits, hipStream_t st, u64* ts) {
+                    int* used_splits, hipStream_t st, u64* ts, float* const* dw, float scale) {
   int rs = 0, imgs = 0;
   DTC_CHECK_ARG(halo_geometry(s, rs, imgs) && splits > 0 && nprob >= 1 && nprob <= DTC_WG_BATCH,
                 "wgrad_halo: unsupported geometry");
@@ -516,8 +551,13 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   p.ts = ts;
   p.nostore = option_get(OPT_WGRAD_DIAG) == 1;
   p.diag = option_get(OPT_WGRAD_DIAG);
+  p.xcd = option_get(OPT_WGRAD_XCD);
   const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
   p.slab_stride = (size_t)used * s.K * 9 * s.C;
+  p.direct = used == 1 && dw != nullptr && option_get(OPT_WGRAD_DIRECT) != 0;
+  if (p.direct)
+    for (int i = 0; i < nprob; ++i) p.dws[i] = dw[i];
+  p.scale = scale;
   dim3 grid((s.C / 64) * (s.K / 64), used, nprob);
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
   const bool deep = option_get(OPT_WGRAD_STAGES) >= 4;
@@ -528,7 +568,7 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
     else { if (pf >= 6) DTC_WH4(3, 6); else DTC_WH4(3, 4); }
 #undef DTC_WH4
     DTC_LAUNCH_CHECK();
-    *used_splits = used;
+    *used_splits = p.direct ? 0 : used;
     return 0;
   }
 #define DTC_WH(NS_, NR_, PF_) hipLaunchKernelGGL((wgrad_halo_kernel<NS_, NR_, PF_>), grid, dim3(512), 0, st, p)
@@ -543,7 +583,7 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   }
 #undef DTC_WH
   DTC_LAUNCH_CHECK();
-  *used_splits = used;
+  *used_splits = p.direct ? 0 : used;
   return 0;
 }
 

@@ -46,6 +46,8 @@ def main():
     dev = torch.device("cuda:0")
     B = args.batch
     variants = [dict(kv.split("=") for kv in v.split(",")) for v in args.variants.split(";")]
+    # every variant starts from the library defaults of the options any variant names (no leaks)
+    defaults = {k: nat.lib.dtc_get_option(k.encode()) for k in sorted({k for v in variants for k in v})}
     results = {i: {} for i in range(len(variants))}
     layers = [l for l in LAYERS if not args.layers or l[0] in args.layers.split(",")]
     passes = args.passes.split(",")
@@ -58,6 +60,7 @@ def main():
         y = torch.empty(B, P, P, K, device=dev).bfloat16()
         dx = torch.empty(B, H, H, C, device=dev).bfloat16()
         dw = torch.empty(K, R, R, C, device=dev)
+        res = torch.randn(B, H, H, C, device=dev).bfloat16()
         stats = ops.new_stats(K, dev)
         d = ops.conv_desc(B, H, H, C, K, R, R, st, pad)
         wsb = max(nat.lib.dtc_conv2d_workspace_size(d, m) for m in range(3))
@@ -68,20 +71,25 @@ def main():
             "fwd": lambda: nat.call("dtc_conv2d_fwd", d, P_(x), P_(w), P_(y), P_(stats), P_(ws), wsb, nat.stream_ptr()),
             "dgrad": lambda: nat.call("dtc_conv2d_dgrad", d, P_(dy), P_(w), P_(dx), None, P_(ws), wsb,
                                       nat.stream_ptr()),
+            # dgrad + residual (identity blocks' conv1: the shortcut's gradient added in the epilogue)
+            "dgradr": lambda: nat.call("dtc_conv2d_dgrad", d, P_(dy), P_(w), P_(dx), P_(res), P_(ws), wsb,
+                                       nat.stream_ptr()),
             "wgrad": lambda: nat.call("dtc_conv2d_wgrad", d, P_(x), P_(dy), P_(dw), 1.0, P_(ws), wsb,
                                       nat.stream_ptr()),
         }
         if name == "stem":
             fns.pop("dgrad")
+            fns.pop("dgradr")
         fns = {k: v for k, v in fns.items() if k in passes}
         if args.fresh:
             xs, dys = x.clone(), dy.clone()
-            copies = {"fwd": lambda: x.copy_(xs), "dgrad": lambda: dy.copy_(dys), "wgrad": lambda: dy.copy_(dys)}
+            copies = {"fwd": lambda: x.copy_(xs), "dgrad": lambda: dy.copy_(dys), "dgradr": lambda: dy.copy_(dys),
+                      "wgrad": lambda: dy.copy_(dys)}
             fns = {k: (lambda f=f, c=copies[k]: (c(), f())) for k, f in fns.items()}
             fns.update({"copy_" + k: copies[k] for k in list(fns)})
         for rnd in range(3):  # interleaved rounds
             for vi, var in enumerate(variants):
-                for k, v in var.items():
+                for k, v in {**defaults, **var}.items():
                     nat.call("dtc_set_option", k.encode(), int(v))
                 for pname, fn in fns.items():
                     fn()

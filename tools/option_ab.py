@@ -26,6 +26,8 @@ def main():
     dev = torch.device("cuda:0")
     B = args.batch
     variants = [dict(kv.split("=") for kv in v.split(",")) for v in args.variants.split(";")]
+    # every variant starts from the library defaults of the options any variant names (no leaks)
+    defaults = {k: nat.lib.dtc_get_option(k.encode()) for k in sorted({k for v in variants for k in v})}
     bad = 0
     g = torch.Generator(device=dev).manual_seed(0)
     for (name, H, C, K, R, st, _) in LAYERS:
@@ -37,7 +39,7 @@ def main():
         d = ops.conv_desc(B, H, H, C, K, R, R, st, pad)
         outs = []
         for var in variants:
-            for k, v in var.items():
+            for k, v in {**defaults, **var}.items():
                 nat.call("dtc_set_option", k.encode(), int(v))
             wsb = max(nat.lib.dtc_conv2d_workspace_size(d, m) for m in range(3))
             ws = torch.empty(wsb // 4 + 64, device=dev)
