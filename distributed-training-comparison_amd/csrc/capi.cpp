@@ -12,11 +12,11 @@
 #include <cstring>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {2}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {0}, {1}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
                                              "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
                                              "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse",
-                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct"};
+                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct", "wgrad_defer", "igemm_tile", "igemm_split", "bn_onepass"};
 static std::atomic<int> g_epoch{0};
 int option_get(int id) { return g_opts[id].load(std::memory_order_relaxed); }
 int option_epoch() { return g_epoch.load(std::memory_order_relaxed); }
@@ -146,6 +146,23 @@ int dtc_bn_bwd_finalize(double* acc, int c, int64_t count, const float* gamma, c
 int dtc_bn_bwd_apply(const uint16_t* dz, const uint16_t* x1, const float* coef1, uint16_t* dx1, const uint16_t* x2,
                      const float* coef2, uint16_t* dx2, int64_t m, int c, void* stream) {
   return bn_bwd_apply(dz, x1, coef1, dx1, x2, coef2, dx2, m, c, S(stream));
+}
+
+int dtc_bn_bwd_onepass_ok(int64_t m, int c, int dual) {
+  int R = 0;
+  return bn_bwd_fused_plan(m, c, dual != 0, &R) > 0 ? 1 : 0;
+}
+int dtc_bn_bwd_onepass(const uint16_t* dy, const uint8_t* mbits, uint16_t* dzo, const uint16_t* x1, const float* mean1,
+                       const float* invstd1, const float* gamma1, double* acc1, float* dgamma1, float* dbeta1,
+                       uint16_t* dx1, const uint16_t* x2, const float* mean2, const float* invstd2, const float* gamma2,
+                       double* acc2, float* dgamma2, float* dbeta2, uint16_t* dx2, int64_t count, float gscale,
+                       int64_t m, int c, int* counter, int* err, void* stream) {
+  BnBwdArgs a1;
+  a1.acc = acc1; a1.count = count; a1.gamma = gamma1; a1.mean = mean1; a1.invstd = invstd1; a1.gscale = gscale;
+  a1.dgamma = dgamma1; a1.dbeta = dbeta1;
+  BnBwdArgs a2 = a1;
+  a2.acc = acc2; a2.gamma = gamma2; a2.mean = mean2; a2.invstd = invstd2; a2.dgamma = dgamma2; a2.dbeta = dbeta2;
+  return bn_bwd_fused(dy, mbits, dzo, x1, a1, dx1, x2, x2 ? &a2 : nullptr, dx2, m, c, counter, err, S(stream));
 }
 
 int dtc_stem_im2col(const float* x, uint16_t* cols, int n, int h, int w, void* stream) {

@@ -721,8 +721,13 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
     if (A == 64) { pl.bm = 64; pl.bn = 256; }
     else { pl.bm = 128; pl.bn = 128; }
     if ((A / pl.bm) * ceil_div(M, pl.bn) < 400) { pl.bm = 64; pl.bn = 64; }
+    const int ft = option_get(OPT_IGEMM_TILE);  // tuning override
+    if (ft == 1) { pl.bm = 64; pl.bn = 64; }
+    else if (ft == 2 && A % 128 == 0) { pl.bm = 128; pl.bn = 128; }
+    else if (ft == 3) { pl.bm = 64; pl.bn = 256; }
     const int tiles = (A / pl.bm) * ceil_div(M, pl.bn);
     pl.splits = (tiles >= 256 || cls) ? 1 : pick_splits(tiles, num_kt, 480, 8);
+    if (option_get(OPT_IGEMM_SPLIT) > 0 && !cls) pl.splits = std::min(option_get(OPT_IGEMM_SPLIT), num_kt);
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * M * A * 4 : 0;
     pl.slab_bytes = std::max(pl.slab_bytes, conv_halo_slab_bytes(s, mode));
     pl.num_kt = num_kt;
@@ -738,8 +743,12 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
     pl.bm = (s.C == 64 || s.K == 64) ? 64 : 128;
     pl.bn = pl.bm;
     if ((s.R * s.S * s.C / pl.bm) * (s.K / pl.bn) < 64) pl.bm = pl.bn = 64;  // few output tiles: more of them
+    const int ft = option_get(OPT_IGEMM_TILE);  // tuning override
+    if (ft == 1) pl.bm = pl.bn = 64;
+    else if (ft == 2 && (s.R * s.S * s.C) % 128 == 0 && s.K % 128 == 0) pl.bm = pl.bn = 128;
     const int tiles = (s.R * s.S * s.C / pl.bm) * (s.K / pl.bn);
     pl.splits = pick_splits(tiles, num_kt, 512, tiles < 64 ? 8 : 16);
+    if (option_get(OPT_IGEMM_SPLIT) > 0) pl.splits = std::min(option_get(OPT_IGEMM_SPLIT), num_kt);
     pl.slab_bytes = (size_t)pl.splits * s.K * s.R * s.S * s.C * 4;
     pl.num_kt = num_kt;
   }

@@ -29,7 +29,7 @@ enum {
                           // kernels: 1 conv_c64, 2 conv_halo, 4 split-K reduce (others: separate pass).
                           // Default 0: measured neutral (c64, split-K) to -1% (halo) at B=256 -- the
                           // epilogue's strided 8-B y/x loads cost what the separate pass costs.
-  OPT_WGRAD_STAGES = 13,   // LDS ring depth of wgrad_halo (2: one step of DMA in flight; 4: three)
+  OPT_WGRAD_STAGES = 13,   // LDS ring depth of wgrad_halo (2: one step of DMA in flight; 4 (default): three)
   OPT_HALO_WSTAGES = 14,   // weight ring depth of conv_halo (2 or 3)
   OPT_WGRAD_DIAG = 15,     // diagnostics only: 1 = wgrad_halo skips its slab stores (WRONG results)
   OPT_WGRAD_PF = 16,       // wgrad_halo LDS fragment prefetch window (0 = compiler-scheduled, 5, 8)
@@ -39,8 +39,15 @@ enum {
   OPT_BARRIER_SPIN = 20,   // dtc_barrier host wait: 1 = poll the completion event, 0 = hipEventSynchronize
   OPT_WGRAD_KERNEL = 21,   // wgrad_halo: 0 = 8 waves (144 x 32 per wave), 1 = 4 waves (144 x 64, one per SIMD)
   OPT_STEM_DIRECT = 22,    // executor (at plan time): 1 = direct stem conv (stem.hip), 0 = im2col + GEMM
-  OPT_WGRAD_XCD = 23,      // wgrad_halo: 1 = the tiles of one (problem, split) are dispatched to one XCD
+  OPT_WGRAD_XCD = 23,      // wgrad_halo: 1 (default) = the tiles of one (problem, split) run on one XCD
   OPT_WGRAD_DIRECT = 24,   // wgrad_halo: 1 = a one-split launch writes the scaled dw itself (no reduce)
+  OPT_WGRAD_DEFER = 25,    // executor: 1 = batched wgrads forked after the layer's last dgrad (see resnet.cpp)
+  OPT_IGEMM_TILE = 26,     // igemm FWD/DGRAD/WGRAD tile: 0 auto, 1 = 64x64, 2 = 128x128, 3 = 64x256 (tuning)
+  OPT_IGEMM_SPLIT = 27,    // igemm split-K: 0 auto, k = k splits where the plan allows (tuning)
+  OPT_BN_ONEPASS = 28,     // executor: 1 = one-pass BN backward (bn_bwd_fused, grid barrier) where it has a
+                           // plan; 2 = the same with release/acquire fences. Default 0: measured slower at
+                           // B=256 (23-52 us per launch vs 11-20 us for the reduce + apply pair: the
+                           // device-wide barrier costs more than the re-read it saves)
   OPT_COUNT
 };
 int option_get(int id);
@@ -187,6 +194,13 @@ int bn_bwd_fin_apply_mask(const u16* dy, const uint8_t* mbits, u16* dzo, const u
                           const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st,
                           u64* ts = nullptr);
 int bn_mask_apply(const u16* dy, const uint8_t* mbits, u16* dz, int64_t M, int C, hipStream_t st);
+// One-pass mask-bit BN backward (bn_bwd_reduce_mask + bn_bwd_fin_apply_mask in one launch with a grid
+// barrier; slice in registers): plan = rows per workgroup (0: no plan, use the two kernels). counter: an
+// int zeroed before the launch; *err set to 1 if the barrier ever timed out.
+int bn_bwd_fused_plan(int64_t M, int C, bool dual, int* R_out);
+int bn_bwd_fused(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
+                 const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, int* counter, int* err,
+                 hipStream_t st, u64* ts = nullptr);
 int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
                      u16* dx2, int64_t M, int C, hipStream_t st);
 int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2, const BnFwdArgs* a2, float* y,
@@ -252,6 +266,8 @@ int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int
 int sgd_nesterov(float* p, const float* g, float* mom, u16* p_bf16, int64_t n, float lr, float wd, float mu,
                  const float* inv_scale, const int* found_inf, hipStream_t st);
 int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st);
+// zero an 8-byte aligned range (a kernel node, unlike hipMemsetAsync's fill dispatch)
+int zero_bytes(void* p, size_t bytes, hipStream_t st);
 // x[i] *= f (loopback test communicator)
 int scale_f32(float* x, int64_t n, float f, hipStream_t st);
 int scale_f64(double* x, int64_t n, double f, hipStream_t st);

@@ -60,6 +60,21 @@ int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st) {
   return 0;
 }
 
+__global__ void zero_kernel(uint2* __restrict__ p, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = uint2{0u, 0u};
+}
+
+// A kernel, not hipMemsetAsync: inside a captured graph a memset node is a separate (fill) dispatch
+int zero_bytes(void* p, size_t bytes, hipStream_t st) {
+  DTC_CHECK_ARG(p && bytes % 8 == 0 && ((uintptr_t)p & 7) == 0, "zero_bytes: 8-byte aligned ranges only");
+  if (bytes == 0) return 0;
+  const int64_t n = (int64_t)(bytes / 8);
+  const int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(zero_kernel, dim3(blocks), dim3(256), 0, st, (uint2*)p, n);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 template <typename T>
 __global__ void scale_kernel(T* __restrict__ x, int64_t n, T f) {
   for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) x[i] *= f;

@@ -47,6 +47,7 @@ struct BNL {
   int64_t rm_off = 0, rv_off = 0;
   int nbt = 0;
   size_t stats = 0, acc = 0, mean = 0, invstd = 0, scale = 0, shift = 0, coef = 0;  // workspace byte offsets
+  size_t bar = 0;  // one-pass backward's grid-barrier counter (zeroed with the slots)
 };
 
 struct BlockL {
@@ -82,6 +83,7 @@ struct Net {
   bool stem_direct = false;  // planned with option stem_direct (bf16): stem.hip instead of im2col + GEMM
   size_t HEADWS = 0, HEADWS_bytes = 0;
   size_t DC0 = 0, SLABW = 0;  // stem conv-output gradient; split-K slab of the side-stream wgrads
+  size_t BNERR = 0;           // int: set by a one-pass BN backward whose grid barrier timed out
   // backward weight gradients run on a side stream (option bwd_streams), overlapped with the
   // data-gradient / BN chain; forked after the conv-output gradient exists, joined at bucket points
   hipStream_t side_st = nullptr;
@@ -319,10 +321,12 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   }
   n.DC0 = take(M0 * 64 * E);
   // BN per-layer state
-  n.stats_lo = off;  // forward statistics of every BN, then backward sums: each zeroed by one memset node
+  n.stats_lo = off;  // forward statistics of every BN, then backward sums: both zeroed by the training forward
   for (BNL* b : n.bns) b->stats = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
   n.acc_lo = off;
   for (BNL* b : n.bns) b->acc = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
+  for (BNL* b : n.bns) b->bar = take(8 * 64);  // BF_LINES counters, 64 B apart
+  n.BNERR = take(256);
   n.stats_hi = off;
   for (BNL* b : n.bns) {
     b->mean = take(b->C * 4);
@@ -529,7 +533,9 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   if (n.f32) return forward_body_f32(n, logits, train, st);
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
   n.prof_next = train ? 0 : Net::PROF_SLOTS;  // eval passes are not timed
-  if (train) DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.acc_lo - n.stats_lo, st));
+  // the forward statistics AND the backward sums of every BN (the backward that follows this training
+  // forward accumulates into zeroed slots; its graph then starts with real work, no memset node)
+  if (train) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));
   if (n.stem_direct) {  // stem.hip: taps gathered per tile from the fp32 input, one K=32 k-step
     PROF(0, 2.0 * M0 * 64 * 27,
          stem_fwd(n.at<float>(n.XIN), n.wbf(n.stem.pidx), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
@@ -598,7 +604,7 @@ static int forward_body_f32(Net& n, float* logits, bool train, hipStream_t st) {
   float* slab = n.at<float>(n.SLAB);
   n.prof_next = train ? 0 : Net::PROF_SLOTS;
   DTC_TRY(f32_stem_pack_weight(n.pf(n.stem.pidx), n.at<float>(n.WSTEM), 64, st));
-  if (train) DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.acc_lo - n.stats_lo, st));
+  if (train) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));  // + the backward sums
   PROF(0, 2.0 * M0 * 64 * 27,
        conv_f32(f32_stem_shape(n), CONV_FWD, n.at<float>(n.X0), n.at<float>(n.WSTEM), n.at<float>(n.C0), nullptr,
                 train ? n.at<double>(n.bn0.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
@@ -640,7 +646,7 @@ static int backward_body_f32(Net& n, const float* dlogits, float gs, const BwdCt
   for (int i = 0; i < 6; ++i) G[i] = n.at<float>(n.G[i]);
   float* slab = n.at<float>(n.SLAB);
   const BlockL& last = n.blocks.back();
-  DTC_HIP(hipMemsetAsync(n.ws + n.acc_lo, 0, n.stats_hi - n.acc_lo, st));
+  // the BN backward sums were zeroed by the training forward (forward_body)
   DTC_TRY(head_bwd(dlogits, n.at<float>(n.FEAT), n.pf(n.fc_w), n.B, last.Hout * last.Wout, 512, n.ncls, gs,
                    n.gf(n.fc_w), n.gf(n.fc_b), G[0], n.at<float>(n.HEADWS), n.HEADWS_bytes, st));
   for (int bi = (int)n.blocks.size() - 1; bi >= 0; --bi) {
@@ -831,6 +837,21 @@ static int bn_bwd_coef_apply(Net& n, BNL& b1, const u16* dz, const u16* x1, u16*
   return bn_bwd_apply(dz, x1, n.at<float>(b1.coef), dx1, x2, b2 ? n.at<float>(b2->coef) : nullptr, dx2, M, b1.C, st);
 }
 
+// One-pass BN backward (bn.hip bn_bwd_fused: reduce + grid barrier + apply in one launch, the slice in
+// registers) where it has a plan; else bn_bwd_reduce_mask + bn_bwd_coef_apply. Same outputs.
+static bool onepass_ok(const Net& n, int64_t M, int C, bool dual) {
+  int R = 0;
+  return option_get(OPT_BN_ONEPASS) != 0 && n.sync == nullptr && bn_fused() && bn_bwd_fused_plan(M, C, dual, &R) > 0;
+}
+static int bn_bwd_onepass(Net& n, BNL& b1, const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, u16* dx1,
+                          BNL* b2, const u16* x2, u16* dx2, int64_t M, float gs, hipStream_t st) {
+  const BnBwdArgs a1 = bwd_args(n, b1, M, gs);
+  const BnBwdArgs a2 = b2 ? bwd_args(n, *b2, M, gs) : BnBwdArgs{};
+  u64* ts = prof_slot(n, 3, (double)M * b1.C * (6.125 + (x2 ? 4.0 : 0.0) + (dzo ? 2.0 : 0.0)));
+  return bn_bwd_fused(dy, mbits, dzo, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, n.at<int>(b1.bar),
+                      n.at<int>(n.BNERR), st, ts);
+}
+
 // Side stream for the weight gradients (fork after their input gradient exists, join before
 // anything reads the weight gradients: bucket all-reduces and the end of backward).
 static bool side_on(const Net& n) { return option_get(OPT_BWD_STREAMS) != 0; }
@@ -914,7 +935,7 @@ static int wg_flush(Net& n, WgQueue& q, float gs, float* slabw, hipStream_t sd) 
   return 0;
 }
 static int wg_issue(Net& n, WgQueue& q, const ConvShape& s, const u16* x, const u16* dy, float* dw, float gs,
-                    float* slabw, hipStream_t sd) {
+                    float* slabw, hipStream_t sd, bool defer = false) {
   const int bmax = wgrad_batch_max();
   if (bmax <= 1 || wgrad_halo_splits(s, 2) <= 0) {
     PROF(2, conv_flops(s), conv_wgrad(s, x, dy, dw, 0, 0, gs, slabw, n.slab_bytes, sd, ts));
@@ -925,7 +946,7 @@ static int wg_issue(Net& n, WgQueue& q, const ConvShape& s, const u16* x, const 
   q.x[q.count] = x;
   q.dy[q.count] = dy;
   q.dw[q.count] = dw;
-  if (++q.count >= bmax) DTC_TRY(wg_flush(n, q, gs, slabw, sd));
+  if (++q.count >= bmax && !defer) DTC_TRY(wg_flush(n, q, gs, slabw, sd));
   return 0;
 }
 // (the plan's bucket points, with or without a communicator: the batches -- and so the split-K
@@ -957,7 +978,7 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   float* slabw = n.at<float>(n.SLABW);
   hipStream_t sd = st;  // weight-gradient stream
   const BlockL& last = n.blocks.back();
-  DTC_HIP(hipMemsetAsync(n.ws + n.acc_lo, 0, n.stats_hi - n.acc_lo, st));
+  // the BN backward sums were zeroed by the training forward (forward_body)
   DTC_TRY(head_bwd(dlogits, n.at<float>(n.FEAT), n.wbf(n.fc_w), n.B, last.Hout * last.Wout, 512, n.ncls, gs,
                    n.gf(n.fc_w), n.gf(n.fc_b), G[0], n.at<float>(n.HEADWS), n.HEADWS_bytes, st));
   WgQueue wq;
@@ -973,29 +994,42 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     const std::string cp = n.capture ? "grad.layer" + std::to_string(bi / 2 + 1) + "." + std::to_string(bi % 2) : "";
     DTC_TRY(cap(n, cp + ".dy", G[0], st));
     DTC_TRY(cap_masked(n, cp + ".dz", G[0], b.MOUT, M, b.Cout, st));
-    // out = relu(bn2(c2) + shortcut): sums of dz = dy * [out > 0] (and of the projection BN)
-    PROF(3, (double)M * b.Cout * (b.proj ? 6.125 : 4.125),
-         bn_bwd_reduce_mask(G[0], mout, n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
-                            n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
-                            b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
-                            b.proj ? n.at<double>(b.bsc.acc) : nullptr, M, b.Cout, st, ts));
+    // out = relu(bn2(c2) + shortcut): sums of dz = dy * [out > 0] (and of the projection BN), then
     // dc2 (and dsc); an identity block also needs dz itself as conv1's dgrad residual: in place in G[0]
-    DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[0], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
-                              b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st, mout, b.proj ? nullptr : G[0]));
+    if (onepass_ok(n, M, b.Cout, b.proj)) {
+      DTC_TRY(bn_bwd_onepass(n, b.b2, G[0], mout, b.proj ? nullptr : G[0], n.at<u16>(b.C2), dc2,
+                             b.proj ? &b.bsc : nullptr, b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st));
+    } else {
+      PROF(3, (double)M * b.Cout * (b.proj ? 6.125 : 4.125),
+           bn_bwd_reduce_mask(G[0], mout, n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
+                              n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
+                              b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
+                              b.proj ? n.at<double>(b.bsc.acc) : nullptr, M, b.Cout, st, ts));
+      DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[0], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
+                                b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st, mout, b.proj ? nullptr : G[0]));
+    }
     DTC_TRY(cap(n, cp + ".dc2", dc2, st));
     if (b.proj) DTC_TRY(cap(n, cp + ".ds", dsc, st));
+    // option wgrad_defer: the halo-geometry wgrads are only queued here; their batched launch is forked
+    // after the layer's last dgrad (below), so it overlaps the HBM-bound BN chain that follows rather
+    // than the dgrads (measured -1% at B=256: the wgrad batch then starves the BN kernels instead)
+    const bool defer = option_get(OPT_WGRAD_DEFER) != 0;
     DTC_TRY(fork_side(n, st, &sd));
-    DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd));
+    DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd, defer));
     PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts));
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
     DTC_TRY(cap_masked(n, cp + ".dz1", G[4], b.MA1, M, b.Cout, st));
-    PROF(3, (double)M * b.Cout * 4.125,
-         bn_bwd_reduce_mask(G[4], ma1, n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
-                            n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, M, b.Cout, st, ts));
-    DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st, ma1));
+    if (onepass_ok(n, M, b.Cout, false)) {
+      DTC_TRY(bn_bwd_onepass(n, b.b1, G[4], ma1, nullptr, n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st));
+    } else {
+      PROF(3, (double)M * b.Cout * 4.125,
+           bn_bwd_reduce_mask(G[4], ma1, n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
+                              n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, M, b.Cout, st, ts));
+      DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st, ma1));
+    }
     DTC_TRY(cap(n, cp + ".dc1", dc1, st));
     DTC_TRY(fork_side(n, st, &sd));
-    DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd));
+    DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, defer));
     if (b.proj) {
       PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
       PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
@@ -1005,17 +1039,28 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
       PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[0], slab, n.slab_bytes, st, ts));
     }
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
-    if (bucket_fires(n, bi)) DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
+    if (!defer) {
+      if (bucket_fires(n, bi)) DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
+    } else if (wq.count > 0 && (bi % 2 == 0 || wq.count >= wgrad_batch_max() || bucket_fires(n, bi))) {
+      // a layer's queued wgrads (its first block is the last one processed), a full queue, or a bucket
+      // point: launch the batch on the side stream once this block's dgrads are done
+      DTC_TRY(fork_side(n, st, &sd));
+      DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
+    }
     DTC_TRY(maybe_bucket(n, bi, cx, st));
   }
   // stem: a0 = relu(bn1(conv1(x)))
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
   u16* dc0 = n.at<u16>(n.DC0);
   const uint8_t* m0 = n.at<uint8_t>(n.MA0);
-  PROF(3, (double)M0 * 64 * 4.125,
-       bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
-                          n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
-  DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[0], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st, m0));
+  if (onepass_ok(n, M0, 64, false)) {
+    DTC_TRY(bn_bwd_onepass(n, n.bn0, G[0], m0, nullptr, n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st));
+  } else {
+    PROF(3, (double)M0 * 64 * 4.125,
+         bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
+                            n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
+    DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[0], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st, m0));
+  }
   DTC_TRY(cap_masked(n, "grad.stem.dz", G[0], n.MA0, M0, 64, st));
   DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
   DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
@@ -1039,7 +1084,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   float* slabw = n.at<float>(n.SLABW);
   hipStream_t sd = st;  // weight-gradient stream
   const BlockL& last = n.blocks.back();
-  DTC_HIP(hipMemsetAsync(n.ws + n.acc_lo, 0, n.stats_hi - n.acc_lo, st));
+  // the BN backward sums were zeroed by the training forward (forward_body)
   DTC_TRY(head_bwd(dlogits, n.at<float>(n.FEAT), n.wbf(n.fc_w), n.B, last.Hout * last.Wout, 512, n.ncls, gs,
                    n.gf(n.fc_w), n.gf(n.fc_b), G[0], n.at<float>(n.HEADWS), n.HEADWS_bytes, st));
   // fuse: the dgrad producing a BN output's gradient also does that BN's backward reduction
@@ -1413,6 +1458,15 @@ int dtc_rn18_forward(dtc_net* net, const float* x, float* logits, int train, voi
 int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_comm* comm, void* stream) {
   DTC_CHECK_ARG(net && net->n.ws && dlogits, "dtc_rn18_backward: unbound net or null pointer");
   return backward(net->n, dlogits, grad_scale, (Comm*)comm, (hipStream_t)stream);
+}
+
+int dtc_rn18_xent_backward(dtc_net* net, const float* logits, const int64_t* labels, const float* lse,
+                           const float* gscale, float grad_scale, dtc_comm* comm, void* stream) {
+  DTC_CHECK_ARG(net && net->n.ws && logits && labels && lse, "dtc_rn18_xent_backward: unbound net or null pointer");
+  Net& n = net->n;
+  float* dl = n.at<float>(n.DLOGITS);
+  DTC_TRY(xent_bwd(logits, labels, lse, gscale, n.B, n.ncls, dl, (hipStream_t)stream));
+  return backward(n, dl, grad_scale, (Comm*)comm, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -151,6 +151,11 @@ class Executor:
         call("dtc_rn18_backward", self.handle, ptr(dlogits), float(grad_scale), comm.handle if comm else None,
              stream_ptr())
 
+    def xent_backward(self, logits, labels, lse, gscale, grad_scale: float, comm) -> None:
+        """CrossEntropy backward into the executor's dlogits buffer + the network backward, one call."""
+        call("dtc_rn18_xent_backward", self.handle, ptr(logits), ptr(labels), ptr(lse), ptr(gscale),
+             float(grad_scale), comm.handle if comm else None, stream_ptr())
+
     def dlogits_buffer(self) -> torch.Tensor:
         """fp32 [batch, num_classes] view of the executor's own dlogits buffer: a loss gradient
         written here is consumed by backward() without the copy-in."""
@@ -256,8 +261,7 @@ class NativeLoss(torch.Tensor):
             if exe.generation != node.gen:
                 raise NativeError("ResNet backward: the executor ran another forward since this graph was built "
                                   "(one forward per backward is supported)")
-            dl = ops.xent_bwd(logits, labels, lse, gscale, out=exe.dlogits_buffer())
-            exe.backward(dl, model._grad_scale, model._comm)
+            exe.xent_backward(logits, labels, lse, gscale, model._grad_scale, model._comm)
             model._ensure_grads()
         else:  # DataParallel's gathered logits: xent backward, then the replicas' backward + reduce-add
             from .parallel import _DPFn

@@ -109,6 +109,18 @@ int dtc_bn_bwd_finalize(double* acc, int c, int64_t count, const float* gamma, c
                         const float* invstd, float gscale, float* dgamma, float* dbeta, float* coef, void* stream);
 int dtc_bn_bwd_apply(const uint16_t* dz, const uint16_t* x1, const float* coef1, uint16_t* dx1, const uint16_t* x2,
                      const float* coef2, uint16_t* dx2, int64_t m, int c, void* stream);
+/* One-pass mask-bit BN backward (the executor's default where it fits): dz = dy * bit (mbits: byte
+ * o/8 of element offset o, bit k = channel 8*(o%c/8)+k; the forward BN apply's ReLU mask), the sums,
+ * a grid barrier, dgamma/dbeta (x gscale) and dx1 = BN1-backward(dz, x1) [, dx2 = BN2-backward(dz, x2)]
+ * [, dzo = dz] in one launch -- dtc_bn_bwd_reduce + _finalize + _apply of both BNs. acc1/acc2: zeroed
+ * [32][2][c] fp64 slots; counter: 128 zeroed bytes; *err set to 1 if the grid barrier timed out.
+ * Returns DTC_EINVAL when (m, c) has no one-pass plan (dtc_bn_bwd_onepass_ok == 0). */
+int dtc_bn_bwd_onepass_ok(int64_t m, int c, int dual);
+int dtc_bn_bwd_onepass(const uint16_t* dy, const uint8_t* mbits, uint16_t* dzo, const uint16_t* x1, const float* mean1,
+                       const float* invstd1, const float* gamma1, double* acc1, float* dgamma1, float* dbeta1,
+                       uint16_t* dx1, const uint16_t* x2, const float* mean2, const float* invstd2, const float* gamma2,
+                       double* acc2, float* dgamma2, float* dbeta2, uint16_t* dx2, int64_t count, float gscale,
+                       int64_t m, int c, int* counter, int* err, void* stream);
 
 /* ------------------------------------------------------------------ stem, head, loss
  * stem: self.conv1 = nn.Conv2d(3, 64, 3, 1, 1) (net.py:91) as im2col [n*h*w][64] + GEMM.
@@ -261,7 +273,8 @@ int dtc_rn18_forward(dtc_net* net, const float* x, float* logits, int train, voi
 /* Gradients of every parameter, scaled by grad_scale (1/world for DDP's mean), written (not
  * accumulated) into the bound flat grad buffer. If comm != NULL each bucket is all-reduced (sum)
  * on the communicator's side stream as soon as backward has produced it; the call returns with
- * `stream` ordered after the last all-reduce. */
+ * `stream` ordered after the last all-reduce. Must follow a training-mode dtc_rn18_forward (one
+ * backward per forward: the forward saves the activations and zeroes the BN backward sums). */
 int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_comm* comm, void* stream);
 /* SyncBatchNorm (replaces nn.SyncBatchNorm.convert_sync_batchnorm(model), torch/nn/modules/
  * batchnorm.py, the conversion README.md:40 recommends; not called by the reference trainers).
@@ -272,6 +285,15 @@ int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_
  * communicator of its own, not the one passed to dtc_rn18_backward. Disables graph replay.
  * comm == NULL: per-rank statistics (the reference's BatchNorm2d). */
 int dtc_rn18_set_sync_bn(dtc_net* net, dtc_comm* comm);
+/* CrossEntropyLoss backward fused with the network backward (the reference's
+ * `scaler.scale(loss).backward()`, ddp/trainer.py:157, when the loss is nn.CrossEntropyLoss of the
+ * network's logits, trainer.py:40,155): dlogits = (softmax(logits) - onehot(labels)) * (*gscale) / N
+ * written into the executor's own dlogits buffer, then dtc_rn18_backward on it -- one call, so the
+ * two launches reach the GPU back to back (this runs right after the per-step barrier, when the GPU
+ * queue is empty). logits [batch][num_classes] fp32, labels int64 [batch], lse = the per-row
+ * log-sum-exp dtc_xent_fwd wrote, gscale: device fp32 scalar or NULL (1). */
+int dtc_rn18_xent_backward(dtc_net* net, const float* logits, const int64_t* labels, const float* lse,
+                           const float* gscale, float grad_scale, dtc_comm* comm, void* stream);
 /* Byte offset into the workspace of the executor's own fp32 [batch][num_classes] dlogits buffer.
  * A caller that writes the loss gradient there (e.g. the fused cross-entropy backward) and passes
  * that pointer to dtc_rn18_backward saves the graph path's copy-in. */

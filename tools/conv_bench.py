@@ -91,6 +91,10 @@ def main():
             for vi, var in enumerate(variants):
                 for k, v in {**defaults, **var}.items():
                     nat.call("dtc_set_option", k.encode(), int(v))
+                need = max(nat.lib.dtc_conv2d_workspace_size(d, m) for m in range(3))  # the variant's plan
+                if need > wsb:
+                    wsb = need
+                    ws = torch.empty(wsb // 4 + 64, device=dev)
                 for pname, fn in fns.items():
                     fn()
                     torch.cuda.synchronize()
