@@ -14,11 +14,12 @@ overflow and grows by 2 after 2000 clean steps. ``found_inf`` and the scale neve
 from __future__ import annotations
 
 import contextlib
+import weakref
 
 import torch
 
 from . import ops
-from .nn import is_autocast_enabled, scaled_loss, set_autocast_enabled
+from .nn import _PRESCALER, is_autocast_enabled, scaled_loss, set_autocast_enabled
 
 
 @contextlib.contextmanager
@@ -48,6 +49,7 @@ class GradScaler:
         self._tracker = None
         self._found_inf = None
         self._unscaled = False
+        self._version = 0  # bumped whenever the scale may change (update): invalidates prescaled losses
 
     def _lazy_init(self, device):
         if self._scale is None:
@@ -55,6 +57,7 @@ class GradScaler:
             self._inv_scale = torch.full((1,), 1.0 / self._init_scale, dtype=torch.float32, device=device)
             self._tracker = torch.zeros(1, dtype=torch.int32, device=device)
             self._found_inf = torch.zeros(1, dtype=torch.int32, device=device)
+            _PRESCALER[0] = weakref.ref(self)
 
     def is_enabled(self):
         return self._enabled
@@ -63,7 +66,7 @@ class GradScaler:
         if not self._enabled:
             return outputs
         self._lazy_init(outputs.device)
-        return scaled_loss(outputs, self._scale)
+        return scaled_loss(outputs, self._scale, self._version)
 
     def unscale_(self, optimizer) -> None:
         if not self._enabled or self._unscaled:
@@ -87,6 +90,7 @@ class GradScaler:
     def update(self, new_scale=None) -> None:
         if not self._enabled or self._scale is None:
             return
+        self._version += 1
         if new_scale is not None:
             self._scale.fill_(float(new_scale))
             self._inv_scale.fill_(1.0 / float(new_scale))

@@ -48,6 +48,9 @@ enum {
                            // plan; 2 = the same with release/acquire fences. Default 0: measured slower at
                            // B=256 (23-52 us per launch vs 11-20 us for the reduce + apply pair: the
                            // device-wide barrier costs more than the re-read it saves)
+  OPT_SC_STREAM = 29,      // executor: 1 = the projection shortcut's conv / dgrad on a stream of its own
+                           // (default 0: measured -2% at B=256, interleaved A/B; cross-stream graph edges
+                           // cost more than the overlap of the small launches gains)
   OPT_COUNT
 };
 int option_get(int id);

@@ -87,6 +87,9 @@ struct Net {
   // backward weight gradients run on a side stream (option bwd_streams), overlapped with the
   // data-gradient / BN chain; forked after the conv-output gradient exists, joined at bucket points
   hipStream_t side_st = nullptr;
+  hipStream_t sc_st = nullptr;  // the projection shortcut's conv (fwd) / dgrad branch (option sc_stream)
+  bool sc_pending = false;
+  size_t SLABSC = 0, slabsc_bytes = 0;  // split-K slab of the shortcut branch
   std::vector<hipEvent_t> evs;
   int ev_next = 0;
   bool side_pending = false;
@@ -356,6 +359,11 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.slab_bytes = slab;
   n.SLAB = take(slab);
   n.SLABW = take(slab);
+  size_t slabsc = 64 * 64 * 4;  // the shortcut branch runs beside the main-stream convs: its own slab
+  for (auto& b : n.blocks)
+    if (b.proj && !n.f32) slabsc = std::max({slabsc, plan_conv(b.sc.s, CONV_FWD).slab_bytes, plan_conv(b.sc.s, CONV_DGRAD).slab_bytes});
+  n.SLABSC = take(slabsc);
+  n.slabsc_bytes = slabsc;
   if (n.capture) {
     auto cap = [&](const std::string& nm, int h, int w, int c) {
       n.caps.push_back({nm, take((size_t)B * h * w * c * E), (int)B, h, w, c});
@@ -527,6 +535,8 @@ static int bn_act(Net& n, int mode, BNL& b, const u16* x, BNL* b2, const u16* x2
 
 static ConvShape f32_stem_shape(const Net& n);
 static int forward_body_f32(Net& n, float* logits, bool train, hipStream_t st);
+static int fork_sc(Net& n, hipStream_t st, hipStream_t* out);
+static int join_sc(Net& n, hipStream_t st);
 
 // everything after the input im2col (reads only executor-owned memory: capturable)
 static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
@@ -548,9 +558,17 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   }
   DTC_TRY(bn_act(n, 1, n.bn0, n.at<u16>(n.C0), nullptr, nullptr, n.at<u16>(n.A0), M0, train, st, n.MA0));
   const u16* in = n.at<u16>(n.A0);
+  n.ev_next = 0;
   for (auto& b : n.blocks) {
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
     float* slab = n.at<float>(n.SLAB);
+    if (b.proj) {  // the shortcut conv first, on its own stream when sc_stream is on (joined below)
+      hipStream_t ss = st;
+      DTC_TRY(fork_sc(n, st, &ss));
+      PROF(0, conv_flops(b.sc.s),
+           conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr,
+                    ss == st ? slab : n.at<float>(n.SLABSC), ss == st ? n.slab_bytes : n.slabsc_bytes, ss, ts));
+    }
     PROF(0, conv_flops(b.c1.s),
          conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
                   n.slab_bytes, st, ts));
@@ -559,9 +577,7 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
          conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
                   train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st, ts));
     if (b.proj) {
-      PROF(0, conv_flops(b.sc.s),
-           conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr,
-                    slab, n.slab_bytes, st, ts));
+      DTC_TRY(join_sc(n, st));
       DTC_TRY(bn_act(n, 3, b.b2, n.at<u16>(b.C2), &b.bsc, n.at<u16>(b.S), n.at<u16>(b.OUT), M, train, st, b.MOUT));
     } else {
       DTC_TRY(bn_act(n, 2, b.b2, n.at<u16>(b.C2), nullptr, in, n.at<u16>(b.OUT), M, train, st, b.MOUT));
@@ -888,6 +904,35 @@ static int join_side(Net& n, hipStream_t st) {
   return 0;
 }
 
+// The projection shortcut's 1x1 stride-2 conv is independent of conv1 / conv2 of its block (forward:
+// it reads the block input; backward: its dgrad needs only dsc). Both are small latency-bound launches,
+// so they run on a stream of their own beside the main chain (option sc_stream) and join before the
+// consumer (the dual BN apply; conv1's dgrad, which adds dx_sc as its residual).
+static bool sc_on(const Net& n) { return option_get(OPT_SC_STREAM) != 0 && !n.f32 && n.sync == nullptr; }
+static int fork_sc(Net& n, hipStream_t st, hipStream_t* out) {
+  if (!sc_on(n)) {
+    *out = st;
+    return 0;
+  }
+  if (!n.sc_st) DTC_HIP(hipStreamCreateWithFlags(&n.sc_st, hipStreamNonBlocking));
+  hipEvent_t ev;
+  DTC_TRY(next_event(n, &ev));
+  DTC_HIP(hipEventRecord(ev, st));
+  DTC_HIP(hipStreamWaitEvent(n.sc_st, ev, 0));
+  n.sc_pending = true;
+  *out = n.sc_st;
+  return 0;
+}
+static int join_sc(Net& n, hipStream_t st) {
+  if (!n.sc_pending) return 0;
+  hipEvent_t ev;
+  DTC_TRY(next_event(n, &ev));
+  DTC_HIP(hipEventRecord(ev, n.sc_st));
+  DTC_HIP(hipStreamWaitEvent(st, ev, 0));
+  n.sc_pending = false;
+  return 0;
+}
+
 // BN-backward reduction of the BN(s) whose post-ReLU output is `y`, for a dgrad epilogue (bnb_epi.h):
 // the conv producing dy stores dz = dy * [y > 0] and accumulates the sums bn_bwd_reduce would.
 static BnbArgs bnb_of(Net& n, size_t y, size_t x1, BNL& b1, size_t x2 = 0, BNL* b2 = nullptr) {
@@ -1010,6 +1055,13 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     }
     DTC_TRY(cap(n, cp + ".dc2", dc2, st));
     if (b.proj) DTC_TRY(cap(n, cp + ".ds", dsc, st));
+    const bool sc_branch = b.proj && sc_on(n);
+    if (sc_branch) {  // dx of the shortcut (conv1's dgrad residual) beside conv2's dgrad and BN1's backward
+      hipStream_t ss = st;
+      DTC_TRY(fork_sc(n, st, &ss));
+      PROF(1, conv_flops(b.sc.s),
+           conv_dgrad(b.sc.s, dsc, n.wbf(b.sc.pidx), G[5], nullptr, n.at<float>(n.SLABSC), n.slabsc_bytes, ss, ts));
+    }
     // option wgrad_defer: the halo-geometry wgrads are only queued here; their batched launch is forked
     // after the layer's last dgrad (below), so it overlaps the HBM-bound BN chain that follows rather
     // than the dgrads (measured -1% at B=256: the wgrad batch then starves the BN kernels instead)
@@ -1032,7 +1084,8 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, defer));
     if (b.proj) {
       PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
-      PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
+      if (sc_branch) DTC_TRY(join_sc(n, st));
+      else PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
       PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts));
       DTC_TRY(cap(n, cp + ".dxs", G[5], st));
     } else {  // residual = dz of this block's output (G[0], written by bn2's apply); dx over it in place
@@ -1271,6 +1324,7 @@ int dtc_rn18_destroy(dtc_net* net) {
     drop_graphs(net->n);
     if (net->n.cap_st) (void)hipStreamDestroy(net->n.cap_st);
     if (net->n.side_st) (void)hipStreamDestroy(net->n.side_st);
+    if (net->n.sc_st) (void)hipStreamDestroy(net->n.sc_st);
     for (auto& e : net->n.evs)
       if (e) (void)hipEventDestroy(e);
     prof_free(net->n);

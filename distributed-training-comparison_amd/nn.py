@@ -304,10 +304,30 @@ def _wrap_loss(value: torch.Tensor, graph_fn, fast, host_copy: bool = False) -> 
     return out
 
 
-def scaled_loss(loss: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
-    """loss * scale (GradScaler.scale); keeps the direct backward chain of a NativeLoss."""
+# The GradScaler most recently initialised (amp.GradScaler._lazy_init): the loss kernel's call also
+# enqueues loss * scale for it, while the GPU is still busy with the forward, so the scaler.scale(loss)
+# after the per-step barrier -- when the GPU queue is empty -- needs no launch of its own.
+_PRESCALER = [None]
+
+
+def prescale(loss: "NativeLoss") -> None:
+    ref = _PRESCALER[0]
+    sc = ref() if ref is not None else None
+    if sc is None or sc._scale is None or not sc._enabled:
+        return
+    loss._dtc_prescaled = (ops.amp_scale(loss.detach(), sc._scale), sc._scale, sc._version)
+
+
+def scaled_loss(loss: torch.Tensor, scale: torch.Tensor, version: int = -1) -> torch.Tensor:
+    """loss * scale (GradScaler.scale); keeps the direct backward chain of a NativeLoss. `version` is
+    the scaler's state version: a product enqueued with the loss for this very scale tensor and state
+    is reused (same value: the scale only changes in update(), which bumps the version)."""
     if isinstance(loss, NativeLoss):
         f = loss._dtc_fast
+        pre = loss.__dict__.get("_dtc_prescaled")
+        if pre is not None and pre[1] is scale and pre[2] == version:
+            return _wrap_loss(pre[0], lambda: loss._dtc_graph * scale,
+                              None if f is None else (f[0], f[1], f[2], f[3], scale))
         # the value on the native kernel (GradScaler K9: no torch elementwise launch in the step)
         return _wrap_loss(ops.amp_scale(loss.detach(), scale), lambda: loss._dtc_graph * scale,
                           None if f is None else (f[0], f[1], f[2], f[3], scale))
@@ -329,7 +349,9 @@ class CrossEntropyLoss(nn.Module):
             from .parallel import _DPFn
 
             if isinstance(node, (_NetFn._backward_cls, _DPFn._backward_cls)):
-                return _wrap_loss(loss, lambda: loss, (node, logits, labels, loss.grad_fn.lse, None), host_copy=True)
+                out = _wrap_loss(loss, lambda: loss, (node, logits, labels, loss.grad_fn.lse, None), host_copy=True)
+                prescale(out)
+                return out
         return loss
 
 

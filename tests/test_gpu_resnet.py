@@ -684,6 +684,33 @@ def test_native_barrier_waits_for_queued_work(dtc, cuda):
         comm.close()
 
 
+def test_scaled_loss_prescaled_with_the_loss(dtc, cuda):
+    """The loss call also enqueues loss * scale for the last initialised GradScaler (before the per-step
+    barrier); scaler.scale(loss) reuses it only for the same scale tensor and scaler state: the value
+    is loss * current scale before and after update() changes the scale, and a loss taken before an
+    update is scaled by the new scale when scale() is called after it."""
+    from importlib import import_module
+
+    nnmod = import_module(dtc.__name__ + ".nn")
+    model, _, x, y = _setup(dtc, cuda, 8, seed=13)
+    crit = dtc.CrossEntropyLoss()
+    scaler = dtc.GradScaler(init_scale=1024.0)
+    xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
+    scaler.scale(crit(model(xd), yd))  # initialises the scaler (registers it for prescaling)
+    loss = crit(model(xd), yd)
+    assert loss.__dict__.get("_dtc_prescaled") is not None
+    s1 = scaler.scale(loss)
+    assert s1.data_ptr() == loss._dtc_prescaled[0].data_ptr()  # no new launch: the prescaled product
+    assert float(s1) == float(loss) * 1024.0
+    stale = crit(model(xd), yd)
+    scaler.update(new_scale=4.0)  # changes the scale after `stale` was prescaled with 1024
+    s2 = scaler.scale(stale)
+    assert s2.data_ptr() != stale._dtc_prescaled[0].data_ptr()
+    assert float(s2) == float(stale) * 4.0
+    s2.backward()  # the direct backward chain still applies
+    assert isinstance(s2, nnmod.NativeLoss)
+
+
 def test_native_loss_item_and_dlogits_buffer(dtc, cuda):
     """NativeLoss.item() reads the pinned host copy taken right after the loss kernel: equal to the
     device value even when read after the backward and the optimizer step have been issued; the
