@@ -42,6 +42,7 @@ struct IGemmParams {
   int num_kt, kt_per_split, tiles_a;
   int xcd_remap;
   int cls;  // DGRAD, stride 2: blockIdx.z = output parity class (h%2, w%2); M counts class pixels
+  int cls_order;  // 1: blockIdx.z runs the classes heaviest first (option dgrad_class_order)
   // WGRAD fast path: each 64-pixel reduction step covers whole rows of one image (PQ % 64 == 0,
   // 64 % Q == 0) or whole images (64 % PQ == 0); tensors < 4 GiB so 32-bit buffer offsets work.
   int wg_fast;
@@ -84,8 +85,11 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   int num_kt = p.num_kt;
   if constexpr (MODE == MODE_DGRAD) {
     if (p.cls) {
-      cls_ph = blockIdx.z >> 1;
-      cls_pw = blockIdx.z & 1;
+      // heaviest class first: classes differ in tap count (pad 1: (0,0) 1 tap, (0,1)/(1,0) 2, (1,1) 4),
+      // and the dispatcher starts workgroups in z order -- the 4-tap class launched last set the tail
+      const int zc = (p.cls_order && (p.pad & 1)) ? 3 - (int)blockIdx.z : (int)blockIdx.z;
+      cls_ph = zc >> 1;
+      cls_pw = zc & 1;
       r0 = (cls_ph + p.pad) & 1;
       s0 = (cls_pw + p.pad) & 1;
       const int Rdim = (p.R - r0 + 1) >> 1;
@@ -818,6 +822,7 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
   p.tiles_a = s.C / pl.bm;
   if (dgrad_class_mode(s)) {  // four parity-class GEMMs in one launch (blockIdx.z), no split-K
     p.cls = 1;
+    p.cls_order = option_get(OPT_DGRAD_CLASS_ORDER);
     p.M = s.N * (s.H / 2) * (s.W / 2);
     p.fd_q = make_fastdiv(s.W / 2);
     p.fd_pq = make_fastdiv((s.H / 2) * (s.W / 2));

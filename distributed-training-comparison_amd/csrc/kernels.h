@@ -51,6 +51,7 @@ enum {
   OPT_SC_STREAM = 29,      // executor: 1 = the projection shortcut's conv / dgrad on a stream of its own
                            // (default 0: measured -2% at B=256, interleaved A/B; cross-stream graph edges
                            // cost more than the overlap of the small launches gains)
+  OPT_DGRAD_CLASS_ORDER = 30,  // stride-2 dgrad parity classes dispatched heaviest first (1) or in z order (0)
   OPT_COUNT
 };
 int option_get(int id);
