@@ -10,14 +10,38 @@
 
 #include <atomic>
 #include <cstring>
+#include <cstdlib>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {0}, {1}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
                                              "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
                                              "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse",
-                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct", "wgrad_defer", "igemm_tile", "igemm_split", "bn_onepass", "sc_stream", "dgrad_class_order"};
+                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct", "wgrad_defer", "igemm_tile", "igemm_split", "bn_onepass", "sc_stream", "dgrad_class_order", "head_fused", "stem_prologue"};
 static std::atomic<int> g_epoch{0};
+// DTC_OPTIONS="name=value,name=value" in the environment overrides defaults at library load (A/B and
+// bisection runs of whole test suites without code changes)
+static int apply_env_options() {
+  const char* e = getenv("DTC_OPTIONS");
+  if (!e) return 0;
+  std::string s(e);
+  size_t pos = 0;
+  while (pos < s.size()) {
+    size_t end = s.find(',', pos);
+    if (end == std::string::npos) end = s.size();
+    const std::string kv = s.substr(pos, end - pos);
+    const size_t eq = kv.find('=');
+    if (eq != std::string::npos) {
+      const std::string k = kv.substr(0, eq);
+      const int v = atoi(kv.c_str() + eq + 1);
+      for (int i = 0; i < OPT_COUNT; ++i)
+        if (k == g_opt_names[i]) g_opts[i].store(v);
+    }
+    pos = end + 1;
+  }
+  return 1;
+}
+static const int g_env_applied = apply_env_options();
 int option_get(int id) { return g_opts[id].load(std::memory_order_relaxed); }
 int option_epoch() { return g_epoch.load(std::memory_order_relaxed); }
 int option_set(const char* name, int value) {

@@ -308,11 +308,60 @@ __global__ void __launch_bounds__(256) head_bwd_x_kernel(const float* __restrict
   }
 }
 
+// One launch for the whole head backward (the first kernels after the per-step barrier, when the GPU
+// queue is empty, so every launch boundary here is exposed): workgroups [0, nw) compute dW / db, one
+// (class, 256-channel) strip each, summing over the images in order (dl[n][j] is workgroup-uniform,
+// feat rows coalesced); workgroups [nw, nw + N) compute dact of one image each (head_bwd_x's work).
+template <typename T>
+__global__ void __launch_bounds__(256) head_bwd_fused_kernel(const float* __restrict__ dl,
+                                                            const float* __restrict__ feat,
+                                                            const T* __restrict__ wfc, int N, int HW, int C, int ncls,
+                                                            float scale, float* __restrict__ dw,
+                                                            float* __restrict__ db, T* __restrict__ dact, int nw) {
+  typedef Elt<T> E;
+  __shared__ float row[1024];
+  const int t = threadIdx.x;
+  if ((int)blockIdx.x < nw) {
+    const int strips = (C + 255) / 256;
+    const int j = blockIdx.x / strips, c = (blockIdx.x - j * strips) * 256 + t;
+    if (c < C) {
+      float a = 0.f;
+#pragma unroll 8
+      for (int n = 0; n < N; ++n) a += dl[(int64_t)n * ncls + j] * feat[(int64_t)n * C + c];
+      dw[(int64_t)j * C + c] = a * scale;
+    }
+    if (c == 0) {
+      float b = 0.f;
+      for (int n = 0; n < N; ++n) b += dl[(int64_t)n * ncls + j];
+      db[j] = b * scale;
+    }
+    return;
+  }
+  const int n = blockIdx.x - nw;
+  for (int j = t; j < ncls; j += 256) row[j] = dl[(int64_t)n * ncls + j];
+  __syncthreads();
+  const float inv = 1.f / (float)HW;
+  T* o = dact + (int64_t)n * HW * C;
+  for (int c = t; c < C; c += 256) {
+    float sum = 0.f;
+    for (int j = 0; j < ncls; ++j) sum += row[j] * E::cvt(wfc[(int64_t)j * C + c]);
+    const T v = E::from(sum * inv);
+    for (int p = 0; p < HW; ++p) o[(int64_t)p * C + c] = v;
+  }
+}
+
 template <typename T>
 static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int N, int HW, int C, int ncls,
                       float scale, float* dw, float* db, T* dact, float* ws, size_t ws_bytes, hipStream_t st) {
   DTC_CHECK_ARG(dlogits && feat && wfc && dw && db && dact && N > 0 && HW > 0 && C > 0 && ncls > 0,
                 "head_bwd: bad args");
+  if (ncls <= 1024 && option_get(OPT_HEAD_FUSED) != 0) {
+    const int nw = ncls * ((C + 255) / 256);
+    hipLaunchKernelGGL(head_bwd_fused_kernel<T>, dim3(nw + N), dim3(256), 0, st, dlogits, feat, wfc, N, HW, C, ncls,
+                       scale, dw, db, dact, nw);
+    DTC_LAUNCH_CHECK();
+    return 0;
+  }
   DTC_CHECK_ARG(ws && ws_bytes >= head_bwd_workspace(N, C, ncls), "head_bwd: workspace too small");
   const int splits = (N + HB_IMGS - 1) / HB_IMGS;
   hipLaunchKernelGGL(head_bwd_w_partial_kernel, dim3((C + 63) / 64, (ncls + 15) / 16, splits), dim3(256), 0, st,

@@ -52,6 +52,9 @@ enum {
                            // (default 0: measured -2% at B=256, interleaved A/B; cross-stream graph edges
                            // cost more than the overlap of the small launches gains)
   OPT_DGRAD_CLASS_ORDER = 30,  // stride-2 dgrad parity classes dispatched heaviest first (1) or in z order (0)
+  OPT_HEAD_FUSED = 31,     // head backward: 1 = one launch (dW/db strips + dact), 0 (default) = partial/reduce/x
+                           // kernels (measured 1% faster: the strip kernel's 256-image loop is latency bound)
+  OPT_STEM_PROLOGUE = 32,  // forward: 1 = input copy + BN slot zeroing in one launch (copy_and_zero)
   OPT_COUNT
 };
 int option_get(int id);
@@ -272,6 +275,8 @@ int sgd_nesterov(float* p, const float* g, float* mom, u16* p_bf16, int64_t n, f
 int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st);
 // zero an 8-byte aligned range (a kernel node, unlike hipMemsetAsync's fill dispatch)
 int zero_bytes(void* p, size_t bytes, hipStream_t st);
+// dst[0:bytes] = src[0:bytes] (16-B aligned) and zp[0:zbytes] = 0 (8-B aligned), one launch
+int copy_and_zero(const void* src, void* dst, size_t bytes, void* zp, size_t zbytes, hipStream_t st);
 // x[i] *= f (loopback test communicator)
 int scale_f32(float* x, int64_t n, float f, hipStream_t st);
 int scale_f64(double* x, int64_t n, double f, hipStream_t st);

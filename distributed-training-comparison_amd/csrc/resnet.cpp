@@ -426,6 +426,11 @@ static u64* prof_slot(Net& n, int kind, double flops) {
 
 // ------------------------------------------------------------------ graph capture helpers
 static void drop_graphs(Net& n) {
+  // a graph exec may still be running (the caller's previous step is asynchronous): destroying it then
+  // frees state its in-flight kernels use (seen as a later crash in a sync), so drain the device first
+  bool any = !n.bwd_segs.empty();
+  for (auto e : n.fwd_exec) any = any || e != nullptr;
+  if (any) (void)hipDeviceSynchronize();
   for (auto& e : n.fwd_exec)
     if (e) {
       (void)hipGraphExecDestroy(e);
@@ -544,8 +549,9 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
   n.prof_next = train ? 0 : Net::PROF_SLOTS;  // eval passes are not timed
   // the forward statistics AND the backward sums of every BN (the backward that follows this training
-  // forward accumulates into zeroed slots; its graph then starts with real work, no memset node)
-  if (train) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));
+  // forward accumulates into zeroed slots; its graph then starts with real work, no memset node) --
+  // done by forward()'s input-copy launch on the direct-stem path
+  if (train && !n.stem_direct) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));
   if (n.stem_direct) {  // stem.hip: taps gathered per tile from the fp32 input, one K=32 k-step
     PROF(0, 2.0 * M0 * 64 * 27,
          stem_fwd(n.at<float>(n.XIN), n.wbf(n.stem.pidx), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
@@ -759,8 +765,16 @@ static int backward_body_f32(Net& n, const float* dlogits, float gs, const BwdCt
 
 static int forward(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
   if (n.f32) DTC_TRY(f32_stem_im2col(x, n.at<float>(n.X0), n.B, n.H, n.W, st));
-  else if (n.stem_direct)  // the graph reads only executor memory: a plain copy of the 12 B/pixel input
-    DTC_HIP(hipMemcpyAsync(n.at<float>(n.XIN), x, (size_t)n.B * 3 * n.H * n.W * 4, hipMemcpyDeviceToDevice, st));
+  else if (n.stem_direct) {  // the graph reads only executor memory: a copy of the 12 B/pixel input (+ the
+    // training step's BN slots zeroed in the same launch)
+    const size_t xb = (size_t)n.B * 3 * n.H * n.W * 4;
+    if (xb % 16 == 0 && ((uintptr_t)x & 15) == 0 && option_get(OPT_STEM_PROLOGUE) != 0) {
+      DTC_TRY(copy_and_zero(x, n.at<float>(n.XIN), xb, n.ws + n.stats_lo, train ? n.stats_hi - n.stats_lo : 0, st));
+    } else {
+      DTC_HIP(hipMemcpyAsync(n.at<float>(n.XIN), x, xb, hipMemcpyDeviceToDevice, st));
+      if (train) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));
+    }
+  }
   else DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
   if (!graphs_on(n)) return forward_body(n, logits, train, st);
   hipGraphExec_t& ex = n.fwd_exec[train ? 1 : 0];

@@ -234,7 +234,16 @@ def test_bn_backward_onepass(dtc, cuda, M, C, dual):
         assert rel_err(dx2.float().cpu().numpy(), dx2_ref) < 1e-2
 
 
-def test_head_and_loss(dtc, cuda):
+@pytest.mark.parametrize("head_fused", [1, 0])
+def test_head_and_loss(dtc, cuda, head_fused):
+    dtc._native.lib.dtc_set_option(b"head_fused", head_fused)
+    try:
+        _head_and_loss(dtc, cuda)
+    finally:
+        dtc._native.lib.dtc_set_option(b"head_fused", 0)
+
+
+def _head_and_loss(dtc, cuda):
     N, C, ncls = 6, 512, 100
     g = np.random.default_rng(7)
     act = O.relu(_rand_bf16((N, 4, 4, C), g))

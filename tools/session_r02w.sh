@@ -1,0 +1,3 @@
+tools/gpu_session.sh \
+ "gB|900|DTC_OPTIONS=stem_prologue=0,dgrad_class_order=0 python -X faulthandler -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread" \
+ "gC|900|DTC_OPTIONS=head_fused=0,dgrad_class_order=0 python -X faulthandler -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread"
