@@ -43,6 +43,8 @@ struct IGemmParams {
   int xcd_remap;
   int cls;  // DGRAD, stride 2: blockIdx.z = output parity class (h%2, w%2); M counts class pixels
   int cls_order;  // 1: blockIdx.z runs the classes heaviest first (option dgrad_class_order)
+  int res_compact;  // DGRAD classes: res is [N][H/2][W/2][C], added to class (0, 0) only (a 1x1 stride-2
+                    // shortcut's dx, which is zero at the other three parities)
   // WGRAD fast path: each 64-pixel reduction step covers whole rows of one image (PQ % 64 == 0,
   // 64 % Q == 0) or whole images (64 % PQ == 0); tensors < 4 GiB so 32-bit buffer offsets work.
   int wg_fast;
@@ -489,8 +491,8 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
         if (pix < p.M) {
           float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
           const size_t o = orow * p.C + ch;
-          if (p.res) {
-            const uint2 rr = *(const uint2*)(p.res + o);
+          if (p.res && (!p.res_compact || (cls_ph == 0 && cls_pw == 0))) {
+            const uint2 rr = *(const uint2*)(p.res + (p.res_compact ? (size_t)pix * p.C + ch : o));
             v[0] += bf_lo(rr.x); v[1] += bf_hi(rr.x); v[2] += bf_lo(rr.y); v[3] += bf_hi(rr.y);
           }
           uint2 w;
@@ -712,6 +714,8 @@ static bool dgrad_class_mode(const ConvShape& s) {
   return s.stride == 2 && (s.H % 2) == 0 && (s.W % 2) == 0 && option_get(OPT_DGRAD_CLASSES) != 0;
 }
 
+bool dgrad_class_ok(const ConvShape& s) { return dgrad_class_mode(s) && !conv_c64_ok(s) && conv_halo_plan(s, CONV_DGRAD).cfg < 0; }
+
 ConvPlan plan_conv(const ConvShape& s, int mode) {
   ConvPlan pl{};
   const int P = (s.H + 2 * s.pad - s.R) / s.stride + 1;
@@ -800,14 +804,16 @@ static int bnb_after(const BnbArgs* bnb, u16* dx, int64_t M, int C, hipStream_t 
 }
 
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
-               size_t slab_bytes, hipStream_t st, u64* ts, const BnbArgs* bnb) {
+               size_t slab_bytes, hipStream_t st, u64* ts, const BnbArgs* bnb, int res_compact) {
   if (bnb != nullptr && bnb->ym == nullptr) bnb = nullptr;
+  DTC_CHECK_ARG(!res_compact || (res && dgrad_class_mode(s) && !conv_c64_ok(s)),
+                "conv_dgrad: a compact residual needs the stride-2 parity-class path");
   const int fz = bnb != nullptr ? option_get(OPT_BNB_FUSE) : 0;  // bit 0: c64, 1: halo, 2: split-K reduce
   const HaloPlan hp = conv_c64_ok(s) ? HaloPlan{-1, 0} : conv_halo_plan(s, CONV_DGRAD);
   const int kind = conv_c64_ok(s) ? 1 : (hp.cfg >= 0 ? 2 : 4);
   const bool split_path = kind != 1 && (kind == 4 || hp.split > 1);  // the epilogue is splitk_reduce's
   if (bnb != nullptr && !(fz & (split_path ? 4 : kind))) {
-    DTC_TRY(conv_dgrad(s, dy, w, dx, res, slab, slab_bytes, st, ts, nullptr));
+    DTC_TRY(conv_dgrad(s, dy, w, dx, res, slab, slab_bytes, st, ts, nullptr, res_compact));
     return bnb_after(bnb, dx, (int64_t)s.N * s.H * s.W, s.C, st);
   }
   if (kind == 1) return conv_c64(s, CONV_DGRAD, dy, w, dx, res, nullptr, st, ts, bnb);
@@ -823,6 +829,7 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
   if (dgrad_class_mode(s)) {  // four parity-class GEMMs in one launch (blockIdx.z), no split-K
     p.cls = 1;
     p.cls_order = option_get(OPT_DGRAD_CLASS_ORDER);
+    p.res_compact = res_compact;
     p.M = s.N * (s.H / 2) * (s.W / 2);
     p.fd_q = make_fastdiv(s.W / 2);
     p.fd_pq = make_fastdiv((s.H / 2) * (s.W / 2));

@@ -55,6 +55,8 @@ enum {
   OPT_HEAD_FUSED = 31,     // head backward: 1 = one launch (dW/db strips + dact), 0 (default) = partial/reduce/x
                            // kernels (measured 1% faster: the strip kernel's 256-image loop is latency bound)
   OPT_STEM_PROLOGUE = 32,  // forward: 1 = input copy + BN slot zeroing in one launch (copy_and_zero)
+  OPT_SC_COMPACT = 33,     // executor: 1 = the shortcut's dx kept at the stride-2 grid (1/4 the bytes) and
+                           // added by conv1's parity-class dgrad epilogue
   OPT_COUNT
 };
 int option_get(int id);
@@ -85,8 +87,13 @@ int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* sta
 // and accumulate the BN-backward sums (bn_bwd_reduce's work) -- in the epilogue where the kernel
 // supports it (conv_c64, conv_halo, split-K reduce), else by a bn_bwd_reduce pass after the conv.
 // dx may alias res (in place: each element is read and written by the same lane).
+// true when conv_dgrad(s) takes the stride-2 parity-class path (the one a compact residual needs)
+bool dgrad_class_ok(const ConvShape& s);
+// res_compact: res is [N][H/2][W/2][C] (a 1x1 stride-2 shortcut's dx at its only nonzero parity),
+// added at the (even, even) pixels only -- stride-2 parity-class dgrads.
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
-               size_t slab_bytes, hipStream_t st, u64* ts = nullptr, const BnbArgs* bnb = nullptr);
+               size_t slab_bytes, hipStream_t st, u64* ts = nullptr, const BnbArgs* bnb = nullptr,
+               int res_compact = 0);
 // dw[k][0:dw_cols] (row stride dw_ld) = scale * sum_pixels dy (x) im2col(x); fp32
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
                float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);

@@ -1070,11 +1070,15 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     DTC_TRY(cap(n, cp + ".dc2", dc2, st));
     if (b.proj) DTC_TRY(cap(n, cp + ".ds", dsc, st));
     const bool sc_branch = b.proj && sc_on(n);
+    // the shortcut's dx at its stride-2 grid only (option sc_compact): the 1x1 stride-2 conv's dgrad
+    // is zero at three of four parities; conv1's parity-class dgrad adds it at the fourth
+    const bool sc_cmp = b.proj && !n.capture && option_get(OPT_SC_COMPACT) != 0 && dgrad_class_ok(b.c1.s);
+    const ConvShape sc_dg = sc_cmp ? ConvShape{b.sc.s.N, b.Hout, b.Wout, b.sc.s.C, b.sc.s.K, 1, 1, 1, 0} : b.sc.s;
     if (sc_branch) {  // dx of the shortcut (conv1's dgrad residual) beside conv2's dgrad and BN1's backward
       hipStream_t ss = st;
       DTC_TRY(fork_sc(n, st, &ss));
       PROF(1, conv_flops(b.sc.s),
-           conv_dgrad(b.sc.s, dsc, n.wbf(b.sc.pidx), G[5], nullptr, n.at<float>(n.SLABSC), n.slabsc_bytes, ss, ts));
+           conv_dgrad(sc_dg, dsc, n.wbf(b.sc.pidx), G[5], nullptr, n.at<float>(n.SLABSC), n.slabsc_bytes, ss, ts));
     }
     // option wgrad_defer: the halo-geometry wgrads are only queued here; their batched launch is forked
     // after the layer's last dgrad (below), so it overlaps the HBM-bound BN chain that follows rather
@@ -1099,8 +1103,9 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     if (b.proj) {
       PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
       if (sc_branch) DTC_TRY(join_sc(n, st));
-      else PROF(1, conv_flops(b.sc.s), conv_dgrad(b.sc.s, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
-      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts));
+      else PROF(1, conv_flops(b.sc.s), conv_dgrad(sc_dg, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
+      PROF(1, conv_flops(b.c1.s),
+           conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts, nullptr, sc_cmp ? 1 : 0));
       DTC_TRY(cap(n, cp + ".dxs", G[5], st));
     } else {  // residual = dz of this block's output (G[0], written by bn2's apply); dx over it in place
       PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[0], slab, n.slab_bytes, st, ts));

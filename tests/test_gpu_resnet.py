@@ -501,6 +501,24 @@ def test_bn_onepass_matches_two_pass(dtc, cuda, graphs):
         assert rel_err(ba[k], bb[k]) < 1e-6, k
 
 
+@pytest.mark.parametrize("batch", [8, 64])
+def test_shortcut_compact_dx_matches_full(dtc, cuda, batch):
+    """Option sc_compact (default): the projection shortcut's dx is computed at its stride-2 grid only
+    (a 1x1 dgrad over the Hout x Wout pixels) and conv1's parity-class dgrad adds it at the (even, even)
+    pixels; the full-resolution path writes the same values plus zeros at the other parities. Same
+    reduction order, no split-K: the gradients agree exactly (graphs on and off)."""
+    lib = dtc._native.lib
+    for graphs in (0, 1):
+        ga = _grads_repeated(dtc, cuda, graphs, batch=batch)
+        lib.dtc_set_option(b"sc_compact", 0)
+        try:
+            gb = _grads_repeated(dtc, cuda, graphs, batch=batch)
+        finally:
+            lib.dtc_set_option(b"sc_compact", 1)
+        for rep in range(2):
+            np.testing.assert_array_equal(ga[rep], gb[rep])
+
+
 def test_graph_recapture_on_option_change(dtc, cuda):
     """Options are baked into captured launches: changing one re-captures (results unchanged)."""
     model, _, x, y = _setup(dtc, cuda, 4, seed=6)
