@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libdtc_amd.so")
+LIB_PATH = os.environ.get("DTC_LIB") or os.path.join(_HERE, "_lib", "libdtc_amd.so")  # DTC_LIB: A/B builds
 
 
 class NativeError(RuntimeError):
