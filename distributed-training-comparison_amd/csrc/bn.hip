@@ -13,6 +13,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "tile_common.h"
+#include "bn_coef.h"
 
 namespace dtc {
 
@@ -212,57 +213,6 @@ DTC_BN_APPLY_DEFS(float)
 constexpr int FA_GROUP = 64;  // channels per workgroup
 constexpr int FA_UNROLL = 4;  // pixel rows in flight per thread
 
-__device__ __forceinline__ void fa_slot_sums(const double* __restrict__ st, int C, int cg, double* part, double& s,
-                                             double& q) {
-  const int t = threadIdx.x, cl = t & 63, g = t >> 6;  // 4 groups of 8 slots
-  double a = 0.0, b = 0.0;
-#pragma unroll
-  for (int j = 0; j < DTC_STAT_SLOTS / 4; ++j) {
-    const size_t k = (size_t)(g * (DTC_STAT_SLOTS / 4) + j);
-    a += st[k * 2 * C + cg + cl];
-    b += st[k * 2 * C + C + cg + cl];
-  }
-  part[(g * 2 + 0) * 64 + cl] = a;
-  part[(g * 2 + 1) * 64 + cl] = b;
-  __syncthreads();
-  s = q = 0.0;
-  if (t < 64) {
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      s += part[(gg * 2 + 0) * 64 + t];
-      q += part[(gg * 2 + 1) * 64 + t];
-    }
-  }
-}
-
-__device__ __forceinline__ void fa_fwd_coef(const BnFwdArgs& A, int C, int cg, double* part, float* sc, float* sh) {
-  double s, q;
-  fa_slot_sums(A.stats, C, cg, part, s, q);
-  const int t = threadIdx.x;
-  if (t < 64) {
-    const int c = cg + t;
-    const double cnt = (double)A.count;
-    const double mu = s / cnt;
-    double var = q / cnt - mu * mu;
-    if (var < 0.0) var = 0.0;
-    const float is = (float)(1.0 / sqrt(var + (double)A.eps));
-    const float a = A.gamma[c] * is;
-    sc[t] = a;
-    sh[t] = A.beta[c] - (float)mu * a;
-    if (blockIdx.x == 0) {
-      A.mean[c] = (float)mu;
-      A.invstd[c] = is;
-      if (A.rmean) {
-        const double unbiased = cnt > 1.0 ? var * cnt / (cnt - 1.0) : var;
-        A.rmean[c] = (float)((1.0 - A.momentum) * A.rmean[c] + A.momentum * mu);
-        A.rvar[c] = (float)((1.0 - A.momentum) * A.rvar[c] + A.momentum * unbiased);
-      }
-      if (t == 0 && blockIdx.y == 0 && A.nbt) *A.nbt += 1;
-    }
-  }
-  __syncthreads();
-}
-
 // mask (optional): the ReLU mask of y, one bit per element (byte o/8 of element offset o, bit k =
 // channel c0 + k): the backward reads it instead of y (0.125 B instead of 2 B per element).
 template <int MODE, typename T>
@@ -275,9 +225,25 @@ __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const T* __restrict__
   __shared__ float coef[4][64];  // scale1, shift1, scale2, shift2
   stamp_start(ts);
   const int cg = blockIdx.y * FA_GROUP;
-  fa_fwd_coef(a1, C, cg, part, coef[0], coef[1]);
-  if constexpr (MODE == APPLY_DUAL_RELU) fa_fwd_coef(a2, C, cg, part, coef[2], coef[3]);
   const int t = threadIdx.x, q8 = (t & 7) * 8, pr = t >> 3;
+  const int64_t m0 = (int64_t)blockIdx.x * rows, m1 = std::min<int64_t>(M, m0 + rows);
+  typename E::V xa[FA_UNROLL], xr[FA_UNROLL];
+  auto load = [&](int64_t mb) {  // branch-free: rows past the block's end load a valid row (unused)
+#pragma unroll
+    for (int u = 0; u < FA_UNROLL; ++u) {
+      const int64_t o = std::min<int64_t>(mb + 32 * u, M - 1) * C + cg + q8;
+      xa[u] = E::ld(x + o);
+      if constexpr (MODE != APPLY_RELU) xr[u] = E::ld(x2 + o);
+    }
+  };
+  // the first trip's loads are issued before the coefficient fold, so their latency overlaps it (the
+  // small layers' launches are one trip per thread)
+  SlotFold f1, f2;
+  fold_issue_fwd(a1, C, cg, f1);
+  if constexpr (MODE == APPLY_DUAL_RELU) fold_issue_fwd(a2, C, cg, f2);
+  load(m0 + pr);
+  fa_fwd_coef_from(a1, f1, C, cg, part, coef[0], coef[1]);
+  if constexpr (MODE == APPLY_DUAL_RELU) fa_fwd_coef_from(a2, f2, C, cg, part, coef[2], coef[3]);
   float sc[8], sh[8], sc2[8], sh2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -288,20 +254,10 @@ __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const T* __restrict__
       sh2[k] = coef[3][q8 + k];
     }
   }
-  const int64_t m0 = (int64_t)blockIdx.x * rows, m1 = std::min<int64_t>(M, m0 + rows);
   // FA_UNROLL rows per thread per trip: every load of the trip is issued before the first
   // dependent use (memory-level parallelism); elementwise, so results are unchanged
   for (int64_t mb = m0 + pr; mb < m1; mb += 32 * FA_UNROLL) {
-    typename E::V xa[FA_UNROLL], xr[FA_UNROLL];
-#pragma unroll
-    for (int u = 0; u < FA_UNROLL; ++u) {
-      const int64_t m = mb + 32 * u;
-      if (m < m1) {
-        const int64_t o = m * C + cg + q8;
-        xa[u] = E::ld(x + o);
-        if constexpr (MODE != APPLY_RELU) xr[u] = E::ld(x2 + o);
-      }
-    }
+    if (mb != m0 + pr) load(mb);
 #pragma unroll
     for (int u = 0; u < FA_UNROLL; ++u) {
       const int64_t m = mb + 32 * u;
@@ -328,7 +284,7 @@ __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const T* __restrict__
 
 static void fa_grid(int64_t M, int C, int& nblk, int& rows) {
   const int groups = C / FA_GROUP;
-  nblk = std::max(1, 1024 / groups);
+  nblk = std::max(1, option_get(OPT_BN_FA_BLOCKS) / groups);  // workgroups per launch (default 1024)
   rows = (int)((M + nblk - 1) / nblk);
   // at least FA_UNROLL rows per thread: each workgroup's prologue folds 32 KB of fp64 slots, which
   // dominated the small (layer3/4) launches at one row per thread
@@ -374,28 +330,6 @@ int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2,
 // ------------------------------------------------------------------ fused finalize + apply (backward)
 // dx = A*dz + B*x + Cc with the coefficients computed per workgroup from the fp64 slots of
 // sum(dz), sum(dz*xhat); the first pixel block writes dgamma / dbeta (x gscale).
-__device__ __forceinline__ void fa_bwd_coef(const BnBwdArgs& A, int C, int cg, double* part, float* ca, float* cb,
-                                            float* cc) {
-  double sd, sx;
-  fa_slot_sums(A.acc, C, cg, part, sd, sx);
-  const int t = threadIdx.x;
-  if (t < 64) {
-    const int c = cg + t;
-    const double cnt = (double)A.count;
-    const double is = A.invstd[c];
-    const double a = (double)A.gamma[c] * is;
-    const double b = -a * is * sx / cnt;
-    ca[t] = (float)a;
-    cb[t] = (float)b;
-    cc[t] = (float)(-a * sd / cnt - b * (double)A.mean[c]);
-    if (blockIdx.x == 0) {
-      if (A.dgamma) A.dgamma[c] = (float)(sx * A.gscale);
-      if (A.dbeta) A.dbeta[c] = (float)(sd * A.gscale);
-    }
-  }
-  __syncthreads();
-}
-
 // MB: dz is formed here from the raw gradient (`dz` = dy) and the forward's ReLU mask bits
 // (dz = dy * [y > 0]; exact), and optionally stored to dzo (may alias dy: each element is read and
 // written by the same lane) for a consumer that needs it (the identity shortcut's residual).
@@ -410,9 +344,26 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restri
   __shared__ float coef[6][64];
   stamp_start(ts);
   const int cg = blockIdx.y * FA_GROUP;
-  fa_bwd_coef(a1, C, cg, part, coef[0], coef[1], coef[2]);
-  if constexpr (DUAL) fa_bwd_coef(a2, C, cg, part, coef[3], coef[4], coef[5]);
   const int t = threadIdx.x, q8 = (t & 7) * 8, pr = t >> 3;
+  const int64_t m0 = (int64_t)blockIdx.x * rows, m1 = std::min<int64_t>(M, m0 + rows);
+  typename E::V vd[FA_UNROLL], va[FA_UNROLL], vb[FA_UNROLL];
+  uint32_t mk[FA_UNROLL];
+  auto load = [&](int64_t mb) {  // branch-free (see bn_fin_apply_kernel)
+#pragma unroll
+    for (int u = 0; u < FA_UNROLL; ++u) {
+      const int64_t o = std::min<int64_t>(mb + 32 * u, M - 1) * C + cg + q8;
+      vd[u] = E::ld(dz + o);
+      va[u] = E::ld(x1 + o);
+      if constexpr (DUAL) vb[u] = E::ld(x2 + o);
+      if constexpr (MB) mk[u] = mbits[o >> 3];
+    }
+  };
+  SlotFold f1, f2;
+  fold_issue_bwd(a1, C, cg, f1);
+  if constexpr (DUAL) fold_issue_bwd(a2, C, cg, f2);
+  load(m0 + pr);  // in flight during the coefficient fold (see bn_fin_apply_kernel)
+  fa_bwd_coef_from(a1, f1, C, cg, part, coef[0], coef[1], coef[2]);
+  if constexpr (DUAL) fa_bwd_coef_from(a2, f2, C, cg, part, coef[3], coef[4], coef[5]);
   float A1[8], B1[8], C1[8], A2[8], B2[8], C2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -421,21 +372,8 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restri
       A2[k] = coef[3][q8 + k]; B2[k] = coef[4][q8 + k]; C2[k] = coef[5][q8 + k];
     }
   }
-  const int64_t m0 = (int64_t)blockIdx.x * rows, m1 = std::min<int64_t>(M, m0 + rows);
   for (int64_t mb = m0 + pr; mb < m1; mb += 32 * FA_UNROLL) {  // loads of a trip first (see bn_fin_apply)
-    typename E::V vd[FA_UNROLL], va[FA_UNROLL], vb[FA_UNROLL];
-    uint32_t mk[FA_UNROLL];
-#pragma unroll
-    for (int u = 0; u < FA_UNROLL; ++u) {
-      const int64_t m = mb + 32 * u;
-      if (m < m1) {
-        const int64_t o = m * C + cg + q8;
-        vd[u] = E::ld(dz + o);
-        va[u] = E::ld(x1 + o);
-        if constexpr (DUAL) vb[u] = E::ld(x2 + o);
-        if constexpr (MB) mk[u] = mbits[o >> 3];
-      }
-    }
+    if (mb != m0 + pr) load(mb);
 #pragma unroll
     for (int u = 0; u < FA_UNROLL; ++u) {
       const int64_t m = mb + 32 * u;
@@ -899,8 +837,11 @@ int bn_bwd_reduce_mask(const u16* dy, const uint8_t* mbits, const u16* x1, const
   DTC_CHECK_ARG(dy && mbits && x1 && mean1 && invstd1 && acc1 && C % 8 == 0 && C <= 2048 && M > 0,
                 "bn_bwd_reduce_mask: bad args");
   const int tpr = C / 8, rpp = 256 / tpr;
+  // >= bn_red_elems elements per workgroup where that still leaves >= bn_red_blocks workgroups
+  const int64_t elems = std::max(1024, option_get(OPT_BN_RED_ELEMS));
+  const int64_t minblk = std::max(1, option_get(OPT_BN_RED_BLOCKS));
   int64_t rpb = std::max<int64_t>({(int64_t)rpp, (M + 1023) / 1024,
-                                   std::min<int64_t>((16384 + C - 1) / C, (M + 255) / 256)});
+                                   std::min<int64_t>((elems + C - 1) / C, (M + minblk - 1) / minblk)});
   rpb = ((rpb + rpp - 1) / rpp) * rpp;
   const int blocks = ceil_div_i(M, rpb);
   if (x2) {

@@ -57,6 +57,17 @@ enum {
   OPT_STEM_PROLOGUE = 32,  // forward: 1 = input copy + BN slot zeroing in one launch (copy_and_zero)
   OPT_SC_COMPACT = 33,     // executor: 1 = the shortcut's dx kept at the stride-2 grid (1/4 the bytes) and
                            // added by conv1's parity-class dgrad epilogue
+  OPT_WGRAD_TAIL = 34,     // executor: >0 = at most this many layer1 weight gradients per batched launch
+                           // (the last batch of the backward runs beside the stem's tail chain). Default
+                           // 0: 2 measured -0.7%, 1 -6% (the 2-conv batch takes as long as the 4-conv one)
+  OPT_STEM_BN_FUSE = 35,   // executor: 1 (default) = the stem BN's backward apply fused into the stem weight
+                           // gradient (stem_wgrad_bn; dc never stored): +0.8% at B=256, interleaved A/B
+  OPT_BN_RED_ELEMS = 36,   // bn_bwd_reduce (mask path): target elements per workgroup (tuning; default 16384)
+  OPT_BN_RED_BLOCKS = 37,  // ... while keeping at least this many workgroups (tuning; default 256;
+                           // 65536 / 64 measured -7%)
+  OPT_BN_FA_BLOCKS = 38,   // BN fin_apply kernels: target workgroups per launch (tuning; default 1024; 256: -1%)
+  OPT_FORK_LAZY = 39,      // executor: 1 = fork the weight-gradient stream only where a wgrad launches
+  OPT_SIDE_PRIO = 40,      // executor (at the side stream's creation): 1 = weight-gradient stream at low priority
   OPT_COUNT
 };
 int option_get(int id);
@@ -253,6 +264,10 @@ int stem_fwd(const float* x, const u16* w27, u16* y, double* stats, int N, int H
 size_t stem_wgrad_slab_bytes(int64_t M);
 int stem_wgrad(const float* x, const u16* dy, float* dw27, float scale, int N, int H, int W, float* slab,
                size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
+// stem weight gradient with the stem BN's backward apply fused: dc = A*(dy*bit) + B*c + Cc formed per
+// tile in LDS from (dy, mask bits, the conv output c) and the BN's slots (a: as bn_bwd_fin_apply's)
+int stem_wgrad_bn(const float* x, const u16* dy, const uint8_t* mbits, const u16* c, const BnBwdArgs& a, float* dw27,
+                  float scale, int N, int H, int W, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 // grad[k][0:ncols] (row stride ldo) = scale * sum_s slab[s][k][0:RSC] (igemm.hip's deterministic reduce)
 int wgrad_reduce_to(const float* slab, int splits, int K, int RSC, int ncols, int ldo, float scale, float* dw,
                     hipStream_t st, u64* ts = nullptr);

@@ -899,7 +899,17 @@ static int fork_side(Net& n, hipStream_t st, hipStream_t* out) {
     *out = st;
     return 0;
   }
-  if (!n.side_st) DTC_HIP(hipStreamCreateWithFlags(&n.side_st, hipStreamNonBlocking));
+  if (!n.side_st) {
+    // option side_prio: the weight-gradient stream at the lowest priority, so the dispatcher prefers the
+    // dgrad / BN chain (the critical path) when both have workgroups ready
+    if (option_get(OPT_SIDE_PRIO) != 0) {
+      int lo = 0, hi = 0;
+      DTC_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));  // lo = least urgent
+      DTC_HIP(hipStreamCreateWithPriority(&n.side_st, hipStreamNonBlocking, lo));
+    } else {
+      DTC_HIP(hipStreamCreateWithFlags(&n.side_st, hipStreamNonBlocking));
+    }
+  }
   hipEvent_t ev;
   DTC_TRY(next_event(n, &ev));
   DTC_HIP(hipEventRecord(ev, st));
@@ -993,19 +1003,31 @@ static int wg_flush(Net& n, WgQueue& q, float gs, float* slabw, hipStream_t sd) 
   PROF(2, conv_flops(q.s) * np, conv_wgrad_batch(q.s, np, q.x, q.dy, q.dw, gs, slabw, n.slab_bytes, sd, ts));
   return 0;
 }
+static int fork_side(Net& n, hipStream_t st, hipStream_t* out);
+// lazy (option fork_lazy): the side stream is forked from `st` here, only when something is launched,
+// instead of by the caller before every wgrad (a queued-only wgrad needs no fork: the launch's fork
+// is later on the main stream, so it covers the queued inputs too)
 static int wg_issue(Net& n, WgQueue& q, const ConvShape& s, const u16* x, const u16* dy, float* dw, float gs,
-                    float* slabw, hipStream_t sd, bool defer = false) {
-  const int bmax = wgrad_batch_max();
+                    float* slabw, hipStream_t& sd, bool defer = false, int bcap = 0, hipStream_t st = nullptr,
+                    bool lazy = false) {
+  const int bmax = bcap > 0 ? std::min(bcap, wgrad_batch_max()) : wgrad_batch_max();
   if (bmax <= 1 || wgrad_halo_splits(s, 2) <= 0) {
+    if (lazy) DTC_TRY(fork_side(n, st, &sd));
     PROF(2, conv_flops(s), conv_wgrad(s, x, dy, dw, 0, 0, gs, slabw, n.slab_bytes, sd, ts));
     return 0;
   }
-  if (q.count > 0 && !same_shape(q.s, s)) DTC_TRY(wg_flush(n, q, gs, slabw, sd));
+  if (q.count > 0 && !same_shape(q.s, s)) {
+    if (lazy) DTC_TRY(fork_side(n, st, &sd));
+    DTC_TRY(wg_flush(n, q, gs, slabw, sd));
+  }
   q.s = s;
   q.x[q.count] = x;
   q.dy[q.count] = dy;
   q.dw[q.count] = dw;
-  if (++q.count >= bmax && !defer) DTC_TRY(wg_flush(n, q, gs, slabw, sd));
+  if (++q.count >= bmax && !defer) {
+    if (lazy) DTC_TRY(fork_side(n, st, &sd));
+    DTC_TRY(wg_flush(n, q, gs, slabw, sd));
+  }
   return 0;
 }
 // (the plan's bucket points, with or without a communicator: the batches -- and so the split-K
@@ -1084,8 +1106,11 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     // after the layer's last dgrad (below), so it overlaps the HBM-bound BN chain that follows rather
     // than the dgrads (measured -1% at B=256: the wgrad batch then starves the BN kernels instead)
     const bool defer = option_get(OPT_WGRAD_DEFER) != 0;
-    DTC_TRY(fork_side(n, st, &sd));
-    DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd, defer));
+    // option wgrad_tail: smaller batches for layer1, whose last batch is the backward's tail
+    const int bcap = bi < 2 ? option_get(OPT_WGRAD_TAIL) : 0;
+    const bool lazy = option_get(OPT_FORK_LAZY) != 0 && !defer;
+    if (!lazy) DTC_TRY(fork_side(n, st, &sd));
+    DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd, defer, bcap, st, lazy));
     PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts));
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
     DTC_TRY(cap_masked(n, cp + ".dz1", G[4], b.MA1, M, b.Cout, st));
@@ -1098,8 +1123,8 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
       DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st, ma1));
     }
     DTC_TRY(cap(n, cp + ".dc1", dc1, st));
-    DTC_TRY(fork_side(n, st, &sd));
-    DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, defer));
+    if (!lazy || b.proj) DTC_TRY(fork_side(n, st, &sd));  // (the shortcut's wgrad below launches)
+    DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, defer, bcap, st, lazy && !b.proj));
     if (b.proj) {
       PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
       if (sc_branch) DTC_TRY(join_sc(n, st));
@@ -1112,7 +1137,10 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     }
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
     if (!defer) {
-      if (bucket_fires(n, bi)) DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
+      if (bucket_fires(n, bi)) {
+        if (lazy && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
+        DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
+      }
     } else if (wq.count > 0 && (bi % 2 == 0 || wq.count >= wgrad_batch_max() || bucket_fires(n, bi))) {
       // a layer's queued wgrads (its first block is the last one processed), a full queue, or a bucket
       // point: launch the batch on the side stream once this block's dgrads are done
@@ -1125,6 +1153,23 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
   u16* dc0 = n.at<u16>(n.DC0);
   const uint8_t* m0 = n.at<uint8_t>(n.MA0);
+  // option stem_bn_fuse: the stem BN's apply runs inside the stem weight gradient (dc0 never stored;
+  // not with parity captures, which want dc0, or SyncBN, whose sums are all-reduced first)
+  if (n.stem_direct && !n.capture && !n.sync && bn_fused() && option_get(OPT_STEM_BN_FUSE) != 0) {
+    PROF(3, (double)M0 * 64 * 4.125,
+         bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
+                            n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
+    if (option_get(OPT_FORK_LAZY) && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
+    DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
+    const BnBwdArgs a0 = bwd_args(n, n.bn0, M0, gs);
+    PROF(2, 2.0 * M0 * 64 * 27,
+         stem_wgrad_bn(n.at<float>(n.XIN), G[0], m0, n.at<u16>(n.C0), a0, n.gf(n.stem.pidx), gs, n.B, n.H, n.W, slab,
+                       n.slab_bytes, st, ts));
+    DTC_TRY(join_side(n, st));  // after the stem kernel: it depends on nothing the side stream computes
+    DTC_TRY(maybe_bucket(n, -1, cx, st));
+    if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
+    return 0;
+  }
   if (onepass_ok(n, M0, 64, false)) {
     DTC_TRY(bn_bwd_onepass(n, n.bn0, G[0], m0, nullptr, n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st));
   } else {
@@ -1135,6 +1180,7 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   }
   DTC_TRY(cap_masked(n, "grad.stem.dz", G[0], n.MA0, M0, 64, st));
   DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
+  if (option_get(OPT_FORK_LAZY) && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
   DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
   DTC_TRY(join_side(n, st));  // the stem wgrad is the last kernel: run it on the main stream
   PROF(2, 2.0 * M0 * 64 * 27,

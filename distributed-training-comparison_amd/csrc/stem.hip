@@ -16,6 +16,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "tile_common.h"
+#include "bn_coef.h"
 
 namespace dtc {
 
@@ -37,28 +38,29 @@ struct StemTile {
   int h0, rt;  // first output row, rows staged (h1 - h0 + 3)
 };
 
-__device__ __forceinline__ StemTile stem_stage(const float* __restrict__ x, uint32_t pix0, const StemGeom& G,
-                                               float* xt) {
+// The tile's staging geometry (T.n = -1: global gathers instead).
+template <int CAP>
+__device__ __forceinline__ StemTile stem_tile(uint32_t pix0, const StemGeom& G) {
   const uint32_t last = min(pix0 + 255u, G.M - 1u);
   const int n = (int)fdiv(pix0, G.fd_hw), nl = (int)fdiv(last, G.fd_hw);
   StemTile T{n, (int)fdiv(pix0 - (uint32_t)n * G.HW, G.fd_w), 0};
   const int h1 = (int)fdiv(last - (uint32_t)nl * G.HW, G.fd_w);
-  const int W2 = G.W + 2;
   T.rt = h1 - T.h0 + 3;
-  if (nl != n || T.rt * 3 * W2 > STEM_LDS_FLOATS) {
-    T.n = -1;
-    return T;
-  }
-  const float* xn = x + (size_t)n * 3 * G.HW;
-  // every load of the tile issued before the first LDS store (one memory latency, not one per row)
-  constexpr int PER_T = STEM_LDS_FLOATS / 256;
-  const int E = 3 * T.rt * W2;
-  float v[PER_T];
-  // every lane loads from a clamped valid address, then selects (a load under a divergent branch gets
-  // its own s_waitcnt: one latency per element); the trip count is uniform
-  const int iters = (E + 255) >> 8;
+  if (nl != n || T.rt * 3 * (G.W + 2) > CAP) T.n = -1;
+  return T;
+}
+
+// Loads of the staged rows into registers (split from the LDS stores so that a caller can put other
+// loads between the two). Every lane loads from a clamped valid address, then selects (a load under a
+// divergent branch gets its own s_waitcnt: one latency per element); the trip count is uniform.
+template <int CAP>
+__device__ __forceinline__ void stem_stage_ld(const float* __restrict__ x, const StemTile& T, const StemGeom& G,
+                                              float (&v)[CAP / 256]) {
+  if (T.n < 0) return;
+  const float* xn = x + (size_t)T.n * 3 * G.HW;
+  const int W2 = G.W + 2, E = 3 * T.rt * W2, iters = (E + 255) >> 8;
 #pragma unroll
-  for (int i = 0; i < PER_T; ++i) {
+  for (int i = 0; i < CAP / 256; ++i) {
     if (i < iters) {
       const int e = threadIdx.x + 256 * i;
       const int rr = (int)fdiv((uint32_t)e, G.fd_w2), col = e - rr * W2;  // staged row rr = c * rt + r
@@ -70,11 +72,27 @@ __device__ __forceinline__ StemTile stem_stage(const float* __restrict__ x, uint
       v[i] = ok ? a : 0.f;
     }
   }
+}
+
+template <int CAP>
+__device__ __forceinline__ void stem_stage_st(const StemTile& T, const StemGeom& G, const float (&v)[CAP / 256],
+                                              float* xt) {
+  if (T.n < 0) return;
+  const int E = 3 * T.rt * (G.W + 2), iters = (E + 255) >> 8;
 #pragma unroll
-  for (int i = 0; i < PER_T; ++i) {
+  for (int i = 0; i < CAP / 256; ++i) {
     const int e = threadIdx.x + 256 * i;
     if (i < iters && e < E) xt[e] = v[i];
   }
+}
+
+// every load of the tile issued before the first LDS store (one memory latency, not one per row)
+__device__ __forceinline__ StemTile stem_stage(const float* __restrict__ x, uint32_t pix0, const StemGeom& G,
+                                               float* xt) {
+  const StemTile T = stem_tile<STEM_LDS_FLOATS>(pix0, G);
+  float v[STEM_LDS_FLOATS / 256];
+  stem_stage_ld<STEM_LDS_FLOATS>(x, T, G, v);
+  stem_stage_st<STEM_LDS_FLOATS>(T, G, v, xt);
   return T;
 }
 
@@ -312,9 +330,11 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const float* __restrict
   stamp_end(ts);
 }
 
-size_t stem_wgrad_slab_bytes(int64_t M) {
+static int stem_bn_grid(int64_t M, int& tiles);
+size_t stem_wgrad_slab_bytes(int64_t M) {  // either weight-gradient kernel's partials
   const int64_t ntiles = (M + 255) / 256;
-  const int64_t nwg = std::min<int64_t>(ntiles, 256);
+  int tiles = 0;
+  const int64_t nwg = std::max<int64_t>(std::min<int64_t>(ntiles, 256), stem_bn_grid(M, tiles));
   return (size_t)nwg * 64 * 32 * 4;
 }
 
@@ -329,6 +349,135 @@ int stem_wgrad(const float* x, const u16* dy, float* dw27, float scale, int N, i
   DTC_CHECK_ARG(slab_bytes >= (size_t)nwg * 64 * 32 * 4, "stem_wgrad: slab workspace too small");
   DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_wgrad: more than 2^31 pixels");
   hipLaunchKernelGGL(stem_wgrad_kernel, dim3(nwg), dim3(256), 0, st, x, dy, slab, stem_geom(N, H, W), tiles, ts);
+  DTC_LAUNCH_CHECK();
+  return wgrad_reduce_to(slab, nwg, 64, 32, 27, 27, scale, dw27, st, ts);
+}
+
+
+// ---------------------------------------------------------------- weight gradient + BN backward apply
+// The stem BN's backward apply fused into the weight gradient (option stem_bn_fuse): the conv-output
+// gradient dc = A*dz + B*c + Cc (dz = dy * ReLU bit; A, B, Cc from the BN's fp64 slots exactly as
+// bn_bwd_fin_apply computes them, same fp32 expression, same bf16 rounding) is formed in registers and
+// written into the LDS dy tile of stem_wgrad_kernel's layout. dc is consumed only by this weight
+// gradient (the stem has no input gradient), so it never goes to HBM: the apply's 2 B/element write,
+// the wgrad's 2 B/element re-read and one launch are gone; per pixel 128 B of dy + 128 B of c + 8 B of
+// mask bits are read. A tile's loads (dy, c, bits, input rows) are issued one tile ahead, into
+// registers, so they are in flight during the previous tile's taps and MFMAs; <= 80 KB of LDS keeps two
+// workgroups on a CU.
+constexpr int STEM_BN_CAP = 2048;  // staged input floats (8 KB): 32-wide images, 8 rows + halo = 1020
+
+template <int CAP>
+__global__ void __launch_bounds__(256, 2) stem_wgrad_bn_kernel(const float* __restrict__ x, const u16* __restrict__ dy,
+                                                             const uint8_t* __restrict__ mbits,
+                                                             const u16* __restrict__ cin, const BnBwdArgs a,
+                                                             float* __restrict__ slab, const StemGeom G, int tiles,
+                                                             u64* ts) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 32768];  // dc tile, col tile
+  __shared__ float xt[CAP];
+  __shared__ double part[4 * 2 * 64];
+  __shared__ float coef[3][64];
+  char* const dyt = smem;
+  char* const colt = smem + 32768;
+  stamp_start(ts);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, c8 = t & 7, r0 = t >> 3;
+  const uint32_t ntiles = (G.M + 255u) / 256u;
+  const uint32_t tile0 = blockIdx.x * (uint32_t)tiles;
+  // register image of one tile: pixel rows r0 + 32u, 16-B channel chunk c8 (coalesced: 8 lanes per row)
+  uint4 vd[8], vc[8];
+  uint32_t mk[8];
+  float xv[CAP / 256];
+  auto load = [&](uint32_t pix0, const StemTile& T) {
+    stem_stage_ld<CAP>(x, T, G, xv);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t p = min(pix0 + r0 + 32u * u, G.M - 1u);  // rows past M: a valid row (zero taps)
+      const size_t o = (size_t)p * 64 + c8 * 8;
+      vd[u] = *(const uint4*)(dy + o);
+      vc[u] = *(const uint4*)(cin + o);
+      mk[u] = mbits[o >> 3];
+    }
+  };
+  SlotFold f;
+  fold_issue_bwd(a, 64, 0, f);  // the fold's loads first (in-order vmcnt), then the first tile's
+  StemTile T = stem_tile<CAP>(tile0 * 256u, G);
+  if (tile0 < ntiles) load(tile0 * 256u, T);
+  fa_bwd_coef_from(a, f, 64, 0, part, coef[0], coef[1], coef[2]);
+  float A[8], B[8], Cc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    A[k] = coef[0][c8 * 8 + k];
+    B[k] = coef[1][c8 * 8 + k];
+    Cc[k] = coef[2][c8 * 8 + k];
+  }
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const int tsw = trswz(t);
+  for (int it = 0; it < tiles; ++it) {
+    const uint32_t tile = tile0 + it;
+    if (tile >= ntiles) break;
+    const uint32_t pix0 = tile * 256u;
+    // this tile's dc rows and input rows into LDS
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      float d[8], c[8], v[8];
+      unpack8(vd[u], d);
+      unpack8(vc[u], c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = (mk[u] >> k) & 1u ? d[k] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = A[k] * d[k] + B[k] * c[k] + Cc[k];
+      const int row = r0 + 32 * u;
+      *(uint4*)(dyt + row * 128 + ((c8 ^ trswz(row)) << 4)) = pack8(v);
+    }
+    stem_stage_st<CAP>(T, G, xv, xt);
+    const StemTile Tc = T;
+    // the next tile's loads, in flight during this tile's taps and MFMAs
+    if (it + 1 < tiles && tile + 1 < ntiles) {
+      T = stem_tile<CAP>(pix0 + 256u, G);
+      load(pix0 + 256u, T);
+    }
+    __syncthreads();
+    uint4 q[4];
+    stem_taps(x, xt, Tc, pix0 + t, G, q);  // zeros past M
+    // chunks 0..3 of a col row (the 27 taps + 5 zeros); frag_tr never reads chunks 4..7
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *(uint4*)(colt + t * 128 + ((j ^ tsw) << 4)) = q[j];
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const bf16x8 fa = frag_tr(dyt, wave * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, frag_tr(colt, j * 16, ks, lane), acc[j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  float* out = slab + (size_t)blockIdx.x * 64 * 32;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[(wave * 16 + 4 * (lane >> 4) + r) * 32 + j * 16 + (lane & 15)] = acc[j][r];
+  stamp_end(ts);
+}
+
+static int stem_bn_grid(int64_t M, int& tiles) {
+  const int64_t ntiles = (M + 255) / 256;
+  const int nwg0 = (int)std::min<int64_t>(ntiles, 512);  // two ~78 KB workgroups per CU
+  tiles = (int)((ntiles + nwg0 - 1) / nwg0);
+  return (int)((ntiles + tiles - 1) / tiles);
+}
+
+int stem_wgrad_bn(const float* x, const u16* dy, const uint8_t* mbits, const u16* c, const BnBwdArgs& a, float* dw27,
+                  float scale, int N, int H, int W, float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
+  DTC_CHECK_ARG(x && dy && mbits && c && dw27 && slab && a.acc && a.gamma && a.mean && a.invstd && N > 0 && H > 0 &&
+                    W > 0,
+                "stem_wgrad_bn: bad args");
+  const int64_t M = (int64_t)N * H * W;
+  DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_wgrad_bn: more than 2^31 pixels");
+  int tiles = 0;
+  const int nwg = stem_bn_grid(M, tiles);
+  DTC_CHECK_ARG(slab_bytes >= (size_t)nwg * 64 * 32 * 4, "stem_wgrad_bn: slab workspace too small");
+  hipLaunchKernelGGL(stem_wgrad_bn_kernel<STEM_BN_CAP>, dim3(nwg), dim3(256), 0, st, x, dy, mbits, c, a, slab,
+                     stem_geom(N, H, W), tiles, ts);
   DTC_LAUNCH_CHECK();
   return wgrad_reduce_to(slab, nwg, 64, 32, 27, 27, scale, dw27, st, ts);
 }

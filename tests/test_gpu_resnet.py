@@ -413,10 +413,13 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
         assert rel_err(ba[k], bb[k]) < 1e-4, k
 
 
-def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5):
+DEFAULT_STEM_BN_FUSE = 1
+
+
+def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5, hw=32):
     dtc._native.lib.dtc_set_option(b"graphs", int(graphs))
     try:
-        model, _, x, y = _setup(dtc, cuda, batch, seed=seed)
+        model, _, x, y = _setup(dtc, cuda, batch, seed=seed, hw=hw)
         crit = dtc.CrossEntropyLoss()
         xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
         out = []
@@ -517,6 +520,32 @@ def test_shortcut_compact_dx_matches_full(dtc, cuda, batch):
             lib.dtc_set_option(b"sc_compact", 1)
         for rep in range(2):
             np.testing.assert_array_equal(ga[rep], gb[rep])
+
+
+@pytest.mark.parametrize("batch,hw", [(8, 32), (256, 32), (8, 8)])
+def test_stem_bn_fused_wgrad_matches_separate(dtc, cuda, batch, hw):
+    """Option stem_bn_fuse: the stem BN's backward apply inside the stem weight gradient (dc formed per
+    tile in LDS, never stored) vs bn_bwd_fin_apply + stem_wgrad. Same coefficients, same fp32 expression
+    and bf16 rounding: every gradient but the stem conv's is identical; the stem conv's differs only by
+    the fp32 grouping of its per-workgroup partials (two tiles per workgroup instead of four at B=256;
+    the same grouping -- so identical -- at small batches). 8x8 images take the global-gather path."""
+    lib = dtc._native.lib
+    for graphs in (1, 0):
+        ga = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
+        lib.dtc_set_option(b"stem_bn_fuse", 1 - DEFAULT_STEM_BN_FUSE)
+        try:
+            gb = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
+        finally:
+            lib.dtc_set_option(b"stem_bn_fuse", DEFAULT_STEM_BN_FUSE)
+        lay = dtc.nn.Layout(100, 25.0)
+        for rep in range(2):
+            for pe in lay.params:
+                a = ga[rep][pe.offset:pe.offset + pe.numel]
+                b = gb[rep][pe.offset:pe.offset + pe.numel]
+                if pe.name == "conv1.weight" and batch > 64:
+                    assert rel_err(a, b) < 1e-5, (rep, pe.name, rel_err(a, b))
+                else:
+                    np.testing.assert_array_equal(a, b, err_msg=f"{pe.name} rep {rep} graphs {graphs}")
 
 
 def test_graph_recapture_on_option_change(dtc, cuda):
