@@ -50,20 +50,29 @@ struct IGemmParams {
   int wg_fast;
   uint32_t src0_bytes, src1_bytes;
   u64* ts;  // optional call timing slot: atomicMin(start), atomicMax(end), s_memrealtime ticks
+  // FWD, SC kernels: the projection shortcut (1x1, stride 2, pad 0) of the same input in the same
+  // launch. Its reduction is exactly the 3x3 conv's centre tap: reduction steps [kt_c0, kt_c1) stage
+  // W_sc's chunk beside W's and run a second set of MFMAs on the same im2col fragments.
+  const u16* src1b;  // W_sc [K][C]
+  u16* out2;         // shortcut output (NPQK)
+  double* stats2;    // its BN statistic slots
+  int kt_c0, kt_c1;
 };
 
-template <int MODE, int BM, int BN, int WR, int WC, bool SLAB, int NSTAGE>
+template <int MODE, int BM, int BN, int WR, int WC, bool SLAB, int NSTAGE, bool SC = false>
 __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   constexpr int FM = BM / (WR * 16);
   constexpr int FN = BN / (WC * 16);
   constexpr int A_BYTES = BM * 128;
-  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int SC_OFF = (BM + BN) * 128;             // SC: W_sc chunk after the A and B images
+  constexpr int STAGE = SC_OFF + (SC ? BM * 128 : 0);
   constexpr int NIA = BM / 32;  // glds instructions per wave per stage, A side
   constexpr int NIB = BN / 32;  // B side
   constexpr bool A_TR = (MODE != MODE_FWD);
   constexpr bool B_TR = (MODE == MODE_WGRAD);
   static_assert(WR * WC == 4, "4 waves");
   static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
+  static_assert(!SC || (MODE == MODE_FWD && !SLAB), "shortcut fusion: forward, no split-K");
 
   static_assert(NSTAGE == 2 || NSTAGE == 3, "stages");
   __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE];
@@ -220,6 +229,15 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
 #pragma unroll
       for (int j = 0; j < NIA; ++j)
         glds16(p.src1 + offA[j] + wadd, sb + (wave + 4 * j) * 1024);
+      if constexpr (SC) {
+        if (kt >= p.kt_c0 && kt < p.kt_c1) {  // centre tap: W_sc rows a0.., chunk cc (same swizzle)
+#pragma unroll
+          for (int j = 0; j < NIA; ++j) {
+            const int row = (wave + 4 * j) * 8 + lrow;
+            glds16(p.src1b + (a0 + row) * p.C + (pc ^ rowswz(row)) * 8 + cc * 64, sb + SC_OFF + (wave + 4 * j) * 1024);
+          }
+        }
+      }
       const int64_t xadd = ((int64_t)r * p.W + s) * p.C + cc * 64;
 #pragma unroll
       for (int j = 0; j < NIB; ++j) {
@@ -311,10 +329,17 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   };
 
   f32x4 acc[FM][FN];
+  f32x4 acc2[SC ? FM : 1][SC ? FN : 1];  // SC: the shortcut's tile
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (SC) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   const int wr = wave / WC, wc = wave % WC;
   const int arow0 = wr * (BM / WR), bcol0 = wc * (BN / WC);
@@ -326,7 +351,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
     }
   };
 
-  auto compute = [&](const char* cur) {
+  auto compute = [&](const char* cur, bool centre) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[FM], bfr[FN];
@@ -345,6 +370,17 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if constexpr (SC) {
+        if (centre) {  // block-uniform
+#pragma unroll
+          for (int i = 0; i < FM; ++i) af[i] = frag_row(cur + SC_OFF, arow0 + i * 16, ks, lane);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc2[i][j], 0, 0, 0);
+        }
+      }
     }
   };
 
@@ -380,7 +416,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
         stage(smem + slot * STAGE, kt_begin + nxt, r, s, cc);
         if constexpr (MODE != MODE_WGRAD) advance(r, s, cc);
       }
-      compute(smem + cur * STAGE);
+      compute(smem + cur * STAGE, SC && kt_begin + it >= p.kt_c0 && kt_begin + it < p.kt_c1);
       cur = (cur + 1 == NSTAGE) ? 0 : cur + 1;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -418,7 +454,8 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
     }
   } else if constexpr (MODE == MODE_FWD) {
     float* red = (float*)smem;  // [WC][BM][2]
-    const bool want_stats = (p.stats != nullptr);
+    auto epi = [&](const f32x4 (&A)[FM][FN], u16* out, double* stats) {
+    const bool want_stats = (stats != nullptr);
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int chl = arow0 + i * 16 + rq;
@@ -430,7 +467,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
         float v[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          v[t] = round_bf(acc[i][j][t]);
+          v[t] = round_bf(A[i][j][t]);
           s4[t] += v[t];
           q4[t] += v[t] * v[t];
         }
@@ -438,7 +475,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
           uint2 w;
           w.x = pack_bf2(v[0], v[1]);
           w.y = pack_bf2(v[2], v[3]);
-          *(uint2*)(p.out + (size_t)pix * p.K + ch) = w;
+          *(uint2*)(out + (size_t)pix * p.K + ch) = w;
         }
       }
       if (want_stats) {
@@ -468,10 +505,16 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
           s += red[(w * BM + threadIdx.x) * 2 + 0];
           q += red[(w * BM + threadIdx.x) * 2 + 1];
         }
-        double* st = p.stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * p.K;
+        double* st = stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * p.K;
         unsafeAtomicAdd(st + a0 + threadIdx.x, (double)s);
         unsafeAtomicAdd(st + p.K + a0 + threadIdx.x, (double)q);
       }
+    }
+    };
+    epi(acc, p.out, p.stats);
+    if constexpr (SC) {
+      __syncthreads();  // the stats scratch is reused
+      epi(acc2, p.out2, p.stats2);
     }
   } else {  // DGRAD bf16 (+ residual)
 #pragma unroll
@@ -688,14 +731,14 @@ static int fill_common(IGemmParams& p, const ConvShape& s) {
   return 0;
 }
 
-template <int MODE, int BM, int BN, int WR, int WC, bool SLAB>
+template <int MODE, int BM, int BN, int WR, int WC, bool SLAB, bool SC = false>
 static int launch_igemm(IGemmParams& p, int tiles_b, int splits, hipStream_t st, int gz = 1) {
   dim3 grid(p.tiles_a * tiles_b, splits, gz);
   p.xcd_remap = option_get(OPT_XCD_REMAP);
   if (option_get(OPT_IGEMM_STAGES) == 3)
-    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 3>), grid, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 3, SC>), grid, dim3(256), 0, st, p);
   else
-    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 2>), grid, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 2, SC>), grid, dim3(256), 0, st, p);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -794,6 +837,41 @@ int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* sta
   if (pl.bn == 64) return launch_igemm<MODE_FWD, 64, 64, 2, 2, false>(p, tiles_b, 1, st);
   if (pl.bm == 64) return launch_igemm<MODE_FWD, 64, 256, 1, 4, false>(p, tiles_b, 1, st);
   return launch_igemm<MODE_FWD, 128, 128, 2, 2, false>(p, tiles_b, 1, st);
+}
+
+// 3x3 stride-2 conv + its block's 1x1 stride-2 projection shortcut in one launch (option sc_fuse):
+// the shortcut's reduction is the centre tap of the 3x3's, so it reuses those im2col tiles (one read
+// of x, one launch). Same per-output MFMA order as the separate launch when that one has no split-K.
+bool conv_fwd_sc_ok(const ConvShape& s, const ConvShape& sc) {
+  if (!(s.R == 3 && s.S == 3 && s.stride == 2 && s.pad == 1 && sc.R == 1 && sc.S == 1 && sc.stride == 2 &&
+        sc.pad == 0 && sc.N == s.N && sc.H == s.H && sc.W == s.W && sc.C == s.C && sc.K == s.K && s.C % 64 == 0))
+    return false;
+  if (conv_c64_ok(s) || conv_halo_plan(s, CONV_FWD).cfg >= 0) return false;
+  const ConvPlan pl = plan_conv(s, CONV_FWD);
+  // 64x64 tiles; 128x128 only with sc_fuse=2 (its W_sc stage takes LDS to 96 KB: one workgroup per CU)
+  return pl.splits <= 1 && (pl.bn == 64 || (pl.bm != 64 && option_get(OPT_SC_FUSE) >= 2));
+}
+
+int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16* w, u16* y, double* stats,
+                const u16* wsc, u16* ysc, double* stats_sc, hipStream_t st, u64* ts) {
+  DTC_CHECK_ARG(conv_fwd_sc_ok(s, sc) && x && w && y && wsc && ysc, "conv_fwd_sc: unsupported shapes");
+  IGemmParams p{};
+  p.ts = ts;
+  DTC_TRY(fill_common(p, s));
+  const ConvPlan pl = plan_conv(s, CONV_FWD);
+  p.src0 = x; p.src1 = w; p.out = y; p.stats = stats;
+  p.src1b = wsc; p.out2 = ysc; p.stats2 = stats_sc;
+  p.M = s.N * p.P * p.Q;
+  p.fd_q = make_fastdiv(p.Q); p.fd_pq = make_fastdiv(p.P * p.Q); p.fd_cc = make_fastdiv(s.C / 64);
+  p.num_kt = pl.num_kt;
+  p.kt_per_split = p.num_kt;
+  const int nchunk = s.C / 64;
+  p.kt_c0 = (1 * s.S + 1) * nchunk;  // tap (r, s) = (1, 1): the pixel (2p, 2q) the 1x1 stride-2 conv reads
+  p.kt_c1 = p.kt_c0 + nchunk;
+  p.tiles_a = s.K / pl.bm;
+  const int tiles_b = ceil_div(p.M, pl.bn);
+  if (pl.bn == 64) return launch_igemm<MODE_FWD, 64, 64, 2, 2, false, true>(p, tiles_b, 1, st);
+  return launch_igemm<MODE_FWD, 128, 128, 2, 2, false, true>(p, tiles_b, 1, st);
 }
 
 // The BN-backward pass after a dgrad whose kernel has no fused epilogue for it (in place on dx).

@@ -66,8 +66,12 @@ enum {
   OPT_BN_RED_BLOCKS = 37,  // ... while keeping at least this many workgroups (tuning; default 256;
                            // 65536 / 64 measured -7%)
   OPT_BN_FA_BLOCKS = 38,   // BN fin_apply kernels: target workgroups per launch (tuning; default 1024; 256: -1%)
-  OPT_FORK_LAZY = 39,      // executor: 1 = fork the weight-gradient stream only where a wgrad launches
+  OPT_FORK_LAZY = 39,      // executor: 1 (default) = fork the weight-gradient stream only where a wgrad
+                           // launches (fewer cross-stream graph edges: +1.1%, two interleaved A/B sessions)
   OPT_SIDE_PRIO = 40,      // executor (at the side stream's creation): 1 = weight-gradient stream at low priority
+                           // (measured within noise; default 0)
+  OPT_SC_FUSE = 41,        // forward: 1 = the projection shortcut computed inside conv1's launch (conv_fwd_sc)
+  OPT_HEAD_DIRECT = 42,    // forward: 1 = the head launched after the graph into the caller's logits (no copy)
   OPT_COUNT
 };
 int option_get(int id);
@@ -93,6 +97,10 @@ ConvPlan plan_conv(const ConvShape& s, int mode);
 // first workgroups and every workgroup's exit time in s_memrealtime ticks (graph-safe per-call timing).
 int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
              size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
+// 3x3 stride-2 conv and the 1x1 stride-2 projection shortcut of the same input in one launch
+bool conv_fwd_sc_ok(const ConvShape& s, const ConvShape& sc);
+int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16* w, u16* y, double* stats,
+                const u16* wsc, u16* ysc, double* stats_sc, hipStream_t st, u64* ts = nullptr);
 // dx = conv_transpose(dy, w) (+ res), bf16 NHWC.
 // bnb (optional): dx is the gradient of a post-ReLU BN output; store dz = dx * [bnb->ym > 0] instead
 // and accumulate the BN-backward sums (bn_bwd_reduce's work) -- in the epilogue where the kernel

@@ -541,9 +541,16 @@ static int bn_act(Net& n, int mode, BNL& b, const u16* x, BNL* b2, const u16* x2
 static ConvShape f32_stem_shape(const Net& n);
 static int forward_body_f32(Net& n, float* logits, bool train, hipStream_t st);
 static int fork_sc(Net& n, hipStream_t st, hipStream_t* out);
+static bool sc_on(const Net& n);
 static int join_sc(Net& n, hipStream_t st);
 
 // everything after the input im2col (reads only executor-owned memory: capturable)
+static int forward_head(Net& n, float* logits, hipStream_t st) {
+  const BlockL& last = n.blocks.back();
+  return head_fwd(n.at<u16>(last.OUT), n.B, last.Hout * last.Wout, 512, n.wbf(n.fc_w), n.pf(n.fc_b), n.ncls,
+                  n.at<float>(n.FEAT), logits, st);
+}
+
 static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   if (n.f32) return forward_body_f32(n, logits, train, st);
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
@@ -568,16 +575,24 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   for (auto& b : n.blocks) {
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
     float* slab = n.at<float>(n.SLAB);
-    if (b.proj) {  // the shortcut conv first, on its own stream when sc_stream is on (joined below)
+    // option sc_fuse: the projection shortcut inside conv1's launch (its centre-tap im2col tiles)
+    const bool scf = b.proj && !sc_on(n) && option_get(OPT_SC_FUSE) != 0 && conv_fwd_sc_ok(b.c1.s, b.sc.s);
+    if (b.proj && !scf) {  // the shortcut conv first, on its own stream when sc_stream is on (joined below)
       hipStream_t ss = st;
       DTC_TRY(fork_sc(n, st, &ss));
       PROF(0, conv_flops(b.sc.s),
            conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr,
                     ss == st ? slab : n.at<float>(n.SLABSC), ss == st ? n.slab_bytes : n.slabsc_bytes, ss, ts));
     }
-    PROF(0, conv_flops(b.c1.s),
-         conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
-                  n.slab_bytes, st, ts));
+    if (scf) {
+      PROF(0, conv_flops(b.c1.s) + conv_flops(b.sc.s),
+           conv_fwd_sc(b.c1.s, b.sc.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr,
+                       n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr, st, ts));
+    } else {
+      PROF(0, conv_flops(b.c1.s),
+           conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
+                    n.slab_bytes, st, ts));
+    }
     DTC_TRY(bn_act(n, 1, b.b1, n.at<u16>(b.C1), nullptr, nullptr, n.at<u16>(b.A1), M, train, st, b.MA1));
     PROF(0, conv_flops(b.c2.s),
          conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
@@ -590,9 +605,8 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
     }
     in = n.at<u16>(b.OUT);
   }
-  const BlockL& last = n.blocks.back();
-  return head_fwd(in, n.B, last.Hout * last.Wout, 512, n.wbf(n.fc_w), n.pf(n.fc_b), n.ncls, n.at<float>(n.FEAT),
-                  logits, st);
+  if (logits == nullptr) return 0;  // graphed forward (option head_direct): head launched by forward()
+  return forward_head(n, logits, st);
 }
 
 // ------------------------------------------------------------------ fp32 mode (no autocast)
@@ -778,12 +792,16 @@ static int forward(Net& n, const float* x, float* logits, bool train, hipStream_
   else DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
   if (!graphs_on(n)) return forward_body(n, logits, train, st);
   hipGraphExec_t& ex = n.fwd_exec[train ? 1 : 0];
+  // option head_direct: the pool + FC head is launched after the graph, straight into the caller's
+  // logits (the graph cannot bake in a per-call pointer), instead of a graph-owned copy + D2D copy
+  const bool direct = !n.f32 && option_get(OPT_HEAD_DIRECT) != 0;
   if (!ex) {
     DTC_TRY(begin_capture(n));
-    const int rc = forward_body(n, n.at<float>(n.LOGITS), train, n.cap_st);
+    const int rc = forward_body(n, direct ? nullptr : n.at<float>(n.LOGITS), train, n.cap_st);
     DTC_TRY(end_capture(n, rc, &ex));
   }
   DTC_HIP(hipGraphLaunch(ex, st));
+  if (direct) return forward_head(n, logits, st);
   DTC_HIP(hipMemcpyAsync(logits, n.at<float>(n.LOGITS), (size_t)n.B * n.ncls * 4, hipMemcpyDeviceToDevice, st));
   return 0;
 }

@@ -414,6 +414,8 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
 
 
 DEFAULT_STEM_BN_FUSE = 1
+DEFAULT_SC_FUSE = 0
+DEFAULT_HEAD_DIRECT = 0
 
 
 def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5, hw=32):
@@ -546,6 +548,48 @@ def test_stem_bn_fused_wgrad_matches_separate(dtc, cuda, batch, hw):
                     assert rel_err(a, b) < 1e-5, (rep, pe.name, rel_err(a, b))
                 else:
                     np.testing.assert_array_equal(a, b, err_msg=f"{pe.name} rep {rep} graphs {graphs}")
+
+
+@pytest.mark.parametrize("level", [1, 2])
+def test_shortcut_fused_forward_matches_separate(dtc, cuda, level):
+    """Option sc_fuse: the projection shortcut (1x1 stride 2) computed inside conv1's launch from the
+    centre-tap im2col tiles (level 1: 64x64-tile plans, layers 3/4; level 2: also layer2's 128x128)
+    vs its own launch. Neither path splits K, and each output element sees the same MFMA sequence, so
+    the shortcut output, every BN statistic and every gradient are identical (graphs on and off)."""
+    lib = dtc._native.lib
+    for graphs in (1, 0):
+        try:
+            lib.dtc_set_option(b"sc_fuse", 0)
+            ga = _grads_repeated(dtc, cuda, graphs, batch=64)
+            lib.dtc_set_option(b"sc_fuse", level)
+            gb = _grads_repeated(dtc, cuda, graphs, batch=64)
+        finally:
+            lib.dtc_set_option(b"sc_fuse", DEFAULT_SC_FUSE)
+        for rep in range(2):
+            np.testing.assert_array_equal(ga[rep], gb[rep])
+
+
+def test_head_direct_matches_copy(dtc, cuda):
+    """Option head_direct: the head kernel launched after the forward graph straight into the caller's
+    logits vs the graph-owned logits + copy: identical logits and gradients (train and eval)."""
+    lib = dtc._native.lib
+    try:
+        lib.dtc_set_option(b"head_direct", 0)
+        ga = _grads_repeated(dtc, cuda, 1, batch=16)
+        model, _, x, _ = _setup(dtc, cuda, 16, seed=3)
+        xd = torch.from_numpy(x).to(cuda)
+        with torch.no_grad():
+            model.eval()
+            ea = _np(model(xd))
+        lib.dtc_set_option(b"head_direct", 1)
+        gb = _grads_repeated(dtc, cuda, 1, batch=16)
+        with torch.no_grad():
+            eb = _np(model(xd))
+    finally:
+        lib.dtc_set_option(b"head_direct", DEFAULT_HEAD_DIRECT)
+    for rep in range(2):
+        np.testing.assert_array_equal(ga[rep], gb[rep])
+    np.testing.assert_array_equal(ea, eb)
 
 
 def test_graph_recapture_on_option_change(dtc, cuda):
