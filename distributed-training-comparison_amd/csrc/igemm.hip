@@ -848,8 +848,14 @@ bool conv_fwd_sc_ok(const ConvShape& s, const ConvShape& sc) {
     return false;
   if (conv_c64_ok(s) || conv_halo_plan(s, CONV_FWD).cfg >= 0) return false;
   const ConvPlan pl = plan_conv(s, CONV_FWD);
-  // 64x64 tiles; 128x128 only with sc_fuse=2 (its W_sc stage takes LDS to 96 KB: one workgroup per CU)
-  return pl.splits <= 1 && (pl.bn == 64 || (pl.bm != 64 && option_get(OPT_SC_FUSE) >= 2));
+  // sc_fuse=1: 64x64-tile plans of at most 512 workgroups (layer4 at B=256: 35.3 us fused vs 8.2 + 31.1
+  // separate); 2: every 64x64 plan (layer3: 35.6 vs 9.7 + 23.0 -- the shortcut's own 1024-workgroup launch
+  // is cheaper than the fused kernel's lower occupancy); 3: also 128x128 (layer2: its W_sc stage takes
+  // LDS to 96 KB, one workgroup per CU: 44.1 vs 11.8 + 21.2)
+  const int lvl = option_get(OPT_SC_FUSE);
+  if (pl.splits > 1) return false;
+  if (pl.bn == 64) return lvl >= 2 || (int64_t)(s.K / 64) * ceil_div(s.N * ((s.H + 1) / 2) * ((s.W + 1) / 2), 64) <= 512;
+  return pl.bm != 64 && lvl >= 3;
 }
 
 int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16* w, u16* y, double* stats,

@@ -70,8 +70,11 @@ enum {
                            // launches (fewer cross-stream graph edges: +1.1%, two interleaved A/B sessions)
   OPT_SIDE_PRIO = 40,      // executor (at the side stream's creation): 1 = weight-gradient stream at low priority
                            // (measured within noise; default 0)
-  OPT_SC_FUSE = 41,        // forward: 1 = the projection shortcut computed inside conv1's launch (conv_fwd_sc)
-  OPT_HEAD_DIRECT = 42,    // forward: 1 = the head launched after the graph into the caller's logits (no copy)
+  OPT_SC_FUSE = 41,        // forward: the projection shortcut computed inside conv1's launch (conv_fwd_sc) for
+                           // 1 (default) layer4-size plans, 2 every 64x64 plan, 3 also 128x128 (igemm.hip)
+  OPT_HEAD_DIRECT = 42,    // forward: 1 (default) = the head launched after the graph into the caller's logits
+                           // (no graph-owned copy + D2D copy kernel)
+  OPT_STEM_RECOMPUTE = 43, // training forward: 1 = stem statistics pass + recompute pass with the BN apply fused
   OPT_COUNT
 };
 int option_get(int id);
@@ -272,6 +275,10 @@ int stem_fwd(const float* x, const u16* w27, u16* y, double* stats, int N, int H
 size_t stem_wgrad_slab_bytes(int64_t M);
 int stem_wgrad(const float* x, const u16* dy, float* dw27, float scale, int N, int H, int W, float* slab,
                size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
+// training forward, second pass (after a statistics-only stem_fwd with y = nullptr): recompute the conv,
+// store y and relu(BN(y)) + its ReLU mask bits (a: as bn_fin_apply's)
+int stem_fwd_bn(const float* x, const u16* w27, u16* y, const BnFwdArgs& a, u16* act, uint8_t* mask, int N, int H,
+                int W, hipStream_t st, u64* ts = nullptr);
 // stem weight gradient with the stem BN's backward apply fused: dc = A*(dy*bit) + B*c + Cc formed per
 // tile in LDS from (dy, mask bits, the conv output c) and the BN's slots (a: as bn_bwd_fin_apply's)
 int stem_wgrad_bn(const float* x, const u16* dy, const uint8_t* mbits, const u16* c, const BnBwdArgs& a, float* dw27,

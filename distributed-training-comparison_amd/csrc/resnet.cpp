@@ -559,7 +559,17 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   // forward accumulates into zeroed slots; its graph then starts with real work, no memset node) --
   // done by forward()'s input-copy launch on the direct-stem path
   if (train && !n.stem_direct) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));
-  if (n.stem_direct) {  // stem.hip: taps gathered per tile from the fp32 input, one K=32 k-step
+  // option stem_recompute: statistics pass + a recompute pass that applies the BN (stem.hip)
+  const bool srec = n.stem_direct && train && !n.sync && bn_fused() && bn_mask_on(n) &&
+                    option_get(OPT_STEM_RECOMPUTE) != 0;
+  if (srec) {
+    PROF(0, 2.0 * M0 * 64 * 27,
+         stem_fwd(n.at<float>(n.XIN), n.wbf(n.stem.pidx), nullptr, n.at<double>(n.bn0.stats), n.B, n.H, n.W, st, ts));
+    const BnFwdArgs a0 = fwd_args(n, n.bn0, M0);
+    PROF(0, 2.0 * M0 * 64 * 27,
+         stem_fwd_bn(n.at<float>(n.XIN), n.wbf(n.stem.pidx), n.at<u16>(n.C0), a0, n.at<u16>(n.A0),
+                     n.at<uint8_t>(n.MA0), n.B, n.H, n.W, st, ts));
+  } else if (n.stem_direct) {  // stem.hip: taps gathered per tile from the fp32 input, one K=32 k-step
     PROF(0, 2.0 * M0 * 64 * 27,
          stem_fwd(n.at<float>(n.XIN), n.wbf(n.stem.pidx), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
                   n.B, n.H, n.W, st, ts));
@@ -569,7 +579,7 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
          conv_fwd(n.stem.s, n.at<u16>(n.X0), n.at<u16>(n.WSTEM), n.at<u16>(n.C0),
                   train ? n.at<double>(n.bn0.stats) : nullptr, n.at<float>(n.SLAB), n.slab_bytes, st, ts));
   }
-  DTC_TRY(bn_act(n, 1, n.bn0, n.at<u16>(n.C0), nullptr, nullptr, n.at<u16>(n.A0), M0, train, st, n.MA0));
+  if (!srec) DTC_TRY(bn_act(n, 1, n.bn0, n.at<u16>(n.C0), nullptr, nullptr, n.at<u16>(n.A0), M0, train, st, n.MA0));
   const u16* in = n.at<u16>(n.A0);
   n.ev_next = 0;
   for (auto& b : n.blocks) {

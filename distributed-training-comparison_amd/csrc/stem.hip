@@ -150,9 +150,16 @@ static StemGeom stem_geom(int N, int H, int W) {
 // ds_read_b128 group read 16 consecutive pixels' same chunk -> 16 distinct 16-B bank slots.
 // <= 40 KB LDS and <= 128 VGPRs: four workgroups per CU, so the 1024 tiles of a 256 x 32 x 32 batch
 // are all resident at once and their load latencies overlap (a workgroup does little else).
+// APPLY (option stem_recompute, training): the stem BN's forward is split around two passes of this
+// kernel -- pass 1 (APPLY = false, y = nullptr) only accumulates the statistics (nothing stored: 12 B
+// of input per pixel read), pass 2 (APPLY) recomputes the conv (0.9 GFLOP), stores y and applies the
+// BN + ReLU to it in the same epilogue (act + ReLU mask bits, bn_fin_apply<RELU>'s arithmetic): the
+// separate apply's 128 B/pixel re-read of y is gone, and so is one launch.
+template <bool APPLY>
 __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restrict__ x, const u16* __restrict__ w27,
                                                       u16* __restrict__ y, double* __restrict__ stats, const StemGeom G,
-                                                      u64* ts) {
+                                                      u64* ts, const BnFwdArgs a, u16* __restrict__ act,
+                                                      uint8_t* __restrict__ mask) {
   // cols (16 KB) + the staged input rows (20 KB); after the MFMAs the first 32 KB hold the output
   // tile [256 pixels][128 B] for 16-B coalesced stores
   __shared__ __attribute__((aligned(16))) char smem[256 * 64 + STEM_LDS_FLOATS * 4];
@@ -163,6 +170,9 @@ __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restric
   stamp_start(ts);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint32_t pix0 = blockIdx.x * 256u;
+  float* const csc = &red[0][0][0];  // APPLY: BN scale / shift of the 64 channels (no statistics here)
+  SlotFold f;
+  if constexpr (APPLY) fold_issue_fwd(a, 64, 0, f);  // first: in-order vmcnt (bn_coef.h)
   // A fragments W[k = i*16 + lane%16][kk = 8*(lane/16) + 0..7] (kk >= 27: 0): all 32 loads issued
   // before the input tile's, so the two latencies overlap
   uint32_t we[4][4];  // bf16 pairs
@@ -174,6 +184,8 @@ __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restric
       const uint32_t a = w27[k * 27 + min(kk, 26)], b = w27[k * 27 + min(kk + 1, 26)];  // branch-free
       we[i][j] = (kk < 27 ? a : 0u) | ((kk + 1 < 27 ? b : 0u) << 16);
     }
+  // the fold's LDS scratch is the cols region (written only after the fold's last barrier)
+  if constexpr (APPLY) fa_fwd_coef_from(a, f, 64, 0, (double*)smem, csc, csc + 64);
   {
     const StemTile T = stem_stage(x, pix0, G, xt);
     __syncthreads();
@@ -224,16 +236,31 @@ __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restric
     }
   }
   __syncthreads();
-  {  // the tile is 256 consecutive pixels = one contiguous 32 KB block of y
+  if (y != nullptr) {  // the tile is 256 consecutive pixels = one contiguous 32 KB block of y
     const uint32_t npx = min(256u, G.M - pix0);
     uint4* dst = (uint4*)(y + (size_t)pix0 * 64);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int g = t + 256 * j, px = g >> 3, c = g & 7;
-      if ((uint32_t)px < npx) dst[g] = *(const uint4*)(ot + px * 128 + ((c ^ (px & 7)) << 4));
+      if ((uint32_t)px < npx) {
+        const uint4 raw = *(const uint4*)(ot + px * 128 + ((c ^ (px & 7)) << 4));
+        dst[g] = raw;
+        if constexpr (APPLY) {  // relu(y * scale + shift) and its mask byte (bn_fin_apply<RELU>)
+          float v[8];
+          unpack8(raw, v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            v[k] = v[k] * csc[c * 8 + k] + csc[64 + c * 8 + k];
+            v[k] = fmaxf(v[k], 0.f);
+          }
+          const uint4 pk = pack8(v);
+          ((uint4*)act)[(size_t)pix0 * 8 + g] = pk;
+          mask[(size_t)pix0 * 8 + g] = (uint8_t)Elt<u16>::mask8(pk);
+        }
+      }
     }
   }
-  if (stats != nullptr) {
+  if (!APPLY && stats != nullptr) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -262,11 +289,24 @@ __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restric
 }
 
 int stem_fwd(const float* x, const u16* w27, u16* y, double* stats, int N, int H, int W, hipStream_t st, u64* ts) {
-  DTC_CHECK_ARG(x && w27 && y && N > 0 && H > 0 && W > 0, "stem_fwd: bad args");
+  DTC_CHECK_ARG(x && w27 && (y || stats) && N > 0 && H > 0 && W > 0, "stem_fwd: bad args");
   const int64_t M = (int64_t)N * H * W;
   DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_fwd: more than 2^31 pixels");
-  hipLaunchKernelGGL(stem_fwd_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y, stats,
-                     stem_geom(N, H, W), ts);
+  hipLaunchKernelGGL(stem_fwd_kernel<false>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y, stats,
+                     stem_geom(N, H, W), ts, BnFwdArgs{}, nullptr, nullptr);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
+int stem_fwd_bn(const float* x, const u16* w27, u16* y, const BnFwdArgs& a, u16* act, uint8_t* mask, int N, int H,
+                int W, hipStream_t st, u64* ts) {
+  DTC_CHECK_ARG(x && w27 && y && act && mask && a.stats && a.gamma && a.beta && a.mean && a.invstd && N > 0 &&
+                    H > 0 && W > 0,
+                "stem_fwd_bn: bad args");
+  const int64_t M = (int64_t)N * H * W;
+  DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_fwd_bn: more than 2^31 pixels");
+  hipLaunchKernelGGL(stem_fwd_kernel<true>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y, nullptr,
+                     stem_geom(N, H, W), ts, a, act, mask);
   DTC_LAUNCH_CHECK();
   return 0;
 }

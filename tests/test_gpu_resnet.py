@@ -414,8 +414,9 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
 
 
 DEFAULT_STEM_BN_FUSE = 1
-DEFAULT_SC_FUSE = 0
-DEFAULT_HEAD_DIRECT = 0
+DEFAULT_SC_FUSE = 1
+DEFAULT_HEAD_DIRECT = 1
+DEFAULT_STEM_RECOMPUTE = 0
 
 
 def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5, hw=32):
@@ -550,11 +551,11 @@ def test_stem_bn_fused_wgrad_matches_separate(dtc, cuda, batch, hw):
                     np.testing.assert_array_equal(a, b, err_msg=f"{pe.name} rep {rep} graphs {graphs}")
 
 
-@pytest.mark.parametrize("level", [1, 2])
+@pytest.mark.parametrize("level", [1, 2, 3])
 def test_shortcut_fused_forward_matches_separate(dtc, cuda, level):
     """Option sc_fuse: the projection shortcut (1x1 stride 2) computed inside conv1's launch from the
-    centre-tap im2col tiles (level 1: 64x64-tile plans, layers 3/4; level 2: also layer2's 128x128)
-    vs its own launch. Neither path splits K, and each output element sees the same MFMA sequence, so
+    centre-tap im2col tiles (level 1: layer4's plan at B=64 and 256; 2: every 64x64-tile plan; 3: also
+    layer2's 128x128) vs its own launch. Neither path splits K, and each output element sees the same MFMA sequence, so
     the shortcut output, every BN statistic and every gradient are identical (graphs on and off)."""
     lib = dtc._native.lib
     for graphs in (1, 0):
@@ -565,6 +566,24 @@ def test_shortcut_fused_forward_matches_separate(dtc, cuda, level):
             gb = _grads_repeated(dtc, cuda, graphs, batch=64)
         finally:
             lib.dtc_set_option(b"sc_fuse", DEFAULT_SC_FUSE)
+        for rep in range(2):
+            np.testing.assert_array_equal(ga[rep], gb[rep])
+
+
+@pytest.mark.parametrize("batch,hw", [(8, 32), (256, 32), (8, 8)])
+def test_stem_recompute_matches_single_pass(dtc, cuda, batch, hw):
+    """Option stem_recompute: a statistics-only stem pass + a recompute pass that stores the conv output
+    and applies the BN + ReLU (+ mask bits) in its epilogue, vs the stem conv + bn_fin_apply. Same conv,
+    same fp64 statistics, same apply arithmetic: identical gradients over two training steps."""
+    lib = dtc._native.lib
+    for graphs in (1, 0):
+        try:
+            lib.dtc_set_option(b"stem_recompute", 0)
+            ga = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
+            lib.dtc_set_option(b"stem_recompute", 1)
+            gb = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
+        finally:
+            lib.dtc_set_option(b"stem_recompute", DEFAULT_STEM_RECOMPUTE)
         for rep in range(2):
             np.testing.assert_array_equal(ga[rep], gb[rep])
 
@@ -614,14 +633,18 @@ def test_live_conv_profile(dtc, cuda):
     model, _, x, y = _setup(dtc, cuda, 8, seed=7)
     crit = dtc.CrossEntropyLoss()
     xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
-    crit(model(xd), yd).backward()
-    exe = model.executor(8, 32, 32)
-    dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
-    steps = 3
-    for _ in range(steps):
+    dtc._native.lib.dtc_set_option(b"sc_fuse", 0)  # one launch per conv (sc_fuse merges conv1 + shortcut)
+    try:
         crit(model(xd), yd).backward()
-    ms, fl, cnt = (C.c_double * 3)(), (C.c_double * 3)(), (C.c_int * 3)()
-    dtc._native.call("dtc_rn18_profile_end", exe.handle, ms, fl, cnt)
+        exe = model.executor(8, 32, 32)
+        dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
+        steps = 3
+        for _ in range(steps):
+            crit(model(xd), yd).backward()
+        ms, fl, cnt = (C.c_double * 3)(), (C.c_double * 3)(), (C.c_int * 3)()
+        dtc._native.call("dtc_rn18_profile_end", exe.handle, ms, fl, cnt)
+    finally:
+        dtc._native.lib.dtc_set_option(b"sc_fuse", DEFAULT_SC_FUSE)
     # 20 convs; the stem has no dgrad; the 13 stride-1 3x3 weight gradients run batched per geometry
     # within a DDP bucket (layer4 3, layer3 3, layer2 3, layer1 4: four launches) beside the 7 others
     assert list(cnt) == [20 * steps, 19 * steps, 11 * steps]
