@@ -75,6 +75,8 @@ enum {
   OPT_HEAD_DIRECT = 42,    // forward: 1 (default) = the head launched after the graph into the caller's logits
                            // (no graph-owned copy + D2D copy kernel)
   OPT_STEM_RECOMPUTE = 43, // training forward: 1 = stem statistics pass + recompute pass with the BN apply fused
+  OPT_STEM_WLDS = 44,      // stem forward: 1 (default) = weight staged in LDS by coalesced loads, not per-lane
+                           // 2-B gathers (stem_bench: 18.7 -> 16.1 us; +1.1% interleaved A/B)
   OPT_COUNT
 };
 int option_get(int id);

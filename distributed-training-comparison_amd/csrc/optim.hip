@@ -155,8 +155,34 @@ __global__ void amp_check_finite_kernel(const float* __restrict__ g, int64_t n, 
   if (__any(bad) && (threadIdx.x & 63) == 0) *found = 1;
 }
 
+// 16-B aligned gradients (the flat buffer): float4 loads, four in flight per thread per trip
+__global__ void amp_check_finite4_kernel(const float* __restrict__ g, int64_t n, int* __restrict__ found) {
+  const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * 256;
+  const f32x4* __restrict__ g4 = (const f32x4*)g;
+  bool bad = false;
+  int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    const f32x4 a = g4[i], b = g4[i + stride], c = g4[i + 2 * stride], d = g4[i + 3 * stride];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bad |= !isfinite(a[k]) | !isfinite(b[k]) | !isfinite(c[k]) | !isfinite(d[k]);
+  }
+  for (; i < n4; i += stride) {
+    const f32x4 a = g4[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bad |= !isfinite(a[k]);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) bad |= !isfinite(g[(n4 << 2) + threadIdx.x]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) *found = 1;
+}
+
 int amp_check_finite(const float* g, int64_t n, int* found_inf, hipStream_t st) {
   DTC_CHECK_ARG(g && found_inf && n > 0, "amp_check_finite: bad args");
+  if (((uintptr_t)g & 15) == 0) {
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n / 4 + 255) / 256));
+    hipLaunchKernelGGL(amp_check_finite4_kernel, dim3(blocks), dim3(256), 0, st, g, n, found_inf);
+    DTC_LAUNCH_CHECK();
+    return 0;
+  }
   const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
   hipLaunchKernelGGL(amp_check_finite_kernel, dim3(blocks), dim3(256), 0, st, g, n, found_inf);
   DTC_LAUNCH_CHECK();

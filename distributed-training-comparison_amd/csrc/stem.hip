@@ -155,19 +155,25 @@ static StemGeom stem_geom(int N, int H, int W) {
 // of input per pixel read), pass 2 (APPLY) recomputes the conv (0.9 GFLOP), stores y and applies the
 // BN + ReLU to it in the same epilogue (act + ReLU mask bits, bn_fin_apply<RELU>'s arithmetic): the
 // separate apply's 128 B/pixel re-read of y is gone, and so is one launch.
-template <bool APPLY>
+// WL (option stem_wlds): the [64][27] bf16 weight is read once per workgroup with coalesced 4-B loads
+// into LDS and the A fragments are gathered from there, instead of 32 scattered 2-B global loads per
+// lane; the staged input rows are capped at 8 KB (STEM_BN_CAP) so the LDS stays at four per CU.
+template <bool APPLY, bool WL = false>
 __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restrict__ x, const u16* __restrict__ w27,
                                                       u16* __restrict__ y, double* __restrict__ stats, const StemGeom G,
                                                       u64* ts, const BnFwdArgs a, u16* __restrict__ act,
                                                       uint8_t* __restrict__ mask) {
-  // cols (16 KB) + the staged input rows (20 KB); after the MFMAs the first 32 KB hold the output
-  // tile [256 pixels][128 B] for 16-B coalesced stores
-  __shared__ __attribute__((aligned(16))) char smem[256 * 64 + STEM_LDS_FLOATS * 4];
+  constexpr int CAP = WL ? 2048 : STEM_LDS_FLOATS;
+  // cols (16 KB) + the staged input rows (20 KB; WL 8 KB); after the MFMAs the first 32 KB hold the
+  // output tile [256 pixels][128 B] for 16-B coalesced stores
+  __shared__ __attribute__((aligned(16))) char smem[(256 * 64 + CAP * 4) > 32768 ? (256 * 64 + CAP * 4) : 32768];
   __shared__ float red[4][64][2];
+  __shared__ uint32_t wsh[WL ? 864 : 1];  // WL: the weight, 64 x 27 bf16 = 864 words
   uint4* const cols = (uint4*)smem;
   float* const xt = (float*)(smem + 256 * 64);
   char* const ot = smem;
   stamp_start(ts);
+  static_assert(!(APPLY && WL), "stem_fwd: WL with the recompute-apply pass is not built");
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint32_t pix0 = blockIdx.x * 256u;
   float* const csc = &red[0][0][0];  // APPLY: BN scale / shift of the 64 channels (no statistics here)
@@ -176,19 +182,44 @@ __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restric
   // A fragments W[k = i*16 + lane%16][kk = 8*(lane/16) + 0..7] (kk >= 27: 0): all 32 loads issued
   // before the input tile's, so the two latencies overlap
   uint32_t we[4][4];  // bf16 pairs
+  if constexpr (!WL) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = i * 16 + (lane & 15), kk = 8 * (lane >> 4) + 2 * j;
-      const uint32_t a = w27[k * 27 + min(kk, 26)], b = w27[k * 27 + min(kk + 1, 26)];  // branch-free
-      we[i][j] = (kk < 27 ? a : 0u) | ((kk + 1 < 27 ? b : 0u) << 16);
-    }
-  // the fold's LDS scratch is the cols region (written only after the fold's last barrier)
-  if constexpr (APPLY) fa_fwd_coef_from(a, f, 64, 0, (double*)smem, csc, csc + 64);
+      for (int j = 0; j < 4; ++j) {
+        const int k = i * 16 + (lane & 15), kk = 8 * (lane >> 4) + 2 * j;
+        const uint32_t a = w27[k * 27 + min(kk, 26)], b = w27[k * 27 + min(kk + 1, 26)];  // branch-free
+        we[i][j] = (kk < 27 ? a : 0u) | ((kk + 1 < 27 ? b : 0u) << 16);
+      }
+  }
+  uint32_t wv[4];
+  if constexpr (WL) {  // 864 words, coalesced (the weight is 4-B aligned: KRSC rows of 27 bf16 from an even offset)
+    const uint32_t* w32 = (const uint32_t*)w27;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) wv[u] = w32[min(t + 256 * u, 863)];
+  }
   {
-    const StemTile T = stem_stage(x, pix0, G, xt);
+    const StemTile T = WL ? stem_tile<CAP>(pix0, G) : stem_tile<STEM_LDS_FLOATS>(pix0, G);
+    float xv[CAP / 256];
+    stem_stage_ld<CAP>(x, T, G, xv);
+    stem_stage_st<CAP>(T, G, xv, xt);
+    if constexpr (WL) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (t + 256 * u < 864) wsh[t + 256 * u] = wv[u];
+    }
     __syncthreads();
+    if constexpr (WL) {
+      const u16* wl = (const u16*)wsh;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = i * 16 + (lane & 15), kk = 8 * (lane >> 4) + 2 * j;
+          const uint32_t a = wl[k * 27 + min(kk, 26)], b = wl[k * 27 + min(kk + 1, 26)];
+          we[i][j] = (kk < 27 ? a : 0u) | ((kk + 1 < 27 ? b : 0u) << 16);
+        }
+    }
     uint4 q[4];
     stem_taps(x, xt, T, pix0 + t, G, q);
 #pragma unroll
@@ -292,8 +323,12 @@ int stem_fwd(const float* x, const u16* w27, u16* y, double* stats, int N, int H
   DTC_CHECK_ARG(x && w27 && (y || stats) && N > 0 && H > 0 && W > 0, "stem_fwd: bad args");
   const int64_t M = (int64_t)N * H * W;
   DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_fwd: more than 2^31 pixels");
-  hipLaunchKernelGGL(stem_fwd_kernel<false>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y, stats,
-                     stem_geom(N, H, W), ts, BnFwdArgs{}, nullptr, nullptr);
+  if (option_get(OPT_STEM_WLDS) != 0 && ((uintptr_t)w27 & 3) == 0)
+    hipLaunchKernelGGL((stem_fwd_kernel<false, true>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y,
+                       stats, stem_geom(N, H, W), ts, BnFwdArgs{}, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL((stem_fwd_kernel<false, false>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y,
+                       stats, stem_geom(N, H, W), ts, BnFwdArgs{}, nullptr, nullptr);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -305,7 +340,7 @@ int stem_fwd_bn(const float* x, const u16* w27, u16* y, const BnFwdArgs& a, u16*
                 "stem_fwd_bn: bad args");
   const int64_t M = (int64_t)N * H * W;
   DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_fwd_bn: more than 2^31 pixels");
-  hipLaunchKernelGGL(stem_fwd_kernel<true>, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y, nullptr,
+  hipLaunchKernelGGL((stem_fwd_kernel<true, false>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y, nullptr,
                      stem_geom(N, H, W), ts, a, act, mask);
   DTC_LAUNCH_CHECK();
   return 0;

@@ -417,6 +417,7 @@ DEFAULT_STEM_BN_FUSE = 1
 DEFAULT_SC_FUSE = 1
 DEFAULT_HEAD_DIRECT = 1
 DEFAULT_STEM_RECOMPUTE = 0
+DEFAULT_STEM_WLDS = 1
 
 
 def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5, hw=32):
@@ -586,6 +587,23 @@ def test_stem_recompute_matches_single_pass(dtc, cuda, batch, hw):
             lib.dtc_set_option(b"stem_recompute", DEFAULT_STEM_RECOMPUTE)
         for rep in range(2):
             np.testing.assert_array_equal(ga[rep], gb[rep])
+
+
+@pytest.mark.parametrize("batch,hw", [(8, 32), (256, 32), (8, 8)])
+def test_stem_weight_lds_matches_gather(dtc, cuda, batch, hw):
+    """Option stem_wlds: the stem forward's weight fragments gathered from an LDS copy (coalesced loads)
+    instead of per-lane global gathers; the input rows capped at 8 KB of LDS (wider tiles take the
+    global-gather path). The same values reach the same MFMAs: identical gradients."""
+    lib = dtc._native.lib
+    try:
+        lib.dtc_set_option(b"stem_wlds", 0)
+        ga = _grads_repeated(dtc, cuda, 1, batch=batch, hw=hw)
+        lib.dtc_set_option(b"stem_wlds", 1)
+        gb = _grads_repeated(dtc, cuda, 1, batch=batch, hw=hw)
+    finally:
+        lib.dtc_set_option(b"stem_wlds", DEFAULT_STEM_WLDS)
+    for rep in range(2):
+        np.testing.assert_array_equal(ga[rep], gb[rep])
 
 
 def test_head_direct_matches_copy(dtc, cuda):

@@ -33,6 +33,15 @@ def timeit(fn, iters):
     return best
 
 
+def _with_opt(nat, name, val, fn):
+    old = nat.lib.dtc_get_option(name.encode())
+    nat.lib.dtc_set_option(name.encode(), val)
+    try:
+        return fn()
+    finally:
+        nat.lib.dtc_set_option(name.encode(), old)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
@@ -57,6 +66,8 @@ def main():
                                                   nat.stream_ptr()), a.iters),
         "stem_fwd": timeit(lambda: nat.call("dtc_stem_fwd", P(x), P(w27), P(y), None, B, S, S, nat.stream_ptr()),
                            a.iters),
+        "stem_fwd+stats (wlds)": _with_opt(nat, "stem_wlds", 1, lambda: timeit(
+            lambda: nat.call("dtc_stem_fwd", P(x), P(w27), P(y), P(stats), B, S, S, nat.stream_ptr()), a.iters)),
         "stem_wgrad(+reduce)": timeit(lambda: nat.call("dtc_stem_wgrad", P(x), P(dy), P(dw), 1.0, B, S, S, P(ws), nb,
                                                        nat.stream_ptr()), a.iters),
         "copy_y_33MB": timeit(lambda: y.copy_(dy), a.iters),
