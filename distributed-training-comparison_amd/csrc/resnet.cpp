@@ -116,6 +116,7 @@ struct Net {
   int graph_epoch = -1;
   hipGraphExec_t fwd_exec[2] = {nullptr, nullptr};
   std::vector<Seg> bwd_segs;
+  std::vector<hipGraphExec_t> retired;  // replaced graph execs, destroyed one drop later (drop_graphs)
   float bwd_gs = 0.f;
   bool bwd_comm = false;
   size_t LOGITS = 0, DLOGITS = 0;  // graph-owned copies of the caller's logits / dlogits
@@ -425,20 +426,29 @@ static u64* prof_slot(Net& n, int kind, double flops) {
   } while (0)
 
 // ------------------------------------------------------------------ graph capture helpers
-static void drop_graphs(Net& n) {
+static void drop_graphs(Net& n, bool final_ = false) {
   // a graph exec may still be running (the caller's previous step is asynchronous): destroying it then
-  // frees state its in-flight kernels use (seen as a later crash in a sync), so drain the device first
+  // frees state its in-flight kernels use (seen as a later crash in a sync), so drain the device first.
+  // Even after the drain the runtime's own completion handling of the last launch can still touch the
+  // exec from a worker thread (a rare crash outside the calling thread in test_live_conv_profile), so
+  // replaced execs are retired here and destroyed at the NEXT drop, when nothing can reference them.
   bool any = !n.bwd_segs.empty();
   for (auto e : n.fwd_exec) any = any || e != nullptr;
-  if (any) (void)hipDeviceSynchronize();
+  if (any || final_) (void)hipDeviceSynchronize();
+  for (auto e : n.retired) (void)hipGraphExecDestroy(e);
+  n.retired.clear();
   for (auto& e : n.fwd_exec)
     if (e) {
-      (void)hipGraphExecDestroy(e);
+      n.retired.push_back(e);
       e = nullptr;
     }
   for (auto& sg : n.bwd_segs)
-    if (sg.exec) (void)hipGraphExecDestroy(sg.exec);
+    if (sg.exec) n.retired.push_back(sg.exec);
   n.bwd_segs.clear();
+  if (final_) {
+    for (auto e : n.retired) (void)hipGraphExecDestroy(e);
+    n.retired.clear();
+  }
 }
 static bool graphs_on(Net& n) {
   if (n.capture || n.sync || option_get(OPT_GRAPHS) == 0) return false;
@@ -1414,7 +1424,7 @@ static void prof_free(Net& n) {
 
 int dtc_rn18_destroy(dtc_net* net) {
   if (net) {
-    drop_graphs(net->n);
+    drop_graphs(net->n, true);
     if (net->n.cap_st) (void)hipStreamDestroy(net->n.cap_st);
     if (net->n.side_st) (void)hipStreamDestroy(net->n.side_st);
     if (net->n.sc_st) (void)hipStreamDestroy(net->n.sc_st);

@@ -198,6 +198,8 @@ __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restric
 #pragma unroll
     for (int u = 0; u < 4; ++u) wv[u] = w32[min(t + 256 * u, 863)];
   }
+  // the fold's LDS scratch is the cols region (written only after the fold's last barrier)
+  if constexpr (APPLY) fa_fwd_coef_from(a, f, 64, 0, (double*)smem, csc, csc + 64);
   {
     const StemTile T = WL ? stem_tile<CAP>(pix0, G) : stem_tile<STEM_LDS_FLOATS>(pix0, G);
     float xv[CAP / 256];

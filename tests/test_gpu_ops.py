@@ -338,6 +338,26 @@ def test_sgd_and_amp(dtc, cuda):
     assert float(scale) == 65536.0 and abs(float(inv) - 1 / 65536.0) < 1e-12
 
 
+@pytest.mark.parametrize("n", [1, 7, 4096, 1_048_579, 11_220_000])
+def test_amp_check_finite_positions(dtc, cuda, n):
+    """found_inf over every region of the vectorised check: the 4-deep float4 trips, the float4
+    remainder trips, the scalar tail (n % 4), an unaligned view (scalar kernel); finite input: 0."""
+    found = torch.zeros(1, dtype=torch.int32, device=cuda)
+    base = torch.zeros(n + 1, device=cuda)
+    dtc.ops.amp_check_finite(base[:n], found)
+    assert int(found.item()) == 0
+    for pos in sorted({p for p in (0, n // 3, n // 2, n - 1 - (n % 4), n - 1) if 0 <= p < n}):
+        for bad in (float("inf"), float("-inf"), float("nan")):
+            g = base.clone()
+            g[pos] = bad
+            found.zero_()
+            dtc.ops.amp_check_finite(g[:n], found)
+            assert int(found.item()) == 1, (n, pos, bad)
+            found.zero_()
+            dtc.ops.amp_check_finite(g[1:n + 1] if pos > 0 else g[:n], found)  # 4-B offset: scalar kernel
+            assert int(found.item()) == 1, (n, pos, bad, "unaligned")
+
+
 @pytest.mark.parametrize("case", [
     (4, 32, 32, 64, 64),    # layer1 geometry: 2 output rows per 64-pixel step
     (3, 8, 8, 64, 128),     # whole 8x8 image per step, 3 steps (ragged split)
