@@ -311,11 +311,18 @@ _PRESCALER = [None]
 
 
 def prescale(loss: "NativeLoss") -> None:
+    """Enqueue loss * scale AND build its NativeLoss wrapper now, while the GPU is busy with the
+    forward: scaler.scale(loss) after the per-step barrier then only looks it up (the wrapper's
+    Tensor._make_subclass and closures cost 10-30 us of host time, all of it GPU idle time there)."""
     ref = _PRESCALER[0]
     sc = ref() if ref is not None else None
     if sc is None or sc._scale is None or not sc._enabled:
         return
-    loss._dtc_prescaled = (ops.amp_scale(loss.detach(), sc._scale), sc._scale, sc._version)
+    scale = sc._scale
+    f = loss._dtc_fast
+    wrapped = _wrap_loss(ops.amp_scale(loss.detach(), scale), lambda: loss._dtc_graph * scale,
+                         None if f is None else (f[0], f[1], f[2], f[3], scale))
+    loss._dtc_prescaled = (wrapped, scale, sc._version)
 
 
 def scaled_loss(loss: torch.Tensor, scale: torch.Tensor, version: int = -1) -> torch.Tensor:
@@ -325,9 +332,10 @@ def scaled_loss(loss: torch.Tensor, scale: torch.Tensor, version: int = -1) -> t
     if isinstance(loss, NativeLoss):
         f = loss._dtc_fast
         pre = loss.__dict__.get("_dtc_prescaled")
-        if pre is not None and pre[1] is scale and pre[2] == version:
-            return _wrap_loss(pre[0], lambda: loss._dtc_graph * scale,
-                              None if f is None else (f[0], f[1], f[2], f[3], scale))
+        if pre is not None and pre[1] is scale and pre[2] == version and pre[0]._dtc_fast is not None:
+            # the wrapper built by prescale() (same value, same backward chain) until a backward has
+            # consumed its direct chain; after that a fresh wrapper is built below
+            return pre[0]
         # the value on the native kernel (GradScaler K9: no torch elementwise launch in the step)
         return _wrap_loss(ops.amp_scale(loss.detach(), scale), lambda: loss._dtc_graph * scale,
                           None if f is None else (f[0], f[1], f[2], f[3], scale))

@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--no-barrier", action="store_true")
+    ap.add_argument("--torch-barrier", action="store_true", help="dist.barrier() instead of bench.py's dtc.barrier()")
     ap.add_argument("--cprofile", action="store_true", help="cProfile the timed steps (top functions by tottime)")
     ap.add_argument("--spin", action="store_true", help="hipSetDeviceFlags(hipDeviceScheduleSpin) before init")
     args = ap.parse_args()
@@ -55,7 +56,10 @@ def main():
             loss = crit(logit, label)
         t.append(time.perf_counter())
         if not args.no_barrier:
-            dist.barrier()
+            if args.torch_barrier:
+                dist.barrier()
+            else:
+                dtc.barrier()
         t.append(time.perf_counter())
         scaled = scaler.scale(loss)
         t.append(time.perf_counter())
