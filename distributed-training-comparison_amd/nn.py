@@ -152,9 +152,13 @@ class Executor:
              stream_ptr())
 
     def xent_backward(self, logits, labels, lse, gscale, grad_scale: float, comm) -> None:
-        """CrossEntropy backward into the executor's dlogits buffer + the network backward, one call."""
-        call("dtc_rn18_xent_backward", self.handle, ptr(logits), ptr(labels), ptr(lse), ptr(gscale),
-             float(grad_scale), comm.handle if comm else None, stream_ptr())
+        """CrossEntropy backward into the executor's dlogits buffer + the network backward, one call.
+        Runs right after the per-step barrier, when the GPU is idle until it returns: the current
+        stream is read with torch's raw-stream call (torch.cuda.current_stream() builds a Stream object
+        through several Python device lookups)."""
+        call("dtc_rn18_xent_backward", self.handle, logits.data_ptr(), labels.data_ptr(), lse.data_ptr(),
+             None if gscale is None else gscale.data_ptr(), float(grad_scale), comm.handle if comm else None,
+             _raw_stream(logits.device.index))
 
     def dlogits_buffer(self) -> torch.Tensor:
         """fp32 [batch, num_classes] view of the executor's own dlogits buffer: a loss gradient
@@ -193,6 +197,16 @@ class Executor:
         if h:
             lib.dtc_rn18_destroy(h)
             self.handle = None
+
+
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _raw_stream(index) -> int:
+    """Current HIP stream of device `index` (same value as stream_ptr() on that device)."""
+    if _RAW_STREAM is not None:
+        return _RAW_STREAM(index if index is not None else torch.cuda.current_device())
+    return stream_ptr()
 
 
 # ----------------------------------------------------------------------------- autograd nodes
