@@ -68,8 +68,8 @@ enum {
   OPT_BN_FA_BLOCKS = 38,   // BN fin_apply kernels: target workgroups per launch (tuning; default 1024; 256: -1%)
   OPT_FORK_LAZY = 39,      // executor: 1 (default) = fork the weight-gradient stream only where a wgrad
                            // launches (fewer cross-stream graph edges: +1.1%, two interleaved A/B sessions)
-  OPT_SIDE_PRIO = 40,      // executor (at the side stream's creation): 1 = weight-gradient stream at low priority
-                           // (measured within noise; default 0)
+  OPT_SIDE_PRIO = 40,      // executor (at the side stream's creation): 1 (default) = weight-gradient stream at
+                           // low priority (+0.35%, higher in 6 of 6 interleaved A/B rounds)
   OPT_SC_FUSE = 41,        // forward: the projection shortcut computed inside conv1's launch (conv_fwd_sc) for
                            // 1 (default) layer4-size plans, 2 every 64x64 plan, 3 also 128x128 (igemm.hip)
   OPT_HEAD_DIRECT = 42,    // forward: 1 (default) = the head launched after the graph into the caller's logits
