@@ -98,3 +98,25 @@ def test_workspace_and_conv_plans(dtc):
     assert 30e9 < ws < 200e9, ws  # well inside 288 GB
     lib.dtc_rn18_destroy(h)
     assert lib.dtc_rn18_create(C.byref(h), 700, 224, 224, 100, 25.0) < 0  # int32 element-index guard
+
+
+# executor / kernel options added by the round-2 performance work, with their defaults (kernels.h)
+_OPTION_DEFAULTS = {
+    "stem_bn_fuse": 1, "fork_lazy": 1, "side_prio": 1, "sc_fuse": 1, "head_direct": 1, "stem_wlds": 1,
+    "stem_recompute": 0, "wgrad_tail": 0, "bn_red_elems": 16384, "bn_red_blocks": 256, "bn_fa_blocks": 1024,
+    "sc_compact": 1, "stem_prologue": 1, "dgrad_class_order": 1, "wgrad_direct": 1, "wgrad_xcd": 1,
+}
+
+
+def test_options_registered_with_defaults(dtc):
+    """dtc_set_option / dtc_get_option (host only): every option has its documented default, a set is
+    read back, an unknown name is an error, and restoring leaves the default."""
+    lib = dtc._native.lib
+    for name, default in _OPTION_DEFAULTS.items():
+        key = name.encode()
+        assert lib.dtc_get_option(key) == default, name
+        assert lib.dtc_set_option(key, default + 1) == 0
+        assert lib.dtc_get_option(key) == default + 1
+        assert lib.dtc_set_option(key, default) == 0
+        assert lib.dtc_get_option(key) == default
+    assert lib.dtc_set_option(b"no_such_option", 1) != 0
