@@ -51,6 +51,7 @@ PConv = C.POINTER(ConvDesc)
 _SIGS = {
     "dtc_abi_version": (i32, []),
     "dtc_last_error": (cstr, []),
+    "dtc_install_crash_handler": (i32, []),
     "dtc_set_option": (i32, [cstr, i32]),
     "dtc_get_option": (i32, [cstr]),
     "dtc_conv2d_workspace_size": (sz, [PConv, i32]),

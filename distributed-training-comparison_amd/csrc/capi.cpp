@@ -11,13 +11,19 @@
 #include <atomic>
 #include <cstring>
 #include <cstdlib>
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <pthread.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {0}, {1}, {1}, {0}, {1}, {16384}, {256}, {1024}, {1}, {1}, {1}, {1}, {0}, {1}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {0}, {1}, {1}, {0}, {1}, {16384}, {256}, {1024}, {1}, {1}, {1}, {1}, {0}, {1}, {1}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
                                              "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
                                              "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse",
-                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct", "wgrad_defer", "igemm_tile", "igemm_split", "bn_onepass", "sc_stream", "dgrad_class_order", "head_fused", "stem_prologue", "sc_compact", "wgrad_tail", "stem_bn_fuse", "bn_red_elems", "bn_red_blocks", "bn_fa_blocks", "fork_lazy", "side_prio", "sc_fuse", "head_direct", "stem_recompute", "stem_wlds"};
+                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct", "wgrad_defer", "igemm_tile", "igemm_split", "bn_onepass", "sc_stream", "dgrad_class_order", "head_fused", "stem_prologue", "sc_compact", "wgrad_tail", "stem_bn_fuse", "bn_red_elems", "bn_red_blocks", "bn_fa_blocks", "fork_lazy", "side_prio", "sc_fuse", "head_direct", "stem_recompute", "stem_wlds", "graph_retire"};
 static std::atomic<int> g_epoch{0};
 // DTC_OPTIONS="name=value,name=value" in the environment overrides defaults at library load (A/B and
 // bisection runs of whole test suites without code changes)
@@ -69,6 +75,66 @@ const char* last_error() { return g_err.c_str(); }
 
 using namespace dtc;
 
+// ------------------------------------------------------------------ native crash report (diagnostics)
+// dtc_install_crash_handler(): on SIGSEGV / SIGBUS / SIGFPE / SIGABRT print the faulting THREAD (tid,
+// name) and its native frames (library + nearest exported symbol + offset) to stderr, then hand the
+// signal to the previous handler (Python's faulthandler prints the Python threads). faulthandler alone
+// cannot say in which native thread -- ours or a runtime worker -- a fault happened.
+static struct sigaction g_prev_sa[32];
+static void put(const char* s) { (void)!write(2, s, strlen(s)); }
+static void put_hex(uintptr_t v) {
+  char b[19] = "0x";
+  for (int i = 0; i < 16; ++i) b[2 + i] = "0123456789abcdef"[(v >> (60 - 4 * i)) & 15];
+  b[18] = 0;
+  put(b);
+}
+static void crash_report(int sig, siginfo_t* si, void* uc) {
+  char name[32] = {0};
+  (void)pthread_getname_np(pthread_self(), name, sizeof(name));
+  put("\n=== dtc crash report: signal ");
+  put(sig == SIGSEGV ? "SIGSEGV" : sig == SIGBUS ? "SIGBUS" : sig == SIGFPE ? "SIGFPE" : "SIGABRT");
+  put(" addr ");
+  put_hex((uintptr_t)(si ? si->si_addr : nullptr));
+  put(" tid ");
+  put_hex((uintptr_t)syscall(SYS_gettid));
+  put(" pid ");
+  put_hex((uintptr_t)getpid());
+  put(" thread '");
+  put(name);
+  put("'\n");
+  void* fr[48];
+  const int nf = backtrace(fr, 48);
+  for (int i = 0; i < nf; ++i) {
+    Dl_info d;
+    put("  #");
+    put_hex((uintptr_t)i);
+    put(" ");
+    if (dladdr(fr[i], &d) && d.dli_fname) {
+      put(d.dli_fname);
+      put(" +");
+      put_hex((uintptr_t)fr[i] - (uintptr_t)d.dli_fbase);
+      if (d.dli_sname) {
+        put(" ");
+        put(d.dli_sname);
+        put(" +");
+        put_hex((uintptr_t)fr[i] - (uintptr_t)d.dli_saddr);
+      }
+    } else {
+      put_hex((uintptr_t)fr[i]);
+    }
+    put("\n");
+  }
+  put("=== end dtc crash report\n");
+  struct sigaction& p = g_prev_sa[sig];
+  if ((p.sa_flags & SA_SIGINFO) && p.sa_sigaction) {
+    p.sa_sigaction(sig, si, uc);
+  } else if (p.sa_handler != SIG_IGN && p.sa_handler != SIG_DFL && p.sa_handler) {
+    p.sa_handler(sig);
+  }
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 static inline ConvShape shape_of(const dtc_conv_desc* d) {
   return ConvShape{d->n, d->h, d->w, d->c, d->k, d->r, d->s, d->stride, d->pad};
@@ -91,6 +157,28 @@ int dtc_get_option(const char* name) {
   return set_error(DTC_EINVAL, "unknown option %s", name ? name : "(null)");
 }
 const char* dtc_last_error(void) { return last_error(); }
+
+int dtc_install_crash_handler(void) {
+  static std::atomic<int> once{0};
+  if (once.exchange(1)) return 0;
+  void* warm[2];
+  (void)backtrace(warm, 2);  // loads the unwinder now, not inside the handler
+  static char altstack[1 << 16];
+  stack_t ss;
+  ss.ss_sp = altstack;
+  ss.ss_size = sizeof(altstack);
+  ss.ss_flags = 0;
+  (void)sigaltstack(&ss, nullptr);
+  for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGABRT}) {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = crash_report;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    if (sigaction(sig, &sa, &g_prev_sa[sig]) != 0) return set_error(DTC_EINVAL, "sigaction failed");
+  }
+  return 0;
+}
 
 size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass) {
   if (!d || pass < 0 || pass > 2) return 0;

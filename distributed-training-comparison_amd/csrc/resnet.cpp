@@ -445,7 +445,7 @@ static void drop_graphs(Net& n, bool final_ = false) {
   for (auto& sg : n.bwd_segs)
     if (sg.exec) n.retired.push_back(sg.exec);
   n.bwd_segs.clear();
-  if (final_) {
+  if (final_ || option_get(OPT_GRAPH_RETIRE) == 0) {
     for (auto e : n.retired) (void)hipGraphExecDestroy(e);
     n.retired.clear();
   }

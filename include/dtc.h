@@ -34,6 +34,9 @@ extern "C" {
 /* ------------------------------------------------------------------ library */
 int dtc_abi_version(void);
 const char* dtc_last_error(void);
+/* Diagnostics: on SIGSEGV/SIGBUS/SIGFPE/SIGABRT print the faulting native thread (tid, name) and its
+ * frames to stderr, then chain to the previous handler (e.g. Python's faulthandler). Idempotent. */
+int dtc_install_crash_handler(void);
 /* Process-wide kernel tuning knobs (atomic; for benchmarking): "igemm_stages" (2 or 3 LDS stages
  * in the conv main loop, default 2), "xcd_remap" (XCD-aware tile order, default 1),
  * "dgrad_classes" (stride-2 data-gradient as 4 parity-class GEMMs, default 1), "wgrad_fast" (buffer-

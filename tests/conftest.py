@@ -24,6 +24,8 @@ def cuda(dtc):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    # a native fault prints the faulting thread and its frames (then Python's faulthandler runs)
+    dtc._native.lib.dtc_install_crash_handler()
     return torch.device("cuda:0")
 
 
