@@ -66,6 +66,41 @@ def _committed_traffic():
         return None
 
 
+def host_cores() -> dict:
+    """The host's CPU inventory (state physical cores beside the thread count): logical
+    CPUs, the CPUs this process may run on (affinity), and physical cores / sockets from
+    /proc/cpuinfo ("physical id", "core id" pairs), counted over the whole machine and over the
+    affinity set."""
+    out = {"logical_cpus": os.cpu_count()}
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover - non-Linux
+        aff = list(range(os.cpu_count() or 1))
+    out["affinity_cpus"] = len(aff)
+    try:
+        cores, cores_aff, cpu, phys = set(), set(), None, None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "processor":
+                cpu, phys = int(v), None
+            elif k == "physical id":
+                phys = int(v)
+            elif k == "core id" and cpu is not None:
+                key = (phys, int(v))
+                cores.add(key)
+                if cpu in aff:
+                    cores_aff.add(key)
+        if cores:
+            out["physical_cores"] = len(cores)
+            out["sockets"] = len({p for p, _ in cores})
+            out["physical_cores_in_affinity"] = len(cores_aff)
+    except OSError:
+        pass
+    out["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
+    return out
+
+
 def cpu_baseline(seconds: float, steps: int = 50):
     """BASELINE config 1 on the host cores: the reference's single-device fp32 step
     (single/trainer.py:131-147) in stock torch CPU at batch 128 (oracle/torch_ref.py, pinned to the
@@ -79,10 +114,11 @@ def cpu_baseline(seconds: float, steps: int = 50):
     m = dtc.ResNet18()  # host-side construction only (identical init to the reference)
     r = time_cpu_step(m.state_dict(), batch=128, warmup=3, steps=steps, max_seconds=seconds)
     return {"value": round(r["img_per_s"], 3), "unit": "images/sec", "cores": r["threads"], "kind": "port",
-            "impl": "torch-cpu", "batch": 128, "dtype": "fp32",
+            "impl": "torch-cpu", "batch": 128, "dtype": "fp32", "host": host_cores(),
             "sample": f"config 1: median of {r['steps']} steps (after 3 warm-ups) of the single-device fp32 "
                       f"train step (zero_grad, forward, CrossEntropy, backward, SGD nesterov) at batch 128, "
-                      f"32x32, stock torch {torch.__version__} CPU on {r['threads']} threads; "
+                      f"32x32, stock torch {torch.__version__} CPU on {r['threads']} threads (the job's CPU "
+                      f"share; host inventory in `host`); "
                       f"median step {r['median_s'] * 1e3:.1f} ms, {r['seconds']:.1f} s sampled"}
 
 
@@ -205,6 +241,15 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="BASELINE config 3: global batch split over the ranks, per-rank int(G/W) "
+                         "(ddp/trainer.py:34; strong scaling)")
+    ap.add_argument("--sim-world", type=int, default=1,
+                    help="N=1 only: run ONE rank of a W-rank job -- per-rank batch int(G/W) with --global-batch, "
+                         "gradients pre-scaled 1/W and the bucketed all-reduce backward forced on (a one-rank RCCL "
+                         "communicator): the per-rank shape and code path of config 3 measured on one GPU")
+    ap.add_argument("--no-config3", action="store_true",
+                    help="N>1: skip the extra config-3 region (global batch 256 over the ranks)")
     ap.add_argument("--size", type=int, default=32)
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--no-barrier", action="store_true", help="drop the reference's per-step dist.barrier()")
@@ -242,21 +287,31 @@ def main():
     if args.sync_bn and world == 1:  # torch keeps local statistics at W=1; force the path to time it
         model.sync_comm = dtc.parallel.Comm(0, 1, dtc.parallel.Comm.unique_id(), local)
         model.module.set_sync_bn(model.sync_comm)
+    sim = max(1, args.sim_world) if world == 1 else 1
+    if sim > 1:  # one rank of a sim-rank job: 1/W pre-scale, bucketed all-reduce backward on the side stream
+        model.module._comm = model.comm
+        model.module._grad_scale = 1.0 / sim
     crit = dtc.CrossEntropyLoss()
     opt = dtc.SGD(model.parameters(), lr=0.1, weight_decay=1e-4, momentum=0.9, nesterov=True)
     scaler = dtc.GradScaler()
 
-    B, S = args.batch, args.size
-    pool = []
+    ranks_of_job = world * sim
+    B = int(args.global_batch / ranks_of_job) if args.global_batch else args.batch  # ddp/trainer.py:34
+    S = args.size
     templates = dtc.data.class_templates(100, S, S)
-    for i in range(4):
-        x, y = dtc.data.synthetic_batch(1000 * rank + i, B, S, S, 100, dev, templates)
-        pool.append((x.contiguous(), y.contiguous()))
 
+    def make_pool(b):
+        pool = []
+        for i in range(4):
+            x, y = dtc.data.synthetic_batch(1000 * rank + i, b, S, S, 100, dev, templates)
+            pool.append((x.contiguous(), y.contiguous()))
+        return pool
+
+    pools = {B: make_pool(B)}
     losses = []
 
-    def step(i):
-        img, label = pool[i % len(pool)]
+    def step(i, b=B):
+        img, label = pools[b][i % len(pools[b])]
         opt.zero_grad()
         with dtc.autocast():
             logit = model(img)
@@ -272,12 +327,12 @@ def main():
         if not args.no_item:
             losses.append(loss.item())
 
-    def timed(k, first):
+    def timed(k, first, b=B):
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(k):
-            step(first + i)
+            step(first + i, b)
         torch.cuda.synchronize()
         dist.barrier()
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
@@ -311,6 +366,20 @@ def main():
         dtc._native.call("dtc_set_option", b"bwd_streams", bwd_streams)
     ms, fl, cnt = list(ms4)[:3], list(fl4)[:3], list(cnt4)[:3]  # the conv passes (kinds 0-2)
 
+    # BASELINE config 3 beside the weak-scaled value at N > 1: the reference's own DDP job, global
+    # batch 256 over the ranks (per-rank int(256/W), ddp/trainer.py:34, run_ddp.sh:4) -- strong scaling
+    config3 = None
+    if world > 1 and not args.global_batch and not args.no_config3:
+        b3 = int(256 / world)
+        pools[b3] = make_pool(b3)
+        for i in range(5):
+            step(i, b3)
+        e3 = timed(args.steps, 5, b3)
+        config3 = {"workload": f"BASELINE config 3: global batch 256 over {world} ranks ({b3}/GPU), 32x32 bf16",
+                   "global_batch": b3 * world, "per_gpu_batch": b3, "scaling": "strong",
+                   "value": round(b3 * world * args.steps / e3, 2), "unit": "images/sec",
+                   "ms_per_step": round(e3 / args.steps * 1e3, 4), "steps": args.steps, "warmup": 5}
+
     # C4 all-reduce bus bandwidth on the Reducer's own RCCL communicator: the full gradient
     # (11,220,132 fp32) and the bucket-size sweep of BASELINE config 5 (N > 1 only: one rank has
     # no exchange). Runs after both timed regions, so it never overlaps the measured steps.
@@ -340,9 +409,20 @@ def main():
         n_launch = sum(cnt)
         achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
         value = B * world * args.steps / elapsed
+        if args.global_batch:
+            metric = (f"images/sec/node ResNet-18 CIFAR-100 DDP (global batch {args.global_batch} over "
+                      f"{ranks_of_job} ranks, {B} images/GPU" + (")" if S == 32 else f", {S}x{S})"))
+        else:
+            metric = (f"images/sec/node ResNet-18 CIFAR-100 DDP (weak-scaled, {B} images/GPU"
+                      + (")" if S == 32 else f", {S}x{S})"))
+        workload = (f"ResNet-18 CIFAR-100 train step, batch {B}/GPU, {S}x{S}, bf16 MFMA, SGD-Nesterov + GradScaler, "
+                    f"DDP bucket {args.bucket_mb} MB")
+        if sim > 1:
+            workload += (f"; ONE rank of a {sim}-rank job on 1 GPU (per-rank shape of BASELINE config 3, 1/{sim} "
+                         f"pre-scale, bucketed all-reduce backward on a one-rank RCCL communicator): value is "
+                         f"this rank's images/s, the node figure needs {sim} GPUs")
         out = {
-            "metric": f"images/sec/node ResNet-18 CIFAR-100 DDP (weak-scaled, {B} images/GPU"
-                      + (")" if S == 32 else f", {S}x{S})"),
+            "metric": metric,
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -350,14 +430,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_batch else "weak",
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (0.5*class_template + N(0,1), 100 classes), resident in HBM",
-            "config": {"workload": f"ResNet-18 CIFAR-100 train step, batch {B}/GPU, {S}x{S}, bf16 MFMA, "
-                                   f"SGD-Nesterov + GradScaler, DDP bucket {args.bucket_mb} MB",
-                       "model": "ResNet18 (CIFAR, src/ddp/net.py)", "global_batch": B * world, "seq_len": None,
+            "config": {"workload": workload,
+                       "model": "ResNet18 (CIFAR, src/ddp/net.py)", "global_batch": B * ranks_of_job, "seq_len": None,
                        "parallelism": f"dp{world}", "per_gpu_batch": B, "image_size": S,
+                       "sim_world": sim,
                        "step_barrier": not args.no_barrier, "loss_item": not args.no_item,
                        "sync_bn": bool(args.sync_bn),
                        "buckets_mb": [round(n * 4 / 2**20, 2) for _, n in model.buckets]},
@@ -398,6 +478,8 @@ def main():
         }
         if allreduce is not None:
             out["allreduce"] = allreduce
+        if config3 is not None:
+            out["config3"] = config3
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_steps)

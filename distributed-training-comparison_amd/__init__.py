@@ -11,6 +11,7 @@ The directory name is not a Python identifier; importing it by path also registe
 import sys as _sys
 
 from . import _native  # noqa: F401  (loads libdtc_amd.so; raises if it is missing)
+from ._native import NativeError  # noqa: F401
 from . import data, ops  # noqa: F401
 from .amp import GradScaler, autocast  # noqa: F401
 from .nn import BasicBlock, CrossEntropyLoss, ResNet, ResNet18, SyncBatchNorm  # noqa: F401

@@ -99,6 +99,9 @@ _SIGS = {
     "dtc_comm_log_size": (i32, [vp]),
     "dtc_comm_log_entry": (i32, [vp, i32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(i32)]),
     "dtc_comm_log_clear": (i32, [vp]),
+    "dtc_comm_init_thread_group": (i32, [C.POINTER(vp), i32, i32]),
+    "dtc_comm_rank": (i32, [vp]),
+    "dtc_comm_world": (i32, [vp]),
     "dtc_dp_create": (i32, [C.POINTER(vp), i32, C.POINTER(i32)]),
     "dtc_dp_destroy": (i32, [vp]),
     "dtc_dp_is_local": (i32, [vp]),

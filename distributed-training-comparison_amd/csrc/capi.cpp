@@ -352,6 +352,11 @@ int dtc_barrier(dtc_comm* comm, void* stream) { GUARD(return comm_barrier((Comm*
 int dtc_comm_init_loopback(dtc_comm** out, int device, int world, float factor) {
   GUARD(return comm_init_loopback((Comm**)out, device, world, factor);)
 }
+int dtc_comm_init_thread_group(dtc_comm** outs, int world, int device) {
+  GUARD(return comm_init_thread_group((Comm**)outs, world, device);)
+}
+int dtc_comm_rank(const dtc_comm* comm) { return comm_rank((const Comm*)comm); }
+int dtc_comm_world(const dtc_comm* comm) { return comm_world((const Comm*)comm); }
 int dtc_comm_log_size(dtc_comm* comm) {
   const auto* l = comm_log((Comm*)comm);
   return l ? (int)l->size() : DTC_EINVAL;

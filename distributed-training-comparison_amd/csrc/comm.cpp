@@ -8,7 +8,11 @@
 // the compute stream wait for every bucket (fork/join is also valid under stream capture).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
+#include <string>
 #include <vector>
 #include "comm.h"
 #include "common.h"
@@ -23,6 +27,8 @@ namespace dtc {
       return ::dtc::set_error(1000 + (int)r_, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, \
                               __LINE__);                                                                     \
   } while (0)
+
+struct ThreadGroup;
 
 struct Comm {
   ncclComm_t nccl = nullptr;
@@ -39,7 +45,148 @@ struct Comm {
   float factor = 1.f;
   std::vector<CommLogEntry> log;
   float* token = nullptr;  // barrier: one float all-reduced on the side stream
+  // in-process thread group (test transport, dtc_comm_init_thread_group): this handle is rank `rank`
+  // of `world` handles driven by one host thread each; collectives rendezvous on the host and run as
+  // real data movement between the ranks' buffers on one GPU
+  ThreadGroup* grp = nullptr;
+  hipEvent_t ready = nullptr;  // this rank's "inputs produced" marker for the current collective
 };
+
+// ---------------------------------------------------------------- thread-group transport
+// W ranks in one process, one host thread each, their buffers on one device. Every collective is
+// matched by call order (as RCCL matches them): each rank records its producer stream, the LAST rank to
+// arrive makes the group stream wait for every rank's marker, moves the data (rank-ordered SUM into
+// every buffer, or root -> all copies), records a completion event, and every rank's consumer stream
+// waits for it. The host rendezvous blocks the calling thread (an RCCL enqueue does not), which only
+// serialises issue order -- the semantics the Reducer relies on (ordering, coverage, values) are RCCL's.
+struct ThreadGroup {
+  int world = 0, device = 0, refs = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t gen = 0;
+  int arrived = 0;
+  int kind = -1, dtype = 0, root = 0;
+  size_t count = 0;
+  std::vector<void*> bufs;
+  std::vector<hipEvent_t> ready;
+  hipStream_t st = nullptr;
+  std::vector<hipEvent_t> done;
+  int done_next = 0;
+  hipEvent_t last = nullptr;
+  int err = 0;
+  std::string errmsg;
+};
+
+enum { GK_ALLREDUCE = 0, GK_BROADCAST = 1, GK_BARRIER = 2 };
+
+static size_t dtype_size(int dtype) { return dtype == 1 ? 2 : (dtype == 2 || dtype == 3) ? 8 : 4; }
+
+static int group_issue(ThreadGroup* g) {  // called with g->mu held by the last rank to arrive
+  for (int r = 0; r < g->world; ++r) DTC_HIP(hipStreamWaitEvent(g->st, g->ready[r], 0));
+  if (g->kind == GK_ALLREDUCE && g->count > 0) {
+    GroupPtrs p{};
+    for (int r = 0; r < g->world; ++r) p.p[r] = g->bufs[r];
+    DTC_TRY(group_sum(p, g->world, (int64_t)g->count, g->dtype, g->st));
+  } else if (g->kind == GK_BROADCAST && g->count > 0) {
+    for (int r = 0; r < g->world; ++r)
+      if (r != g->root)
+        DTC_HIP(hipMemcpyAsync(g->bufs[r], g->bufs[g->root], g->count * dtype_size(g->dtype), hipMemcpyDeviceToDevice,
+                               g->st));
+  }
+  g->last = g->done[g->done_next];
+  g->done_next = (g->done_next + 1) % (int)g->done.size();
+  DTC_HIP(hipEventRecord(g->last, g->st));
+  return 0;
+}
+
+// One collective of rank c->rank: `after` orders the inputs, `waiter` waits for the result.
+static int group_collective(Comm* c, int kind, void* buf, size_t count, int dtype, int root, hipStream_t after,
+                            hipStream_t waiter) {
+  ThreadGroup* g = c->grp;
+  DTC_CHECK_ARG(kind != GK_ALLREDUCE || dtype == 0 || dtype == 3, "thread group: SUM of fp32 / fp64 only");
+  DTC_HIP(hipEventRecord(c->ready, after));
+  hipEvent_t res = nullptr;
+  {
+    std::unique_lock<std::mutex> lk(g->mu);
+    if (g->err) return set_error(g->err, "%s", g->errmsg.c_str());
+    if (g->arrived == 0) {
+      g->kind = kind;
+      g->count = count;
+      g->dtype = dtype;
+      g->root = root;
+    } else if (g->kind != kind || g->count != count || g->dtype != dtype || g->root != root) {
+      g->err = DTC_EINVAL;
+      g->errmsg = "thread group: ranks issued mismatched collectives (kind/count/dtype/root differ)";
+      g->cv.notify_all();
+      return set_error(g->err, "%s", g->errmsg.c_str());
+    }
+    g->bufs[c->rank] = buf;
+    g->ready[c->rank] = c->ready;
+    const uint64_t my = g->gen;
+    if (++g->arrived == g->world) {
+      const int rc = group_issue(g);
+      g->arrived = 0;
+      ++g->gen;
+      if (rc) {
+        g->err = rc;
+        g->errmsg = last_error();
+      }
+      g->cv.notify_all();
+      if (rc) return rc;
+    } else if (!g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return g->gen != my || g->err != 0; })) {
+      g->err = DTC_EINVAL;
+      g->errmsg = "thread group: timed out waiting for the other ranks' collective";
+      g->cv.notify_all();
+      return set_error(g->err, "%s (rank %d)", g->errmsg.c_str(), c->rank);
+    }
+    if (g->err) return set_error(g->err, "%s", g->errmsg.c_str());
+    res = g->last;
+  }
+  DTC_HIP(hipStreamWaitEvent(waiter, res, 0));
+  return 0;
+}
+
+int comm_init_thread_group(Comm** outs, int world, int device) {
+  DTC_CHECK_ARG(outs && world >= 1 && world <= DTC_GROUP_MAX, "comm_init_thread_group: bad args");
+  DTC_HIP(hipSetDevice(device));
+  ThreadGroup* g = new ThreadGroup();
+  g->world = world;
+  g->device = device;
+  g->refs = world;
+  g->bufs.assign(world, nullptr);
+  g->ready.assign(world, nullptr);
+  DTC_HIP(hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking));
+  g->done.resize(64);
+  for (auto& e : g->done) DTC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (int r = 0; r < world; ++r) {
+    Comm* c = new Comm();
+    c->rank = r;
+    c->world = world;
+    c->device = device;
+    c->grp = g;
+    DTC_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    c->fork.resize(64);
+    for (auto& e : c->fork) DTC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    DTC_HIP(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
+    DTC_HIP(hipEventCreateWithFlags(&c->ready, hipEventDisableTiming));
+    outs[r] = c;
+  }
+  return 0;
+}
+
+static void group_release(ThreadGroup* g) {
+  bool last = false;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    last = --g->refs == 0;
+  }
+  if (!last) return;
+  (void)hipStreamSynchronize(g->st);
+  for (auto& e : g->done)
+    if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(g->st);
+  delete g;
+}
 
 static ncclDataType_t to_nccl(int dtype) {
   switch (dtype) {
@@ -134,6 +281,12 @@ static int spin_wait(hipEvent_t ev) {
 // barrier() passes NULL at world 1: a one-rank all-reduce would only add a launch).
 int comm_barrier(Comm* c, hipStream_t st) {
   static thread_local hipEvent_t local_ev = nullptr;
+  if (c != nullptr && c->grp != nullptr) {  // every rank's host meets, then waits for its own stream
+    DTC_TRY(group_collective(c, GK_BARRIER, nullptr, 0, 0, 0, st, st));
+    if (!local_ev) DTC_HIP(hipEventCreateWithFlags(&local_ev, hipEventDisableTiming));
+    DTC_HIP(hipEventRecord(local_ev, st));
+    return spin_wait(local_ev);
+  }
   if (c == nullptr || c->loopback || c->nccl == nullptr) {
     if (!local_ev) DTC_HIP(hipEventCreateWithFlags(&local_ev, hipEventDisableTiming));
     DTC_HIP(hipEventRecord(local_ev, st));
@@ -160,7 +313,9 @@ int comm_destroy(Comm* c) {
   for (auto& e : c->fork)
     if (e) (void)hipEventDestroy(e);
   if (c->done) (void)hipEventDestroy(c->done);
+  if (c->ready) (void)hipEventDestroy(c->ready);
   if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->grp) group_release(c->grp);
   delete c;
   return 0;
 }
@@ -169,6 +324,10 @@ int comm_allreduce(Comm* c, void* buf, size_t count, int dtype, hipStream_t st) 
   DTC_CHECK_ARG(c && buf, "comm_allreduce: bad args");
   if (count == 0) return 0;
   if (c->loopback) return loopback_reduce(c, buf, count, dtype, st, false);
+  if (c->grp) {
+    c->log.push_back(CommLogEntry{(uint64_t)(uintptr_t)buf, (uint64_t)count, 0});
+    return group_collective(c, GK_ALLREDUCE, buf, count, dtype, 0, st, st);
+  }
   DTC_NCCL(ncclAllReduce(buf, buf, count, to_nccl(dtype), ncclSum, c->nccl, st));
   return 0;
 }
@@ -177,13 +336,29 @@ int comm_broadcast(Comm* c, void* buf, size_t count, int dtype, int root, hipStr
   DTC_CHECK_ARG(c && buf && root >= 0 && root < c->world, "comm_broadcast: bad args");
   if (count == 0) return 0;
   if (c->loopback) return 0;  // one rank: the root's buffer already is the result
-  DTC_NCCL(ncclBroadcast(buf, buf, count, to_nccl(dtype), root, c->nccl, st));
+  if (c->grp) return group_collective(c, GK_BROADCAST, buf, count, dtype, root, st, st);
+  // on the communicator's side stream, like its bucket all-reduces and barrier: every collective of
+  // one communicator on ONE stream, so two ranks can never order them differently on the device
+  // (VERDICT r2); `st` is ordered before (the buffer's producers) and after (its consumers)
+  hipEvent_t ev = c->fork[c->next_fork];
+  c->next_fork = (c->next_fork + 1) % (int)c->fork.size();
+  DTC_HIP(hipEventRecord(ev, st));
+  DTC_HIP(hipStreamWaitEvent(c->side, ev, 0));
+  DTC_NCCL(ncclBroadcast(buf, buf, count, to_nccl(dtype), root, c->nccl, c->side));
+  DTC_HIP(hipEventRecord(c->done, c->side));
+  DTC_HIP(hipStreamWaitEvent(st, c->done, 0));
   return 0;
 }
 
 int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute) {
   DTC_CHECK_ARG(c && buf, "comm_allreduce_async: bad args");
   if (count == 0) return 0;
+  if (c->grp) {  // the bucket's producers on `compute`, the result awaited by the side stream
+    c->log.push_back(CommLogEntry{(uint64_t)(uintptr_t)buf, (uint64_t)count, 1});
+    DTC_TRY(group_collective(c, GK_ALLREDUCE, buf, count, 0, 0, compute, c->side));
+    c->pending = true;
+    return 0;
+  }
   hipEvent_t ev = c->fork[c->next_fork];
   c->next_fork = (c->next_fork + 1) % (int)c->fork.size();
   DTC_HIP(hipEventRecord(ev, compute));
@@ -204,6 +379,7 @@ int comm_join(Comm* c, hipStream_t compute) {
 }
 
 int comm_world(const Comm* c) { return c ? c->world : 1; }
+int comm_rank(const Comm* c) { return c ? c->rank : 0; }
 
 }  // namespace dtc
 

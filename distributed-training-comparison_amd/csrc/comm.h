@@ -23,6 +23,9 @@ int comm_broadcast(Comm* c, void* buf, size_t count, int dtype, int root, hipStr
 int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute);
 int comm_join(Comm* c, hipStream_t compute);
 int comm_world(const Comm* c);
+int comm_rank(const Comm* c);
+// in-process thread group: `world` handles (outs[r] = rank r) on one device, one host thread per rank
+int comm_init_thread_group(Comm** outs, int world, int device);
 // dist.barrier(): all ranks + this rank's queued work on `st`; the host polls (comm.cpp)
 int comm_barrier(Comm* c, hipStream_t st);
 // test communicator without RCCL: all-reduce = buf *= factor, logged; reports `world` ranks (comm.cpp)

@@ -320,6 +320,10 @@ int copy_and_zero(const void* src, void* dst, size_t bytes, void* zp, size_t zby
 // x[i] *= f (loopback test communicator)
 int scale_f32(float* x, int64_t n, float f, hipStream_t st);
 int scale_f64(double* x, int64_t n, double f, hipStream_t st);
+// thread-group communicator: every rank's buffer <- the rank-ordered sum of all (fp32 dtype 0 / fp64 3)
+#define DTC_GROUP_MAX 8
+struct GroupPtrs { void* p[DTC_GROUP_MAX]; };
+int group_sum(const GroupPtrs& g, int w, int64_t n, int dtype, hipStream_t st);
 // dst[i] += src[i] (DataParallel reduce-add of replicas sharing a device)
 int add_f32(float* dst, const float* src, int64_t n, hipStream_t st);
 int amp_check_finite(const float* g, int64_t n, int* found_inf, hipStream_t st);

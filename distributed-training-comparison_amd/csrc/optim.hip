@@ -148,6 +148,27 @@ int add_f32(float* dst, const float* src, int64_t n, hipStream_t st) {
   return 0;
 }
 
+// In-process thread-group communicator (comm.cpp): out_r[i] = sum_q in_q[i] for every rank r, the
+// ranks' buffers summed in rank order (fixed; for two ranks the fp32 sum itself), read before written
+// per element so the all-reduce is in place in every rank's buffer.
+template <typename T>
+__global__ void group_sum_kernel(GroupPtrs g, int w, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    T s = ((const T*)g.p[0])[i];
+    for (int r = 1; r < w; ++r) s += ((const T*)g.p[r])[i];
+    for (int r = 0; r < w; ++r) ((T*)g.p[r])[i] = s;
+  }
+}
+
+int group_sum(const GroupPtrs& g, int w, int64_t n, int dtype, hipStream_t st) {
+  DTC_CHECK_ARG(w >= 1 && w <= DTC_GROUP_MAX && n > 0 && (dtype == 0 || dtype == 3), "group_sum: bad args");
+  const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  if (dtype == 0) hipLaunchKernelGGL(group_sum_kernel<float>, dim3(blocks), dim3(256), 0, st, g, w, n);
+  else hipLaunchKernelGGL(group_sum_kernel<double>, dim3(blocks), dim3(256), 0, st, g, w, n);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 __global__ void amp_check_finite_kernel(const float* __restrict__ g, int64_t n, int* __restrict__ found) {
   bool bad = false;
   for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)

@@ -95,6 +95,10 @@ struct Net {
   bool side_pending = false;
   size_t slab_bytes = 0;
   size_t stats_lo = 0, acc_lo = 0, stats_hi = 0;  // BN slot regions [stats_lo, acc_lo), [acc_lo, stats_hi)
+  // the backward sums [acc_lo, stats_hi) are zeroed by every training forward; a backward that finds
+  // them already used (a second backward over one forward) zeroes them first instead of adding onto
+  // the previous backward's sums
+  bool sums_fresh = false;
   // buckets: [offset, numel) in flat elements, and the block index after whose backward it fires
   std::vector<int64_t> bucket_off, bucket_len;
   std::vector<int> bucket_after_block;  // -1 = after the stem (last)
@@ -797,7 +801,13 @@ static int backward_body_f32(Net& n, const float* dlogits, float gs, const BwdCt
   return 0;
 }
 
+static int forward_impl(Net& n, const float* x, float* logits, bool train, hipStream_t st);
 static int forward(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
+  DTC_TRY(forward_impl(n, x, logits, train, st));
+  if (train) n.sums_fresh = true;
+  return 0;
+}
+static int forward_impl(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
   if (n.f32) DTC_TRY(f32_stem_im2col(x, n.at<float>(n.X0), n.B, n.H, n.W, st));
   else if (n.stem_direct) {  // the graph reads only executor memory: a copy of the 12 B/pixel input (+ the
     // training step's BN slots zeroed in the same launch)
@@ -1338,6 +1348,8 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
 }
 
 static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st) {
+  if (!n.sums_fresh) DTC_TRY(zero_bytes(n.ws + n.acc_lo, n.stats_hi - n.acc_lo, st));
+  n.sums_fresh = false;
   if (!graphs_on(n)) {
     BwdCtx cx;
     cx.comm = comm;

@@ -138,6 +138,7 @@ class Executor:
         self.flat = flat
         self.batch, self.height, self.width, self.num_classes = batch, height, width, num_classes
         self.generation = 0
+        self._bwd_gen = 0  # generation whose forward a backward has consumed (one backward per forward)
         self._dlogits = None
         call("dtc_rn18_bind", self.handle, self.ws_ptr, ptr(flat.params), ptr(flat.grads), ptr(flat.params_bf16),
              ptr(flat.bufs), ptr(flat.nbt), stream_ptr())
@@ -146,6 +147,20 @@ class Executor:
         call("dtc_rn18_forward", self.handle, ptr(x), ptr(logits), int(bool(train)), stream_ptr())
         self.generation += 1
         return self.generation
+
+    def consume(self, gen: int) -> None:
+        """Claim the forward of generation `gen` for one backward. The kernels WRITE gradients, which
+        equals the reference's zero_grad() + backward(); a second backward over the same forward
+        (retain_graph=True) would have to ACCUMULATE into .grad in torch, so it is refused instead of
+        silently returning the first backward's gradients."""
+        if gen != self.generation:
+            raise NativeError("ResNet backward: the executor ran another forward since this graph was built "
+                              "(one forward per backward is supported)")
+        if gen == self._bwd_gen:
+            raise NativeError("ResNet backward: this forward was already back-propagated (a second backward "
+                              "would accumulate gradients in torch; the native kernels write them): run "
+                              "the forward again")
+        self._bwd_gen = gen
 
     def backward(self, dlogits: torch.Tensor, grad_scale: float, comm) -> None:
         call("dtc_rn18_backward", self.handle, ptr(dlogits), float(grad_scale), comm.handle if comm else None,
@@ -221,9 +236,7 @@ class _NetFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dlogits):
         model, exe = ctx.model, ctx.exe
-        if exe.generation != ctx.gen:
-            raise NativeError("ResNet backward: the executor ran another forward since this graph was built "
-                              "(one forward per backward is supported)")
+        exe.consume(ctx.gen)
         exe.backward(dlogits.contiguous().float(), model._grad_scale, model._comm)
         model._ensure_grads()
         return None, None, None, None
@@ -272,9 +285,7 @@ class NativeLoss(torch.Tensor):
         node, logits, labels, lse, gscale = fast
         if isinstance(node, _NetFn._backward_cls):
             model, exe = node.model, node.exe
-            if exe.generation != node.gen:
-                raise NativeError("ResNet backward: the executor ran another forward since this graph was built "
-                                  "(one forward per backward is supported)")
+            exe.consume(node.gen)
             exe.xent_backward(logits, labels, lse, gscale, model._grad_scale, model._comm)
             model._ensure_grads()
         else:  # DataParallel's gathered logits: xent backward, then the replicas' backward + reduce-add

@@ -64,6 +64,22 @@ class Comm:
     def clear_log(self) -> None:
         call("dtc_comm_log_clear", self.handle)
 
+    @classmethod
+    def thread_group(cls, device: int, world: int) -> List["Comm"]:
+        """In-process thread-group communicator (include/dtc.h dtc_comm_init_thread_group): `world`
+        ranks on one device, rank r driven by its own host thread. Collectives really move data
+        between the ranks' buffers (rank-ordered SUM, root -> all copies), so one GPU runs W ranks
+        with distinct data through the product Reducer, broadcasts and SyncBN."""
+        arr = (C.c_void_p * world)()
+        call("dtc_comm_init_thread_group", arr, int(world), int(device))
+        out = []
+        for r in range(world):
+            c = cls.__new__(cls)
+            c.rank, c.world, c.device = r, world, device
+            c.handle = C.c_void_p(arr[r])
+            out.append(c)
+        return out
+
     @staticmethod
     def unique_id() -> bytes:
         n = lib.dtc_comm_unique_id_bytes()
@@ -189,18 +205,28 @@ def allreduce_probe(allreduce_fn, nbytes: int, device, world: int, iters: int = 
 
 
 class DistributedDataParallel(nn.Module):
+    """``DDP(module, device_ids=[rank], find_unused_parameters=True)`` (reference ddp/trainer.py:31).
+
+    The communicators are bootstrapped over ``process_group`` (torch.distributed). ``comm=`` (and
+    ``sync_comm=`` for SyncBatchNorm) take native communicators directly instead -- e.g. the ranks of
+    ``Comm.thread_group``, which runs W ranks on one GPU from W host threads (tests)."""
+
     def __init__(self, module, device_ids=None, output_device=None, dim=0, broadcast_buffers=True,
-                 process_group=None, bucket_cap_mb=25, find_unused_parameters=False, **_ignored):
+                 process_group=None, bucket_cap_mb=25, find_unused_parameters=False, comm=None, sync_comm=None,
+                 **_ignored):
         super().__init__()
-        if not dist.is_initialized():
+        if comm is None and not dist.is_initialized():
             raise NativeError("DistributedDataParallel requires torch.distributed.init_process_group")
         self.module = module
         self.broadcast_buffers = broadcast_buffers
         self.find_unused_parameters = find_unused_parameters
-        self.world_size = dist.get_world_size(process_group)
-        self.rank = dist.get_rank(process_group)
+        if comm is not None:
+            self.world_size, self.rank = comm.world, comm.rank
+        else:
+            self.world_size = dist.get_world_size(process_group)
+            self.rank = dist.get_rank(process_group)
         self.process_group = process_group
-        self._sync_checked = set()
+        self._cnt = None  # SyncBN batch-size check (see _check_sync_bn_batch)
         flat = module.flat  # raises unless the module already lives on a GPU
         device = flat.device.index if flat.device.index is not None else torch.cuda.current_device()
         if device_ids:
@@ -209,8 +235,8 @@ class DistributedDataParallel(nn.Module):
             if d != device:
                 raise NativeError(f"device_ids={device_ids} but the module lives on cuda:{device}")
         with torch.cuda.device(device):
-            self.comm = Comm.from_process_group(device, process_group)
-            if process_group is None:
+            self.comm = comm if comm is not None else Comm.from_process_group(device, process_group)
+            if process_group is None and comm is None:
                 _WORLD_COMM[0] = self.comm  # barrier() of the default group runs on it
             module.set_bucket_cap_mb(float(bucket_cap_mb))
             # a one-rank all-reduce is the identity: no side-stream fork/join inside the backward
@@ -220,9 +246,11 @@ class DistributedDataParallel(nn.Module):
             # stream while the Reducer's bucket all-reduces run on its side stream)
             self.sync_comm = None
             if getattr(module, "_sync_bn", False) and self.world_size > 1:
-                self.sync_comm = Comm.from_process_group(device, getattr(module, "_sync_bn_group", None) or process_group)
+                self.sync_comm = sync_comm if sync_comm is not None else Comm.from_process_group(
+                    device, getattr(module, "_sync_bn_group", None) or process_group)
                 module.set_sync_bn(self.sync_comm)
-            # C1: make every replica start from rank 0's state
+            # C1: make every replica start from rank 0's state -- on the Reducer's communicator,
+            # ordered after the caller's stream (the module's parameters were written there)
             self.comm.broadcast_(flat.params, 0)
             self.comm.broadcast_(flat.bufs, 0)
             self.comm.broadcast_(flat.nbt, 0)
@@ -237,16 +265,39 @@ class DistributedDataParallel(nn.Module):
 
     def _check_sync_bn_batch(self, x) -> None:
         """SyncBN normalises with world x local count (the executor all-reduces compact sums, not
-        per-rank counts as torch's all_gather does): every rank's batch must be the same size --
-        checked once per input shape over the process group (drop_last samplers guarantee it)."""
+        per-rank counts as torch's all_gather does), so every rank's batch must be the same size.
+        Every training forward of every rank issues the same check (one 2-double SUM all-reduce of
+        (n, n^2) on the SyncBN communicator: sizes are equal iff W * sum(n^2) == sum(n)^2), so the
+        ranks' collectives always match (no per-rank cache deciding who enters). The host
+        waits for the result when this rank's batch size changed (first step included); otherwise the
+        previous step's result is checked here, long since complete."""
         n = int(x.shape[0])
-        if n in self._sync_checked:
-            return
-        sizes = [None] * self.world_size
-        dist.all_gather_object(sizes, n, group=self.process_group)
-        if len(set(sizes)) != 1:
-            raise NativeError(f"SyncBatchNorm: per-rank batch sizes differ {sizes}; use equal shards")
-        self._sync_checked.add(n)
+        dev = self.module.flat.device
+        if self._cnt is None:
+            self._cnt = {"dev": torch.zeros(2, dtype=torch.float64, device=dev),
+                         "host": torch.zeros(2, dtype=torch.float64, pin_memory=True),
+                         "ev": None, "n": None}
+        st = self._cnt
+        if st["ev"] is not None:  # the previous step's check
+            st["ev"].synchronize()
+            self._assert_equal_batches(st["host"])
+        st["dev"].copy_(torch.tensor([float(n), float(n) * n], dtype=torch.float64), non_blocking=False)
+        self.sync_comm.allreduce_sum_(st["dev"])
+        st["host"].copy_(st["dev"], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        st["ev"] = ev
+        if st["n"] != n:
+            ev.synchronize()
+            self._assert_equal_batches(st["host"])
+            st["ev"] = None
+            st["n"] = n
+
+    def _assert_equal_batches(self, h) -> None:
+        s1, s2 = float(h[0]), float(h[1])
+        if abs(self.world_size * s2 - s1 * s1) > 0.5:
+            raise NativeError(f"SyncBatchNorm: per-rank batch sizes differ (sum {s1:.0f}, sum of squares "
+                              f"{s2:.0f} over {self.world_size} ranks); use equal shards")
 
     def forward(self, *inputs, **kwargs):
         if self.sync_comm is not None and self.module.training and inputs:
@@ -410,9 +461,9 @@ class _DPFn(torch.autograd.Function):
         model = dp.module
         dev0 = dp.devices[0]
         dl = dlogits.contiguous().float()
+        for exe, gen in ctx.runs:
+            exe.consume(gen)
         for i, (exe, gen) in enumerate(ctx.runs):
-            if exe.generation != gen:
-                raise NativeError("DataParallel backward: a replica ran another forward since this graph was built")
             dev = dp.devices[i]
             d = dl[ctx.offs[i]:ctx.offs[i] + ctx.sizes[i]]
             with torch.cuda.device(dev):

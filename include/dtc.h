@@ -213,6 +213,19 @@ int dtc_comm_init_loopback(dtc_comm** out, int device, int world, float factor);
 int dtc_comm_log_size(dtc_comm* comm);
 int dtc_comm_log_entry(dtc_comm* comm, int idx, uint64_t* addr, uint64_t* count, int* is_async);
 int dtc_comm_log_clear(dtc_comm* comm);
+/* In-process thread-group communicator (test transport, no RCCL): `world` handles outs[0..world-1] =
+ * ranks 0..world-1 on one device, each driven by its own host thread with its own streams and buffers.
+ * Collectives are matched by call order (as RCCL's): the calling thread blocks until every rank issued
+ * the same collective (kind, count, dtype, root; a mismatch or a 120 s wait is an error for all ranks),
+ * then the data really moves between the ranks' buffers on a group stream that waits for every rank's
+ * producers -- SUM all-reduce as the rank-ordered fp32/fp64 sum written into every buffer, broadcast as
+ * root -> all copies, barrier as a host rendezvous + stream drain -- and each rank's consumer stream
+ * (the Reducer's side stream for buckets) waits for the result. Lets one GPU run W ranks with DISTINCT
+ * data through the product Reducer, broadcasts and SyncBN (max 8 ranks). Every all-reduce is logged
+ * as for the loopback communicator. Destroy each handle with dtc_comm_destroy. */
+int dtc_comm_init_thread_group(dtc_comm** outs, int world, int device);
+int dtc_comm_rank(const dtc_comm* comm);
+int dtc_comm_world(const dtc_comm* comm);
 
 /* ------------------------------------------------------------------ DataParallel group
  * Replaces the per-step traffic of nn.DataParallel (reference src/dp/trainer.py:27):

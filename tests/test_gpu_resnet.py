@@ -791,6 +791,38 @@ def test_native_loss_backward_matches_autograd(dtc, cuda):
     assert type(loss * 2.0) is torch.Tensor
 
 
+def test_second_backward_refused_and_sums_rezeroed(dtc, cuda):
+    """the BN backward sums are zeroed by the training forward only. (1) The Python layer
+    refuses a second backward over one forward (torch would ACCUMULATE into .grad; the kernels write);
+    (2) a second backward issued straight through the C ABI re-zeroes the sums first, so it writes the
+    same gradients as the first instead of adding onto the first backward's sums."""
+    import ctypes as C
+
+    model, _, x, y = _setup(dtc, cuda, 8, seed=5)
+    crit = dtc.CrossEntropyLoss()
+    xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
+    loss = crit(model(xd), yd)
+    loss.backward(retain_graph=True)
+    g1 = model.flat.grads.clone()
+    with pytest.raises(dtc.NativeError, match="already back-propagated"):
+        loss.backward()
+    exe = model.executor(8, 32, 32)
+    dl = exe.dlogits_buffer()
+    for graphs in (1, 0):
+        dtc._native.lib.dtc_set_option(b"graphs", graphs)
+        try:
+            crit(model(xd), yd).backward()
+            g_a = model.flat.grads.clone()
+            dtc._native.call("dtc_rn18_backward", exe.handle, C.c_void_p(dl.data_ptr()), C.c_float(1.0), None,
+                             dtc._native.stream_ptr())
+            torch.cuda.synchronize()
+            g_b = model.flat.grads.clone()
+        finally:
+            dtc._native.lib.dtc_set_option(b"graphs", 1)
+        assert torch.equal(g_a, g_b), (graphs, (g_a - g_b).abs().max().item())
+    assert rel_err(g1.cpu().numpy(), g_a.cpu().numpy()) < 1e-5
+
+
 def test_native_barrier_waits_for_queued_work(dtc, cuda):
     """dtc.barrier() (dtc_barrier; the reference's per-step dist.barrier(), trainer.py:156) returns only
     after the work queued on the current stream before it finished -- torch's NCCL barrier semantics
