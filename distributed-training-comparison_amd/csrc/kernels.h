@@ -77,7 +77,6 @@ enum {
   OPT_STEM_RECOMPUTE = 43, // training forward: 1 = stem statistics pass + recompute pass with the BN apply fused
   OPT_STEM_WLDS = 44,      // stem forward: 1 (default) = weight staged in LDS by coalesced loads, not per-lane
                            // 2-B gathers (stem_bench: 18.7 -> 16.1 us; +1.1% interleaved A/B)
-  OPT_GRAPH_RETIRE = 45,  // executor: 1 = replaced graph execs destroyed one drop later; 0 = at the drop
   OPT_COUNT
 };
 int option_get(int id);

@@ -107,6 +107,10 @@ struct Net {
   // Graph-safe: the slot pointers are baked at capture, nothing happens on the host per call.
   static constexpr int PROF_SLOTS = 256, PROF_BWD0 = 96;  // forward calls use [0,96), backward [96,256)
   bool profiling = false;
+  // both in the caller-owned workspace (planned by plan_workspace): the slot pointers baked into the
+  // profiled graphs stay valid for the executor's lifetime, so arming / disarming profiling neither
+  // frees memory nor destroys graphs (it switches between the two graph sets below)
+  size_t PROF_TS = 0, PROF_ACC = 0;
   u64* prof_ts = nullptr;   // [PROF_SLOTS][DTC_PROF_SLOT_U64] device
   u64* prof_acc = nullptr;  // [PROF_SLOTS][2] device: (sum ticks, calls)
   int prof_next = 0;
@@ -118,11 +122,14 @@ struct Net {
   struct Seg { hipGraphExec_t exec = nullptr; std::vector<int> buckets; };
   hipStream_t cap_st = nullptr;
   int graph_epoch = -1;
-  hipGraphExec_t fwd_exec[2] = {nullptr, nullptr};
-  std::vector<Seg> bwd_segs;
-  std::vector<hipGraphExec_t> retired;  // replaced graph execs, destroyed one drop later (drop_graphs)
-  float bwd_gs = 0.f;
-  bool bwd_comm = false;
+  // graph sets indexed [profiling]: the profiled set carries the timing stamps and the per-step fold
+  hipGraphExec_t fwd_exec[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [profiling][train]
+  std::vector<Seg> bwd_segs[2];
+  float bwd_gs[2] = {0.f, 0.f};
+  bool bwd_comm[2] = {false, false};
+  // recorded on the launch stream after every graph launch: drop_graphs waits for it before destroying
+  hipEvent_t launch_ev = nullptr;
+  bool launched = false;
   size_t LOGITS = 0, DLOGITS = 0;  // graph-owned copies of the caller's logits / dlogits
   // activation registry (per-layer parity): name, workspace byte offset, N,H,W,C
   struct Act { std::string name; size_t off; int n, h, w, c; };
@@ -329,6 +336,8 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   }
   n.DC0 = take(M0 * 64 * E);
   // BN per-layer state
+  n.PROF_TS = take((size_t)Net::PROF_SLOTS * DTC_PROF_SLOT_U64 * sizeof(u64));
+  n.PROF_ACC = take((size_t)Net::PROF_SLOTS * 2 * sizeof(u64));
   n.stats_lo = off;  // forward statistics of every BN, then backward sums: both zeroed by the training forward
   for (BNL* b : n.bns) b->stats = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
   n.acc_lo = off;
@@ -430,29 +439,39 @@ static u64* prof_slot(Net& n, int kind, double flops) {
   } while (0)
 
 // ------------------------------------------------------------------ graph capture helpers
-static void drop_graphs(Net& n, bool final_ = false) {
-  // a graph exec may still be running (the caller's previous step is asynchronous): destroying it then
-  // frees state its in-flight kernels use (seen as a later crash in a sync), so drain the device first.
-  // Even after the drain the runtime's own completion handling of the last launch can still touch the
-  // exec from a worker thread (a rare crash outside the calling thread in test_live_conv_profile), so
-  // replaced execs are retired here and destroyed at the NEXT drop, when nothing can reference them.
-  bool any = !n.bwd_segs.empty();
-  for (auto e : n.fwd_exec) any = any || e != nullptr;
-  if (any || final_) (void)hipDeviceSynchronize();
-  for (auto e : n.retired) (void)hipGraphExecDestroy(e);
-  n.retired.clear();
-  for (auto& e : n.fwd_exec)
-    if (e) {
-      n.retired.push_back(e);
-      e = nullptr;
-    }
-  for (auto& sg : n.bwd_segs)
-    if (sg.exec) n.retired.push_back(sg.exec);
-  n.bwd_segs.clear();
-  if (final_ || option_get(OPT_GRAPH_RETIRE) == 0) {
-    for (auto e : n.retired) (void)hipGraphExecDestroy(e);
-    n.retired.clear();
+static void drop_graphs(Net& n) {
+  // An exec may still be running (the caller's previous step is asynchronous). Round 2 saw a rare
+  // crash in a HIP runtime thread (no Python frame) when execs were destroyed right after a device
+  // drain and the profiling slots their kernels stamp were freed next (dtc_rn18_profile_end). The
+  // slots now live in the workspace (never freed while an exec exists) and an exec is destroyed only
+  // after (1) the event recorded behind its LAST launch on the launch stream has completed -- the
+  // runtime has retired every command of that launch, in stream order -- and (2) a device drain.
+  bool any = false;
+  for (auto& set : n.fwd_exec)
+    for (auto e : set) any = any || e != nullptr;
+  for (auto& v : n.bwd_segs) any = any || !v.empty();
+  if (!any) return;
+  if (n.launched && n.launch_ev) (void)hipEventSynchronize(n.launch_ev);
+  (void)hipDeviceSynchronize();
+  for (auto& set : n.fwd_exec)
+    for (auto& e : set)
+      if (e) {
+        (void)hipGraphExecDestroy(e);
+        e = nullptr;
+      }
+  for (auto& v : n.bwd_segs) {
+    for (auto& sg : v)
+      if (sg.exec) (void)hipGraphExecDestroy(sg.exec);
+    v.clear();
   }
+  n.launched = false;
+}
+static int graph_launch(Net& n, hipGraphExec_t ex, hipStream_t st) {
+  DTC_HIP(hipGraphLaunch(ex, st));
+  if (!n.launch_ev) DTC_HIP(hipEventCreateWithFlags(&n.launch_ev, hipEventDisableTiming));
+  DTC_HIP(hipEventRecord(n.launch_ev, st));
+  n.launched = true;
+  return 0;
 }
 static bool graphs_on(Net& n) {
   if (n.capture || n.sync || option_get(OPT_GRAPHS) == 0) return false;
@@ -821,7 +840,7 @@ static int forward_impl(Net& n, const float* x, float* logits, bool train, hipSt
   }
   else DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
   if (!graphs_on(n)) return forward_body(n, logits, train, st);
-  hipGraphExec_t& ex = n.fwd_exec[train ? 1 : 0];
+  hipGraphExec_t& ex = n.fwd_exec[n.profiling ? 1 : 0][train ? 1 : 0];
   // option head_direct: the pool + FC head is launched after the graph, straight into the caller's
   // logits (the graph cannot bake in a per-call pointer), instead of a graph-owned copy + D2D copy
   const bool direct = !n.f32 && option_get(OPT_HEAD_DIRECT) != 0;
@@ -830,7 +849,7 @@ static int forward_impl(Net& n, const float* x, float* logits, bool train, hipSt
     const int rc = forward_body(n, direct ? nullptr : n.at<float>(n.LOGITS), train, n.cap_st);
     DTC_TRY(end_capture(n, rc, &ex));
   }
-  DTC_HIP(hipGraphLaunch(ex, st));
+  DTC_TRY(graph_launch(n, ex, st));
   if (direct) return forward_head(n, logits, st);
   DTC_HIP(hipMemcpyAsync(logits, n.at<float>(n.LOGITS), (size_t)n.B * n.ncls * 4, hipMemcpyDeviceToDevice, st));
   return 0;
@@ -1355,8 +1374,9 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
     cx.comm = comm;
     DTC_TRY(backward_body(n, dlogits, gs, cx, st));
   } else {
-    if (!n.bwd_segs.empty() && (n.bwd_gs != gs || n.bwd_comm != (comm != nullptr))) drop_graphs(n);
-    if (n.bwd_segs.empty()) {
+    const int pi = n.profiling ? 1 : 0;
+    if (!n.bwd_segs[pi].empty() && (n.bwd_gs[pi] != gs || n.bwd_comm[pi] != (comm != nullptr))) drop_graphs(n);
+    if (n.bwd_segs[pi].empty()) {
       std::vector<Net::Seg> segs;
       BwdCtx cx;
       cx.comm = comm;
@@ -1371,14 +1391,14 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
         return rc;
       }
       segs.push_back(tail);
-      n.bwd_segs = segs;
-      n.bwd_gs = gs;
-      n.bwd_comm = comm != nullptr;
+      n.bwd_segs[pi] = segs;
+      n.bwd_gs[pi] = gs;
+      n.bwd_comm[pi] = comm != nullptr;
     }
     if (dlogits != n.at<float>(n.DLOGITS))
       DTC_HIP(hipMemcpyAsync(n.at<float>(n.DLOGITS), dlogits, (size_t)n.B * n.ncls * 4, hipMemcpyDeviceToDevice, st));
-    for (const auto& sg : n.bwd_segs) {
-      if (sg.exec) DTC_HIP(hipGraphLaunch(sg.exec, st));
+    for (const auto& sg : n.bwd_segs[pi]) {
+      if (sg.exec) DTC_TRY(graph_launch(n, sg.exec, st));
       for (int i : sg.buckets)
         DTC_TRY(comm_allreduce_async(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st));
     }
@@ -1427,22 +1447,15 @@ int dtc_rn18_create(dtc_net** out, int batch, int height, int width, int num_cla
   return 0;
 }
 
-static void prof_free(Net& n) {
-  if (n.prof_ts) (void)hipFree(n.prof_ts);
-  if (n.prof_acc) (void)hipFree(n.prof_acc);
-  n.prof_ts = n.prof_acc = nullptr;
-  n.profiling = false;
-}
-
 int dtc_rn18_destroy(dtc_net* net) {
   if (net) {
-    drop_graphs(net->n, true);
+    drop_graphs(net->n);
     if (net->n.cap_st) (void)hipStreamDestroy(net->n.cap_st);
     if (net->n.side_st) (void)hipStreamDestroy(net->n.side_st);
     if (net->n.sc_st) (void)hipStreamDestroy(net->n.sc_st);
     for (auto& e : net->n.evs)
       if (e) (void)hipEventDestroy(e);
-    prof_free(net->n);
+    if (net->n.launch_ev) (void)hipEventDestroy(net->n.launch_ev);
   }
   delete net;
   return 0;
@@ -1503,6 +1516,8 @@ int dtc_rn18_bind(dtc_net* net, void* workspace, float* params, float* grads, ui
   n.pb = params_bf16;
   n.bufs = bufs;
   n.nbt = num_batches_tracked;
+  n.prof_ts = n.at<u64>(n.PROF_TS);
+  n.prof_acc = n.at<u64>(n.PROF_ACC);
   drop_graphs(n);  // captured launches hold the previous pointers
   DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.stats_hi - n.stats_lo, (hipStream_t)stream));
   return 0;
@@ -1557,25 +1572,22 @@ int dtc_rn18_dlogits_buffer(const dtc_net* net, size_t* ws_offset) {
 }
 
 int dtc_rn18_profile_begin(dtc_net* net, int capacity) {
-  DTC_CHECK_ARG(net && capacity > 0, "dtc_rn18_profile_begin: bad args");
+  DTC_CHECK_ARG(net && capacity > 0 && net->n.ws, "dtc_rn18_profile_begin: bad args or unbound net");
   Net& n = net->n;
   const size_t bytes = (size_t)Net::PROF_SLOTS * 2 * sizeof(u64);
   const size_t ts_bytes = (size_t)Net::PROF_SLOTS * DTC_PROF_SLOT_U64 * sizeof(u64);
-  if (!n.prof_ts) {
-    int dev = 0;
-    DTC_HIP(hipGetDevice(&dev));
-    DTC_HIP(hipDeviceGetAttribute(&n.prof_khz, hipDeviceAttributeWallClockRate, dev));
-    DTC_CHECK_ARG(n.prof_khz > 0, "dtc_rn18_profile_begin: no wall clock rate");
-    DTC_HIP(hipMalloc(&n.prof_ts, ts_bytes));
-    DTC_HIP(hipMalloc(&n.prof_acc, bytes));
-    drop_graphs(n);  // re-capture with the timing slots
-  }
+  int dev = 0;
+  DTC_HIP(hipGetDevice(&dev));
+  DTC_HIP(hipDeviceGetAttribute(&n.prof_khz, hipDeviceAttributeWallClockRate, dev));
+  DTC_CHECK_ARG(n.prof_khz > 0, "dtc_rn18_profile_begin: no wall clock rate");
+  // the previous step may still run (its profiled graphs stamp these slots): drain, then reset.
   // slots -> (~0, 0) (folding all-zero slots adds nothing and resets them), then totals -> 0
+  DTC_HIP(hipDeviceSynchronize());
   DTC_HIP(hipMemset(n.prof_ts, 0, ts_bytes));
   DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, nullptr));
   DTC_HIP(hipMemset(n.prof_acc, 0, bytes));
   DTC_HIP(hipDeviceSynchronize());
-  n.profiling = true;
+  n.profiling = true;  // the next calls launch (capturing on first use) the profiled graph set
   return 0;
 }
 
@@ -1592,7 +1604,7 @@ int dtc_rn18_profile_end_ex(dtc_net* net, int nkinds, double* ms_by_kind, double
     if (flops_by_kind) flops_by_kind[k] = 0;
     if (count_by_kind) count_by_kind[k] = 0;
   }
-  if (!n.prof_ts) return 0;
+  if (!n.profiling) return 0;
   std::vector<u64> acc((size_t)Net::PROF_SLOTS * 2);
   DTC_HIP(hipDeviceSynchronize());
   DTC_HIP(hipMemcpy(acc.data(), n.prof_acc, acc.size() * sizeof(u64), hipMemcpyDeviceToHost));
@@ -1605,8 +1617,7 @@ int dtc_rn18_profile_end_ex(dtc_net* net, int nkinds, double* ms_by_kind, double
     if (flops_by_kind) flops_by_kind[k] += n.prof_flops[i] * (double)calls;
     if (count_by_kind) count_by_kind[k] += (int)calls;
   }
-  drop_graphs(n);
-  prof_free(n);
+  n.profiling = false;  // back to the plain graph set; both sets stay captured
   return 0;
 }
 

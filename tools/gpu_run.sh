@@ -10,6 +10,9 @@
 #   pmc              rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs) -> gpurun_out/pmc_TAG_{fetch,write}
 #   ab:SPEC          tools/bench_ab.sh $AB_ROUNDS SPEC... (SPEC = "tagA|opts;tagB|opts")
 #   py:FILE          python FILE $PY_ARGS                 -> gpurun_out/TAG_FILE.log
+#   config3          BASELINE config 3 per-rank shapes on one GPU: bench.py --global-batch 256 --sim-world W
+#                    for W = 2, 4, 8 (B = 128, 64, 32), each with a rocprofv3 kernel trace
+#                    -> gpurun_out/TAG_c3_wW_bench.json, gpurun_out/prof_TAG_c3_wW
 # Every step runs under its own time limit via tools/gpu_session.sh (stops on crash / hang).
 set -u
 TAG=$1; shift
@@ -28,6 +31,10 @@ for st in "$@"; do
          specs+=("${TAG}_pmcw|150|cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $ROOT/gpurun_out/pmc_${TAG}_write -o run -- python3 $ROOT/bench.py --steps 10 --warmup 3 $QUIET $BA") ;;
     ab:*) IFS=';' read -ra parts <<< "${st#ab:}"; q=""; for p in "${parts[@]}"; do q="$q '$p'"; done
           specs+=("${TAG}_ab|900|tools/bench_ab.sh ${AB_ROUNDS:-4}$q") ;;
+    config3) for w in 2 4 8; do
+               specs+=("${TAG}_c3_w${w}|300|python bench.py --global-batch 256 --sim-world $w --no-cpu-baseline $BA > gpurun_out/${TAG}_c3_w${w}_bench.json")
+               specs+=("${TAG}_c3_w${w}_prof|300|cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats -d $ROOT/gpurun_out/prof_${TAG}_c3_w${w} -o prof -- python3 $ROOT/bench.py --global-batch 256 --sim-world $w --steps 20 --warmup 5 $QUIET $BA")
+             done ;;
     py:*) f="${st#py:}"; specs+=("${TAG}_$(basename "$f" .py)|300|python -u $f ${PY_ARGS:-}") ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac

@@ -1,10 +1,10 @@
 """Graph-exec lifecycle stress (diagnostics for the round-2 intermittent crash in
-test_live_conv_profile, DESIGN.md "Graph execs"): repeatedly re-capture the step graphs (option
-epoch changes and profile begin/end both drop them) with graph_retire=0, i.e. every replaced exec
-destroyed at the drop right after the device drain. The native crash handler reports the faulting
-thread and its frames if the destroy races anything.
+test_live_conv_profile, DESIGN.md "Graph execs"): every cycle changes an option (the next step drops
+and destroys the step graphs and re-captures them) and arms / disarms the live conv profile (which
+switches between the plain and the profiled graph sets). The native crash handler reports the
+faulting thread and its frames if a destroy races anything.
 
-usage: python tools/graph_churn.py [cycles] [retire] [batch]
+usage: python tools/graph_churn.py [cycles] [batch]
 """
 import ctypes as C
 import sys
@@ -21,10 +21,8 @@ lib = dtc._native.lib
 
 def main():
     cycles = int(sys.argv[1]) if len(sys.argv) > 1 else 60
-    retire = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-    batch = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     lib.dtc_install_crash_handler()
-    lib.dtc_set_option(b"graph_retire", retire)
     dev = torch.device("cuda:0")
     torch.manual_seed(42)
     model = dtc.ResNet18().to(dev)
@@ -47,7 +45,7 @@ def main():
             print(f"cycle {i} ok ({time.time() - t0:.1f} s), calls {list(cnt)}", flush=True)
     torch.cuda.synchronize()
     lib.dtc_set_option(b"sc_fuse", 1)
-    print(f"graph churn: {cycles} cycles, retire={retire}: no crash ({time.time() - t0:.1f} s)", flush=True)
+    print(f"graph churn: {cycles} cycles: no crash ({time.time() - t0:.1f} s)", flush=True)
 
 
 if __name__ == "__main__":
