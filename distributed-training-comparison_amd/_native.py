@@ -57,6 +57,10 @@ _SIGS = {
     "dtc_conv2d_workspace_size": (sz, [PConv, i32]),
     "dtc_conv2d_fwd": (i32, [PConv, vp, vp, vp, vp, vp, sz, vp]),
     "dtc_conv2d_dgrad": (i32, [PConv, vp, vp, vp, vp, vp, sz, vp]),
+    "dtc_conv2d_fwd_sc": (i32, [PConv, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "dtc_conv2d_dgrad_sc": (i32, [PConv, vp, vp, vp, vp, vp, vp]),
+    "dtc_conv2d_wgrad_sc_workspace_size": (sz, [PConv]),
+    "dtc_conv2d_wgrad_sc": (i32, [PConv, vp, vp, vp, vp, vp, f32, vp, sz, vp]),
     "dtc_conv2d_dgrad_bn": (i32, [PConv, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]),
     "dtc_conv2d_wgrad": (i32, [PConv, vp, vp, vp, f32, vp, sz, vp]),
     "dtc_conv2d_wgrad_batch_workspace_size": (sz, [PConv, i32]),

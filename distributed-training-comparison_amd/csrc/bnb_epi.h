@@ -16,7 +16,10 @@
 namespace dtc {
 
 struct BnbArgs {
-  const u16* ym = nullptr;  // post-ReLU activation y (mask source); null: plain dgrad epilogue
+  const u16* ym = nullptr;  // post-ReLU activation y (mask source); null (and mb null): plain dgrad epilogue
+  // the forward's ReLU mask bits of y instead (option bnb_mask; bit e & 7 of byte e >> 3 for element e):
+  // 1/16 of ym's bytes
+  const uint8_t* mb = nullptr;
   const u16* x1 = nullptr;  // input of the (first) BN: the conv output it normalised
   const float* mean1 = nullptr;
   const float* invstd1 = nullptr;
@@ -26,6 +29,16 @@ struct BnbArgs {
   const float* invstd2 = nullptr;
   double* acc2 = nullptr;
 };
+
+__host__ __device__ __forceinline__ bool bnb_on(const BnbArgs& a) { return a.ym != nullptr || a.mb != nullptr; }
+
+// The 4 ReLU-mask bits of the elements o .. o + 3 (o % 4 == 0) as y-like values (1.0 = kept, 0 = masked).
+__device__ __forceinline__ uint2 bnb_bits_as_y(const uint8_t* mb, size_t o) {
+  const uint32_t nib = (uint32_t)(mb[o >> 3] >> (o & 4)) & 15u;
+  // bf16 1.0 = 0x3F80 in the lanes whose bit is set
+  return uint2{((nib & 1u) ? 0x3F80u : 0u) | ((nib & 2u) ? 0x3F800000u : 0u),
+               ((nib & 4u) ? 0x3F80u : 0u) | ((nib & 8u) ? 0x3F800000u : 0u)};
+}
 
 // Per-lane state for 4 consecutive channels (one MFMA output row group of a fragment column).
 struct Bnb4 {
@@ -72,7 +85,7 @@ __device__ __forceinline__ void bnb4_vals(uint2 y, uint2 x, uint2 x2, bool valid
 __device__ __forceinline__ void bnb4_apply(const BnbArgs& a, size_t o, bool valid, bool dual, float v[4], Bnb4& b) {
   uint2 y{0u, 0u}, x{0u, 0u}, x2{0u, 0u};
   if (valid) {
-    y = *(const uint2*)(a.ym + o);
+    y = a.mb ? bnb_bits_as_y(a.mb, o) : *(const uint2*)(a.ym + o);
     x = *(const uint2*)(a.x1 + o);
     if (dual) x2 = *(const uint2*)(a.x2 + o);
   }

@@ -19,11 +19,11 @@
 #include <unistd.h>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {0}, {1}, {1}, {0}, {1}, {16384}, {256}, {1024}, {1}, {1}, {1}, {1}, {0}, {1}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {0}, {1}, {1}, {0}, {1}, {16384}, {256}, {1024}, {1}, {1}, {1}, {1}, {0}, {1}, {1}, {0}, {0}, {0}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
                                              "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
                                              "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse",
-                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct", "wgrad_defer", "igemm_tile", "igemm_split", "bn_onepass", "sc_stream", "dgrad_class_order", "head_fused", "stem_prologue", "sc_compact", "wgrad_tail", "stem_bn_fuse", "bn_red_elems", "bn_red_blocks", "bn_fa_blocks", "fork_lazy", "side_prio", "sc_fuse", "head_direct", "stem_recompute", "stem_wlds"};
+                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct", "wgrad_defer", "igemm_tile", "igemm_split", "bn_onepass", "sc_stream", "dgrad_class_order", "head_fused", "stem_prologue", "sc_compact", "wgrad_tail", "stem_bn_fuse", "bn_red_elems", "bn_red_blocks", "bn_fa_blocks", "fork_lazy", "side_prio", "sc_fuse", "head_direct", "stem_recompute", "stem_wlds", "halo_s2", "wgrad_s2", "dgrad_scf", "bnb_mask"};
 static std::atomic<int> g_epoch{0};
 // DTC_OPTIONS="name=value,name=value" in the environment overrides defaults at library load (A/B and
 // bisection runs of whole test suites without code changes)
@@ -191,6 +191,15 @@ int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w,
   GUARD(return conv_fwd(shape_of(d), x, w, y, stats, (float*)ws, ws ? ws_bytes : 0, S(stream));)
 }
 
+int dtc_conv2d_fwd_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats,
+                      const uint16_t* wsc, uint16_t* ysc, double* stats_sc, void* stream) {
+  DTC_CHECK_ARG(d && x && w && y && wsc && ysc, "dtc_conv2d_fwd_sc: null argument");
+  const ConvShape s = shape_of(d);
+  const ConvShape sc{s.N, s.H, s.W, s.C, s.K, 1, 1, 2, 0};
+  DTC_CHECK_ARG(conv_fwd_sc_ok(s, sc), "dtc_conv2d_fwd_sc: no fused plan for this geometry");
+  GUARD(return conv_fwd_sc(s, sc, x, w, y, stats, wsc, ysc, stats_sc, S(stream));)
+}
+
 int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx, const uint16_t* res,
                      void* ws, size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && dy && w && dx, "dtc_conv2d_dgrad: null argument");
@@ -209,10 +218,29 @@ int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16
   GUARD(return conv_dgrad(shape_of(d), dy, w, dx, res, (float*)ws, ws ? ws_bytes : 0, S(stream), nullptr, &a);)
 }
 
+int dtc_conv2d_dgrad_sc(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
+                        const uint16_t* dsc, const uint16_t* wsc, void* stream) {
+  DTC_CHECK_ARG(d && dy && w && dx && dsc && wsc, "dtc_conv2d_dgrad_sc: null argument");
+  DTC_CHECK_ARG(conv_dgrad_sc_ok(shape_of(d)), "dtc_conv2d_dgrad_sc: no fused plan for this geometry");
+  GUARD(return conv_dgrad_sc(shape_of(d), dy, w, dx, dsc, wsc, S(stream));)
+}
+
 int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* dw, float scale, void* ws,
                      size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && dy && dw && ws, "dtc_conv2d_wgrad: null argument (workspace is required)");
   GUARD(return conv_wgrad(shape_of(d), x, dy, dw, 0, 0, scale, (float*)ws, ws_bytes, S(stream));)
+}
+
+size_t dtc_conv2d_wgrad_sc_workspace_size(const dtc_conv_desc* d) {
+  if (!d) return 0;
+  const ConvShape s = shape_of(d);
+  return wgrad_s2_splits(s) > 0 ? conv_wgrad_s2_slab_bytes(s) : 0;
+}
+
+int dtc_conv2d_wgrad_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, const uint16_t* dsc, float* dw,
+                        float* dw_sc, float scale, void* ws, size_t ws_bytes, void* stream) {
+  DTC_CHECK_ARG(d && x && dy && dsc && dw && dw_sc, "dtc_conv2d_wgrad_sc: null argument");
+  GUARD(return conv_wgrad_s2(shape_of(d), x, dy, dsc, dw, dw_sc, scale, (float*)ws, ws ? ws_bytes : 0, S(stream));)
 }
 
 size_t dtc_conv2d_wgrad_batch_workspace_size(const dtc_conv_desc* d, int n) {

@@ -133,8 +133,11 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   const __amdgpu_buffer_rsrc_t rrsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)(RES ? p.res : p.out), 0, RES ? p.out_bytes : 0, 0x00020000);
   const uint32_t halo_lds = __builtin_amdgcn_readfirstlane(lds_u32(halo));
-  const __amdgpu_buffer_rsrc_t yrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(BNB ? p.bnb.ym : p.out), 0, BNB ? p.out_bytes : 0, 0x00020000);
+  // mask source: the bf16 y, or (bnb.mb) the forward's ReLU mask bits -- 1 byte per 8 channels
+  const bool mbits = BNB && p.bnb.mb != nullptr;
+  const __amdgpu_buffer_rsrc_t yrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(BNB ? (mbits ? (const void*)p.bnb.mb : (const void*)p.bnb.ym) : (const void*)p.out), 0,
+      BNB ? (mbits ? p.out_bytes / 16 : p.out_bytes) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t xrsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)(BNB ? p.bnb.x1 : p.out), 0, BNB ? p.out_bytes : 0, 0x00020000);
 
@@ -193,7 +196,15 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     for (int i = 0; i < FM; ++i) {
       off[i] = ok ? epi_off(tile, j, i) : 0x80000000u;
       if constexpr (BNB) {  // out-of-range lanes read zeros (descriptor bound): masked to 0, no sums
-        yy[i] = __builtin_amdgcn_raw_buffer_load_b64(yrsrc, off[i], 0, 0);
+        if (mbits) {  // element e = off / 2: bits (e & 4) .. + 3 of byte e >> 3
+          const uint32_t e = off[i] >> 1;
+          const uint32_t by = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(yrsrc, off[i] == 0x80000000u ? 0x80000000u : e >> 3, 0, 0);
+          const uint32_t nib = (by >> (e & 4)) & 15u;
+          yy[i].x = (int)(((nib & 1u) ? 0x3F80u : 0u) | ((nib & 2u) ? 0x3F800000u : 0u));
+          yy[i].y = (int)(((nib & 4u) ? 0x3F80u : 0u) | ((nib & 8u) ? 0x3F800000u : 0u));
+        } else {
+          yy[i] = __builtin_amdgcn_raw_buffer_load_b64(yrsrc, off[i], 0, 0);
+        }
         xx[i] = __builtin_amdgcn_raw_buffer_load_b64(xrsrc, off[i], 0, 0);
       }
     }
@@ -385,7 +396,7 @@ bool conv_c64_ok(const ConvShape& s) {
 int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, double* stats,
              hipStream_t st, u64* ts, const BnbArgs* bnb) {
   DTC_CHECK_ARG(conv_c64_ok(s) && (mode == CONV_FWD || mode == CONV_DGRAD), "conv_c64: unsupported shape");
-  const bool fuse = mode == CONV_DGRAD && bnb != nullptr && bnb->ym != nullptr;
+  const bool fuse = mode == CONV_DGRAD && bnb != nullptr && bnb_on(*bnb);
   DTC_CHECK_ARG(!fuse || (bnb->x1 && bnb->mean1 && bnb->invstd1 && bnb->acc1), "conv_c64: BN-backward args");
   C64Params p{};
   p.src = src; p.w = w; p.out = out; p.res = res; p.stats = stats;
@@ -427,9 +438,13 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   }
 #undef DTC_C64
   DTC_LAUNCH_CHECK();
-  if (fuse && !in_kernel)
+  if (fuse && !in_kernel) {
+    if (bnb->mb)
+      return bn_bwd_reduce_mask(out, bnb->mb, bnb->x1, bnb->mean1, bnb->invstd1, bnb->acc1, bnb->x2, bnb->mean2,
+                                bnb->invstd2, bnb->acc2, M, 64, st);
     return bn_bwd_reduce(out, bnb->ym, bnb->x1, bnb->mean1, bnb->invstd1, bnb->acc1, bnb->x2, bnb->mean2,
                          bnb->invstd2, bnb->acc2, out, M, 64, st);
+  }
   return 0;
 }
 

@@ -68,9 +68,22 @@ struct HConvParams {
   BnbArgs bnb;  // DGRAD: fused BN-backward prologue (bnb.ym null: off)
   FastDiv fd_hb, fd_w2, fd_spx, fd_w;
   u64* ts;
+  // output dims (Ho, Wo) and halo row pitch; stride 1: (H, W) and W + 2
+  int Ho, Wo, pitch;
+  // stride 2 (FWD, ST = 2): the halo is stored column-split -- padded input column 2j at halo column j,
+  // 2j + 1 at hwh + j (hwh = Wo + 1) -- so the output pixels of a fragment read CONSECUTIVE halo rows
+  // for every tap, as at stride 1 (bank-conflict-free with the stride-1 swizzle; the row pitch is
+  // padded per geometry where a fragment spans output rows: tools/halo_banks.py)
+  int hwh;
+  // SC (stride-2 FWD): the block's 1x1 stride-2 projection shortcut reads exactly the centre tap's
+  // pixels; its weight chunk [BM][64] is staged next to the ring and a second set of MFMAs on the
+  // centre tap's B fragments accumulates the shortcut output tile (one read of x, one launch)
+  const u16* wsc;  // [Cout][C]
+  u16* out2;
+  double* stats2;
 };
 
-template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP, int WS>
+template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP, int WS, int ST = 1, bool SC = false>
 __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) {
   constexpr int FM = BM / (WR * 16);
   constexpr int FN = BN / (WC * 16);
@@ -78,9 +91,13 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   constexpr int HBYTES = HCAP * 128;
   constexpr int NIW = BM / 32;       // weight DMA instructions per wave per step
   constexpr int NHI = HCAP / 32;     // max halo DMA instructions per wave
+  constexpr int SCBYTES = SC ? WBYTES : 0;
   static_assert(WR * WC == 4 && HCAP % 32 == 0 && (WS == 2 || WS == 3), "shape");
-  __shared__ __attribute__((aligned(1024))) char smem[NHB * HBYTES + WS * WBYTES];
+  static_assert(ST == 1 || (ST == 2 && MODE == 0 && NHB == 1), "stride 2: forward, single halo buffer");
+  static_assert(!SC || (ST == 2 && WS == 3), "shortcut fusion: stride-2 forward, 3-slot weight ring");
+  __shared__ __attribute__((aligned(1024))) char smem[NHB * HBYTES + WS * WBYTES + SCBYTES];
   char* const wbase = smem + NHB * HBYTES;
+  char* const scbase = wbase + WS * WBYTES;
 
   stamp_start(p.ts);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -100,9 +117,9 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     n0 = tb * p.imgs;
     y0 = 0;
   }
-  const int W2 = p.W + 2;
-  const int px0 = (n0 * p.H + y0) * p.W;
-  const int M = p.N * p.H * p.W;
+  const int W2 = p.pitch;
+  const int px0 = (n0 * p.Ho + y0) * p.Wo;
+  const int M = p.N * p.Ho * p.Wo;
   const int lrow = lane >> 3, pc = lane & 7;
   const int RSC = 9 * p.C;
 
@@ -136,7 +153,15 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     if (q < p.nhi && hr < p.nh) {
       const int i = (int)fdiv((uint32_t)hr, p.fd_hb), rem = hr - i * p.hb;
       const int hy = (int)fdiv((uint32_t)rem, p.fd_w2), hx = rem - hy * W2;
-      const int n = n0 + i, y = y0 + hy - 1, x = hx - 1;
+      int y, x;
+      if constexpr (ST == 1) {
+        y = y0 + hy - 1;
+        x = hx - 1;
+      } else {  // column-split halo: input row 2*y0 - 1 + hy, padded column 2*hx or 2*(hx - hwh) + 1
+        y = 2 * y0 + hy - 1;
+        x = hx < p.hwh ? 2 * hx - 1 : (hx < 2 * p.hwh ? 2 * (hx - p.hwh) : -1);
+      }
+      const int n = n0 + i;
       if (n < p.N && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W)
         off = (uint32_t)((((n * p.H + y) * p.W + x) * p.Cin + (pc ^ hswz(hr)) * 8) * 2);
     }
@@ -155,15 +180,15 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   // ---- B fragments: halo row of each of this lane's pixels (tap (0,0))
   const int wr = wave / WC, wc = wave % WC;
   const int arow0 = wr * (BM / WR), bcol0 = wc * (BN / WC);
-  const int spx = p.rows * p.W;  // pixels per image slice
-  const int fpx = frag_pixel(lane & 15, p.W);
+  const int spx = p.rows * p.Wo;  // pixels per image slice
+  const int fpx = ST == 1 ? frag_pixel(lane & 15, p.W) : (lane & 15);
   int hbr[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int l = bcol0 + j * 16 + fpx;
     const int i = (int)fdiv((uint32_t)l, p.fd_spx), rem = l - i * spx;
-    const int y = (int)fdiv((uint32_t)rem, p.fd_w), x = rem - y * p.W;
-    hbr[j] = i * p.hb + y * W2 + x;
+    const int y = (int)fdiv((uint32_t)rem, p.fd_w), x = rem - y * p.Wo;
+    hbr[j] = i * p.hb + y * (ST * W2) + x;
   }
 
   f32x4 acc[FM][FN];
@@ -181,7 +206,8 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int row = hbr[j] + (t / 3) * W2 + (t % 3);
+      const int ts = t % 3;
+      const int row = hbr[j] + (t / 3) * W2 + (ST == 1 ? ts : (ts & 1) * p.hwh + (ts >> 1));
       boff[t][j] = (uint32_t)(row * 128 + (((lane >> 4) ^ hswz(row)) << 4));
     }
   typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
@@ -230,6 +256,37 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     }
   };
 
+  f32x4 acc2[SC ? FM : 1][SC ? FN : 1];
+  if constexpr (SC) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // SC: the shortcut's weight chunk cc (rows a0.., the W row-image swizzle) into its slot
+  auto stage_sc = [&](int cc) {
+#pragma unroll
+    for (int j = 0; j < NIW; ++j) {
+      const int row = (wave + 4 * j) * 8 + lrow;
+      glds16(p.wsc + (a0 + row) * p.C + cc * 64 + (pc ^ rowswz(row)) * 8, scbase + (wave + 4 * j) * 1024);
+    }
+  };
+  auto compute_sc = [&](const char* hbuf) {  // centre tap (t = 4): the same B fragments, the W_sc chunk
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = *(const lds_bf16x8*)(hbuf + (boff[4][j] ^ (uint32_t)(ks * 64)));
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = frag_row(scbase, arow0 + i * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc2[i][j], 0, 0, 0);
+    }
+  };
+
   // ---- main loop: chunk pairs x 9 unrolled taps. Weights: a WS-slot ring; step (c, tap) reads slot
   // (c + tap) & 1 (WS = 2; 9 is odd) or tap % 3 (WS = 3; 9 = 3 x 3) -- static after the unrolling.
   // WS = 2: the next step's weights are issued right before this step's MFMAs and waited for with
@@ -265,6 +322,11 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
         if constexpr (WS == 3) {  // weights of step + 2 into the slot step - 1 used
           if (tap + 2 <= 8) stage_w(wbase + ((tap + 2) % 3) * WBYTES, c0 + c, tap + 2);
           else if (c + 1 < p.nchunk) stage_w(wbase + ((tap + 2) % 3) * WBYTES, c0 + c + 1, tap + 2 - 9);
+          // SC: W_sc chunk c issued right after the centre tap's weights (step + 2 = (c, 4)): it is older
+          // than the step-(c, 5) weights, so the centre step's counted vmcnt(NIW) covers it
+          if constexpr (SC) {
+            if (tap == 2) stage_sc(c0 + c);
+          }
         } else {
           const int par = (half + tap) & 1;
           if (tap < 8) stage_w(wbase + (par ^ 1) * WBYTES, c0 + c, tap + 1);
@@ -277,6 +339,9 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
           }
         }
         compute(hbuf, wbase + (WS == 3 ? (tap % 3) : ((half + tap) & 1)) * WBYTES, tap);
+        if constexpr (SC) {
+          if (tap == 4) compute_sc(hbuf);
+        }
         if (NHB == 1 && tap == 8 && c + 1 < p.nchunk) {  // every wave is done with the halo: refill it
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
@@ -303,60 +368,68 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     }
   } else if constexpr (MODE == 0) {
     float* red = (float*)smem;  // [WC][BM][2]
-    const bool want_stats = p.stats != nullptr;
+    auto epi_fwd = [&](f32x4 (&A)[SC ? FM : 1][SC ? FN : 1], f32x4 (&B)[FM][FN], bool second, u16* outp, double* stp) {
+      const bool want_stats = stp != nullptr;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int chl = arow0 + i * 16 + rq;
-      const int ch = a0 + chl;
-      float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < FM; ++i) {
+        const int chl = arow0 + i * 16 + rq;
+        const int ch = a0 + chl;
+        float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int pix = px0 + bcol0 + j * 16 + cl;
-        float v[4];
+        for (int j = 0; j < FN; ++j) {
+          const int pix = px0 + bcol0 + j * 16 + cl;
+          const f32x4 a = second ? A[SC ? i : 0][SC ? j : 0] : B[i][j];
+          float v[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = round_bf(acc[i][j][t]);
-        if (pix < M) {
+          for (int t = 0; t < 4; ++t) v[t] = round_bf(a[t]);
+          if (pix < M) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              s4[t] += v[t];
+              q4[t] += v[t] * v[t];
+            }
+            uint2 wv;
+            wv.x = pack_bf2(v[0], v[1]);
+            wv.y = pack_bf2(v[2], v[3]);
+            *(uint2*)(outp + (size_t)pix * p.Cout + ch) = wv;
+          }
+        }
+        if (want_stats) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            s4[t] += v[t];
-            q4[t] += v[t] * v[t];
+            s4[t] = row16_sum(s4[t]);
+            q4[t] = row16_sum(q4[t]);
           }
-          uint2 wv;
-          wv.x = pack_bf2(v[0], v[1]);
-          wv.y = pack_bf2(v[2], v[3]);
-          *(uint2*)(p.out + (size_t)pix * p.Cout + ch) = wv;
+          if ((lane & 15) == 0) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              red[(wc * BM + chl + t) * 2 + 0] = s4[t];
+              red[(wc * BM + chl + t) * 2 + 1] = q4[t];
+            }
+          }
         }
       }
       if (want_stats) {
+        __syncthreads();
+        if ((int)threadIdx.x < BM) {
+          float s = 0.f, q = 0.f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          s4[t] = row16_sum(s4[t]);
-          q4[t] = row16_sum(q4[t]);
-        }
-        if ((lane & 15) == 0) {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            red[(wc * BM + chl + t) * 2 + 0] = s4[t];
-            red[(wc * BM + chl + t) * 2 + 1] = q4[t];
+          for (int w = 0; w < WC; ++w) {
+            s += red[(w * BM + threadIdx.x) * 2 + 0];
+            q += red[(w * BM + threadIdx.x) * 2 + 1];
           }
+          double* st = stp + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * p.Cout;
+          unsafeAtomicAdd(st + a0 + threadIdx.x, (double)s);
+          unsafeAtomicAdd(st + p.Cout + a0 + threadIdx.x, (double)q);
         }
       }
+    };
+    epi_fwd(acc2, acc, false, p.out, p.stats);
+    if constexpr (SC) {
+      __syncthreads();  // the statistics staging area is reused
+      epi_fwd(acc2, acc, true, p.out2, p.stats2);
     }
-    if (want_stats) {
-      __syncthreads();
-      if ((int)threadIdx.x < BM) {
-        float s = 0.f, q = 0.f;
-#pragma unroll
-        for (int w = 0; w < WC; ++w) {
-          s += red[(w * BM + threadIdx.x) * 2 + 0];
-          q += red[(w * BM + threadIdx.x) * 2 + 1];
-        }
-        double* st = p.stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * p.Cout;
-        unsafeAtomicAdd(st + a0 + threadIdx.x, (double)s);
-        unsafeAtomicAdd(st + p.Cout + a0 + threadIdx.x, (double)q);
-      }
-    }
-  } else if (p.bnb.ym != nullptr) {  // DGRAD (+ residual) -> dz = bf16(dx) * [y > 0] and BN sums
+  } else if (bnb_on(p.bnb)) {  // DGRAD (+ residual) -> dz = bf16(dx) * [y > 0] and BN sums
     const bool dual = p.bnb.x2 != nullptr;
     const bool has_res = p.res != nullptr;
     float* red = (float*)smem;  // [WC][BM][3]
@@ -372,7 +445,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
         const int pix = px0 + bcol0 + j * 16 + cl;
         const size_t o = (size_t)(pix < M ? pix : 0) * p.Cout + ch;
         rr[j] = has_res ? *(const uint2*)(p.res + o) : uint2{0u, 0u};
-        yy[j] = *(const uint2*)(p.bnb.ym + o);
+        yy[j] = p.bnb.mb ? bnb_bits_as_y(p.bnb.mb, o) : *(const uint2*)(p.bnb.ym + o);
         xx[j] = *(const uint2*)(p.bnb.x1 + o);
         x2[j] = dual ? *(const uint2*)(p.bnb.x2 + o) : uint2{0u, 0u};
       }
@@ -440,69 +513,107 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
 
 // ---------------------------------------------------------------- host side
 struct HaloCfg {
-  int bm, bn, nhb, hcap;
+  int bm, bn, nhb, hcap, st;
 };
-// Template instances (launch_halo below). LDS: NHB * HCAP * 128 + 2 * BM * 128 bytes.
+// Template instances (launch_halo below). LDS: NHB * HCAP * 128 + WS * BM * 128 (+ BM * 128 with SC).
 static const HaloCfg kHaloCfgs[] = {
-    {64, 256, 1, 416},   // 0: 70 KB, 2 WG/CU: big images / many tiles
-    {64, 128, 2, 288},   // 1: 90 KB: double-buffered halo, no chunk bubbles
-    {64, 128, 1, 288},   // 2: 53 KB, 3 WG/CU
-    {128, 256, 1, 416},  // 3: 86 KB: wide output-channel tiles
-    {128, 128, 1, 288},  // 4: 69 KB, 2 WG/CU: 64x64 per wave
-    {128, 128, 2, 288},  // 5: 106 KB: 64x64 per wave, double-buffered halo
-    {64, 128, 2, 224},   // 6: 72 KB, 2 WG/CU: double-buffered halo of up to 224 rows (2 images of 8x8)
-    {64, 64, 2, 160},    // 7: 56 KB: double-buffered halo of up to 160 rows (4 images of 4x4)
+    {64, 256, 1, 416, 1},   // 0: 70 KB, 2 WG/CU: big images / many tiles
+    {64, 128, 2, 288, 1},   // 1: 90 KB: double-buffered halo, no chunk bubbles
+    {64, 128, 1, 288, 1},   // 2: 53 KB, 3 WG/CU
+    {128, 256, 1, 416, 1},  // 3: 86 KB: wide output-channel tiles
+    {128, 128, 1, 288, 1},  // 4: 69 KB, 2 WG/CU: 64x64 per wave
+    {128, 128, 2, 288, 1},  // 5: 106 KB: 64x64 per wave, double-buffered halo
+    {64, 128, 2, 224, 1},   // 6: 72 KB, 2 WG/CU: double-buffered halo of up to 224 rows (2 images of 8x8)
+    {64, 64, 2, 160, 1},    // 7: 56 KB: double-buffered halo of up to 160 rows (4 images of 4x4)
+    // stride 2 (FWD, column-split halo; the 64-pixel tile of a 16-wide output needs 9 x 34 input halo rows)
+    {64, 64, 1, 384, 2},    // 8: 80 KB with the shortcut slot, 2 WG/CU, 32x32 per wave
+    {64, 128, 1, 768, 2},   // 9: 128 KB, 1 WG/CU, 64x32 per wave
+    {128, 64, 1, 384, 2},   // 10: 112 KB, 1 WG/CU, 64x32 per wave
 };
 constexpr int kNumHaloCfgs = (int)(sizeof(kHaloCfgs) / sizeof(kHaloCfgs[0]));
+constexpr int kFirstS2Cfg = 8;
 
-static bool halo_geometry(const ConvShape& s, int bn, int hcap, int& rows, int& imgs, int& nh) {
-  const int hw = s.H * s.W;
+// Halo row pitch of the column-split stride-2 layout: 2 (Wo + 1) input columns, +2 where a 16-pixel
+// fragment spans output rows of width Wo = 8 mod 16 (the +1-output-row offset 2 * pitch must be 8 mod
+// 16 rows there for the ds_read_b128 lane groups to hit distinct bank slots; tools/halo_banks.py).
+static int s2_pitch(int wo) { return 2 * (wo + 1) + ((wo % 16) == 8 ? 2 : 0); }
+
+// Output tile geometry: `rows` output rows of one image slice or `imgs` whole images per tile, the
+// halo rows per slice (hb) and per tile (nh), the halo row pitch and (stride 2) the split point hwh.
+struct HaloGeom {
+  int rows, imgs, hb, nh, pitch, hwh, ho, wo;
+};
+static bool halo_geometry(const ConvShape& s, int st, int bn, int hcap, HaloGeom& g) {
+  g.ho = s.H / st;
+  g.wo = s.W / st;
+  const int hw = g.ho * g.wo;
   if (hw >= bn) {
-    if (bn % s.W) return false;
-    rows = bn / s.W;
-    if (s.H % rows) return false;
-    imgs = 1;
+    if (bn % g.wo) return false;
+    g.rows = bn / g.wo;
+    if (g.ho % g.rows) return false;
+    g.imgs = 1;
   } else {
     if (bn % hw) return false;
-    imgs = bn / hw;
-    rows = s.H;
+    g.imgs = bn / hw;
+    g.rows = g.ho;
   }
-  nh = imgs * (rows + 2) * (s.W + 2);
-  return nh <= hcap;
+  if (st == 1) {
+    g.pitch = s.W + 2;
+    g.hwh = 0;
+    g.hb = (g.rows + 2) * g.pitch;
+  } else {
+    g.pitch = s2_pitch(g.wo);
+    g.hwh = g.wo + 1;
+    g.hb = (2 * g.rows + 1) * g.pitch;
+  }
+  g.nh = g.imgs * g.hb;
+  return g.nh <= hcap;
 }
 
-static bool halo_shape_ok(const ConvShape& s) {
-  return s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.C % 64 == 0 && s.K % 64 == 0 &&
-         (uint64_t)s.N * s.H * s.W * std::max(s.C, s.K) * 2 < (1ull << 31);
+static bool halo_shape_ok(const ConvShape& s, int st) {
+  if (!(s.R == 3 && s.S == 3 && s.stride == st && s.pad == 1 && s.C % 64 == 0 && s.K % 64 == 0)) return false;
+  if (st == 2 && (s.H % 2 || s.W % 2)) return false;
+  return (uint64_t)s.N * s.H * s.W * std::max(s.C, s.K) * 2 < (1ull << 31);
 }
 
-static int halo_tiles_b(const ConvShape& s, int rows, int imgs) {
-  return imgs == 1 ? s.N * (s.H / rows) : (s.N + imgs - 1) / imgs;
+static int halo_tiles_b(const ConvShape& s, const HaloGeom& g) {
+  return g.imgs == 1 ? s.N * (g.ho / g.rows) : (s.N + g.imgs - 1) / g.imgs;
 }
 
 static bool cfg_fits(const ConvShape& s, int cfg, int cout) {
-  int rows, imgs, nh;
+  HaloGeom g;
   const HaloCfg& c = kHaloCfgs[cfg];
-  return cout % c.bm == 0 && halo_geometry(s, c.bn, c.hcap, rows, imgs, nh);
+  return cout % c.bm == 0 && halo_geometry(s, c.st, c.bn, c.hcap, g);
 }
 
 // Plan for pass `mode` (CONV_FWD / CONV_DGRAD): configuration (-1: not applicable / disabled) and
 // split-K factor over the reduction chunks.
 HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
   HaloPlan hp{-1, 1};
+  if (s.stride == 2) {  // FWD only, column-split halo (option halo_s2: 0 off, 1 auto, 2+k force config 8+k)
+    const int o2 = option_get(OPT_HALO_S2);
+    if (o2 == 0 || mode != CONV_FWD || !halo_shape_ok(s, 2)) return hp;
+    // auto: only where the reduction has >= 2 chunks -- with one 64-channel chunk (layer2.0.conv1) the whole
+    // halo must land before the first MFMA and the implicit GEMM's per-tap pipeline is faster (20 vs 28 us
+    // at B=256; layer3 20.7 -> 19.6, layer4 22.2 -> 17.1, the shortcut-fused launches 29.2 -> 24.1 / 20.3)
+    if (o2 == 1 && s.C < 128) return hp;
+    const int cfg = o2 >= 2 ? std::min(kFirstS2Cfg + o2 - 2, kNumHaloCfgs - 1) : kFirstS2Cfg;
+    if (cfg_fits(s, cfg, s.K)) hp.cfg = cfg;
+    return hp;  // no split-K: the shortcut fusion and the BN statistics live in the epilogue
+  }
   const int opt = option_get(OPT_HALO_CONV);
-  if (opt == 0 || !halo_shape_ok(s)) return hp;
+  if (opt == 0 || !halo_shape_ok(s, 1)) return hp;
   const int cout = mode == CONV_FWD ? s.K : s.C;
   const int cin = mode == CONV_FWD ? s.C : s.K;
   const int nchunk = cin / 64;
   auto tiles = [&](int cfg) {
-    int rows = 1, imgs = 1, nh = 0;
+    HaloGeom g;
     const HaloCfg& c = kHaloCfgs[cfg];
-    halo_geometry(s, c.bn, c.hcap, rows, imgs, nh);
-    return halo_tiles_b(s, rows, imgs) * (cout / c.bm);
+    halo_geometry(s, c.st, c.bn, c.hcap, g);
+    return halo_tiles_b(s, g) * (cout / c.bm);
   };
   if (opt >= 2) {  // forced configuration opt-2 (tuning)
-    const int cfg = std::min(opt - 2, kNumHaloCfgs - 1);
+    const int cfg = std::min(opt - 2, kFirstS2Cfg - 1);
     if (!cfg_fits(s, cfg, cout)) return hp;
     hp.cfg = cfg;
   } else {
@@ -554,39 +665,59 @@ static int launch_halo(const HConvParams& p, int cfg, dim3 grid, hipStream_t st)
   return launch_halo_ws<MODE, 2>(p, cfg, grid, st);
 }
 
+// stride-2 forward instances (3-slot weight ring), with or without the fused shortcut
+template <bool SC>
+static int launch_halo_s2(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
+  switch (cfg) {
+    case 8: hipLaunchKernelGGL((conv_halo_kernel<0, 64, 64, 2, 2, 1, 384, 3, 2, SC>), grid, dim3(256), 0, st, p); break;
+    case 9: hipLaunchKernelGGL((conv_halo_kernel<0, 64, 128, 1, 4, 1, 768, 3, 2, SC>), grid, dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((conv_halo_kernel<0, 128, 64, 2, 2, 1, 384, 3, 2, SC>), grid, dim3(256), 0, st, p); break;
+  }
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
               const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
-              const BnbArgs* bnb) {
-  DTC_CHECK_ARG(hp.cfg >= 0 && hp.cfg < kNumHaloCfgs && halo_shape_ok(s) && (mode == CONV_FWD || mode == CONV_DGRAD),
-                "conv_halo: unsupported shape / configuration");
+              const BnbArgs* bnb, const u16* wsc, u16* out2, double* stats2) {
+  DTC_CHECK_ARG(hp.cfg >= 0 && hp.cfg < kNumHaloCfgs && (mode == CONV_FWD || mode == CONV_DGRAD),
+                "conv_halo: unsupported configuration");
   const HaloCfg& c = kHaloCfgs[hp.cfg];
+  DTC_CHECK_ARG(halo_shape_ok(s, c.st) && (c.st == 1 || mode == CONV_FWD), "conv_halo: unsupported shape / pass");
+  DTC_CHECK_ARG(wsc == nullptr || (c.st == 2 && out2 != nullptr), "conv_halo: the shortcut fusion is stride-2 FWD");
   HConvParams p{};
   p.src = src; p.w = w; p.out = out; p.res = res; p.stats = stats;
+  p.wsc = wsc; p.out2 = out2; p.stats2 = stats2;
   p.N = s.N; p.H = s.H; p.W = s.W; p.C = s.C;
   p.Cin = mode == CONV_FWD ? s.C : s.K;
   p.Cout = mode == CONV_FWD ? s.K : s.C;
   DTC_CHECK_ARG(p.Cout % c.bm == 0, "conv_halo: output channels %d not a multiple of %d", p.Cout, c.bm);
-  DTC_CHECK_ARG(halo_geometry(s, c.bn, c.hcap, p.rows, p.imgs, p.nh), "conv_halo: geometry does not fit config %d",
-                hp.cfg);
-  const int M = s.N * s.H * s.W;
+  HaloGeom g;
+  DTC_CHECK_ARG(halo_geometry(s, c.st, c.bn, c.hcap, g), "conv_halo: geometry does not fit config %d", hp.cfg);
+  p.rows = g.rows; p.imgs = g.imgs; p.nh = g.nh; p.hb = g.hb;
+  p.Ho = g.ho; p.Wo = g.wo; p.pitch = g.pitch; p.hwh = g.hwh;
+  const int M = s.N * g.ho * g.wo;
   int split = hp.split;
   if (split > 1 && (slab == nullptr || slab_bytes < (size_t)split * M * p.Cout * 4)) split = 1;
   DTC_CHECK_ARG((p.Cin / 64) % split == 0, "conv_halo: split %d does not divide the reduction", split);
+  DTC_CHECK_ARG(split == 1 || c.st == 1, "conv_halo: stride 2 has no split-K");
   p.slab = split > 1 ? slab : nullptr;
-  p.src_bytes = (uint32_t)((uint64_t)M * p.Cin * 2);
-  p.hb = (p.rows + 2) * (s.W + 2);
+  p.src_bytes = (uint32_t)((uint64_t)s.N * s.H * s.W * p.Cin * 2);
   p.nhi = (p.nh + 31) / 32;
-  p.tiles_y = s.H / p.rows;
+  p.tiles_y = g.ho / p.rows;
   p.tiles_a = p.Cout / c.bm;
   p.nchunk = p.Cin / 64 / split;
   p.xcd_remap = option_get(OPT_XCD_REMAP);
   p.fd_hb = make_fastdiv(p.hb);
-  p.fd_w2 = make_fastdiv(s.W + 2);
-  p.fd_spx = make_fastdiv(p.rows * s.W);
-  p.fd_w = make_fastdiv(s.W);
+  p.fd_w2 = make_fastdiv(p.pitch);
+  p.fd_spx = make_fastdiv(p.rows * g.wo);
+  p.fd_w = make_fastdiv(g.wo);
   p.ts = ts;
   if (bnb != nullptr && split <= 1) p.bnb = *bnb;  // (split-K: the reduction kernel applies it)
-  const dim3 grid(halo_tiles_b(s, p.rows, p.imgs) * p.tiles_a, split);
+  const dim3 grid(halo_tiles_b(s, g) * p.tiles_a, split);
+  if (c.st == 2) {
+    return wsc ? launch_halo_s2<true>(p, hp.cfg, grid, st) : launch_halo_s2<false>(p, hp.cfg, grid, st);
+  }
   DTC_TRY(mode == CONV_FWD ? launch_halo<0>(p, hp.cfg, grid, st) : launch_halo<1>(p, hp.cfg, grid, st));
   if (split > 1) return splitk_reduce(slab, split, M, p.Cout, out, res, stats, st, ts, bnb);
   return 0;

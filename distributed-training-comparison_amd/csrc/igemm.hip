@@ -57,6 +57,12 @@ struct IGemmParams {
   u16* out2;         // shortcut output (NPQK)
   double* stats2;    // its BN statistic slots
   int kt_c0, kt_c1;
+  // DGRAD classes, shortcut fused (sc_kt > 0): the 1x1 stride-2 shortcut's input gradient is nonzero only
+  // at the (even, even) pixels, where it is dsc[u][v] . W_sc -- a 1x1 GEMM on the class-(0, 0) grid with
+  // the same reduction length as that class's single tap. Class (0, 0) runs sc_kt extra reduction steps
+  // reading dsc (src0b) and W_sc^T (src1b), so dx there is one sum over [dc1 | dsc] x [W(1,1) ; W_sc].
+  const u16* src0b;  // dsc (NPQK)
+  int sc_kt;
 };
 
 template <int MODE, int BM, int BN, int WR, int WC, bool SLAB, int NSTAGE, bool SC = false>
@@ -109,8 +115,10 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
       dr = (cls_ph + p.pad - r0) >> 1;
       dsh = (cls_pw + p.pad - s0) >> 1;
       num_kt = Rdim * Sdim * (int)p.fd_cc.d;
+      if (cls_ph == 0 && cls_pw == 0) num_kt += p.sc_kt;  // + the fused shortcut's steps (kt >= kt_sc0)
     }
   }
+  const int kt_sc0 = num_kt - ((MODE == MODE_DGRAD && cls_ph == 0 && cls_pw == 0) ? p.sc_kt : 0);
   const int kt_begin = blockIdx.y * p.kt_per_split;
   const int kt_end = min(num_kt, kt_begin + p.kt_per_split);
   const int lrow = lane >> 3, pc = lane & 7;
@@ -129,6 +137,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
   int wl_ih[2] = {0, 0}, wl_row[2] = {0, 0};
   bool wl_iwok[2] = {false, false};
 
+  int offAs[MODE == MODE_DGRAD ? NIA : 1];  // DGRAD: the W_sc^T tr image (row stride C)
   if constexpr (MODE == MODE_FWD) {
 #pragma unroll
     for (int j = 0; j < NIA; ++j) {
@@ -161,6 +170,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
       const int img = ia >> 3, rowin = (ia & 7) * 8 + lrow;
       const int lc = pc ^ trswz(rowin);
       offA[j] = rowin * p.RSC + a0 + img * 64 + lc * 8;
+      offAs[j] = rowin * p.C + a0 + img * 64 + lc * 8;
     }
 #pragma unroll
     for (int j = 0; j < NIB; ++j) {
@@ -247,6 +257,19 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
         glds16(src, sb + A_BYTES + (wave + 4 * j) * 1024);
       }
     } else if constexpr (MODE == MODE_DGRAD) {
+      if (kt >= kt_sc0) {  // fused shortcut step (class (0, 0)): W_sc^T chunk x dsc at the class pixel
+        const int cs = kt - kt_sc0;
+#pragma unroll
+        for (int j = 0; j < NIA; ++j)
+          glds16(p.src1b + offAs[j] + (int64_t)cs * 64 * p.C, sb + (wave + 4 * j) * 1024);
+#pragma unroll
+        for (int j = 0; j < NIB; ++j) {
+          const bool ok = ((unsigned)hB[j] < (unsigned)p.P) && ((unsigned)wB[j] < (unsigned)p.Q);
+          const u16* src = ok ? (p.src0b + ((baseB[j] + hB[j]) * p.Q + wB[j]) * p.K + cs * 64 + colB[j]) : zp;
+          glds16(src, sb + A_BYTES + (wave + 4 * j) * 1024);
+        }
+        return;
+      }
       const int wr_ = r0 + tstep * r, ws_ = s0 + tstep * s;  // filter tap
       const int64_t wadd = (int64_t)cc * 64 * p.RSC + (wr_ * p.S + ws_) * p.C;
 #pragma unroll
@@ -599,7 +622,13 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
       }
       if constexpr (BNB) {
         float yv[8], xv[8], xw[8];
-        unpack8(*(const uint4*)(bnb.ym + o), yv);
+        if (bnb.mb) {  // mask bits: one byte per 8 channels (o % 8 == 0)
+          const uint32_t by = bnb.mb[o >> 3];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) yv[k] = ((by >> k) & 1u) ? 1.f : 0.f;
+        } else {
+          unpack8(*(const uint4*)(bnb.ym + o), yv);
+        }
         unpack8(*(const uint4*)(bnb.x1 + o), xv);
         if constexpr (DUAL) unpack8(*(const uint4*)(bnb.x2 + o), xw);
 #pragma unroll
@@ -782,6 +811,12 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * M * A * 4 : 0;
     pl.slab_bytes = std::max(pl.slab_bytes, conv_halo_slab_bytes(s, mode));
     pl.num_kt = num_kt;
+  } else if (const int s2 = wgrad_s2_splits(s)) {  // stride-2 column-split halo kernel (wgrad_halo.hip)
+    pl.bm = 576;
+    pl.bn = 64;
+    pl.splits = s2;
+    pl.num_kt = s.N * P * Q / 64;
+    pl.slab_bytes = conv_wgrad_s2_slab_bytes(s);
   } else if (const int hs = wgrad_halo_splits(s)) {  // halo-tiled kernel (wgrad_halo.hip)
     pl.bm = 576;
     pl.bn = 64;
@@ -846,7 +881,8 @@ bool conv_fwd_sc_ok(const ConvShape& s, const ConvShape& sc) {
   if (!(s.R == 3 && s.S == 3 && s.stride == 2 && s.pad == 1 && sc.R == 1 && sc.S == 1 && sc.stride == 2 &&
         sc.pad == 0 && sc.N == s.N && sc.H == s.H && sc.W == s.W && sc.C == s.C && sc.K == s.K && s.C % 64 == 0))
     return false;
-  if (conv_c64_ok(s) || conv_halo_plan(s, CONV_FWD).cfg >= 0) return false;
+  if (conv_c64_ok(s)) return false;
+  if (conv_halo_plan(s, CONV_FWD).cfg >= 0) return s.stride == 2;  // column-split halo kernel with SC
   const ConvPlan pl = plan_conv(s, CONV_FWD);
   // sc_fuse=1: 64x64-tile plans of at most 512 workgroups (layer4 at B=256: 35.3 us fused vs 8.2 + 31.1
   // separate); 2: every 64x64 plan (layer3: 35.6 vs 9.7 + 23.0 -- the shortcut's own 1024-workgroup launch
@@ -861,6 +897,11 @@ bool conv_fwd_sc_ok(const ConvShape& s, const ConvShape& sc) {
 int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16* w, u16* y, double* stats,
                 const u16* wsc, u16* ysc, double* stats_sc, hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(conv_fwd_sc_ok(s, sc) && x && w && y && wsc && ysc, "conv_fwd_sc: unsupported shapes");
+  {
+    const HaloPlan hp = conv_halo_plan(s, CONV_FWD);
+    if (hp.cfg >= 0)
+      return conv_halo(s, CONV_FWD, hp, x, w, y, nullptr, stats, nullptr, 0, st, ts, nullptr, wsc, ysc, stats_sc);
+  }
   IGemmParams p{};
   p.ts = ts;
   DTC_TRY(fill_common(p, s));
@@ -882,17 +923,21 @@ int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16
 
 // The BN-backward pass after a dgrad whose kernel has no fused epilogue for it (in place on dx).
 static int bnb_after(const BnbArgs* bnb, u16* dx, int64_t M, int C, hipStream_t st) {
-  if (bnb == nullptr || bnb->ym == nullptr) return 0;
+  if (bnb == nullptr || !bnb_on(*bnb)) return 0;
+  if (bnb->mb)  // mask bits: the sums only (dx stays the raw gradient; the BN apply masks it)
+    return bn_bwd_reduce_mask(dx, bnb->mb, bnb->x1, bnb->mean1, bnb->invstd1, bnb->acc1, bnb->x2, bnb->mean2,
+                              bnb->invstd2, bnb->acc2, M, C, st);
   return bn_bwd_reduce(dx, bnb->ym, bnb->x1, bnb->mean1, bnb->invstd1, bnb->acc1, bnb->x2, bnb->mean2, bnb->invstd2,
                        bnb->acc2, dx, M, C, st);
 }
 
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
                size_t slab_bytes, hipStream_t st, u64* ts, const BnbArgs* bnb, int res_compact) {
-  if (bnb != nullptr && bnb->ym == nullptr) bnb = nullptr;
+  if (bnb != nullptr && !bnb_on(*bnb)) bnb = nullptr;
   DTC_CHECK_ARG(!res_compact || (res && dgrad_class_mode(s) && !conv_c64_ok(s)),
                 "conv_dgrad: a compact residual needs the stride-2 parity-class path");
-  const int fz = bnb != nullptr ? option_get(OPT_BNB_FUSE) : 0;  // bit 0: c64, 1: halo, 2: split-K reduce
+  // bit 0: c64, 1: halo, 2: split-K reduce; mask-bit sources (bnb->mb, option bnb_mask) fuse everywhere
+  const int fz = bnb != nullptr ? (bnb->mb ? 7 : option_get(OPT_BNB_FUSE)) : 0;
   const HaloPlan hp = conv_c64_ok(s) ? HaloPlan{-1, 0} : conv_halo_plan(s, CONV_DGRAD);
   const int kind = conv_c64_ok(s) ? 1 : (hp.cfg >= 0 ? 2 : 4);
   const bool split_path = kind != 1 && (kind == 4 || hp.split > 1);  // the epilogue is splitk_reduce's
@@ -944,6 +989,36 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
   return bnb_after(bnb, dx, p.M, s.C, st);
 }
 
+// conv1 (3x3 stride 2) of a projection block and its 1x1 stride-2 shortcut: dx = dgrad(dc1, W1) +
+// dgrad(dsc, W_sc) in ONE parity-class launch (the shortcut's term lives at class (0, 0) only, as extra
+// reduction steps there: no separate shortcut dgrad launch and no compact residual pass).
+bool conv_dgrad_sc_ok(const ConvShape& s) { return dgrad_class_ok(s) && s.R == 3 && s.pad == 1 && option_get(OPT_DGRAD_SCF) != 0; }
+int conv_dgrad_sc(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* dsc, const u16* wsc,
+                  hipStream_t st, u64* ts, const BnbArgs* bnb) {
+  DTC_CHECK_ARG(conv_dgrad_sc_ok(s) && dy && w && dx && dsc && wsc, "conv_dgrad_sc: unsupported geometry / args");
+  if (bnb != nullptr && !bnb_on(*bnb)) bnb = nullptr;
+  IGemmParams p{};
+  p.ts = ts;
+  DTC_TRY(fill_common(p, s));
+  ConvPlan pl = plan_conv(s, CONV_DGRAD);
+  p.src0 = dy; p.src1 = w; p.out = dx; p.res = nullptr;
+  p.src0b = dsc; p.src1b = wsc; p.sc_kt = s.K / 64;
+  p.fd_cc = make_fastdiv(s.K / 64);
+  p.num_kt = pl.num_kt;
+  p.tiles_a = s.C / pl.bm;
+  p.cls = 1;
+  p.cls_order = option_get(OPT_DGRAD_CLASS_ORDER);
+  p.M = s.N * (s.H / 2) * (s.W / 2);
+  p.fd_q = make_fastdiv(s.W / 2);
+  p.fd_pq = make_fastdiv((s.H / 2) * (s.W / 2));
+  p.kt_per_split = p.num_kt;
+  const int tb = ceil_div(p.M, pl.bn);
+  if (pl.bn == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 64, 2, 2, false>(p, tb, 1, st, 4)));
+  else if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 256, 1, 4, false>(p, tb, 1, st, 4)));
+  else DTC_TRY((launch_igemm<MODE_DGRAD, 128, 128, 2, 2, false>(p, tb, 1, st, 4)));
+  return bnb_after(bnb, dx, (int64_t)s.N * s.H * s.W, s.C, st);
+}
+
 static int launch_wgrad_reduce(const float* slab, int splits, int K, int RSC, int ncols, int ldo, float scale,
                                const WgOuts& outs, int nprob, size_t prob_stride, hipStream_t st, u64* ts) {
   const size_t nv = (size_t)K * RSC / 4;
@@ -966,6 +1041,9 @@ static int launch_wgrad_reduce(const float* slab, int splits, int K, int RSC, in
 
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
                float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
+  if (wgrad_s2_splits(s) > 0 && (dw_cols <= 0 || dw_cols == 9 * s.C) && (dw_ld <= 0 || dw_ld == 9 * s.C) &&
+      slab_bytes >= conv_wgrad_s2_slab_bytes(s))
+    return conv_wgrad_s2(s, x, dy, nullptr, dw, nullptr, scale, slab, slab_bytes, st, ts);
   IGemmParams p{};
   p.ts = ts;
   DTC_TRY(fill_common(p, s));
@@ -1035,7 +1113,7 @@ int conv_wgrad_batch(const ConvShape& s, int nprob, const u16* const* x, const u
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
                   hipStream_t st, u64* ts, const BnbArgs* bnb) {
   DTC_CHECK_ARG(Nc % 8 == 0 && Nc <= 2048, "splitk_reduce: channels %d", Nc);
-  const bool fuse = bnb != nullptr && bnb->ym != nullptr;
+  const bool fuse = bnb != nullptr && bnb_on(*bnb);
   DTC_CHECK_ARG(!fuse || (stats == nullptr && bnb->x1 && bnb->mean1 && bnb->invstd1 && bnb->acc1 &&
                           (!bnb->x2 || (bnb->mean2 && bnb->invstd2 && bnb->acc2))),
                 "splitk_reduce: BN-backward epilogue args");

@@ -77,6 +77,14 @@ enum {
   OPT_STEM_RECOMPUTE = 43, // training forward: 1 = stem statistics pass + recompute pass with the BN apply fused
   OPT_STEM_WLDS = 44,      // stem forward: 1 (default) = weight staged in LDS by coalesced loads, not per-lane
                            // 2-B gathers (stem_bench: 18.7 -> 16.1 us; +1.1% interleaved A/B)
+  OPT_HALO_S2 = 45,        // stride-2 3x3 FWD on the column-split halo kernel (conv_halo.hip; + the fused 1x1
+                           // shortcut): 0 off (implicit GEMM), 1 auto, 2+k force configuration 8+k (tuning)
+  OPT_WGRAD_S2 = 46,       // stride-2 3x3 weight gradient (+ the fused 1x1 shortcut's) on the column-split
+                           // halo kernel (wgrad_halo.hip): 0 off (implicit GEMM, one tap per workgroup), 1 on
+  OPT_DGRAD_SCF = 47,      // executor: the projection shortcut's dgrad fused into conv1's parity-class dgrad
+                           // (extra reduction steps of class (0, 0); igemm.hip conv_dgrad_sc)
+  OPT_BNB_MASK = 48,       // executor (mask-bit backward): each BN's backward sums accumulated in the epilogue
+                           // of the dgrad producing its gradient, from the ReLU mask bits (no reduction pass)
   OPT_COUNT
 };
 int option_get(int id);
@@ -115,6 +123,11 @@ int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16
 bool dgrad_class_ok(const ConvShape& s);
 // res_compact: res is [N][H/2][W/2][C] (a 1x1 stride-2 shortcut's dx at its only nonzero parity),
 // added at the (even, even) pixels only -- stride-2 parity-class dgrads.
+// dx = dgrad(dy, w) + dgrad_1x1_s2(dsc, wsc) for a projection block's 3x3 stride-2 conv1 and its shortcut
+// in one parity-class launch (dsc [N][H/2][W/2][K], wsc [K][C])
+bool conv_dgrad_sc_ok(const ConvShape& s);
+int conv_dgrad_sc(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* dsc, const u16* wsc,
+                  hipStream_t st, u64* ts = nullptr, const BnbArgs* bnb = nullptr);
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
                size_t slab_bytes, hipStream_t st, u64* ts = nullptr, const BnbArgs* bnb = nullptr,
                int res_compact = 0);
@@ -128,6 +141,13 @@ constexpr int DTC_WG_BATCH = 4;
 int wgrad_halo_splits(const ConvShape& s, int nprob = 1);
 // dw (optional): when the launch uses ONE split its epilogue writes dw[i] = scale * sum directly (no
 // slab, no reduce; *used_splits = 0 tells the caller), else slab[nprob][used][K][9C] as above.
+// 3x3 stride-2 weight gradient (conv1 of a projection block) on the column-split halo kernel, and with
+// dsc != null the block's 1x1 stride-2 shortcut's (dw_sc[k][c] from dsc) in the same launch; split-K over
+// output pixels into slab ([splits][K][9C] then [splits][K][C]) + deterministic reduces.
+int wgrad_s2_splits(const ConvShape& s);  // 0: no plan (option wgrad_s2 off or geometry)
+size_t conv_wgrad_s2_slab_bytes(const ConvShape& s);
+int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* dsc, float* dw, float* dw_sc,
+                  float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* slab, int splits,
                     int* used_splits, hipStream_t st, u64* ts, float* const* dw = nullptr, float scale = 1.f);
 // nprob (<= DTC_WG_BATCH) independent weight gradients of one 3x3 stride-1 geometry in one halo
@@ -148,8 +168,8 @@ struct HaloPlan {
 HaloPlan conv_halo_plan(const ConvShape& s, int mode);
 size_t conv_halo_slab_bytes(const ConvShape& s, int mode);  // fp32 split-K slab the plan needs
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
-              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
-              const BnbArgs* bnb = nullptr);
+              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr,
+              const BnbArgs* bnb = nullptr, const u16* wsc = nullptr, u16* out2 = nullptr, double* stats2 = nullptr);
 // bnb (optional, non-null ym): out = dz = bf16(sum + res) * [ym > 0] and the BN-backward sums of
 // dz into bnb->acc1 (/acc2) -- the work of bn_bwd_reduce on the value the reduction holds.
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,

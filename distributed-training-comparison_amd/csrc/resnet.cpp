@@ -1117,9 +1117,24 @@ static int cap_masked(Net& n, const std::string& name, const u16* dy, size_t mas
   return set_error(DTC_EINVAL, "capture slot %s missing", name.c_str());
 }
 
+// BN-backward sums of the BN(s) whose post-ReLU output gradient a dgrad writes, from the mask bits
+static BnbArgs bnb_mask_of(Net& n, size_t mbits, size_t x1, BNL& b1, size_t x2 = 0, BNL* b2 = nullptr) {
+  BnbArgs a = bnb_of(n, 0, x1, b1, x2, b2);
+  a.ym = nullptr;
+  a.mb = n.at<uint8_t>(mbits);
+  return a;
+}
+
 static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdCtx& cx, hipStream_t st) {
   n.prof_next = Net::PROF_BWD0;
   n.ev_next = 0;
+  // option bnb_mask: each BN's backward sums come from the epilogue of the dgrad that produces its
+  // gradient (conv2's dgrad -> bn1; the next block's conv1 dgrad -> bn2 (+ the projection BN); layer1.0's
+  // conv1 dgrad -> the stem BN), read with the forward's mask bits: no separate reduction pass. That dgrad
+  // stores dz = dy * bit; the mask-bit apply below masks again (idempotent). Not with parity captures,
+  // which record the raw dy.
+  const bool bmf = !n.capture && option_get(OPT_BNB_MASK) != 0;
+  bool sums_ready = false;  // this block's bn2 (+ projection BN) sums were accumulated by the later dgrad
   u16* G[6];
   for (int i = 0; i < 6; ++i) G[i] = n.at<u16>(n.G[i]);
   float* slab = n.at<float>(n.SLAB);
@@ -1144,7 +1159,12 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     DTC_TRY(cap_masked(n, cp + ".dz", G[0], b.MOUT, M, b.Cout, st));
     // out = relu(bn2(c2) + shortcut): sums of dz = dy * [out > 0] (and of the projection BN), then
     // dc2 (and dsc); an identity block also needs dz itself as conv1's dgrad residual: in place in G[0]
-    if (onepass_ok(n, M, b.Cout, b.proj)) {
+    if (sums_ready) {  // the sums are in the slots (bnb_mask). G[0] holds dz, or the raw dy where a
+      // stride-2 class dgrad produced it (sums by a separate mask-bit pass): an identity block's apply
+      // writes dz over it as before (the residual of its conv1 dgrad; idempotent on dz)
+      DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[0], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
+                                b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st, mout, b.proj ? nullptr : G[0]));
+    } else if (onepass_ok(n, M, b.Cout, b.proj)) {
       DTC_TRY(bn_bwd_onepass(n, b.b2, G[0], mout, b.proj ? nullptr : G[0], n.at<u16>(b.C2), dc2,
                              b.proj ? &b.bsc : nullptr, b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st));
     } else {
@@ -1163,6 +1183,8 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     // is zero at three of four parities; conv1's parity-class dgrad adds it at the fourth
     const bool sc_cmp = b.proj && !n.capture && option_get(OPT_SC_COMPACT) != 0 && dgrad_class_ok(b.c1.s);
     const ConvShape sc_dg = sc_cmp ? ConvShape{b.sc.s.N, b.Hout, b.Wout, b.sc.s.C, b.sc.s.K, 1, 1, 1, 0} : b.sc.s;
+    // option dgrad_scf: the shortcut's dgrad as extra reduction steps of conv1's class-(0, 0) dgrad (one launch)
+    const bool dscf = b.proj && !n.capture && !sc_branch && conv_dgrad_sc_ok(b.c1.s);
     if (sc_branch) {  // dx of the shortcut (conv1's dgrad residual) beside conv2's dgrad and BN1's backward
       hipStream_t ss = st;
       DTC_TRY(fork_sc(n, st, &ss));
@@ -1178,10 +1200,16 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     const bool lazy = option_get(OPT_FORK_LAZY) != 0 && !defer;
     if (!lazy) DTC_TRY(fork_side(n, st, &sd));
     DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd, defer, bcap, st, lazy));
-    PROF(1, conv_flops(b.c2.s), conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts));
+    {
+      const BnbArgs bz = bnb_mask_of(n, b.MA1, b.C1, b.b1);
+      PROF(1, conv_flops(b.c2.s),
+           conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts, bmf ? &bz : nullptr));
+    }
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
     DTC_TRY(cap_masked(n, cp + ".dz1", G[4], b.MA1, M, b.Cout, st));
-    if (onepass_ok(n, M, b.Cout, false)) {
+    if (bmf) {  // bn1's sums came with conv2's dgrad
+      DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st, ma1));
+    } else if (onepass_ok(n, M, b.Cout, false)) {
       DTC_TRY(bn_bwd_onepass(n, b.b1, G[4], ma1, nullptr, n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st));
     } else {
       PROF(3, (double)M * b.Cout * 4.125,
@@ -1191,17 +1219,43 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     }
     DTC_TRY(cap(n, cp + ".dc1", dc1, st));
     if (!lazy || b.proj) DTC_TRY(fork_side(n, st, &sd));  // (the shortcut's wgrad below launches)
-    DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, defer, bcap, st, lazy && !b.proj));
+    // option wgrad_s2: conv1 (3x3 stride 2) and the shortcut (1x1 stride 2) weight gradients in one
+    // column-split halo launch (x read once; the shortcut is conv1's centre tap against dsc)
+    const bool wsc = b.proj && wgrad_s2_splits(b.c1.s) > 0 && n.slab_bytes >= conv_wgrad_s2_slab_bytes(b.c1.s) &&
+                     b.sc.s.R == 1 && b.sc.s.stride == 2 && b.sc.s.C == b.c1.s.C && b.sc.s.K == b.c1.s.K;
+    if (wsc) {
+      PROF(2, conv_flops(b.c1.s) + conv_flops(b.sc.s),
+           conv_wgrad_s2(b.c1.s, in, dc1, dsc, n.gf(b.c1.pidx), n.gf(b.sc.pidx), gs, slabw, n.slab_bytes, sd, ts));
+    } else {
+      DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, defer, bcap, st, lazy && !b.proj));
+    }
+    BnbArgs bp;  // the block input's gradient feeds the previous block's bn2 (+ its projection BN) or the stem BN
+    if (bmf) {
+      if (bi > 0) {
+        BlockL& pb = n.blocks[bi - 1];
+        bp = bnb_mask_of(n, pb.MOUT, pb.C2, pb.b2, pb.proj ? pb.S : 0, pb.proj ? &pb.bsc : nullptr);
+      } else {
+        bp = bnb_mask_of(n, n.MA0, n.C0, n.bn0);
+      }
+    }
+    const BnbArgs* bpp = bmf ? &bp : nullptr;
     if (b.proj) {
-      PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
-      if (sc_branch) DTC_TRY(join_sc(n, st));
-      else PROF(1, conv_flops(b.sc.s), conv_dgrad(sc_dg, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
-      PROF(1, conv_flops(b.c1.s),
-           conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts, nullptr, sc_cmp ? 1 : 0));
+      if (!wsc)
+        PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+      if (dscf) {
+        PROF(1, conv_flops(b.c1.s) + conv_flops(b.sc.s),
+             conv_dgrad_sc(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], dsc, n.wbf(b.sc.pidx), st, ts, bpp));
+      } else {
+        if (sc_branch) DTC_TRY(join_sc(n, st));
+        else PROF(1, conv_flops(b.sc.s), conv_dgrad(sc_dg, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
+        PROF(1, conv_flops(b.c1.s),
+             conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts, bpp, sc_cmp ? 1 : 0));
+      }
       DTC_TRY(cap(n, cp + ".dxs", G[5], st));
     } else {  // residual = dz of this block's output (G[0], written by bn2's apply); dx over it in place
-      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[0], slab, n.slab_bytes, st, ts));
+      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[0], slab, n.slab_bytes, st, ts, bpp));
     }
+    sums_ready = bmf;
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
     if (!defer) {
       if (bucket_fires(n, bi)) {
@@ -1223,9 +1277,10 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   // option stem_bn_fuse: the stem BN's apply runs inside the stem weight gradient (dc0 never stored;
   // not with parity captures, which want dc0, or SyncBN, whose sums are all-reduced first)
   if (n.stem_direct && !n.capture && !n.sync && bn_fused() && option_get(OPT_STEM_BN_FUSE) != 0) {
-    PROF(3, (double)M0 * 64 * 4.125,
-         bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
-                            n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
+    if (!sums_ready)
+      PROF(3, (double)M0 * 64 * 4.125,
+           bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
+                              n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
     if (option_get(OPT_FORK_LAZY) && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
     DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
     const BnBwdArgs a0 = bwd_args(n, n.bn0, M0, gs);
@@ -1237,7 +1292,9 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
     return 0;
   }
-  if (onepass_ok(n, M0, 64, false)) {
+  if (sums_ready) {
+    DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[0], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st, m0));
+  } else if (onepass_ok(n, M0, 64, false)) {
     DTC_TRY(bn_bwd_onepass(n, n.bn0, G[0], m0, nullptr, n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st));
   } else {
     PROF(3, (double)M0 * 64 * 4.125,

@@ -44,6 +44,16 @@ struct HaloParams {
   int diag;        // diagnostics only: 2 = no halo DMA after the first stage, 3 = no dy DMA after it
   int xcd;         // 1: XCD-grouped decode of the workgroup id (wg_coords)
   u64* ts;
+  // halo row pitch (stride 1: W + 2) and output dims (stride 1: H, W); stride 2 (ST = 2): the x halo is
+  // column-split as in conv_halo.hip (padded column 2j at j, 2j + 1 at hwh + j), so the 64 output pixels
+  // of a step read consecutive halo rows for every tap and the tr-read swizzle stays conflict-free
+  int pitch, hwh, ho, wo;
+  // SC (stride 2): the block's 1x1 stride-2 projection shortcut's weight gradient in the same launch --
+  // dW_sc[k][c] = sum_p dsc[p][k] x[2p][c] is the centre tap (r, s) = (1, 1) of conv1's A operand
+  // against a second dy tile (dsc): one extra 64-pixel DMA and 2 MFMAs per k-step and wave
+  const u16* dsc;
+  float* slab_sc;  // [splits][K][C] (or, direct, dw_sc)
+  float* dw_sc;
 };
 
 // (output tile, split, problem) of this workgroup. Workgroups are dispatched to the 8 XCDs round-robin
@@ -78,11 +88,11 @@ __device__ __forceinline__ T* uniform_ptr(T* ptr) {
 
 // LDS per pipeline stage: the halo (NR DMA rounds of 64 rows of 128 B) + the dy tile (64 pixels x 64
 // channels). NS stages form a ring; NS - 1 of them are in flight while one is computed.
-template <int NR>
+template <int NR, bool SC = false>
 struct WgStage {
   static constexpr int HALO_ROWS = 64 * NR;
   static constexpr int HALO_BYTES = HALO_ROWS * 128;
-  static constexpr int BYTES = HALO_BYTES + 64 * 128;
+  static constexpr int BYTES = HALO_BYTES + 64 * 128 * (SC ? 2 : 1);
 };
 
 // Tr-image fragment from the halo: lane holds column (channel) cin + lane&15, reduction rows =
@@ -103,10 +113,12 @@ __device__ __forceinline__ bf16x8 frag_halo(const char* halo, int cin, int ra, i
 // window: the step's 22 operand fragments (per k-step: 2 dy, 9 halo) are read PF fragments ahead
 // of the MFMAs that consume them, one fragment (two ds_read_b64_tr_b16) issued per consumed halo
 // fragment, so an LDS read's latency hides behind the MFMAs of the PF fragments before it.
-template <int NS, int NR, int PF>
+template <int NS, int NR, int PF, int ST = 1, bool SC = false>
 __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
-  typedef WgStage<NR> SG;
-  constexpr int PER = NR + 1;  // LDS-DMA instructions per wave per stage (halo rounds + dy tile)
+  typedef WgStage<NR, SC> SG;
+  constexpr int PER = NR + 1 + (SC ? 1 : 0);  // LDS-DMA instructions per wave per stage (halo rounds + dy (+ dsc))
+  static_assert(ST == 1 || (ST == 2 && PF == 0), "stride 2: compiler-scheduled fragment reads");
+  static_assert(!SC || ST == 2, "shortcut fusion: stride 2");
   __shared__ __attribute__((aligned(1024))) char smem[NS * SG::BYTES];
   stamp_start(p.ts);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -121,7 +133,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   const u16* const pdy = uniform_ptr(z == 0 ? p.dys[0] : z == 1 ? p.dys[1] : z == 2 ? p.dys[2] : p.dys[3]);
   const int st_begin = split * p.steps_per_split;
   const int st_end = min(p.nsteps, st_begin + p.steps_per_split);
-  const int W2 = p.W + 2;
+  const int W2 = p.pitch;
 
   // ---- halo DMA: round j covers LDS rows j*64 + wave*8 + lane/8, 16-B chunk lane%8
   int hrel[NR], hrow_in[NR];
@@ -132,9 +144,11 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     const int ii = hrow / p.hb, rem = hrow - ii * p.hb;
     const int hr = rem / W2, wc = rem - hr * W2;
     const int src_chunk = (lane & 7) ^ trswz(hrow);
-    hcol[j] = hrow < p.nh && wc >= 1 && wc <= p.W;
-    hrow_in[j] = hr - 1;  // input row relative to the step's first output row
-    hrel[j] = (((ii * p.H + hr - 1) * p.W + wc - 1) * p.C + c0 + src_chunk * 8) * 2;
+    // input column of this halo column (stride 2: column-split layout), -1 = padding / out of range
+    const int col = ST == 1 ? wc - 1 : (wc < p.hwh ? 2 * wc - 1 : (wc < 2 * p.hwh ? 2 * (wc - p.hwh) : -1));
+    hcol[j] = hrow < p.nh && col >= 0 && col < p.W;
+    hrow_in[j] = hr - 1;  // input row relative to the step's first input row (ST x its first output row)
+    hrel[j] = (((ii * p.H + hr - 1) * p.W + col) * p.C + c0 + src_chunk * 8) * 2;
   }
   // ---- dy DMA: row t = wave*8 + lane/8 of the 64-pixel step
   const int trow = wave * 8 + (lane >> 3);
@@ -143,7 +157,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   auto stage = [&](char* sb, int step) {
     const int m0 = step * 64;
     const int n0 = (int)fdiv((uint32_t)m0, p.fd_hw);
-    const int p0 = (int)fdiv((uint32_t)(m0 - n0 * (int)p.fd_hw.d), p.fd_w);
+    const int p0 = (int)fdiv((uint32_t)(m0 - n0 * (int)p.fd_hw.d), p.fd_w) * ST;  // first INPUT row
     const int base = ((n0 * p.H + p0) * p.W) * p.C * 2;
     const bool first = step == st_begin;
     if (p.diag != 2 || first) {
@@ -154,6 +168,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       }
     }
     if (p.diag != 3 || first) glds16(pdy + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + wave * 1024);
+    if constexpr (SC) glds16(p.dsc + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + 8192 + wave * 1024);
   };
 
   // ---- per-lane halo rows of the pixels this lane reads: t = ks*32 + 8*(lane>>4) + (lane&15)/4 (+4)
@@ -164,9 +179,14 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     for (int h = 0; h < 2; ++h) {
       const int t = ks * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2) + 4 * h;
       const int ii = t / p.spi, rem = t - ii * p.spi;
-      const int pr = rem / p.W, q = rem - pr * p.W;
-      hm[ks][h] = ii * p.hb + pr * W2 + q;
+      const int pr = rem / p.wo, q = rem - pr * p.wo;
+      hm[ks][h] = ii * p.hb + pr * (ST * W2) + q;
     }
+  // halo row offset of tap t (stride 2: row r*pitch, column-split column shift)
+  auto tap_off = [&](int tap) {
+    const int ts = tap % 3;
+    return (tap / 3) * W2 + (ST == 1 ? ts : (ts & 1) * p.hwh + (ts >> 1));
+  };
 
   const int wm = wave >> 1, wn = wave & 1;
   f32x4 acc[9][2];
@@ -186,7 +206,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     for (int i = 0; i < 9; ++i) {
       const int row = wm * 144 + i * 16;  // GEMM row = tap*64 + channel
       const int tap = row >> 6, cin = row & 63;
-      const int toff = (tap / 3) * W2 + (tap % 3);
+      const int toff = tap_off(tap);
       const int unit = (cin >> 2) + (lane & 3);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -208,6 +228,18 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       }
     }
   }
+  // SC: the centre tap's A fragment of channels wm*16.. (the shortcut's 64 output rows, 16 per wave row)
+  uint32_t aoff_sc[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ra = hm[ks][h] + tap_off(4);
+      const int unit = ((wm * 16) >> 2) + (lane & 3);
+      const int f = (((ra >> 1) & 1) << 2) | (((ra >> 3) & 1) << 3);
+      aoff_sc[ks][h] = (uint32_t)(ra * 128 + ((unit ^ f) << 3));
+    }
+  f32x4 acc_sc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   typedef __attribute__((address_space(3))) bf16x4_t lds_v4;
   auto tr8 = [&](const char* sb, uint32_t o0, uint32_t o1) {
     const bf16x4_t t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(sb + o0));
@@ -226,6 +258,14 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
           const bf16x8 af = tr8(sb, aoff[ks][i][0], aoff[ks][i][1]);
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+        }
+        if constexpr (SC) {  // the shortcut: centre-tap A fragment x the dsc tile's B fragments
+          const bf16x8 af = tr8(sb, aoff_sc[ks][0], aoff_sc[ks][1]);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const bf16x8 bs = tr8(sb, boff[ks][j][0] + 8192, boff[ks][j][1] + 8192);
+            acc_sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bs, acc_sc[j], 0, 0, 0);
+          }
         }
       }
     } else {
@@ -300,6 +340,15 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     for (int j = 0; j < 2; ++j) {
       const int kout = k0 + wn * 32 + j * 16 + (lane & 15);
       *(f32x4*)(slab + (size_t)kout * RSC + rsc) = acc[i][j] * osc;
+    }
+  }
+  if constexpr (SC) {  // slab_sc[split][k][c] (direct: dw_sc)
+    float* const ss = p.direct ? p.dw_sc : p.slab_sc + (size_t)split * p.K * p.C;
+    const int c = c0 + wm * 16 + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kout = k0 + wn * 32 + j * 16 + (lane & 15);
+      *(f32x4*)(ss + (size_t)kout * p.C + c) = acc_sc[j] * osc;
     }
   }
   stamp_end(p.ts);
@@ -548,6 +597,9 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   p.hb = (rs + 2) * (s.W + 2);
   p.nh = imgs * p.hb;
   p.spi = rs * s.W;
+  p.pitch = s.W + 2;
+  p.ho = s.H;
+  p.wo = s.W;
   p.ts = ts;
   p.nostore = option_get(OPT_WGRAD_DIAG) == 1;
   p.diag = option_get(OPT_WGRAD_DIAG);
@@ -584,6 +636,96 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
 #undef DTC_WH
   DTC_LAUNCH_CHECK();
   *used_splits = p.direct ? 0 : used;
+  return 0;
+}
+
+// ---------------------------------------------------------------- stride 2 (+ shortcut)
+// conv1 of a projection block (3x3, stride 2, pad 1) and, optionally, its 1x1 stride-2 shortcut: one
+// halo launch over the OUTPUT pixels, the x halo column-split (conv_halo.hip's s2 layout: row pitch
+// 2 (Wo + 1) [+2 where 2 * pitch must be 8 mod 16 rows for the tr reads of a 64-pixel step spanning
+// output rows]); 9 taps + the shortcut from one x halo per step instead of one im2col gather per tap.
+static int s2_pitch_w(int wo) { return 2 * (wo + 1) + ((wo % 16) == 8 ? 2 : 0); }
+static bool halo_geometry_s2(const ConvShape& s, int& rs, int& imgs, int& pitch, int& hb, int& nh) {
+  if (!(s.R == 3 && s.S == 3 && s.stride == 2 && s.pad == 1 && s.C % 64 == 0 && s.K % 64 == 0 && s.H % 2 == 0 &&
+        s.W % 2 == 0))
+    return false;
+  const int ho = s.H / 2, wo = s.W / 2, hw = ho * wo;
+  if (wo > 64 || 64 % wo != 0) return false;
+  if (hw % 64 == 0) {
+    rs = 64 / wo;
+    imgs = 1;
+  } else if (64 % hw == 0) {
+    rs = ho;
+    imgs = 64 / hw;
+  } else {
+    return false;
+  }
+  pitch = s2_pitch_w(wo);
+  hb = (2 * rs + 1) * pitch;
+  nh = imgs * hb;
+  return nh <= 384 && ((int64_t)s.N * hw) % 64 == 0 && (uint64_t)s.N * s.H * s.W * s.C * 2 < (1ull << 31) &&
+         (uint64_t)s.N * hw * s.K * 2 < (1ull << 31);
+}
+
+int wgrad_s2_splits(const ConvShape& s) {
+  int rs, imgs, pitch, hb, nh;
+  if (option_get(OPT_WGRAD_S2) == 0 || !halo_geometry_s2(s, rs, imgs, pitch, hb, nh)) return 0;
+  const int tiles = (s.C / 64) * (s.K / 64);
+  const int nsteps = s.N * (s.H / 2) * (s.W / 2) / 64;
+  int splits = std::max(1, std::max(64, option_get(OPT_WGRAD_HALO)) / tiles);
+  return std::min(splits, std::max(1, nsteps / 4));
+}
+
+size_t conv_wgrad_s2_slab_bytes(const ConvShape& s) {
+  const int sp = wgrad_s2_splits(s);
+  return sp > 0 ? (size_t)sp * s.K * 10 * s.C * 4 : 0;  // 9 taps + the shortcut's [K][C]
+}
+
+int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* dsc, float* dw, float* dw_sc,
+                  float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
+  int rs = 0, imgs = 0, pitch = 0, hb = 0, nh = 0;
+  const int splits = wgrad_s2_splits(s);
+  DTC_CHECK_ARG(splits > 0 && halo_geometry_s2(s, rs, imgs, pitch, hb, nh) && x && dy && dw && (!dsc || dw_sc),
+                "conv_wgrad_s2: unsupported geometry or arguments");
+  HaloParams p{};
+  p.xs[0] = x;
+  p.dys[0] = dy;
+  p.N = s.N; p.H = s.H; p.W = s.W; p.C = s.C; p.K = s.K;
+  p.x_bytes = (uint32_t)((uint64_t)s.N * s.H * s.W * s.C * 2);
+  p.ho = s.H / 2;
+  p.wo = s.W / 2;
+  p.fd_hw = make_fastdiv(p.ho * p.wo);
+  p.fd_w = make_fastdiv(p.wo);
+  p.nsteps = s.N * p.ho * p.wo / 64;
+  p.steps_per_split = (p.nsteps + splits - 1) / splits;
+  p.rs = rs;
+  p.hb = hb;
+  p.nh = nh;
+  p.spi = rs * p.wo;
+  p.pitch = pitch;
+  p.hwh = p.wo + 1;
+  p.ts = ts;
+  p.xcd = option_get(OPT_WGRAD_XCD);
+  const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
+  p.direct = used == 1 && option_get(OPT_WGRAD_DIRECT) != 0;
+  DTC_CHECK_ARG(p.direct || (slab && slab_bytes >= (size_t)used * s.K * 10 * s.C * 4), "conv_wgrad_s2: slab too small");
+  p.slab = slab;
+  p.slab_stride = (size_t)used * s.K * 9 * s.C;
+  p.slab_sc = slab + p.slab_stride;  // [used][K][C] after the taps
+  p.dws[0] = dw;
+  p.dw_sc = dw_sc;
+  p.dsc = dsc;
+  p.scale = scale;
+  const dim3 grid((s.C / 64) * (s.K / 64), used, 1);
+  const int nr = (nh + 63) / 64;
+#define DTC_WS2(NR_, SC_) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 0, 2, SC_>), grid, dim3(512), 0, st, p)
+  if (nr <= 5) { if (dsc) DTC_WS2(5, true); else DTC_WS2(5, false); }
+  else { if (dsc) DTC_WS2(6, true); else DTC_WS2(6, false); }
+#undef DTC_WS2
+  DTC_LAUNCH_CHECK();
+  if (p.direct) return 0;  // one split: dw (and dw_sc) written by the halo kernel
+  DTC_TRY(wgrad_reduce_to(slab, used, s.K, 9 * s.C, 9 * s.C, 9 * s.C, scale, dw, st, ts));
+  if (dsc) DTC_TRY(wgrad_reduce_to(p.slab_sc, used, s.K, s.C, s.C, s.C, scale, dw_sc, st, ts));
   return 0;
 }
 

@@ -44,6 +44,20 @@ def conv2d_fwd(x, w, stride, pad, stats=None):
     return y
 
 
+def conv2d_fwd_sc(x, w, wsc, stats=None, stats_sc=None):
+    """3x3 stride-2 conv + the 1x1 stride-2 projection shortcut of the same x in one launch (net.py:18-19,
+    29-36): x [N,H,W,C], w [K,3,3,C], wsc [K,C] bf16 -> (y, ysc) [N,H/2,W/2,K] bf16."""
+    require_cuda(x, w, wsc)
+    N, H, W, Cc = x.shape
+    K = w.shape[0]
+    d = conv_desc(N, H, W, Cc, K, 3, 3, 2, 1)
+    P, Q = conv_out_hw(H, W, 3, 3, 2, 1)
+    y = torch.empty(N, P, Q, K, dtype=torch.bfloat16, device=x.device)
+    ysc = torch.empty_like(y)
+    call("dtc_conv2d_fwd_sc", d, ptr(x), ptr(w), ptr(y), ptr(stats), ptr(wsc), ptr(ysc), ptr(stats_sc), stream_ptr())
+    return y, ysc
+
+
 def conv2d_dgrad(dy, w, in_hw, stride, pad, res=None):
     """dy [N,P,Q,K] bf16, w [K,R,S,C] -> dx [N,H,W,C] bf16 (+ res)."""
     require_cuda(dy, w)
@@ -85,6 +99,37 @@ def conv2d_wgrad(x, dy, r, s, stride, pad, scale=1.0):
     ws, nb = _ws(d, 2, x.device)
     call("dtc_conv2d_wgrad", d, ptr(x), ptr(dy), ptr(dw), float(scale), ptr(ws), nb, stream_ptr())
     return dw
+
+
+def conv2d_dgrad_sc(dy, w, dsc, wsc, in_hw):
+    """dx through a projection block's conv1 (3x3 stride 2) and its 1x1 stride-2 shortcut in one launch
+    (dtc_conv2d_dgrad_sc): dy / dsc [N,P,Q,K], w [K,3,3,C], wsc [K,C] bf16 -> dx [N,H,W,C] bf16."""
+    require_cuda(dy, w, dsc, wsc)
+    N, _, _, K = dy.shape
+    Cc = w.shape[3]
+    H, W = in_hw
+    d = conv_desc(N, H, W, Cc, K, 3, 3, 2, 1)
+    dx = torch.empty(N, H, W, Cc, dtype=torch.bfloat16, device=dy.device)
+    call("dtc_conv2d_dgrad_sc", d, ptr(dy), ptr(w), ptr(dx), ptr(dsc), ptr(wsc), stream_ptr())
+    return dx
+
+
+def conv2d_wgrad_sc(x, dy, dsc, scale=1.0):
+    """Weight gradients of a projection block's 3x3 stride-2 conv1 and its 1x1 stride-2 shortcut in one
+    launch (dtc_conv2d_wgrad_sc): x [N,H,W,C], dy / dsc [N,H/2,W/2,K] bf16 -> (dw [K,3,3,C], dw_sc [K,C])."""
+    require_cuda(x, dy, dsc)
+    N, H, W, Cc = x.shape
+    K = dy.shape[3]
+    d = conv_desc(N, H, W, Cc, K, 3, 3, 2, 1)
+    nb = lib.dtc_conv2d_wgrad_sc_workspace_size(d)
+    if nb == 0:
+        raise ValueError(f"conv2d_wgrad_sc: no fused plan for {(N, H, W, Cc, K)}")
+    ws = torch.empty(nb // 4 + 64, dtype=torch.float32, device=x.device)
+    dw = torch.empty(K, 3, 3, Cc, dtype=torch.float32, device=x.device)
+    dw_sc = torch.empty(K, Cc, dtype=torch.float32, device=x.device)
+    call("dtc_conv2d_wgrad_sc", d, ptr(x), ptr(dy), ptr(dsc), ptr(dw), ptr(dw_sc), float(scale), ptr(ws), nb,
+         stream_ptr())
+    return dw, dw_sc
 
 
 def conv2d_wgrad_batch(xs, dys, scale=1.0):

@@ -66,6 +66,12 @@ size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass);
 int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats,
                    void* ws, size_t ws_bytes, void* stream);
 /* dx = conv^T(dy, w) (+ res if non-NULL): the input gradient of Conv2d */
+/* 3x3 stride-2 conv (desc) and its BasicBlock's 1x1 stride-2 projection shortcut (net.py:18-19, 29-36) of
+ * the same input in one launch: y = conv(x, w), ysc = conv1x1_s2(x, wsc [K][C]); optional BN statistics of
+ * each. The shortcut reads exactly the 3x3's centre-tap pixels, so x is read once. Returns
+ * DTC_EINVAL for geometries without a fused plan (callers then run the two convs separately). */
+int dtc_conv2d_fwd_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats,
+                      const uint16_t* wsc, uint16_t* ysc, double* stats_sc, void* stream);
 int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
                      const uint16_t* res, void* ws, size_t ws_bytes, void* stream);
 /* The same dgrad when dx is the gradient of a post-ReLU BatchNorm output y = relu(bn(x1) [+ bn2(x2)])
@@ -76,6 +82,11 @@ int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16
                         const uint16_t* res, const uint16_t* ymask, const uint16_t* x1, const float* mean1,
                         const float* invstd1, double* acc1, const uint16_t* x2, const float* mean2,
                         const float* invstd2, double* acc2, void* ws, size_t ws_bytes, void* stream);
+/* dx of a projection block's input through conv1 (3x3 stride 2, desc) AND the 1x1 stride-2 shortcut
+ * (net.py:18-19, 29-36) in one launch: dx = dgrad(dy, w) + dgrad(dsc, wsc [K][C]); the shortcut's term is
+ * nonzero only at the (even, even) pixels and runs as extra reduction steps of that parity class. */
+int dtc_conv2d_dgrad_sc(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
+                        const uint16_t* dsc, const uint16_t* wsc, void* stream);
 /* dw[k][r][s][c] (fp32) = scale * sum over pixels of dy (x) im2col(x): the weight gradient */
 int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* dw, float scale,
                      void* ws, size_t ws_bytes, void* stream);
@@ -85,6 +96,13 @@ int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* 
  * dtc_conv2d_wgrad's. Replaces the weight-gradient halves of n `nn.Conv2d` backward passes
  * (net.py:18-24, 29-35) that autograd would run one by one. Workspace: ..._batch_workspace_size
  * (0 = no halo plan for this geometry: use dtc_conv2d_wgrad per problem). */
+/* The weight gradients of a projection block's 3x3 stride-2 conv1 (desc) and its 1x1 stride-2 shortcut
+ * (net.py:18-19, 29-36) in one launch (+ two fixed-order reduces): dw [K][3][3][C] from (x, dy), dw_sc [K][C]
+ * from (x, dsc); the shortcut is the centre tap of conv1's operand, so x is read once. Workspace size 0:
+ * no fused plan for the geometry (callers then run dtc_conv2d_wgrad for each). */
+size_t dtc_conv2d_wgrad_sc_workspace_size(const dtc_conv_desc* d);
+int dtc_conv2d_wgrad_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, const uint16_t* dsc, float* dw,
+                        float* dw_sc, float scale, void* ws, size_t ws_bytes, void* stream);
 size_t dtc_conv2d_wgrad_batch_workspace_size(const dtc_conv_desc* d, int n);
 int dtc_conv2d_wgrad_batch(const dtc_conv_desc* d, int n, const uint16_t* const* x, const uint16_t* const* dy,
                            float* const* dw, float scale, void* ws, size_t ws_bytes, void* stream);

@@ -41,6 +41,44 @@ def _to_dev_bf16(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev).to(torch.bfloat16)
 
 
+# stride-2 3x3 forward on the column-split halo kernel (option halo_s2; conv_halo.hip ST = 2), alone and
+# with the block's 1x1 stride-2 projection shortcut fused (dtc_conv2d_fwd_sc): ResNet-18's three stride-2
+# geometries (output widths 16 / 8 / 4: one-row fragments, fragments spanning 2 rows with the padded
+# pitch, 4 images per tile) plus a ragged batch, against the oracle
+S2_CASES = [(8, 32, 32, 64, 128), (8, 16, 16, 128, 256), (8, 8, 8, 256, 512), (5, 16, 16, 128, 256), (2, 8, 8, 64, 128)]
+
+
+@pytest.mark.parametrize("case", S2_CASES)
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4])
+def test_conv_fwd_stride2_halo_and_shortcut(dtc, cuda, case, cfg):
+    N, H, W, C, K = case
+    lib = dtc._native.lib
+    g = np.random.default_rng(3)
+    x = _rand_bf16((N, H, W, C), g)
+    w = _rand_bf16((K, 3, 3, C), g, 0.05)
+    wsc = _rand_bf16((K, 1, 1, C), g, 0.1)
+    ref = O.conv2d_fwd(x, w, 2, 1)
+    ref_sc = O.conv2d_fwd(x, wsc, 2, 0)
+    xd, wd, wscd = _to_dev_bf16(x, cuda), _to_dev_bf16(w, cuda), _to_dev_bf16(wsc.reshape(K, C), cuda)
+    prev = lib.dtc_get_option(b"halo_s2")
+    try:
+        lib.dtc_set_option(b"halo_s2", cfg)
+        st = dtc.ops.new_stats(K, cuda)
+        y = dtc.ops.conv2d_fwd(xd, wd, 2, 1, stats=st).float().cpu().numpy()
+        st1, st2 = dtc.ops.new_stats(K, cuda), dtc.ops.new_stats(K, cuda)
+        y2, ysc = dtc.ops.conv2d_fwd_sc(xd, wd, wscd, stats=st1, stats_sc=st2)
+        torch.cuda.synchronize()
+    finally:
+        lib.dtc_set_option(b"halo_s2", prev)
+    y2, ysc = y2.float().cpu().numpy(), ysc.float().cpu().numpy()
+    assert rel_err(y, ref) < 1e-2 and rel_err(y2, ref) < 1e-2 and rel_err(ysc, ref_sc) < 1e-2
+    for out, stt in ((y, st), (y2, st1), (ysc, st2)):  # BN statistics of the bf16 outputs, fp64 slots
+        s_ = stt.sum(0).cpu().numpy()
+        yb = out.reshape(-1, K).astype(np.float64)
+        np.testing.assert_allclose(s_[0], yb.sum(0), rtol=1e-5, atol=1e-3)
+        np.testing.assert_allclose(s_[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_fwd(dtc, cuda, case):
     N, H, W, C, K, R, st = case
@@ -91,6 +129,60 @@ def test_conv_wgrad(dtc, cuda, case):
     ref = 0.5 * O.conv2d_wgrad(x, dy, R, R, st, pad)
     # fp32 accumulation of exact bf16 products: only summation-order differences remain
     assert rel_err(dw.cpu().numpy(), ref) < 1e-5
+
+
+@pytest.mark.parametrize("case", S2_CASES)
+def test_conv_wgrad_stride2_halo_and_shortcut(dtc, cuda, case):
+    """Option wgrad_s2: the 3x3 stride-2 weight gradient on the column-split halo kernel (all nine taps
+    from one x halo per 64-pixel step), alone and with the 1x1 stride-2 shortcut's fused in (its centre
+    tap against dsc: dtc_conv2d_wgrad_sc), against the oracle; geometries without a plan fall back."""
+    N, H, W, C, K = case
+    lib = dtc._native.lib
+    g = np.random.default_rng(7)
+    x = _rand_bf16((N, H, W, C), g)
+    dy = _rand_bf16((N, H // 2, W // 2, K), g)
+    dsc = _rand_bf16((N, H // 2, W // 2, K), g)
+    ref = 0.5 * O.conv2d_wgrad(x, dy, 3, 3, 2, 1)
+    ref_sc = 0.5 * O.conv2d_wgrad(x, dsc, 1, 1, 2, 0).reshape(K, C)
+    xd, dyd, dscd = _to_dev_bf16(x, cuda), _to_dev_bf16(dy, cuda), _to_dev_bf16(dsc, cuda)
+    prev = lib.dtc_get_option(b"wgrad_s2")
+    try:
+        lib.dtc_set_option(b"wgrad_s2", 1)
+        dw = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 2, 1, scale=0.5).cpu().numpy()
+        d = dtc.ops.conv_desc(N, H, W, C, K, 3, 3, 2, 1)
+        fused = lib.dtc_conv2d_wgrad_sc_workspace_size(d) > 0
+        if fused:
+            dw2, dwsc = dtc.ops.conv2d_wgrad_sc(xd, dyd, dscd, scale=0.5)
+            dw2, dwsc = dw2.cpu().numpy(), dwsc.cpu().numpy()
+    finally:
+        lib.dtc_set_option(b"wgrad_s2", prev)
+    assert rel_err(dw, ref) < 1e-5
+    assert fused == (N * (H // 2) * (W // 2) % 64 == 0)
+    if fused:
+        assert rel_err(dw2, ref) < 1e-5 and rel_err(dwsc, ref_sc) < 1e-5
+
+
+@pytest.mark.parametrize("case", S2_CASES)
+def test_conv_dgrad_stride2_with_fused_shortcut(dtc, cuda, case):
+    """Option dgrad_scf: dx through conv1 (3x3 stride 2) + the 1x1 stride-2 shortcut in one parity-class
+    launch (dtc_conv2d_dgrad_sc; the shortcut as extra reduction steps of class (0, 0)) vs the oracle."""
+    N, H, W, C, K = case
+    lib = dtc._native.lib
+    g = np.random.default_rng(9)
+    dy = _rand_bf16((N, H // 2, W // 2, K), g)
+    dsc = _rand_bf16((N, H // 2, W // 2, K), g)
+    w = _rand_bf16((K, 3, 3, C), g, 0.05)
+    wsc = _rand_bf16((K, 1, 1, C), g, 0.1)
+    ref = O.conv2d_dgrad(dy, w, (H, W), 2, 1) + O.conv2d_dgrad(dsc, wsc, (H, W), 2, 0)
+    prev = lib.dtc_get_option(b"dgrad_scf")
+    try:
+        lib.dtc_set_option(b"dgrad_scf", 1)
+        dx = dtc.ops.conv2d_dgrad_sc(_to_dev_bf16(dy, cuda), _to_dev_bf16(w, cuda), _to_dev_bf16(dsc, cuda),
+                                     _to_dev_bf16(wsc.reshape(K, C), cuda), (H, W))
+        torch.cuda.synchronize()
+    finally:
+        lib.dtc_set_option(b"dgrad_scf", prev)
+    assert rel_err(dx.float().cpu().numpy(), ref) < 1e-2
 
 
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[6] == 2])

@@ -237,6 +237,24 @@ def test_per_layer_teacher_forced_config3_per_rank(dtc, cuda, batch):
     assert len(errs) > 90
 
 
+@pytest.mark.parametrize("batch,stages", [(8, (0, 1, 2, 3, 4)), (64, (2, 3, 4))])
+@pytest.mark.parametrize("opts", [{"halo_s2": 1}, {"wgrad_s2": 1}, {"halo_s2": 2, "wgrad_s2": 1}, {"dgrad_scf": 1}])
+def test_per_layer_teacher_forced_halo_s2(dtc, cuda, batch, stages, opts):
+    """The stride-2 convs on the column-split halo kernels with the shortcut fused (options halo_s2:
+    forward, wgrad_s2: weight gradients; halo_s2=2 forces the halo forward on layer2.0.conv1 too):
+    every layer against the oracle."""
+    lib = dtc._native.lib
+    prev = {k: lib.dtc_get_option(k.encode()) for k in opts}
+    try:
+        for k, v in opts.items():
+            lib.dtc_set_option(k.encode(), v)
+        errs = _teacher_forced(dtc, cuda, batch, stages=stages, seed=31)
+    finally:
+        for k, v in prev.items():
+            lib.dtc_set_option(k.encode(), v)
+    assert len(errs) >= 20
+
+
 def test_per_layer_teacher_forced_224(dtc, cuda):
     """BASELINE config 5's geometry (224x224, global pool; SURVEY §7 viii) at batch 2: every layer,
     through the 64-bit-addressed implicit-GEMM path the 224x224 shapes take."""
@@ -566,19 +584,96 @@ def test_stem_bn_fused_wgrad_matches_separate(dtc, cuda, batch, hw):
 def test_shortcut_fused_forward_matches_separate(dtc, cuda, level):
     """Option sc_fuse: the projection shortcut (1x1 stride 2) computed inside conv1's launch from the
     centre-tap im2col tiles (level 1: layer4's plan at B=64 and 256; 2: every 64x64-tile plan; 3: also
-    layer2's 128x128) vs its own launch. Neither path splits K, and each output element sees the same MFMA sequence, so
-    the shortcut output, every BN statistic and every gradient are identical (graphs on and off)."""
+    layer2's 128x128) vs its own launch. With the implicit-GEMM fusion (halo_s2=0) neither path splits K and
+    both tile the shortcut identically, so every output element sees the same MFMA sequence and every BN
+    statistic the same fp32 partials: the gradients are identical. With the column-split halo forward
+    (halo_s2=1, default: layer3/4 fused in conv_halo) the shortcut's MFMA sequence per element is the same
+    but its BN statistics are reduced over the halo tiles instead of the 1x1 GEMM's (other fp32 partials):
+    the gradients then agree to the bf16 propagation of last-bit statistic differences (1e-2)."""
     lib = dtc._native.lib
+    for s2 in (0, 1):
+        for graphs in (1, 0):
+            try:
+                lib.dtc_set_option(b"halo_s2", s2)
+                lib.dtc_set_option(b"sc_fuse", 0)
+                ga = _grads_repeated(dtc, cuda, graphs, batch=64)
+                lib.dtc_set_option(b"sc_fuse", level)
+                gb = _grads_repeated(dtc, cuda, graphs, batch=64)
+            finally:
+                lib.dtc_set_option(b"sc_fuse", DEFAULT_SC_FUSE)
+                lib.dtc_set_option(b"halo_s2", 1)
+            for rep in range(2):
+                if s2 == 0:
+                    np.testing.assert_array_equal(ga[rep], gb[rep])
+                else:
+                    assert np.isfinite(gb[rep]).all() and rel_err(gb[rep], ga[rep]) < 1e-2, rel_err(gb[rep], ga[rep])
+
+
+@pytest.mark.parametrize("batch,hw", [(8, 32), (64, 32), (256, 32), (8, 8)])
+def test_bn_sums_in_dgrad_epilogues_match_reduce_pass(dtc, cuda, batch, hw):
+    """Option bnb_mask: every BN's backward sums (sum dz, sum dz * xhat) accumulated in the epilogue of the
+    dgrad producing its gradient (conv_c64 / conv_halo / split-K reduce; the stride-2 class dgrads keep a
+    separate mask-bit pass) from the forward's ReLU mask bits, vs the separate reduction kernels. Same
+    values summed over other fp32 partials (the dgrad tiles instead of the reduction's slices): what the
+    backward computes before the first fused BN (linear, layer4.1's conv2 and bn2) agrees to 1e-5, every
+    other gradient to 1e-2 (last-bit BN-coefficient differences flip bf16 roundings of the data
+    gradients, which propagate -- a wrong sum would be off by O(1)); graphs on and off, finite."""
+    lib = dtc._native.lib
+    lay = dtc.nn.Layout(100, 25.0)
     for graphs in (1, 0):
         try:
-            lib.dtc_set_option(b"sc_fuse", 0)
-            ga = _grads_repeated(dtc, cuda, graphs, batch=64)
-            lib.dtc_set_option(b"sc_fuse", level)
-            gb = _grads_repeated(dtc, cuda, graphs, batch=64)
+            lib.dtc_set_option(b"bnb_mask", 0)
+            ga = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
+            lib.dtc_set_option(b"bnb_mask", 1)
+            gb = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
         finally:
-            lib.dtc_set_option(b"sc_fuse", DEFAULT_SC_FUSE)
+            lib.dtc_set_option(b"bnb_mask", 0)
         for rep in range(2):
-            np.testing.assert_array_equal(ga[rep], gb[rep])
+            assert np.isfinite(gb[rep]).all()
+            for pe in lay.params:
+                a = ga[rep][pe.offset:pe.offset + pe.numel]
+                b = gb[rep][pe.offset:pe.offset + pe.numel]
+                tol = 1e-5 if pe.name.startswith(("linear", "layer4.1.conv2", "layer4.1.bn2")) else 1e-2
+                assert rel_err(b, a) < tol, (graphs, rep, pe.name, rel_err(b, a))
+
+
+@pytest.mark.parametrize("batch", [8, 64])
+def test_fused_shortcut_dgrad_and_wgrad_match_separate(dtc, cuda, batch):
+    """Options wgrad_s2 (conv1's and the projection shortcut's weight gradients in one column-split halo
+    launch) and dgrad_scf (the shortcut's dgrad as extra reduction steps of conv1's class-(0,0) dgrad) vs
+    the separate launches, graphs on and off. wgrad_s2 changes only the fp32 summation order of those
+    weight gradients: every parameter gradient within 1e-5. dgrad_scf changes the bf16 rounding of the
+    data gradient entering layer3 (one fp32 sum instead of two bf16-rounded ones added): everything the
+    backward computes before it (layer4, linear) is bit-identical, the first BN behind it (layer3.1.bn2)
+    within 1e-2, and the rest finite (further down, rounding differences are amplified as in any two
+    correct bf16 implementations -- DESIGN.md §4)."""
+    lib = dtc._native.lib
+    lay = dtc.nn.Layout(100, 25.0)
+
+    def run(opts, graphs):
+        prev = {k: lib.dtc_get_option(k) for k in opts}
+        try:
+            for k, v in opts.items():
+                lib.dtc_set_option(k, v)
+            return _grads_repeated(dtc, cuda, graphs, batch=batch)
+        finally:
+            for k, v in prev.items():
+                lib.dtc_set_option(k, v)
+
+    for graphs in (1, 0):
+        base = run({b"dgrad_scf": 0, b"wgrad_s2": 0}, graphs)
+        ws2 = run({b"dgrad_scf": 0, b"wgrad_s2": 1}, graphs)
+        dsf = run({b"dgrad_scf": 1, b"wgrad_s2": 0}, graphs)
+        for rep in range(2):
+            for pe in lay.params:
+                a = base[rep][pe.offset:pe.offset + pe.numel]
+                assert rel_err(ws2[rep][pe.offset:pe.offset + pe.numel], a) < 1e-5, (graphs, rep, pe.name)
+                b = dsf[rep][pe.offset:pe.offset + pe.numel]
+                if pe.name.startswith(("layer4", "linear")):
+                    assert np.array_equal(a, b), (graphs, rep, pe.name)
+                elif pe.name.startswith("layer3.1.bn2"):
+                    assert rel_err(b, a) < 1e-2, (graphs, rep, pe.name, rel_err(b, a))
+                assert np.isfinite(b).all()
 
 
 @pytest.mark.parametrize("batch,hw", [(8, 32), (256, 32), (8, 8)])

@@ -66,6 +66,7 @@ def main():
         wsb = max(nat.lib.dtc_conv2d_workspace_size(d, m) for m in range(3))
         ws = torch.empty(wsb // 4 + 64, device=dev)
         flops = 2.0 * B * P * P * K * R * R * C
+        flops_of = {"fwdsc": flops * 10.0 / 9.0, "wgradsc": flops * 10.0 / 9.0}
         P_ = nat.ptr
         fns = {
             "fwd": lambda: nat.call("dtc_conv2d_fwd", d, P_(x), P_(w), P_(y), P_(stats), P_(ws), wsb, nat.stream_ptr()),
@@ -77,6 +78,22 @@ def main():
             "wgrad": lambda: nat.call("dtc_conv2d_wgrad", d, P_(x), P_(dy), P_(dw), 1.0, P_(ws), wsb,
                                       nat.stream_ptr()),
         }
+        if R == 3 and st == 2:  # + the block's 1x1 stride-2 shortcut in the same launch (dtc_conv2d_fwd_sc)
+            wsc = (torch.randn(K, C, device=dev) * 0.05).bfloat16()
+            ysc = torch.empty_like(y)
+            stats2 = ops.new_stats(K, dev)
+            fns["fwdsc"] = lambda: nat.call("dtc_conv2d_fwd_sc", d, P_(x), P_(w), P_(y), P_(stats), P_(wsc), P_(ysc),
+                                            P_(stats2), nat.stream_ptr())
+            dwsc = torch.empty(K, C, device=dev)
+            dsc = torch.randn(B, P, P, K, device=dev).bfloat16()
+
+            def wgradsc():
+                nb = nat.lib.dtc_conv2d_wgrad_sc_workspace_size(d)
+                if nb == 0 or nb > wsb:
+                    raise RuntimeError("no fused wgrad plan / workspace")
+                nat.call("dtc_conv2d_wgrad_sc", d, P_(x), P_(dy), P_(dsc), P_(dw), P_(dwsc), 1.0, P_(ws), wsb,
+                         nat.stream_ptr())
+            fns["wgradsc"] = wgradsc
         if name == "stem":
             fns.pop("dgrad")
             fns.pop("dgradr")
@@ -91,12 +108,17 @@ def main():
             for vi, var in enumerate(variants):
                 for k, v in {**defaults, **var}.items():
                     nat.call("dtc_set_option", k.encode(), int(v))
-                need = max(nat.lib.dtc_conv2d_workspace_size(d, m) for m in range(3))  # the variant's plan
+                need = max([nat.lib.dtc_conv2d_workspace_size(d, m) for m in range(3)] +
+                           [nat.lib.dtc_conv2d_wgrad_sc_workspace_size(d)])  # the variant's plan
                 if need > wsb:
                     wsb = need
                     ws = torch.empty(wsb // 4 + 64, device=dev)
                 for pname, fn in fns.items():
-                    fn()
+                    try:
+                        fn()
+                    except Exception as e:  # no plan for this pass under this variant (e.g. fwdsc)
+                        print(f"  skip {name} {pname} {var}: {e}")
+                        continue
                     torch.cuda.synchronize()
                     g = torch.cuda.CUDAGraph()
                     s = torch.cuda.Stream()
@@ -114,7 +136,7 @@ def main():
                     us = e0.elapsed_time(e1) * 1e3 / args.iters
                     key = (name, pname)
                     prev = results[vi].get(key)
-                    results[vi][key] = (min(us, prev[0]) if prev else us, flops, cnt)
+                    results[vi][key] = (min(us, prev[0]) if prev else us, flops_of.get(pname, flops), cnt)
                     del g
     for vi, var in enumerate(variants):
         print(f"=== variant {var}")
