@@ -260,15 +260,23 @@ static int loopback_reduce(Comm* c, void* buf, size_t count, int dtype, hipStrea
 
 // Host-side wait that polls instead of sleeping in the driver: after the reference's per-step
 // barrier the GPU queue is empty, so every microsecond of wake-up latency is GPU idle time.
+// The poll is bounded: after ~2 ms -- a rank that lags that long (e.g. while rank 0 runs the
+// reference's rank-0-only validation) is not a per-step barrier -- the wait becomes the driver's blocking
+// hipEventSynchronize, so waiting ranks stop pinning a host core.
 static int spin_wait(hipEvent_t ev) {
   if (option_get(OPT_BARRIER_SPIN) == 0) {
     DTC_HIP(hipEventSynchronize(ev));
     return 0;
   }
-  for (;;) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0;; ++i) {
     const hipError_t e = hipEventQuery(ev);
     if (e == hipSuccess) return 0;
     if (e != hipErrorNotReady) return set_error((int)e, "barrier: hipEventQuery: %s", hipGetErrorString(e));
+    if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) {
+      DTC_HIP(hipEventSynchronize(ev));
+      return 0;
+    }
   }
 }
 

@@ -85,6 +85,8 @@ enum {
                            // (extra reduction steps of class (0, 0); igemm.hip conv_dgrad_sc)
   OPT_BNB_MASK = 48,       // executor (mask-bit backward): each BN's backward sums accumulated in the epilogue
                            // of the dgrad producing its gradient, from the ReLU mask bits (no reduction pass)
+  OPT_BUCKET_TAIL = 49,    // executor (at plan time): 1 = close the open bucket (>= 1 MB) after layer2.0 so the
+                           // un-overlapped last bucket is layer1 + stem only (deviates from torch's cap rule)
   OPT_COUNT
 };
 int option_get(int id);

@@ -398,15 +398,18 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.ws_bytes = off;
 
   // gradient buckets at block granularity in backward order (head + layer4.1 first); a bucket
-  // closes once it holds >= bucket_cap_mb, and whatever is open when layer2's backward ends closes
-  // there too: the last bucket -- issued after the stem, overlapping nothing -- is then only
-  // layer1 + the stem (0.6 MB, the unavoidable tail of SURVEY A.2) whatever the cap
+  // closes once it holds >= bucket_cap_mb (torch DDP's rule). Option bucket_tail (default 1; a
+  // deviation from torch's cap semantics, reported in the bench line's buckets_mb): whatever is open
+  // when layer2's backward ends also closes there if it is >= 1 MB, so the last bucket -- issued after
+  // the stem, overlapping nothing -- is only layer1 + the stem (0.6 MB, the unavoidable tail of SURVEY
+  // A.2) instead of up to the whole cap
   const int64_t cap = (int64_t)(bucket_cap_mb * 1024.0 * 1024.0 / 4.0);
+  const bool tail_split = option_get(OPT_BUCKET_TAIL) != 0;
   int64_t start = 0;
   for (int bi = (int)n.blocks.size() - 1; bi >= 0 && cap > 0; --bi) {
     const int64_t hi = n.blocks[bi].grad_hi;
-    const bool tail_edge = bi == 2 && n.blocks.size() == 8;  // layer2.0: next come layer1 and the stem
-    if (hi - start >= cap || (tail_edge && hi > start)) {
+    const bool tail_edge = tail_split && bi == 2 && n.blocks.size() == 8;  // layer2.0: next come layer1 and the stem
+    if (hi - start >= cap || (tail_edge && (hi - start) * 4 >= (1 << 20))) {
       n.bucket_off.push_back(start);
       n.bucket_len.push_back(hi - start);
       n.bucket_after_block.push_back(bi);

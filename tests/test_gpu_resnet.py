@@ -787,9 +787,29 @@ def _perturb_ulp(model, seed):
             prm.mul_(1 + sign * 2.0 ** -23)
 
 
+_LC_BATCHES = {}
+
+
+def _lc_batches(lc, cuda):
+    """The 200 seeded synthetic batches of the loss-curve fixture (tests/golden/make_golden.py::
+    synthetic_stream: labels randint(1234 + step), x = 0.5 * T[y] + randn), generated once on the host in
+    the fixture's order and kept on the GPU for every curve of the ensemble."""
+    key = (lc["batch"], lc["steps"])
+    if key not in _LC_BATCHES:
+        batch, steps = key
+        templates = torch.randn(100, 3, 32, 32, generator=torch.Generator().manual_seed(1234))
+        out = []
+        for s in range(steps):
+            gen = torch.Generator().manual_seed(1234 + s)
+            y = torch.randint(0, 100, (batch,), generator=gen)
+            x = 0.5 * templates[y] + torch.randn(batch, 3, 32, 32, generator=gen)
+            out.append((x.to(cuda), y.to(cuda)))
+        _LC_BATCHES[key] = out
+    return _LC_BATCHES[key]
+
+
 def _loss_curve(dtc, cuda, lc, ulp_seed=0):
-    batch, steps = lc["batch"], lc["steps"]
-    templates = torch.randn(100, 3, 32, 32, generator=torch.Generator().manual_seed(1234))
+    batches = _lc_batches(lc, cuda)
     torch.manual_seed(42)
     model = dtc.ResNet18()
     if ulp_seed:
@@ -798,31 +818,29 @@ def _loss_curve(dtc, cuda, lc, ulp_seed=0):
     crit = dtc.CrossEntropyLoss()
     opt = dtc.SGD(model.parameters(), lr=lc["lr"], weight_decay=lc["wd"], momentum=lc["momentum"], nesterov=True)
     losses = []
-    for s in range(steps):
-        gen = torch.Generator().manual_seed(1234 + s)
-        y = torch.randint(0, 100, (batch,), generator=gen)
-        x = 0.5 * templates[y] + torch.randn(batch, 3, 32, 32, generator=gen)
+    for x, y in batches:
         opt.zero_grad()
         with dtc.autocast():
-            loss = crit(model(x.to(cuda)), y.to(cuda))
+            loss = crit(model(x), y)
         loss.backward()
         opt.step()
         losses.append(loss.detach())
-    return np.array([float(v) for v in losses])
+    return np.array([float(v) for v in torch.stack(losses).cpu()])
 
 
 def test_loss_curve_200_steps(dtc, cuda):
-    """north_star: 200-step loss curve within 1%.
+    """north_star: 200-step loss curve within 1% of the reference.
 
     Fixture (tests/golden/make_golden.py loss, loss_chaos): the REFERENCE net + SGD recipe
-    (src/single/net.py, utils.fix_seed(42), SGD nesterov lr 0.1 wd 1e-4) on the seeded synthetic
-    stream, batch 128, bf16 autocast; once from the seed-42 init and once from each of 8 inits
-    perturbed by 1 ulp (9 curves). Training is chaotic: the reference's OWN 1-ulp reruns spread the
-    200-step mean loss with a standard deviation of 2.4% (0.632 +- 0.015), so one curve cannot be
-    held to 1%, and the ensemble mean of 9 curves still carries a 0.8% standard error. The criterion
-    is therefore statistical: our ensemble (same 9 inits) must have a mean loss within
-    max(1%, 3 standard errors of the difference of the two ensemble means) of the reference's, and
-    the first 5 steps, before the trajectories decorrelate, within 1% per step."""
+    (src/single/net.py, utils.fix_seed(42), SGD nesterov lr 0.1 wd 1e-4; single/trainer.py:131-147) on
+    the seeded synthetic stream, batch 128, bf16 autocast: once from the seed-42 init and once from each
+    of 99 inits perturbed by 1 ulp (100 curves). Training is chaotic: the reference's OWN 1-ulp reruns
+    spread the 200-step mean loss by ~1.8% (s.d.), so one curve cannot be held to 1%; the ensemble of 100
+    resolves it (3 standard errors of the difference of the two ensemble means ~0.75%). Criterion: our
+    ensemble over the same 100 inits has a 200-step mean loss within 1% of the reference's, with the 3-s.e.
+    resolution printed beside it (and required < 1%, i.e. the check really resolves 1%); and the
+    per-step ensemble means within 1% over the leading steps where the reference ensemble itself resolves
+    1% (before the trajectories decorrelate)."""
     import json
     import os
 
@@ -836,11 +854,7 @@ def test_loss_curve_200_steps(dtc, cuda):
     mr = np.array([c.mean() for c in ref_curves])
     n = len(mr)
     se = np.sqrt(mo.var(ddof=1) / n + mr.var(ddof=1) / n) / mr.mean()
-    tol = max(1e-2, 3.0 * se)
     rel = (mo.mean() - mr.mean()) / mr.mean()
-    # per-step ensemble means: the 1% bound held step by step over the steps where the reference's own
-    # 1-ulp ensemble is still tight enough to resolve 1% (3 standard errors of the step's ensemble-mean
-    # difference < 1%); past that the trajectories have decorrelated and only the statistic above applies
     O_ = np.stack(ours)
     R_ = np.stack(ref_curves)
     step_rel = (O_.mean(0) - R_.mean(0)) / R_.mean(0)
@@ -848,15 +862,18 @@ def test_loss_curve_200_steps(dtc, cuda):
     resolvable = 3.0 * step_se < 1e-2
     K = int(np.argmin(resolvable)) if not resolvable.all() else len(resolvable)
     worst_k = float(np.abs(step_rel[:K]).max()) if K else 0.0
-    report = (f"loss-curve parity (n={n} ensembles x {O_.shape[1]} steps): 200-step mean ours {mo.mean():.4f} "
-              f"ref {mr.mean():.4f} rel {rel:+.4f} (se {se:.4f}; bound max(1%, 3se) = {tol:.4f}); per-step "
-              f"ensemble mean over the first {K} resolvable steps: max |rel| {worst_k:.4f} (bound 0.01)")
+    report = (f"loss-curve parity (n={n} curves per side x {O_.shape[1]} steps): 200-step ensemble mean ours "
+              f"{mo.mean():.4f} ref {mr.mean():.4f} rel {rel:+.4f} (bound 0.01; resolution 3 s.e. = {3 * se:.4f}); "
+              f"per-step ensemble means over the first {K} resolvable steps: max |rel| {worst_k:.4f} (bound 0.01)")
     print(report)
     import warnings
 
     warnings.warn(report, UserWarning)  # lands in the pytest warnings summary of the GPU test log
     assert K >= 5 and worst_k < 1e-2, report
-    assert abs(rel) < tol, report
+    if n >= 100:  # the full ensemble: north_star's 1% itself, and the check resolves it
+        assert 3 * se < 1e-2 and abs(rel) < 1e-2, report
+    else:  # a partial fixture (ensemble still being generated): the statistical bound of round 2
+        assert abs(rel) < max(1e-2, 3.0 * se), report
 
 
 def test_native_loss_backward_matches_autograd(dtc, cuda):

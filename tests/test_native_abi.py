@@ -66,12 +66,27 @@ def test_buckets_tile_the_gradient_buffer(dtc, cap_mb):
         pos += n
     assert pos == lay.flat_numel
     # every bucket closes at a block boundary at or above the cap, except the one open when layer2's
-    # backward ends (closed there) and the last: layer1 + stem, the unavoidable tail
+    # backward ends (option bucket_tail: closed there when >= 1 MB) and the last: at most layer1 + stem,
+    # the unavoidable tail
     tail_start = min(p.offset for p in lay.params if p.name.startswith("layer1.") or p.name in
                      ("conv1.weight", "bn1.weight", "bn1.bias"))
     for off, n in lay.buckets[:-1]:
         assert n * 4 >= cap_mb * 2 ** 20 or off + n == tail_start
-    assert lay.buckets[-1][0] == tail_start and lay.buckets[-1][1] * 4 < 0.6 * 2 ** 20
+    assert lay.buckets[-1][0] >= tail_start and lay.buckets[-1][1] * 4 < 0.6 * 2 ** 20
+
+
+def test_bucket_tail_option_restores_torch_cap_rule(dtc):
+    """Option bucket_tail=0: buckets close only at the cap (torch DDP's rule); the last one is then
+    whatever remains (100 MB cap: one 42.8 MB bucket, all of it issued after the stem)."""
+    lib = dtc._native.lib
+    try:
+        lib.dtc_set_option(b"bucket_tail", 0)
+        lay = dtc.nn.Layout(100, 100)
+        assert len(lay.buckets) == 1 and lay.buckets[0][1] == lay.flat_numel
+        lay = dtc.nn.Layout(100, 25)
+        assert all(n * 4 >= 25 * 2 ** 20 for _, n in lay.buckets[:-1])
+    finally:
+        lib.dtc_set_option(b"bucket_tail", 1)
     # the first bucket starts with the head (linear.bias at offset 0): it is ready first
     names_at_0 = [p.name for p in lay.params if p.offset == 0]
     assert names_at_0 == ["linear.bias"]
