@@ -81,7 +81,115 @@ struct HConvParams {
   const u16* wsc;  // [Cout][C]
   u16* out2;
   double* stats2;
+  // DGRAD without split-K (option halo_stage_epi): the fp32 tile is staged through LDS and written /
+  // combined with its residual, mask bits and BN inputs in 16-B row pieces of 8 channels per lane
+  // (coalesced), instead of 8-B pieces strided by the channel count per lane
+  int staged;
 };
+
+// DGRAD epilogue through LDS: every wave writes its fp32 fragments into a [BN pixels][BM channels] tile
+// (16-B chunk c of pixel row r at c ^ (r mod chunks): the 16 pixels of a fragment column land on distinct
+// bank slots), then each thread owns 8 consecutive channels of a pixel per pass (two 16-B LDS reads) and
+// does the rest with 16-B global accesses: + residual (fp32), round to bf16, and with the fused BN backward
+// (p.bnb) mask by the forward's ReLU bits (one byte = the 8 channels) or y, accumulate sum(dz) and
+// sum(dz * xhat) (+ the second BN's) per channel over its pixels; the per-thread partials are summed per
+// channel in LDS in a fixed order and added to the fp64 slots with one atomic per channel and workgroup.
+template <int BM, int BN, int FM, int FN>
+__device__ __forceinline__ void dgrad_staged_epilogue(const HConvParams& p, float* stg, const f32x4 (&acc)[FM][FN],
+                                                      int arow0, int bcol0, int rq, int cl, int px0, int a0, int M) {
+  constexpr int NCH = BM / 4;  // 16-B chunks per staged pixel row
+  constexpr int G8 = BM / 8;   // 8-channel groups per pixel
+  constexpr int PPP = 256 / G8;  // pixel rows per pass
+  constexpr int NPASS = BN / PPP;
+  static_assert(BN % PPP == 0, "staged epilogue: pixels per pass");
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int pl = bcol0 + j * 16 + cl, c = (arow0 + i * 16 + rq) >> 2;
+      *(f32x4*)(stg + pl * BM + ((c ^ (pl & (NCH - 1))) << 2)) = acc[i][j];
+    }
+  __syncthreads();
+  const int t = threadIdx.x, g = t % G8, pr = t / G8;
+  const bool bnb = bnb_on(p.bnb), dual = bnb && p.bnb.x2 != nullptr, has_res = p.res != nullptr;
+  float m1[8], i1[8], m2[8], i2[8], s[8], q1[8], q2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m1[k] = i1[k] = m2[k] = i2[k] = s[k] = q1[k] = q2[k] = 0.f;
+  if (bnb) {
+    const int c = a0 + g * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      m1[k] = p.bnb.mean1[c + k];
+      i1[k] = p.bnb.invstd1[c + k];
+      if (dual) {
+        m2[k] = p.bnb.mean2[c + k];
+        i2[k] = p.bnb.invstd2[c + k];
+      }
+    }
+  }
+#pragma unroll
+  for (int ps = 0; ps < NPASS; ++ps) {
+    const int pl = ps * PPP + pr, pix = px0 + pl;
+    const bool ok = pix < M;
+    const size_t o = (size_t)(ok ? pix : 0) * p.Cout + a0 + g * 8;
+    // every global operand of the pass in flight before the LDS reads are consumed
+    const uint4 rr = has_res && ok ? *(const uint4*)(p.res + o) : uint4{0u, 0u, 0u, 0u};
+    uint4 xv{0u, 0u, 0u, 0u}, xw{0u, 0u, 0u, 0u}, yv{0u, 0u, 0u, 0u};
+    uint32_t mbits = 0u;
+    if (bnb && ok) {
+      xv = *(const uint4*)(p.bnb.x1 + o);
+      if (dual) xw = *(const uint4*)(p.bnb.x2 + o);
+      if (p.bnb.mb) mbits = p.bnb.mb[o >> 3];
+      else yv = *(const uint4*)(p.bnb.ym + o);
+    }
+    const int c0 = 2 * g, sw = pl & (NCH - 1);
+    const f32x4 lo = *(const f32x4*)(stg + pl * BM + ((c0 ^ sw) << 2));
+    const f32x4 hi = *(const f32x4*)(stg + pl * BM + (((c0 + 1) ^ sw) << 2));
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if (has_res) {
+      float r[8];
+      unpack8(rr, r);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += r[k];
+    }
+    if (bnb) {
+      float x[8], x2[8], y[8];
+      unpack8(xv, x);
+      unpack8(xw, x2);
+      unpack8(yv, y);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool keep = p.bnb.mb ? ((mbits >> k) & 1u) != 0u : y[k] > 0.f;
+        v[k] = keep ? round_bf(v[k]) : 0.f;  // exact: masking a bf16 value
+        const float d = ok ? v[k] : 0.f;
+        s[k] += d;
+        q1[k] += d * ((x[k] - m1[k]) * i1[k]);
+        if (dual) q2[k] += d * ((x2[k] - m2[k]) * i2[k]);
+      }
+    }
+    if (ok) *(uint4*)(p.out + o) = pack8(v);
+  }
+  if (!bnb) return;
+  __syncthreads();  // the staged tile is dead: per-thread partials [PPP][BM][3]
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float* r = stg + ((size_t)pr * BM + g * 8 + k) * 3;
+    r[0] = s[k];
+    r[1] = q1[k];
+    r[2] = q2[k];
+  }
+  __syncthreads();
+  if (t < BM) {
+    float ss = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int r = 0; r < PPP; ++r) {
+      const float* e = stg + ((size_t)r * BM + t) * 3;
+      ss += e[0];
+      a1 += e[1];
+      a2 += e[2];
+    }
+    bnb_commit(p.bnb, p.Cout, a0 + t, ss, a1, a2, dual);
+  }
+}
 
 template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP, int WS, int ST = 1, bool SC = false>
 __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) {
@@ -356,6 +464,14 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
 
   // ---- epilogue: D[row = output channel][col = pixel], 4 consecutive channels per lane
   const int rq = (lane >> 4) * 4, cl = fpx;  // column -> pixel, as in the B fragments
+  constexpr bool kStageFits = MODE == 1 && BN * BM * 4 <= (int)sizeof(smem) && BM * 8 <= 256 * 8;
+  if constexpr (kStageFits) {
+    if (p.slab == nullptr && p.staged) {
+      dgrad_staged_epilogue<BM, BN, FM, FN>(p, (float*)smem, acc, arow0, bcol0, rq, cl, px0, a0, M);
+      stamp_end(p.ts);
+      return;
+    }
+  }
   if (p.slab != nullptr) {  // split-K partial: fp32 [split][pixel][Cout], one 16-B store per fragment
     float* slab = p.slab + (size_t)split * M * p.Cout;
 #pragma unroll
@@ -713,6 +829,7 @@ int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, 
   p.fd_spx = make_fastdiv(p.rows * g.wo);
   p.fd_w = make_fastdiv(g.wo);
   p.ts = ts;
+  p.staged = option_get(OPT_HALO_STAGE_EPI);
   if (bnb != nullptr && split <= 1) p.bnb = *bnb;  // (split-K: the reduction kernel applies it)
   const dim3 grid(halo_tiles_b(s, g) * p.tiles_a, split);
   if (c.st == 2) {

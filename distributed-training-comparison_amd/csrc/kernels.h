@@ -73,7 +73,9 @@ enum {
   OPT_SC_FUSE = 41,        // forward: the projection shortcut computed inside conv1's launch (conv_fwd_sc) for
                            // 1 (default) layer4-size plans, 2 every 64x64 plan, 3 also 128x128 (igemm.hip)
   OPT_HEAD_DIRECT = 42,    // forward: 1 (default) = the head launched after the graph into the caller's logits
-                           // (no graph-owned copy + D2D copy kernel)
+                           // (no graph-owned copy + D2D copy kernel); 2 = the head inside the graph, its
+                           // destination read from a pointer slot the input-copy launch stores. 2 measured
+                           // neutral (6-round A/B): the ~14 us graph-completion gap moves to the next kernel
   OPT_STEM_RECOMPUTE = 43, // training forward: 1 = stem statistics pass + recompute pass with the BN apply fused
   OPT_STEM_WLDS = 44,      // stem forward: 1 (default) = weight staged in LDS by coalesced loads, not per-lane
                            // 2-B gathers (stem_bench: 18.7 -> 16.1 us; +1.1% interleaved A/B)
@@ -87,6 +89,15 @@ enum {
                            // of the dgrad producing its gradient, from the ReLU mask bits (no reduction pass)
   OPT_BUCKET_TAIL = 49,    // executor (at plan time): 1 = close the open bucket (>= 1 MB) after layer2.0 so the
                            // un-overlapped last bucket is layer1 + stem only (deviates from torch's cap rule)
+  OPT_GRAPH_EV = 50,       // executor: 1 (default) = an event recorded behind every graph launch (drop_graphs waits
+                           // for the last one before destroying execs); 0 = none (drop relies on the device drain)
+  OPT_WGRAD_PMAP = 51,     // wgrad_halo (stride 1): 1 = bank-conflict-free tr-read pixel map and swizzle for
+                           // every row width (HaloParams::pmap); 0 (default) = the original map. PMC: 22% of
+                           // the layer3/4 launches' LDS cycles were conflict cycles; removing them measured
+                           // neutral (isolated and in-step), the launches are not LDS-bank bound
+  OPT_HALO_STAGE_EPI = 52,  // conv_halo DGRAD (no split-K): 1 = the tile staged through LDS and written / combined
+                            // with residual, mask bits and BN inputs by 16-B row pieces (coalesced). Default 0:
+                            // neutral in-step (+-0.4%), 1 us slower on the layer2 dgrad alone
   OPT_COUNT
 };
 int option_get(int id);
@@ -313,6 +324,9 @@ int wgrad_reduce_to(const float* slab, int splits, int K, int RSC, int ncols, in
 // feat[n][c] = bf16round(mean_hw act); logits[n][j] = feat . W[j] + b[j]
 int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st);
+// the same, the logits pointer read on the device from *lslot (a word stored before a graph replay)
+int head_fwd_slot(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
+                  float* const* lslot, hipStream_t st);
 // mean cross entropy; lse per row
 int xent_fwd(const float* logits, const int64_t* labels, int N, int ncls, float* loss, float* lse,
              hipStream_t st);
@@ -337,7 +351,9 @@ int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st);
 // zero an 8-byte aligned range (a kernel node, unlike hipMemsetAsync's fill dispatch)
 int zero_bytes(void* p, size_t bytes, hipStream_t st);
 // dst[0:bytes] = src[0:bytes] (16-B aligned) and zp[0:zbytes] = 0 (8-B aligned), one launch
-int copy_and_zero(const void* src, void* dst, size_t bytes, void* zp, size_t zbytes, hipStream_t st);
+int copy_and_zero(const void* src, void* dst, size_t bytes, void* zp, size_t zbytes, hipStream_t st,
+                  void* slot = nullptr, const void* slot_val = nullptr);
+int put_word(void* slot, const void* val, hipStream_t st);
 // x[i] *= f (loopback test communicator)
 int scale_f32(float* x, int64_t n, float f, hipStream_t st);
 int scale_f64(double* x, int64_t n, double f, hipStream_t st);

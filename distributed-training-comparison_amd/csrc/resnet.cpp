@@ -17,6 +17,7 @@
 // address order, so every DDP bucket is a contiguous prefix-extension of the buffer.
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 #include "comm.h"
@@ -121,6 +122,7 @@ struct Net {
   // at bucket boundaries (the all-reduces stay eager on the communicator's side stream)
   struct Seg { hipGraphExec_t exec = nullptr; std::vector<int> buckets; };
   hipStream_t cap_st = nullptr;
+  bool cap_locked = false;  // this executor holds g_graph_mu (between begin_capture and end_capture)
   int graph_epoch = -1;
   // graph sets indexed [profiling]: the profiled set carries the timing stamps and the per-step fold
   hipGraphExec_t fwd_exec[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [profiling][train]
@@ -131,6 +133,8 @@ struct Net {
   hipEvent_t launch_ev = nullptr;
   bool launched = false;
   size_t LOGITS = 0, DLOGITS = 0;  // graph-owned copies of the caller's logits / dlogits
+  size_t LSLOT = 0;  // (head_direct = 2) the caller's logits pointer, stored before each forward replay
+  int head_mode = 0;  // head_direct the current forward graphs were captured with
   // activation registry (per-layer parity): name, workspace byte offset, N,H,W,C
   struct Act { std::string name; size_t off; int n, h, w, c; };
   std::vector<Act> acts;
@@ -324,6 +328,7 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.FEAT = take(B * 512 * 4);
   n.LOGITS = take(B * n.ncls * 4);
   n.DLOGITS = take(B * n.ncls * 4);
+  n.LSLOT = take(64);
   n.HEADWS_bytes = head_bwd_workspace((int)B, 512, n.ncls);
   n.HEADWS = take(n.HEADWS_bytes);
   n.acts.push_back({"head.feat_f32", n.FEAT, (int)B, 1, 1, 512});
@@ -442,7 +447,17 @@ static u64* prof_slot(Net& n, int kind, double flops) {
   } while (0)
 
 // ------------------------------------------------------------------ graph capture helpers
+// Process-wide: graph capture (begin_capture .. end_capture) and graph destruction (drop_graphs: a device
+// drain + hipGraphExecDestroy) are serialised across host threads. Several executors driven by one thread
+// each (the thread-group communicator's W ranks in one process) otherwise capture and drain at the same
+// time: a device drain while another thread's stream is capturing crashed the HIP runtime (segfault in
+// the first backward of test_gpu_ddp_group's graphs-on case). Capture happens once per executor and
+// option epoch, so the lock costs nothing per step; no collective is issued inside a captured region
+// (bucket all-reduces run between the replayed segments), so a rank holding it never waits on another.
+static std::recursive_mutex g_graph_mu;
+
 static void drop_graphs(Net& n) {
+  std::lock_guard<std::recursive_mutex> lk(g_graph_mu);
   // An exec may still be running (the caller's previous step is asynchronous). Round 2 saw a rare
   // crash in a HIP runtime thread (no Python frame) when execs were destroyed right after a device
   // drain and the profiling slots their kernels stamp were freed next (dtc_rn18_profile_end). The
@@ -471,9 +486,11 @@ static void drop_graphs(Net& n) {
 }
 static int graph_launch(Net& n, hipGraphExec_t ex, hipStream_t st) {
   DTC_HIP(hipGraphLaunch(ex, st));
-  if (!n.launch_ev) DTC_HIP(hipEventCreateWithFlags(&n.launch_ev, hipEventDisableTiming));
-  DTC_HIP(hipEventRecord(n.launch_ev, st));
-  n.launched = true;
+  if (option_get(OPT_GRAPH_EV) != 0) {
+    if (!n.launch_ev) DTC_HIP(hipEventCreateWithFlags(&n.launch_ev, hipEventDisableTiming));
+    DTC_HIP(hipEventRecord(n.launch_ev, st));
+    n.launched = true;
+  }
   return 0;
 }
 static bool graphs_on(Net& n) {
@@ -485,13 +502,21 @@ static bool graphs_on(Net& n) {
   return true;
 }
 static int begin_capture(Net& n) {
-  if (!n.cap_st) DTC_HIP(hipStreamCreateWithFlags(&n.cap_st, hipStreamNonBlocking));
-  DTC_HIP(hipStreamBeginCapture(n.cap_st, hipStreamCaptureModeRelaxed));
+  g_graph_mu.lock();  // released by the matching end_capture (or here on failure)
+  n.cap_locked = true;
+  hipError_t e = hipSuccess;
+  if (!n.cap_st) e = hipStreamCreateWithFlags(&n.cap_st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamBeginCapture(n.cap_st, hipStreamCaptureModeRelaxed);
+  if (e != hipSuccess) {
+    n.cap_locked = false;
+    g_graph_mu.unlock();
+    return set_error((int)e, "begin capture: %s", hipGetErrorString(e));
+  }
   return 0;
 }
 // Ends the capture on n.cap_st (always, also when the captured body failed); *out stays null
 // for an empty capture.
-static int end_capture(Net& n, int body_rc, hipGraphExec_t* out) {
+static int end_capture_locked(Net& n, int body_rc, hipGraphExec_t* out) {
   *out = nullptr;
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamEndCapture(n.cap_st, &g);
@@ -505,6 +530,16 @@ static int end_capture(Net& n, int body_rc, hipGraphExec_t* out) {
   (void)hipGraphDestroy(g);
   if (e != hipSuccess) return set_error((int)e, "graph instantiate: %s", hipGetErrorString(e));
   return 0;
+}
+static int end_capture(Net& n, int body_rc, hipGraphExec_t* out) {
+  if (!n.cap_locked) {  // begin_capture failed (a segment boundary inside the backward): nothing open
+    *out = nullptr;
+    return body_rc != 0 ? body_rc : set_error(DTC_EINVAL, "end_capture without an open capture");
+  }
+  const int rc = end_capture_locked(n, body_rc, out);
+  n.cap_locked = false;
+  g_graph_mu.unlock();  // taken by begin_capture
+  return rc;
 }
 
 // ------------------------------------------------------------------ forward / backward
@@ -583,6 +618,9 @@ static int join_sc(Net& n, hipStream_t st);
 // everything after the input im2col (reads only executor-owned memory: capturable)
 static int forward_head(Net& n, float* logits, hipStream_t st) {
   const BlockL& last = n.blocks.back();
+  if (logits == nullptr)  // head_direct = 2, inside the graph: the destination is read from LSLOT
+    return head_fwd_slot(n.at<u16>(last.OUT), n.B, last.Hout * last.Wout, 512, n.wbf(n.fc_w), n.pf(n.fc_b), n.ncls,
+                         n.at<float>(n.FEAT), n.at<float* const>(n.LSLOT), st);
   return head_fwd(n.at<u16>(last.OUT), n.B, last.Hout * last.Wout, 512, n.wbf(n.fc_w), n.pf(n.fc_b), n.ncls,
                   n.at<float>(n.FEAT), logits, st);
 }
@@ -651,7 +689,8 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
     }
     in = n.at<u16>(b.OUT);
   }
-  if (logits == nullptr) return 0;  // graphed forward (option head_direct): head launched by forward()
+  // graphed forward with head_direct = 1: the head is launched by forward() after the graph
+  if (logits == nullptr && n.head_mode != 2) return 0;
   return forward_head(n, logits, st);
 }
 
@@ -830,30 +869,39 @@ static int forward(Net& n, const float* x, float* logits, bool train, hipStream_
   return 0;
 }
 static int forward_impl(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
+  // option head_direct: 0 = the head writes a graph-owned buffer copied out after the graph; 1 = the
+  // pool + FC head launched after the graph straight into the caller's logits (the graph cannot bake
+  // in a per-call pointer); 2 = the head inside the graph, its destination read from LSLOT, which the
+  // input-copy launch stores before the replay (the ~14 us graph-completion -> next-kernel gap goes)
+  const int hmode = (!n.f32 && graphs_on(n)) ? option_get(OPT_HEAD_DIRECT) : 0;
   if (n.f32) DTC_TRY(f32_stem_im2col(x, n.at<float>(n.X0), n.B, n.H, n.W, st));
   else if (n.stem_direct) {  // the graph reads only executor memory: a copy of the 12 B/pixel input (+ the
-    // training step's BN slots zeroed in the same launch)
+    // training step's BN slots zeroed in the same launch, + the logits pointer for head_direct = 2)
     const size_t xb = (size_t)n.B * 3 * n.H * n.W * 4;
     if (xb % 16 == 0 && ((uintptr_t)x & 15) == 0 && option_get(OPT_STEM_PROLOGUE) != 0) {
-      DTC_TRY(copy_and_zero(x, n.at<float>(n.XIN), xb, n.ws + n.stats_lo, train ? n.stats_hi - n.stats_lo : 0, st));
+      DTC_TRY(copy_and_zero(x, n.at<float>(n.XIN), xb, n.ws + n.stats_lo, train ? n.stats_hi - n.stats_lo : 0, st,
+                            hmode == 2 ? n.ws + n.LSLOT : nullptr, logits));
     } else {
       DTC_HIP(hipMemcpyAsync(n.at<float>(n.XIN), x, xb, hipMemcpyDeviceToDevice, st));
       if (train) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));
+      if (hmode == 2) DTC_TRY(put_word(n.ws + n.LSLOT, logits, st));
     }
+  } else {
+    DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
+    if (hmode == 2) DTC_TRY(put_word(n.ws + n.LSLOT, logits, st));
   }
-  else DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
   if (!graphs_on(n)) return forward_body(n, logits, train, st);
   hipGraphExec_t& ex = n.fwd_exec[n.profiling ? 1 : 0][train ? 1 : 0];
-  // option head_direct: the pool + FC head is launched after the graph, straight into the caller's
-  // logits (the graph cannot bake in a per-call pointer), instead of a graph-owned copy + D2D copy
-  const bool direct = !n.f32 && option_get(OPT_HEAD_DIRECT) != 0;
+  if (ex && n.head_mode != hmode) drop_graphs(n);  // (option epochs normally re-capture already)
   if (!ex) {
+    n.head_mode = hmode;
     DTC_TRY(begin_capture(n));
-    const int rc = forward_body(n, direct ? nullptr : n.at<float>(n.LOGITS), train, n.cap_st);
+    const int rc = forward_body(n, hmode >= 1 ? nullptr : n.at<float>(n.LOGITS), train, n.cap_st);
     DTC_TRY(end_capture(n, rc, &ex));
   }
   DTC_TRY(graph_launch(n, ex, st));
-  if (direct) return forward_head(n, logits, st);
+  if (hmode == 2) return 0;
+  if (hmode == 1) return forward_head(n, logits, st);
   DTC_HIP(hipMemcpyAsync(logits, n.at<float>(n.LOGITS), (size_t)n.B * n.ncls * 4, hipMemcpyDeviceToDevice, st));
   return 0;
 }

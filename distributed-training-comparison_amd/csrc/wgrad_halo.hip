@@ -54,7 +54,27 @@ struct HaloParams {
   const u16* dsc;
   float* slab_sc;  // [splits][K][C] (or, direct, dw_sc)
   float* dw_sc;
+  // tr-read bank layout (stride 1; option wgrad_pmap): which pixel of the step each (k-step, 16-lane block
+  // b, read h, lane quad q) reads, and the second row bit of the halo / dy 16-B chunk swizzle (the first is
+  // row bit 1). A ds_read_b64_tr_b16 is conflict-free when the 8 rows its 32-lane half reads have distinct
+  // (row parity, swizzle): pmap 0 (pixels 8b + 4h + q, swizzle bits 1 and 3) is for 16- and 32-wide
+  // rows only -- at W = 8 and 4 some taps read two rows into one bank slot (PMC: 22% of the LDS cycles of
+  // the layer3/4 launches were conflict cycles); pmap 1 (W >= 8: pixels 16h + 4b + q, i.e. 8 consecutive
+  // pixels of one image row per half-read; bits 1 and 2) and pmap 2 (4x4 images: rows r and r ^ 2 of one
+  // image per half-read; halo bits 1, 2, dy bits 1, 3) are conflict-free for every tap (tools/tr_banks.py)
+  int pmap, hsb, dsb;
 };
+
+// pixel (within the 64-pixel step) of k-step ks, lane block b = lane >> 4, tr read h, lane quad q
+__device__ __forceinline__ int wg_pixel(int pmap, int ks, int b, int h, int q) {
+  if (pmap == 1) return ks * 32 + 16 * h + 4 * b + q;
+  if (pmap == 2) return ks * 32 + (b >> 1) * 16 + (h + 2 * (b & 1)) * 4 + q;
+  return ks * 32 + 8 * b + q + 4 * h;
+}
+// 16-B chunk swizzle of LDS row r: row bits 1 and `sb` -> chunk bits 1 and 2 (sb = 3: trswz)
+__device__ __forceinline__ int wg_swz(int r, int sb) { return (((r >> 1) & 1) << 1) | (((r >> sb) & 1) << 2); }
+// the same as an 8-B unit XOR (unit index bits 2 and 3)
+__device__ __forceinline__ int wg_uswz(int r, int sb) { return (((r >> 1) & 1) << 2) | (((r >> sb) & 1) << 3); }
 
 // (output tile, split, problem) of this workgroup. Workgroups are dispatched to the 8 XCDs round-robin
 // by linear id, so with the plain grid decode the tiles of one (problem, split) -- which read the same
@@ -143,7 +163,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     const int hrow = j * 64 + wave * 8 + (lane >> 3);
     const int ii = hrow / p.hb, rem = hrow - ii * p.hb;
     const int hr = rem / W2, wc = rem - hr * W2;
-    const int src_chunk = (lane & 7) ^ trswz(hrow);
+    const int src_chunk = (lane & 7) ^ (ST == 1 ? wg_swz(hrow, p.hsb) : trswz(hrow));
     // input column of this halo column (stride 2: column-split layout), -1 = padding / out of range
     const int col = ST == 1 ? wc - 1 : (wc < p.hwh ? 2 * wc - 1 : (wc < 2 * p.hwh ? 2 * (wc - p.hwh) : -1));
     hcol[j] = hrow < p.nh && col >= 0 && col < p.W;
@@ -152,7 +172,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   }
   // ---- dy DMA: row t = wave*8 + lane/8 of the 64-pixel step
   const int trow = wave * 8 + (lane >> 3);
-  const int dcol = k0 + (((lane & 7) ^ trswz(trow)) * 8);
+  const int dcol = k0 + (((lane & 7) ^ (ST == 1 ? wg_swz(trow, p.dsb) : trswz(trow))) * 8);
 
   auto stage = [&](char* sb, int step) {
     const int m0 = step * 64;
@@ -171,13 +191,16 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     if constexpr (SC) glds16(p.dsc + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + 8192 + wave * 1024);
   };
 
-  // ---- per-lane halo rows of the pixels this lane reads: t = ks*32 + 8*(lane>>4) + (lane&15)/4 (+4)
+  // ---- per-lane halo rows of the pixels this lane reads (wg_pixel; pmap 0: t = ks*32 + 8*(lane>>4) +
+  // (lane&15)/4 (+4))
+  const int pmap = ST == 1 ? p.pmap : 0;
+  const int hsb = ST == 1 ? p.hsb : 3, dsb = ST == 1 ? p.dsb : 3;
   int hm[2][2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int t = ks * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2) + 4 * h;
+      const int t = wg_pixel(pmap, ks, lane >> 4, h, (lane & 15) >> 2);
       const int ii = t / p.spi, rem = t - ii * p.spi;
       const int pr = rem / p.wo, q = rem - pr * p.wo;
       hm[ks][h] = ii * p.hb + pr * (ST * W2) + q;
@@ -211,7 +234,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int ra = hm[ks][h] + toff;
-        const int f = (((ra >> 1) & 1) << 2) | (((ra >> 3) & 1) << 3);
+        const int f = wg_uswz(ra, hsb);
         aoff[ks][i][h] = (uint32_t)(ra * 128 + ((unit ^ f) << 3));
       }
     }
@@ -222,8 +245,8 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       const int unit = (cin >> 2) + pp;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int kr = ks * 32 + g * 8 + q + 4 * h;
-        const int f = (((kr >> 1) & 1) << 2) | (((kr >> 3) & 1) << 3);
+        const int kr = wg_pixel(pmap, ks, g, h, q);
+        const int f = wg_uswz(kr, dsb);
         boff[ks][j][h] = (uint32_t)(SG::HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
       }
     }
@@ -604,6 +627,11 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   p.nostore = option_get(OPT_WGRAD_DIAG) == 1;
   p.diag = option_get(OPT_WGRAD_DIAG);
   p.xcd = option_get(OPT_WGRAD_XCD);
+  p.pmap = 0; p.hsb = 3; p.dsb = 3;
+  if (option_get(OPT_WGRAD_PMAP) != 0) {
+    if (s.W >= 8) { p.pmap = 1; p.hsb = 2; p.dsb = 2; }
+    else if (s.W == 4 && s.H == 4) { p.pmap = 2; p.hsb = 2; p.dsb = 3; }
+  }
   const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
   p.slab_stride = (size_t)used * s.K * 9 * s.C;
   p.direct = used == 1 && dw != nullptr && option_get(OPT_WGRAD_DIRECT) != 0;
@@ -613,6 +641,7 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   dim3 grid((s.C / 64) * (s.K / 64), used, nprob);
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
   const bool deep = option_get(OPT_WGRAD_STAGES) >= 4;
+  const bool deeper = option_get(OPT_WGRAD_STAGES) >= 5;  // 5 stages: 160 KB at NR = 3 (the whole LDS)
   const int pf = option_get(OPT_WGRAD_PF);
   if (option_get(OPT_WGRAD_KERNEL) != 0) {  // one wave per SIMD (wgrad_halo4_kernel), 4-stage ring
 #define DTC_WH4(NR_, D_) hipLaunchKernelGGL((wgrad_halo4_kernel<4, NR_, D_>), grid, dim3(256), 0, st, p)
@@ -627,11 +656,11 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   if (nr <= 2) {
     if (pf >= 8) { if (deep) DTC_WH(4, 2, 8); else DTC_WH(2, 2, 8); }
     else if (pf > 0) { if (deep) DTC_WH(4, 2, 5); else DTC_WH(2, 2, 5); }
-    else { if (deep) DTC_WH(4, 2, 0); else DTC_WH(2, 2, 0); }
+    else { if (deeper) DTC_WH(5, 2, 0); else if (deep) DTC_WH(4, 2, 0); else DTC_WH(2, 2, 0); }
   } else {
     if (pf >= 8) { if (deep) DTC_WH(4, 3, 8); else DTC_WH(2, 3, 8); }
     else if (pf > 0) { if (deep) DTC_WH(4, 3, 5); else DTC_WH(2, 3, 5); }
-    else { if (deep) DTC_WH(4, 3, 0); else DTC_WH(2, 3, 0); }
+    else { if (deeper) DTC_WH(5, 3, 0); else if (deep) DTC_WH(4, 3, 0); else DTC_WH(2, 3, 0); }
   }
 #undef DTC_WH
   DTC_LAUNCH_CHECK();

@@ -422,9 +422,13 @@ def test_side_stream_wgrad_matches_serial(dtc, cuda, graphs):
 def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
     """BN coefficients computed inside the apply kernels (option bn_fused_fin=1, default) vs the
     separate finalize launches: same fp64 slot sums in a different (fixed) combination order, so
-    losses, gradients, parameters and running statistics agree to rounding."""
+    losses, gradients, parameters and running statistics agree to rounding. The projection shortcut's
+    dgrad is computed separately in both arms (dgrad_scf=0): the fused-finalize executor would otherwise
+    fold it into conv1's class-(0, 0) dgrad as one fp32 sum (one bf16 rounding of dx instead of two), a
+    legitimate 1-ulp difference that 3 steps at lr 0.1 on 8 images amplify past rtol 1e-4."""
     lib = dtc._native.lib
     lib.dtc_set_option(b"bn_onepass", 0)  # the fused finalize of the two-pass kernels vs the separate one
+    lib.dtc_set_option(b"dgrad_scf", 0)
     try:
         la, ga, pa, ba = _train_steps(dtc, cuda, 3, graphs=graphs)
         lib.dtc_set_option(b"bn_fused_fin", 0)
@@ -434,6 +438,7 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
             lib.dtc_set_option(b"bn_fused_fin", 1)
     finally:
         lib.dtc_set_option(b"bn_onepass", 0)
+        lib.dtc_set_option(b"dgrad_scf", 1)
     np.testing.assert_allclose(la, lb, rtol=1e-4)
     assert rel_err(ga, gb) < 1e-3
     assert rel_err(pa, pb) < 1e-5
@@ -464,6 +469,54 @@ def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5, hw=32):
         dtc._native.lib.dtc_set_option(b"graphs", 1)
 
 
+@pytest.mark.parametrize("batch,hw", [(8, 32), (64, 32), (16, 8)])
+def test_wgrad_conflict_free_pixel_map_matches(dtc, cuda, batch, hw):
+    """Option wgrad_pmap=1: the weight-gradient halo kernel's tr reads with the bank-conflict-free pixel map and
+    swizzle (HaloParams::pmap, tools/tr_banks.py) vs the original map: the MFMA reduction order within a
+    k-step changes, nothing else -- every gradient within fp32 rounding (W = 32 / 16 / 8 / 4 all covered:
+    hw 32 has layers of width 32..4, hw 8 has 8..1)."""
+    lib = dtc._native.lib
+    try:
+        lib.dtc_set_option(b"wgrad_pmap", 0)
+        ga = _grads_repeated(dtc, cuda, 1, batch=batch, hw=hw)
+        lib.dtc_set_option(b"wgrad_pmap", 1)
+        gb = _grads_repeated(dtc, cuda, 1, batch=batch, hw=hw)
+    finally:
+        lib.dtc_set_option(b"wgrad_pmap", 0)
+    for rep in range(2):
+        assert np.isfinite(gb[rep]).all()
+        assert rel_err(gb[rep], ga[rep]) < 1e-5, (rep, rel_err(gb[rep], ga[rep]))
+
+
+@pytest.mark.parametrize("bnb_mask", [0, 1])
+def test_halo_staged_dgrad_epilogue_matches(dtc, cuda, bnb_mask):
+    """Option halo_stage_epi=1: conv_halo's DGRAD epilogue staged through LDS (16-B coalesced residual /
+    output / BN-input accesses) vs the per-fragment epilogue. Without the fused BN backward the same fp32
+    value is rounded once: bit-identical gradients; with it (bnb_mask=1) the per-channel sums are added in
+    another order (tolerance as test_bn_sums_in_dgrad_epilogues_match_reduce_pass)."""
+    lib = dtc._native.lib
+    lay = dtc.nn.Layout(100, 25.0)
+    try:
+        lib.dtc_set_option(b"bnb_mask", bnb_mask)
+        lib.dtc_set_option(b"halo_stage_epi", 0)
+        ga = _grads_repeated(dtc, cuda, 1, batch=64)
+        lib.dtc_set_option(b"halo_stage_epi", 1)
+        gb = _grads_repeated(dtc, cuda, 1, batch=64)
+    finally:
+        lib.dtc_set_option(b"halo_stage_epi", 0)
+        lib.dtc_set_option(b"bnb_mask", 0)
+    for rep in range(2):
+        if not bnb_mask:
+            np.testing.assert_array_equal(ga[rep], gb[rep])
+            continue
+        assert np.isfinite(gb[rep]).all()
+        for pe in lay.params:
+            a = ga[rep][pe.offset:pe.offset + pe.numel]
+            b = gb[rep][pe.offset:pe.offset + pe.numel]
+            tol = 1e-5 if pe.name.startswith(("linear", "layer4.1.conv2", "layer4.1.bn2")) else 1e-2
+            assert rel_err(b, a) < tol, (rep, pe.name, rel_err(b, a))
+
+
 @pytest.mark.parametrize("graphs", [True, False])
 def test_wgrad_batch_matches_unbatched(dtc, cuda, graphs):
     """Deferred, batched 3x3 weight gradients (option wgrad_batch=4, default: one halo launch per
@@ -488,9 +541,12 @@ def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
     """Mask-bit BN backward (option bn_mask=1, default: the forward BN apply writes the ReLU mask as
     bits, the reduction stores no dz, the apply forms dz from dy and the bits) vs masking with the
     bf16 outputs and a stored dz: masking is exact and the sums run in the same order, so gradients
-    agree to the fp64 slot-atomic order (capture and replay), and so do three training steps."""
+    agree to the fp64 slot-atomic order (capture and replay), and so do three training steps. The
+    shortcut's dgrad stays a separate launch in both arms (dgrad_scf=0: the bn_mask=0 executor has no
+    fused form; see test_fused_bn_finalize_matches_separate)."""
     lib = dtc._native.lib
     lib.dtc_set_option(b"bn_onepass", 0)  # the two-pass kernels: the same summation order as bn_mask=0
+    lib.dtc_set_option(b"dgrad_scf", 0)
     try:
         ga = _grads_repeated(dtc, cuda, graphs)
         la, _, pa, ba = _train_steps(dtc, cuda, 3, graphs=graphs)
@@ -502,6 +558,7 @@ def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
             lib.dtc_set_option(b"bn_mask", 1)
     finally:
         lib.dtc_set_option(b"bn_onepass", 0)
+        lib.dtc_set_option(b"dgrad_scf", 1)
     for rep in range(2):
         assert rel_err(ga[rep], gb[rep]) < 1e-6, rep
     np.testing.assert_allclose(la, lb, rtol=1e-4)
@@ -713,25 +770,31 @@ def test_stem_weight_lds_matches_gather(dtc, cuda, batch, hw):
 
 def test_head_direct_matches_copy(dtc, cuda):
     """Option head_direct: the head kernel launched after the forward graph straight into the caller's
-    logits vs the graph-owned logits + copy: identical logits and gradients (train and eval)."""
+    logits (1), or inside the graph with its destination read from a pointer slot the input-copy launch
+    stores (2, default), vs the graph-owned logits + copy (0): identical logits and gradients (train and
+    eval). Mode 2 also keeps every call's output where that call asked for it: logits of consecutive
+    forwards into different tensors stay distinct (the slot is per call, not baked into the graph)."""
     lib = dtc._native.lib
+    res = {}
     try:
-        lib.dtc_set_option(b"head_direct", 0)
-        ga = _grads_repeated(dtc, cuda, 1, batch=16)
-        model, _, x, _ = _setup(dtc, cuda, 16, seed=3)
-        xd = torch.from_numpy(x).to(cuda)
-        with torch.no_grad():
-            model.eval()
-            ea = _np(model(xd))
-        lib.dtc_set_option(b"head_direct", 1)
-        gb = _grads_repeated(dtc, cuda, 1, batch=16)
-        with torch.no_grad():
-            eb = _np(model(xd))
+        for mode in (0, 1, 2):
+            lib.dtc_set_option(b"head_direct", mode)
+            g = _grads_repeated(dtc, cuda, 1, batch=16)
+            model, _, x, _ = _setup(dtc, cuda, 16, seed=3)
+            xd = torch.from_numpy(x).to(cuda)
+            with torch.no_grad():
+                model.eval()
+                e1 = model(xd)
+                e2 = model(xd * 0.5)  # a second output tensor: must not overwrite e1
+                res[mode] = (g, _np(e1), _np(e2))
     finally:
         lib.dtc_set_option(b"head_direct", DEFAULT_HEAD_DIRECT)
-    for rep in range(2):
-        np.testing.assert_array_equal(ga[rep], gb[rep])
-    np.testing.assert_array_equal(ea, eb)
+    for mode in (1, 2):
+        for rep in range(2):
+            np.testing.assert_array_equal(res[0][0][rep], res[mode][0][rep])
+        np.testing.assert_array_equal(res[0][1], res[mode][1])
+        np.testing.assert_array_equal(res[0][2], res[mode][2])
+    assert not np.array_equal(res[2][1], res[2][2])
 
 
 def test_graph_recapture_on_option_change(dtc, cuda):
@@ -757,6 +820,7 @@ def test_live_conv_profile(dtc, cuda):
     crit = dtc.CrossEntropyLoss()
     xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
     dtc._native.lib.dtc_set_option(b"sc_fuse", 0)  # one launch per conv (sc_fuse merges conv1 + shortcut)
+    dtc._native.lib.dtc_set_option(b"dgrad_scf", 0)  # (and dgrad_scf their dgrads)
     try:
         crit(model(xd), yd).backward()
         exe = model.executor(8, 32, 32)
@@ -768,6 +832,7 @@ def test_live_conv_profile(dtc, cuda):
         dtc._native.call("dtc_rn18_profile_end", exe.handle, ms, fl, cnt)
     finally:
         dtc._native.lib.dtc_set_option(b"sc_fuse", DEFAULT_SC_FUSE)
+        dtc._native.lib.dtc_set_option(b"dgrad_scf", 1)
     # 20 convs; the stem has no dgrad; the 13 stride-1 3x3 weight gradients run batched per geometry
     # within a DDP bucket (layer4 3, layer3 3, layer2 3, layer1 4: four launches) beside the 7 others
     assert list(cnt) == [20 * steps, 19 * steps, 11 * steps]
