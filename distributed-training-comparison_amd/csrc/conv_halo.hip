@@ -81,6 +81,12 @@ struct HConvParams {
   const u16* wsc;  // [Cout][C]
   u16* out2;
   double* stats2;
+  // general tile geometry (GEN kernels, stride 1; option halo_gen): a tile is grs rows x gseg columns of one
+  // image in BN slots (slot l < grs * gseg: row l / gseg, column l % gseg; the rest padded: read any halo
+  // row, stored nowhere), its halo (grs + 2) x (gseg + 2) pixels addressed from a 64-bit per-tile base --
+  // the 224x224 model's 224 / 112 / 56 / 28-wide rows (seg 56 or the row, activations past 2 GB)
+  int gseg, grs, gtpi, gspr;
+  FastDiv fd_gtpi, fd_gspr;
   // DGRAD without split-K (option halo_stage_epi): the fp32 tile is staged through LDS and written /
   // combined with its residual, mask bits and BN inputs in 16-B row pieces of 8 channels per lane
   // (coalesced), instead of 8-B pieces strided by the channel count per lane
@@ -191,7 +197,8 @@ __device__ __forceinline__ void dgrad_staged_epilogue(const HConvParams& p, floa
   }
 }
 
-template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP, int WS, int ST = 1, bool SC = false>
+template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP, int WS, int ST = 1, bool SC = false,
+          bool GEN = false>
 __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) {
   constexpr int FM = BM / (WR * 16);
   constexpr int FN = BN / (WC * 16);
@@ -203,6 +210,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   static_assert(WR * WC == 4 && HCAP % 32 == 0 && (WS == 2 || WS == 3), "shape");
   static_assert(ST == 1 || (ST == 2 && MODE == 0 && NHB == 1), "stride 2: forward, single halo buffer");
   static_assert(!SC || (ST == 2 && WS == 3), "shortcut fusion: stride-2 forward, 3-slot weight ring");
+  static_assert(!GEN || (ST == 1 && !SC), "general tile geometry: stride 1");
   __shared__ __attribute__((aligned(1024))) char smem[NHB * HBYTES + WS * WBYTES + SCBYTES];
   char* const wbase = smem + NHB * HBYTES;
   char* const scbase = wbase + WS * WBYTES;
@@ -217,8 +225,13 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   const int ta = bid % p.tiles_a, tb = bid / p.tiles_a;
   const int a0 = ta * BM;
   const int split = blockIdx.y, c0 = split * p.nchunk;  // first reduction chunk of this split
-  int n0, y0;
-  if (p.imgs == 1) {
+  int n0, y0, q0 = 0;
+  if constexpr (GEN) {
+    n0 = (int)fdiv((uint32_t)tb, p.fd_gtpi);
+    const int rem = tb - n0 * p.gtpi, yb = (int)fdiv((uint32_t)rem, p.fd_gspr);
+    y0 = yb * p.grs;
+    q0 = (rem - yb * p.gspr) * p.gseg;
+  } else if (p.imgs == 1) {
     n0 = tb / p.tiles_y;
     y0 = (tb - n0 * p.tiles_y) * p.rows;
   } else {
@@ -226,8 +239,19 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     y0 = 0;
   }
   const int W2 = p.pitch;
-  const int px0 = (n0 * p.Ho + y0) * p.Wo;
+  const int px0 = (n0 * p.Ho + y0) * p.Wo + q0;
   const int M = p.N * p.Ho * p.Wo;
+  // output pixel of tile slot l (M: a padded slot of the general geometry -- every epilogue skips pix >= M)
+  auto slot_pix = [&](int l) -> int {
+    if constexpr (GEN) {
+      if (l >= p.grs * p.gseg) return M;
+      const int r = l / p.gseg;
+      return px0 + r * p.Wo + (l - r * p.gseg);
+    }
+    return px0 + l;
+  };
+  // GEN: the halo box corner (input row y0 - 1, column q0 - 1) as a 64-bit base; DMA offsets are relative
+  const u16* const gsrc = GEN ? p.src + ((int64_t)(n0 * p.H + y0 - 1) * p.W + (q0 - 1)) * p.Cin : p.src;
   const int lrow = lane >> 3, pc = lane & 7;
   const int RSC = 9 * p.C;
 
@@ -262,7 +286,14 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
       const int i = (int)fdiv((uint32_t)hr, p.fd_hb), rem = hr - i * p.hb;
       const int hy = (int)fdiv((uint32_t)rem, p.fd_w2), hx = rem - hy * W2;
       int y, x;
-      if constexpr (ST == 1) {
+      if constexpr (GEN) {
+        y = y0 + hy - 1;
+        x = q0 + hx - 1;
+        if (n0 < p.N && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W)
+          off = (uint32_t)(((hy * p.W + hx) * p.Cin + (pc ^ hswz(hr)) * 8) * 2);
+        hoff[q] = off;
+        continue;
+      } else if constexpr (ST == 1) {
         y = y0 + hy - 1;
         x = hx - 1;
       } else {  // column-split halo: input row 2*y0 - 1 + hy, padded column 2*hx or 2*(hx - hwh) + 1
@@ -280,7 +311,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     for (int q = 0; q < NHI; ++q) {
       if (q >= q_lo && q < q_hi && q < p.nhi) {
         const uint32_t o = hoff[q] == 0x80000000u ? 0x80000000u : hoff[q] + (uint32_t)(cc * 128);
-        buf_lds16(p.src, p.src_bytes, dst + (wave + 4 * q) * 1024, o);
+        buf_lds16(gsrc, GEN ? 0x7ffffff0u : p.src_bytes, dst + (wave + 4 * q) * 1024, o);
       }
     }
   };
@@ -289,11 +320,16 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   const int wr = wave / WC, wc = wave % WC;
   const int arow0 = wr * (BM / WR), bcol0 = wc * (BN / WC);
   const int spx = p.rows * p.Wo;  // pixels per image slice
-  const int fpx = ST == 1 ? frag_pixel(lane & 15, p.W) : (lane & 15);
+  const int fpx = ST == 1 && !GEN ? frag_pixel(lane & 15, p.W) : (lane & 15);
   int hbr[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int l = bcol0 + j * 16 + fpx;
+    if constexpr (GEN) {  // slot -> (row, column) of the tile; padded slots read halo row 0
+      const int r = l / p.gseg;
+      hbr[j] = l < p.grs * p.gseg ? r * W2 + (l - r * p.gseg) : 0;
+      continue;
+    }
     const int i = (int)fdiv((uint32_t)l, p.fd_spx), rem = l - i * spx;
     const int y = (int)fdiv((uint32_t)rem, p.fd_w), x = rem - y * p.Wo;
     hbr[j] = i * p.hb + y * (ST * W2) + x;
@@ -464,7 +500,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
 
   // ---- epilogue: D[row = output channel][col = pixel], 4 consecutive channels per lane
   const int rq = (lane >> 4) * 4, cl = fpx;  // column -> pixel, as in the B fragments
-  constexpr bool kStageFits = MODE == 1 && BN * BM * 4 <= (int)sizeof(smem) && BM * 8 <= 256 * 8;
+  constexpr bool kStageFits = MODE == 1 && !GEN && BN * BM * 4 <= (int)sizeof(smem) && BM * 8 <= 256 * 8;
   if constexpr (kStageFits) {
     if (p.slab == nullptr && p.staged) {
       dgrad_staged_epilogue<BM, BN, FM, FN>(p, (float*)smem, acc, arow0, bcol0, rq, cl, px0, a0, M);
@@ -476,7 +512,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     float* slab = p.slab + (size_t)split * M * p.Cout;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int pix = px0 + bcol0 + j * 16 + cl;
+      const int pix = slot_pix(bcol0 + j * 16 + cl);
       if (pix >= M) continue;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -493,7 +529,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
         float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-          const int pix = px0 + bcol0 + j * 16 + cl;
+          const int pix = slot_pix(bcol0 + j * 16 + cl);
           const f32x4 a = second ? A[SC ? i : 0][SC ? j : 0] : B[i][j];
           float v[4];
 #pragma unroll
@@ -558,7 +594,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
       uint2 rr[FN], yy[FN], xx[FN], x2[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int pix = px0 + bcol0 + j * 16 + cl;
+        const int pix = slot_pix(bcol0 + j * 16 + cl);
         const size_t o = (size_t)(pix < M ? pix : 0) * p.Cout + ch;
         rr[j] = has_res ? *(const uint2*)(p.res + o) : uint2{0u, 0u};
         yy[j] = p.bnb.mb ? bnb_bits_as_y(p.bnb.mb, o) : *(const uint2*)(p.bnb.ym + o);
@@ -567,7 +603,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int pix = px0 + bcol0 + j * 16 + cl;
+        const int pix = slot_pix(bcol0 + j * 16 + cl);
         const bool ok = pix < M;
         float v[4] = {acc[i][j][0] + bf_lo(rr[j].x), acc[i][j][1] + bf_hi(rr[j].x), acc[i][j][2] + bf_lo(rr[j].y),
                       acc[i][j][3] + bf_hi(rr[j].y)};
@@ -603,7 +639,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   } else {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int pix = px0 + bcol0 + j * 16 + cl;
+      const int pix = slot_pix(bcol0 + j * 16 + cl);
       if (pix >= M) continue;
       uint2 rr[FM];  // the residuals of all FM fragments in flight before the first store
 #pragma unroll
@@ -696,6 +732,27 @@ static int halo_tiles_b(const ConvShape& s, const HaloGeom& g) {
   return g.imgs == 1 ? s.N * (g.ho / g.rows) : (s.N + g.imgs - 1) / g.imgs;
 }
 
+// General tile geometry (stride 1, option halo_gen): gseg columns per row segment (the row if it has at most
+// 64 pixels, else a 64- / 56- / 32-pixel piece of it), grs rows of segments per tile (the most that fit BN
+// slots and divide H). Used where the classic whole-row / whole-image tiles do not fit (the 224x224 model).
+struct HaloGen {
+  int seg = 0, rs = 0, spr = 0, tpi = 0, nh = 0;
+};
+static bool halo_gen_geometry(const ConvShape& s, int bn, int hcap, HaloGen& g) {
+  if (option_get(OPT_HALO_GEN) == 0) return false;
+  if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.C % 64 == 0 && s.K % 64 == 0)) return false;
+  g.seg = s.W <= 64 ? s.W : s.W % 64 == 0 ? 64 : s.W % 56 == 0 ? 56 : s.W % 32 == 0 ? 32 : 0;
+  if (g.seg == 0 || g.seg > bn) return false;
+  g.rs = std::min(bn / g.seg, s.H);
+  while (g.rs > 1 && s.H % g.rs != 0) --g.rs;
+  g.spr = s.W / g.seg;
+  g.tpi = (s.H / g.rs) * g.spr;
+  g.nh = (g.rs + 2) * (g.seg + 2);
+  // at least half the slots real; 32-bit per-tile offsets and pixel indices
+  return g.nh <= hcap && 2 * g.rs * g.seg >= bn && (int64_t)s.N * g.tpi < (1ll << 31) &&
+         (int64_t)s.N * s.H * s.W < (1ll << 31) && (int64_t)(g.rs + 2) * s.W * std::max(s.C, s.K) * 2 < (1ll << 31);
+}
+
 static bool cfg_fits(const ConvShape& s, int cfg, int cout) {
   HaloGeom g;
   const HaloCfg& c = kHaloCfgs[cfg];
@@ -718,10 +775,24 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
     return hp;  // no split-K: the shortcut fusion and the BN statistics live in the epilogue
   }
   const int opt = option_get(OPT_HALO_CONV);
-  if (opt == 0 || !halo_shape_ok(s, 1)) return hp;
+  if (opt == 0) return hp;
   const int cout = mode == CONV_FWD ? s.K : s.C;
   const int cin = mode == CONV_FWD ? s.C : s.K;
   const int nchunk = cin / 64;
+  if (!halo_shape_ok(s, 1) || (opt == 1 && !cfg_fits(s, 0, cout) && !cfg_fits(s, 2, cout) && !cfg_fits(s, 6, cout))) {
+    // the general tile geometry: 64 x 256 tiles (4 rows of a 56-pixel segment at 224 / 112 / 56 wide rows), or
+    // 64 x 128 where the tile count would leave CUs idle; no split-K (these layers have >= 1024 tiles)
+    HaloGen g0, g2;
+    const bool f0 = cout % 64 == 0 && halo_gen_geometry(s, 256, 416, g0);
+    const bool f2 = cout % 64 == 0 && halo_gen_geometry(s, 128, 288, g2);
+    if (f0 && (int64_t)s.N * g0.tpi * (cout / 64) >= 512) hp.cfg = 0;
+    else if (f2) hp.cfg = 2;
+    else if (f0) hp.cfg = 0;
+    else return hp;
+    hp.gen = 1;
+    hp.split = 1;
+    return hp;
+  }
   auto tiles = [&](int cfg) {
     HaloGeom g;
     const HaloCfg& c = kHaloCfgs[cfg];
@@ -781,6 +852,17 @@ static int launch_halo(const HConvParams& p, int cfg, dim3 grid, hipStream_t st)
   return launch_halo_ws<MODE, 2>(p, cfg, grid, st);
 }
 
+// general tile geometry instances (3-slot weight ring): configurations 0 (64 x 256) and 2 (64 x 128)
+template <int MODE>
+static int launch_halo_gen(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
+  if (cfg == 0)
+    hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 256, 1, 4, 1, 416, 3, 1, false, true>), grid, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 1, 288, 3, 1, false, true>), grid, dim3(256), 0, st, p);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 // stride-2 forward instances (3-slot weight ring), with or without the fused shortcut
 template <bool SC>
 static int launch_halo_s2(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
@@ -793,12 +875,52 @@ static int launch_halo_s2(const HConvParams& p, int cfg, dim3 grid, hipStream_t 
   return 0;
 }
 
+static int conv_halo_general(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
+                             const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
+                             const BnbArgs* bnb) {
+  DTC_CHECK_ARG(hp.cfg == 0 || hp.cfg == 2, "conv_halo: general geometry needs configuration 0 or 2");
+  const HaloCfg& c = kHaloCfgs[hp.cfg];
+  HaloGen g;
+  DTC_CHECK_ARG(halo_gen_geometry(s, c.bn, c.hcap, g), "conv_halo: general geometry does not fit config %d", hp.cfg);
+  HConvParams p{};
+  p.src = src; p.w = w; p.out = out; p.res = res; p.stats = stats;
+  p.N = s.N; p.H = s.H; p.W = s.W; p.C = s.C;
+  p.Cin = mode == CONV_FWD ? s.C : s.K;
+  p.Cout = mode == CONV_FWD ? s.K : s.C;
+  DTC_CHECK_ARG(p.Cout % c.bm == 0, "conv_halo: output channels %d not a multiple of %d", p.Cout, c.bm);
+  p.rows = g.rs; p.imgs = 1; p.nh = g.nh; p.hb = g.nh;
+  p.Ho = s.H; p.Wo = s.W; p.pitch = g.seg + 2; p.hwh = 0;
+  p.gseg = g.seg; p.grs = g.rs; p.gtpi = g.tpi; p.gspr = g.spr;
+  p.fd_gtpi = make_fastdiv(g.tpi);
+  p.fd_gspr = make_fastdiv(g.spr);
+  p.slab = nullptr;  // (no split-K: >= 1024 tiles at the sizes this geometry serves)
+  p.src_bytes = 0;
+  p.nhi = (p.nh + 31) / 32;
+  p.tiles_y = s.H / g.rs;
+  p.tiles_a = p.Cout / c.bm;
+  p.nchunk = p.Cin / 64;
+  p.xcd_remap = option_get(OPT_XCD_REMAP);
+  p.fd_hb = make_fastdiv(p.hb);
+  p.fd_w2 = make_fastdiv(p.pitch);
+  p.fd_spx = make_fastdiv(g.rs * g.seg);
+  p.fd_w = make_fastdiv(s.W);
+  p.ts = ts;
+  p.staged = 0;
+  if (bnb != nullptr) p.bnb = *bnb;
+  (void)slab; (void)slab_bytes;
+  const int64_t ntiles = (int64_t)s.N * g.tpi * p.tiles_a;
+  DTC_CHECK_ARG(ntiles < (1ll << 31), "conv_halo: too many tiles");
+  const dim3 grid((unsigned)ntiles, 1);
+  return mode == CONV_FWD ? launch_halo_gen<0>(p, hp.cfg, grid, st) : launch_halo_gen<1>(p, hp.cfg, grid, st);
+}
+
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
               const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
               const BnbArgs* bnb, const u16* wsc, u16* out2, double* stats2) {
   DTC_CHECK_ARG(hp.cfg >= 0 && hp.cfg < kNumHaloCfgs && (mode == CONV_FWD || mode == CONV_DGRAD),
                 "conv_halo: unsupported configuration");
   const HaloCfg& c = kHaloCfgs[hp.cfg];
+  if (hp.gen) return conv_halo_general(s, mode, hp, src, w, out, res, stats, slab, slab_bytes, st, ts, bnb);
   DTC_CHECK_ARG(halo_shape_ok(s, c.st) && (c.st == 1 || mode == CONV_FWD), "conv_halo: unsupported shape / pass");
   DTC_CHECK_ARG(wsc == nullptr || (c.st == 2 && out2 != nullptr), "conv_halo: the shortcut fusion is stride-2 FWD");
   HConvParams p{};

@@ -41,7 +41,7 @@ enum {
   OPT_STEM_DIRECT = 22,    // executor (at plan time): 1 = direct stem conv (stem.hip), 0 = im2col + GEMM
   OPT_WGRAD_XCD = 23,      // wgrad_halo: 1 (default) = the tiles of one (problem, split) run on one XCD
   OPT_WGRAD_DIRECT = 24,   // wgrad_halo: 1 = a one-split launch writes the scaled dw itself (no reduce)
-  OPT_WGRAD_DEFER = 25,    // executor: 1 = batched wgrads forked after the layer's last dgrad (see resnet.cpp)
+  OPT_WGRAD_DEFER = 25,    // executor: 1 = batched wgrads forked after the layer's last dgrad (see resnet.cpp); 2 = layer1 only
   OPT_IGEMM_TILE = 26,     // igemm FWD/DGRAD/WGRAD tile: 0 auto, 1 = 64x64, 2 = 128x128, 3 = 64x256 (tuning)
   OPT_IGEMM_SPLIT = 27,    // igemm split-K: 0 auto, k = k splits where the plan allows (tuning)
   OPT_BN_ONEPASS = 28,     // executor: 1 = one-pass BN backward (bn_bwd_fused, grid barrier) where it has a
@@ -98,6 +98,11 @@ enum {
   OPT_HALO_STAGE_EPI = 52,  // conv_halo DGRAD (no split-K): 1 = the tile staged through LDS and written / combined
                             // with residual, mask bits and BN inputs by 16-B row pieces (coalesced). Default 0:
                             // neutral in-step (+-0.4%), 1 us slower on the layer2 dgrad alone
+  OPT_WGRAD_GEN = 53,      // wgrad_halo: 1 (default) = the general step geometry (row segments, 64-bit per-step
+                           // bases) for stride-1 3x3 shapes the classic 64-pixel whole-row steps do not fit
+                           // (the 224x224 model); 0 = those go to the implicit GEMM
+  OPT_HALO_GEN = 54,       // conv_halo: 1 (default) = the general tile geometry for stride-1 3x3 shapes the classic
+                           // whole-row tiles do not fit (the 224x224 model); 0 = those go to the implicit GEMM
   OPT_COUNT
 };
 int option_get(int id);
@@ -177,6 +182,7 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
              hipStream_t st, u64* ts, const BnbArgs* bnb = nullptr);
 struct HaloPlan {
   int cfg, split;
+  int gen = 0;  // 1: general tile geometry (rows of seg columns, 64-bit tile bases; conv_halo.hip)
 };
 HaloPlan conv_halo_plan(const ConvShape& s, int mode);
 size_t conv_halo_slab_bytes(const ConvShape& s, int mode);  // fp32 split-K slab the plan needs

@@ -1245,7 +1245,10 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     // option wgrad_defer: the halo-geometry wgrads are only queued here; their batched launch is forked
     // after the layer's last dgrad (below), so it overlaps the HBM-bound BN chain that follows rather
     // than the dgrads (measured -1% at B=256: the wgrad batch then starves the BN kernels instead)
-    const bool defer = option_get(OPT_WGRAD_DEFER) != 0;
+    // (wgrad_defer = 2: layer1 only -- its 4-conv batch then runs beside the stem's tail instead of beside
+    // layer1.0's last dgrad, the persistent conv_c64 kernel that wants every CU)
+    const int dopt = option_get(OPT_WGRAD_DEFER);
+    const bool defer = dopt == 1 || (dopt == 2 && bi < 2);
     // option wgrad_tail: smaller batches for layer1, whose last batch is the backward's tail
     const int bcap = bi < 2 ? option_get(OPT_WGRAD_TAIL) : 0;
     const bool lazy = option_get(OPT_FORK_LAZY) != 0 && !defer;

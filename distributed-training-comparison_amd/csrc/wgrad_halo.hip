@@ -63,6 +63,12 @@ struct HaloParams {
   // pixels of one image row per half-read; bits 1 and 2) and pmap 2 (4x4 images: rows r and r ^ 2 of one
   // image per half-read; halo bits 1, 2, dy bits 1, 3) are conflict-free for every tap (tools/tr_banks.py)
   int pmap, hsb, dsb;
+  // general geometry (GEN kernels; stride 1, e.g. the 224x224 model's 224/112/56/28-wide rows): a step is
+  // rs rows x seg columns of one image (rs * seg <= 64 real pixels; the remaining MFMA reduction slots of
+  // the 64-pixel step carry zero dy), its halo (rs + 2) x (seg + 2) pixels; every step addresses x and dy
+  // from a 64-bit per-step base, so an activation may exceed 2 GB (512 x 224 x 224 x 64 bf16 = 3.3 GB)
+  int seg, spimg;      // pixels per row segment, steps per image
+  FastDiv fd_spimg, fd_spr, fd_seg, fd_seg2;  // steps per image, segments per row, seg, seg + 2
 };
 
 // pixel (within the 64-pixel step) of k-step ks, lane block b = lane >> 4, tr read h, lane quad q
@@ -133,12 +139,13 @@ __device__ __forceinline__ bf16x8 frag_halo(const char* halo, int cin, int ra, i
 // window: the step's 22 operand fragments (per k-step: 2 dy, 9 halo) are read PF fragments ahead
 // of the MFMAs that consume them, one fragment (two ds_read_b64_tr_b16) issued per consumed halo
 // fragment, so an LDS read's latency hides behind the MFMAs of the PF fragments before it.
-template <int NS, int NR, int PF, int ST = 1, bool SC = false>
+template <int NS, int NR, int PF, int ST = 1, bool SC = false, bool GEN = false>
 __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   typedef WgStage<NR, SC> SG;
   constexpr int PER = NR + 1 + (SC ? 1 : 0);  // LDS-DMA instructions per wave per stage (halo rounds + dy (+ dsc))
   static_assert(ST == 1 || (ST == 2 && PF == 0), "stride 2: compiler-scheduled fragment reads");
   static_assert(!SC || ST == 2, "shortcut fusion: stride 2");
+  static_assert(!GEN || (ST == 1 && PF == 0 && !SC), "general geometry: stride 1, compiler-scheduled reads");
   __shared__ __attribute__((aligned(1024))) char smem[NS * SG::BYTES];
   stamp_start(p.ts);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -156,11 +163,21 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   const int W2 = p.pitch;
 
   // ---- halo DMA: round j covers LDS rows j*64 + wave*8 + lane/8, 16-B chunk lane%8
-  int hrel[NR], hrow_in[NR];
+  int hrel[NR], hrow_in[NR], hcc[NR];
   bool hcol[NR];
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int hrow = j * 64 + wave * 8 + (lane >> 3);
+    if constexpr (GEN) {  // halo row -> (row, column) of the step's (rs + 2) x (seg + 2) box, from its corner
+      const int hr = (int)fdiv((uint32_t)hrow, p.fd_seg2), hc = hrow - hr * (p.seg + 2);
+      const int src_chunk = (lane & 7) ^ wg_swz(hrow, p.hsb);
+      hcol[j] = hrow < p.nh;
+      hrow_in[j] = hr - 1;
+      hcc[j] = hc - 1;
+      hrel[j] = ((hr * p.W + hc) * p.C + c0 + src_chunk * 8) * 2;
+      continue;
+    }
+    hcc[j] = 0;
     const int ii = hrow / p.hb, rem = hrow - ii * p.hb;
     const int hr = rem / W2, wc = rem - hr * W2;
     const int src_chunk = (lane & 7) ^ (ST == 1 ? wg_swz(hrow, p.hsb) : trswz(hrow));
@@ -173,8 +190,31 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   // ---- dy DMA: row t = wave*8 + lane/8 of the 64-pixel step
   const int trow = wave * 8 + (lane >> 3);
   const int dcol = k0 + (((lane & 7) ^ (ST == 1 ? wg_swz(trow, p.dsb) : trswz(trow))) * 8);
+  // GEN: this lane's dy row of the step (pixel trow = (row, column) of the rs x seg segment; padded -> zero)
+  uint32_t drel = 0x80000000u;
+  if constexpr (GEN) {
+    const int tr = (int)fdiv((uint32_t)trow, p.fd_seg), tc = trow - tr * p.seg;
+    if (trow < p.rs * p.seg) drel = (uint32_t)(((tr * p.W + tc) * p.K + dcol) * 2);
+  }
 
+  auto stage_gen = [&](char* sb, int step) {  // GEN: per-step 64-bit bases, zero-fill out of the image
+    const int img = (int)fdiv((uint32_t)step, p.fd_spimg), r = step - img * p.spimg;
+    const int yb = (int)fdiv((uint32_t)r, p.fd_spr), qs = r - yb * (int)p.fd_spr.d;
+    const int y0 = yb * p.rs, q0 = qs * p.seg;
+    const u16* xb = px + ((int64_t)(img * p.H + y0 - 1) * p.W + (q0 - 1)) * p.C;  // the halo box corner
+    const u16* db = pdy + ((int64_t)(img * p.H + y0) * p.W + q0) * p.K;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const bool ok = hcol[j] && (unsigned)(y0 + hrow_in[j]) < (unsigned)p.H && (unsigned)(q0 + hcc[j]) < (unsigned)p.W;
+      buf_lds16(xb, 0x7ffffff0u, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)hrel[j] : 0x80000000u);
+    }
+    buf_lds16(db, 0x7ffffff0u, sb + SG::HALO_BYTES + wave * 1024, drel);
+  };
   auto stage = [&](char* sb, int step) {
+    if constexpr (GEN) {
+      stage_gen(sb, step);
+      return;
+    }
     const int m0 = step * 64;
     const int n0 = (int)fdiv((uint32_t)m0, p.fd_hw);
     const int p0 = (int)fdiv((uint32_t)(m0 - n0 * (int)p.fd_hw.d), p.fd_w) * ST;  // first INPUT row
@@ -201,6 +241,11 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int t = wg_pixel(pmap, ks, lane >> 4, h, (lane & 15) >> 2);
+      if constexpr (GEN) {  // padded slots (t >= rs * seg, zero dy) read any in-range halo row: row 0
+        const int pr = t / p.seg, q = t - pr * p.seg;
+        hm[ks][h] = t < p.rs * p.seg ? pr * W2 + q : 0;
+        continue;
+      }
       const int ii = t / p.spi, rem = t - ii * p.spi;
       const int pr = rem / p.wo, q = rem - pr * p.wo;
       hm[ks][h] = ii * p.hb + pr * (ST * W2) + q;
@@ -570,40 +615,69 @@ __global__ void __launch_bounds__(256, 1) wgrad_halo4_kernel(const HaloParams p)
 }
 
 // ---------------------------------------------------------------- host side
-static bool halo_geometry(const ConvShape& s, int& rs, int& imgs) {
+// Step geometry. Classic (gen = 0): 64-pixel steps of whole rows (rs = 64 / W) or whole images, tensors
+// under 2 GB (32-bit offsets). General (gen = 1, option wgrad_gen): rs rows x seg columns of one image per
+// step -- seg = W for rows of at most 64 pixels (rs = 64 / W, H a multiple of rs), else a 56- / 64- / 32-
+// pixel segment that divides the row -- with 64-bit per-step bases: the 224x224 model's 224 / 112 / 56 / 28
+// wide rows (56 real pixels per 64-slot step at every width).
+struct WgGeom {
+  int gen = 0, rs = 0, imgs = 1, seg = 0, spr = 1, spimg = 0, hb = 0, nh = 0;
+  int64_t nsteps = 0;
+};
+static bool wg_geometry(const ConvShape& s, WgGeom& g) {
   if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.C % 64 == 0 && s.K % 64 == 0)) return false;
-  if (s.W > 64 || 64 % s.W != 0) return false;
   const int hw = s.H * s.W;
-  if (hw % 64 == 0) {
-    rs = 64 / s.W;
-    imgs = 1;
-  } else if (64 % hw == 0) {
-    rs = s.H;
-    imgs = 64 / hw;
-  } else {
-    return false;
+  if (s.W <= 64 && 64 % s.W == 0 && (hw % 64 == 0 || 64 % hw == 0)) {
+    g.gen = 0;
+    if (hw % 64 == 0) {
+      g.rs = 64 / s.W;
+      g.imgs = 1;
+    } else {
+      g.rs = s.H;
+      g.imgs = 64 / hw;
+    }
+    g.hb = (g.rs + 2) * (s.W + 2);
+    g.nh = g.imgs * g.hb;
+    g.nsteps = (int64_t)s.N * hw / 64;
+    // whole 64-pixel steps only (multi-image steps need N a multiple of the images per step)
+    if (g.nh <= 192 && ((int64_t)s.N * hw) % 64 == 0 && (uint64_t)s.N * hw * s.C * 2 < (1ull << 31)) return true;
   }
-  const int nh = imgs * (rs + 2) * (s.W + 2);
-  // whole 64-pixel steps only (multi-image steps need N a multiple of the images per step)
-  return nh <= 192 && ((int64_t)s.N * hw) % 64 == 0 && (uint64_t)s.N * hw * s.C * 2 < (1ull << 31);
+  if (option_get(OPT_WGRAD_GEN) == 0) return false;
+  g = WgGeom{};
+  g.gen = 1;
+  if (s.W <= 64) {
+    g.seg = s.W;
+    g.rs = 64 / s.W;
+    if (s.H % g.rs != 0) return false;
+  } else {
+    g.seg = s.W % 64 == 0 ? 64 : s.W % 56 == 0 ? 56 : s.W % 32 == 0 ? 32 : 0;
+    if (g.seg == 0) return false;
+    g.rs = 1;
+  }
+  g.spr = s.W / g.seg;
+  g.spimg = (s.H / g.rs) * g.spr;
+  g.hb = g.nh = (g.rs + 2) * (g.seg + 2);
+  g.nsteps = (int64_t)s.N * g.spimg;
+  return g.nh <= 192 && g.rs * g.seg <= 64 && g.nsteps < (1ll << 31) &&
+         (int64_t)(g.rs + 2) * s.W * std::max(s.C, s.K) * 2 < (1ll << 31);
 }
 
 int wgrad_halo_splits(const ConvShape& s, int nprob) {
   const int target = option_get(OPT_WGRAD_HALO);
-  int rs = 0, imgs = 0;
-  if (target <= 0 || nprob < 1 || nprob > DTC_WG_BATCH || !halo_geometry(s, rs, imgs)) return 0;
+  WgGeom g;
+  if (target <= 0 || nprob < 1 || nprob > DTC_WG_BATCH || !wg_geometry(s, g)) return 0;
   const int tiles = (s.C / 64) * (s.K / 64);
-  const int nsteps = s.N * s.H * s.W / 64;
   int splits = std::max(1, target / (tiles * nprob));
-  splits = std::min(splits, std::max(1, nsteps / 4));  // >= 4 pixel steps per workgroup
+  splits = (int)std::min<int64_t>(splits, std::max<int64_t>(1, g.nsteps / 4));  // >= 4 pixel steps per workgroup
   return splits;
 }
 
 int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* slab, int splits,
                     int* used_splits, hipStream_t st, u64* ts, float* const* dw, float scale) {
-  int rs = 0, imgs = 0;
-  DTC_CHECK_ARG(halo_geometry(s, rs, imgs) && splits > 0 && nprob >= 1 && nprob <= DTC_WG_BATCH,
+  WgGeom g;
+  DTC_CHECK_ARG(wg_geometry(s, g) && splits > 0 && nprob >= 1 && nprob <= DTC_WG_BATCH,
                 "wgrad_halo: unsupported geometry");
+  const int rs = g.rs, imgs = g.imgs;
   HaloParams p{};
   for (int i = 0; i < nprob; ++i) {
     p.xs[i] = x[i];
@@ -611,24 +685,33 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   }
   p.slab = slab;
   p.N = s.N; p.H = s.H; p.W = s.W; p.C = s.C; p.K = s.K;
-  p.x_bytes = (uint32_t)((uint64_t)s.N * s.H * s.W * s.C * 2);
+  p.x_bytes = g.gen ? 0u : (uint32_t)((uint64_t)s.N * s.H * s.W * s.C * 2);
   p.fd_hw = make_fastdiv(s.H * s.W);
   p.fd_w = make_fastdiv(s.W);
-  p.nsteps = s.N * s.H * s.W / 64;
+  p.nsteps = (int)g.nsteps;
   p.steps_per_split = (p.nsteps + splits - 1) / splits;
   p.rs = rs;
-  p.hb = (rs + 2) * (s.W + 2);
-  p.nh = imgs * p.hb;
+  p.hb = g.hb;
+  p.nh = g.nh;
   p.spi = rs * s.W;
-  p.pitch = s.W + 2;
+  p.pitch = (g.gen ? g.seg : s.W) + 2;
   p.ho = s.H;
   p.wo = s.W;
+  if (g.gen) {
+    p.seg = g.seg;
+    p.spimg = g.spimg;
+    p.fd_spimg = make_fastdiv(g.spimg);
+    p.fd_spr = make_fastdiv(g.spr);
+    p.fd_seg = make_fastdiv(g.seg);
+    p.fd_seg2 = make_fastdiv(g.seg + 2);
+  }
+  (void)imgs;
   p.ts = ts;
   p.nostore = option_get(OPT_WGRAD_DIAG) == 1;
   p.diag = option_get(OPT_WGRAD_DIAG);
   p.xcd = option_get(OPT_WGRAD_XCD);
   p.pmap = 0; p.hsb = 3; p.dsb = 3;
-  if (option_get(OPT_WGRAD_PMAP) != 0) {
+  if (option_get(OPT_WGRAD_PMAP) != 0 && !g.gen) {
     if (s.W >= 8) { p.pmap = 1; p.hsb = 2; p.dsb = 2; }
     else if (s.W == 4 && s.H == 4) { p.pmap = 2; p.hsb = 2; p.dsb = 3; }
   }
@@ -643,6 +726,13 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   const bool deep = option_get(OPT_WGRAD_STAGES) >= 4;
   const bool deeper = option_get(OPT_WGRAD_STAGES) >= 5;  // 5 stages: 160 KB at NR = 3 (the whole LDS)
   const int pf = option_get(OPT_WGRAD_PF);
+  if (g.gen) {  // general geometry: 4-stage ring, compiler-scheduled fragment reads
+    if (nr <= 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, 2, 0, 1, false, true>), grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_halo_kernel<4, 3, 0, 1, false, true>), grid, dim3(512), 0, st, p);
+    DTC_LAUNCH_CHECK();
+    *used_splits = p.direct ? 0 : used;
+    return 0;
+  }
   if (option_get(OPT_WGRAD_KERNEL) != 0) {  // one wave per SIMD (wgrad_halo4_kernel), 4-stage ring
 #define DTC_WH4(NR_, D_) hipLaunchKernelGGL((wgrad_halo4_kernel<4, NR_, D_>), grid, dim3(256), 0, st, p)
     if (nr <= 2) { if (pf >= 6) DTC_WH4(2, 6); else DTC_WH4(2, 4); }

@@ -459,9 +459,18 @@ def test_amp_check_finite_positions(dtc, cuda, n):
     (2, 2, 2, 64, 64),      # 2x2 images: halo too tall -> generic loader
     (2, 4, 4, 512, 512),    # 32 pixels: no whole 64-pixel step -> generic loader
     (3, 4, 4, 64, 64),      # 48 pixels (N not a multiple of 4 images) -> generic loader
+    # general step geometry (option wgrad_gen; the 224x224 model's rows): rs rows x seg columns per step
+    (2, 14, 224, 64, 64),   # 56-pixel segments, 4 per row
+    (2, 12, 112, 64, 128),  # 56-pixel segments, 2 per row
+    (3, 10, 56, 128, 64),   # one 56-pixel row per step
+    (2, 28, 28, 256, 128),  # two 28-pixel rows per step
+    (2, 6, 96, 64, 64),     # 32-pixel segments
+    (1, 5, 40, 64, 64),     # one 40-pixel row per step (24 padded slots)
 ])
 def test_conv_wgrad_halo(dtc, cuda, case):
-    """Halo-tiled 3x3 weight gradient == generic loader == oracle (fp32 sums of exact products)."""
+    """Halo-tiled 3x3 weight gradient == generic loader == oracle (fp32 sums of exact products); the rows
+    wider than 64 pixels or not dividing 64 run the general-geometry kernels (per-step 64-bit bases, zero-dy
+    padded slots), which must match too."""
     N, H, W, C, K = case
     g = np.random.default_rng(7)
     x = _rand_bf16((N, H, W, C), g)
@@ -484,6 +493,8 @@ def test_conv_wgrad_halo(dtc, cuda, case):
     (8, 16, 16, 128, 128, 3),  # 2x2 output tiles, three problems
     (12, 4, 4, 512, 512, 4),   # multi-image halo, one split per problem
     (3, 8, 8, 64, 128, 2),     # ragged split of 3 steps
+    (2, 8, 224, 64, 64, 4),    # general geometry (56-pixel row segments), the 224x224 layer1 batch
+    (2, 14, 28, 128, 128, 3),  # general geometry, two 28-pixel rows per step
 ])
 def test_conv_wgrad_batch(dtc, cuda, case):
     """dtc_conv2d_wgrad_batch: n independent weight gradients in one halo launch (blockIdx.z =
@@ -552,6 +563,50 @@ def test_conv_halo_configs(dtc, cuda, case, cfg, split):
     np.testing.assert_allclose(s[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
     ref = O.conv2d_dgrad(dy, w, (H, W), 1, 1) + res
     assert rel_err(dx.float().cpu().numpy(), ref) < 1e-2
+
+
+GEN_CASES = [
+    # (N, H, W, C, K): stride-1 3x3 shapes the classic whole-row halo tiles do not fit (option halo_gen)
+    (2, 8, 224, 64, 64),     # 56-pixel row segments, 2 rows per 128-slot tile
+    (2, 6, 112, 128, 64),    # 2 segments per row, C > K
+    (3, 4, 56, 64, 128),     # one 56-pixel row segment per row
+    (2, 8, 28, 128, 128),    # 4 rows of 28 per 128-slot tile
+    (32, 8, 224, 64, 128),   # >= 512 tiles: the 64 x 256 configuration (4 rows of a segment)
+]
+
+
+@pytest.mark.parametrize("case", GEN_CASES)
+def test_conv_halo_general_geometry(dtc, cuda, case):
+    """conv_halo's general tile geometry (rows of 56- / 28-pixel segments, padded slots, 64-bit per-tile
+    bases; the 224x224 model's layers): FWD (+BN statistics: padded slots must not count) and DGRAD
+    (+residual) against the oracle, and against the implicit GEMM (option halo_gen=0) on the same operands."""
+    N, H, W, C, K = case
+    g = np.random.default_rng(41)
+    x = _rand_bf16((N, H, W, C), g)
+    w = _rand_bf16((K, 3, 3, C), g, 0.05)
+    dy = _rand_bf16((N, H, W, K), g)
+    res = _rand_bf16((N, H, W, C), g)
+    xd, wd, dyd, rd = (_to_dev_bf16(a, cuda) for a in (x, w, dy, res))
+
+    def run():
+        stats = dtc.ops.new_stats(K, cuda)
+        y = dtc.ops.conv2d_fwd(xd, wd, 1, 1, stats=stats)
+        dx = dtc.ops.conv2d_dgrad(dyd, wd, (H, W), 1, 1, res=rd)
+        torch.cuda.synchronize()
+        return y.float().cpu().numpy(), stats.sum(0).cpu().numpy(), dx.float().cpu().numpy()
+
+    yk, s, dxk = run()
+    dtc._native.call("dtc_set_option", b"halo_gen", 0)
+    try:
+        yi, si, dxi = run()
+    finally:
+        dtc._native.call("dtc_set_option", b"halo_gen", 1)
+    assert rel_err(yk, O.conv2d_fwd(x, w, 1, 1)) < 1e-2
+    yb = yk.reshape(-1, K).astype(np.float64)
+    np.testing.assert_allclose(s[0], yb.sum(0), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
+    assert rel_err(dxk, O.conv2d_dgrad(dy, w, (H, W), 1, 1) + res) < 1e-2
+    assert rel_err(yk, yi) < 1e-2 and rel_err(dxk, dxi) < 1e-2
 
 
 C64_CASES = [(2, 32, 32), (3, 16, 16), (5, 32, 32)]
