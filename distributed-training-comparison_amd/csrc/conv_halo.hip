@@ -100,9 +100,10 @@ struct HConvParams {
 // (p.bnb) mask by the forward's ReLU bits (one byte = the 8 channels) or y, accumulate sum(dz) and
 // sum(dz * xhat) (+ the second BN's) per channel over its pixels; the per-thread partials are summed per
 // channel in LDS in a fixed order and added to the fp64 slots with one atomic per channel and workgroup.
-template <int BM, int BN, int FM, int FN>
+template <int BM, int BN, int FM, int FN, typename SlotPix>
 __device__ __forceinline__ void dgrad_staged_epilogue(const HConvParams& p, float* stg, const f32x4 (&acc)[FM][FN],
-                                                      int arow0, int bcol0, int rq, int cl, int px0, int a0, int M) {
+                                                      int arow0, int bcol0, int rq, int cl, const SlotPix& slot_pix,
+                                                      int a0, int M) {
   constexpr int NCH = BM / 4;  // 16-B chunks per staged pixel row
   constexpr int G8 = BM / 8;   // 8-channel groups per pixel
   constexpr int PPP = 256 / G8;  // pixel rows per pass
@@ -135,7 +136,7 @@ __device__ __forceinline__ void dgrad_staged_epilogue(const HConvParams& p, floa
   }
 #pragma unroll
   for (int ps = 0; ps < NPASS; ++ps) {
-    const int pl = ps * PPP + pr, pix = px0 + pl;
+    const int pl = ps * PPP + pr, pix = slot_pix(pl);  // (M: a padded slot of the general geometry)
     const bool ok = pix < M;
     const size_t o = (size_t)(ok ? pix : 0) * p.Cout + a0 + g * 8;
     // every global operand of the pass in flight before the LDS reads are consumed
@@ -500,10 +501,10 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
 
   // ---- epilogue: D[row = output channel][col = pixel], 4 consecutive channels per lane
   const int rq = (lane >> 4) * 4, cl = fpx;  // column -> pixel, as in the B fragments
-  constexpr bool kStageFits = MODE == 1 && !GEN && BN * BM * 4 <= (int)sizeof(smem) && BM * 8 <= 256 * 8;
+  constexpr bool kStageFits = MODE == 1 && BN * BM * 4 <= (int)sizeof(smem) && BM * 8 <= 256 * 8;
   if constexpr (kStageFits) {
     if (p.slab == nullptr && p.staged) {
-      dgrad_staged_epilogue<BM, BN, FM, FN>(p, (float*)smem, acc, arow0, bcol0, rq, cl, px0, a0, M);
+      dgrad_staged_epilogue<BM, BN, FM, FN>(p, (float*)smem, acc, arow0, bcol0, rq, cl, slot_pix, a0, M);
       stamp_end(p.ts);
       return;
     }
@@ -905,7 +906,9 @@ static int conv_halo_general(const ConvShape& s, int mode, const HaloPlan& hp, c
   p.fd_spx = make_fastdiv(g.rs * g.seg);
   p.fd_w = make_fastdiv(s.W);
   p.ts = ts;
-  p.staged = 0;
+  // the LDS-staged epilogue (16-B coalesced residual / output; option halo_stage_epi: 1 always, 2 = only the
+  // general geometry, the default -- its long launches are where the per-lane strided residual loads cost)
+  p.staged = option_get(OPT_HALO_STAGE_EPI) != 0;
   if (bnb != nullptr) p.bnb = *bnb;
   (void)slab; (void)slab_bytes;
   const int64_t ntiles = (int64_t)s.N * g.tpi * p.tiles_a;
@@ -951,7 +954,7 @@ int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, 
   p.fd_spx = make_fastdiv(p.rows * g.wo);
   p.fd_w = make_fastdiv(g.wo);
   p.ts = ts;
-  p.staged = option_get(OPT_HALO_STAGE_EPI);
+  p.staged = option_get(OPT_HALO_STAGE_EPI) == 1;
   if (bnb != nullptr && split <= 1) p.bnb = *bnb;  // (split-K: the reduction kernel applies it)
   const dim3 grid(halo_tiles_b(s, g) * p.tiles_a, split);
   if (c.st == 2) {

@@ -81,8 +81,10 @@ enum {
                            // 2-B gathers (stem_bench: 18.7 -> 16.1 us; +1.1% interleaved A/B)
   OPT_HALO_S2 = 45,        // stride-2 3x3 FWD on the column-split halo kernel (conv_halo.hip; + the fused 1x1
                            // shortcut): 0 off (implicit GEMM), 1 auto, 2+k force configuration 8+k (tuning)
-  OPT_WGRAD_S2 = 46,       // stride-2 3x3 weight gradient (+ the fused 1x1 shortcut's) on the column-split
-                           // halo kernel (wgrad_halo.hip): 0 off (implicit GEMM, one tap per workgroup), 1 on
+  OPT_WGRAD_S2 = 46,       // stride-2 3x3 weight gradient (+ the fused 1x1 shortcut's) on the column-split halo
+                           // kernel (wgrad_halo.hip): 0 off (implicit GEMM, one tap per workgroup), 1 every shape
+                           // it tiles, 2 (default) only the general-geometry shapes (224x224; at 32x32 the classic
+                           // kernel measured slower in-step than the implicit GEMM + separate 1x1)
   OPT_DGRAD_SCF = 47,      // executor: the projection shortcut's dgrad fused into conv1's parity-class dgrad
                            // (extra reduction steps of class (0, 0); igemm.hip conv_dgrad_sc)
   OPT_BNB_MASK = 48,       // executor (mask-bit backward): each BN's backward sums accumulated in the epilogue
@@ -95,9 +97,10 @@ enum {
                            // every row width (HaloParams::pmap); 0 (default) = the original map. PMC: 22% of
                            // the layer3/4 launches' LDS cycles were conflict cycles; removing them measured
                            // neutral (isolated and in-step), the launches are not LDS-bank bound
-  OPT_HALO_STAGE_EPI = 52,  // conv_halo DGRAD (no split-K): 1 = the tile staged through LDS and written / combined
-                            // with residual, mask bits and BN inputs by 16-B row pieces (coalesced). Default 0:
-                            // neutral in-step (+-0.4%), 1 us slower on the layer2 dgrad alone
+  OPT_HALO_STAGE_EPI = 52,  // conv_halo DGRAD (no split-K): the tile staged through LDS and written / combined with
+                            // residual, mask bits and BN inputs by 16-B row pieces (coalesced): 1 = always, 2 =
+                            // general-geometry tiles only, 0 (default) = never. Measured neutral: classic tiles
+                            // in-step, and at 224x224 (the residual's cost there is its bytes, not the pattern)
   OPT_WGRAD_GEN = 53,      // wgrad_halo: 1 (default) = the general step geometry (row segments, 64-bit per-step
                            // bases) for stride-1 3x3 shapes the classic 64-pixel whole-row steps do not fit
                            // (the 224x224 model); 0 = those go to the implicit GEMM

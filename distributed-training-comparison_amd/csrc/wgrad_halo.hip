@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   constexpr int PER = NR + 1 + (SC ? 1 : 0);  // LDS-DMA instructions per wave per stage (halo rounds + dy (+ dsc))
   static_assert(ST == 1 || (ST == 2 && PF == 0), "stride 2: compiler-scheduled fragment reads");
   static_assert(!SC || ST == 2, "shortcut fusion: stride 2");
-  static_assert(!GEN || (ST == 1 && PF == 0 && !SC), "general geometry: stride 1, compiler-scheduled reads");
+  static_assert(!GEN || PF == 0, "general geometry: compiler-scheduled reads");
   __shared__ __attribute__((aligned(1024))) char smem[NS * SG::BYTES];
   stamp_start(p.ts);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -168,13 +168,16 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int hrow = j * 64 + wave * 8 + (lane >> 3);
-    if constexpr (GEN) {  // halo row -> (row, column) of the step's (rs + 2) x (seg + 2) box, from its corner
-      const int hr = (int)fdiv((uint32_t)hrow, p.fd_seg2), hc = hrow - hr * (p.seg + 2);
-      const int src_chunk = (lane & 7) ^ wg_swz(hrow, p.hsb);
-      hcol[j] = hrow < p.nh;
+    if constexpr (GEN) {  // halo row -> (row, column) of the step's input box, relative to its corner
+      // stride 1: (rs + 2) x (seg + 2) box, row pitch seg + 2. Stride 2: (2 rs + 1) input rows x (2 seg + 1)
+      // columns stored column-split (box column 2j at halo column j, 2j + 1 at hwh + j; pitch p.pitch)
+      const int hr = (int)fdiv((uint32_t)hrow, p.fd_seg2), hc = hrow - hr * (int)p.fd_seg2.d;
+      const int src_chunk = (lane & 7) ^ (ST == 1 ? wg_swz(hrow, p.hsb) : trswz(hrow));
+      const int lc = ST == 1 ? hc : (hc < p.hwh ? 2 * hc : (hc < 2 * p.hwh - 1 ? 2 * (hc - p.hwh) + 1 : -1000000));
+      hcol[j] = hrow < p.nh && lc >= 0;
       hrow_in[j] = hr - 1;
-      hcc[j] = hc - 1;
-      hrel[j] = ((hr * p.W + hc) * p.C + c0 + src_chunk * 8) * 2;
+      hcc[j] = lc - 1;
+      hrel[j] = ((hr * p.W + (lc >= 0 ? lc : 0)) * p.C + c0 + src_chunk * 8) * 2;
       continue;
     }
     hcc[j] = 0;
@@ -192,23 +195,25 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   const int dcol = k0 + (((lane & 7) ^ (ST == 1 ? wg_swz(trow, p.dsb) : trswz(trow))) * 8);
   // GEN: this lane's dy row of the step (pixel trow = (row, column) of the rs x seg segment; padded -> zero)
   uint32_t drel = 0x80000000u;
-  if constexpr (GEN) {
+  if constexpr (GEN) {  // (output grid: wo columns; stride 1 wo = W)
     const int tr = (int)fdiv((uint32_t)trow, p.fd_seg), tc = trow - tr * p.seg;
-    if (trow < p.rs * p.seg) drel = (uint32_t)(((tr * p.W + tc) * p.K + dcol) * 2);
+    if (trow < p.rs * p.seg) drel = (uint32_t)(((tr * p.wo + tc) * p.K + dcol) * 2);
   }
 
   auto stage_gen = [&](char* sb, int step) {  // GEN: per-step 64-bit bases, zero-fill out of the image
     const int img = (int)fdiv((uint32_t)step, p.fd_spimg), r = step - img * p.spimg;
     const int yb = (int)fdiv((uint32_t)r, p.fd_spr), qs = r - yb * (int)p.fd_spr.d;
-    const int y0 = yb * p.rs, q0 = qs * p.seg;
-    const u16* xb = px + ((int64_t)(img * p.H + y0 - 1) * p.W + (q0 - 1)) * p.C;  // the halo box corner
-    const u16* db = pdy + ((int64_t)(img * p.H + y0) * p.W + q0) * p.K;
+    const int y0 = yb * p.rs, q0 = qs * p.seg;  // first OUTPUT row / column of the step
+    const int iy0 = ST * y0, iq0 = ST * q0;       // ... and the input pixel of its (0, 0) tap centre
+    const u16* xb = px + ((int64_t)(img * p.H + iy0 - 1) * p.W + (iq0 - 1)) * p.C;  // the halo box corner
+    const int64_t dro = ((int64_t)(img * p.ho + y0) * p.wo + q0) * p.K;
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
-      const bool ok = hcol[j] && (unsigned)(y0 + hrow_in[j]) < (unsigned)p.H && (unsigned)(q0 + hcc[j]) < (unsigned)p.W;
+      const bool ok = hcol[j] && (unsigned)(iy0 + hrow_in[j]) < (unsigned)p.H && (unsigned)(iq0 + hcc[j]) < (unsigned)p.W;
       buf_lds16(xb, 0x7ffffff0u, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)hrel[j] : 0x80000000u);
     }
-    buf_lds16(db, 0x7ffffff0u, sb + SG::HALO_BYTES + wave * 1024, drel);
+    buf_lds16(pdy + dro, 0x7ffffff0u, sb + SG::HALO_BYTES + wave * 1024, drel);
+    if constexpr (SC) buf_lds16(p.dsc + dro, 0x7ffffff0u, sb + SG::HALO_BYTES + 8192 + wave * 1024, drel);
   };
   auto stage = [&](char* sb, int step) {
     if constexpr (GEN) {
@@ -243,7 +248,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       const int t = wg_pixel(pmap, ks, lane >> 4, h, (lane & 15) >> 2);
       if constexpr (GEN) {  // padded slots (t >= rs * seg, zero dy) read any in-range halo row: row 0
         const int pr = t / p.seg, q = t - pr * p.seg;
-        hm[ks][h] = t < p.rs * p.seg ? pr * W2 + q : 0;
+        hm[ks][h] = t < p.rs * p.seg ? pr * (ST * W2) + q : 0;
         continue;
       }
       const int ii = t / p.spi, rem = t - ii * p.spi;
@@ -703,7 +708,7 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
     p.fd_spimg = make_fastdiv(g.spimg);
     p.fd_spr = make_fastdiv(g.spr);
     p.fd_seg = make_fastdiv(g.seg);
-    p.fd_seg2 = make_fastdiv(g.seg + 2);
+    p.fd_seg2 = make_fastdiv(p.pitch);
   }
   (void)imgs;
   p.ts = ts;
@@ -786,13 +791,55 @@ static bool halo_geometry_s2(const ConvShape& s, int& rs, int& imgs, int& pitch,
          (uint64_t)s.N * hw * s.K * 2 < (1ull << 31);
 }
 
-int wgrad_s2_splits(const ConvShape& s) {
+// General stride-2 geometry (GEN kernels; the 224x224 model's conv1 of layers 2-4): rs output rows x seg
+// output columns per step (seg = the output row if <= 64 pixels, else a 56- / 64- / 32-pixel piece), the
+// input box (2 rs + 1) x (2 seg + 1) stored column-split, 64-bit per-step bases.
+struct WgGeomS2 {
+  int rs = 0, seg = 0, spr = 0, spimg = 0, pitch = 0, nh = 0;
+  int64_t nsteps = 0;
+};
+static bool wg_geometry_s2_gen(const ConvShape& s, WgGeomS2& g) {
+  if (!(s.R == 3 && s.S == 3 && s.stride == 2 && s.pad == 1 && s.C % 64 == 0 && s.K % 64 == 0 && s.H % 2 == 0 &&
+        s.W % 2 == 0))
+    return false;
+  const int ho = s.H / 2, wo = s.W / 2;
+  g.seg = wo <= 64 ? wo : wo % 64 == 0 ? 64 : wo % 56 == 0 ? 56 : wo % 32 == 0 ? 32 : 0;
+  if (g.seg == 0) return false;
+  g.rs = 64 / g.seg;
+  while (g.rs > 1 && ho % g.rs != 0) --g.rs;
+  g.pitch = s2_pitch_w(g.seg);
+  g.nh = (2 * g.rs + 1) * g.pitch;
+  g.spr = wo / g.seg;
+  g.spimg = (ho / g.rs) * g.spr;
+  g.nsteps = (int64_t)s.N * g.spimg;
+  return g.nh <= 384 && 2 * g.rs * g.seg >= 64 && g.nsteps < (1ll << 31) &&
+         (int64_t)(2 * g.rs + 2) * s.W * std::max(s.C, s.K) * 2 < (1ll << 31);
+}
+
+// option wgrad_s2: 0 off, 1 every stride-2 3x3 shape it tiles, 2 (default) the general-geometry shapes only
+static bool wgrad_s2_plan(const ConvShape& s, bool& gen, int64_t& nsteps) {
+  const int o = option_get(OPT_WGRAD_S2);
+  if (o == 0) return false;
   int rs, imgs, pitch, hb, nh;
-  if (option_get(OPT_WGRAD_S2) == 0 || !halo_geometry_s2(s, rs, imgs, pitch, hb, nh)) return 0;
+  if (halo_geometry_s2(s, rs, imgs, pitch, hb, nh)) {
+    gen = false;
+    nsteps = (int64_t)s.N * (s.H / 2) * (s.W / 2) / 64;
+    return o == 1;
+  }
+  WgGeomS2 g;
+  if (option_get(OPT_WGRAD_GEN) == 0 || !wg_geometry_s2_gen(s, g)) return false;
+  gen = true;
+  nsteps = g.nsteps;
+  return true;
+}
+
+int wgrad_s2_splits(const ConvShape& s) {
+  bool gen = false;
+  int64_t nsteps = 0;
+  if (!wgrad_s2_plan(s, gen, nsteps)) return 0;
   const int tiles = (s.C / 64) * (s.K / 64);
-  const int nsteps = s.N * (s.H / 2) * (s.W / 2) / 64;
   int splits = std::max(1, std::max(64, option_get(OPT_WGRAD_HALO)) / tiles);
-  return std::min(splits, std::max(1, nsteps / 4));
+  return (int)std::min<int64_t>(splits, std::max<int64_t>(1, nsteps / 4));
 }
 
 size_t conv_wgrad_s2_slab_bytes(const ConvShape& s) {
@@ -804,8 +851,17 @@ int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* ds
                   float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
   int rs = 0, imgs = 0, pitch = 0, hb = 0, nh = 0;
   const int splits = wgrad_s2_splits(s);
-  DTC_CHECK_ARG(splits > 0 && halo_geometry_s2(s, rs, imgs, pitch, hb, nh) && x && dy && dw && (!dsc || dw_sc),
+  bool gen = false;
+  int64_t gsteps = 0;
+  DTC_CHECK_ARG(splits > 0 && wgrad_s2_plan(s, gen, gsteps) && x && dy && dw && (!dsc || dw_sc),
                 "conv_wgrad_s2: unsupported geometry or arguments");
+  WgGeomS2 gg;
+  if (gen) {
+    wg_geometry_s2_gen(s, gg);
+    rs = gg.rs; imgs = 1; pitch = gg.pitch; hb = nh = gg.nh;
+  } else {
+    halo_geometry_s2(s, rs, imgs, pitch, hb, nh);
+  }
   HaloParams p{};
   p.xs[0] = x;
   p.dys[0] = dy;
@@ -815,7 +871,7 @@ int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* ds
   p.wo = s.W / 2;
   p.fd_hw = make_fastdiv(p.ho * p.wo);
   p.fd_w = make_fastdiv(p.wo);
-  p.nsteps = s.N * p.ho * p.wo / 64;
+  p.nsteps = (int)gsteps;
   p.steps_per_split = (p.nsteps + splits - 1) / splits;
   p.rs = rs;
   p.hb = hb;
@@ -823,6 +879,16 @@ int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* ds
   p.spi = rs * p.wo;
   p.pitch = pitch;
   p.hwh = p.wo + 1;
+  if (gen) {
+    p.x_bytes = 0;
+    p.hwh = gg.seg + 1;
+    p.seg = gg.seg;
+    p.spimg = gg.spimg;
+    p.fd_spimg = make_fastdiv(gg.spimg);
+    p.fd_spr = make_fastdiv(gg.spr);
+    p.fd_seg = make_fastdiv(gg.seg);
+    p.fd_seg2 = make_fastdiv(gg.pitch);
+  }
   p.ts = ts;
   p.xcd = option_get(OPT_WGRAD_XCD);
   const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
@@ -837,9 +903,14 @@ int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* ds
   p.scale = scale;
   const dim3 grid((s.C / 64) * (s.K / 64), used, 1);
   const int nr = (nh + 63) / 64;
-#define DTC_WS2(NR_, SC_) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 0, 2, SC_>), grid, dim3(512), 0, st, p)
-  if (nr <= 5) { if (dsc) DTC_WS2(5, true); else DTC_WS2(5, false); }
-  else { if (dsc) DTC_WS2(6, true); else DTC_WS2(6, false); }
+#define DTC_WS2(NR_, SC_, G_) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 0, 2, SC_, G_>), grid, dim3(512), 0, st, p)
+  if (gen) {
+    if (nr <= 5) { if (dsc) DTC_WS2(5, true, true); else DTC_WS2(5, false, true); }
+    else { if (dsc) DTC_WS2(6, true, true); else DTC_WS2(6, false, true); }
+  } else {
+    if (nr <= 5) { if (dsc) DTC_WS2(5, true, false); else DTC_WS2(5, false, false); }
+    else { if (dsc) DTC_WS2(6, true, false); else DTC_WS2(6, false, false); }
+  }
 #undef DTC_WS2
   DTC_LAUNCH_CHECK();
   if (p.direct) return 0;  // one split: dw (and dw_sc) written by the halo kernel

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", default="halo_conv=1;halo_conv=0")
     ap.add_argument("--layers", default="")
+    ap.add_argument("--scale", type=int, default=1, help="image side multiplier (7: the 224x224 model's layers)")
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     ap.add_argument("--fresh", action="store_true",
                     help="re-write each call's input right before it (as the BN kernel does in the training step) "
@@ -52,6 +53,7 @@ def main():
     layers = [l for l in LAYERS if not args.layers or l[0] in args.layers.split(",")]
     passes = args.passes.split(",")
     for (name, H, C, K, R, st, cnt) in layers:
+        H = H * args.scale
         pad = 1 if R == 3 else 0
         P = (H + 2 * pad - R) // st + 1
         x = torch.randn(B, H, H, C, device=dev).bfloat16()
