@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   static_assert(WR * WC == 4 && HCAP % 32 == 0 && (WS == 2 || WS == 3), "shape");
   static_assert(ST == 1 || (ST == 2 && MODE == 0 && NHB == 1), "stride 2: forward, single halo buffer");
   static_assert(!SC || (ST == 2 && WS == 3), "shortcut fusion: stride-2 forward, 3-slot weight ring");
-  static_assert(!GEN || (ST == 1 && !SC), "general tile geometry: stride 1");
+  static_assert(!GEN || ST == 1 || (MODE == 0 && NHB == 1), "general tile geometry: stride 2 is FWD only");
   __shared__ __attribute__((aligned(1024))) char smem[NHB * HBYTES + WS * WBYTES + SCBYTES];
   char* const wbase = smem + NHB * HBYTES;
   char* const scbase = wbase + WS * WBYTES;
@@ -251,8 +251,9 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     }
     return px0 + l;
   };
-  // GEN: the halo box corner (input row y0 - 1, column q0 - 1) as a 64-bit base; DMA offsets are relative
-  const u16* const gsrc = GEN ? p.src + ((int64_t)(n0 * p.H + y0 - 1) * p.W + (q0 - 1)) * p.Cin : p.src;
+  // GEN: the halo box corner (input row ST y0 - 1, column ST q0 - 1) as a 64-bit base; DMA offsets are relative
+  const u16* const gsrc =
+      GEN ? p.src + ((int64_t)(n0 * p.H + ST * y0 - 1) * p.W + (ST * q0 - 1)) * p.Cin : p.src;
   const int lrow = lane >> 3, pc = lane & 7;
   const int RSC = 9 * p.C;
 
@@ -287,11 +288,12 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
       const int i = (int)fdiv((uint32_t)hr, p.fd_hb), rem = hr - i * p.hb;
       const int hy = (int)fdiv((uint32_t)rem, p.fd_w2), hx = rem - hy * W2;
       int y, x;
-      if constexpr (GEN) {
-        y = y0 + hy - 1;
-        x = q0 + hx - 1;
-        if (n0 < p.N && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W)
-          off = (uint32_t)(((hy * p.W + hx) * p.Cin + (pc ^ hswz(hr)) * 8) * 2);
+      if constexpr (GEN) {  // box row hy; box (padded-local) column lc: stride 2 column-split as below
+        const int lc = ST == 1 ? hx : (hx < p.hwh ? 2 * hx : (hx < 2 * p.hwh - 1 ? 2 * (hx - p.hwh) + 1 : -1));
+        y = ST * y0 + hy - 1;
+        x = ST * q0 + lc - 1;
+        if (lc >= 0 && n0 < p.N && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W)
+          off = (uint32_t)(((hy * p.W + lc) * p.Cin + (pc ^ hswz(hr)) * 8) * 2);
         hoff[q] = off;
         continue;
       } else if constexpr (ST == 1) {
@@ -328,7 +330,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     const int l = bcol0 + j * 16 + fpx;
     if constexpr (GEN) {  // slot -> (row, column) of the tile; padded slots read halo row 0
       const int r = l / p.gseg;
-      hbr[j] = l < p.grs * p.gseg ? r * W2 + (l - r * p.gseg) : 0;
+      hbr[j] = l < p.grs * p.gseg ? r * (ST * W2) + (l - r * p.gseg) : 0;
       continue;
     }
     const int i = (int)fdiv((uint32_t)l, p.fd_spx), rem = l - i * spx;
@@ -754,6 +756,24 @@ static bool halo_gen_geometry(const ConvShape& s, int bn, int hcap, HaloGen& g) 
          (int64_t)s.N * s.H * s.W < (1ll << 31) && (int64_t)(g.rs + 2) * s.W * std::max(s.C, s.K) * 2 < (1ll << 31);
 }
 
+// the same for the stride-2 forward (output grid Ho x Wo, column-split input box (2 rs + 1) x pitch)
+static bool halo_gen_geometry_s2(const ConvShape& s, int bn, int hcap, HaloGen& g) {
+  if (option_get(OPT_HALO_GEN) == 0) return false;
+  if (!(s.R == 3 && s.S == 3 && s.stride == 2 && s.pad == 1 && s.C % 64 == 0 && s.K % 64 == 0 && s.H % 2 == 0 &&
+        s.W % 2 == 0))
+    return false;
+  const int ho = s.H / 2, wo = s.W / 2;
+  g.seg = wo <= 64 ? wo : wo % 64 == 0 ? 64 : wo % 56 == 0 ? 56 : wo % 32 == 0 ? 32 : 0;
+  if (g.seg == 0 || g.seg > bn) return false;
+  g.rs = std::min(bn / g.seg, ho);
+  while (g.rs > 1 && ho % g.rs != 0) --g.rs;
+  g.spr = wo / g.seg;
+  g.tpi = (ho / g.rs) * g.spr;
+  g.nh = (2 * g.rs + 1) * s2_pitch(g.seg);
+  return g.nh <= hcap && 2 * g.rs * g.seg >= bn && (int64_t)s.N * g.tpi < (1ll << 31) &&
+         (int64_t)s.N * ho * wo < (1ll << 31) && (int64_t)(2 * g.rs + 1) * s.W * std::max(s.C, s.K) * 2 < (1ll << 31);
+}
+
 static bool cfg_fits(const ConvShape& s, int cfg, int cout) {
   HaloGeom g;
   const HaloCfg& c = kHaloCfgs[cfg];
@@ -766,7 +786,18 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
   HaloPlan hp{-1, 1};
   if (s.stride == 2) {  // FWD only, column-split halo (option halo_s2: 0 off, 1 auto, 2+k force config 8+k)
     const int o2 = option_get(OPT_HALO_S2);
-    if (o2 == 0 || mode != CONV_FWD || !halo_shape_ok(s, 2)) return hp;
+    if (o2 == 0 || mode != CONV_FWD) return hp;
+    if (!halo_shape_ok(s, 2) || !cfg_fits(s, kFirstS2Cfg, s.K)) {
+      // general geometry (the 224x224 model): forced settings only (halo_s2 >= 2) -- at 224x224 the 64 x 64
+      // column-split tiles (56 real slots, a 3 x 116-row input halo each) measured 1.3-1.8x the implicit GEMM's
+      // 128 x 128 tiles (l2.0.conv1 419 vs 233 us at batch 64; -2% in-step), so auto keeps the GEMM
+      HaloGen g;
+      if (o2 >= 2 && s.K % 64 == 0 && halo_gen_geometry_s2(s, 64, 384, g)) {
+        hp.cfg = kFirstS2Cfg;
+        hp.gen = 1;
+      }
+      return hp;
+    }
     // auto: only where the reduction has >= 2 chunks -- with one 64-channel chunk (layer2.0.conv1) the whole
     // halo must land before the first MFMA and the implicit GEMM's per-tap pipeline is faster (20 vs 28 us
     // at B=256; layer3 20.7 -> 19.6, layer4 22.2 -> 17.1, the shortcut-fused launches 29.2 -> 24.1 / 20.3)
@@ -853,10 +884,16 @@ static int launch_halo(const HConvParams& p, int cfg, dim3 grid, hipStream_t st)
   return launch_halo_ws<MODE, 2>(p, cfg, grid, st);
 }
 
-// general tile geometry instances (3-slot weight ring): configurations 0 (64 x 256) and 2 (64 x 128)
+// general tile geometry instances (3-slot weight ring): configurations 0 (64 x 256) and 2 (64 x 128); the
+// stride-2 forward in configuration 8 (64 x 64), with or without the fused shortcut
 template <int MODE>
 static int launch_halo_gen(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
-  if (cfg == 0)
+  if (cfg == kFirstS2Cfg) {
+    if (p.wsc)
+      hipLaunchKernelGGL((conv_halo_kernel<0, 64, 64, 2, 2, 1, 384, 3, 2, true, true>), grid, dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL((conv_halo_kernel<0, 64, 64, 2, 2, 1, 384, 3, 2, false, true>), grid, dim3(256), 0, st, p);
+  } else if (cfg == 0)
     hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 256, 1, 4, 1, 416, 3, 1, false, true>), grid, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 1, 288, 3, 1, false, true>), grid, dim3(256), 0, st, p);
@@ -878,33 +915,40 @@ static int launch_halo_s2(const HConvParams& p, int cfg, dim3 grid, hipStream_t 
 
 static int conv_halo_general(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
                              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
-                             const BnbArgs* bnb) {
-  DTC_CHECK_ARG(hp.cfg == 0 || hp.cfg == 2, "conv_halo: general geometry needs configuration 0 or 2");
+                             const BnbArgs* bnb, const u16* wsc, u16* out2, double* stats2) {
+  DTC_CHECK_ARG(hp.cfg == 0 || hp.cfg == 2 || hp.cfg == kFirstS2Cfg, "conv_halo: general geometry configuration");
   const HaloCfg& c = kHaloCfgs[hp.cfg];
+  const int ST = c.st;
+  DTC_CHECK_ARG(ST == 1 || (mode == CONV_FWD && res == nullptr), "conv_halo: general stride 2 is FWD only");
+  DTC_CHECK_ARG(wsc == nullptr || (ST == 2 && out2 != nullptr), "conv_halo: the shortcut fusion is stride-2 FWD");
   HaloGen g;
-  DTC_CHECK_ARG(halo_gen_geometry(s, c.bn, c.hcap, g), "conv_halo: general geometry does not fit config %d", hp.cfg);
+  DTC_CHECK_ARG(ST == 1 ? halo_gen_geometry(s, c.bn, c.hcap, g) : halo_gen_geometry_s2(s, c.bn, c.hcap, g),
+                "conv_halo: general geometry does not fit config %d", hp.cfg);
   HConvParams p{};
   p.src = src; p.w = w; p.out = out; p.res = res; p.stats = stats;
+  p.wsc = wsc; p.out2 = out2; p.stats2 = stats2;
   p.N = s.N; p.H = s.H; p.W = s.W; p.C = s.C;
   p.Cin = mode == CONV_FWD ? s.C : s.K;
   p.Cout = mode == CONV_FWD ? s.K : s.C;
   DTC_CHECK_ARG(p.Cout % c.bm == 0, "conv_halo: output channels %d not a multiple of %d", p.Cout, c.bm);
   p.rows = g.rs; p.imgs = 1; p.nh = g.nh; p.hb = g.nh;
-  p.Ho = s.H; p.Wo = s.W; p.pitch = g.seg + 2; p.hwh = 0;
+  p.Ho = s.H / ST; p.Wo = s.W / ST;
+  p.pitch = ST == 1 ? g.seg + 2 : s2_pitch(g.seg);
+  p.hwh = ST == 1 ? 0 : g.seg + 1;
   p.gseg = g.seg; p.grs = g.rs; p.gtpi = g.tpi; p.gspr = g.spr;
   p.fd_gtpi = make_fastdiv(g.tpi);
   p.fd_gspr = make_fastdiv(g.spr);
   p.slab = nullptr;  // (no split-K: >= 1024 tiles at the sizes this geometry serves)
   p.src_bytes = 0;
   p.nhi = (p.nh + 31) / 32;
-  p.tiles_y = s.H / g.rs;
+  p.tiles_y = p.Ho / g.rs;
   p.tiles_a = p.Cout / c.bm;
   p.nchunk = p.Cin / 64;
   p.xcd_remap = option_get(OPT_XCD_REMAP);
   p.fd_hb = make_fastdiv(p.hb);
   p.fd_w2 = make_fastdiv(p.pitch);
   p.fd_spx = make_fastdiv(g.rs * g.seg);
-  p.fd_w = make_fastdiv(s.W);
+  p.fd_w = make_fastdiv(p.Wo);
   p.ts = ts;
   // the LDS-staged epilogue (16-B coalesced residual / output; option halo_stage_epi: 1 always, 2 = only the
   // general geometry, the default -- its long launches are where the per-lane strided residual loads cost)
@@ -923,7 +967,7 @@ int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, 
   DTC_CHECK_ARG(hp.cfg >= 0 && hp.cfg < kNumHaloCfgs && (mode == CONV_FWD || mode == CONV_DGRAD),
                 "conv_halo: unsupported configuration");
   const HaloCfg& c = kHaloCfgs[hp.cfg];
-  if (hp.gen) return conv_halo_general(s, mode, hp, src, w, out, res, stats, slab, slab_bytes, st, ts, bnb);
+  if (hp.gen) return conv_halo_general(s, mode, hp, src, w, out, res, stats, slab, slab_bytes, st, ts, bnb, wsc, out2, stats2);
   DTC_CHECK_ARG(halo_shape_ok(s, c.st) && (c.st == 1 || mode == CONV_FWD), "conv_halo: unsupported shape / pass");
   DTC_CHECK_ARG(wsc == nullptr || (c.st == 2 && out2 != nullptr), "conv_halo: the shortcut fusion is stride-2 FWD");
   HConvParams p{};

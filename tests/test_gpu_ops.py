@@ -46,11 +46,17 @@ def _to_dev_bf16(a, dev):
 # geometries (output widths 16 / 8 / 4: one-row fragments, fragments spanning 2 rows with the padded
 # pitch, 4 images per tile) plus a ragged batch, against the oracle
 S2_CASES = [(8, 32, 32, 64, 128), (8, 16, 16, 128, 256), (8, 8, 8, 256, 512), (5, 16, 16, 128, 256), (2, 8, 8, 64, 128)]
+# general stride-2 geometry (the 224x224 model's conv1 of layers 2-4: output rows of 112 / 56 / 28)
+S2_GEN_CASES = [(2, 8, 224, 64, 128), (1, 4, 112, 128, 64), (2, 12, 56, 64, 64)]
 
 
-@pytest.mark.parametrize("case", S2_CASES)
+@pytest.mark.parametrize("case", S2_CASES + S2_GEN_CASES)
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4])
 def test_conv_fwd_stride2_halo_and_shortcut(dtc, cuda, case, cfg):
+    """Option halo_s2: the stride-2 forward on the column-split halo kernel (auto / forced configurations),
+    alone and with the 1x1 shortcut fused, + BN statistics, against the oracle; the general-geometry cases
+    (rows of 112 / 56 / 28 output pixels: 64-bit per-tile bases, padded slots) take configuration 8's
+    general instances at the forced settings (cfg >= 2) and the implicit GEMM at auto (cfg 1)."""
     N, H, W, C, K = case
     lib = dtc._native.lib
     g = np.random.default_rng(3)
@@ -129,10 +135,6 @@ def test_conv_wgrad(dtc, cuda, case):
     ref = 0.5 * O.conv2d_wgrad(x, dy, R, R, st, pad)
     # fp32 accumulation of exact bf16 products: only summation-order differences remain
     assert rel_err(dw.cpu().numpy(), ref) < 1e-5
-
-
-# + general stride-2 geometry (the 224x224 model's conv1 of layers 2-4: output rows of 112 / 56 / 28)
-S2_GEN_CASES = [(2, 8, 224, 64, 128), (1, 4, 112, 128, 64), (2, 12, 56, 64, 64)]
 
 
 @pytest.mark.parametrize("case", S2_CASES + S2_GEN_CASES)
