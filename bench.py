@@ -50,6 +50,9 @@ def init_dist():
     return dist.get_rank(), dist.get_world_size(), local
 
 
+BN_IDEAL_BYTES_PER_IMAGE = 6.144e6  # non-GEMM HBM bytes per 32x32 image at ideal fusion
+
+
 def _committed_traffic():
     """HBM bytes per conv call from the newest committed PMC summary (profiles/*conv_traffic.json,
     written by tools/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench);
@@ -470,7 +473,14 @@ def main():
                             "calls_per_step": cnt4[3] // max(1, args.steps),
                             "achieved_GBps": round(fl4[3] / (ms4[3] * 1e-3) / 1e9, 1) if ms4[3] > 0 else None,
                             "peak_GBps": HBM_PEAK_GBPS,
-                            "frac": round(fl4[3] / (ms4[3] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if ms4[3] > 0 else None}
+                            "frac": round(fl4[3] / (ms4[3] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if ms4[3] > 0 else None,
+                            # SURVEY §8(d)'s ideal non-GEMM bytes (every BN / ReLU / residual tensor touched once
+                            # under ideal fusion: 6.144 MB per 32x32 image) over the same measured time -- the
+                            # fraction a perfectly fused design would be charged with
+                            "ideal_bytes_per_step": round(BN_IDEAL_BYTES_PER_IMAGE * (S * S / 1024) * B),
+                            "frac_vs_ideal_bytes": (round(BN_IDEAL_BYTES_PER_IMAGE * (S * S / 1024) * B
+                                                          / (ms4[3] / args.steps * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                                                    if ms4[3] > 0 else None)}
                            if not args.no_live_roofline else None),
             "step_flop_fraction_of_peak": round(FLOPS_PER_IMAGE * (S * S / 1024) * B / (elapsed / args.steps) / 1e12
                                                 / BF16_PEAK_TFLOPS, 4),

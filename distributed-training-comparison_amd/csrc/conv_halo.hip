@@ -849,6 +849,12 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
   if (split <= 0) {
     split = 1;
     while (tiles(hp.cfg) * split * 2 <= 512 && nchunk % (split * 2) == 0 && nchunk / (split * 2) >= 2) split *= 2;
+    // option halo_nosplit: where the plan would split the reduction (layer4: 256 tiles x 2 + a reduce launch),
+    // the 64 x 64 double-buffered-halo tiles instead (512 workgroups, no slab, no reduce launch)
+    if (split > 1 && opt == 1 && option_get(OPT_HALO_NOSPLIT) != 0 && cfg_fits(s, 7, cout) && tiles(7) >= 512) {
+      hp.cfg = 7;
+      split = 1;
+    }
   }
   if (nchunk % split != 0) split = 1;
   hp.split = split;
