@@ -107,6 +107,7 @@ enum {
   OPT_HALO_GEN = 54,       // conv_halo: 1 (default) = the general tile geometry for stride-1 3x3 shapes the classic
                            // whole-row tiles do not fit (the 224x224 model); 0 = those go to the implicit GEMM
   OPT_HALO_NOSPLIT = 55,   // conv_halo: 1 = 64 x 64 tiles without split-K where the plan would split (layer4)
+  OPT_WGRAD_PRIO = 56,     // wgrad_halo (8 waves, 2 per SIMD): 1 = waves 4-7 at static s_setprio 1
   OPT_COUNT
 };
 int option_get(int id);

@@ -67,6 +67,7 @@ struct HaloParams {
   // rs rows x seg columns of one image (rs * seg <= 64 real pixels; the remaining MFMA reduction slots of
   // the 64-pixel step carry zero dy), its halo (rs + 2) x (seg + 2) pixels; every step addresses x and dy
   // from a 64-bit per-step base, so an activation may exceed 2 GB (512 x 224 x 224 x 64 bf16 = 3.3 GB)
+  int prio;            // 1: waves 4-7 at s_setprio 1 (MI355X_MICROARCH "Two waves per SIMD" item 4; option wgrad_prio)
   int seg, spimg;      // pixels per row segment, steps per image
   FastDiv fd_spimg, fd_spr, fd_seg, fd_seg2;  // steps per image, segments per row, seg, seg + 2
 };
@@ -149,6 +150,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   __shared__ __attribute__((aligned(1024))) char smem[NS * SG::BYTES];
   stamp_start(p.ts);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (p.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second half (no flips)
   const int ktiles = p.K >> 6;
   int tile, split;
   unsigned z;
@@ -715,6 +717,7 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   p.nostore = option_get(OPT_WGRAD_DIAG) == 1;
   p.diag = option_get(OPT_WGRAD_DIAG);
   p.xcd = option_get(OPT_WGRAD_XCD);
+  p.prio = option_get(OPT_WGRAD_PRIO);
   p.pmap = 0; p.hsb = 3; p.dsb = 3;
   if (option_get(OPT_WGRAD_PMAP) != 0 && !g.gen) {
     if (s.W >= 8) { p.pmap = 1; p.hsb = 2; p.dsb = 2; }
