@@ -1,4 +1,3 @@
 # scratch GPU session (overwritten per session; see tools/gpu_run.sh for the standard steps)
 tools/gpu_session.sh \
-  "wb|300|python tools/wgrad_bench.py --check --variants 'wgrad_prio=0;wgrad_prio=1' > gpurun_out/r03w_wb.txt" \
-  "ab|900|tools/bench_ab.sh 5 'base|' 'pr|--opt wgrad_prio=1'"
+  "cb|400|python tools/conv_bench.py --layers l3,l4 --passes fwd,dgrad --variants 'halo_conv=1;halo_conv=6,halo_split=2;halo_conv=6,halo_split=4;halo_conv=6,halo_split=1;halo_conv=7,halo_split=2;halo_conv=4,halo_split=4;halo_conv=9,halo_split=1;halo_conv=9,halo_split=2;halo_conv=8,halo_split=2' > gpurun_out/r03z_cb.txt"
