@@ -719,7 +719,7 @@ int bn_bwd_fused(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, c
 // ------------------------------------------------------------------ backward
 // MASK: dz = dy * [ym > 0], stored. MB: dz = dy * mask bit (the forward's ReLU mask), not stored
 // (bn_bwd_fin_apply_mask forms it again from the same bits): 4.125 B per element instead of 8.
-template <bool MASK, bool DUAL, typename T, bool MB = false>
+template <bool MASK, bool DUAL, typename T, bool MB = false, int RU = 4>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const T* __restrict__ dy, const T* __restrict__ ym, const T* __restrict__ x1,
     const float* __restrict__ mean1, const float* __restrict__ invstd1, double* __restrict__ acc1,
@@ -745,23 +745,23 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
   float sd[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t m_begin = (int64_t)blockIdx.x * rows_per_block;
   const int64_t m_end = std::min<int64_t>(M, m_begin + rows_per_block);
-  for (int64_t m = m_begin + rr; m < m_end; m += rpp) {
-    const int64_t o = m * C + c0;
+  // one row of this thread: the loaded operands -> the running sums (same order as a plain loop)
+  auto accumulate = [&](int64_t o, const typename E::V& vd, uint32_t mk, const typename E::V& vy,
+                        const typename E::V& va, const typename E::V& vb) {
     float d[8], a[8];
-    E::unpack(E::ld(dy + o), d);
+    E::unpack(vd, d);
     if constexpr (MB) {
-      const uint32_t mk = mbits[o >> 3];
 #pragma unroll
       for (int k = 0; k < 8; ++k) d[k] = (mk >> k) & 1u ? d[k] : 0.f;
     }
     if constexpr (MASK) {
       float yv[8];
-      E::unpack(E::ld(ym + o), yv);
+      E::unpack(vy, yv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
       E::st(dz + o, E::pack(d));  // exact: masking is exact
     }
-    E::unpack(E::ld(x1 + o), a);
+    E::unpack(va, a);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       sd[k] += d[k];
@@ -769,10 +769,38 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     }
     if constexpr (DUAL) {
       float b[8];
-      E::unpack(E::ld(x2 + o), b);
+      E::unpack(vb, b);
 #pragma unroll
       for (int k = 0; k < 8; ++k) s2[k] += d[k] * ((b[k] - m2[k]) * i2[k]);
     }
+  };
+  // RU rows per thread per round, all their loads issued before the first row's math: RU x the bytes in
+  // flight of a load-use loop (RU = 1: it waited on every row, ~33 B per thread in flight -- the layer1
+  // reductions ran at 3.6-4.2 TB/s against ~5.8 for the apply kernels, which already batch 4 rows)
+  typename E::V vd[RU], vy[RU], va[RU], vb[RU];
+  uint32_t mk[RU];
+  int64_t m = m_begin + rr;
+  for (; m + (RU - 1) * rpp < m_end; m += RU * rpp) {
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int64_t o = (m + u * rpp) * C + c0;
+      vd[u] = E::ld(dy + o);
+      mk[u] = MB ? (uint32_t)mbits[o >> 3] : 0u;
+      if constexpr (MASK) vy[u] = E::ld(ym + o);
+      va[u] = E::ld(x1 + o);
+      if constexpr (DUAL) vb[u] = E::ld(x2 + o);
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) accumulate((m + u * rpp) * C + c0, vd[u], mk[u], vy[u], va[u], vb[u]);
+  }
+  for (; m < m_end; m += rpp) {
+    const int64_t o = m * C + c0;
+    vd[0] = E::ld(dy + o);
+    mk[0] = MB ? (uint32_t)mbits[o >> 3] : 0u;
+    if constexpr (MASK) vy[0] = E::ld(ym + o);
+    va[0] = E::ld(x1 + o);
+    if constexpr (DUAL) vb[0] = E::ld(x2 + o);
+    accumulate(o, vd[0], mk[0], vy[0], va[0], vb[0]);
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -844,14 +872,21 @@ int bn_bwd_reduce_mask(const u16* dy, const uint8_t* mbits, const u16* x1, const
                                    std::min<int64_t>((elems + C - 1) / C, (M + minblk - 1) / minblk)});
   rpb = ((rpb + rpp - 1) / rpp) * rpp;
   const int blocks = ceil_div_i(M, rpb);
+  if (x2) DTC_CHECK_ARG(mean2 && invstd2 && acc2, "bn_bwd_reduce_mask: dual branch args");
+  const int ru = option_get(OPT_BN_RED_UNROLL);
+#define DTC_BRM(D_, R_)                                                                                            \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, D_, u16, true, R_>), dim3(blocks), dim3(256), 0, st, dy, nullptr, \
+                     x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, nullptr, M, C, (int)rpb, mbits, ts)
   if (x2) {
-    DTC_CHECK_ARG(mean2 && invstd2 && acc2, "bn_bwd_reduce_mask: dual branch args");
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, true, u16, true>), dim3(blocks), dim3(256), 0, st, dy, nullptr, x1,
-                       mean1, invstd1, acc1, x2, mean2, invstd2, acc2, nullptr, M, C, (int)rpb, mbits, ts);
+    if (ru <= 1) DTC_BRM(true, 1);
+    else if (ru == 2) DTC_BRM(true, 2);
+    else DTC_BRM(true, 4);
   } else {
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false, u16, true>), dim3(blocks), dim3(256), 0, st, dy, nullptr, x1,
-                       mean1, invstd1, acc1, x2, mean2, invstd2, acc2, nullptr, M, C, (int)rpb, mbits, ts);
+    if (ru <= 1) DTC_BRM(false, 1);
+    else if (ru == 2) DTC_BRM(false, 2);
+    else DTC_BRM(false, 4);
   }
+#undef DTC_BRM
   DTC_LAUNCH_CHECK();
   return 0;
 }

@@ -108,6 +108,7 @@ enum {
                            // whole-row tiles do not fit (the 224x224 model); 0 = those go to the implicit GEMM
   OPT_HALO_NOSPLIT = 55,   // conv_halo: 1 = 64 x 64 tiles without split-K where the plan would split (layer4)
   OPT_WGRAD_PRIO = 56,     // wgrad_halo (8 waves, 2 per SIMD): 1 = waves 4-7 at static s_setprio 1
+  OPT_BN_RED_UNROLL = 57,  // bn_bwd_reduce: rows per thread whose loads are issued together (1 = load-use loop; 2, 4)
   OPT_COUNT
 };
 int option_get(int id);

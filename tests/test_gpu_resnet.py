@@ -488,6 +488,25 @@ def test_wgrad_conflict_free_pixel_map_matches(dtc, cuda, batch, hw):
         assert rel_err(gb[rep], ga[rep]) < 1e-5, (rep, rel_err(gb[rep], ga[rep]))
 
 
+@pytest.mark.parametrize("batch,hw", [(8, 32), (3, 32), (5, 8)])
+def test_bn_reduce_unrolled_loads_bit_identical(dtc, cuda, batch, hw):
+    """Option bn_red_unroll (default 4): the mask-bit BN-backward reduction issues the loads of 4 (or 2) rows
+    per thread before their math instead of a load-use loop (1). Each thread adds its rows in the same order,
+    so every gradient is bit-identical -- including ragged row counts that leave a remainder loop (batch 3 / 5)."""
+    lib = dtc._native.lib
+    try:
+        lib.dtc_set_option(b"bn_red_unroll", 1)
+        ga = _grads_repeated(dtc, cuda, 1, batch=batch, hw=hw)
+        for ru in (2, 4):
+            lib.dtc_set_option(b"bn_red_unroll", ru)
+            gb = _grads_repeated(dtc, cuda, 1, batch=batch, hw=hw)
+            for rep in range(2):
+                assert np.isfinite(gb[rep]).all()
+                assert np.array_equal(gb[rep], ga[rep]), (ru, rep, rel_err(gb[rep], ga[rep]))
+    finally:
+        lib.dtc_set_option(b"bn_red_unroll", 4)
+
+
 @pytest.mark.parametrize("bnb_mask", [0, 1])
 def test_halo_staged_dgrad_epilogue_matches(dtc, cuda, bnb_mask):
     """Option halo_stage_epi=1: conv_halo's DGRAD epilogue staged through LDS (16-B coalesced residual /
