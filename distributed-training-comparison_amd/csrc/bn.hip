@@ -843,18 +843,17 @@ static int bwd_reduce(const T* dy, const T* ymask, const T* x1, const float* mea
   const int blocks = ceil_div_i(M, rpb);
   const bool dual = x2 != nullptr;
   if (dual) DTC_CHECK_ARG(mean2 && invstd2 && acc2, "bn_bwd_reduce: dual branch args");
-  if (ymask && dual)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, true, T>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1, invstd1,
-                       acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
-  else if (ymask)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, false, T>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
-                       invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
-  else if (dual)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, true, T>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
-                       invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
-  else
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false, T>), dim3(blocks), dim3(256), 0, st, dy, ymask, x1, mean1,
-                       invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);
+  const bool ru1 = option_get(OPT_BN_RED_UNROLL) <= 1;  // as the mask-bit path: 1 = the load-use loop
+#define DTC_BR(MK_, D_)                                                                                          \
+  if (ru1) hipLaunchKernelGGL((bn_bwd_reduce_kernel<MK_, D_, T, false, 1>), dim3(blocks), dim3(256), 0, st, dy,  \
+                              ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);    \
+  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<MK_, D_, T, false, 4>), dim3(blocks), dim3(256), 0, st, dy,      \
+                          ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb)
+  if (ymask && dual) { DTC_BR(true, true); }
+  else if (ymask) { DTC_BR(true, false); }
+  else if (dual) { DTC_BR(false, true); }
+  else { DTC_BR(false, false); }
+#undef DTC_BR
   DTC_LAUNCH_CHECK();
   return 0;
 }

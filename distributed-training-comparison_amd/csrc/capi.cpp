@@ -19,11 +19,11 @@
 #include <unistd.h>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {0}, {1}, {1}, {0}, {1}, {16384}, {256}, {1024}, {1}, {1}, {1}, {1}, {0}, {1}, {1}, {2}, {1}, {0}, {1}, {1}, {0}, {0}, {1}, {1}, {0}, {0}, {4}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {0}, {1}, {1}, {0}, {1}, {16384}, {256}, {1024}, {1}, {1}, {1}, {1}, {0}, {1}, {1}, {2}, {1}, {0}, {1}, {1}, {0}, {0}, {1}, {1}, {0}, {0}, {4}, {1}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
                                              "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
                                              "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse",
-                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct", "wgrad_defer", "igemm_tile", "igemm_split", "bn_onepass", "sc_stream", "dgrad_class_order", "head_fused", "stem_prologue", "sc_compact", "wgrad_tail", "stem_bn_fuse", "bn_red_elems", "bn_red_blocks", "bn_fa_blocks", "fork_lazy", "side_prio", "sc_fuse", "head_direct", "stem_recompute", "stem_wlds", "halo_s2", "wgrad_s2", "dgrad_scf", "bnb_mask", "bucket_tail", "graph_ev", "wgrad_pmap", "halo_stage_epi", "wgrad_gen", "halo_gen", "halo_nosplit", "wgrad_prio", "bn_red_unroll"};
+                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct", "wgrad_defer", "igemm_tile", "igemm_split", "bn_onepass", "sc_stream", "dgrad_class_order", "head_fused", "stem_prologue", "sc_compact", "wgrad_tail", "stem_bn_fuse", "bn_red_elems", "bn_red_blocks", "bn_fa_blocks", "fork_lazy", "side_prio", "sc_fuse", "head_direct", "stem_recompute", "stem_wlds", "halo_s2", "wgrad_s2", "dgrad_scf", "bnb_mask", "bucket_tail", "graph_ev", "wgrad_pmap", "halo_stage_epi", "wgrad_gen", "halo_gen", "halo_nosplit", "wgrad_prio", "bn_red_unroll", "c64_gen"};
 static std::atomic<int> g_epoch{0};
 // DTC_OPTIONS="name=value,name=value" in the environment overrides defaults at library load (A/B and
 // bisection runs of whole test suites without code changes)

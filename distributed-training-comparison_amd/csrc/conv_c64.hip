@@ -17,6 +17,12 @@
 //   * FWD accumulates the BN batch statistics of the bf16-rounded outputs in registers across
 //     all tiles of the workgroup and adds them to the fp64 slots once.
 // Halo layout, swizzle and DGRAD tap mirroring are those of conv_halo.hip.
+//
+// General geometry (template flag GEN, option c64_gen; the 224x224 model's 224-wide layer1): rows whose
+// width does not divide 256 are cut into 32-pixel segments and a tile is 8 rows x one segment of one image
+// -- the LDS image of a tile is then exactly the classic 32-wide tile's (a 10 x 34 halo, the same B-fragment
+// offsets) -- while HBM is addressed from a 64-bit per-tile base (the halo box corner / the tile's first
+// pixel) with 32-bit offsets inside the box: activations past 2 GB (512 x 224 x 224 x 64 bf16 = 3.3 GB).
 #include "common.h"
 #include "kernels.h"
 #include "tile_common.h"
@@ -36,6 +42,9 @@ struct C64Params {
   uint32_t src_bytes, out_bytes;
   int rows, imgs, hb, nh, tiles_y, ntiles;
   FastDiv fd_hb, fd_w2, fd_spx, fd_w;
+  // GEN: tiles per image and 32-pixel segments per row (a tile = rows 8*yb.. x columns 32*sb.. of image n)
+  int tpi, spr;
+  FastDiv fd_tpi, fd_spr;
   u64* ts;
 };
 
@@ -58,7 +67,9 @@ __device__ __forceinline__ bf16x8 lds_frag(uint32_t addr) {
 // instead of running after them on the wave's single SIMD (one wave per SIMD: nothing else would
 // hide it). Per-lane B-fragment LDS offsets for all nine taps and both k-steps, and the
 // tile-invariant part of the halo DMA addressing, are computed once per workgroup.
-template <int MODE, bool PF>
+constexpr int C64_SEG = 32, C64_GROWS = 8;  // GEN tile: 8 rows x 32 columns
+
+template <int MODE, bool PF, bool GEN = false>
 __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   constexpr int FM = 4, FN = 4;  // wave tile: 64 channels x 64 pixels
   constexpr bool FWD = MODE == 0, RES = MODE == 2 || MODE == 4, BNB = MODE >= 3;
@@ -68,8 +79,21 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bcol0 = wave * 64;
   const int lrow = lane >> 3, pc = lane & 7;
-  const int W2 = p.W + 2;
+  const int LW = GEN ? C64_SEG : p.W;  // width of the tile's LDS image
+  const int W2 = LW + 2;
   const int M = p.N * p.H * p.W;
+  // GEN: tile -> (image, first row, first column) and the 64-bit element index of its first pixel
+  auto gen_tile = [&](int tile, int& n0, int& y0, int& q0) {
+    n0 = (int)fdiv((uint32_t)tile, p.fd_tpi);
+    const int rem = tile - n0 * p.tpi, yb = (int)fdiv((uint32_t)rem, p.fd_spr);
+    y0 = yb * C64_GROWS;
+    q0 = (rem - yb * p.spr) * C64_SEG;
+  };
+  auto gen_base = [&](int tile) -> int64_t {
+    int n0, y0, q0;
+    gen_tile(tile, n0, y0, q0);
+    return ((int64_t)n0 * p.H + y0) * p.W + q0;
+  };
 
   // ---- filter -> LDS, once: nine tap images of 64 rows x 128 B (read as MFMA A fragments per tap)
 #pragma unroll
@@ -88,7 +112,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   for (int j = 0; j < FN; ++j) {
     const int l = bcol0 + j * 16 + fpx;
     const int i = (int)fdiv((uint32_t)l, p.fd_spx), rem = l - i * spx;
-    const int y = (int)fdiv((uint32_t)rem, p.fd_w), x = rem - y * p.W;
+    const int y = (int)fdiv((uint32_t)rem, p.fd_w), x = rem - y * LW;
     const int hbr = i * p.hb + y * W2 + x;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -98,7 +122,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     }
   }
   // ---- halo DMA: tile-invariant per-lane parts (row decomposition, x range, swizzled channel chunk)
-  int hrel[C64_NHI], hyy[C64_NHI], hii[C64_NHI];
+  int hrel[C64_NHI], hyy[C64_NHI], hii[C64_NHI], hxx[C64_NHI];
   bool hok[C64_NHI];
 #pragma unroll
   for (int q = 0; q < C64_NHI; ++q) {
@@ -106,12 +130,32 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     const int hr = g * 8 + lrow;
     const int i = (int)fdiv((uint32_t)hr, p.fd_hb), rem = hr - i * p.hb;
     const int hy = (int)fdiv((uint32_t)rem, p.fd_w2), hx = rem - hy * W2;
-    hok[q] = g < C64_HCAP / 8 && hr < p.nh && (unsigned)(hx - 1) < (unsigned)p.W;
     hyy[q] = hy - 1;
     hii[q] = i;
-    hrel[q] = (((i * p.H + hy - 1) * p.W + hx - 1) * 64 + (pc ^ c64_hswz(hr)) * 8) * 2;
+    if constexpr (GEN) {  // box row hy, column hx: byte offset from the box corner (row y0 - 1, column q0 - 1)
+      hok[q] = g < C64_HCAP / 8 && hr < p.nh;
+      hxx[q] = hx - 1;
+      hrel[q] = ((hy * p.W + hx) * 64 + (pc ^ c64_hswz(hr)) * 8) * 2;
+    } else {
+      hok[q] = g < C64_HCAP / 8 && hr < p.nh && (unsigned)(hx - 1) < (unsigned)p.W;
+      hxx[q] = 0;
+      hrel[q] = (((i * p.H + hy - 1) * p.W + hx - 1) * 64 + (pc ^ c64_hswz(hr)) * 8) * 2;
+    }
   }
   auto stage_halo = [&](char* dst, int tile) {
+    if constexpr (GEN) {
+      int n0, y0, q0;
+      gen_tile(tile, n0, y0, q0);
+      const u16* const box = p.src + (((int64_t)n0 * p.H + y0 - 1) * p.W + (q0 - 1)) * 64;
+#pragma unroll
+      for (int q = 0; q < C64_NHI; ++q) {
+        const int g = wave + 4 * q;
+        if (g >= C64_HCAP / 8) break;
+        const bool ok = hok[q] && (unsigned)(y0 + hyy[q]) < (unsigned)p.H && (unsigned)(q0 + hxx[q]) < (unsigned)p.W;
+        buf_lds16(box, 0x7ffffff0u, dst + g * 1024, ok ? (uint32_t)hrel[q] : 0x80000000u);
+      }
+      return;
+    }
     int n0, y0;
     if (p.imgs == 1) {
       n0 = (int)((unsigned)tile / (unsigned)p.tiles_y);
@@ -129,9 +173,15 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
       buf_lds16(p.src, p.src_bytes, dst + g * 1024, ok ? (uint32_t)(tbase + hrel[q]) : 0x80000000u);
     }
   };
+  // buffer descriptors of the output-side tensors; GEN: rebased at a tile's first pixel (tile_rsrc below)
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.out, 0, p.out_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rrsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)(RES ? p.res : p.out), 0, RES ? p.out_bytes : 0, 0x00020000);
+  // GEN: a descriptor starting `byte_base` bytes into a tensor (a tile's first pixel: 128 B per pixel of the
+  // bf16 tensors, 8 B per pixel of the mask bits); offsets inside the tile stay 32-bit
+  auto tile_rsrc = [&](const void* t, int64_t byte_base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)t + byte_base), 0, 0x7ffffff0u, 0x00020000);
+  };
   const uint32_t halo_lds = __builtin_amdgcn_readfirstlane(lds_u32(halo));
   // mask source: the bf16 y, or (bnb.mb) the forward's ReLU mask bits -- 1 byte per 8 channels
   const bool mbits = BNB && p.bnb.mb != nullptr;
@@ -172,16 +222,21 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   // VMEM ops the previous tile's epilogue leaves in flight per wave at the halo wait: stores (+ y, x)
   constexpr int EPI_VM = 16 + (BNB ? 32 : 0);
   auto epi_off = [&](int tile, int j, int i) {
-    const int pix = tile * 256 + bcol0 + j * 16 + fpx;  // tiles are 256 consecutive pixels
+    const int l = bcol0 + j * 16 + fpx;
+    if constexpr (GEN) {  // slot l = row l / 32, column l % 32 of the tile; byte offset from its first pixel
+      return (uint32_t)((((l >> 5) * p.W + (l & 31)) * 64 + i * 16 + rq) * 2);
+    }
+    const int pix = tile * 256 + l;  // tiles are 256 consecutive pixels
     return pix < M ? (uint32_t)((pix * 64 + i * 16 + rq) * 2) : 0x80000000u;
   };
   auto prefetch = [&](EpiOps& o, int tile) {
+    const __amdgpu_buffer_rsrc_t rr = GEN ? tile_rsrc(RES ? p.res : p.out, gen_base(tile) * 128) : rrsrc;
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const uint32_t off = epi_off(tile, j, i);
-        o.r[j][i] = __builtin_amdgcn_raw_buffer_load_b64(rrsrc, off, 0, 0);
+        o.r[j][i] = __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0);
       }
   };
 
@@ -189,7 +244,16 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   // of no tile (have == false), are dropped by the descriptor bound
   auto epilogue_col = [&](const f32x4 (&a)[FM][FN], const EpiOps& o, int tile, bool have, int j) {
     const int pix = tile * 256 + bcol0 + j * 16 + fpx;
-    const bool ok = have && pix < M;
+    const bool ok = have && (GEN || pix < M);  // GEN tiles have no slot past the tensor
+    __amdgpu_buffer_rsrc_t ors = orsrc, yrs = yrsrc, xrs = xrsrc;
+    if constexpr (GEN) {
+      const int64_t b = have ? gen_base(tile) : 0;
+      ors = tile_rsrc(p.out, b * 128);
+      if constexpr (BNB) {
+        yrs = mbits ? tile_rsrc(p.bnb.mb, b * 8) : tile_rsrc(p.bnb.ym, b * 128);
+        xrs = tile_rsrc(p.bnb.x1, b * 128);
+      }
+    }
     uint32_t off[FM];
     i32x2 yy[FM], xx[FM];
 #pragma unroll
@@ -198,14 +262,14 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
       if constexpr (BNB) {  // out-of-range lanes read zeros (descriptor bound): masked to 0, no sums
         if (mbits) {  // element e = off / 2: bits (e & 4) .. + 3 of byte e >> 3
           const uint32_t e = off[i] >> 1;
-          const uint32_t by = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(yrsrc, off[i] == 0x80000000u ? 0x80000000u : e >> 3, 0, 0);
+          const uint32_t by = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(yrs, off[i] == 0x80000000u ? 0x80000000u : e >> 3, 0, 0);
           const uint32_t nib = (by >> (e & 4)) & 15u;
           yy[i].x = (int)(((nib & 1u) ? 0x3F80u : 0u) | ((nib & 2u) ? 0x3F800000u : 0u));
           yy[i].y = (int)(((nib & 4u) ? 0x3F80u : 0u) | ((nib & 8u) ? 0x3F800000u : 0u));
         } else {
-          yy[i] = __builtin_amdgcn_raw_buffer_load_b64(yrsrc, off[i], 0, 0);
+          yy[i] = __builtin_amdgcn_raw_buffer_load_b64(yrs, off[i], 0, 0);
         }
-        xx[i] = __builtin_amdgcn_raw_buffer_load_b64(xrsrc, off[i], 0, 0);
+        xx[i] = __builtin_amdgcn_raw_buffer_load_b64(xrs, off[i], 0, 0);
       }
     }
 #pragma unroll
@@ -243,7 +307,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
       i32x2 wv;
       wv.x = (int)pack_bf2(v[0], v[1]);
       wv.y = (int)pack_bf2(v[2], v[3]);
-      __builtin_amdgcn_raw_buffer_store_b64(wv, orsrc, off[i], 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(wv, ors, off[i], 0, 0);
     }
   };
   auto epilogue = [&](const f32x4 (&a)[FM][FN], const EpiOps& o, int tile, bool have) {
@@ -373,8 +437,20 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
 }
 
 // ---------------------------------------------------------------- host side
+static bool c64_classic_ok(const ConvShape& s);
+// GEN geometry: 8 rows x 32-column segments (rows whose width does not divide 256, or tensors past 2 GB)
+static bool c64_gen_ok(const ConvShape& s) {
+  if (option_get(OPT_C64_GEN) == 0) return false;
+  if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.C == 64 && s.K == 64)) return false;
+  if (s.W % C64_SEG != 0 || s.H % C64_GROWS != 0) return false;
+  const int64_t M = (int64_t)s.N * s.H * s.W;
+  return M / 256 < (1ll << 31) && M < (1ll << 31) && (int64_t)C64_GROWS * s.W * 128 < (1ll << 31);
+}
 bool conv_c64_ok(const ConvShape& s) {
   if (option_get(OPT_CONV_C64) == 0) return false;
+  return c64_classic_ok(s) || c64_gen_ok(s);
+}
+static bool c64_classic_ok(const ConvShape& s) {
   if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.C == 64 && s.K == 64)) return false;
   if (s.W < 16 || 256 % s.W != 0) return false;  // fragments of 16 contiguous pixels in one image row
   const int hw = s.H * s.W;
@@ -401,33 +477,46 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   C64Params p{};
   p.src = src; p.w = w; p.out = out; p.res = res; p.stats = stats;
   p.N = s.N; p.H = s.H; p.W = s.W;
-  const int hw = s.H * s.W;
-  if (hw >= 256) {
-    p.rows = 256 / s.W;
+  const int64_t hw = (int64_t)s.H * s.W;
+  const int64_t M = s.N * hw;
+  const bool gen = !c64_classic_ok(s);
+  const int lw = gen ? C64_SEG : s.W;  // the LDS tile width
+  if (gen) {
+    p.rows = C64_GROWS;
     p.imgs = 1;
+    p.spr = s.W / C64_SEG;
+    p.tpi = (s.H / C64_GROWS) * p.spr;
+    p.fd_tpi = make_fastdiv(p.tpi);
+    p.fd_spr = make_fastdiv(p.spr);
+    p.src_bytes = p.out_bytes = 0x7ffffff0u;  // unused: every access goes through a per-tile base
   } else {
-    p.imgs = 256 / hw;
-    p.rows = s.H;
+    if (hw >= 256) {
+      p.rows = 256 / s.W;
+      p.imgs = 1;
+    } else {
+      p.imgs = (int)(256 / hw);
+      p.rows = s.H;
+    }
+    p.src_bytes = (uint32_t)(M * 128);
+    p.out_bytes = (uint32_t)(M * 128);
   }
-  p.hb = (p.rows + 2) * (s.W + 2);
+  p.hb = (p.rows + 2) * (lw + 2);
   p.nh = p.imgs * p.hb;
   p.tiles_y = s.H / p.rows;
-  const int64_t M = (int64_t)s.N * hw;
   p.ntiles = (int)(M / 256);
-  p.src_bytes = (uint32_t)(M * 128);
-  p.out_bytes = (uint32_t)(M * 128);
   p.fd_hb = make_fastdiv(p.hb);
-  p.fd_w2 = make_fastdiv(s.W + 2);
-  p.fd_spx = make_fastdiv(p.rows * s.W);
-  p.fd_w = make_fastdiv(s.W);
+  p.fd_w2 = make_fastdiv(lw + 2);
+  p.fd_spx = make_fastdiv(p.rows * lw);
+  p.fd_w = make_fastdiv(lw);
   p.ts = ts;
   const int grid = std::min(p.ntiles, 256);
   const bool in_kernel = fuse && bnb->x2 == nullptr;  // one BN per epilogue (layer1 has no projection)
   if (in_kernel) p.bnb = *bnb;
   const int kmode = mode == CONV_FWD ? 0 : in_kernel ? (res == nullptr ? 3 : 4) : (res == nullptr ? 1 : 2);
   const bool pf = option_get(OPT_C64_PF) != 0;
-#define DTC_C64(M_)                                                                          \
-  if (pf) hipLaunchKernelGGL((conv_c64_kernel<M_, true>), dim3(grid), dim3(256), 0, st, p); \
+#define DTC_C64(M_)                                                                                \
+  if (gen) hipLaunchKernelGGL((conv_c64_kernel<M_, true, true>), dim3(grid), dim3(256), 0, st, p); \
+  else if (pf) hipLaunchKernelGGL((conv_c64_kernel<M_, true>), dim3(grid), dim3(256), 0, st, p);   \
   else hipLaunchKernelGGL((conv_c64_kernel<M_, false>), dim3(grid), dim3(256), 0, st, p)
   switch (kmode) {
     case 0: DTC_C64(0); break;

@@ -109,6 +109,8 @@ enum {
   OPT_HALO_NOSPLIT = 55,   // conv_halo: 1 = 64 x 64 tiles without split-K where the plan would split (layer4)
   OPT_WGRAD_PRIO = 56,     // wgrad_halo (8 waves, 2 per SIMD): 1 = waves 4-7 at static s_setprio 1
   OPT_BN_RED_UNROLL = 57,  // bn_bwd_reduce: rows per thread whose loads are issued together (1 = load-use loop; 2, 4)
+  OPT_C64_GEN = 58,        // conv_c64: 1 (default) = 8-row x 32-column tiles with 64-bit per-tile bases for layer1
+                           // shapes the classic whole-row tiles do not fit (the 224x224 model); 0 = conv_halo
   OPT_COUNT
 };
 int option_get(int id);

@@ -641,6 +641,48 @@ def test_conv_c64(dtc, cuda, case):
     assert rel_err(dx.float().cpu().numpy(), O.conv2d_dgrad(dy, w, (H, W), 1, 1) + res) < 1e-2
 
 
+C64_GEN_CASES = [(2, 16, 224), (3, 8, 64), (2, 40, 96)]
+
+
+@pytest.mark.parametrize("case", C64_GEN_CASES)
+def test_conv_c64_general_geometry(dtc, cuda, case):
+    """conv_c64's general geometry (8-row x 32-column tiles, 64-bit per-tile bases; rows of 224 / 64 / 96
+    pixels that the classic whole-row tiles do not fit -- the 224x224 model's layer1): FWD (+BN statistics)
+    and DGRAD (+residual) against the oracle, and against conv_halo (option c64_gen=0) on the same operands:
+    the same nine taps x two k-steps per pixel in the same order, so the bf16 outputs are bit-identical."""
+    N, H, W = case
+    g = np.random.default_rng(33)
+    x = _rand_bf16((N, H, W, 64), g)
+    w = _rand_bf16((64, 3, 3, 64), g, 0.05)
+    dy = _rand_bf16((N, H, W, 64), g)
+    res = _rand_bf16((N, H, W, 64), g)
+    xd, wd, dyd, rd = (_to_dev_bf16(a, cuda) for a in (x, w, dy, res))
+
+    def run():
+        stats = dtc.ops.new_stats(64, cuda)
+        y = dtc.ops.conv2d_fwd(xd, wd, 1, 1, stats=stats)
+        dx = dtc.ops.conv2d_dgrad(dyd, wd, (H, W), 1, 1, res=rd)
+        dx0 = dtc.ops.conv2d_dgrad(dyd, wd, (H, W), 1, 1)
+        torch.cuda.synchronize()
+        return y.float().cpu().numpy(), stats.sum(0).cpu().numpy(), dx.float().cpu().numpy(), dx0.float().cpu().numpy()
+
+    yk, s, dxk, dx0k = run()
+    dtc._native.call("dtc_set_option", b"c64_gen", 0)
+    try:
+        yh, sh, dxh, dx0h = run()
+    finally:
+        dtc._native.call("dtc_set_option", b"c64_gen", 1)
+    assert rel_err(yk, O.conv2d_fwd(x, w, 1, 1)) < 1e-2
+    yb = yk.reshape(-1, 64).astype(np.float64)
+    np.testing.assert_allclose(s[0], yb.sum(0), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
+    ref = O.conv2d_dgrad(dy, w, (H, W), 1, 1)
+    assert rel_err(dxk, ref + res) < 1e-2 and rel_err(dx0k, ref) < 1e-2
+    np.testing.assert_array_equal(yk, yh)
+    np.testing.assert_array_equal(dx0k, dx0h)
+    assert rel_err(dxk, dxh) < 1e-2  # + residual: conv_halo rounds the same sum (fp32 order may differ)
+
+
 def test_conv_c64_large_grid(dtc, cuda):
     """More tiles than resident workgroups (1024 tiles / 256 workgroups at the bench shape's
     layer1 geometry, batch 64 here): every tile of every workgroup's walk is computed, against
@@ -671,6 +713,8 @@ BNB_CASES = [
     (5, 8, 8, 256, 256, 3, 1, True, False),    # conv_halo
     (9, 4, 4, 512, 512, 3, 1, True, True),     # layer4 geometry (split-K reduce or implicit GEMM)
     (4, 16, 16, 64, 128, 3, 2, True, True),    # stride-2 parity classes: separate reduction pass
+    (2, 8, 224, 64, 64, 3, 1, True, False),    # conv_c64 general geometry (224-wide rows), mode 4
+    (2, 8, 96, 64, 64, 3, 1, False, False),    # conv_c64 general geometry, mode 3
 ]
 
 
