@@ -19,7 +19,7 @@
 #include <unistd.h>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {1}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {0}, {1}, {1}, {0}, {1}, {16384}, {256}, {1024}, {1}, {1}, {1}, {1}, {0}, {1}, {1}, {2}, {1}, {0}, {1}, {1}, {0}, {0}, {1}, {1}, {0}, {0}, {4}, {1}};
+static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {4}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {0}, {1}, {1}, {0}, {1}, {16384}, {256}, {1024}, {1}, {1}, {1}, {1}, {0}, {1}, {1}, {2}, {1}, {0}, {1}, {1}, {0}, {0}, {1}, {1}, {0}, {0}, {4}, {1}};
 static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
                                              "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
                                              "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse",

@@ -15,7 +15,7 @@ enum {
   OPT_XCD_REMAP = 1,
   OPT_DGRAD_CLASSES = 2,
   OPT_WGRAD_FAST = 3,
-  OPT_GRAPHS = 4,
+  OPT_GRAPHS = 4,  // 0 eager, 1 forward + backward hipGraphs, 2 forward only, 3 backward only, 4 auto (resnet.cpp)
   OPT_WGRAD_HALO = 5,  // target workgroup count of the halo WGRAD kernel (0 = generic loader only)
   OPT_HALO_CONV = 6,   // halo FWD/DGRAD for 3x3 s1: 0 off, 1 auto, 2+k force configuration k (tuning)
   OPT_HALO_SPLIT = 7,  // halo FWD/DGRAD split-K over reduction chunks: 0 auto, k forced

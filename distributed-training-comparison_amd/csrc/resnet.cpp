@@ -493,8 +493,18 @@ static int graph_launch(Net& n, hipGraphExec_t ex, hipStream_t st) {
   }
   return 0;
 }
-static bool graphs_on(Net& n) {
-  if (n.capture || n.sync || option_get(OPT_GRAPHS) == 0) return false;
+// option graphs: 0 = eager launches, 1 = forward and backward replayed from hipGraphs, 2 = forward only,
+// 3 = backward only, 4 (default) = the forward always, the backward where its eager launches would make
+// the host the bottleneck: with a communicator (its per-bucket collectives are host-issued) or below
+// kEagerBwdMinPixels per batch. Measured (tools/bench_ab.sh, one MI355X): without a communicator the
+// replayed backward is 4-5% slower than eager launches at batch 192-256 (its cross-stream edges cost more
+// than the launches the host has time for), with one it is 27% faster at batch 256 (`bwd`: which segment
+// asks; `comm`: the backward has a communicator)
+constexpr int64_t kEagerBwdMinPixels = 192ll * 32 * 32;
+static bool graphs_on(Net& n, bool bwd, bool comm = false) {
+  const int g = option_get(OPT_GRAPHS);
+  if (n.capture || n.sync || g == 0 || (g == 2 && bwd) || (g == 3 && !bwd)) return false;
+  if (g == 4 && bwd && !comm && (int64_t)n.B * n.H * n.W >= kEagerBwdMinPixels) return false;
   if (n.graph_epoch != option_epoch()) {  // options are baked into captured launches
     drop_graphs(n);
     n.graph_epoch = option_epoch();
@@ -873,7 +883,7 @@ static int forward_impl(Net& n, const float* x, float* logits, bool train, hipSt
   // pool + FC head launched after the graph straight into the caller's logits (the graph cannot bake
   // in a per-call pointer); 2 = the head inside the graph, its destination read from LSLOT, which the
   // input-copy launch stores before the replay (the ~14 us graph-completion -> next-kernel gap goes)
-  const int hmode = (!n.f32 && graphs_on(n)) ? option_get(OPT_HEAD_DIRECT) : 0;
+  const int hmode = (!n.f32 && graphs_on(n, false)) ? option_get(OPT_HEAD_DIRECT) : 0;
   if (n.f32) DTC_TRY(f32_stem_im2col(x, n.at<float>(n.X0), n.B, n.H, n.W, st));
   else if (n.stem_direct) {  // the graph reads only executor memory: a copy of the 12 B/pixel input (+ the
     // training step's BN slots zeroed in the same launch, + the logits pointer for head_direct = 2)
@@ -890,7 +900,7 @@ static int forward_impl(Net& n, const float* x, float* logits, bool train, hipSt
     DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
     if (hmode == 2) DTC_TRY(put_word(n.ws + n.LSLOT, logits, st));
   }
-  if (!graphs_on(n)) return forward_body(n, logits, train, st);
+  if (!graphs_on(n, false)) return forward_body(n, logits, train, st);
   hipGraphExec_t& ex = n.fwd_exec[n.profiling ? 1 : 0][train ? 1 : 0];
   if (ex && n.head_mode != hmode) drop_graphs(n);  // (option epochs normally re-capture already)
   if (!ex) {
@@ -1480,7 +1490,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
 static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st) {
   if (!n.sums_fresh) DTC_TRY(zero_bytes(n.ws + n.acc_lo, n.stats_hi - n.acc_lo, st));
   n.sums_fresh = false;
-  if (!graphs_on(n)) {
+  if (!graphs_on(n, true, comm != nullptr)) {
     BwdCtx cx;
     cx.comm = comm;
     DTC_TRY(backward_body(n, dlogits, gs, cx, st));

@@ -75,6 +75,7 @@ def _model(dtc, cuda, cap_mb, sync_bn=False):
 def test_ddp_two_ranks_distinct_data_allreduce_equals_fp32_sum(dtc, cuda, graphs, cap_mb):
     world, batch = 2, 32
     xs, ys = _shard(world, batch, seed=7 + int(cap_mb))
+    _graphs_prev = dtc._native.lib.dtc_get_option(b"graphs")
     dtc._native.lib.dtc_set_option(b"graphs", graphs)
     try:
         # no-communicator reference: rank r's own gradient with the DDP pre-scale 1/W, from rank 0's
@@ -137,7 +138,7 @@ def test_ddp_two_ranks_distinct_data_allreduce_equals_fp32_sum(dtc, cuda, graphs
         # both ranks end with identical gradients (every bucket reduced into every rank's buffer)
         assert np.array_equal(res[0][1], res[1][1])
     finally:
-        dtc._native.lib.dtc_set_option(b"graphs", 1)
+        dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
 
 
 def test_sync_batchnorm_two_ranks_distinct_data_equals_concatenated_batch(dtc, cuda):

@@ -88,6 +88,7 @@ def test_autocast_selects_executor_precision(dtc, cuda):
 def test_fp32_sgd_steps_graph_and_eager(dtc, cuda, graphs):
     """Three fp32 training steps (forward, backward, fused SGD) with graph replay and eagerly: the
     same numbers (graph replay changes nothing but launch overhead), finite decreasing-ish loss."""
+    _graphs_prev = dtc._native.lib.dtc_get_option(b"graphs")
     dtc._native.lib.dtc_set_option(b"graphs", graphs)
     try:
         torch.manual_seed(42)
@@ -107,7 +108,7 @@ def test_fp32_sgd_steps_graph_and_eager(dtc, cuda, graphs):
         assert np.isfinite(losses).all() and losses[-1] < losses[0]
         test_fp32_sgd_steps_graph_and_eager.results[graphs] = (losses, _np(model.flat.params))
     finally:
-        dtc._native.lib.dtc_set_option(b"graphs", 1)
+        dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
     res = test_fp32_sgd_steps_graph_and_eager.results
     if len(res) == 2:
         np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-6)

@@ -371,6 +371,7 @@ def test_sgd_step_in_situ(dtc, cuda):
 
 
 def _train_steps(dtc, cuda, steps, graphs, batch=8, seed=5):
+    _graphs_prev = dtc._native.lib.dtc_get_option(b"graphs")
     dtc._native.lib.dtc_set_option(b"graphs", int(graphs))
     try:
         model, _, x, y = _setup(dtc, cuda, batch, seed=seed)
@@ -387,13 +388,15 @@ def _train_steps(dtc, cuda, steps, graphs, batch=8, seed=5):
             losses.append(float(loss))
         return np.array(losses), grads, _np(model.flat.params), {k: _np(v) for k, v in model.named_buffers()}
     finally:
-        dtc._native.lib.dtc_set_option(b"graphs", 1)
+        dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
 
 
-def test_graph_replay_matches_eager(dtc, cuda):
-    """hipGraph replay (default) vs eager launches of the same step: identical kernels and
-    arguments, so results agree up to the order of the fp64 BN-statistics atomics."""
-    lg, gg, pg, bg = _train_steps(dtc, cuda, 3, graphs=True)
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_graph_replay_matches_eager(dtc, cuda, mode):
+    """hipGraph replay (option graphs: 1 forward and backward, 2 forward only, 3 backward only) vs eager
+    launches of the same step: identical kernels and arguments, so results agree up to the order of the
+    fp64 BN-statistics atomics."""
+    lg, gg, pg, bg = _train_steps(dtc, cuda, 3, graphs=mode)
     le, ge, pe, be = _train_steps(dtc, cuda, 3, graphs=False)
     np.testing.assert_allclose(lg, le, rtol=1e-4)
     assert rel_err(gg, ge) < 1e-3
@@ -454,6 +457,7 @@ DEFAULT_STEM_WLDS = 1
 
 
 def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5, hw=32):
+    _graphs_prev = dtc._native.lib.dtc_get_option(b"graphs")
     dtc._native.lib.dtc_set_option(b"graphs", int(graphs))
     try:
         model, _, x, y = _setup(dtc, cuda, batch, seed=seed, hw=hw)
@@ -466,7 +470,7 @@ def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5, hw=32):
             out.append(_np(model.flat.grads).copy())
         return out
     finally:
-        dtc._native.lib.dtc_set_option(b"graphs", 1)
+        dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
 
 
 @pytest.mark.parametrize("batch,hw", [(8, 32), (64, 32), (16, 8)])
@@ -1015,6 +1019,7 @@ def test_second_backward_refused_and_sums_rezeroed(dtc, cuda):
     exe = model.executor(8, 32, 32)
     dl = exe.dlogits_buffer()
     for graphs in (1, 0):
+        _graphs_prev = dtc._native.lib.dtc_get_option(b"graphs")
         dtc._native.lib.dtc_set_option(b"graphs", graphs)
         try:
             crit(model(xd), yd).backward()
@@ -1024,7 +1029,7 @@ def test_second_backward_refused_and_sums_rezeroed(dtc, cuda):
             torch.cuda.synchronize()
             g_b = model.flat.grads.clone()
         finally:
-            dtc._native.lib.dtc_set_option(b"graphs", 1)
+            dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
         assert torch.equal(g_a, g_b), (graphs, (g_a - g_b).abs().max().item())
     assert rel_err(g1.cpu().numpy(), g_a.cpu().numpy()) < 1e-5
 
@@ -1254,6 +1259,7 @@ def test_reducer_reduces_every_bucket_once_after_its_producers(dtc, cuda, graphs
       * with the DDP mean pre-scale of 1/2 (module._grad_scale, W=2) the result equals the local
         gradient (the mean over two identical ranks).
     The last bucket of the plan is only layer1 + the stem (the unavoidable exposed tail)."""
+    _graphs_prev = dtc._native.lib.dtc_get_option(b"graphs")
     dtc._native.lib.dtc_set_option(b"graphs", graphs)
     comm = dtc.parallel.Comm.loopback(cuda.index or 0, 2.0)
     try:
@@ -1286,13 +1292,14 @@ def test_reducer_reduces_every_bucket_once_after_its_producers(dtc, cuda, graphs
         model._comm, model._grad_scale = None, 1.0
     finally:
         comm.close()
-        dtc._native.lib.dtc_set_option(b"graphs", 1)
+        dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
 
 
 @pytest.mark.parametrize("graphs", [1, 0])
 def test_bucketed_allreduce_backward_one_rank_rccl(dtc, cuda, graphs):
     """The same backward through a real one-rank RCCL communicator (the production transport; a
     one-rank SUM is the identity): gradients equal the no-communicator backward, capture and replay."""
+    _graphs_prev = dtc._native.lib.dtc_get_option(b"graphs")
     dtc._native.lib.dtc_set_option(b"graphs", graphs)
     comm = dtc.parallel.Comm(0, 1, dtc.parallel.Comm.unique_id(), cuda.index or 0)
     try:
@@ -1311,7 +1318,7 @@ def test_bucketed_allreduce_backward_one_rank_rccl(dtc, cuda, graphs):
         model._comm = None
     finally:
         comm.close()
-        dtc._native.lib.dtc_set_option(b"graphs", 1)
+        dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
 
 
 def test_sync_batchnorm_two_identical_ranks_loopback(dtc, cuda):

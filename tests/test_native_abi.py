@@ -121,7 +121,7 @@ _OPTION_DEFAULTS = {
     "stem_recompute": 0, "wgrad_tail": 0, "bn_red_elems": 16384, "bn_red_blocks": 256, "bn_fa_blocks": 1024,
     "sc_compact": 1, "stem_prologue": 1, "dgrad_class_order": 1, "wgrad_direct": 1, "wgrad_xcd": 1,
     # round 3
-    "halo_s2": 1, "wgrad_s2": 2, "dgrad_scf": 1, "bnb_mask": 0, "bucket_tail": 1, "graph_ev": 1, "wgrad_pmap": 0, "halo_stage_epi": 0, "wgrad_gen": 1, "halo_gen": 1, "halo_nosplit": 0, "wgrad_prio": 0, "bn_red_unroll": 4, "c64_gen": 1,
+    "halo_s2": 1, "wgrad_s2": 2, "dgrad_scf": 1, "bnb_mask": 0, "bucket_tail": 1, "graph_ev": 1, "wgrad_pmap": 0, "halo_stage_epi": 0, "wgrad_gen": 1, "halo_gen": 1, "halo_nosplit": 0, "wgrad_prio": 0, "bn_red_unroll": 4, "c64_gen": 1, "graphs": 4,
 }
 
 
