@@ -1,2 +1,3 @@
 # scratch GPU session (overwritten per session; see tools/gpu_run.sh for the standard steps)
-AB_ROUNDS=4 tools/gpu_run.sh r03am tests "ab:auto|;g1|--opt graphs=1;b64a|--batch 64;b64g1|--batch 64 --opt graphs=1"
+tools/gpu_session.sh \
+  "ab|900|tools/bench_ab.sh 4 'base|' 'scs|--opt sc_stream=1' 'pr|--opt wgrad_prio=1' 'd2|--opt wgrad_defer=2' 'bm|--opt bnb_mask=1'"
