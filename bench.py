@@ -6,8 +6,10 @@ overlapped inside the native backward), scaler.step (fused Nesterov SGD), scaler
 loss.item(). Per-GPU batch is fixed (256 images of 3x32x32, BASELINE config 2 at N=1), so the
 multi-GPU runs are weak-scaled; synthetic inputs are resident in HBM before timing starts.
 
-Launch: `python bench.py` (N=1) or `python -m torch.distributed.run --nproc-per-node N ...
-bench.py --gpus N`. Rank 0 prints one JSON line.
+Launch: `python bench.py` (N=1), `python bench.py --gpus N` (bench.py starts the N rank
+processes itself, as ddp/main.py:46-49's mp.spawn does) or `python -m torch.distributed.run
+--nproc-per-node N ... bench.py --gpus N`. The world size must equal --gpus. Rank 0 prints one
+JSON line.
 """
 from __future__ import annotations
 
@@ -39,7 +41,46 @@ def _free_port() -> int:
     return p
 
 
-def init_dist():
+def rank_envs(n: int, port: int, base=None) -> list:
+    """The environment of each of `n` rank processes on this node (torchrun's variables, rendezvous
+    on 127.0.0.1): what ddp/main.py:46-49's mp.spawn + init_process_group(tcp://127.0.0.1) set up."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def spawn_ranks(n: int, argv: list, script: str = None, poll_s: float = 0.2) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (one per GPU,
+    as the reference's ddp/main.py:46-49 mp.spawn does) BEFORE anything in this process touches the
+    GPU, pass argv through unchanged, and wait. Rank 0's stdout (the JSON line) is inherited. If a rank
+    fails, the others are terminated by PID and the first failing exit status is returned."""
+    import subprocess
+
+    script = script or os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=e)
+             for e in rank_envs(n, _free_port())]
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for q in live:  # a rank died: the rest would wait in a collective forever
+                    q.terminate()
+        time.sleep(poll_s)
+    return rc
+
+
+def init_dist(gpus: int = 1):
     if "RANK" not in os.environ:
         os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                           MASTER_PORT=str(_free_port()))
@@ -47,7 +88,15 @@ def init_dist():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    check_world(dist.get_world_size(), gpus)
     return dist.get_rank(), dist.get_world_size(), local
+
+
+def check_world(world: int, gpus: int) -> None:
+    """--gpus N must be the job's world size: a run that times fewer ranks than it claims is refused."""
+    if world != gpus:
+        raise SystemExit(f"bench.py: world size {world} != --gpus {gpus} (launch with --gpus {world}, or let "
+                         f"bench.py start the ranks itself: `python bench.py --gpus {gpus}`)")
 
 
 BN_IDEAL_BYTES_PER_IMAGE = 6.144e6  # SURVEY §8(d): non-GEMM HBM bytes per 32x32 image at ideal fusion
@@ -274,8 +323,14 @@ def main():
     args = ap.parse_args()
     if args.mode == "dp":
         return bench_dp(args)
+    if args.gpus > 1 and "RANK" not in os.environ:
+        # no launcher: start the ranks here (device_count does not initialise the GPU on this image)
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible")
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
-    rank, world, local = init_dist()
+    rank, world, local = init_dist(args.gpus)
     dev = torch.device("cuda", local)
     dtc = dtc_import.load()
     for kv in args.opt:

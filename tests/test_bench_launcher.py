@@ -1,0 +1,74 @@
+"""bench.py's own multi-rank launcher: `python bench.py --gpus N` starts N rank
+processes itself, as the reference's ddp/main.py:46-49 (`mp.spawn(main_worker, nprocs=ngpus)`) does,
+instead of silently timing one GPU. CPU only: the rank processes here are a stand-in script."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    sys.path.insert(0, ROOT)
+    import bench as b
+    return b
+
+
+def test_rank_envs_are_torchrun_shaped(bench):
+    envs = bench.rank_envs(4, 29511, base={"KEEP": "1", "RANK": "9"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    for e in envs:
+        assert (e["WORLD_SIZE"], e["LOCAL_WORLD_SIZE"], e["MASTER_ADDR"], e["MASTER_PORT"]) == ("4", "4", "127.0.0.1",
+                                                                                                  "29511")
+        assert e["KEEP"] == "1"  # the caller's environment travels (HSA_ENABLE_IPC_MODE_LEGACY, OMP_NUM_THREADS ...)
+
+
+def test_spawn_ranks_propagates_argv_and_env(bench, tmp_path):
+    child = tmp_path / "child.py"
+    child.write_text(textwrap.dedent(f"""
+        import json, os, sys
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+        out = {{k: os.environ[k] for k in keys}}
+        out["argv"] = sys.argv[1:]
+        open(os.path.join({str(tmp_path)!r}, "rank%s.json" % os.environ["RANK"]), "w").write(json.dumps(out))
+    """))
+    argv = ["--gpus", "3", "--steps", "7", "--opt", "graphs=1"]
+    assert bench.spawn_ranks(3, argv, script=str(child), poll_s=0.01) == 0
+    got = [json.loads((tmp_path / f"rank{r}.json").read_text()) for r in range(3)]
+    assert [g["RANK"] for g in got] == ["0", "1", "2"] and [g["LOCAL_RANK"] for g in got] == ["0", "1", "2"]
+    assert {g["WORLD_SIZE"] for g in got} == {"3"} and {g["MASTER_ADDR"] for g in got} == {"127.0.0.1"}
+    assert len({g["MASTER_PORT"] for g in got}) == 1  # one rendezvous for the job
+    assert all(g["argv"] == argv for g in got)
+
+
+def test_spawn_ranks_failure_terminates_the_others(bench, tmp_path):
+    child = tmp_path / "child.py"
+    child.write_text("import os, sys, time\n"
+                     "if os.environ['RANK'] == '1':\n    sys.exit(3)\n"
+                     "time.sleep(120)\n")
+    t0 = time.perf_counter()
+    rc = bench.spawn_ranks(3, [], script=str(child), poll_s=0.01)
+    assert rc == 3
+    assert time.perf_counter() - t0 < 30  # the sleeping ranks were terminated, not waited for
+
+
+def test_world_size_must_equal_gpus(bench):
+    bench.check_world(4, 4)
+    with pytest.raises(SystemExit, match="world size 1 != --gpus 8"):
+        bench.check_world(1, 8)
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    # no GPU in this container: `--gpus 2` must abort before starting anything, never time one rank
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=300, env={k: v for k, v in os.environ.items() if k != "RANK"})
+    assert r.returncode != 0
+    assert "GPU(s) visible" in r.stderr
+    assert r.stdout.strip() == ""
