@@ -72,9 +72,6 @@ _SIGS = {
     "dtc_bn_bwd_reduce": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
     "dtc_bn_bwd_finalize": (i32, [vp, i32, i64, vp, vp, vp, f32, vp, vp, vp, vp]),
     "dtc_bn_bwd_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
-    "dtc_bn_bwd_onepass_ok": (i32, [i64, i32, i32]),
-    "dtc_bn_bwd_onepass": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, f32,
-                                 i64, i32, vp, vp, vp]),
     "dtc_stem_im2col": (i32, [vp, vp, i32, i32, i32, vp]),
     "dtc_stem_pack_weight": (i32, [vp, vp, i32, vp]),
     "dtc_stem_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),

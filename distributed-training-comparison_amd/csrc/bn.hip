@@ -440,282 +440,6 @@ int bn_bwd_fin_apply(const float* dz, const float* x1, const BnBwdArgs& a1, floa
   return bwd_fin_apply<float>(dz, x1, a1, dx1, x2, a2, dx2, M, C, st);
 }
 
-// ------------------------------------------------------------------ one-pass backward (grid barrier)
-// The BN backward of one BatchNorm2d (+ ReLU mask bits, + the projection shortcut's second BN) in ONE
-// launch: every workgroup loads its slice of (dy, mask bits, x [, x2]) into registers once, forms
-// dz = dy * bit, adds its per-channel sums sum(dz), sum(dz * xhat) into nslot fp64 slots, arrives at a
-// grid barrier, folds the slots into the coefficients, and writes dx (and dz / dx2) from the registers.
-// Against bn_bwd_reduce + bn_bwd_fin_apply this reads (dy, bits, x) once instead of twice
-// (6.125 instead of 10.25 B per element) and saves a launch and its kernel boundary per BN. The grid
-// is at most one workgroup per CU (the launcher checks), so every workgroup is resident and the
-// barrier completes; a bounded spin gives up instead of hanging if that ever fails (*err is set).
-constexpr int BF_THREADS = 512;
-constexpr int BF_LINES = 8;  // barrier arrival counters (ints 16 apart: 64-B lines)
-
-struct BnFusedArgs {
-  const u16* dy;
-  const uint8_t* mbits;
-  u16* dzo;  // optional: dz (may alias dy)
-  const u16* x[2];
-  u16* dx[2];
-  BnBwdArgs a[2];
-  int nslot;      // fp64 slots used (a power of two <= DTC_STAT_SLOTS)
-  int* counter;   // zeroed before the launch (the training forward zeroes every BN's)
-  int* err;       // set to 1 if the barrier timed out
-  int fence;      // 1: release / acquire fences around the barrier (diagnostics; 0 = waitcnt only)
-  int64_t M;
-  int C, rows;    // rows per workgroup
-};
-
-template <bool DUAL, int R>
-__global__ void __launch_bounds__(BF_THREADS) bn_bwd_fused_kernel(const BnFusedArgs p, u64* ts) {
-  __shared__ float red[BF_THREADS * 3];  // per thread, one channel's partials at a time
-  __shared__ float coef[6][512];
-  stamp_start(ts);
-  const int C = p.C, tpr = C >> 3, rpp = BF_THREADS / tpr;
-  const int t = threadIdx.x, g = t % tpr, rr = t / tpr, c0 = g * 8;
-  const int64_t m0 = (int64_t)blockIdx.x * p.rows;
-  // ---- load the slice: R pixel rows x 8 channels per thread, all loads before any use
-  uint4 vd[R], v1[R], v2[R];
-  uint32_t mk[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int64_t m = m0 + rr + (int64_t)r * rpp;
-    if (m < p.M) {
-      const int64_t o = m * C + c0;
-      vd[r] = *(const uint4*)(p.dy + o);
-      v1[r] = *(const uint4*)(p.x[0] + o);
-      if constexpr (DUAL) v2[r] = *(const uint4*)(p.x[1] + o);
-      mk[r] = p.mbits[o >> 3];
-    } else {
-      vd[r] = v1[r] = uint4{0u, 0u, 0u, 0u};
-      if constexpr (DUAL) v2[r] = uint4{0u, 0u, 0u, 0u};
-      mk[r] = 0u;
-    }
-  }
-  float mean1[8], is1[8], mean2[8], is2[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    mean1[k] = p.a[0].mean[c0 + k];
-    is1[k] = p.a[0].invstd[c0 + k];
-    if constexpr (DUAL) {
-      mean2[k] = p.a[1].mean[c0 + k];
-      is2[k] = p.a[1].invstd[c0 + k];
-    }
-  }
-  float sd[8], s1[8], s2[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) sd[k] = s1[k] = s2[k] = 0.f;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    float d[8], a[8];
-    unpack8(vd[r], d);
-    unpack8(v1[r], a);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      d[k] = (mk[r] >> k) & 1u ? d[k] : 0.f;
-      sd[k] += d[k];
-      s1[k] += d[k] * ((a[k] - mean1[k]) * is1[k]);
-    }
-    if constexpr (DUAL) {
-      unpack8(v2[r], a);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) s2[k] += d[k] * ((a[k] - mean2[k]) * is2[k]);
-    }
-  }
-  // ---- per-channel workgroup sums (fixed order over the rpp row groups) -> fp64 slot atomics
-  const size_t slot = (size_t)(blockIdx.x & (p.nslot - 1)) * 2 * C;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    red[t * 3 + 0] = sd[k];
-    red[t * 3 + 1] = s1[k];
-    red[t * 3 + 2] = s2[k];
-    __syncthreads();
-    if (t < tpr) {  // thread t sums channel 8t + k over the row groups
-      float a = 0.f, b = 0.f, e = 0.f;
-      for (int q = 0; q < rpp; ++q) {
-        const float* v = red + (q * tpr + t) * 3;
-        a += v[0];
-        b += v[1];
-        e += v[2];
-      }
-      const int c = t * 8 + k;
-      double* const acc1 = const_cast<double*>(p.a[0].acc);
-      unsafeAtomicAdd(acc1 + slot + c, (double)a);
-      unsafeAtomicAdd(acc1 + slot + C + c, (double)b);
-      if constexpr (DUAL) {
-        double* const acc2 = const_cast<double*>(p.a[1].acc);
-        unsafeAtomicAdd(acc2 + slot + c, (double)a);
-        unsafeAtomicAdd(acc2 + slot + C + c, (double)e);
-      }
-    }
-    __syncthreads();
-  }
-  // ---- grid barrier: release this workgroup's sums, wait for every workgroup's. Everything another
-  // workgroup reads (slots, counters) is written by device-scope atomics, performed at the coherence
-  // point; a workgroup only has to wait for its own atomics to complete before it arrives (fence == 0:
-  // s_waitcnt), no cache maintenance. fence == 1: C++ release / acquire fences (an L2 write-back and
-  // invalidate per workgroup).
-  if (p.fence) __atomic_thread_fence(__ATOMIC_RELEASE);
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // Arrivals are spread over BF_LINES counters (one 64-B line each: workgroup b -> line b % BF_LINES,
-  // i.e. per XCD), so no single address takes every increment; one lane per workgroup polls them with
-  // RELAXED loads (an acquire load would invalidate the L2 on every poll) and one acquire fence follows.
-  if (t < 64) {
-    if (t == 0) __hip_atomic_fetch_add(p.counter + (blockIdx.x % BF_LINES) * 16, 1, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-    const int n = (int)gridDim.x;
-    int spins = 0;
-    for (;;) {
-      const int v = t < BF_LINES ? __hip_atomic_load(p.counter + t * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-      if (wave_sum((float)v) >= (float)n) break;
-      __builtin_amdgcn_s_sleep(4);
-      if (++spins > (1 << 20)) {  // ~0.1 s: never expected; give up rather than hang the GPU
-        if (t == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  if (p.fence) __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  // ---- fold the slots (fixed order) into the coefficients dx = A*dz + B*x + Cc
-  for (int c = t; c < C; c += BF_THREADS) {
-#pragma unroll
-    for (int j = 0; j < (DUAL ? 2 : 1); ++j) {
-      const BnBwdArgs& A = p.a[j];
-      // device-scope (coherence-point) loads of the slots, all issued before the sums
-      double dv[DTC_STAT_SLOTS], xv[DTC_STAT_SLOTS];
-      double* const acc = const_cast<double*>(A.acc);
-#pragma unroll
-      for (int k = 0; k < DTC_STAT_SLOTS; ++k)
-        if (k < p.nslot) {
-          dv[k] = __hip_atomic_load(acc + (size_t)k * 2 * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          xv[k] = __hip_atomic_load(acc + (size_t)k * 2 * C + C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      double dsum = 0.0, xsum = 0.0;
-#pragma unroll
-      for (int k = 0; k < DTC_STAT_SLOTS; ++k)
-        if (k < p.nslot) {
-          dsum += dv[k];
-          xsum += xv[k];
-        }
-      const double cnt = (double)A.count;
-      const double is = A.invstd[c];
-      const double a = (double)A.gamma[c] * is;
-      const double b = -a * is * xsum / cnt;
-      coef[3 * j + 0][c] = (float)a;
-      coef[3 * j + 1][c] = (float)b;
-      coef[3 * j + 2][c] = (float)(-a * dsum / cnt - b * (double)A.mean[c]);
-      if (blockIdx.x == 0) {
-        if (A.dgamma) A.dgamma[c] = (float)(xsum * A.gscale);
-        if (A.dbeta) A.dbeta[c] = (float)(dsum * A.gscale);
-      }
-    }
-  }
-  __syncthreads();
-  float A1[8], B1[8], C1[8], A2[8], B2[8], C2[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    A1[k] = coef[0][c0 + k]; B1[k] = coef[1][c0 + k]; C1[k] = coef[2][c0 + k];
-    if constexpr (DUAL) {
-      A2[k] = coef[3][c0 + k]; B2[k] = coef[4][c0 + k]; C2[k] = coef[5][c0 + k];
-    }
-  }
-  // ---- dx (and dz, dx2) from the registers
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int64_t m = m0 + rr + (int64_t)r * rpp;
-    if (m >= p.M) break;
-    const int64_t o = m * C + c0;
-    float d[8], a[8], v[8];
-    unpack8(vd[r], d);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = (mk[r] >> k) & 1u ? d[k] : 0.f;
-    if (p.dzo != nullptr) *(uint4*)(p.dzo + o) = pack8(d);  // exact: masking is exact
-    unpack8(v1[r], a);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = A1[k] * d[k] + B1[k] * a[k] + C1[k];
-    *(uint4*)(p.dx[0] + o) = pack8(v);
-    if constexpr (DUAL) {
-      unpack8(v2[r], a);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = A2[k] * d[k] + B2[k] * a[k] + C2[k];
-      *(uint4*)(p.dx[1] + o) = pack8(v);
-    }
-  }
-  stamp_end(ts);
-}
-
-static int g_cu_count = 0;
-static int cu_count() {
-  if (g_cu_count == 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      g_cu_count = n;
-  }
-  return g_cu_count > 0 ? g_cu_count : 256;
-}
-
-// rows per workgroup for the one-pass kernel (0: the slice does not fit, use the two-pass kernels)
-// (register budget: R <= 8 rows per thread for one BN, <= 4 with the projection's second BN -- more
-// spills at 512 threads; layer1-size tensors take the two-pass kernels at B=256)
-int bn_bwd_fused_plan(int64_t M, int C, bool dual, int* R_out) {
-  if (C % 64 != 0 || C > 512 || C < 64) return 0;
-  const int tpr = C / 8, rpp = BF_THREADS / tpr;
-  const int ncu = cu_count();
-  for (int R = 1; R <= (dual ? 4 : 8); R *= 2) {
-    const int64_t rows = (int64_t)rpp * R;
-    if ((M + rows - 1) / rows <= ncu) {
-      *R_out = R;
-      return (int)rows;
-    }
-  }
-  return 0;
-}
-
-int bn_bwd_fused(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
-                 const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, int* counter, int* err,
-                 hipStream_t st, u64* ts) {
-  DTC_CHECK_ARG(dy && mbits && x1 && dx1 && counter && err && a1.acc && a1.gamma && a1.mean && a1.invstd && M > 0,
-                "bn_bwd_fused: bad args");
-  DTC_CHECK_ARG(!x2 || (a2 && a2->acc && dx2), "bn_bwd_fused: dual branch args");
-  int R = 0;
-  const int rows = bn_bwd_fused_plan(M, C, x2 != nullptr, &R);
-  DTC_CHECK_ARG(rows > 0, "bn_bwd_fused: no one-pass plan for M=%lld C=%d", (long long)M, C);
-  BnFusedArgs p{};
-  p.dy = dy; p.mbits = mbits; p.dzo = dzo;
-  p.x[0] = x1; p.x[1] = x2; p.dx[0] = dx1; p.dx[1] = dx2;
-  p.a[0] = a1;
-  if (x2) p.a[1] = *a2;
-  p.nslot = std::max(1, std::min(DTC_STAT_SLOTS, 2048 / C));  // the fold reads nslot * 2 * C doubles
-  p.counter = counter; p.err = err;
-  p.fence = option_get(OPT_BN_ONEPASS) == 2;
-  p.M = M; p.C = C; p.rows = rows;
-  const int grid = (int)((M + rows - 1) / rows);
-#define DTC_BF(D_, R_) hipLaunchKernelGGL((bn_bwd_fused_kernel<D_, R_>), dim3(grid), dim3(BF_THREADS), 0, st, p, ts)
-#define DTC_BF_R(D_)                   \
-  switch (R) {                         \
-    case 1: DTC_BF(D_, 1); break;      \
-    case 2: DTC_BF(D_, 2); break;      \
-    case 4: DTC_BF(D_, 4); break;      \
-    default: DTC_BF(D_, 8); break;     \
-  }
-  if (x2) {
-    switch (R) {
-      case 1: DTC_BF(true, 1); break;
-      case 2: DTC_BF(true, 2); break;
-      default: DTC_BF(true, 4); break;
-    }
-  } else {
-    DTC_BF_R(false);
-  }
-#undef DTC_BF_R
-#undef DTC_BF
-  DTC_LAUNCH_CHECK();
-  return 0;
-}
-
 // ------------------------------------------------------------------ backward
 // MASK: dz = dy * [ym > 0], stored. MB: dz = dy * mask bit (the forward's ReLU mask), not stored
 // (bn_bwd_fin_apply_mask forms it again from the same bits): 4.125 B per element instead of 8.

@@ -19,11 +19,16 @@
 #include <unistd.h>
 
 namespace dtc {
-static std::atomic<int> g_opts[OPT_COUNT] = {{2}, {1}, {1}, {1}, {4}, {256}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {4}, {3}, {0}, {0}, {1}, {4}, {1}, {1}, {0}, {1}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {0}, {1}, {1}, {0}, {1}, {16384}, {256}, {1024}, {1}, {1}, {1}, {1}, {0}, {1}, {1}, {2}, {1}, {0}, {1}, {1}, {0}, {0}, {1}, {1}, {0}, {0}, {4}, {1}};
-static const char* g_opt_names[OPT_COUNT] = {"igemm_stages", "xcd_remap",  "dgrad_classes", "wgrad_fast", "graphs",
-                                             "wgrad_halo",   "halo_conv",  "halo_split",    "bwd_streams",
-                                             "conv_c64",     "bn_fused_fin", "halo_nhb2",     "bnb_fuse",
-                                             "wgrad_stages", "halo_wstages", "wgrad_diag", "wgrad_pf", "c64_pf", "wgrad_batch", "bn_mask", "barrier_spin", "wgrad_kernel", "stem_direct", "wgrad_xcd", "wgrad_direct", "wgrad_defer", "igemm_tile", "igemm_split", "bn_onepass", "sc_stream", "dgrad_class_order", "head_fused", "stem_prologue", "sc_compact", "wgrad_tail", "stem_bn_fuse", "bn_red_elems", "bn_red_blocks", "bn_fa_blocks", "fork_lazy", "side_prio", "sc_fuse", "head_direct", "stem_recompute", "stem_wlds", "halo_s2", "wgrad_s2", "dgrad_scf", "bnb_mask", "bucket_tail", "graph_ev", "wgrad_pmap", "halo_stage_epi", "wgrad_gen", "halo_gen", "halo_nosplit", "wgrad_prio", "bn_red_unroll", "c64_gen"};
+static std::atomic<int> g_opts[OPT_COUNT] = {
+#define DTC_OPT_DEF(id, name, def) {def},
+    DTC_OPTION_LIST(DTC_OPT_DEF)
+#undef DTC_OPT_DEF
+};
+static const char* g_opt_names[OPT_COUNT] = {
+#define DTC_OPT_NAME(id, name, def) #name,
+    DTC_OPTION_LIST(DTC_OPT_NAME)
+#undef DTC_OPT_NAME
+};
 static std::atomic<int> g_epoch{0};
 // DTC_OPTIONS="name=value,name=value" in the environment overrides defaults at library load (A/B and
 // bisection runs of whole test suites without code changes)
@@ -125,10 +130,14 @@ static void crash_report(int sig, siginfo_t* si, void* uc) {
     put("\n");
   }
   put("=== end dtc crash report\n");
-  struct sigaction& p = g_prev_sa[sig];
-  if ((p.sa_flags & SA_SIGINFO) && p.sa_sigaction) {
+  // our own disposition goes first (a re-entry ends in the default action, never a loop), and
+  // the previous handler is called only when it is not this one -- if Python's faulthandler was enabled
+  // again after us, each records the other as "previous" and chaining both ways would recurse
+  signal(sig, SIG_DFL);
+  const struct sigaction& p = g_prev_sa[sig];
+  if ((p.sa_flags & SA_SIGINFO) && p.sa_sigaction && p.sa_sigaction != crash_report) {
     p.sa_sigaction(sig, si, uc);
-  } else if (p.sa_handler != SIG_IGN && p.sa_handler != SIG_DFL && p.sa_handler) {
+  } else if (!(p.sa_flags & SA_SIGINFO) && p.sa_handler != SIG_IGN && p.sa_handler != SIG_DFL && p.sa_handler) {
     p.sa_handler(sig);
   }
   signal(sig, SIG_DFL);
@@ -286,23 +295,6 @@ int dtc_bn_bwd_finalize(double* acc, int c, int64_t count, const float* gamma, c
 int dtc_bn_bwd_apply(const uint16_t* dz, const uint16_t* x1, const float* coef1, uint16_t* dx1, const uint16_t* x2,
                      const float* coef2, uint16_t* dx2, int64_t m, int c, void* stream) {
   return bn_bwd_apply(dz, x1, coef1, dx1, x2, coef2, dx2, m, c, S(stream));
-}
-
-int dtc_bn_bwd_onepass_ok(int64_t m, int c, int dual) {
-  int R = 0;
-  return bn_bwd_fused_plan(m, c, dual != 0, &R) > 0 ? 1 : 0;
-}
-int dtc_bn_bwd_onepass(const uint16_t* dy, const uint8_t* mbits, uint16_t* dzo, const uint16_t* x1, const float* mean1,
-                       const float* invstd1, const float* gamma1, double* acc1, float* dgamma1, float* dbeta1,
-                       uint16_t* dx1, const uint16_t* x2, const float* mean2, const float* invstd2, const float* gamma2,
-                       double* acc2, float* dgamma2, float* dbeta2, uint16_t* dx2, int64_t count, float gscale,
-                       int64_t m, int c, int* counter, int* err, void* stream) {
-  BnBwdArgs a1;
-  a1.acc = acc1; a1.count = count; a1.gamma = gamma1; a1.mean = mean1; a1.invstd = invstd1; a1.gscale = gscale;
-  a1.dgamma = dgamma1; a1.dbeta = dbeta1;
-  BnBwdArgs a2 = a1;
-  a2.acc = acc2; a2.gamma = gamma2; a2.mean = mean2; a2.invstd = invstd2; a2.dgamma = dgamma2; a2.dbeta = dbeta2;
-  return bn_bwd_fused(dy, mbits, dzo, x1, a1, dx1, x2, x2 ? &a2 : nullptr, dx2, m, c, counter, err, S(stream));
 }
 
 int dtc_stem_im2col(const float* x, uint16_t* cols, int n, int h, int w, void* stream) {

@@ -811,7 +811,7 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
   const int cout = mode == CONV_FWD ? s.K : s.C;
   const int cin = mode == CONV_FWD ? s.C : s.K;
   const int nchunk = cin / 64;
-  if (!halo_shape_ok(s, 1) || (opt == 1 && !cfg_fits(s, 0, cout) && !cfg_fits(s, 2, cout) && !cfg_fits(s, 6, cout))) {
+  if (!halo_shape_ok(s, 1) || (opt == 1 && !cfg_fits(s, 0, cout) && !cfg_fits(s, 2, cout))) {
     // the general tile geometry: 64 x 256 tiles (4 rows of a 56-pixel segment at 224 / 112 / 56 wide rows), or
     // 64 x 128 where the tile count would leave CUs idle; no split-K (these layers have >= 1024 tiles)
     HaloGen g0, g2;
@@ -840,7 +840,6 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
     // (layer1/2); else 64x128 tiles at 3 workgroups per CU, split-K up to ~2 workgroups per CU
     // (layer3: 512 tiles; layer4: 256 tiles x 2 splits)
     if (cfg_fits(s, 0, cout) && tiles(0) >= 512) hp.cfg = 0;
-    else if (option_get(OPT_HALO_NHB2) && cfg_fits(s, 6, cout)) hp.cfg = 6;
     else if (cfg_fits(s, 2, cout)) hp.cfg = 2;
     else if (cfg_fits(s, 0, cout)) hp.cfg = 0;
     else return hp;
@@ -849,12 +848,6 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
   if (split <= 0) {
     split = 1;
     while (tiles(hp.cfg) * split * 2 <= 512 && nchunk % (split * 2) == 0 && nchunk / (split * 2) >= 2) split *= 2;
-    // option halo_nosplit: where the plan would split the reduction (layer4: 256 tiles x 2 + a reduce launch),
-    // the 64 x 64 double-buffered-halo tiles instead (512 workgroups, no slab, no reduce launch)
-    if (split > 1 && opt == 1 && option_get(OPT_HALO_NOSPLIT) != 0 && cfg_fits(s, 7, cout) && tiles(7) >= 512) {
-      hp.cfg = 7;
-      split = 1;
-    }
   }
   if (nchunk % split != 0) split = 1;
   hp.split = split;

@@ -85,10 +85,8 @@ int stem_pack_weight(const u16* w27, u16* w64, int K, hipStream_t st) {
 template <typename T>
 __global__ void __launch_bounds__(256) head_fwd_kernel(const T* __restrict__ act, int HW, int C,
                                                       const T* __restrict__ wfc, const float* __restrict__ bfc,
-                                                      int ncls, float* __restrict__ feat, float* __restrict__ logits,
-                                                      float* const* __restrict__ lslot) {
+                                                      int ncls, float* __restrict__ feat, float* __restrict__ logits) {
   typedef Elt<T> E;
-  if (lslot != nullptr) logits = *lslot;  // head_direct = 2: the destination the input-copy launch stored
   extern __shared__ float hsm[];  // [C] feat, then [256 / (C/8)][C] pool partials
   const int n = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int tpr = C >> 3, groups = max(1, 256 / tpr);
@@ -143,23 +141,19 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const T* __restrict__ act
 
 template <typename T>
 static int head_fwd_t(const T* act, int N, int HW, int C, const T* wfc, const float* bfc, int ncls, float* feat,
-                      float* logits, hipStream_t st, float* const* lslot = nullptr) {
-  DTC_CHECK_ARG(act && wfc && bfc && feat && (logits || lslot) && N > 0 && HW > 0 && C > 0 && C % 32 == 0 && C <= 2048 &&
+                      float* logits, hipStream_t st) {
+  DTC_CHECK_ARG(act && wfc && bfc && feat && logits && N > 0 && HW > 0 && C > 0 && C % 32 == 0 && C <= 2048 &&
                     ncls > 0,
                 "head_fwd: bad args");
   const int groups = std::max(1, 256 / (C / 8));
   const size_t lds = (size_t)(C + std::max(groups * C, 256)) * sizeof(float);
-  hipLaunchKernelGGL(head_fwd_kernel<T>, dim3(N), dim3(256), lds, st, act, HW, C, wfc, bfc, ncls, feat, logits, lslot);
+  hipLaunchKernelGGL(head_fwd_kernel<T>, dim3(N), dim3(256), lds, st, act, HW, C, wfc, bfc, ncls, feat, logits);
   DTC_LAUNCH_CHECK();
   return 0;
 }
 int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st) {
   return head_fwd_t<u16>(act, N, HW, C, wfc, bfc, ncls, feat, logits, st);
-}
-int head_fwd_slot(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
-                  float* const* lslot, hipStream_t st) {
-  return head_fwd_t<u16>(act, N, HW, C, wfc, bfc, ncls, feat, nullptr, st, lslot);
 }
 int head_fwd(const float* act, int N, int HW, int C, const float* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st) {

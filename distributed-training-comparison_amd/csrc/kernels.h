@@ -10,107 +10,58 @@
 namespace dtc {
 
 // ------------------------------------------------------------------ tuning options (atomic ints)
+// X(ID, name, default): the live options only. Variants that measured negative or neutral were
+// deleted with their code paths (round 4; their numbers are in DESIGN.md).
+#define DTC_OPTION_LIST(X)                                                                                   \
+  X(IGEMM_STAGES, igemm_stages, 2)      /* LDS ring depth of the implicit GEMM (2 or 3) */                  \
+  X(XCD_REMAP, xcd_remap, 1)            /* igemm: tiles sharing operands on one XCD */                       \
+  X(DGRAD_CLASSES, dgrad_classes, 1)    /* stride-2 dgrad as output-parity classes */                        \
+  X(WGRAD_FAST, wgrad_fast, 1)          /* igemm WGRAD fast loader */                                         \
+  X(GRAPHS, graphs, 4)                  /* 0 eager, 1 fwd + bwd hipGraphs, 2 fwd only, 3 bwd only, 4 auto */ \
+  X(WGRAD_HALO, wgrad_halo, 256)        /* target workgroups of the halo WGRAD kernel (0 = igemm only) */   \
+  X(HALO_CONV, halo_conv, 1)            /* halo FWD/DGRAD for 3x3 s1: 0 off, 1 auto, 2+k force cfg k */     \
+  X(HALO_SPLIT, halo_split, 0)          /* halo FWD/DGRAD split-K: 0 auto, k forced */                        \
+  X(BWD_STREAMS, bwd_streams, 1)        /* weight gradients on a side stream beside the dgrad/BN chain */    \
+  X(CONV_C64, conv_c64, 1)              /* persistent 64->64 3x3 conv (conv_c64.hip) for layer1 */           \
+  X(BN_FUSED_FIN, bn_fused_fin, 1)      /* BN coefficients folded into the apply kernels */                   \
+  X(BNB_FUSE, bnb_fuse, 0)              /* non-mask backward only: BN reduction in dgrad epilogues */        \
+  X(HALO_WSTAGES, halo_wstages, 3)      /* weight ring depth of conv_halo (2 or 3) */                         \
+  X(C64_PF, c64_pf, 1)                  /* conv_c64: next (tap, k-step) fragments read ahead */               \
+  X(WGRAD_BATCH, wgrad_batch, 4)        /* up to this many 3x3 s1 wgrads of a bucket per launch */            \
+  X(BN_MASK, bn_mask, 1)                /* ReLU mask bits from the forward drive the BN backward */          \
+  X(BARRIER_SPIN, barrier_spin, 1)      /* dtc_barrier: 1 poll the event, 0 hipEventSynchronize */           \
+  X(STEM_DIRECT, stem_direct, 1)        /* (plan time) direct stem conv, 0 = im2col + GEMM */                 \
+  X(WGRAD_XCD, wgrad_xcd, 1)            /* wgrad_halo: tiles of one (problem, split) on one XCD */           \
+  X(WGRAD_DIRECT, wgrad_direct, 1)      /* wgrad_halo: a one-split launch writes the scaled dw itself */     \
+  X(IGEMM_TILE, igemm_tile, 0)          /* igemm tile: 0 auto, 1 64x64, 2 128x128, 3 64x256 (tuning) */     \
+  X(IGEMM_SPLIT, igemm_split, 0)        /* igemm split-K: 0 auto, k forced (tuning) */                        \
+  X(DGRAD_CLASS_ORDER, dgrad_class_order, 1) /* stride-2 dgrad classes heaviest first */                      \
+  X(STEM_PROLOGUE, stem_prologue, 1)    /* input copy + BN slot zeroing in one launch */                      \
+  X(SC_COMPACT, sc_compact, 1)          /* shortcut dx at the stride-2 grid, added by conv1's dgrad */        \
+  X(STEM_BN_FUSE, stem_bn_fuse, 1)      /* stem BN backward apply inside the stem weight gradient */          \
+  X(BN_RED_ELEMS, bn_red_elems, 16384)  /* bn_bwd_reduce: target elements per workgroup (tuning) */           \
+  X(BN_RED_BLOCKS, bn_red_blocks, 256)  /* ... while keeping at least this many workgroups (tuning) */        \
+  X(BN_FA_BLOCKS, bn_fa_blocks, 1024)   /* BN fin_apply: target workgroups per launch (tuning) */             \
+  X(FORK_LAZY, fork_lazy, 1)            /* fork the wgrad stream only where a wgrad launches */               \
+  X(SIDE_PRIO, side_prio, 1)            /* (side stream creation) weight-gradient stream at low priority */  \
+  X(SC_FUSE, sc_fuse, 1)                /* projection shortcut inside conv1's forward: 1 layer4, 2/3 wider */ \
+  X(STEM_WLDS, stem_wlds, 1)            /* stem forward weight staged in LDS */                               \
+  X(HALO_S2, halo_s2, 1)                /* stride-2 3x3 FWD on the column-split halo kernel */                \
+  X(WGRAD_S2, wgrad_s2, 2)              /* stride-2 wgrad (+ shortcut) on the halo kernel: 0 off, 1 all, 2 GEN */ \
+  X(DGRAD_SCF, dgrad_scf, 1)            /* shortcut dgrad fused into conv1's parity-class dgrad */            \
+  X(BNB_MASK, bnb_mask, 0)              /* mask-bit backward: BN sums in the producing dgrad's epilogue */    \
+  X(HEAD_FUSED, head_fused, 0)          /* head backward in one launch (dW/db strips + dact) */               \
+  X(HALO_STAGE_EPI, halo_stage_epi, 0)  /* conv_halo DGRAD epilogue staged through LDS: 1 always, 2 GEN only */ \
+  X(BUCKET_TAIL, bucket_tail, 1)        /* (plan time) close the open bucket (>= 1 MB) after layer2.0 */      \
+  X(WGRAD_GEN, wgrad_gen, 1)            /* wgrad_halo general step geometry (224x224 model) */                \
+  X(HALO_GEN, halo_gen, 1)              /* conv_halo general tile geometry (224x224 model) */                 \
+  X(BN_RED_UNROLL, bn_red_unroll, 4)    /* bn_bwd_reduce: rows per thread whose loads go together */          \
+  X(C64_GEN, c64_gen, 1)                /* conv_c64 general tiles (224x224 layer1) */
+
 enum {
-  OPT_IGEMM_STAGES = 0,
-  OPT_XCD_REMAP = 1,
-  OPT_DGRAD_CLASSES = 2,
-  OPT_WGRAD_FAST = 3,
-  OPT_GRAPHS = 4,  // 0 eager, 1 forward + backward hipGraphs, 2 forward only, 3 backward only, 4 auto (resnet.cpp)
-  OPT_WGRAD_HALO = 5,  // target workgroup count of the halo WGRAD kernel (0 = generic loader only)
-  OPT_HALO_CONV = 6,   // halo FWD/DGRAD for 3x3 s1: 0 off, 1 auto, 2+k force configuration k (tuning)
-  OPT_HALO_SPLIT = 7,  // halo FWD/DGRAD split-K over reduction chunks: 0 auto, k forced
-  OPT_BWD_STREAMS = 8,  // 1 (default): weight gradients on a side stream, overlapped with the
-                        // dgrad/BN chain (the MFMA-bound wgrads beside the HBM-bound BN kernels:
-                        // +2% at B=256 once the wgrads were batched; 5% slower before)
-  OPT_CONV_C64 = 9,     // persistent 64->64 channel 3x3 conv (conv_c64.hip) for layer1 FWD/DGRAD
-  OPT_BN_FUSED_FIN = 10,  // 1: BN coefficients computed by the apply kernels (no finalize launches)
-  OPT_HALO_NHB2 = 11,     // 1: prefer the double-buffered-halo conv_halo tiles where they fit 2 WG/CU
-  OPT_BNB_FUSE = 12,      // BN-backward reduction (mask + sums) fused into dgrad epilogues, bit mask of
-                          // kernels: 1 conv_c64, 2 conv_halo, 4 split-K reduce (others: separate pass).
-                          // Default 0: measured neutral (c64, split-K) to -1% (halo) at B=256 -- the
-                          // epilogue's strided 8-B y/x loads cost what the separate pass costs.
-  OPT_WGRAD_STAGES = 13,   // LDS ring depth of wgrad_halo (2: one step of DMA in flight; 4 (default): three)
-  OPT_HALO_WSTAGES = 14,   // weight ring depth of conv_halo (2 or 3)
-  OPT_WGRAD_DIAG = 15,     // diagnostics only: 1 = wgrad_halo skips its slab stores (WRONG results)
-  OPT_WGRAD_PF = 16,       // wgrad_halo LDS fragment prefetch window (0 = compiler-scheduled, 5, 8)
-  OPT_C64_PF = 17,         // conv_c64: 1 = next (tap, k-step) fragments read before this group's MFMAs
-  OPT_WGRAD_BATCH = 18,    // executor: up to this many 3x3 stride-1 weight gradients of a bucket per launch
-  OPT_BN_MASK = 19,        // executor: 1 = ReLU mask bits from the forward BN apply drive the BN backward
-  OPT_BARRIER_SPIN = 20,   // dtc_barrier host wait: 1 = poll the completion event, 0 = hipEventSynchronize
-  OPT_WGRAD_KERNEL = 21,   // wgrad_halo: 0 = 8 waves (144 x 32 per wave), 1 = 4 waves (144 x 64, one per SIMD)
-  OPT_STEM_DIRECT = 22,    // executor (at plan time): 1 = direct stem conv (stem.hip), 0 = im2col + GEMM
-  OPT_WGRAD_XCD = 23,      // wgrad_halo: 1 (default) = the tiles of one (problem, split) run on one XCD
-  OPT_WGRAD_DIRECT = 24,   // wgrad_halo: 1 = a one-split launch writes the scaled dw itself (no reduce)
-  OPT_WGRAD_DEFER = 25,    // executor: 1 = batched wgrads forked after the layer's last dgrad (see resnet.cpp); 2 = layer1 only
-  OPT_IGEMM_TILE = 26,     // igemm FWD/DGRAD/WGRAD tile: 0 auto, 1 = 64x64, 2 = 128x128, 3 = 64x256 (tuning)
-  OPT_IGEMM_SPLIT = 27,    // igemm split-K: 0 auto, k = k splits where the plan allows (tuning)
-  OPT_BN_ONEPASS = 28,     // executor: 1 = one-pass BN backward (bn_bwd_fused, grid barrier) where it has a
-                           // plan; 2 = the same with release/acquire fences. Default 0: measured slower at
-                           // B=256 (23-52 us per launch vs 11-20 us for the reduce + apply pair: the
-                           // device-wide barrier costs more than the re-read it saves)
-  OPT_SC_STREAM = 29,      // executor: 1 = the projection shortcut's conv / dgrad on a stream of its own
-                           // (default 0: measured -2% at B=256, interleaved A/B; cross-stream graph edges
-                           // cost more than the overlap of the small launches gains)
-  OPT_DGRAD_CLASS_ORDER = 30,  // stride-2 dgrad parity classes dispatched heaviest first (1) or in z order (0)
-  OPT_HEAD_FUSED = 31,     // head backward: 1 = one launch (dW/db strips + dact), 0 (default) = partial/reduce/x
-                           // kernels (measured 1% faster: the strip kernel's 256-image loop is latency bound)
-  OPT_STEM_PROLOGUE = 32,  // forward: 1 = input copy + BN slot zeroing in one launch (copy_and_zero)
-  OPT_SC_COMPACT = 33,     // executor: 1 = the shortcut's dx kept at the stride-2 grid (1/4 the bytes) and
-                           // added by conv1's parity-class dgrad epilogue
-  OPT_WGRAD_TAIL = 34,     // executor: >0 = at most this many layer1 weight gradients per batched launch
-                           // (the last batch of the backward runs beside the stem's tail chain). Default
-                           // 0: 2 measured -0.7%, 1 -6% (the 2-conv batch takes as long as the 4-conv one)
-  OPT_STEM_BN_FUSE = 35,   // executor: 1 (default) = the stem BN's backward apply fused into the stem weight
-                           // gradient (stem_wgrad_bn; dc never stored): +0.8% at B=256, interleaved A/B
-  OPT_BN_RED_ELEMS = 36,   // bn_bwd_reduce (mask path): target elements per workgroup (tuning; default 16384)
-  OPT_BN_RED_BLOCKS = 37,  // ... while keeping at least this many workgroups (tuning; default 256;
-                           // 65536 / 64 measured -7%)
-  OPT_BN_FA_BLOCKS = 38,   // BN fin_apply kernels: target workgroups per launch (tuning; default 1024; 256: -1%)
-  OPT_FORK_LAZY = 39,      // executor: 1 (default) = fork the weight-gradient stream only where a wgrad
-                           // launches (fewer cross-stream graph edges: +1.1%, two interleaved A/B sessions)
-  OPT_SIDE_PRIO = 40,      // executor (at the side stream's creation): 1 (default) = weight-gradient stream at
-                           // low priority (+0.35%, higher in 6 of 6 interleaved A/B rounds)
-  OPT_SC_FUSE = 41,        // forward: the projection shortcut computed inside conv1's launch (conv_fwd_sc) for
-                           // 1 (default) layer4-size plans, 2 every 64x64 plan, 3 also 128x128 (igemm.hip)
-  OPT_HEAD_DIRECT = 42,    // forward: 1 (default) = the head launched after the graph into the caller's logits
-                           // (no graph-owned copy + D2D copy kernel); 2 = the head inside the graph, its
-                           // destination read from a pointer slot the input-copy launch stores. 2 measured
-                           // neutral (6-round A/B): the ~14 us graph-completion gap moves to the next kernel
-  OPT_STEM_RECOMPUTE = 43, // training forward: 1 = stem statistics pass + recompute pass with the BN apply fused
-  OPT_STEM_WLDS = 44,      // stem forward: 1 (default) = weight staged in LDS by coalesced loads, not per-lane
-                           // 2-B gathers (stem_bench: 18.7 -> 16.1 us; +1.1% interleaved A/B)
-  OPT_HALO_S2 = 45,        // stride-2 3x3 FWD on the column-split halo kernel (conv_halo.hip; + the fused 1x1
-                           // shortcut): 0 off (implicit GEMM), 1 auto, 2+k force configuration 8+k (tuning)
-  OPT_WGRAD_S2 = 46,       // stride-2 3x3 weight gradient (+ the fused 1x1 shortcut's) on the column-split halo
-                           // kernel (wgrad_halo.hip): 0 off (implicit GEMM, one tap per workgroup), 1 every shape
-                           // it tiles, 2 (default) only the general-geometry shapes (224x224; at 32x32 the classic
-                           // kernel measured slower in-step than the implicit GEMM + separate 1x1)
-  OPT_DGRAD_SCF = 47,      // executor: the projection shortcut's dgrad fused into conv1's parity-class dgrad
-                           // (extra reduction steps of class (0, 0); igemm.hip conv_dgrad_sc)
-  OPT_BNB_MASK = 48,       // executor (mask-bit backward): each BN's backward sums accumulated in the epilogue
-                           // of the dgrad producing its gradient, from the ReLU mask bits (no reduction pass)
-  OPT_BUCKET_TAIL = 49,    // executor (at plan time): 1 = close the open bucket (>= 1 MB) after layer2.0 so the
-                           // un-overlapped last bucket is layer1 + stem only (deviates from torch's cap rule)
-  OPT_GRAPH_EV = 50,       // executor: 1 (default) = an event recorded behind every graph launch (drop_graphs waits
-                           // for the last one before destroying execs); 0 = none (drop relies on the device drain)
-  OPT_WGRAD_PMAP = 51,     // wgrad_halo (stride 1): 1 = bank-conflict-free tr-read pixel map and swizzle for
-                           // every row width (HaloParams::pmap); 0 (default) = the original map. PMC: 22% of
-                           // the layer3/4 launches' LDS cycles were conflict cycles; removing them measured
-                           // neutral (isolated and in-step), the launches are not LDS-bank bound
-  OPT_HALO_STAGE_EPI = 52,  // conv_halo DGRAD (no split-K): the tile staged through LDS and written / combined with
-                            // residual, mask bits and BN inputs by 16-B row pieces (coalesced): 1 = always, 2 =
-                            // general-geometry tiles only, 0 (default) = never. Measured neutral: classic tiles
-                            // in-step, and at 224x224 (the residual's cost there is its bytes, not the pattern)
-  OPT_WGRAD_GEN = 53,      // wgrad_halo: 1 (default) = the general step geometry (row segments, 64-bit per-step
-                           // bases) for stride-1 3x3 shapes the classic 64-pixel whole-row steps do not fit
-                           // (the 224x224 model); 0 = those go to the implicit GEMM
-  OPT_HALO_GEN = 54,       // conv_halo: 1 (default) = the general tile geometry for stride-1 3x3 shapes the classic
-                           // whole-row tiles do not fit (the 224x224 model); 0 = those go to the implicit GEMM
-  OPT_HALO_NOSPLIT = 55,   // conv_halo: 1 = 64 x 64 tiles without split-K where the plan would split (layer4)
-  OPT_WGRAD_PRIO = 56,     // wgrad_halo (8 waves, 2 per SIMD): 1 = waves 4-7 at static s_setprio 1
-  OPT_BN_RED_UNROLL = 57,  // bn_bwd_reduce: rows per thread whose loads are issued together (1 = load-use loop; 2, 4)
-  OPT_C64_GEN = 58,        // conv_c64: 1 (default) = 8-row x 32-column tiles with 64-bit per-tile bases for layer1
-                           // shapes the classic whole-row tiles do not fit (the 224x224 model); 0 = conv_halo
+#define DTC_OPT_ENUM(id, name, def) OPT_##id,
+  DTC_OPTION_LIST(DTC_OPT_ENUM)
+#undef DTC_OPT_ENUM
   OPT_COUNT
 };
 int option_get(int id);
@@ -279,13 +230,6 @@ int bn_bwd_fin_apply_mask(const u16* dy, const uint8_t* mbits, u16* dzo, const u
                           const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st,
                           u64* ts = nullptr);
 int bn_mask_apply(const u16* dy, const uint8_t* mbits, u16* dz, int64_t M, int C, hipStream_t st);
-// One-pass mask-bit BN backward (bn_bwd_reduce_mask + bn_bwd_fin_apply_mask in one launch with a grid
-// barrier; slice in registers): plan = rows per workgroup (0: no plan, use the two kernels). counter: an
-// int zeroed before the launch; *err set to 1 if the barrier ever timed out.
-int bn_bwd_fused_plan(int64_t M, int C, bool dual, int* R_out);
-int bn_bwd_fused(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
-                 const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, int* counter, int* err,
-                 hipStream_t st, u64* ts = nullptr);
 int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
                      u16* dx2, int64_t M, int C, hipStream_t st);
 int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2, const BnFwdArgs* a2, float* y,
@@ -324,10 +268,6 @@ int stem_fwd(const float* x, const u16* w27, u16* y, double* stats, int N, int H
 size_t stem_wgrad_slab_bytes(int64_t M);
 int stem_wgrad(const float* x, const u16* dy, float* dw27, float scale, int N, int H, int W, float* slab,
                size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
-// training forward, second pass (after a statistics-only stem_fwd with y = nullptr): recompute the conv,
-// store y and relu(BN(y)) + its ReLU mask bits (a: as bn_fin_apply's)
-int stem_fwd_bn(const float* x, const u16* w27, u16* y, const BnFwdArgs& a, u16* act, uint8_t* mask, int N, int H,
-                int W, hipStream_t st, u64* ts = nullptr);
 // stem weight gradient with the stem BN's backward apply fused: dc = A*(dy*bit) + B*c + Cc formed per
 // tile in LDS from (dy, mask bits, the conv output c) and the BN's slots (a: as bn_bwd_fin_apply's)
 int stem_wgrad_bn(const float* x, const u16* dy, const uint8_t* mbits, const u16* c, const BnBwdArgs& a, float* dw27,
@@ -338,9 +278,6 @@ int wgrad_reduce_to(const float* slab, int splits, int K, int RSC, int ncols, in
 // feat[n][c] = bf16round(mean_hw act); logits[n][j] = feat . W[j] + b[j]
 int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st);
-// the same, the logits pointer read on the device from *lslot (a word stored before a graph replay)
-int head_fwd_slot(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
-                  float* const* lslot, hipStream_t st);
 // mean cross entropy; lse per row
 int xent_fwd(const float* logits, const int64_t* labels, int N, int ncls, float* loss, float* lse,
              hipStream_t st);
@@ -365,9 +302,7 @@ int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st);
 // zero an 8-byte aligned range (a kernel node, unlike hipMemsetAsync's fill dispatch)
 int zero_bytes(void* p, size_t bytes, hipStream_t st);
 // dst[0:bytes] = src[0:bytes] (16-B aligned) and zp[0:zbytes] = 0 (8-B aligned), one launch
-int copy_and_zero(const void* src, void* dst, size_t bytes, void* zp, size_t zbytes, hipStream_t st,
-                  void* slot = nullptr, const void* slot_val = nullptr);
-int put_word(void* slot, const void* val, hipStream_t st);
+int copy_and_zero(const void* src, void* dst, size_t bytes, void* zp, size_t zbytes, hipStream_t st);
 // x[i] *= f (loopback test communicator)
 int scale_f32(float* x, int64_t n, float f, hipStream_t st);
 int scale_f64(double* x, int64_t n, double f, hipStream_t st);

@@ -76,38 +76,26 @@ int zero_bytes(void* p, size_t bytes, hipStream_t st) {
 }
 
 // The executor's forward prologue: the caller's input copied into the executor's own buffer (the
-// captured forward graph reads a fixed address) and the BN slots zeroed, in one launch. `slot`
-// (optional): the caller's logits pointer stored into an executor-owned word, read by the head kernel
-// inside the captured graph (option head_direct = 2: no launch after the graph).
+// captured forward graph reads a fixed address) and the BN slots zeroed, in one launch.
 __global__ void copy_zero_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16,
-                                 uint2* __restrict__ z, int64_t n8, uint64_t* __restrict__ slot, uint64_t val) {
+                                 uint2* __restrict__ z, int64_t n8) {
   const int64_t stride = (int64_t)gridDim.x * 256;
-  if (slot != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *slot = val;
   for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
   for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n8; i += stride) z[i] = uint2{0u, 0u};
 }
 
-int copy_and_zero(const void* src, void* dst, size_t bytes, void* zp, size_t zbytes, hipStream_t st, void* slot,
-                  const void* slot_val) {
+int copy_and_zero(const void* src, void* dst, size_t bytes, void* zp, size_t zbytes, hipStream_t st) {
   DTC_CHECK_ARG(src && dst && zp && bytes % 16 == 0 && zbytes % 8 == 0 && ((uintptr_t)src & 15) == 0 &&
-                    ((uintptr_t)dst & 15) == 0 && ((uintptr_t)zp & 7) == 0 && ((uintptr_t)slot & 7) == 0,
-                "copy_and_zero: 16-byte aligned copy, 8-byte aligned zero range and slot");
+                    ((uintptr_t)dst & 15) == 0 && ((uintptr_t)zp & 7) == 0,
+                "copy_and_zero: 16-byte aligned copy, 8-byte aligned zero range");
   const int64_t n16 = (int64_t)(bytes / 16), n8 = (int64_t)(zbytes / 8);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (std::max(n16, n8) + 255) / 256));
   hipLaunchKernelGGL(copy_zero_kernel, dim3(blocks), dim3(256), 0, st, (const uint4*)src, (uint4*)dst, n16, (uint2*)zp,
-                     n8, (uint64_t*)slot, (uint64_t)(uintptr_t)slot_val);
+                     n8);
   DTC_LAUNCH_CHECK();
   return 0;
 }
 
-// One pointer-sized word stored on the stream (the head's logits slot where copy_and_zero is not used).
-__global__ void put_word_kernel(uint64_t* slot, uint64_t val) { *slot = val; }
-int put_word(void* slot, const void* val, hipStream_t st) {
-  DTC_CHECK_ARG(slot && ((uintptr_t)slot & 7) == 0, "put_word: 8-byte aligned slot");
-  hipLaunchKernelGGL(put_word_kernel, dim3(1), dim3(1), 0, st, (uint64_t*)slot, (uint64_t)(uintptr_t)val);
-  DTC_LAUNCH_CHECK();
-  return 0;
-}
 
 template <typename T>
 __global__ void scale_kernel(T* __restrict__ x, int64_t n, T f) {

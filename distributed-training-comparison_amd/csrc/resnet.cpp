@@ -48,7 +48,6 @@ struct BNL {
   int64_t rm_off = 0, rv_off = 0;
   int nbt = 0;
   size_t stats = 0, acc = 0, mean = 0, invstd = 0, scale = 0, shift = 0, coef = 0;  // workspace byte offsets
-  size_t bar = 0;  // one-pass backward's grid-barrier counter (zeroed with the slots)
 };
 
 struct BlockL {
@@ -90,7 +89,6 @@ struct Net {
   hipStream_t side_st = nullptr;
   hipStream_t sc_st = nullptr;  // the projection shortcut's conv (fwd) / dgrad branch (option sc_stream)
   bool sc_pending = false;
-  size_t SLABSC = 0, slabsc_bytes = 0;  // split-K slab of the shortcut branch
   std::vector<hipEvent_t> evs;
   int ev_next = 0;
   bool side_pending = false;
@@ -133,8 +131,6 @@ struct Net {
   hipEvent_t launch_ev = nullptr;
   bool launched = false;
   size_t LOGITS = 0, DLOGITS = 0;  // graph-owned copies of the caller's logits / dlogits
-  size_t LSLOT = 0;  // (head_direct = 2) the caller's logits pointer, stored before each forward replay
-  int head_mode = 0;  // head_direct the current forward graphs were captured with
   // activation registry (per-layer parity): name, workspace byte offset, N,H,W,C
   struct Act { std::string name; size_t off; int n, h, w, c; };
   std::vector<Act> acts;
@@ -328,7 +324,6 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.FEAT = take(B * 512 * 4);
   n.LOGITS = take(B * n.ncls * 4);
   n.DLOGITS = take(B * n.ncls * 4);
-  n.LSLOT = take(64);
   n.HEADWS_bytes = head_bwd_workspace((int)B, 512, n.ncls);
   n.HEADWS = take(n.HEADWS_bytes);
   n.acts.push_back({"head.feat_f32", n.FEAT, (int)B, 1, 1, 512});
@@ -347,7 +342,6 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   for (BNL* b : n.bns) b->stats = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
   n.acc_lo = off;
   for (BNL* b : n.bns) b->acc = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
-  for (BNL* b : n.bns) b->bar = take(8 * 64);  // BF_LINES counters, 64 B apart
   n.BNERR = take(256);
   n.stats_hi = off;
   for (BNL* b : n.bns) {
@@ -378,11 +372,6 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.slab_bytes = slab;
   n.SLAB = take(slab);
   n.SLABW = take(slab);
-  size_t slabsc = 64 * 64 * 4;  // the shortcut branch runs beside the main-stream convs: its own slab
-  for (auto& b : n.blocks)
-    if (b.proj && !n.f32) slabsc = std::max({slabsc, plan_conv(b.sc.s, CONV_FWD).slab_bytes, plan_conv(b.sc.s, CONV_DGRAD).slab_bytes});
-  n.SLABSC = take(slabsc);
-  n.slabsc_bytes = slabsc;
   if (n.capture) {
     auto cap = [&](const std::string& nm, int h, int w, int c) {
       n.caps.push_back({nm, take((size_t)B * h * w * c * E), (int)B, h, w, c});
@@ -486,11 +475,10 @@ static void drop_graphs(Net& n) {
 }
 static int graph_launch(Net& n, hipGraphExec_t ex, hipStream_t st) {
   DTC_HIP(hipGraphLaunch(ex, st));
-  if (option_get(OPT_GRAPH_EV) != 0) {
-    if (!n.launch_ev) DTC_HIP(hipEventCreateWithFlags(&n.launch_ev, hipEventDisableTiming));
-    DTC_HIP(hipEventRecord(n.launch_ev, st));
-    n.launched = true;
-  }
+  // drop_graphs waits on this event (the exec's last launch retired) before destroying an exec
+  if (!n.launch_ev) DTC_HIP(hipEventCreateWithFlags(&n.launch_ev, hipEventDisableTiming));
+  DTC_HIP(hipEventRecord(n.launch_ev, st));
+  n.launched = true;
   return 0;
 }
 // option graphs: 0 = eager launches, 1 = forward and backward replayed from hipGraphs, 2 = forward only,
@@ -621,16 +609,10 @@ static int bn_act(Net& n, int mode, BNL& b, const u16* x, BNL* b2, const u16* x2
 
 static ConvShape f32_stem_shape(const Net& n);
 static int forward_body_f32(Net& n, float* logits, bool train, hipStream_t st);
-static int fork_sc(Net& n, hipStream_t st, hipStream_t* out);
-static bool sc_on(const Net& n);
-static int join_sc(Net& n, hipStream_t st);
 
 // everything after the input im2col (reads only executor-owned memory: capturable)
 static int forward_head(Net& n, float* logits, hipStream_t st) {
   const BlockL& last = n.blocks.back();
-  if (logits == nullptr)  // head_direct = 2, inside the graph: the destination is read from LSLOT
-    return head_fwd_slot(n.at<u16>(last.OUT), n.B, last.Hout * last.Wout, 512, n.wbf(n.fc_w), n.pf(n.fc_b), n.ncls,
-                         n.at<float>(n.FEAT), n.at<float* const>(n.LSLOT), st);
   return head_fwd(n.at<u16>(last.OUT), n.B, last.Hout * last.Wout, 512, n.wbf(n.fc_w), n.pf(n.fc_b), n.ncls,
                   n.at<float>(n.FEAT), logits, st);
 }
@@ -643,17 +625,7 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   // forward accumulates into zeroed slots; its graph then starts with real work, no memset node) --
   // done by forward()'s input-copy launch on the direct-stem path
   if (train && !n.stem_direct) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));
-  // option stem_recompute: statistics pass + a recompute pass that applies the BN (stem.hip)
-  const bool srec = n.stem_direct && train && !n.sync && bn_fused() && bn_mask_on(n) &&
-                    option_get(OPT_STEM_RECOMPUTE) != 0;
-  if (srec) {
-    PROF(0, 2.0 * M0 * 64 * 27,
-         stem_fwd(n.at<float>(n.XIN), n.wbf(n.stem.pidx), nullptr, n.at<double>(n.bn0.stats), n.B, n.H, n.W, st, ts));
-    const BnFwdArgs a0 = fwd_args(n, n.bn0, M0);
-    PROF(0, 2.0 * M0 * 64 * 27,
-         stem_fwd_bn(n.at<float>(n.XIN), n.wbf(n.stem.pidx), n.at<u16>(n.C0), a0, n.at<u16>(n.A0),
-                     n.at<uint8_t>(n.MA0), n.B, n.H, n.W, st, ts));
-  } else if (n.stem_direct) {  // stem.hip: taps gathered per tile from the fp32 input, one K=32 k-step
+  if (n.stem_direct) {  // stem.hip: taps gathered per tile from the fp32 input, one K=32 k-step
     PROF(0, 2.0 * M0 * 64 * 27,
          stem_fwd(n.at<float>(n.XIN), n.wbf(n.stem.pidx), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
                   n.B, n.H, n.W, st, ts));
@@ -663,21 +635,18 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
          conv_fwd(n.stem.s, n.at<u16>(n.X0), n.at<u16>(n.WSTEM), n.at<u16>(n.C0),
                   train ? n.at<double>(n.bn0.stats) : nullptr, n.at<float>(n.SLAB), n.slab_bytes, st, ts));
   }
-  if (!srec) DTC_TRY(bn_act(n, 1, n.bn0, n.at<u16>(n.C0), nullptr, nullptr, n.at<u16>(n.A0), M0, train, st, n.MA0));
+  DTC_TRY(bn_act(n, 1, n.bn0, n.at<u16>(n.C0), nullptr, nullptr, n.at<u16>(n.A0), M0, train, st, n.MA0));
   const u16* in = n.at<u16>(n.A0);
   n.ev_next = 0;
   for (auto& b : n.blocks) {
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
     float* slab = n.at<float>(n.SLAB);
     // option sc_fuse: the projection shortcut inside conv1's launch (its centre-tap im2col tiles)
-    const bool scf = b.proj && !sc_on(n) && option_get(OPT_SC_FUSE) != 0 && conv_fwd_sc_ok(b.c1.s, b.sc.s);
-    if (b.proj && !scf) {  // the shortcut conv first, on its own stream when sc_stream is on (joined below)
-      hipStream_t ss = st;
-      DTC_TRY(fork_sc(n, st, &ss));
+    const bool scf = b.proj && option_get(OPT_SC_FUSE) != 0 && conv_fwd_sc_ok(b.c1.s, b.sc.s);
+    if (b.proj && !scf)  // the shortcut conv first
       PROF(0, conv_flops(b.sc.s),
-           conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr,
-                    ss == st ? slab : n.at<float>(n.SLABSC), ss == st ? n.slab_bytes : n.slabsc_bytes, ss, ts));
-    }
+           conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr, slab,
+                    n.slab_bytes, st, ts));
     if (scf) {
       PROF(0, conv_flops(b.c1.s) + conv_flops(b.sc.s),
            conv_fwd_sc(b.c1.s, b.sc.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr,
@@ -692,15 +661,14 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
          conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
                   train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st, ts));
     if (b.proj) {
-      DTC_TRY(join_sc(n, st));
       DTC_TRY(bn_act(n, 3, b.b2, n.at<u16>(b.C2), &b.bsc, n.at<u16>(b.S), n.at<u16>(b.OUT), M, train, st, b.MOUT));
     } else {
       DTC_TRY(bn_act(n, 2, b.b2, n.at<u16>(b.C2), nullptr, in, n.at<u16>(b.OUT), M, train, st, b.MOUT));
     }
     in = n.at<u16>(b.OUT);
   }
-  // graphed forward with head_direct = 1: the head is launched by forward() after the graph
-  if (logits == nullptr && n.head_mode != 2) return 0;
+  // graphed forward: the head is launched by forward() after the graph, into the caller's logits
+  if (logits == nullptr) return 0;
   return forward_head(n, logits, st);
 }
 
@@ -879,39 +847,31 @@ static int forward(Net& n, const float* x, float* logits, bool train, hipStream_
   return 0;
 }
 static int forward_impl(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
-  // option head_direct: 0 = the head writes a graph-owned buffer copied out after the graph; 1 = the
-  // pool + FC head launched after the graph straight into the caller's logits (the graph cannot bake
-  // in a per-call pointer); 2 = the head inside the graph, its destination read from LSLOT, which the
-  // input-copy launch stores before the replay (the ~14 us graph-completion -> next-kernel gap goes)
-  const int hmode = (!n.f32 && graphs_on(n, false)) ? option_get(OPT_HEAD_DIRECT) : 0;
+  // graphed bf16 forward: the pool + FC head is launched after the graph straight into the caller's logits
+  // (the graph cannot bake in a per-call pointer); the fp32 executor's graph writes a graph-owned buffer
+  // that is copied out after the replay
   if (n.f32) DTC_TRY(f32_stem_im2col(x, n.at<float>(n.X0), n.B, n.H, n.W, st));
   else if (n.stem_direct) {  // the graph reads only executor memory: a copy of the 12 B/pixel input (+ the
-    // training step's BN slots zeroed in the same launch, + the logits pointer for head_direct = 2)
+    // training step's BN slots zeroed in the same launch)
     const size_t xb = (size_t)n.B * 3 * n.H * n.W * 4;
     if (xb % 16 == 0 && ((uintptr_t)x & 15) == 0 && option_get(OPT_STEM_PROLOGUE) != 0) {
-      DTC_TRY(copy_and_zero(x, n.at<float>(n.XIN), xb, n.ws + n.stats_lo, train ? n.stats_hi - n.stats_lo : 0, st,
-                            hmode == 2 ? n.ws + n.LSLOT : nullptr, logits));
+      DTC_TRY(copy_and_zero(x, n.at<float>(n.XIN), xb, n.ws + n.stats_lo, train ? n.stats_hi - n.stats_lo : 0, st));
     } else {
       DTC_HIP(hipMemcpyAsync(n.at<float>(n.XIN), x, xb, hipMemcpyDeviceToDevice, st));
       if (train) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));
-      if (hmode == 2) DTC_TRY(put_word(n.ws + n.LSLOT, logits, st));
     }
   } else {
     DTC_TRY(stem_im2col(x, n.at<u16>(n.X0), n.B, n.H, n.W, st));
-    if (hmode == 2) DTC_TRY(put_word(n.ws + n.LSLOT, logits, st));
   }
   if (!graphs_on(n, false)) return forward_body(n, logits, train, st);
   hipGraphExec_t& ex = n.fwd_exec[n.profiling ? 1 : 0][train ? 1 : 0];
-  if (ex && n.head_mode != hmode) drop_graphs(n);  // (option epochs normally re-capture already)
   if (!ex) {
-    n.head_mode = hmode;
     DTC_TRY(begin_capture(n));
-    const int rc = forward_body(n, hmode >= 1 ? nullptr : n.at<float>(n.LOGITS), train, n.cap_st);
+    const int rc = forward_body(n, n.f32 ? n.at<float>(n.LOGITS) : nullptr, train, n.cap_st);
     DTC_TRY(end_capture(n, rc, &ex));
   }
   DTC_TRY(graph_launch(n, ex, st));
-  if (hmode == 2) return 0;
-  if (hmode == 1) return forward_head(n, logits, st);
+  if (!n.f32) return forward_head(n, logits, st);
   DTC_HIP(hipMemcpyAsync(logits, n.at<float>(n.LOGITS), (size_t)n.B * n.ncls * 4, hipMemcpyDeviceToDevice, st));
   return 0;
 }
@@ -995,21 +955,6 @@ static int bn_bwd_coef_apply(Net& n, BNL& b1, const u16* dz, const u16* x1, u16*
   return bn_bwd_apply(dz, x1, n.at<float>(b1.coef), dx1, x2, b2 ? n.at<float>(b2->coef) : nullptr, dx2, M, b1.C, st);
 }
 
-// One-pass BN backward (bn.hip bn_bwd_fused: reduce + grid barrier + apply in one launch, the slice in
-// registers) where it has a plan; else bn_bwd_reduce_mask + bn_bwd_coef_apply. Same outputs.
-static bool onepass_ok(const Net& n, int64_t M, int C, bool dual) {
-  int R = 0;
-  return option_get(OPT_BN_ONEPASS) != 0 && n.sync == nullptr && bn_fused() && bn_bwd_fused_plan(M, C, dual, &R) > 0;
-}
-static int bn_bwd_onepass(Net& n, BNL& b1, const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, u16* dx1,
-                          BNL* b2, const u16* x2, u16* dx2, int64_t M, float gs, hipStream_t st) {
-  const BnBwdArgs a1 = bwd_args(n, b1, M, gs);
-  const BnBwdArgs a2 = b2 ? bwd_args(n, *b2, M, gs) : BnBwdArgs{};
-  u64* ts = prof_slot(n, 3, (double)M * b1.C * (6.125 + (x2 ? 4.0 : 0.0) + (dzo ? 2.0 : 0.0)));
-  return bn_bwd_fused(dy, mbits, dzo, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, n.at<int>(b1.bar),
-                      n.at<int>(n.BNERR), st, ts);
-}
-
 // Side stream for the weight gradients (fork after their input gradient exists, join before
 // anything reads the weight gradients: bucket all-reduces and the end of backward).
 static bool side_on(const Net& n) { return option_get(OPT_BWD_STREAMS) != 0; }
@@ -1053,35 +998,6 @@ static int join_side(Net& n, hipStream_t st) {
   DTC_HIP(hipEventRecord(ev, n.side_st));
   DTC_HIP(hipStreamWaitEvent(st, ev, 0));
   n.side_pending = false;
-  return 0;
-}
-
-// The projection shortcut's 1x1 stride-2 conv is independent of conv1 / conv2 of its block (forward:
-// it reads the block input; backward: its dgrad needs only dsc). Both are small latency-bound launches,
-// so they run on a stream of their own beside the main chain (option sc_stream) and join before the
-// consumer (the dual BN apply; conv1's dgrad, which adds dx_sc as its residual).
-static bool sc_on(const Net& n) { return option_get(OPT_SC_STREAM) != 0 && !n.f32 && n.sync == nullptr; }
-static int fork_sc(Net& n, hipStream_t st, hipStream_t* out) {
-  if (!sc_on(n)) {
-    *out = st;
-    return 0;
-  }
-  if (!n.sc_st) DTC_HIP(hipStreamCreateWithFlags(&n.sc_st, hipStreamNonBlocking));
-  hipEvent_t ev;
-  DTC_TRY(next_event(n, &ev));
-  DTC_HIP(hipEventRecord(ev, st));
-  DTC_HIP(hipStreamWaitEvent(n.sc_st, ev, 0));
-  n.sc_pending = true;
-  *out = n.sc_st;
-  return 0;
-}
-static int join_sc(Net& n, hipStream_t st) {
-  if (!n.sc_pending) return 0;
-  hipEvent_t ev;
-  DTC_TRY(next_event(n, &ev));
-  DTC_HIP(hipEventRecord(ev, n.sc_st));
-  DTC_HIP(hipStreamWaitEvent(st, ev, 0));
-  n.sc_pending = false;
   return 0;
 }
 
@@ -1136,9 +1052,8 @@ static int fork_side(Net& n, hipStream_t st, hipStream_t* out);
 // instead of by the caller before every wgrad (a queued-only wgrad needs no fork: the launch's fork
 // is later on the main stream, so it covers the queued inputs too)
 static int wg_issue(Net& n, WgQueue& q, const ConvShape& s, const u16* x, const u16* dy, float* dw, float gs,
-                    float* slabw, hipStream_t& sd, bool defer = false, int bcap = 0, hipStream_t st = nullptr,
-                    bool lazy = false) {
-  const int bmax = bcap > 0 ? std::min(bcap, wgrad_batch_max()) : wgrad_batch_max();
+                    float* slabw, hipStream_t& sd, hipStream_t st = nullptr, bool lazy = false) {
+  const int bmax = wgrad_batch_max();
   if (bmax <= 1 || wgrad_halo_splits(s, 2) <= 0) {
     if (lazy) DTC_TRY(fork_side(n, st, &sd));
     PROF(2, conv_flops(s), conv_wgrad(s, x, dy, dw, 0, 0, gs, slabw, n.slab_bytes, sd, ts));
@@ -1152,7 +1067,7 @@ static int wg_issue(Net& n, WgQueue& q, const ConvShape& s, const u16* x, const 
   q.x[q.count] = x;
   q.dy[q.count] = dy;
   q.dw[q.count] = dw;
-  if (++q.count >= bmax && !defer) {
+  if (++q.count >= bmax) {
     if (lazy) DTC_TRY(fork_side(n, st, &sd));
     DTC_TRY(wg_flush(n, q, gs, slabw, sd));
   }
@@ -1225,9 +1140,6 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
       // writes dz over it as before (the residual of its conv1 dgrad; idempotent on dz)
       DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[0], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
                                 b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st, mout, b.proj ? nullptr : G[0]));
-    } else if (onepass_ok(n, M, b.Cout, b.proj)) {
-      DTC_TRY(bn_bwd_onepass(n, b.b2, G[0], mout, b.proj ? nullptr : G[0], n.at<u16>(b.C2), dc2,
-                             b.proj ? &b.bsc : nullptr, b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st));
     } else {
       PROF(3, (double)M * b.Cout * (b.proj ? 6.125 : 4.125),
            bn_bwd_reduce_mask(G[0], mout, n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
@@ -1239,31 +1151,15 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     }
     DTC_TRY(cap(n, cp + ".dc2", dc2, st));
     if (b.proj) DTC_TRY(cap(n, cp + ".ds", dsc, st));
-    const bool sc_branch = b.proj && sc_on(n);
     // the shortcut's dx at its stride-2 grid only (option sc_compact): the 1x1 stride-2 conv's dgrad
     // is zero at three of four parities; conv1's parity-class dgrad adds it at the fourth
     const bool sc_cmp = b.proj && !n.capture && option_get(OPT_SC_COMPACT) != 0 && dgrad_class_ok(b.c1.s);
     const ConvShape sc_dg = sc_cmp ? ConvShape{b.sc.s.N, b.Hout, b.Wout, b.sc.s.C, b.sc.s.K, 1, 1, 1, 0} : b.sc.s;
     // option dgrad_scf: the shortcut's dgrad as extra reduction steps of conv1's class-(0, 0) dgrad (one launch)
-    const bool dscf = b.proj && !n.capture && !sc_branch && conv_dgrad_sc_ok(b.c1.s);
-    if (sc_branch) {  // dx of the shortcut (conv1's dgrad residual) beside conv2's dgrad and BN1's backward
-      hipStream_t ss = st;
-      DTC_TRY(fork_sc(n, st, &ss));
-      PROF(1, conv_flops(b.sc.s),
-           conv_dgrad(sc_dg, dsc, n.wbf(b.sc.pidx), G[5], nullptr, n.at<float>(n.SLABSC), n.slabsc_bytes, ss, ts));
-    }
-    // option wgrad_defer: the halo-geometry wgrads are only queued here; their batched launch is forked
-    // after the layer's last dgrad (below), so it overlaps the HBM-bound BN chain that follows rather
-    // than the dgrads (measured -1% at B=256: the wgrad batch then starves the BN kernels instead)
-    // (wgrad_defer = 2: layer1 only -- its 4-conv batch then runs beside the stem's tail instead of beside
-    // layer1.0's last dgrad, the persistent conv_c64 kernel that wants every CU)
-    const int dopt = option_get(OPT_WGRAD_DEFER);
-    const bool defer = dopt == 1 || (dopt == 2 && bi < 2);
-    // option wgrad_tail: smaller batches for layer1, whose last batch is the backward's tail
-    const int bcap = bi < 2 ? option_get(OPT_WGRAD_TAIL) : 0;
-    const bool lazy = option_get(OPT_FORK_LAZY) != 0 && !defer;
+    const bool dscf = b.proj && !n.capture && conv_dgrad_sc_ok(b.c1.s);
+    const bool lazy = option_get(OPT_FORK_LAZY) != 0;
     if (!lazy) DTC_TRY(fork_side(n, st, &sd));
-    DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd, defer, bcap, st, lazy));
+    DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd, st, lazy));
     {
       const BnbArgs bz = bnb_mask_of(n, b.MA1, b.C1, b.b1);
       PROF(1, conv_flops(b.c2.s),
@@ -1273,8 +1169,6 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     DTC_TRY(cap_masked(n, cp + ".dz1", G[4], b.MA1, M, b.Cout, st));
     if (bmf) {  // bn1's sums came with conv2's dgrad
       DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st, ma1));
-    } else if (onepass_ok(n, M, b.Cout, false)) {
-      DTC_TRY(bn_bwd_onepass(n, b.b1, G[4], ma1, nullptr, n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st));
     } else {
       PROF(3, (double)M * b.Cout * 4.125,
            bn_bwd_reduce_mask(G[4], ma1, n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
@@ -1291,7 +1185,7 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
       PROF(2, conv_flops(b.c1.s) + conv_flops(b.sc.s),
            conv_wgrad_s2(b.c1.s, in, dc1, dsc, n.gf(b.c1.pidx), n.gf(b.sc.pidx), gs, slabw, n.slab_bytes, sd, ts));
     } else {
-      DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, defer, bcap, st, lazy && !b.proj));
+      DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, st, lazy && !b.proj));
     }
     BnbArgs bp;  // the block input's gradient feeds the previous block's bn2 (+ its projection BN) or the stem BN
     if (bmf) {
@@ -1310,8 +1204,7 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
         PROF(1, conv_flops(b.c1.s) + conv_flops(b.sc.s),
              conv_dgrad_sc(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], dsc, n.wbf(b.sc.pidx), st, ts, bpp));
       } else {
-        if (sc_branch) DTC_TRY(join_sc(n, st));
-        else PROF(1, conv_flops(b.sc.s), conv_dgrad(sc_dg, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
+        PROF(1, conv_flops(b.sc.s), conv_dgrad(sc_dg, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
         PROF(1, conv_flops(b.c1.s),
              conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts, bpp, sc_cmp ? 1 : 0));
       }
@@ -1321,15 +1214,8 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     }
     sums_ready = bmf;
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
-    if (!defer) {
-      if (bucket_fires(n, bi)) {
-        if (lazy && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
-        DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
-      }
-    } else if (wq.count > 0 && (bi % 2 == 0 || wq.count >= wgrad_batch_max() || bucket_fires(n, bi))) {
-      // a layer's queued wgrads (its first block is the last one processed), a full queue, or a bucket
-      // point: launch the batch on the side stream once this block's dgrads are done
-      DTC_TRY(fork_side(n, st, &sd));
+    if (bucket_fires(n, bi)) {
+      if (lazy && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
       DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
     }
     DTC_TRY(maybe_bucket(n, bi, cx, st));
@@ -1358,8 +1244,6 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   }
   if (sums_ready) {
     DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[0], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st, m0));
-  } else if (onepass_ok(n, M0, 64, false)) {
-    DTC_TRY(bn_bwd_onepass(n, n.bn0, G[0], m0, nullptr, n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st));
   } else {
     PROF(3, (double)M0 * 64 * 4.125,
          bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
@@ -1702,7 +1586,10 @@ int dtc_rn18_profile_begin(dtc_net* net, int capacity) {
   DTC_HIP(hipDeviceGetAttribute(&n.prof_khz, hipDeviceAttributeWallClockRate, dev));
   DTC_CHECK_ARG(n.prof_khz > 0, "dtc_rn18_profile_begin: no wall clock rate");
   // the previous step may still run (its profiled graphs stamp these slots): drain, then reset.
-  // slots -> (~0, 0) (folding all-zero slots adds nothing and resets them), then totals -> 0
+  // slots -> (~0, 0) (folding all-zero slots adds nothing and resets them), then totals -> 0.
+  // The drains hold g_graph_mu like drop_graphs: no device drain while another host
+  // thread's stream is capturing.
+  std::lock_guard<std::recursive_mutex> lk(g_graph_mu);
   DTC_HIP(hipDeviceSynchronize());
   DTC_HIP(hipMemset(n.prof_ts, 0, ts_bytes));
   DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, nullptr));
@@ -1727,6 +1614,7 @@ int dtc_rn18_profile_end_ex(dtc_net* net, int nkinds, double* ms_by_kind, double
   }
   if (!n.profiling) return 0;
   std::vector<u64> acc((size_t)Net::PROF_SLOTS * 2);
+  std::lock_guard<std::recursive_mutex> lk(g_graph_mu);  // as profile_begin
   DTC_HIP(hipDeviceSynchronize());
   DTC_HIP(hipMemcpy(acc.data(), n.prof_acc, acc.size() * sizeof(u64), hipMemcpyDeviceToHost));
   for (int i = 0; i < Net::PROF_SLOTS; ++i) {

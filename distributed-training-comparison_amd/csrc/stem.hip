@@ -150,19 +150,13 @@ static StemGeom stem_geom(int N, int H, int W) {
 // ds_read_b128 group read 16 consecutive pixels' same chunk -> 16 distinct 16-B bank slots.
 // <= 40 KB LDS and <= 128 VGPRs: four workgroups per CU, so the 1024 tiles of a 256 x 32 x 32 batch
 // are all resident at once and their load latencies overlap (a workgroup does little else).
-// APPLY (option stem_recompute, training): the stem BN's forward is split around two passes of this
-// kernel -- pass 1 (APPLY = false, y = nullptr) only accumulates the statistics (nothing stored: 12 B
-// of input per pixel read), pass 2 (APPLY) recomputes the conv (0.9 GFLOP), stores y and applies the
-// BN + ReLU to it in the same epilogue (act + ReLU mask bits, bn_fin_apply<RELU>'s arithmetic): the
-// separate apply's 128 B/pixel re-read of y is gone, and so is one launch.
 // WL (option stem_wlds): the [64][27] bf16 weight is read once per workgroup with coalesced 4-B loads
 // into LDS and the A fragments are gathered from there, instead of 32 scattered 2-B global loads per
 // lane; the staged input rows are capped at 8 KB (STEM_BN_CAP) so the LDS stays at four per CU.
-template <bool APPLY, bool WL = false>
+template <bool WL = false>
 __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restrict__ x, const u16* __restrict__ w27,
                                                       u16* __restrict__ y, double* __restrict__ stats, const StemGeom G,
-                                                      u64* ts, const BnFwdArgs a, u16* __restrict__ act,
-                                                      uint8_t* __restrict__ mask) {
+                                                      u64* ts) {
   constexpr int CAP = WL ? 2048 : STEM_LDS_FLOATS;
   // cols (16 KB) + the staged input rows (20 KB; WL 8 KB); after the MFMAs the first 32 KB hold the
   // output tile [256 pixels][128 B] for 16-B coalesced stores
@@ -173,12 +167,8 @@ __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restric
   float* const xt = (float*)(smem + 256 * 64);
   char* const ot = smem;
   stamp_start(ts);
-  static_assert(!(APPLY && WL), "stem_fwd: WL with the recompute-apply pass is not built");
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint32_t pix0 = blockIdx.x * 256u;
-  float* const csc = &red[0][0][0];  // APPLY: BN scale / shift of the 64 channels (no statistics here)
-  SlotFold f;
-  if constexpr (APPLY) fold_issue_fwd(a, 64, 0, f);  // first: in-order vmcnt (bn_coef.h)
   // A fragments W[k = i*16 + lane%16][kk = 8*(lane/16) + 0..7] (kk >= 27: 0): all 32 loads issued
   // before the input tile's, so the two latencies overlap
   uint32_t we[4][4];  // bf16 pairs
@@ -198,8 +188,6 @@ __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restric
 #pragma unroll
     for (int u = 0; u < 4; ++u) wv[u] = w32[min(t + 256 * u, 863)];
   }
-  // the fold's LDS scratch is the cols region (written only after the fold's last barrier)
-  if constexpr (APPLY) fa_fwd_coef_from(a, f, 64, 0, (double*)smem, csc, csc + 64);
   {
     const StemTile T = WL ? stem_tile<CAP>(pix0, G) : stem_tile<STEM_LDS_FLOATS>(pix0, G);
     float xv[CAP / 256];
@@ -278,22 +266,10 @@ __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restric
       if ((uint32_t)px < npx) {
         const uint4 raw = *(const uint4*)(ot + px * 128 + ((c ^ (px & 7)) << 4));
         dst[g] = raw;
-        if constexpr (APPLY) {  // relu(y * scale + shift) and its mask byte (bn_fin_apply<RELU>)
-          float v[8];
-          unpack8(raw, v);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            v[k] = v[k] * csc[c * 8 + k] + csc[64 + c * 8 + k];
-            v[k] = fmaxf(v[k], 0.f);
-          }
-          const uint4 pk = pack8(v);
-          ((uint4*)act)[(size_t)pix0 * 8 + g] = pk;
-          mask[(size_t)pix0 * 8 + g] = (uint8_t)Elt<u16>::mask8(pk);
-        }
       }
     }
   }
-  if (!APPLY && stats != nullptr) {
+  if (stats != nullptr) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -326,24 +302,11 @@ int stem_fwd(const float* x, const u16* w27, u16* y, double* stats, int N, int H
   const int64_t M = (int64_t)N * H * W;
   DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_fwd: more than 2^31 pixels");
   if (option_get(OPT_STEM_WLDS) != 0 && ((uintptr_t)w27 & 3) == 0)
-    hipLaunchKernelGGL((stem_fwd_kernel<false, true>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y,
-                       stats, stem_geom(N, H, W), ts, BnFwdArgs{}, nullptr, nullptr);
+    hipLaunchKernelGGL((stem_fwd_kernel<true>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y,
+                       stats, stem_geom(N, H, W), ts);
   else
-    hipLaunchKernelGGL((stem_fwd_kernel<false, false>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y,
-                       stats, stem_geom(N, H, W), ts, BnFwdArgs{}, nullptr, nullptr);
-  DTC_LAUNCH_CHECK();
-  return 0;
-}
-
-int stem_fwd_bn(const float* x, const u16* w27, u16* y, const BnFwdArgs& a, u16* act, uint8_t* mask, int N, int H,
-                int W, hipStream_t st, u64* ts) {
-  DTC_CHECK_ARG(x && w27 && y && act && mask && a.stats && a.gamma && a.beta && a.mean && a.invstd && N > 0 &&
-                    H > 0 && W > 0,
-                "stem_fwd_bn: bad args");
-  const int64_t M = (int64_t)N * H * W;
-  DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_fwd_bn: more than 2^31 pixels");
-  hipLaunchKernelGGL((stem_fwd_kernel<true, false>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y, nullptr,
-                     stem_geom(N, H, W), ts, a, act, mask);
+    hipLaunchKernelGGL((stem_fwd_kernel<false>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y,
+                       stats, stem_geom(N, H, W), ts);
   DTC_LAUNCH_CHECK();
   return 0;
 }

@@ -40,8 +40,6 @@ struct HaloParams {
   int steps_per_split, nsteps;
   int rs, hb, nh;  // output rows per image per step, halo rows per image block, halo rows per step
   int spi;         // pixels per image block of a step (rs * W)
-  int nostore;     // diagnostics only (option wgrad_diag = 1): skip the slab stores (wrong results)
-  int diag;        // diagnostics only: 2 = no halo DMA after the first stage, 3 = no dy DMA after it
   int xcd;         // 1: XCD-grouped decode of the workgroup id (wg_coords)
   u64* ts;
   // halo row pitch (stride 1: W + 2) and output dims (stride 1: H, W); stride 2 (ST = 2): the x halo is
@@ -54,34 +52,18 @@ struct HaloParams {
   const u16* dsc;
   float* slab_sc;  // [splits][K][C] (or, direct, dw_sc)
   float* dw_sc;
-  // tr-read bank layout (stride 1; option wgrad_pmap): which pixel of the step each (k-step, 16-lane block
-  // b, read h, lane quad q) reads, and the second row bit of the halo / dy 16-B chunk swizzle (the first is
-  // row bit 1). A ds_read_b64_tr_b16 is conflict-free when the 8 rows its 32-lane half reads have distinct
-  // (row parity, swizzle): pmap 0 (pixels 8b + 4h + q, swizzle bits 1 and 3) is for 16- and 32-wide
-  // rows only -- at W = 8 and 4 some taps read two rows into one bank slot (PMC: 22% of the LDS cycles of
-  // the layer3/4 launches were conflict cycles); pmap 1 (W >= 8: pixels 16h + 4b + q, i.e. 8 consecutive
-  // pixels of one image row per half-read; bits 1 and 2) and pmap 2 (4x4 images: rows r and r ^ 2 of one
-  // image per half-read; halo bits 1, 2, dy bits 1, 3) are conflict-free for every tap (tools/tr_banks.py)
-  int pmap, hsb, dsb;
   // general geometry (GEN kernels; stride 1, e.g. the 224x224 model's 224/112/56/28-wide rows): a step is
   // rs rows x seg columns of one image (rs * seg <= 64 real pixels; the remaining MFMA reduction slots of
   // the 64-pixel step carry zero dy), its halo (rs + 2) x (seg + 2) pixels; every step addresses x and dy
   // from a 64-bit per-step base, so an activation may exceed 2 GB (512 x 224 x 224 x 64 bf16 = 3.3 GB)
-  int prio;            // 1: waves 4-7 at s_setprio 1 (MI355X_MICROARCH "Two waves per SIMD" item 4; option wgrad_prio)
   int seg, spimg;      // pixels per row segment, steps per image
   FastDiv fd_spimg, fd_spr, fd_seg, fd_seg2;  // steps per image, segments per row, seg, seg + 2
 };
 
 // pixel (within the 64-pixel step) of k-step ks, lane block b = lane >> 4, tr read h, lane quad q
-__device__ __forceinline__ int wg_pixel(int pmap, int ks, int b, int h, int q) {
-  if (pmap == 1) return ks * 32 + 16 * h + 4 * b + q;
-  if (pmap == 2) return ks * 32 + (b >> 1) * 16 + (h + 2 * (b & 1)) * 4 + q;
-  return ks * 32 + 8 * b + q + 4 * h;
-}
-// 16-B chunk swizzle of LDS row r: row bits 1 and `sb` -> chunk bits 1 and 2 (sb = 3: trswz)
-__device__ __forceinline__ int wg_swz(int r, int sb) { return (((r >> 1) & 1) << 1) | (((r >> sb) & 1) << 2); }
-// the same as an 8-B unit XOR (unit index bits 2 and 3)
-__device__ __forceinline__ int wg_uswz(int r, int sb) { return (((r >> 1) & 1) << 2) | (((r >> sb) & 1) << 3); }
+__device__ __forceinline__ int wg_pixel(int ks, int b, int h, int q) { return ks * 32 + 8 * b + q + 4 * h; }
+// the trswz swizzle of LDS row r as an 8-B unit XOR (unit index bits 2 and 3)
+__device__ __forceinline__ int wg_uswz(int r) { return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3); }
 
 // (output tile, split, problem) of this workgroup. Workgroups are dispatched to the 8 XCDs round-robin
 // by linear id, so with the plain grid decode the tiles of one (problem, split) -- which read the same
@@ -122,35 +104,16 @@ struct WgStage {
   static constexpr int BYTES = HALO_BYTES + 64 * 128 * (SC ? 2 : 1);
 };
 
-// Tr-image fragment from the halo: lane holds column (channel) cin + lane&15, reduction rows =
-// the pixels whose halo rows are ra (4 pixels) and rb (next 4), already shifted by the tap.
-__device__ __forceinline__ bf16x8 frag_halo(const char* halo, int cin, int ra, int rb, int lane) {
-  const int unit = (cin >> 2) + (lane & 3);
-  const int fa = (((ra >> 1) & 1) << 2) | (((ra >> 3) & 1) << 3);
-  const int fb = (((rb >> 1) & 1) << 2) | (((rb >> 3) & 1) << 3);
-  typedef __attribute__((address_space(3))) bf16x4_t lds_v4;
-  bf16x4_t t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(halo + ra * 128 + ((unit ^ fa) << 3)));
-  bf16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(halo + rb * 128 + ((unit ^ fb) << 3)));
-  return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
 // NS: pipeline stages in the LDS ring (2: wait for the next step's DMA at every step; 4: three
-// steps of DMA in flight, a counted s_waitcnt per step). NR: halo DMA rounds per step (2 or 3).
-// PF: 0 = fragments read next to their MFMAs (compiler-scheduled), > 0 = explicit LDS prefetch
-// window: the step's 22 operand fragments (per k-step: 2 dy, 9 halo) are read PF fragments ahead
-// of the MFMAs that consume them, one fragment (two ds_read_b64_tr_b16) issued per consumed halo
-// fragment, so an LDS read's latency hides behind the MFMAs of the PF fragments before it.
-template <int NS, int NR, int PF, int ST = 1, bool SC = false, bool GEN = false>
+// steps of DMA in flight, a counted s_waitcnt per step). NR: halo DMA rounds per step.
+template <int NS, int NR, int ST = 1, bool SC = false, bool GEN = false>
 __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   typedef WgStage<NR, SC> SG;
   constexpr int PER = NR + 1 + (SC ? 1 : 0);  // LDS-DMA instructions per wave per stage (halo rounds + dy (+ dsc))
-  static_assert(ST == 1 || (ST == 2 && PF == 0), "stride 2: compiler-scheduled fragment reads");
   static_assert(!SC || ST == 2, "shortcut fusion: stride 2");
-  static_assert(!GEN || PF == 0, "general geometry: compiler-scheduled reads");
   __shared__ __attribute__((aligned(1024))) char smem[NS * SG::BYTES];
   stamp_start(p.ts);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (p.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second half (no flips)
   const int ktiles = p.K >> 6;
   int tile, split;
   unsigned z;
@@ -174,7 +137,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       // stride 1: (rs + 2) x (seg + 2) box, row pitch seg + 2. Stride 2: (2 rs + 1) input rows x (2 seg + 1)
       // columns stored column-split (box column 2j at halo column j, 2j + 1 at hwh + j; pitch p.pitch)
       const int hr = (int)fdiv((uint32_t)hrow, p.fd_seg2), hc = hrow - hr * (int)p.fd_seg2.d;
-      const int src_chunk = (lane & 7) ^ (ST == 1 ? wg_swz(hrow, p.hsb) : trswz(hrow));
+      const int src_chunk = (lane & 7) ^ trswz(hrow);
       const int lc = ST == 1 ? hc : (hc < p.hwh ? 2 * hc : (hc < 2 * p.hwh - 1 ? 2 * (hc - p.hwh) + 1 : -1000000));
       hcol[j] = hrow < p.nh && lc >= 0;
       hrow_in[j] = hr - 1;
@@ -185,7 +148,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     hcc[j] = 0;
     const int ii = hrow / p.hb, rem = hrow - ii * p.hb;
     const int hr = rem / W2, wc = rem - hr * W2;
-    const int src_chunk = (lane & 7) ^ (ST == 1 ? wg_swz(hrow, p.hsb) : trswz(hrow));
+    const int src_chunk = (lane & 7) ^ trswz(hrow);
     // input column of this halo column (stride 2: column-split layout), -1 = padding / out of range
     const int col = ST == 1 ? wc - 1 : (wc < p.hwh ? 2 * wc - 1 : (wc < 2 * p.hwh ? 2 * (wc - p.hwh) : -1));
     hcol[j] = hrow < p.nh && col >= 0 && col < p.W;
@@ -194,7 +157,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   }
   // ---- dy DMA: row t = wave*8 + lane/8 of the 64-pixel step
   const int trow = wave * 8 + (lane >> 3);
-  const int dcol = k0 + (((lane & 7) ^ (ST == 1 ? wg_swz(trow, p.dsb) : trswz(trow))) * 8);
+  const int dcol = k0 + (((lane & 7) ^ trswz(trow)) * 8);
   // GEN: this lane's dy row of the step (pixel trow = (row, column) of the rs x seg segment; padded -> zero)
   uint32_t drel = 0x80000000u;
   if constexpr (GEN) {  // (output grid: wo columns; stride 1 wo = W)
@@ -226,28 +189,22 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     const int n0 = (int)fdiv((uint32_t)m0, p.fd_hw);
     const int p0 = (int)fdiv((uint32_t)(m0 - n0 * (int)p.fd_hw.d), p.fd_w) * ST;  // first INPUT row
     const int base = ((n0 * p.H + p0) * p.W) * p.C * 2;
-    const bool first = step == st_begin;
-    if (p.diag != 2 || first) {
 #pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        const bool ok = hcol[j] && (unsigned)(p0 + hrow_in[j]) < (unsigned)p.H;
-        buf_lds16(px, p.x_bytes, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)(base + hrel[j]) : 0x80000000u);
-      }
+    for (int j = 0; j < NR; ++j) {
+      const bool ok = hcol[j] && (unsigned)(p0 + hrow_in[j]) < (unsigned)p.H;
+      buf_lds16(px, p.x_bytes, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)(base + hrel[j]) : 0x80000000u);
     }
-    if (p.diag != 3 || first) glds16(pdy + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + wave * 1024);
+    glds16(pdy + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + wave * 1024);
     if constexpr (SC) glds16(p.dsc + (size_t)(m0 + trow) * p.K + dcol, sb + SG::HALO_BYTES + 8192 + wave * 1024);
   };
 
-  // ---- per-lane halo rows of the pixels this lane reads (wg_pixel; pmap 0: t = ks*32 + 8*(lane>>4) +
-  // (lane&15)/4 (+4))
-  const int pmap = ST == 1 ? p.pmap : 0;
-  const int hsb = ST == 1 ? p.hsb : 3, dsb = ST == 1 ? p.dsb : 3;
+  // ---- per-lane halo rows of the pixels this lane reads (wg_pixel: t = ks*32 + 8*(lane>>4) + (lane&15)/4 (+4))
   int hm[2][2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int t = wg_pixel(pmap, ks, lane >> 4, h, (lane & 15) >> 2);
+      const int t = wg_pixel(ks, lane >> 4, h, (lane & 15) >> 2);
       if constexpr (GEN) {  // padded slots (t >= rs * seg, zero dy) read any in-range halo row: row 0
         const int pr = t / p.seg, q = t - pr * p.seg;
         hm[ks][h] = t < p.rs * p.seg ? pr * (ST * W2) + q : 0;
@@ -286,7 +243,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int ra = hm[ks][h] + toff;
-        const int f = wg_uswz(ra, hsb);
+        const int f = wg_uswz(ra);
         aoff[ks][i][h] = (uint32_t)(ra * 128 + ((unit ^ f) << 3));
       }
     }
@@ -297,8 +254,8 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       const int unit = (cin >> 2) + pp;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int kr = wg_pixel(pmap, ks, g, h, q);
-        const int f = wg_uswz(kr, dsb);
+        const int kr = wg_pixel(ks, g, h, q);
+        const int f = wg_uswz(kr);
         boff[ks][j][h] = (uint32_t)(SG::HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
       }
     }
@@ -322,51 +279,23 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
   };
   auto compute = [&](const char* sb) {
-    if constexpr (PF == 0) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 bfr[2];
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 bfr[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bfr[j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
+      for (int j = 0; j < 2; ++j) bfr[j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
 #pragma unroll
-        for (int i = 0; i < 9; ++i) {
-          const bf16x8 af = tr8(sb, aoff[ks][i][0], aoff[ks][i][1]);
+      for (int i = 0; i < 9; ++i) {
+        const bf16x8 af = tr8(sb, aoff[ks][i][0], aoff[ks][i][1]);
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
-        }
-        if constexpr (SC) {  // the shortcut: centre-tap A fragment x the dsc tile's B fragments
-          const bf16x8 af = tr8(sb, aoff_sc[ks][0], aoff_sc[ks][1]);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const bf16x8 bs = tr8(sb, boff[ks][j][0] + 8192, boff[ks][j][1] + 8192);
-            acc_sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bs, acc_sc[j], 0, 0, 0);
-          }
-        }
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
       }
-    } else {
-      constexpr int NF = 22;  // fragment q: k-step q / 11; slot q % 11: 0, 1 = dy (B), 2..10 = halo (A)
-      bf16x8 f[NF];
-      auto ld = [&](int q) {
-        const int ks = q / 11, r = q % 11;
-        f[q] = r < 2 ? tr8(sb, boff[ks][r][0], boff[ks][r][1]) : tr8(sb, aoff[ks][r - 2][0], aoff[ks][r - 2][1]);
-      };
+      if constexpr (SC) {  // the shortcut: centre-tap A fragment x the dsc tile's B fragments
+        const bf16x8 af = tr8(sb, aoff_sc[ks][0], aoff_sc[ks][1]);
 #pragma unroll
-      for (int q = 0; q < PF; ++q) ld(q);
-      int next = PF;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-          const int q = ks * 11 + 2 + i;
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[q], f[ks * 11 + j], acc[i][j], 0, 0, 0);
-          if (next < NF) {
-            ld(next);
-            ++next;
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // the two MFMAs,
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // then this slot's two LDS reads
+        for (int j = 0; j < 2; ++j) {
+          const bf16x8 bs = tr8(sb, boff[ks][j][0] + 8192, boff[ks][j][1] + 8192);
+          acc_sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bs, acc_sc[j], 0, 0, 0);
         }
       }
     }
@@ -398,10 +327,6 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   }
 
   // ---- epilogue: slab[split][k][tap*C + c0 + c] (4 consecutive c per lane: one 16-B store)
-  if (p.nostore) {
-    stamp_end(p.ts);
-    return;
-  }
   const int RSC = 9 * p.C;
   // one split: the final weight gradient itself (scale * sum, exactly what wgrad_reduce would write)
   float* const slab = p.direct ? uniform_ptr(z == 0 ? p.dws[0] : z == 1 ? p.dws[1] : z == 2 ? p.dws[2] : p.dws[3])
@@ -424,198 +349,6 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     for (int j = 0; j < 2; ++j) {
       const int kout = k0 + wn * 32 + j * 16 + (lane & 15);
       *(f32x4*)(ss + (size_t)kout * p.C + c) = acc_sc[j] * osc;
-    }
-  }
-  stamp_end(p.ts);
-}
-
-// ---------------------------------------------------------------- one wave per SIMD
-// The same GEMM with 4 waves, each owning 144 GEMM rows (9 A fragments) x ALL 64 output channels
-// (4 B fragments): 13 fragment reads per 36 MFMAs per k-step (0.36 per MFMA, vs 0.61 with 8 waves
-// of 144 x 32), so LDS reads (and their latency) per MFMA drop by 40%; the accumulators (144
-// registers) live in AGPRs. With one wave per SIMD nothing else hides an LDS read's latency, so the
-// step's 26 fragments (k-step 0: B0..B3, A0..A8; k-step 1 likewise) are read D fragments ahead of
-// the MFMA group that consumes them, in one unrolled stream: at most ~2D tr reads in flight (the
-// lgkmcnt field counts 15), each read's latency behind the MFMAs of the fragments before it.
-// NS-stage LDS ring as wgrad_halo_kernel; each wave issues 2*NR halo + 2 dy DMA instructions per
-// stage (two 32-row halves of every 64-row round).
-template <int NS, int NR, int D>
-__global__ void __launch_bounds__(256, 1) wgrad_halo4_kernel(const HaloParams p) {
-  typedef WgStage<NR> SG;
-  constexpr int HI = 2 * NR;  // halo DMA instructions per wave per stage
-  constexpr int PER = HI + 2;  // + dy
-  static_assert((NS - 2) * PER < 64, "vmcnt range");
-  __shared__ __attribute__((aligned(1024))) char smem[NS * SG::BYTES];
-  stamp_start(p.ts);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ktiles = p.K >> 6;
-  int tile, split;
-  unsigned z;
-  wg_coords(p, tile, split, z);
-  const int c0 = (tile / ktiles) * 64, k0 = (tile % ktiles) * 64;
-  const u16* const px = uniform_ptr(z == 0 ? p.xs[0] : z == 1 ? p.xs[1] : z == 2 ? p.xs[2] : p.xs[3]);
-  const u16* const pdy = uniform_ptr(z == 0 ? p.dys[0] : z == 1 ? p.dys[1] : z == 2 ? p.dys[2] : p.dys[3]);
-  const int st_begin = split * p.steps_per_split;
-  const int st_end = min(p.nsteps, st_begin + p.steps_per_split);
-  const int W2 = p.W + 2;
-
-  // ---- halo DMA: instruction u covers LDS rows (u/2)*64 + ((u%2)*4 + wave)*8 + lane/8, chunk lane%8
-  int hrel[HI], hrow_in[HI];
-  bool hcol[HI];
-#pragma unroll
-  for (int u = 0; u < HI; ++u) {
-    const int hrow = (u >> 1) * 64 + ((u & 1) * 4 + wave) * 8 + (lane >> 3);
-    const int ii = hrow / p.hb, rem = hrow - ii * p.hb;
-    const int hr = rem / W2, wc = rem - hr * W2;
-    const int src_chunk = (lane & 7) ^ trswz(hrow);
-    hcol[u] = hrow < p.nh && wc >= 1 && wc <= p.W;
-    hrow_in[u] = hr - 1;
-    hrel[u] = (((ii * p.H + hr - 1) * p.W + wc - 1) * p.C + c0 + src_chunk * 8) * 2;
-  }
-  // ---- dy DMA: instruction v covers rows (v*4 + wave)*8 + lane/8 of the 64-pixel step
-  int trow[2], dcol[2];
-#pragma unroll
-  for (int v = 0; v < 2; ++v) {
-    trow[v] = (v * 4 + wave) * 8 + (lane >> 3);
-    dcol[v] = k0 + (((lane & 7) ^ trswz(trow[v])) * 8);
-  }
-  auto stage = [&](char* sb, int step) {
-    const int m0 = step * 64;
-    const int n0 = (int)fdiv((uint32_t)m0, p.fd_hw);
-    const int p0 = (int)fdiv((uint32_t)(m0 - n0 * (int)p.fd_hw.d), p.fd_w);
-    const int base = ((n0 * p.H + p0) * p.W) * p.C * 2;
-#pragma unroll
-    for (int u = 0; u < HI; ++u) {
-      const bool ok = hcol[u] && (unsigned)(p0 + hrow_in[u]) < (unsigned)p.H;
-      buf_lds16(px, p.x_bytes, sb + ((u >> 1) * 64 + ((u & 1) * 4 + wave) * 8) * 128,
-                ok ? (uint32_t)(base + hrel[u]) : 0x80000000u);
-    }
-#pragma unroll
-    for (int v = 0; v < 2; ++v)
-      glds16(pdy + (size_t)(m0 + trow[v]) * p.K + dcol[v], sb + SG::HALO_BYTES + (v * 4 + wave) * 1024);
-  };
-
-  // ---- per-lane LDS byte offsets of every fragment half (as wgrad_halo_kernel, wm = wave, wn = 0)
-  int hm[2][2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int t = ks * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2) + 4 * h;
-      const int ii = t / p.spi, rem = t - ii * p.spi;
-      const int pr = rem / p.W, q = rem - pr * p.W;
-      hm[ks][h] = ii * p.hb + pr * W2 + q;
-    }
-  uint32_t aoff[2][9][2], boff[2][4][2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int row = wave * 144 + i * 16;
-      const int tap = row >> 6, cin = row & 63;
-      const int toff = (tap / 3) * W2 + (tap % 3);
-      const int unit = (cin >> 2) + (lane & 3);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int ra = hm[ks][h] + toff;
-        const int f = (((ra >> 1) & 1) << 2) | (((ra >> 3) & 1) << 3);
-        aoff[ks][i][h] = (uint32_t)(ra * 128 + ((unit ^ f) << 3));
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int li = lane & 15, q = li >> 2, pp = li & 3, g = lane >> 4;
-      const int unit = ((j * 16) >> 2) + pp;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int kr = ks * 32 + g * 8 + q + 4 * h;
-        const int f = (((kr >> 1) & 1) << 2) | (((kr >> 3) & 1) << 3);
-        boff[ks][j][h] = (uint32_t)(SG::HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
-      }
-    }
-  }
-  typedef __attribute__((address_space(3))) bf16x4_t lds_v4;
-  auto tr8 = [&](const char* sb, uint32_t o0, uint32_t o1) {
-    const bf16x4_t t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(sb + o0));
-    const bf16x4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(sb + o1));
-    return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
-
-  f32x4 acc[9][4];
-#pragma unroll
-  for (int i = 0; i < 9; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // fragment q of a step: k-step q / 13; r = q % 13: 0..3 = B (dy) fragment r, 4..12 = A (halo) r - 4
-  auto compute = [&](const char* sb, bf16x8 fz) {
-    constexpr int NF = 26;
-    bf16x8 f[NF];
-    auto ld = [&](int q) {
-      const int ks = q / 13, r = q % 13;
-      if (p.diag == 4) {  // diagnostics: no LDS reads in the loop (fragments read once per step)
-        f[q] = fz;
-        return;
-      }
-      f[q] = r < 4 ? tr8(sb, boff[ks][r][0], boff[ks][r][1]) : tr8(sb, aoff[ks][r - 4][0], aoff[ks][r - 4][1]);
-    };
-    int cur = 0;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        const int q = ks * 13 + 4 + i;  // the A fragment this group consumes
-        const int target = q + 1 + D < NF ? q + 1 + D : NF;
-#pragma unroll
-        for (; cur < target; ++cur) ld(cur);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[q], f[ks * 13 + j], acc[i][j], 0, 0, 0);
-        // pin the order: the scheduler would otherwise sink each read next to its first use
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-
-  if (st_begin < st_end) {
-    const int nk = st_end - st_begin;
-#pragma unroll
-    for (int i = 0; i < NS - 1; ++i)
-      if (i < nk) stage(smem + i * SG::BYTES, st_begin + i);
-    for (int it = 0; it < nk; it += NS) {
-#pragma unroll
-      for (int u = 0; u < NS; ++u) {
-        const int k = it + u;
-        if (k >= nk) break;
-        if (k + NS - 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PER) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        // diagnostics (option wgrad_diag, WRONG results): 5 = no DMA after the prologue
-        if (k + NS - 1 < nk && p.diag != 5) stage(smem + ((u + NS - 1) % NS) * SG::BYTES, st_begin + k + NS - 1);
-        const bf16x8 fz = p.diag == 4 ? tr8(smem + u * SG::BYTES, aoff[0][0][0], aoff[0][0][1]) : bf16x8{};
-        compute(smem + u * SG::BYTES, fz);
-      }
-    }
-  }
-
-  if (p.nostore) {
-    stamp_end(p.ts);
-    return;
-  }
-  const int RSC = 9 * p.C;
-  // one split: the final weight gradient itself (scale * sum, exactly what wgrad_reduce would write)
-  float* const slab = p.direct ? uniform_ptr(z == 0 ? p.dws[0] : z == 1 ? p.dws[1] : z == 2 ? p.dws[2] : p.dws[3])
-                               : p.slab + z * p.slab_stride + (size_t)split * p.K * RSC;
-  const float osc = p.direct ? p.scale : 1.f;
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int row = wave * 144 + i * 16 + 4 * (lane >> 4);
-    const int rsc = (row >> 6) * p.C + c0 + (row & 63);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kout = k0 + j * 16 + (lane & 15);
-      *(f32x4*)(slab + (size_t)kout * RSC + rsc) = acc[i][j] * osc;
     }
   }
   stamp_end(p.ts);
@@ -714,15 +447,7 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   }
   (void)imgs;
   p.ts = ts;
-  p.nostore = option_get(OPT_WGRAD_DIAG) == 1;
-  p.diag = option_get(OPT_WGRAD_DIAG);
   p.xcd = option_get(OPT_WGRAD_XCD);
-  p.prio = option_get(OPT_WGRAD_PRIO);
-  p.pmap = 0; p.hsb = 3; p.dsb = 3;
-  if (option_get(OPT_WGRAD_PMAP) != 0 && !g.gen) {
-    if (s.W >= 8) { p.pmap = 1; p.hsb = 2; p.dsb = 2; }
-    else if (s.W == 4 && s.H == 4) { p.pmap = 2; p.hsb = 2; p.dsb = 3; }
-  }
   const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
   p.slab_stride = (size_t)used * s.K * 9 * s.C;
   p.direct = used == 1 && dw != nullptr && option_get(OPT_WGRAD_DIRECT) != 0;
@@ -731,36 +456,14 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   p.scale = scale;
   dim3 grid((s.C / 64) * (s.K / 64), used, nprob);
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
-  const bool deep = option_get(OPT_WGRAD_STAGES) >= 4;
-  const bool deeper = option_get(OPT_WGRAD_STAGES) >= 5;  // 5 stages: 160 KB at NR = 3 (the whole LDS)
-  const int pf = option_get(OPT_WGRAD_PF);
-  if (g.gen) {  // general geometry: 4-stage ring, compiler-scheduled fragment reads
-    if (nr <= 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, 2, 0, 1, false, true>), grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((wgrad_halo_kernel<4, 3, 0, 1, false, true>), grid, dim3(512), 0, st, p);
-    DTC_LAUNCH_CHECK();
-    *used_splits = p.direct ? 0 : used;
-    return 0;
-  }
-  if (option_get(OPT_WGRAD_KERNEL) != 0) {  // one wave per SIMD (wgrad_halo4_kernel), 4-stage ring
-#define DTC_WH4(NR_, D_) hipLaunchKernelGGL((wgrad_halo4_kernel<4, NR_, D_>), grid, dim3(256), 0, st, p)
-    if (nr <= 2) { if (pf >= 6) DTC_WH4(2, 6); else DTC_WH4(2, 4); }
-    else { if (pf >= 6) DTC_WH4(3, 6); else DTC_WH4(3, 4); }
-#undef DTC_WH4
-    DTC_LAUNCH_CHECK();
-    *used_splits = p.direct ? 0 : used;
-    return 0;
-  }
-#define DTC_WH(NS_, NR_, PF_) hipLaunchKernelGGL((wgrad_halo_kernel<NS_, NR_, PF_>), grid, dim3(512), 0, st, p)
-  if (nr <= 2) {
-    if (pf >= 8) { if (deep) DTC_WH(4, 2, 8); else DTC_WH(2, 2, 8); }
-    else if (pf > 0) { if (deep) DTC_WH(4, 2, 5); else DTC_WH(2, 2, 5); }
-    else { if (deeper) DTC_WH(5, 2, 0); else if (deep) DTC_WH(4, 2, 0); else DTC_WH(2, 2, 0); }
+  // 4-stage LDS ring (three steps of DMA in flight), compiler-scheduled fragment reads
+  if (g.gen) {  // general geometry
+    if (nr <= 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, 2, 1, false, true>), grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_halo_kernel<4, 3, 1, false, true>), grid, dim3(512), 0, st, p);
   } else {
-    if (pf >= 8) { if (deep) DTC_WH(4, 3, 8); else DTC_WH(2, 3, 8); }
-    else if (pf > 0) { if (deep) DTC_WH(4, 3, 5); else DTC_WH(2, 3, 5); }
-    else { if (deeper) DTC_WH(5, 3, 0); else if (deep) DTC_WH(4, 3, 0); else DTC_WH(2, 3, 0); }
+    if (nr <= 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, 2>), grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_halo_kernel<4, 3>), grid, dim3(512), 0, st, p);
   }
-#undef DTC_WH
   DTC_LAUNCH_CHECK();
   *used_splits = p.direct ? 0 : used;
   return 0;
@@ -906,7 +609,7 @@ int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* ds
   p.scale = scale;
   const dim3 grid((s.C / 64) * (s.K / 64), used, 1);
   const int nr = (nh + 63) / 64;
-#define DTC_WS2(NR_, SC_, G_) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 0, 2, SC_, G_>), grid, dim3(512), 0, st, p)
+#define DTC_WS2(NR_, SC_, G_) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 2, SC_, G_>), grid, dim3(512), 0, st, p)
   if (gen) {
     if (nr <= 5) { if (dsc) DTC_WS2(5, true, true); else DTC_WS2(5, false, true); }
     else { if (dsc) DTC_WS2(6, true, true); else DTC_WS2(6, false, true); }

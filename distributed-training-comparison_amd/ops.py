@@ -228,31 +228,6 @@ def bn_mask_bits(y):
     return (b * w).sum(-1).to(torch.uint8).contiguous()
 
 
-def bn_bwd_onepass(dy, mbits, x1, mean1, invstd1, gamma1, x2=None, mean2=None, invstd2=None, gamma2=None,
-                   gscale=1.0, dz_out=False):
-    """One-pass mask-bit BN backward (dtc_bn_bwd_onepass): returns dx1, dx2, dgamma1, dbeta1,
-    dgamma2, dbeta2, dz (None where absent)."""
-    c = x1.shape[-1]
-    m = x1.numel() // c
-    dev = x1.device
-    f = lambda: torch.empty(c, dtype=torch.float32, device=dev)  # noqa: E731
-    acc1 = new_stats(c, dev)
-    acc2 = new_stats(c, dev) if x2 is not None else None
-    dg1, db1 = f(), f()
-    dg2, db2 = (f(), f()) if x2 is not None else (None, None)
-    dx1 = torch.empty_like(x1)
-    dx2 = torch.empty_like(x2) if x2 is not None else None
-    dz = torch.empty_like(dy) if dz_out else None
-    ctr = torch.zeros(128, dtype=torch.int32, device=dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
-    call("dtc_bn_bwd_onepass", ptr(dy), ptr(mbits), ptr(dz), ptr(x1), ptr(mean1), ptr(invstd1), ptr(gamma1), ptr(acc1),
-         ptr(dg1), ptr(db1), ptr(dx1), ptr(x2), ptr(mean2), ptr(invstd2), ptr(gamma2), ptr(acc2), ptr(dg2), ptr(db2),
-         ptr(dx2), m, float(gscale), m, c, ptr(ctr), ptr(err), stream_ptr())
-    if int(err.item()):
-        raise NativeError("bn_bwd_onepass: grid barrier timed out")
-    return dx1, dx2, dg1, db1, dg2, db2, dz
-
-
 def stem_im2col(x):
     n, _, h, w = x.shape
     cols = torch.empty(n, h, w, 64, dtype=torch.bfloat16, device=x.device)

@@ -268,18 +268,22 @@ class DistributedDataParallel(nn.Module):
         per-rank counts as torch's all_gather does), so every rank's batch must be the same size.
         Every training forward of every rank issues the same check (one 2-double SUM all-reduce of
         (n, n^2) on the SyncBN communicator: sizes are equal iff W * sum(n^2) == sum(n)^2), so the
-        ranks' collectives always match (no per-rank cache deciding who enters). The host
-        waits for the result when this rank's batch size changed (first step included); otherwise the
-        previous step's result is checked here, long since complete."""
+        ranks' collectives always match (no per-rank cache deciding who enters). Whether the
+        host waits is decided the same way on every rank: the FIRST check is waited for
+        (every rank is on its first training forward), every later one is read at the next training
+        forward, long since complete. A batch size that changes on one rank after the first step is
+        therefore refused one step late, but on every rank at the same step: no rank ever waits for a
+        result while another has gone on into the forward's SyncBN all-reduces."""
         n = int(x.shape[0])
         dev = self.module.flat.device
         if self._cnt is None:
             self._cnt = {"dev": torch.zeros(2, dtype=torch.float64, device=dev),
                          "host": torch.zeros(2, dtype=torch.float64, pin_memory=True),
-                         "ev": None, "n": None}
+                         "ev": None, "first": True}
         st = self._cnt
         if st["ev"] is not None:  # the previous step's check
             st["ev"].synchronize()
+            st["ev"] = None
             self._assert_equal_batches(st["host"])
         st["dev"].copy_(torch.tensor([float(n), float(n) * n], dtype=torch.float64), non_blocking=False)
         self.sync_comm.allreduce_sum_(st["dev"])
@@ -287,11 +291,11 @@ class DistributedDataParallel(nn.Module):
         ev = torch.cuda.Event()
         ev.record()
         st["ev"] = ev
-        if st["n"] != n:
+        if st["first"]:
+            st["first"] = False
             ev.synchronize()
-            self._assert_equal_batches(st["host"])
             st["ev"] = None
-            st["n"] = n
+            self._assert_equal_batches(st["host"])
 
     def _assert_equal_batches(self, h) -> None:
         s1, s2 = float(h[0]), float(h[1])

@@ -130,18 +130,6 @@ int dtc_bn_bwd_finalize(double* acc, int c, int64_t count, const float* gamma, c
                         const float* invstd, float gscale, float* dgamma, float* dbeta, float* coef, void* stream);
 int dtc_bn_bwd_apply(const uint16_t* dz, const uint16_t* x1, const float* coef1, uint16_t* dx1, const uint16_t* x2,
                      const float* coef2, uint16_t* dx2, int64_t m, int c, void* stream);
-/* One-pass mask-bit BN backward (the executor's default where it fits): dz = dy * bit (mbits: byte
- * o/8 of element offset o, bit k = channel 8*(o%c/8)+k; the forward BN apply's ReLU mask), the sums,
- * a grid barrier, dgamma/dbeta (x gscale) and dx1 = BN1-backward(dz, x1) [, dx2 = BN2-backward(dz, x2)]
- * [, dzo = dz] in one launch -- dtc_bn_bwd_reduce + _finalize + _apply of both BNs. acc1/acc2: zeroed
- * [32][2][c] fp64 slots; counter: 128 zeroed bytes; *err set to 1 if the grid barrier timed out.
- * Returns DTC_EINVAL when (m, c) has no one-pass plan (dtc_bn_bwd_onepass_ok == 0). */
-int dtc_bn_bwd_onepass_ok(int64_t m, int c, int dual);
-int dtc_bn_bwd_onepass(const uint16_t* dy, const uint8_t* mbits, uint16_t* dzo, const uint16_t* x1, const float* mean1,
-                       const float* invstd1, const float* gamma1, double* acc1, float* dgamma1, float* dbeta1,
-                       uint16_t* dx1, const uint16_t* x2, const float* mean2, const float* invstd2, const float* gamma2,
-                       double* acc2, float* dgamma2, float* dbeta2, uint16_t* dx2, int64_t count, float gscale,
-                       int64_t m, int c, int* counter, int* err, void* stream);
 
 /* ------------------------------------------------------------------ stem, head, loss
  * stem: self.conv1 = nn.Conv2d(3, 64, 3, 1, 1) (net.py:91) as im2col [n*h*w][64] + GEMM.

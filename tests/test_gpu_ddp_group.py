@@ -204,6 +204,31 @@ def test_sync_batchnorm_unequal_shards_refused(dtc, cuda):
     assert all(m is not None and "batch sizes differ" in m for m in msgs), msgs
 
 
+def test_sync_batchnorm_batch_change_on_one_rank_refused_on_every_rank(dtc, cuda):
+    """equal shards (8, 8) on the first step, then only rank 1's batch changes (8, 12). The
+    wait-or-defer decision is the same on every rank, so neither rank waits while the other enters the
+    forward's SyncBN all-reduces (which would hang over RCCL): both ranks raise, at the same forward."""
+    world = 2
+    comms = dtc.parallel.Comm.thread_group(cuda.index or 0, world)
+    syncs = dtc.parallel.Comm.thread_group(cuda.index or 0, world)
+    models = [_model(dtc, cuda, 25.0, sync_bn=True) for _ in range(world)]
+
+    def rank(r):
+        ddp = dtc.DistributedDataParallel(models[r], device_ids=[0], comm=comms[r], sync_comm=syncs[r])
+        for step, b in enumerate((8, 8 + 4 * r, 8, 8)):
+            x = torch.randn(b, 3, 32, 32, device=cuda)
+            try:
+                with dtc.autocast():
+                    ddp(x)
+            except dtc.NativeError as e:
+                return step, str(e)
+        return None
+
+    res = _run_ranks(rank, world)  # a hang would fail here ("a rank thread hung" / the 120 s group timeout)
+    assert all(x is not None and "batch sizes differ" in x[1] for x in res), res
+    assert res[0][0] == res[1][0] == 2, res  # refused one step late, on both ranks together
+
+
 def test_thread_group_barrier_and_mismatch(dtc, cuda):
     """dtc_barrier over the thread group returns on every rank only after all ranks called it and each
     rank's own queued work finished; mismatched collectives are reported to every rank, not hung."""

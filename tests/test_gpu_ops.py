@@ -297,42 +297,6 @@ def test_bn_backward(dtc, cuda, C, dual):
         assert rel_err(dx2.float().cpu().numpy(), dx2_ref) < 1e-2
 
 
-@pytest.mark.parametrize("M,C,dual", [(256, 64, False), (4096, 128, True), (65536, 128, False), (16384, 256, True),
-                                       (4096, 512, True), (4096, 512, False), (8192, 64, False)])
-def test_bn_backward_onepass(dtc, cuda, M, C, dual):
-    """One-pass BN backward (reduce + grid barrier + apply, one launch, mask bits) against the oracle
-    on the same bf16 operands: dgamma / dbeta / dx of both BNs and dz; the B=256 layer2-4 shapes
-    (grids of up to one workgroup per CU) and small ones."""
-    if not dtc._native.lib.dtc_bn_bwd_onepass_ok(M, C, int(dual)):
-        pytest.skip("no one-pass plan")
-    g = np.random.default_rng(16)
-    x = O.bf16(_rand_bf16((M, C), g, 1.5) + 0.2)
-    x2 = O.bf16(_rand_bf16((M, C), g, 0.7) - 0.1)
-    y = O.relu(_rand_bf16((M, C), g))  # post-ReLU output: its mask drives dz
-    dy = _rand_bf16((M, C), g)
-    gamma = g.uniform(0.5, 1.5, C).astype(np.float32)
-    gamma2 = g.uniform(0.5, 1.5, C).astype(np.float32)
-    _, mean, invstd, _, _ = O.bn_train_fwd(x, gamma, np.zeros(C))
-    _, mean2, invstd2, _, _ = O.bn_train_fwd(x2, gamma2, np.zeros(C))
-    t = lambda a: torch.from_numpy(np.asarray(a, np.float32)).to(cuda)  # noqa: E731
-    b = lambda a: _to_dev_bf16(a, cuda)  # noqa: E731
-    bits = dtc.ops.bn_mask_bits(b(y))
-    dx1, dx2, dg1, db1, dg2, db2, dz = dtc.ops.bn_bwd_onepass(
-        b(dy), bits, b(x), t(mean), t(invstd), t(gamma), b(x2) if dual else None, t(mean2) if dual else None,
-        t(invstd2) if dual else None, t(gamma2) if dual else None, gscale=0.5, dz_out=True)
-    dz_ref = np.where(y > 0, dy, 0)
-    np.testing.assert_array_equal(dz.float().cpu().numpy(), dz_ref)
-    dx_ref, dg_ref, db_ref = O.bn_train_bwd(dz_ref, x, gamma, mean, invstd)
-    np.testing.assert_allclose(dg1.cpu().numpy(), 0.5 * dg_ref, rtol=1e-4, atol=1e-3)
-    np.testing.assert_allclose(db1.cpu().numpy(), 0.5 * db_ref, rtol=1e-4, atol=1e-3)
-    assert rel_err(dx1.float().cpu().numpy(), dx_ref) < 1e-2
-    if dual:
-        dx2_ref, dg2_ref, db2_ref = O.bn_train_bwd(dz_ref, x2, gamma2, mean2, invstd2)
-        np.testing.assert_allclose(dg2.cpu().numpy(), 0.5 * dg2_ref, rtol=1e-4, atol=1e-3)
-        np.testing.assert_allclose(db2.cpu().numpy(), 0.5 * db2_ref, rtol=1e-4, atol=1e-3)
-        assert rel_err(dx2.float().cpu().numpy(), dx2_ref) < 1e-2
-
-
 @pytest.mark.parametrize("head_fused", [1, 0])
 def test_head_and_loss(dtc, cuda, head_fused):
     dtc._native.lib.dtc_set_option(b"head_fused", head_fused)

@@ -430,7 +430,6 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
     fold it into conv1's class-(0, 0) dgrad as one fp32 sum (one bf16 rounding of dx instead of two), a
     legitimate 1-ulp difference that 3 steps at lr 0.1 on 8 images amplify past rtol 1e-4."""
     lib = dtc._native.lib
-    lib.dtc_set_option(b"bn_onepass", 0)  # the fused finalize of the two-pass kernels vs the separate one
     lib.dtc_set_option(b"dgrad_scf", 0)
     try:
         la, ga, pa, ba = _train_steps(dtc, cuda, 3, graphs=graphs)
@@ -440,7 +439,6 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
         finally:
             lib.dtc_set_option(b"bn_fused_fin", 1)
     finally:
-        lib.dtc_set_option(b"bn_onepass", 0)
         lib.dtc_set_option(b"dgrad_scf", 1)
     np.testing.assert_allclose(la, lb, rtol=1e-4)
     assert rel_err(ga, gb) < 1e-3
@@ -451,8 +449,6 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
 
 DEFAULT_STEM_BN_FUSE = 1
 DEFAULT_SC_FUSE = 1
-DEFAULT_HEAD_DIRECT = 1
-DEFAULT_STEM_RECOMPUTE = 0
 DEFAULT_STEM_WLDS = 1
 
 
@@ -471,25 +467,6 @@ def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5, hw=32):
         return out
     finally:
         dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
-
-
-@pytest.mark.parametrize("batch,hw", [(8, 32), (64, 32), (16, 8)])
-def test_wgrad_conflict_free_pixel_map_matches(dtc, cuda, batch, hw):
-    """Option wgrad_pmap=1: the weight-gradient halo kernel's tr reads with the bank-conflict-free pixel map and
-    swizzle (HaloParams::pmap, tools/tr_banks.py) vs the original map: the MFMA reduction order within a
-    k-step changes, nothing else -- every gradient within fp32 rounding (W = 32 / 16 / 8 / 4 all covered:
-    hw 32 has layers of width 32..4, hw 8 has 8..1)."""
-    lib = dtc._native.lib
-    try:
-        lib.dtc_set_option(b"wgrad_pmap", 0)
-        ga = _grads_repeated(dtc, cuda, 1, batch=batch, hw=hw)
-        lib.dtc_set_option(b"wgrad_pmap", 1)
-        gb = _grads_repeated(dtc, cuda, 1, batch=batch, hw=hw)
-    finally:
-        lib.dtc_set_option(b"wgrad_pmap", 0)
-    for rep in range(2):
-        assert np.isfinite(gb[rep]).all()
-        assert rel_err(gb[rep], ga[rep]) < 1e-5, (rep, rel_err(gb[rep], ga[rep]))
 
 
 @pytest.mark.parametrize("batch,hw", [(8, 32), (3, 32), (5, 8)])
@@ -568,7 +545,6 @@ def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
     shortcut's dgrad stays a separate launch in both arms (dgrad_scf=0: the bn_mask=0 executor has no
     fused form; see test_fused_bn_finalize_matches_separate)."""
     lib = dtc._native.lib
-    lib.dtc_set_option(b"bn_onepass", 0)  # the two-pass kernels: the same summation order as bn_mask=0
     lib.dtc_set_option(b"dgrad_scf", 0)
     try:
         ga = _grads_repeated(dtc, cuda, graphs)
@@ -580,7 +556,6 @@ def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
         finally:
             lib.dtc_set_option(b"bn_mask", 1)
     finally:
-        lib.dtc_set_option(b"bn_onepass", 0)
         lib.dtc_set_option(b"dgrad_scf", 1)
     for rep in range(2):
         assert rel_err(ga[rep], gb[rep]) < 1e-6, rep
@@ -588,32 +563,6 @@ def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
     assert rel_err(pa, pb) < 1e-5
     for k in ba:
         assert rel_err(ba[k], bb[k]) < 1e-4, k
-
-
-@pytest.mark.parametrize("graphs", [False, True])
-def test_bn_onepass_matches_two_pass(dtc, cuda, graphs):
-    """One-pass BN backward (option bn_onepass=1, off by default: reduce + grid barrier + apply in one launch,
-    the slice held in registers; used where the slice fits, layers 2-4 at B=256, every BN at small
-    batch) vs the two-pass kernels. The per-thread fp32 partial sums are grouped differently, so the
-    BN coefficients differ in their last fp32 bits and some bf16 outputs round the other way; through
-    20 BN layers that gives ~0.5% on the concatenated gradient of one step (two correct bf16
-    implementations differ by far more) -- exactness is the op test's job
-    (tests/test_gpu_ops.py::test_bn_backward_onepass). One step is compared; longer runs of this
-    8-image memorisation diverge chaotically."""
-    lib = dtc._native.lib
-    lib.dtc_set_option(b"bn_onepass", 1)
-    try:
-        ga = _grads_repeated(dtc, cuda, graphs)
-        la, _, _, ba = _train_steps(dtc, cuda, 1, graphs=graphs)
-    finally:
-        lib.dtc_set_option(b"bn_onepass", 0)
-    gb = _grads_repeated(dtc, cuda, graphs)
-    lb, _, _, bb = _train_steps(dtc, cuda, 1, graphs=graphs)
-    for rep in range(2):
-        assert rel_err(ga[rep], gb[rep]) < 2e-2, rep
-    np.testing.assert_allclose(la, lb, rtol=1e-6)  # the first step's loss is the forward's
-    for k in ba:  # running statistics after one step: forward only
-        assert rel_err(ba[k], bb[k]) < 1e-6, k
 
 
 @pytest.mark.parametrize("batch", [8, 64])
@@ -757,24 +706,6 @@ def test_fused_shortcut_dgrad_and_wgrad_match_separate(dtc, cuda, batch):
 
 
 @pytest.mark.parametrize("batch,hw", [(8, 32), (256, 32), (8, 8)])
-def test_stem_recompute_matches_single_pass(dtc, cuda, batch, hw):
-    """Option stem_recompute: a statistics-only stem pass + a recompute pass that stores the conv output
-    and applies the BN + ReLU (+ mask bits) in its epilogue, vs the stem conv + bn_fin_apply. Same conv,
-    same fp64 statistics, same apply arithmetic: identical gradients over two training steps."""
-    lib = dtc._native.lib
-    for graphs in (1, 0):
-        try:
-            lib.dtc_set_option(b"stem_recompute", 0)
-            ga = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
-            lib.dtc_set_option(b"stem_recompute", 1)
-            gb = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
-        finally:
-            lib.dtc_set_option(b"stem_recompute", DEFAULT_STEM_RECOMPUTE)
-        for rep in range(2):
-            np.testing.assert_array_equal(ga[rep], gb[rep])
-
-
-@pytest.mark.parametrize("batch,hw", [(8, 32), (256, 32), (8, 8)])
 def test_stem_weight_lds_matches_gather(dtc, cuda, batch, hw):
     """Option stem_wlds: the stem forward's weight fragments gathered from an LDS copy (coalesced loads)
     instead of per-lane global gathers; the input rows capped at 8 KB of LDS (wider tiles take the
@@ -791,32 +722,30 @@ def test_stem_weight_lds_matches_gather(dtc, cuda, batch, hw):
         np.testing.assert_array_equal(ga[rep], gb[rep])
 
 
-def test_head_direct_matches_copy(dtc, cuda):
-    """Option head_direct: the head kernel launched after the forward graph straight into the caller's
-    logits (1), or inside the graph with its destination read from a pointer slot the input-copy launch
-    stores (2, default), vs the graph-owned logits + copy (0): identical logits and gradients (train and
-    eval). Mode 2 also keeps every call's output where that call asked for it: logits of consecutive
-    forwards into different tensors stay distinct (the slot is per call, not baked into the graph)."""
+def test_head_after_forward_graph_matches_eager(dtc, cuda):
+    """The replayed forward's head is launched after the graph straight into each call's own logits
+    tensor (the graph cannot bake in a per-call pointer): identical logits and gradients to the eager
+    forward (train and eval), and the logits of consecutive forwards into different tensors stay distinct."""
     lib = dtc._native.lib
+    prev = lib.dtc_get_option(b"graphs")
     res = {}
     try:
-        for mode in (0, 1, 2):
-            lib.dtc_set_option(b"head_direct", mode)
-            g = _grads_repeated(dtc, cuda, 1, batch=16)
+        for graphs in (0, 2):
+            lib.dtc_set_option(b"graphs", graphs)
+            g = _grads_repeated(dtc, cuda, graphs, batch=16)
             model, _, x, _ = _setup(dtc, cuda, 16, seed=3)
             xd = torch.from_numpy(x).to(cuda)
             with torch.no_grad():
                 model.eval()
                 e1 = model(xd)
                 e2 = model(xd * 0.5)  # a second output tensor: must not overwrite e1
-                res[mode] = (g, _np(e1), _np(e2))
+                res[graphs] = (g, _np(e1), _np(e2))
     finally:
-        lib.dtc_set_option(b"head_direct", DEFAULT_HEAD_DIRECT)
-    for mode in (1, 2):
-        for rep in range(2):
-            np.testing.assert_array_equal(res[0][0][rep], res[mode][0][rep])
-        np.testing.assert_array_equal(res[0][1], res[mode][1])
-        np.testing.assert_array_equal(res[0][2], res[mode][2])
+        lib.dtc_set_option(b"graphs", prev)
+    for rep in range(2):
+        np.testing.assert_array_equal(res[0][0][rep], res[2][0][rep])
+    np.testing.assert_array_equal(res[0][1], res[2][1])
+    np.testing.assert_array_equal(res[0][2], res[2][2])
     assert not np.array_equal(res[2][1], res[2][2])
 
 

@@ -117,12 +117,17 @@ def test_workspace_and_conv_plans(dtc):
 
 # executor / kernel options added by the round-2 performance work, with their defaults (kernels.h)
 _OPTION_DEFAULTS = {
-    "stem_bn_fuse": 1, "fork_lazy": 1, "side_prio": 1, "sc_fuse": 1, "head_direct": 1, "stem_wlds": 1,
-    "stem_recompute": 0, "wgrad_tail": 0, "bn_red_elems": 16384, "bn_red_blocks": 256, "bn_fa_blocks": 1024,
+    "stem_bn_fuse": 1, "fork_lazy": 1, "side_prio": 1, "sc_fuse": 1, "stem_wlds": 1,
+    "bn_red_elems": 16384, "bn_red_blocks": 256, "bn_fa_blocks": 1024,
     "sc_compact": 1, "stem_prologue": 1, "dgrad_class_order": 1, "wgrad_direct": 1, "wgrad_xcd": 1,
     # round 3
-    "halo_s2": 1, "wgrad_s2": 2, "dgrad_scf": 1, "bnb_mask": 0, "bucket_tail": 1, "graph_ev": 1, "wgrad_pmap": 0, "halo_stage_epi": 0, "wgrad_gen": 1, "halo_gen": 1, "halo_nosplit": 0, "wgrad_prio": 0, "bn_red_unroll": 4, "c64_gen": 1, "graphs": 4,
+    "halo_s2": 1, "wgrad_s2": 2, "dgrad_scf": 1, "bnb_mask": 0, "bucket_tail": 1, "halo_stage_epi": 0, "wgrad_gen": 1,
+    "halo_gen": 1, "bn_red_unroll": 4, "c64_gen": 1, "graphs": 4, "head_fused": 0,
 }
+# measured-negative variants deleted in round 4 with their code paths (DESIGN.md keeps their numbers)
+_REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", "wgrad_pmap", "wgrad_prio",
+                    "halo_nhb2", "wgrad_kernel", "head_direct", "halo_nosplit", "graph_ev", "wgrad_tail",
+                    "wgrad_stages", "wgrad_pf", "wgrad_diag")
 
 
 def test_options_registered_with_defaults(dtc):
@@ -137,3 +142,5 @@ def test_options_registered_with_defaults(dtc):
         assert lib.dtc_set_option(key, default) == 0
         assert lib.dtc_get_option(key) == default
     assert lib.dtc_set_option(b"no_such_option", 1) != 0
+    for name in _REMOVED_OPTIONS:
+        assert lib.dtc_set_option(name.encode(), 1) != 0, name

@@ -3,7 +3,7 @@ under each variant on the same random operands; variants that only change schedu
 tile walks) must give identical outputs. Prints the max |difference| per (layer, pass) vs variant 0
 and exits non-zero if any differs.
 
-usage: python tools/option_ab.py --variants "wgrad_stages=2;wgrad_stages=4" [--batch 64]"""
+usage: python tools/option_ab.py --variants "wgrad_xcd=0;wgrad_xcd=1" [--batch 64]"""
 import argparse
 import os
 import sys

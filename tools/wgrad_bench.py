@@ -5,7 +5,7 @@ Each geometry's call is captured ITERS times into a CUDA graph (raw C-ABI calls,
 preallocated) and replayed, so the figure is device time. Option variants are interleaved in one
 process. Prints us per launch and TFLOP/s (algorithmic 2*N*H*W*K*9*C per conv) per variant.
 
-usage: python tools/wgrad_bench.py --variants "wgrad_stages=2;wgrad_stages=4" [--batch 256]"""
+usage: python tools/wgrad_bench.py --variants "wgrad_xcd=0;wgrad_xcd=1" [--batch 256]"""
 import argparse
 import ctypes as C
 import json
