@@ -48,6 +48,7 @@ namespace dtc {
   X(STEM_WLDS, stem_wlds, 1)            /* stem forward weight staged in LDS */                               \
   X(HALO_S2, halo_s2, 1)                /* stride-2 3x3 FWD on the column-split halo kernel */                \
   X(WGRAD_S2, wgrad_s2, 2)              /* stride-2 wgrad (+ shortcut) on the halo kernel: 0 off, 1 all, 2 GEN */ \
+  X(WGRAD_S2_WGS, wgrad_s2_wgs, 256)    /* stride-2 halo wgrad: target workgroups (split-K slab = wgs x tile) */ \
   X(DGRAD_SCF, dgrad_scf, 1)            /* shortcut dgrad fused into conv1's parity-class dgrad */            \
   X(BNB_MASK, bnb_mask, 0)              /* mask-bit backward: BN sums in the producing dgrad's epilogue */    \
   X(HEAD_FUSED, head_fused, 0)          /* head backward in one launch (dW/db strips + dact) */               \

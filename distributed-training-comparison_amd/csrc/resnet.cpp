@@ -885,17 +885,31 @@ struct BwdCtx {
   std::vector<Net::Seg>* segs = nullptr;
 };
 static int join_side(Net& n, hipStream_t st);
+static int next_event(Net& n, hipEvent_t* ev);
 static int maybe_bucket(Net& n, int after_block, const BwdCtx& cx, hipStream_t st) {
   if (!cx.comm) return 0;
   std::vector<int> ids;
   for (size_t i = 0; i < n.bucket_off.size(); ++i)
     if (n.bucket_after_block[i] == after_block) ids.push_back((int)i);
   if (ids.empty()) return 0;
-  DTC_TRY(join_side(n, st));  // the bucket's weight gradients come from the side stream
   if (!cx.capturing) {
-    for (int i : ids) DTC_TRY(comm_allreduce_async(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st));
+    // The bucket's producers are the compute stream (BN dgamma / dbeta, the head) and the weight-gradient
+    // side stream. The compute stream does NOT wait for the side stream here (that join would stall the
+    // dgrad / BN chain behind the queued weight gradients at every bucket point): the side stream is
+    // forked from the compute stream instead, so it holds both producers, and the collective is ordered
+    // after it. The side stream is joined into the compute stream once, at the end of the backward.
+    hipStream_t prod = st;
+    if (n.side_pending) {
+      hipEvent_t ev;
+      DTC_TRY(next_event(n, &ev));
+      DTC_HIP(hipEventRecord(ev, st));
+      DTC_HIP(hipStreamWaitEvent(n.side_st, ev, 0));
+      prod = n.side_st;
+    }
+    for (int i : ids) DTC_TRY(comm_allreduce_async(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], prod));
     return 0;
   }
+  DTC_TRY(join_side(n, st));  // a graph segment ends here: every stream forked in it joins back
   Net::Seg sg;
   sg.buckets = ids;
   DTC_TRY(end_capture(n, 0, &sg.exec));

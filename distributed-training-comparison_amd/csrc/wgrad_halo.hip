@@ -544,7 +544,7 @@ int wgrad_s2_splits(const ConvShape& s) {
   int64_t nsteps = 0;
   if (!wgrad_s2_plan(s, gen, nsteps)) return 0;
   const int tiles = (s.C / 64) * (s.K / 64);
-  int splits = std::max(1, std::max(64, option_get(OPT_WGRAD_HALO)) / tiles);
+  int splits = std::max(1, std::max(16, option_get(OPT_WGRAD_S2_WGS)) / tiles);
   return (int)std::min<int64_t>(splits, std::max<int64_t>(1, nsteps / 4));
 }
 

@@ -1,11 +1,16 @@
 """Summarise a rocprofv3 --kernel-trace --stats run of bench.py into a markdown file for profiles/.
 
-usage: python tools/prof_summary.py <rocprof output dir> <out.md> [--steps-from-bench bench.json]
+usage: python tools/prof_summary.py <rocprof output dir> <out.md> [--bench bench.json] [--gflop-per-step G]
 
-Reports: top kernels (calls, total, average), the conv family (igemm + split-K/wgrad reductions:
-the roofline kernel of bench.py) per training step, and the per-step timeline of the steady
-state (busy time vs wall time between the first and last kernel of a step, i.e. launch gaps).
-A training step is delimited by the SGD kernel (one launch per step).
+Reports: top kernels (calls, total, average), the conv family (every conv launch bench.py's
+`roofline` times: igemm, halo, c64, wgrad_halo, stem fwd / wgrad, and their split-K / wgrad
+reductions) per training step with its achieved TFLOP/s and fraction of the bf16 dense peak
+(algorithmic conv FLOPs per step, SURVEY §8(d): 852.2 GFLOP at B=256, 32x32 -- or --gflop-per-step,
+or the bench line's algorithmic_gflop_per_step), and the per-step timeline of the steady state (busy
+time vs wall time between the first and last kernel of a step, i.e. launch gaps). A training step is
+delimited by the SGD kernel (one launch per step). Run it on a trace of the SERIALIZED step
+(`--opt bwd_streams=0`: no side-stream overlap, every kernel's duration is its own) to reproduce
+bench.py's roofline.frac; on an overlapped trace the per-kernel durations are inflated by sharing.
 """
 import csv
 import glob
@@ -15,7 +20,8 @@ import sys
 from collections import defaultdict
 
 CONV = ("igemm_kernel", "conv_halo_kernel", "conv_c64_kernel", "wgrad_halo_kernel", "splitk_reduce_kernel",
-        "wgrad_reduce_kernel")
+        "wgrad_reduce_kernel", "stem_fwd_kernel", "stem_wgrad_kernel", "stem_wgrad_bn_kernel")
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 
 
 def short(name):
@@ -40,6 +46,15 @@ def load_rows(src):
 
 def main():
     src, out = sys.argv[1], sys.argv[2]
+    args = sys.argv[3:]
+    bench = args[args.index("--bench") + 1] if "--bench" in args else None
+    gflop = float(args[args.index("--gflop-per-step") + 1]) if "--gflop-per-step" in args else None
+    if gflop is None and bench:
+        try:
+            gflop = json.loads([l for l in open(bench) if l.startswith("{")][-1])["roofline"]["algorithmic_gflop_per_step"]
+        except Exception:
+            gflop = None
+    gflop = gflop or 852.215
     rows = load_rows(src)
     rows.sort()
     # steps: delimited by the fused SGD kernel
@@ -96,7 +111,9 @@ def main():
                   f"* wall (first kernel start to last kernel end): {avg(wall):.1f} us",
                   f"* GPU busy (union of kernel intervals): {avg(busy):.1f} us "
                   f"({100 * sum(busy) / sum(wall):.1f}% of wall)",
-                  f"* conv family (igemm + split-K / wgrad reductions): {avg(conv):.1f} us per step", "",
+                  f"* conv family (every conv launch incl. stem and split-K / wgrad reductions): {avg(conv):.1f} us "
+                  f"per step = {gflop:.1f} GFLOP / {avg(conv):.1f} us = {gflop / avg(conv) * 1e3:.1f} TFLOP/s = "
+                  f"{gflop / avg(conv) * 1e3 / BF16_PEAK_TFLOPS:.4f} of the {BF16_PEAK_TFLOPS:.0f} TFLOP/s bf16 dense peak", "",
                   "| kernel | calls/step | us/step | avg us |", "|---|---|---|---|"]
         for k, (c, d) in sorted(per_kernel.items(), key=lambda kv: -kv[1][1]):
             lines.append(f"| `{k}` | {c / ns:.0f} | {d / ns / 1e3:.1f} | {d / c / 1e3:.2f} |")
@@ -105,9 +122,9 @@ def main():
                   "| after | before | per step | us/step |", "|---|---|---|---|"]
         for (k0, k1), (c, d) in sorted(gaps.items(), key=lambda kv: -kv[1][1])[:15]:
             lines.append(f"| `{k0}` | `{k1}` | {c / ns:.1f} | {d / ns / 1e3:.1f} |")
-    if len(sys.argv) > 4 and sys.argv[3] == "--bench":
+    if bench:
         try:
-            b = json.loads([l for l in open(sys.argv[4]) if l.startswith("{")][-1])
+            b = json.loads([l for l in open(bench) if l.startswith("{")][-1])
             rf = b.get("roofline", {})
             lines += ["", "## bench.py line of the same run", "", "```", json.dumps(b, indent=1), "```", "",
                       f"bench live conv time per step: {rf.get('conv_ms_per_step')} ms "
