@@ -300,6 +300,10 @@ def main():
                     help="N=1 only: run ONE rank of a W-rank job -- per-rank batch int(G/W) with --global-batch, "
                          "gradients pre-scaled 1/W and the bucketed all-reduce backward forced on (a one-rank RCCL "
                          "communicator): the per-rank shape and code path of config 3 measured on one GPU")
+    ap.add_argument("--sim-comm", choices=("rccl", "loopback"), default="rccl",
+                    help="--sim-world's communicator: the one-rank RCCL communicator (RCCL special-cases one rank: "
+                         "no kernel, host-side copies) or the loopback communicator (an identity scale kernel per "
+                         "bucket on the collective's side stream: the executor's own overlap cost, no RCCL)")
     ap.add_argument("--no-config3", action="store_true",
                     help="N>1: skip the extra config-3 region (global batch 256 over the ranks)")
     ap.add_argument("--size", type=int, default=32)
@@ -347,7 +351,8 @@ def main():
         model.module.set_sync_bn(model.sync_comm)
     sim = max(1, args.sim_world) if world == 1 else 1
     if sim > 1:  # one rank of a sim-rank job: 1/W pre-scale, bucketed all-reduce backward on the side stream
-        model.module._comm = model.comm
+        model.module._comm = (dtc.parallel.Comm.loopback(local, factor=1.0, world=sim) if args.sim_comm == "loopback"
+                              else model.comm)
         model.module._grad_scale = 1.0 / sim
     crit = dtc.CrossEntropyLoss()
     opt = dtc.SGD(model.parameters(), lr=0.1, weight_decay=1e-4, momentum=0.9, nesterov=True)
@@ -401,27 +406,33 @@ def main():
         step(i)
     # Region 1 (the reported value): K plain steps.
     elapsed = timed(args.steps, args.warmup)
-    # Region 2 (roofline): the same K steps with live conv timing armed. Every conv call stamps its
-    # first-workgroup start and each workgroup's end (s_memrealtime) into a device slot that one
-    # kernel per step folds into totals; arming re-captures the step graphs, so two untimed steps
-    # follow the arming and the totals are re-zeroed before the region.
+    # Region 2 (roofline): the same K steps, serialized and eager (options bwd_streams=0, graphs=0: every
+    # kernel has the chip to itself and is launched on the compute stream), with every timed launcher call
+    # bracketed by two HIP timing events on that stream (dtc_rn18_profile_events: its launch duration as
+    # the rocprofv3 kernel trace of the same command -- `--opt bwd_streams=0 --opt graphs=0` -- sees it).
+    # The kernels' own s_memrealtime stamps (first workgroup start .. last workgroup end, folded on the
+    # device) are kept beside them as `stamp_*`. Two untimed steps follow the arming; totals re-zeroed.
     import ctypes as C
-    ms4, fl4, cnt4 = (C.c_double * 4)(), (C.c_double * 4)(), (C.c_int * 4)()
+    ms4, fl4, cnt4 = (C.c_double * 4)(), (C.c_double * 4)(), (C.c_int * 4)()  # events
+    sms4, sfl4, scnt4 = (C.c_double * 4)(), (C.c_double * 4)(), (C.c_int * 4)()  # stamps
     prof_elapsed = None
     if not args.no_live_roofline:
         exe = model.module.executor(B, S, S, "bf16")
-        # kernel efficiency: the weight gradients back on the compute stream, so every conv launch
-        # has the chip to itself (region 1 overlaps them with the dgrad / BN chain on a side stream)
-        bwd_streams = int(dtc._native.lib.dtc_get_option(b"bwd_streams"))
+        saved = {k: int(dtc._native.lib.dtc_get_option(k)) for k in (b"bwd_streams", b"graphs")}
         dtc._native.call("dtc_set_option", b"bwd_streams", 0)
+        dtc._native.call("dtc_set_option", b"graphs", 0)
         dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
+        dtc._native.call("dtc_rn18_profile_events", exe.handle, 256 * 2)
         for i in range(2):
             step(args.warmup + args.steps + i)
         torch.cuda.synchronize()
         dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
+        dtc._native.call("dtc_rn18_profile_events", exe.handle, 256 * (args.steps + 1))
         prof_elapsed = timed(args.steps, args.warmup + args.steps + 2)
-        dtc._native.call("dtc_rn18_profile_end_ex", exe.handle, 4, ms4, fl4, cnt4)
-        dtc._native.call("dtc_set_option", b"bwd_streams", bwd_streams)
+        dtc._native.call("dtc_rn18_profile_events_result", exe.handle, 4, ms4, fl4, cnt4)
+        dtc._native.call("dtc_rn18_profile_end_ex", exe.handle, 4, sms4, sfl4, scnt4)
+        for k, v in saved.items():
+            dtc._native.call("dtc_set_option", k, v)
     ms, fl, cnt = list(ms4)[:3], list(fl4)[:3], list(cnt4)[:3]  # the conv passes (kinds 0-2)
 
     # BASELINE config 3 beside the weak-scaled value at N > 1: the reference's own DDP job, global
@@ -477,7 +488,7 @@ def main():
                     f"DDP bucket {args.bucket_mb} MB")
         if sim > 1:
             workload += (f"; ONE rank of a {sim}-rank job on 1 GPU (per-rank shape of BASELINE config 3, 1/{sim} "
-                         f"pre-scale, bucketed all-reduce backward on a one-rank RCCL communicator): value is "
+                         f"pre-scale, bucketed all-reduce backward on a {'loopback' if args.sim_comm == 'loopback' else 'one-rank RCCL'} communicator): value is "
                          f"this rank's images/s, the node figure needs {sim} GPUs")
         out = {
             "metric": metric,
@@ -506,12 +517,18 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved / BF16_PEAK_TFLOPS, 4) if achieved else None,
                 "traffic": _committed_traffic(),
-                "kernel": "implicit-GEMM conv (fwd+dgrad+wgrad incl. split-K reduce), all launches in the timed "
-                          "region; per-call duration = last workgroup end - first workgroup start (s_memrealtime, "
-                          "stamped by the kernels on the compute stream); measured over a second timed region of "
-                          "the same K steps with the stamps armed (region_ms_per_step) and the weight gradients on "
-                          "the compute stream (bwd_streams=0: each launch has the chip to itself), value from the "
-                          "first (weight gradients overlapped on a side stream)",
+                "kernel": "every conv launch of the step (stem, halo / c64 / implicit-GEMM fwd, dgrad, wgrad incl. "
+                          "split-K and wgrad reductions); per-call duration = HIP timing events recorded on the "
+                          "launch (compute) stream before and after the call, in a second timed region of the same "
+                          "K steps run serialized and eager (bwd_streams=0, graphs=0: each launch has the chip to "
+                          "itself; region_ms_per_step) -- reproduce with tools/prof_summary.py on a rocprofv3 "
+                          "kernel trace of `bench.py --opt bwd_streams=0 --opt graphs=0`; value from the first "
+                          "region (weight gradients overlapped on a side stream, forward replayed)",
+                "stamp_conv_ms_per_step": round(sum(list(sms4)[:3]) / args.steps, 4),
+                "stamp_frac": (round(sum(list(sfl4)[:3]) / (sum(list(sms4)[:3]) * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, 4)
+                               if sum(list(sms4)[:3]) > 0 else None),
+                "stamp_note": "kernel self-stamps (first workgroup start .. last workgroup end, s_memrealtime) of the "
+                              "same calls: excludes each dispatch's ramp before its first workgroup",
                 "traffic_unit": "HBM bytes per conv call (PMC, profiles/*conv_traffic.json)",
                 "conv_ms_per_step": round(conv_ms / args.steps, 4),
                 "region_ms_per_step": round(prof_elapsed / args.steps * 1e3, 4) if prof_elapsed else None,
@@ -524,6 +541,8 @@ def main():
             # finalize+apply of all 20 BNs), measured live in region 2 like the convs: algorithmic bytes
             # (each tensor read / written once) / summed kernel durations
             "bn_in_step": ({"ms_per_step": round(ms4[3] / args.steps, 4),
+                            "stamp_ms_per_step": round(sms4[3] / args.steps, 4),
+                            "timing": "HIP events around each BN launch, serialized eager region (as roofline)",
                             "bytes_per_step": round(fl4[3] / args.steps),
                             "calls_per_step": cnt4[3] // max(1, args.steps),
                             "achieved_GBps": round(fl4[3] / (ms4[3] * 1e-3) / 1e9, 1) if ms4[3] > 0 else None,

@@ -116,6 +116,14 @@ struct Net {
   int prof_kind[PROF_SLOTS] = {};
   double prof_flops[PROF_SLOTS] = {};
   int prof_khz = 100000;
+  // event timing (dtc_rn18_profile_events; bench.py's roofline, the serialized eager step): every timed
+  // launcher call is bracketed by two timing events on the compute stream -- its launch duration as a
+  // rocprofv3 kernel trace of the same step sees it (dispatch to completion), summed per kind at the end
+  bool prof_events = false;
+  hipStream_t prof_st = nullptr;
+  std::vector<hipEvent_t> prof_evpool;  // 2 per bracketed call, created up front
+  size_t prof_evn = 0;                  // pairs used
+  std::vector<std::pair<int, double>> prof_evwork;  // (kind, work) per pair
   // hipGraph replay (option "graphs"): the forward per train flag, the backward as segments split
   // at bucket boundaries (the all-reduces stay eager on the communicator's side stream)
   struct Seg { hipGraphExec_t exec = nullptr; std::vector<int> buckets; };
@@ -429,10 +437,28 @@ static u64* prof_slot(Net& n, int kind, double flops) {
   n.prof_flops[i] = flops;
   return n.prof_ts + (size_t)i * DTC_PROF_SLOT_U64;
 }
+static bool side_on(const Net& n);
+// event bracket of one launcher call (-1: not recorded -- events off, a capture in progress, the weight
+// gradients on a side stream the compute-stream events would not cover, or the pool used up)
+static int prof_ev_open(Net& n, int kind, double work) {
+  if (!n.profiling || !n.prof_events || n.cap_locked || !n.prof_st || side_on(n) || n.prof_evn * 2 + 1 >= n.prof_evpool.size())
+    return -1;
+  const int i = (int)n.prof_evn++;
+  if (n.prof_evwork.size() < n.prof_evn) n.prof_evwork.resize(n.prof_evn);
+  n.prof_evwork[i] = {kind, work};
+  if (hipEventRecord(n.prof_evpool[2 * i], n.prof_st) != hipSuccess) return -1;
+  return i;
+}
+static void prof_ev_close(Net& n, int i) {
+  if (i >= 0) (void)hipEventRecord(n.prof_evpool[2 * i + 1], n.prof_st);
+}
 #define PROF(kind, flops, call)                        \
   do {                                                 \
     u64* ts = prof_slot(n, (kind), (flops));           \
-    DTC_TRY(call);                                     \
+    const int pev_ = prof_ev_open(n, (kind), (flops)); \
+    const int prc_ = (call);                           \
+    prof_ev_close(n, pev_);                            \
+    DTC_TRY(prc_);                                     \
   } while (0)
 
 // ------------------------------------------------------------------ graph capture helpers
@@ -595,8 +621,12 @@ static int bn_act(Net& n, int mode, BNL& b, const u16* x, BNL* b2, const u16* x2
     const BnFwdArgs a1 = fwd_args(n, b, cnt);
     const BnFwdArgs a2 = b2 ? fwd_args(n, *b2, cnt) : BnFwdArgs{};
     uint8_t* mask = bn_mask_on(n) && mask_off ? n.at<uint8_t>(mask_off) : nullptr;
-    u64* ts = prof_slot(n, 3, (double)M * b.C * (4.0 + (mode != 1 ? 2.0 : 0.0) + (mask ? 0.125 : 0.0)));
-    return bn_fin_apply(mode, x, a1, x2, b2 ? &a2 : nullptr, y, M, b.C, st, mask, ts);
+    const double work = (double)M * b.C * (4.0 + (mode != 1 ? 2.0 : 0.0) + (mask ? 0.125 : 0.0));
+    u64* ts = prof_slot(n, 3, work);
+    const int ev = prof_ev_open(n, 3, work);
+    const int rc = bn_fin_apply(mode, x, a1, x2, b2 ? &a2 : nullptr, y, M, b.C, st, mask, ts);
+    prof_ev_close(n, ev);
+    return rc;
   }
   DTC_TRY(bn_finalize_fwd(n, b, cnt, train, st));
   if (b2) DTC_TRY(bn_finalize_fwd(n, *b2, cnt, train, st));
@@ -847,6 +877,7 @@ static int forward(Net& n, const float* x, float* logits, bool train, hipStream_
   return 0;
 }
 static int forward_impl(Net& n, const float* x, float* logits, bool train, hipStream_t st) {
+  n.prof_st = st;
   // graphed bf16 forward: the pool + FC head is launched after the graph straight into the caller's logits
   // (the graph cannot bake in a per-call pointer); the fp32 executor's graph writes a graph-owned buffer
   // that is copied out after the replay
@@ -955,8 +986,12 @@ static int bn_bwd_coef_apply(Net& n, BNL& b1, const u16* dz, const u16* x1, u16*
     const BnBwdArgs a1 = bwd_args(n, b1, cnt, gs);
     const BnBwdArgs a2 = b2 ? bwd_args(n, *b2, cnt, gs) : BnBwdArgs{};
     if (mbits) {
-      u64* ts = prof_slot(n, 3, (double)M * b1.C * (6.125 + (x2 ? 4.0 : 0.0) + (dzo ? 2.0 : 0.0)));
-      return bn_bwd_fin_apply_mask(dz, mbits, dzo, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st, ts);
+      const double work = (double)M * b1.C * (6.125 + (x2 ? 4.0 : 0.0) + (dzo ? 2.0 : 0.0));
+      u64* ts = prof_slot(n, 3, work);
+      const int ev = prof_ev_open(n, 3, work);
+      const int rc = bn_bwd_fin_apply_mask(dz, mbits, dzo, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st, ts);
+      prof_ev_close(n, ev);
+      return rc;
     }
     return bn_bwd_fin_apply(dz, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st);
   }
@@ -1386,6 +1421,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
 }
 
 static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st) {
+  n.prof_st = st;
   if (!n.sums_fresh) DTC_TRY(zero_bytes(n.ws + n.acc_lo, n.stats_hi - n.acc_lo, st));
   n.sums_fresh = false;
   if (!graphs_on(n, true, comm != nullptr)) {
@@ -1610,6 +1646,44 @@ int dtc_rn18_profile_begin(dtc_net* net, int capacity) {
   DTC_HIP(hipMemset(n.prof_acc, 0, bytes));
   DTC_HIP(hipDeviceSynchronize());
   n.profiling = true;  // the next calls launch (capturing on first use) the profiled graph set
+  return 0;
+}
+
+int dtc_rn18_profile_events(dtc_net* net, int pairs) {
+  DTC_CHECK_ARG(net && pairs >= 0, "dtc_rn18_profile_events: bad args");
+  Net& n = net->n;
+  n.prof_events = pairs > 0;
+  n.prof_evn = 0;
+  const size_t want = (size_t)pairs * 2;
+  while (n.prof_evpool.size() < want) {
+    hipEvent_t e;
+    DTC_HIP(hipEventCreate(&e));  // timing events
+    n.prof_evpool.push_back(e);
+  }
+  return 0;
+}
+
+int dtc_rn18_profile_events_result(dtc_net* net, int nkinds, double* ms_by_kind, double* work_by_kind,
+                                   int* count_by_kind) {
+  DTC_CHECK_ARG(net != nullptr && nkinds >= 1 && nkinds <= 4, "dtc_rn18_profile_events_result: bad args");
+  Net& n = net->n;
+  for (int k = 0; k < nkinds; ++k) {
+    if (ms_by_kind) ms_by_kind[k] = 0;
+    if (work_by_kind) work_by_kind[k] = 0;
+    if (count_by_kind) count_by_kind[k] = 0;
+  }
+  for (size_t i = 0; i < n.prof_evn; ++i) {
+    const int k = n.prof_evwork[i].first;
+    if (k >= nkinds) continue;
+    DTC_HIP(hipEventSynchronize(n.prof_evpool[2 * i + 1]));
+    float ms = 0.f;
+    DTC_HIP(hipEventElapsedTime(&ms, n.prof_evpool[2 * i], n.prof_evpool[2 * i + 1]));
+    if (ms_by_kind) ms_by_kind[k] += ms;
+    if (work_by_kind) work_by_kind[k] += n.prof_evwork[i].second;
+    if (count_by_kind) count_by_kind[k] += 1;
+  }
+  n.prof_evn = 0;
+  n.prof_events = false;
   return 0;
 }
 

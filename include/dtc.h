@@ -344,6 +344,14 @@ int dtc_rn18_profile_end(dtc_net* net, double* ms_by_kind, double* flops_by_kind
  * (forward finalize+apply, backward reduce, backward finalize+apply), work = algorithmic HBM bytes
  * (every tensor the kernel must touch, read or written once: the in-step BN HBM roofline). */
 int dtc_rn18_profile_end_ex(dtc_net* net, int nkinds, double* ms_by_kind, double* work_by_kind, int* count_by_kind);
+/* Event timing of the same launcher calls (bench.py's roofline): while profiling is armed and `pairs` > 0,
+ * every timed launcher call of an EAGER step whose weight gradients run on the compute stream (options
+ * graphs = 0, bwd_streams = 0) is bracketed by two timing events on the compute stream (at most `pairs`
+ * calls; `pairs` = 0 switches it off). _result synchronises, sums the elapsed times (ms) and algorithmic
+ * work per kind as profile_end_ex does, and resets. */
+int dtc_rn18_profile_events(dtc_net* net, int pairs);
+int dtc_rn18_profile_events_result(dtc_net* net, int nkinds, double* ms_by_kind, double* work_by_kind,
+                                   int* count_by_kind);
 
 #ifdef __cplusplus
 }
