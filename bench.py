@@ -373,13 +373,13 @@ def main():
     pools = {B: make_pool(B)}
     losses = []
 
-    def step(i, b=B):
+    def step(i, b=B, host_sync=True):
         img, label = pools[b][i % len(pools[b])]
         opt.zero_grad()
         with dtc.autocast():
             logit = model(img)
             loss = crit(logit, label)
-        if not args.no_barrier:
+        if host_sync and not args.no_barrier:
             if args.torch_barrier:
                 dist.barrier()
             else:
@@ -387,15 +387,15 @@ def main():
         scaler.scale(loss).backward()
         scaler.step(opt)
         scaler.update()
-        if not args.no_item:
+        if host_sync and not args.no_item:
             losses.append(loss.item())
 
-    def timed(k, first, b=B):
+    def timed(k, first, b=B, host_sync=True):
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(k):
-            step(first + i, b)
+            step(first + i, b, host_sync)
         torch.cuda.synchronize()
         dist.barrier()
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
@@ -428,7 +428,9 @@ def main():
         torch.cuda.synchronize()
         dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
         dtc._native.call("dtc_rn18_profile_events", exe.handle, 256 * (args.steps + 1))
-        prof_elapsed = timed(args.steps, args.warmup + args.steps + 2)
+        # (no per-step barrier / loss.item() host sync in this region: the host stays ahead of the GPU,
+        # so an event pair times its launch, not a launch plus the host catching up after a drain)
+        prof_elapsed = timed(args.steps, args.warmup + args.steps + 2, host_sync=False)
         dtc._native.call("dtc_rn18_profile_events_result", exe.handle, 4, ms4, fl4, cnt4)
         dtc._native.call("dtc_rn18_profile_end_ex", exe.handle, 4, sms4, sfl4, scnt4)
         for k, v in saved.items():
@@ -521,7 +523,7 @@ def main():
                           "split-K and wgrad reductions); per-call duration = HIP timing events recorded on the "
                           "launch (compute) stream before and after the call, in a second timed region of the same "
                           "K steps run serialized and eager (bwd_streams=0, graphs=0: each launch has the chip to "
-                          "itself; region_ms_per_step) -- reproduce with tools/prof_summary.py on a rocprofv3 "
+                          "itself) without the per-step host syncs (the host stays ahead; region_ms_per_step) -- reproduce with tools/prof_summary.py on a rocprofv3 "
                           "kernel trace of `bench.py --opt bwd_streams=0 --opt graphs=0`; value from the first "
                           "region (weight gradients overlapped on a side stream, forward replayed)",
                 "stamp_conv_ms_per_step": round(sum(list(sms4)[:3]) / args.steps, 4),

@@ -441,7 +441,8 @@ static bool side_on(const Net& n);
 // event bracket of one launcher call (-1: not recorded -- events off, a capture in progress, the weight
 // gradients on a side stream the compute-stream events would not cover, or the pool used up)
 static int prof_ev_open(Net& n, int kind, double work) {
-  if (!n.profiling || !n.prof_events || n.cap_locked || !n.prof_st || side_on(n) || n.prof_evn * 2 + 1 >= n.prof_evpool.size())
+  // (prof_st may be the null stream: the caller's default stream)
+  if (!n.profiling || !n.prof_events || n.cap_locked || side_on(n) || n.prof_evn * 2 + 1 >= n.prof_evpool.size())
     return -1;
   const int i = (int)n.prof_evn++;
   if (n.prof_evwork.size() < n.prof_evn) n.prof_evwork.resize(n.prof_evn);
@@ -1657,7 +1658,9 @@ int dtc_rn18_profile_events(dtc_net* net, int pairs) {
   const size_t want = (size_t)pairs * 2;
   while (n.prof_evpool.size() < want) {
     hipEvent_t e;
-    DTC_HIP(hipEventCreate(&e));  // timing events
+    // timing events without the system-scope release fence at completion (no L2 write-back between the
+    // bracketed launches: the kernels see the caches the unbracketed step gives them)
+    DTC_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     n.prof_evpool.push_back(e);
   }
   return 0;
