@@ -440,6 +440,159 @@ int bn_bwd_fin_apply(const float* dz, const float* x1, const BnBwdArgs& a1, floa
   return bwd_fin_apply<float>(dz, x1, a1, dx1, x2, a2, dx2, M, C, st);
 }
 
+// ------------------------------------------------------------------ one-pass backward, channel groups
+// Small BN tensors (M <= 4096 pixels, 2048 with the projection's second BN: layer4 at batch 256, layers 3-4 at the per-rank batches
+// of BASELINE config 3) are launch-latency bound: the reduce + apply pair costs two kernel boundaries for a
+// few MB. Here ONE launch does both without any cross-workgroup step: workgroup g owns channels 8g..8g+7 of
+// EVERY pixel (grid = C / 8), holds its slice of (dy, mask bits, x [, x2]) in registers (CG_NP pixels per
+// thread), reduces sum(dz) and sum(dz * xhat) over the whole batch inside the workgroup (fixed order: lane
+// butterflies, then the waves in order, in fp64), computes the coefficients as fa_bwd_coef_from does and
+// writes dx (and dz / dx2) from the registers: 6.125 B per element read / written once, one launch.
+constexpr int CG_THREADS = 512;
+template <bool DUAL>
+constexpr int cg_np() { return DUAL ? 4 : 8; }  // pixels per thread (the dual form holds a third tensor)
+
+template <bool DUAL>
+__global__ void __launch_bounds__(CG_THREADS) bn_bwd_cg_kernel(const u16* __restrict__ dy, const uint8_t* __restrict__ mbits,
+                                                            u16* dzo, const u16* __restrict__ x1, const BnBwdArgs a1,
+                                                            u16* __restrict__ dx1, const u16* __restrict__ x2,
+                                                            const BnBwdArgs a2, u16* __restrict__ dx2, int M, int C,
+                                                            u64* ts) {
+  __shared__ float wred[CG_THREADS / 64][24];
+  __shared__ float coef[6][8];
+  stamp_start(ts);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c0 = blockIdx.x * 8;
+  constexpr int CG_NP = cg_np<DUAL>();
+  uint4 vd[CG_NP], va[CG_NP], vb[CG_NP];
+  uint32_t mk[CG_NP];
+#pragma unroll
+  for (int u = 0; u < CG_NP; ++u) {  // branch-free loads (clamped): all in flight together
+    const int m = min(t + u * CG_THREADS, M - 1);
+    const size_t o = (size_t)m * C + c0;
+    vd[u] = *(const uint4*)(dy + o);
+    va[u] = *(const uint4*)(x1 + o);
+    if constexpr (DUAL) vb[u] = *(const uint4*)(x2 + o);
+    mk[u] = mbits[o >> 3];
+  }
+  // the 8 channels' mean / invstd (both BNs) in LDS: broadcast reads, no 32 registers held across the loads
+  __shared__ float mi[4][8];
+  if (t < 32) {
+    const int k = t & 7, w = t >> 3;
+    const float* src = w == 0 ? a1.mean : w == 1 ? a1.invstd : w == 2 ? (DUAL ? a2.mean : a1.mean) : (DUAL ? a2.invstd : a1.invstd);
+    mi[w][k] = src[c0 + k];
+  }
+  __syncthreads();
+  float sd[8], s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sd[k] = s1[k] = s2[k] = 0.f;
+#pragma unroll
+  for (int u = 0; u < CG_NP; ++u) {
+    const bool ok = t + u * CG_THREADS < M;
+    float d[8], a[8], b[8];
+    unpack8(vd[u], d);
+    unpack8(va[u], a);
+    if constexpr (DUAL) unpack8(vb[u], b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      d[k] = ok && ((mk[u] >> k) & 1u) ? d[k] : 0.f;
+      sd[k] += d[k];
+      s1[k] += d[k] * ((a[k] - mi[0][k]) * mi[1][k]);
+      if constexpr (DUAL) s2[k] += d[k] * ((b[k] - mi[2][k]) * mi[3][k]);
+    }
+    vd[u] = pack8(d);  // dz (exact: masking is exact)
+  }
+  // fixed-order workgroup reduction: lane butterfly, then the waves in order (fp64)
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float a = wave_sum(sd[k]), b = wave_sum(s1[k]);
+    const float e = DUAL ? wave_sum(s2[k]) : 0.f;
+    if (lane == 0) {
+      wred[wave][k] = a;
+      wred[wave][8 + k] = b;
+      wred[wave][16 + k] = e;
+    }
+  }
+  __syncthreads();
+  if (t < 8) {
+    double d = 0.0, x = 0.0, y = 0.0;
+#pragma unroll
+    for (int w = 0; w < CG_THREADS / 64; ++w) {
+      d += wred[w][t];
+      x += wred[w][8 + t];
+      y += wred[w][16 + t];
+    }
+    const int c = c0 + t;
+    const double cnt = (double)a1.count;
+    {
+      const double is = mi[1][t], a = (double)a1.gamma[c] * is, b = -a * is * x / cnt;
+      coef[0][t] = (float)a;
+      coef[1][t] = (float)b;
+      coef[2][t] = (float)(-a * d / cnt - b * (double)mi[0][t]);
+      if (a1.dgamma) a1.dgamma[c] = (float)(x * a1.gscale);
+      if (a1.dbeta) a1.dbeta[c] = (float)(d * a1.gscale);
+    }
+    if constexpr (DUAL) {
+      const double is = mi[3][t], a = (double)a2.gamma[c] * is, b = -a * is * y / cnt;
+      coef[3][t] = (float)a;
+      coef[4][t] = (float)b;
+      coef[5][t] = (float)(-a * d / cnt - b * (double)mi[2][t]);
+      if (a2.dgamma) a2.dgamma[c] = (float)(y * a2.gscale);
+      if (a2.dbeta) a2.dbeta[c] = (float)(d * a2.gscale);
+    }
+  }
+  __syncthreads();
+  float A1[8], B1[8], C1[8], A2[8], B2[8], C2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    A1[k] = coef[0][k]; B1[k] = coef[1][k]; C1[k] = coef[2][k];
+    if constexpr (DUAL) {
+      A2[k] = coef[3][k]; B2[k] = coef[4][k]; C2[k] = coef[5][k];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < CG_NP; ++u) {
+    const int m = t + u * CG_THREADS;
+    if (m >= M) break;
+    const size_t o = (size_t)m * C + c0;
+    float d[8], a[8], v[8];
+    unpack8(vd[u], d);
+    if (dzo != nullptr) *(uint4*)(dzo + o) = vd[u];
+    unpack8(va[u], a);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = A1[k] * d[k] + B1[k] * a[k] + C1[k];
+    *(uint4*)(dx1 + o) = pack8(v);
+    if constexpr (DUAL) {
+      unpack8(vb[u], a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = A2[k] * d[k] + B2[k] * a[k] + C2[k];
+      *(uint4*)(dx2 + o) = pack8(v);
+    }
+  }
+  stamp_end(ts);
+}
+
+bool bn_bwd_cg_ok(int64_t M, int C, bool dual) {
+  return M >= 1 && M <= (int64_t)CG_THREADS * (dual ? cg_np<true>() : cg_np<false>()) && C % 8 == 0 && C >= 8;
+}
+
+int bn_bwd_cg(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
+              const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st, u64* ts) {
+  DTC_CHECK_ARG(dy && mbits && x1 && dx1 && a1.gamma && a1.mean && a1.invstd && M >= 1,
+                "bn_bwd_cg: bad args (M=%lld C=%d)", (long long)M, C);
+  DTC_CHECK_ARG(bn_bwd_cg_ok(M, C, x2 != nullptr), "bn_bwd_cg: M=%lld too large", (long long)M);
+  DTC_CHECK_ARG(!x2 || (a2 && a2->gamma && a2->mean && a2->invstd && dx2), "bn_bwd_cg: dual branch args");
+  const BnBwdArgs none{};
+  if (x2)
+    hipLaunchKernelGGL(bn_bwd_cg_kernel<true>, dim3(C / 8), dim3(CG_THREADS), 0, st, dy, mbits, dzo, x1, a1, dx1, x2,
+                       *a2, dx2, (int)M, C, ts);
+  else
+    hipLaunchKernelGGL(bn_bwd_cg_kernel<false>, dim3(C / 8), dim3(CG_THREADS), 0, st, dy, mbits, dzo, x1, a1, dx1,
+                       nullptr, none, nullptr, (int)M, C, ts);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 // ------------------------------------------------------------------ backward
 // MASK: dz = dy * [ym > 0], stored. MB: dz = dy * mask bit (the forward's ReLU mask), not stored
 // (bn_bwd_fin_apply_mask forms it again from the same bits): 4.125 B per element instead of 8.

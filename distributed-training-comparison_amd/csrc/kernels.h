@@ -51,6 +51,8 @@ namespace dtc {
   X(WGRAD_S2_WGS, wgrad_s2_wgs, 256)    /* stride-2 halo wgrad: target workgroups (split-K slab = wgs x tile) */ \
   X(DGRAD_SCF, dgrad_scf, 1)            /* shortcut dgrad fused into conv1's parity-class dgrad */            \
   X(BNB_MASK, bnb_mask, 0)              /* mask-bit backward: BN sums in the producing dgrad's epilogue */    \
+  X(BN_CG, bn_cg, 1)                    /* small BN backward as one launch (bn_bwd_cg) ...                  */ \
+  X(BN_CG_ELEMS, bn_cg_elems, 262144)   /* ... for tensors of at most this many elements                    */ \
   X(HEAD_FUSED, head_fused, 0)          /* head backward in one launch (dW/db strips + dact) */               \
   X(HALO_STAGE_EPI, halo_stage_epi, 0)  /* conv_halo DGRAD epilogue staged through LDS: 1 always, 2 GEN only */ \
   X(BUCKET_TAIL, bucket_tail, 1)        /* (plan time) close the open bucket (>= 1 MB) after layer2.0 */      \
@@ -231,6 +233,12 @@ int bn_bwd_fin_apply_mask(const u16* dy, const uint8_t* mbits, u16* dzo, const u
                           const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st,
                           u64* ts = nullptr);
 int bn_mask_apply(const u16* dy, const uint8_t* mbits, u16* dz, int64_t M, int C, hipStream_t st);
+// One-launch mask-bit BN backward of a small tensor (bn_bwd_cg_ok: M <= 4096 pixels, 2048 dual): reduce +
+// coefficients + apply (dz, dx1 [, dx2], dgamma / dbeta x gscale) in one workgroup per 8 channels; the fp64
+// slots are unused
+bool bn_bwd_cg_ok(int64_t M, int C, bool dual);
+int bn_bwd_cg(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
+              const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st, u64* ts = nullptr);
 int bn_bwd_fin_apply(const u16* dz, const u16* x1, const BnBwdArgs& a1, u16* dx1, const u16* x2, const BnBwdArgs* a2,
                      u16* dx2, int64_t M, int C, hipStream_t st);
 int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2, const BnFwdArgs* a2, float* y,

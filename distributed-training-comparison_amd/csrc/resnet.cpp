@@ -974,6 +974,28 @@ static BnBwdArgs bwd_args(Net& n, BNL& b, int64_t count, float gs) {
 
 // dx1 = BN-backward apply of b1 on (dz, x1) [; dx2 of b2 on (dz, x2)], coefficients from the sums
 // bn_bwd_reduce accumulated; dgamma / dbeta into the flat gradient buffer.
+// Small tensors (option bn_cg, bn_bwd_cg_ok): the mask-bit BN backward -- reduction, coefficients, apply --
+// as ONE launch (bn.hip bn_bwd_cg: one workgroup per 8 channels over the whole batch, no fp64 slots); not
+// with SyncBN (its sums are all-reduced between the two passes)
+// Measured (kernel trace r04e, batch 256): at layer4's 4096 x 512 the one launch took 26-30 us against
+// 11 us for the pair -- 64 workgroups of 16-B pieces strided by the channel count -- so it is used only
+// for tensors of at most 256K elements (layer4 at the per-rank batch 32 of config 3)
+static bool bn_cg_on(const Net& n, int64_t M, int C, bool dual) {
+  return option_get(OPT_BN_CG) != 0 && !n.sync && !n.f32 && bn_fused() && M * C <= (int64_t)option_get(OPT_BN_CG_ELEMS) &&
+         bn_bwd_cg_ok(M, C, dual);
+}
+static int bn_bwd_one_launch(Net& n, BNL& b1, const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, u16* dx1,
+                             BNL* b2, const u16* x2, u16* dx2, int64_t M, float gs, hipStream_t st) {
+  const BnBwdArgs a1 = bwd_args(n, b1, M, gs);
+  const BnBwdArgs a2 = b2 ? bwd_args(n, *b2, M, gs) : BnBwdArgs{};
+  const double work = (double)M * b1.C * (6.125 + (x2 ? 4.0 : 0.0) + (dzo ? 2.0 : 0.0));
+  u64* ts = prof_slot(n, 3, work);
+  const int ev = prof_ev_open(n, 3, work);
+  const int rc = bn_bwd_cg(dy, mbits, dzo, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st, ts);
+  prof_ev_close(n, ev);
+  return rc;
+}
+
 static int bn_bwd_coef_apply(Net& n, BNL& b1, const u16* dz, const u16* x1, u16* dx1, BNL* b2, const u16* x2, u16* dx2,
                              int64_t M, float gs, hipStream_t st, const uint8_t* mbits = nullptr,
                              u16* dzo = nullptr) {
@@ -1190,6 +1212,9 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
       // writes dz over it as before (the residual of its conv1 dgrad; idempotent on dz)
       DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[0], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
                                 b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st, mout, b.proj ? nullptr : G[0]));
+    } else if (bn_cg_on(n, M, b.Cout, b.proj)) {
+      DTC_TRY(bn_bwd_one_launch(n, b.b2, G[0], mout, b.proj ? nullptr : G[0], n.at<u16>(b.C2), dc2,
+                                b.proj ? &b.bsc : nullptr, b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st));
     } else {
       PROF(3, (double)M * b.Cout * (b.proj ? 6.125 : 4.125),
            bn_bwd_reduce_mask(G[0], mout, n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
@@ -1219,6 +1244,8 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     DTC_TRY(cap_masked(n, cp + ".dz1", G[4], b.MA1, M, b.Cout, st));
     if (bmf) {  // bn1's sums came with conv2's dgrad
       DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st, ma1));
+    } else if (bn_cg_on(n, M, b.Cout, false)) {
+      DTC_TRY(bn_bwd_one_launch(n, b.b1, G[4], ma1, nullptr, n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st));
     } else {
       PROF(3, (double)M * b.Cout * 4.125,
            bn_bwd_reduce_mask(G[4], ma1, n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
