@@ -377,6 +377,18 @@ int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute) 
   return 0;
 }
 
+int comm_allreduce_on(Comm* c, void* buf, size_t count, hipStream_t st) {
+  DTC_CHECK_ARG(c && buf, "comm_allreduce_on: bad args");
+  if (count == 0) return 0;
+  if (c->grp) {
+    c->log.push_back(CommLogEntry{(uint64_t)(uintptr_t)buf, (uint64_t)count, 1});
+    return group_collective(c, GK_ALLREDUCE, buf, count, 0, 0, st, st);
+  }
+  if (c->loopback) return loopback_reduce(c, buf, count, 0, st, true);
+  DTC_NCCL(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c->nccl, st));
+  return 0;
+}
+
 int comm_join(Comm* c, hipStream_t compute) {
   if (!c || !c->pending) return 0;
   DTC_HIP(hipEventRecord(c->done, c->side));

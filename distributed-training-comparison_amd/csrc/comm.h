@@ -22,6 +22,9 @@ int comm_broadcast(Comm* c, void* buf, size_t count, int dtype, int root, hipStr
 // enqueued so far on `compute`; join orders `compute` after all outstanding buckets.
 int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute);
 int comm_join(Comm* c, hipStream_t compute);
+// a bucket all-reduce issued directly on `st` (its producers already ordered before it on `st`): no fork,
+// no join -- the executor's weight-gradient stream carries it (one stream fewer in the backward)
+int comm_allreduce_on(Comm* c, void* buf, size_t count, hipStream_t st);
 int comm_world(const Comm* c);
 int comm_rank(const Comm* c);
 // in-process thread group: `world` handles (outs[r] = rank r) on one device, one host thread per rank

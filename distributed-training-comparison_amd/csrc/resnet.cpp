@@ -938,7 +938,15 @@ static int maybe_bucket(Net& n, int after_block, const BwdCtx& cx, hipStream_t s
       DTC_HIP(hipStreamWaitEvent(n.side_st, ev, 0));
       prod = n.side_st;
     }
-    for (int i : ids) DTC_TRY(comm_allreduce_async(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], prod));
+    // option comm_on_side: the collective on the weight-gradient stream itself (it holds both producers
+    // now; the stream is joined into the compute stream at the end of the backward) -- one HIP stream
+    // fewer competing for the process's hardware queues (GPU_MAX_HW_QUEUES); the weight gradients of
+    // later buckets then queue behind it on that stream
+    const bool on_side = option_get(OPT_COMM_ON_SIDE) != 0 && prod == n.side_st;
+    for (int i : ids) {
+      if (on_side) DTC_TRY(comm_allreduce_on(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], prod));
+      else DTC_TRY(comm_allreduce_async(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], prod));
+    }
     return 0;
   }
   DTC_TRY(join_side(n, st));  // a graph segment ends here: every stream forked in it joins back

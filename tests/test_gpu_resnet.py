@@ -1204,9 +1204,9 @@ def _grads_with(model, crit, x, y, comm):
     return model.flat.grads.detach().cpu().numpy().copy()
 
 
-@pytest.mark.parametrize("graphs", [1, 0])
+@pytest.mark.parametrize("graphs,on_side", [(1, 0), (0, 0), (0, 1)])
 @pytest.mark.parametrize("cap_mb", [1.0, 5.0, 25.0])
-def test_reducer_reduces_every_bucket_once_after_its_producers(dtc, cuda, graphs, cap_mb):
+def test_reducer_reduces_every_bucket_once_after_its_producers(dtc, cuda, graphs, on_side, cap_mb):
     """The N>1 DDP backward (ddp/trainer.py:157) on one GPU, made observable: a loopback
     communicator (dtc_comm_init_loopback) replaces each bucket's ncclAllReduce with `bucket *= 2` on
     the communicator's side stream and logs (address, count). Then, on capture AND on replay:
@@ -1217,9 +1217,11 @@ def test_reducer_reduces_every_bucket_once_after_its_producers(dtc, cuda, graphs
         gradient, so the doubling would be overwritten: 1x) fails;
       * with the DDP mean pre-scale of 1/2 (module._grad_scale, W=2) the result equals the local
         gradient (the mean over two identical ranks).
-    The last bucket of the plan is only layer1 + the stem (the unavoidable exposed tail)."""
+    The last bucket of the plan is only layer1 + the stem (the unavoidable exposed tail). on_side: the eager
+    backward's bucket collectives on the weight-gradient stream itself (option comm_on_side)."""
     _graphs_prev = dtc._native.lib.dtc_get_option(b"graphs")
     dtc._native.lib.dtc_set_option(b"graphs", graphs)
+    dtc._native.lib.dtc_set_option(b"comm_on_side", on_side)
     comm = dtc.parallel.Comm.loopback(cuda.index or 0, 2.0)
     try:
         torch.manual_seed(42)
@@ -1252,6 +1254,7 @@ def test_reducer_reduces_every_bucket_once_after_its_producers(dtc, cuda, graphs
     finally:
         comm.close()
         dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
+        dtc._native.lib.dtc_set_option(b"comm_on_side", 0)
 
 
 @pytest.mark.parametrize("graphs", [1, 0])
