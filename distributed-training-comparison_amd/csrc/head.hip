@@ -355,7 +355,10 @@ static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int
                       float scale, float* dw, float* db, T* dact, float* ws, size_t ws_bytes, hipStream_t st) {
   DTC_CHECK_ARG(dlogits && feat && wfc && dw && db && dact && N > 0 && HW > 0 && C > 0 && ncls > 0,
                 "head_bwd: bad args");
-  if (ncls <= 1024 && option_get(OPT_HEAD_FUSED) != 0) {
+  // option head_fused: 1 always, 2 (auto) at most 64 images -- the dW strips loop over the images, so at
+  // batch 256 the three-launch form measured 1% faster; at the per-rank batches of config 3 the launches cost more
+  const int hf = option_get(OPT_HEAD_FUSED);
+  if (ncls <= 1024 && (hf == 1 || (hf == 2 && N <= 64))) {
     const int nw = ncls * ((C + 255) / 256);
     hipLaunchKernelGGL(head_bwd_fused_kernel<T>, dim3(nw + N), dim3(256), 0, st, dlogits, feat, wfc, N, HW, C, ncls,
                        scale, dw, db, dact, nw);

@@ -53,9 +53,9 @@ namespace dtc {
   X(BNB_MASK, bnb_mask, 0)              /* mask-bit backward: BN sums in the producing dgrad's epilogue */    \
   X(BN_CG, bn_cg, 1)                    /* small BN backward as one launch (bn_bwd_cg) ...                  */ \
   X(BN_CG_ELEMS, bn_cg_elems, 262144)   /* ... for tensors of at most this many elements                    */ \
-  X(HEAD_FUSED, head_fused, 0)          /* head backward in one launch (dW/db strips + dact) */               \
+  X(HEAD_FUSED, head_fused, 2)          /* head backward in one launch: 1 always, 2 at <= 64 images */       \
   X(HALO_STAGE_EPI, halo_stage_epi, 0)  /* conv_halo DGRAD epilogue staged through LDS: 1 always, 2 GEN only */ \
-  X(COMM_ON_SIDE, comm_on_side, 0)      /* eager backward: bucket all-reduces on the weight-gradient stream */ \
+  X(COMM_ON_SIDE, comm_on_side, 1)      /* bucket all-reduces on the weight-gradient stream (no comm stream) */ \
   X(BUCKET_TAIL, bucket_tail, 1)        /* (plan time) close the open bucket (>= 1 MB) after layer2.0 */      \
   X(WGRAD_GEN, wgrad_gen, 1)            /* wgrad_halo general step geometry (224x224 model) */                \
   X(HALO_GEN, halo_gen, 1)              /* conv_halo general tile geometry (224x224 model) */                 \

@@ -519,7 +519,10 @@ constexpr int64_t kEagerBwdMinPixels = 192ll * 32 * 32;
 static bool graphs_on(Net& n, bool bwd, bool comm = false) {
   const int g = option_get(OPT_GRAPHS);
   if (n.capture || n.sync || g == 0 || (g == 2 && bwd) || (g == 3 && !bwd)) return false;
-  if (g == 4 && bwd && !comm && (int64_t)n.B * n.H * n.W >= kEagerBwdMinPixels) return false;
+  // (with a communicator too once its bucket collectives ride the weight-gradient stream, option comm_on_side:
+  // 125.5k vs 117.8k img/s at batch 256 per rank, loopback A/B r04f; the N=1 step without one: 129.1k)
+  if (g == 4 && bwd && (!comm || option_get(OPT_COMM_ON_SIDE) != 0) && (int64_t)n.B * n.H * n.W >= kEagerBwdMinPixels)
+    return false;
   if (n.graph_epoch != option_epoch()) {  // options are baked into captured launches
     drop_graphs(n);
     n.graph_epoch = option_epoch();
@@ -1488,11 +1491,23 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
     }
     if (dlogits != n.at<float>(n.DLOGITS))
       DTC_HIP(hipMemcpyAsync(n.at<float>(n.DLOGITS), dlogits, (size_t)n.B * n.ncls * 4, hipMemcpyDeviceToDevice, st));
+    // option comm_on_side: each bucket's collective on the weight-gradient stream forked from the compute
+    // stream after its segment (that stream is idle between the replayed segments), joined once at the end:
+    // no stream of the communicator's own in the backward
+    const bool on_side = option_get(OPT_COMM_ON_SIDE) != 0 && comm != nullptr;
     for (const auto& sg : n.bwd_segs[pi]) {
       if (sg.exec) DTC_TRY(graph_launch(n, sg.exec, st));
-      for (int i : sg.buckets)
-        DTC_TRY(comm_allreduce_async(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st));
+      for (int i : sg.buckets) {
+        if (on_side) {
+          hipStream_t sd = st;
+          DTC_TRY(fork_side(n, st, &sd));
+          DTC_TRY(comm_allreduce_on(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], sd));
+        } else {
+          DTC_TRY(comm_allreduce_async(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st));
+        }
+      }
     }
+    if (on_side) DTC_TRY(join_side(n, st));
   }
   if (comm) DTC_TRY(comm_join(comm, st));
   return 0;

@@ -70,7 +70,7 @@ def _model(dtc, cuda, cap_mb, sync_bn=False):
     return m
 
 
-@pytest.mark.parametrize("graphs,on_side", [(1, 0), (0, 0), (0, 1)])
+@pytest.mark.parametrize("graphs,on_side", [(1, 0), (1, 1), (0, 0), (0, 1)])
 @pytest.mark.parametrize("cap_mb", [1.0, 5.0, 25.0])
 def test_ddp_two_ranks_distinct_data_allreduce_equals_fp32_sum(dtc, cuda, graphs, on_side, cap_mb):
     world, batch = 2, 32
@@ -140,7 +140,7 @@ def test_ddp_two_ranks_distinct_data_allreduce_equals_fp32_sum(dtc, cuda, graphs
         assert np.array_equal(res[0][1], res[1][1])
     finally:
         dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
-        dtc._native.lib.dtc_set_option(b"comm_on_side", 0)
+        dtc._native.lib.dtc_set_option(b"comm_on_side", 1)
 
 
 def test_sync_batchnorm_two_ranks_distinct_data_equals_concatenated_batch(dtc, cuda):

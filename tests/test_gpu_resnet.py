@@ -1204,7 +1204,7 @@ def _grads_with(model, crit, x, y, comm):
     return model.flat.grads.detach().cpu().numpy().copy()
 
 
-@pytest.mark.parametrize("graphs,on_side", [(1, 0), (0, 0), (0, 1)])
+@pytest.mark.parametrize("graphs,on_side", [(1, 0), (1, 1), (0, 0), (0, 1)])
 @pytest.mark.parametrize("cap_mb", [1.0, 5.0, 25.0])
 def test_reducer_reduces_every_bucket_once_after_its_producers(dtc, cuda, graphs, on_side, cap_mb):
     """The N>1 DDP backward (ddp/trainer.py:157) on one GPU, made observable: a loopback
@@ -1254,7 +1254,7 @@ def test_reducer_reduces_every_bucket_once_after_its_producers(dtc, cuda, graphs
     finally:
         comm.close()
         dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
-        dtc._native.lib.dtc_set_option(b"comm_on_side", 0)
+        dtc._native.lib.dtc_set_option(b"comm_on_side", 1)
 
 
 @pytest.mark.parametrize("graphs", [1, 0])
