@@ -1,8 +1,8 @@
 # scratch GPU session (overwritten per session; see tools/gpu_run.sh for the standard steps)
-S2='--sim-world 2 --global-batch 512 --sim-comm loopback'
 W2='--sim-world 2 --global-batch 256 --sim-comm loopback'
+W4='--sim-world 4 --global-batch 256 --sim-comm loopback'
 S8='--sim-world 8 --global-batch 256 --sim-comm loopback'
 tools/gpu_session.sh \
-  "r04g_tests|600|python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k 'reducer or ddp_two or config3 or head or bucketed'" \
-  "r04g_ab|1000|tools/bench_ab.sh 3 'base|' 'sim2|$S2' 'sim2r|$S2 --opt graphs=1' 'w2|$W2' 'w2old|$W2 --opt comm_on_side=0' 'w8|$S8' 'w8old|$S8 --opt comm_on_side=0 --opt head_fused=0'" \
-  "r04g_bench|300|python bench.py --gpus 1 --steps 50 --warmup 10 > gpurun_out/r04g_bench.json"
+  "r04h_ab|1000|tools/bench_ab.sh 3 'w2|$W2' 'w2e|$W2 --opt graphs=2' 'w4|$W4' 'w4e|$W4 --opt graphs=2' 'w8|$S8' 'w8e|$S8 --opt graphs=2'" \
+  "r04h_cb32|300|python tools/conv_bench.py --batch 32 --passes fwd,dgrad --layers l2,l3,l4,l3.0.c1,l4.0.c1 --variants 'halo_split=0;halo_split=1' > gpurun_out/r04h_cb32.txt" \
+  "r04h_w8prof|300|tools/prof_run.sh r04h_w8 $S8"
