@@ -81,9 +81,13 @@ def spawn_ranks(n: int, argv: list, script: str = None, poll_s: float = 0.2) -> 
 
 
 def init_dist(gpus: int = 1):
-    if "RANK" not in os.environ:
-        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                          MASTER_PORT=str(_free_port()))
+    if "RANK" not in os.environ:  # one rank, no launcher: an in-process store (no TCP port to race for)
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0), store=dist.HashStore(), rank=0,
+                                world_size=1)
+        check_world(dist.get_world_size(), gpus)
+        return 0, 1, 0
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)

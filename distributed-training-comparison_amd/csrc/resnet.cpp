@@ -519,10 +519,12 @@ constexpr int64_t kEagerBwdMinPixels = 192ll * 32 * 32;
 static bool graphs_on(Net& n, bool bwd, bool comm = false) {
   const int g = option_get(OPT_GRAPHS);
   if (n.capture || n.sync || g == 0 || (g == 2 && bwd) || (g == 3 && !bwd)) return false;
-  // (with a communicator too once its bucket collectives ride the weight-gradient stream, option comm_on_side:
-  // 125.5k vs 117.8k img/s at batch 256 per rank, loopback A/B r04f; the N=1 step without one: 129.1k)
-  if (g == 4 && bwd && (!comm || option_get(OPT_COMM_ON_SIDE) != 0) && (int64_t)n.B * n.H * n.W >= kEagerBwdMinPixels)
-    return false;
+  // With a communicator whose bucket collectives ride the weight-gradient stream (option comm_on_side) the
+  // backward is eager at every batch: loopback A/B r04g / r04h, per-rank images/s replayed -> eager: batch 256
+  // 116.1k -> 125.9k, 128 78.3k -> 87.7k, 64 49.5k -> 57.0k, 32 27.0k -> 31.1k (four segment-graph launches
+  // per step cost the host more than ~90 eager launches do)
+  if (g == 4 && bwd && comm && option_get(OPT_COMM_ON_SIDE) != 0) return false;
+  if (g == 4 && bwd && !comm && (int64_t)n.B * n.H * n.W >= kEagerBwdMinPixels) return false;
   if (n.graph_epoch != option_epoch()) {  // options are baked into captured launches
     drop_graphs(n);
     n.graph_epoch = option_epoch();
