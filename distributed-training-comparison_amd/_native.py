@@ -81,6 +81,7 @@ _SIGS = {
     "dtc_head_bwd_workspace_size": (sz, [i32, i32, i32]),
     "dtc_head_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, sz, vp]),
     "dtc_xent_fwd": (i32, [vp, vp, i32, i32, vp, vp, vp]),
+    "dtc_xent_fwd_ex": (i32, [vp, vp, i32, i32, vp, vp, vp, vp, vp, vp]),
     "dtc_xent_bwd": (i32, [vp, vp, vp, vp, i32, i32, vp, vp]),
     "dtc_sgd_nesterov_flat": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, vp, vp, vp]),
     "dtc_cast_f32_bf16": (i32, [vp, vp, i64, vp]),

@@ -326,6 +326,10 @@ int dtc_head_bwd(const float* dlogits, const float* feat, const uint16_t* wfc, i
 int dtc_xent_fwd(const float* logits, const int64_t* labels, int n, int ncls, float* loss, float* lse, void* stream) {
   return xent_fwd(logits, labels, n, ncls, loss, lse, S(stream));
 }
+int dtc_xent_fwd_ex(const float* logits, const int64_t* labels, int n, int ncls, float* loss, float* lse,
+                    const float* scale, float* scaled, float* host_loss, void* stream) {
+  GUARD(return xent_fwd_fused(logits, labels, n, ncls, loss, lse, scale, scaled, host_loss, S(stream));)
+}
 int dtc_xent_bwd(const float* logits, const int64_t* labels, const float* lse, const float* gscale, int n, int ncls,
                  float* dlogits, void* stream) {
   return xent_bwd(logits, labels, lse, gscale, n, ncls, dlogits, S(stream));

@@ -203,6 +203,63 @@ int xent_fwd(const float* logits, const int64_t* labels, int N, int ncls, float*
   return 0;
 }
 
+// The training step's loss in ONE launch (one 1024-thread workgroup, N <= XF_MAX_ROWS): the per-row
+// log-sum-exp exactly as xent_lse_kernel computes it (a wave per row), the mean exactly as xent_mean_kernel
+// sums it (same lanes, same order: bit-identical loss), then loss x scale (GradScaler.scale, amp_scale's
+// multiply) and the loss stored into a pinned host word (the item() value: no copy launch). Replaces
+// xent_lse + xent_mean + a device-to-host copy + amp_scale on the path to the per-step barrier.
+constexpr int XF_MAX_ROWS = 4096;
+__global__ void __launch_bounds__(1024) xent_fwd_fused_kernel(const float* __restrict__ logits,
+                                                             const int64_t* __restrict__ labels, int N, int ncls,
+                                                             float* __restrict__ loss, float* __restrict__ lse,
+                                                             const float* __restrict__ scale, float* __restrict__ scaled,
+                                                             float* host) {
+  __shared__ float slse[XF_MAX_ROWS];
+  __shared__ float part[4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  for (int b = wave; b < N; b += 16) {
+    const float* z = logits + (int64_t)b * ncls;
+    float m = -INFINITY;
+    for (int j = lane; j < ncls; j += 64) m = fmaxf(m, z[j]);
+    m = wave_max(m);
+    float s = 0.f;
+    for (int j = lane; j < ncls; j += 64) s += expf(z[j] - m);
+    s = wave_sum(s);
+    if (lane == 0) {
+      const float v = m + logf(s);
+      lse[b] = v;
+      slse[b] = v;
+    }
+  }
+  __syncthreads();
+  if (t < 256) {
+    float acc = 0.f;
+    for (int b = t; b < N; b += 256) {
+      const int64_t y = labels[b];
+      acc += (y >= 0 && y < ncls) ? (slse[b] - logits[(int64_t)b * ncls + y]) : NAN;
+    }
+    acc = wave_sum(acc);
+    if ((t & 63) == 0) part[t >> 6] = acc;
+  }
+  __syncthreads();
+  if (t == 0) {
+    const float l = (part[0] + part[1] + part[2] + part[3]) / (float)N;
+    *loss = l;
+    if (scaled) *scaled = l * *scale;
+    if (host) *host = l;
+  }
+}
+
+int xent_fwd_fused(const float* logits, const int64_t* labels, int N, int ncls, float* loss, float* lse,
+                   const float* scale, float* scaled, float* host, hipStream_t st) {
+  DTC_CHECK_ARG(logits && labels && loss && lse && N > 0 && N <= XF_MAX_ROWS && ncls > 0 && (!scaled || scale),
+                "xent_fwd_fused: bad args (N=%d)", N);
+  hipLaunchKernelGGL(xent_fwd_fused_kernel, dim3(1), dim3(1024), 0, st, logits, labels, N, ncls, loss, lse, scale,
+                     scaled, host);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 __global__ void __launch_bounds__(256) xent_bwd_kernel(const float* __restrict__ logits,
                                                       const int64_t* __restrict__ labels,
                                                       const float* __restrict__ lse, const float* __restrict__ gscale,

@@ -289,6 +289,9 @@ int wgrad_reduce_to(const float* slab, int splits, int K, int RSC, int ncols, in
 int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st);
 // mean cross entropy; lse per row
+// the same plus loss * (*scale) into `scaled` and the loss into the host word `host` (optional), one launch
+int xent_fwd_fused(const float* logits, const int64_t* labels, int N, int ncls, float* loss, float* lse,
+                   const float* scale, float* scaled, float* host, hipStream_t st);
 int xent_fwd(const float* logits, const int64_t* labels, int N, int ncls, float* loss, float* lse,
              hipStream_t st);
 // dlogits = (softmax - onehot) * (*gscale) / N

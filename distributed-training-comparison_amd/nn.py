@@ -242,10 +242,54 @@ class _NetFn(torch.autograd.Function):
         return None, None, None, None
 
 
+# (scale tensor or None, scaled-loss output or None, pinned host word) for the next _XentFn.forward: the
+# training step's loss, scaled loss and host copy in one launch (dtc_xent_fwd_ex)
+_XENT_EXTRA = [None]
+
+
+class _HostWords:
+    """A ring of pinned host words the loss launch writes its value into (the item() read). The ring is
+    owned here, not by torch's pinned-memory cache: a word a kernel may still write is never handed to
+    another tensor. Reusing a slot first waits for the event of the step that last wrote it."""
+
+    N = 256
+
+    def __init__(self):
+        self.buf = torch.empty(self.N, dtype=torch.float32, pin_memory=True)
+        self.events = [None] * self.N
+        self.i = 0
+        self.mu = threading.Lock()  # rank threads of the thread-group communicator share the ring
+
+    def take(self):
+        with self.mu:
+            k = self.i % self.N
+            self.i += 1
+            ev = self.events[k]
+            self.events[k] = None
+        if ev is not None:
+            ev.synchronize()
+        return k, self.buf[k]
+
+    def done(self, k, ev):
+        self.events[k] = ev
+
+
+_HOST_WORDS: List[Optional[_HostWords]] = [None]
+
+
 class _XentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels):
-        loss, lse = ops.xent_fwd(logits, labels)
+        extra = _XENT_EXTRA[0]
+        if extra is not None:
+            scale, scaled, host = extra
+            n, ncls = logits.shape
+            loss = torch.empty((), dtype=torch.float32, device=logits.device)
+            lse = torch.empty(n, dtype=torch.float32, device=logits.device)
+            call("dtc_xent_fwd_ex", ptr(logits), ptr(labels), n, ncls, ptr(loss), ptr(lse), ptr(scale), ptr(scaled),
+                 host.data_ptr(), stream_ptr())
+        else:
+            loss, lse = ops.xent_fwd(logits, labels)
         ctx.save_for_backward(logits, labels, lse)
         ctx.lse = lse
         return loss
@@ -335,18 +379,27 @@ def _wrap_loss(value: torch.Tensor, graph_fn, fast, host_copy: bool = False) -> 
 _PRESCALER = [None]
 
 
-def prescale(loss: "NativeLoss") -> None:
-    """Enqueue loss * scale AND build its NativeLoss wrapper now, while the GPU is busy with the
-    forward: scaler.scale(loss) after the per-step barrier then only looks it up (the wrapper's
-    Tensor._make_subclass and closures cost 10-30 us of host time, all of it GPU idle time there)."""
+def _prescaler():
+    """The live GradScaler whose scale the loss kernel's call pre-multiplies, or None."""
     ref = _PRESCALER[0]
     sc = ref() if ref is not None else None
     if sc is None or sc._scale is None or not sc._enabled:
+        return None
+    return sc
+
+
+def prescale(loss: "NativeLoss", scaled: Optional[torch.Tensor] = None, sc=None) -> None:
+    """Enqueue loss * scale AND build its NativeLoss wrapper now, while the GPU is busy with the
+    forward: scaler.scale(loss) after the per-step barrier then only looks it up (the wrapper's
+    Tensor._make_subclass and closures cost 10-30 us of host time, all of it GPU idle time there).
+    `scaled`: the product already computed by the loss launch (dtc_xent_fwd_ex) for scaler `sc`."""
+    sc = sc if scaled is not None else _prescaler()
+    if sc is None:
         return
     scale = sc._scale
     f = loss._dtc_fast
-    wrapped = _wrap_loss(ops.amp_scale(loss.detach(), scale), lambda: loss._dtc_graph * scale,
-                         None if f is None else (f[0], f[1], f[2], f[3], scale))
+    wrapped = _wrap_loss(scaled if scaled is not None else ops.amp_scale(loss.detach(), scale),
+                         lambda: loss._dtc_graph * scale, None if f is None else (f[0], f[1], f[2], f[3], scale))
     loss._dtc_prescaled = (wrapped, scale, sc._version)
 
 
@@ -376,16 +429,35 @@ class CrossEntropyLoss(nn.Module):
             logits = logits.float()
         logits = logits.contiguous()
         labels = labels.long().contiguous()
-        loss = _XentFn.apply(logits, labels)
         node = logits.grad_fn
         if torch.is_grad_enabled() and node is not None:
             from .parallel import _DPFn
 
             if isinstance(node, (_NetFn._backward_cls, _DPFn._backward_cls)):
+                if logits.shape[0] <= 4096:  # loss + scaled loss + host copy: one launch
+                    sc = _prescaler()
+                    if _HOST_WORDS[0] is None:
+                        _HOST_WORDS[0] = _HostWords()
+                    slot, host = _HOST_WORDS[0].take()
+                    scaled = torch.empty((), dtype=torch.float32, device=logits.device) if sc is not None else None
+                    _XENT_EXTRA[0] = (sc._scale if sc is not None else None, scaled, host)
+                    try:
+                        loss = _XentFn.apply(logits, labels)
+                    finally:
+                        _XENT_EXTRA[0] = None
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    _HOST_WORDS[0].done(slot, ev)
+                    out = _wrap_loss(loss, lambda: loss, (node, logits, labels, loss.grad_fn.lse, None))
+                    out._dtc_host = (host, ev)
+                    if sc is not None:
+                        prescale(out, scaled, sc)
+                    return out
+                loss = _XentFn.apply(logits, labels)
                 out = _wrap_loss(loss, lambda: loss, (node, logits, labels, loss.grad_fn.lse, None), host_copy=True)
                 prescale(out)
                 return out
-        return loss
+        return _XentFn.apply(logits, labels)
 
 
 # ----------------------------------------------------------------------------- modules

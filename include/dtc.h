@@ -154,6 +154,11 @@ int dtc_head_bwd(const float* dlogits, const float* feat, const uint16_t* wfc, i
                  float scale, float* dw, float* db, uint16_t* dact, void* ws, size_t ws_bytes, void* stream);
 int dtc_xent_fwd(const float* logits, const int64_t* labels, int n, int ncls, float* loss, float* lse,
                  void* stream);
+/* The training step's loss in one launch (n <= 4096): loss and lse as dtc_xent_fwd (bit-identical), plus
+ * scaled = loss * (*scale) when scaled != NULL (GradScaler.scale) and the loss stored into host_loss (a
+ * pinned, device-accessible host word; NULL = none) -- read after an event recorded behind the launch. */
+int dtc_xent_fwd_ex(const float* logits, const int64_t* labels, int n, int ncls, float* loss, float* lse,
+                    const float* scale, float* scaled, float* host_loss, void* stream);
 int dtc_xent_bwd(const float* logits, const int64_t* labels, const float* lse, const float* gscale, int n, int ncls,
                  float* dlogits, void* stream);
 

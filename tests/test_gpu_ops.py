@@ -332,6 +332,36 @@ def _head_and_loss(dtc, cuda):
     assert rel_err(dact.float().cpu().numpy(), dact_ref) < 1e-2
 
 
+@pytest.mark.parametrize("n", [1, 6, 256, 300, 4096])
+def test_xent_fwd_one_launch(dtc, cuda, n):
+    """dtc_xent_fwd_ex (the training step's loss in one launch): loss and lse bit-identical to the
+    two-kernel dtc_xent_fwd, scaled = loss * scale (amp_scale's multiply), the loss in a pinned host word;
+    and against the oracle."""
+    g = torch.Generator(device=cuda).manual_seed(n)
+    logits = torch.randn(n, 100, device=cuda, generator=g) * 3
+    lab = torch.randint(0, 100, (n,), device=cuda, generator=g)
+    loss0, lse0 = dtc.ops.xent_fwd(logits, lab)
+    scale = torch.full((), 65536.0, device=cuda)
+    loss = torch.empty((), device=cuda)
+    lse = torch.empty(n, device=cuda)
+    scaled = torch.empty((), device=cuda)
+    host = torch.full((4,), -1.0).pin_memory()
+    P = dtc._native.ptr
+    dtc._native.call("dtc_xent_fwd_ex", P(logits), P(lab), n, 100, P(loss), P(lse), P(scale), P(scaled),
+                     host[1:2].data_ptr(), dtc._native.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss0) and torch.equal(lse, lse0)
+    assert float(scaled) == float(loss) * 65536.0
+    assert float(host[1]) == float(loss) and float(host[0]) == -1.0 and float(host[2]) == -1.0
+    loss_ref, _, lse_ref = O.cross_entropy(logits.cpu().numpy(), lab.cpu().numpy())
+    assert abs(float(loss) - loss_ref) < 1e-5 * max(1.0, abs(loss_ref))
+    # without the optional outputs
+    dtc._native.call("dtc_xent_fwd_ex", P(logits), P(lab), n, 100, P(loss), P(lse), None, None, None,
+                     dtc._native.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss0)
+
+
 def test_stem_im2col(dtc, cuda):
     g = np.random.default_rng(8)
     x = g.standard_normal((2, 3, 6, 5)).astype(np.float32)
