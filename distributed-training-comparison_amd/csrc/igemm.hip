@@ -937,7 +937,9 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
   DTC_CHECK_ARG(!res_compact || (res && dgrad_class_mode(s) && !conv_c64_ok(s)),
                 "conv_dgrad: a compact residual needs the stride-2 parity-class path");
   // bit 0: c64, 1: halo, 2: split-K reduce; mask-bit sources (bnb->mb, option bnb_mask) fuse everywhere
-  const int fz = bnb != nullptr ? (bnb->mb ? 7 : option_get(OPT_BNB_FUSE)) : 0;
+  // (bnb_mask=1) or in the halo and split-K epilogues only (2: the persistent layer1 kernel's strided
+  // epilogue costs more than the separate reduction it saves)
+  const int fz = bnb != nullptr ? (bnb->mb ? (option_get(OPT_BNB_MASK) == 2 ? 6 : 7) : option_get(OPT_BNB_FUSE)) : 0;
   const HaloPlan hp = conv_c64_ok(s) ? HaloPlan{-1, 0} : conv_halo_plan(s, CONV_DGRAD);
   const int kind = conv_c64_ok(s) ? 1 : (hp.cfg >= 0 ? 2 : 4);
   const bool split_path = kind != 1 && (kind == 4 || hp.split > 1);  // the epilogue is splitk_reduce's

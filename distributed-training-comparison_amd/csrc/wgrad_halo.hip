@@ -106,8 +106,14 @@ struct WgStage {
 
 // NS: pipeline stages in the LDS ring (2: wait for the next step's DMA at every step; 4: three
 // steps of DMA in flight, a counted s_waitcnt per step). NR: halo DMA rounds per step.
-template <int NS, int NR, int ST = 1, bool SC = false, bool GEN = false>
+// KL: wave layout. 0: 4 waves along the 576 rows x 2 along the 64 output channels, each wave both
+// 32-pixel halves of a step (9 A + 2 B fragment reads per 18 MFMAs). 1 (option wgrad_ksplit): 4 along
+// the rows x 2 along the step's pixels -- each wave all 64 channels of one 32-pixel half (9 A + 4 B
+// reads per 36 MFMAs: 41% fewer LDS reads per MFMA); the two halves' sums are added through LDS after
+// the loop (acc(half 0) + acc(half 1): one fixed order).
+template <int NS, int NR, int ST = 1, bool SC = false, bool GEN = false, int KL = 0>
 __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
+  static_assert(KL == 0 || !SC, "wgrad_ksplit: stride-1 kernels only");
   typedef WgStage<NR, SC> SG;
   constexpr int PER = NR + 1 + (SC ? 1 : 0);  // LDS-DMA instructions per wave per stage (halo rounds + dy (+ dsc))
   static_assert(!SC || ST == 2, "shortcut fusion: stride 2");
@@ -220,20 +226,22 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     return (tap / 3) * W2 + (ST == 1 ? ts : (ts & 1) * p.hwh + (ts >> 1));
   };
 
-  const int wm = wave >> 1, wn = wave & 1;
-  f32x4 acc[9][2];
+  const int wm = wave >> 1, wn = wave & 1;  // KL = 1: wn is the wave's 32-pixel half of the step
+  constexpr int NJ = KL ? 4 : 2;             // B fragments (16 output channels each) per wave
+  f32x4 acc[9][NJ];
 #pragma unroll
   for (int i = 0; i < 9; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // Per-lane LDS byte offsets (within a stage) of every fragment half a step reads, computed once:
   // A = the x halo read transposed at each tap's shift, B = the dy tile read transposed. The step
   // loop is unrolled by NS so each stage base is a constant the ds_read offset field absorbs: the
   // MFMA stream carries no address arithmetic.
-  uint32_t aoff[2][9][2], boff[2][2][2];
+  constexpr int NKS = KL ? 1 : 2;  // 32-pixel halves a wave computes (KL = 1: its own, at index 0)
+  uint32_t aoff[NKS][9][2], boff[NKS][NJ][2];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
+  for (int ks = 0; ks < NKS; ++ks) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
       const int row = wm * 144 + i * 16;  // GEMM row = tap*64 + channel
@@ -242,19 +250,19 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       const int unit = (cin >> 2) + (lane & 3);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int ra = hm[ks][h] + toff;
+        const int ra = hm[KL ? wn : ks][h] + toff;
         const int f = wg_uswz(ra);
         aoff[ks][i][h] = (uint32_t)(ra * 128 + ((unit ^ f) << 3));
       }
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int cin = wn * 32 + j * 16;
+    for (int j = 0; j < NJ; ++j) {
+      const int cin = KL ? j * 16 : wn * 32 + j * 16;
       const int li = lane & 15, q = li >> 2, pp = li & 3, g = lane >> 4;
       const int unit = (cin >> 2) + pp;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int kr = wg_pixel(ks, g, h, q);
+        const int kr = wg_pixel(KL ? wn : ks, g, h, q);
         const int f = wg_uswz(kr);
         boff[ks][j][h] = (uint32_t)(SG::HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
       }
@@ -280,15 +288,15 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   };
   auto compute = [&](const char* sb) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 bfr[2];
+    for (int ks = 0; ks < NKS; ++ks) {
+      bf16x8 bfr[NJ];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
+      for (int j = 0; j < NJ; ++j) bfr[j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
 #pragma unroll
       for (int i = 0; i < 9; ++i) {
         const bf16x8 af = tr8(sb, aoff[ks][i][0], aoff[ks][i][1]);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
       }
       if constexpr (SC) {  // the shortcut: centre-tap A fragment x the dsc tile's B fragments
         const bf16x8 af = tr8(sb, aoff_sc[ks][0], aoff_sc[ks][1]);
@@ -332,6 +340,38 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   float* const slab = p.direct ? uniform_ptr(z == 0 ? p.dws[0] : z == 1 ? p.dws[1] : z == 2 ? p.dws[2] : p.dws[3])
                                : p.slab + z * p.slab_stride + (size_t)split * p.K * RSC;
   const float osc = p.direct ? p.scale : 1.f;
+  if constexpr (KL == 1) {
+    // the two pixel halves' sums: each wave finalises two of its four column fragments (half 0 the
+    // first two, half 1 the last two), receiving the other half's partials through LDS in two rounds
+    // of fragments (rows i < 5, then i >= 5: 10 / 8 KB per wave). The ring is free after a barrier.
+    __syncthreads();
+    f32x4* const xb = (f32x4*)smem;
+#pragma unroll
+    for (int rnd = 0; rnd < 2; ++rnd) {
+      const int i0 = rnd ? 5 : 0, i1 = rnd ? 9 : 5;
+#pragma unroll
+      for (int i = i0; i < i1; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)  // send the fragments the partner wave finalises
+          xb[((wave * 10 + (i - i0) * 2 + jj) << 6) + lane] = acc[i][(wn ? 0 : 2) + jj];
+      __syncthreads();
+#pragma unroll
+      for (int i = i0; i < i1; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int j = (wn ? 2 : 0) + jj;
+          const f32x4 o = xb[(((wave ^ 1) * 10 + (i - i0) * 2 + jj) << 6) + lane];
+          const f32x4 v = wn ? o + acc[i][j] : acc[i][j] + o;  // half 0 + half 1
+          const int row = wm * 144 + i * 16 + 4 * (lane >> 4);
+          const int rsc = (row >> 6) * p.C + c0 + (row & 63);
+          const int kout = k0 + j * 16 + (lane & 15);
+          *(f32x4*)(slab + (size_t)kout * RSC + rsc) = v * osc;
+        }
+      __syncthreads();
+    }
+    stamp_end(p.ts);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int row = wm * 144 + i * 16 + 4 * (lane >> 4);
@@ -457,13 +497,18 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   dim3 grid((s.C / 64) * (s.K / 64), used, nprob);
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
   // 4-stage LDS ring (three steps of DMA in flight), compiler-scheduled fragment reads
+  const bool kl = option_get(OPT_WGRAD_KSPLIT) != 0;
+#define DTC_WGH(NR_, GEN_)                                                                                    \
+  if (kl) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 1>), grid, dim3(512), 0, st, p);     \
+  else hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 0>), grid, dim3(512), 0, st, p)
   if (g.gen) {  // general geometry
-    if (nr <= 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, 2, 1, false, true>), grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((wgrad_halo_kernel<4, 3, 1, false, true>), grid, dim3(512), 0, st, p);
+    if (nr <= 2) { DTC_WGH(2, true); }
+    else { DTC_WGH(3, true); }
   } else {
-    if (nr <= 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, 2>), grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((wgrad_halo_kernel<4, 3>), grid, dim3(512), 0, st, p);
+    if (nr <= 2) { DTC_WGH(2, false); }
+    else { DTC_WGH(3, false); }
   }
+#undef DTC_WGH
   DTC_LAUNCH_CHECK();
   *used_splits = p.direct ? 0 : used;
   return 0;

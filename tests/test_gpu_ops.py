@@ -468,22 +468,26 @@ def test_amp_check_finite_positions(dtc, cuda, n):
     (2, 6, 96, 64, 64),     # 32-pixel segments
     (1, 5, 40, 64, 64),     # one 40-pixel row per step (24 padded slots)
 ])
-def test_conv_wgrad_halo(dtc, cuda, case):
+@pytest.mark.parametrize("ksplit", [0, 1])
+def test_conv_wgrad_halo(dtc, cuda, case, ksplit):
     """Halo-tiled 3x3 weight gradient == generic loader == oracle (fp32 sums of exact products); the rows
     wider than 64 pixels or not dividing 64 run the general-geometry kernels (per-step 64-bit bases, zero-dy
-    padded slots), which must match too."""
+    padded slots), which must match too. ksplit: option wgrad_ksplit (the waves split each step's pixels,
+    the two halves' sums added after the loop)."""
     N, H, W, C, K = case
     g = np.random.default_rng(7)
     x = _rand_bf16((N, H, W, C), g)
     dy = _rand_bf16((N, H, W, K), g)
     xd, dyd = _to_dev_bf16(x, cuda), _to_dev_bf16(dy, cuda)
     ref = O.conv2d_wgrad(x, dy, 3, 3, 1, 1)
-    halo = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
-    dtc._native.lib.dtc_set_option(b"wgrad_halo", 0)
     try:
+        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", ksplit)
+        halo = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
+        dtc._native.lib.dtc_set_option(b"wgrad_halo", 0)
         generic = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
     finally:
         dtc._native.lib.dtc_set_option(b"wgrad_halo", 256)
+        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", 0)
     assert rel_err(halo, ref) < 1e-5
     assert rel_err(generic, ref) < 1e-5
 
@@ -497,21 +501,27 @@ def test_conv_wgrad_halo(dtc, cuda, case):
     (2, 8, 224, 64, 64, 4),    # general geometry (56-pixel row segments), the 224x224 layer1 batch
     (2, 14, 28, 128, 128, 3),  # general geometry, two 28-pixel rows per step
 ])
-def test_conv_wgrad_batch(dtc, cuda, case):
+@pytest.mark.parametrize("ksplit", [0, 1])
+def test_conv_wgrad_batch(dtc, cuda, case, ksplit):
     """dtc_conv2d_wgrad_batch: n independent weight gradients in one halo launch (blockIdx.z =
     problem, 1/n of the splits each) + one reduce launch == the oracle per problem, and == the
-    one-by-one dtc_conv2d_wgrad to fp32 summation order (different split counts)."""
+    one-by-one dtc_conv2d_wgrad to fp32 summation order (different split counts); both wave layouts."""
     N, H, W, C, K, n = case
     g = np.random.default_rng(11)
     xs = [_rand_bf16((N, H, W, C), g) for _ in range(n)]
     dys = [_rand_bf16((N, H, W, K), g) for _ in range(n)]
     xd = [_to_dev_bf16(a, cuda) for a in xs]
     dyd = [_to_dev_bf16(a, cuda) for a in dys]
-    got = dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.25)
+    try:
+        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", ksplit)
+        got = dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.25)
+        ones = [dtc.ops.conv2d_wgrad(xd[i], dyd[i], 3, 3, 1, 1, scale=0.25).cpu().numpy() for i in range(n)]
+    finally:
+        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", 0)
     assert len(got) == n
     for i in range(n):
         ref = 0.25 * O.conv2d_wgrad(xs[i], dys[i], 3, 3, 1, 1)
-        one = dtc.ops.conv2d_wgrad(xd[i], dyd[i], 3, 3, 1, 1, scale=0.25).cpu().numpy()
+        one = ones[i]
         assert rel_err(got[i].cpu().numpy(), ref) < 1e-5, i
         assert rel_err(got[i].cpu().numpy(), one) < 1e-6, i
 

@@ -668,22 +668,25 @@ def test_shortcut_fused_forward_matches_separate(dtc, cuda, level):
                     assert np.isfinite(gb[rep]).all() and rel_err(gb[rep], ga[rep]) < 1e-2, rel_err(gb[rep], ga[rep])
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("batch,hw", [(8, 32), (64, 32), (256, 32), (8, 8)])
-def test_bn_sums_in_dgrad_epilogues_match_reduce_pass(dtc, cuda, batch, hw):
+def test_bn_sums_in_dgrad_epilogues_match_reduce_pass(dtc, cuda, batch, hw, mode):
     """Option bnb_mask: every BN's backward sums (sum dz, sum dz * xhat) accumulated in the epilogue of the
     dgrad producing its gradient (conv_c64 / conv_halo / split-K reduce; the stride-2 class dgrads keep a
     separate mask-bit pass) from the forward's ReLU mask bits, vs the separate reduction kernels. Same
     values summed over other fp32 partials (the dgrad tiles instead of the reduction's slices): what the
     backward computes before the first fused BN (linear, layer4.1's conv2 and bn2) agrees to 1e-5, every
     other gradient to 1e-2 (last-bit BN-coefficient differences flip bf16 roundings of the data
-    gradients, which propagate -- a wrong sum would be off by O(1)); graphs on and off, finite."""
+    gradients, which propagate -- a wrong sum would be off by O(1)); graphs on and off, finite. Mode 2
+    fuses in the halo and split-K epilogues only (the persistent layer1 kernel's BNs keep the separate
+    mask-bit pass, after the dgrad)."""
     lib = dtc._native.lib
     lay = dtc.nn.Layout(100, 25.0)
     for graphs in (1, 0):
         try:
             lib.dtc_set_option(b"bnb_mask", 0)
             ga = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
-            lib.dtc_set_option(b"bnb_mask", 1)
+            lib.dtc_set_option(b"bnb_mask", mode)
             gb = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
         finally:
             lib.dtc_set_option(b"bnb_mask", 0)

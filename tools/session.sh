@@ -1,7 +1,6 @@
 # scratch GPU session (overwritten per session; see tools/gpu_run.sh for the standard steps)
-S8='--sim-world 8 --global-batch 256 --sim-comm loopback'
 tools/gpu_session.sh \
-  "r04i_tests|900|python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
-  "r04i_ab|900|tools/bench_ab.sh 3 'b64|--batch 64' 'b64e|--batch 64 --opt graphs=2' 'b128|--batch 128' 'b128e|--batch 128 --opt graphs=2' 'w8|$S8'" \
-  "r04i_w8prof|300|tools/prof_run.sh r04i_w8 $S8" \
-  "r04i_bench|300|python bench.py --gpus 1 --steps 50 --warmup 10 > gpurun_out/r04i_bench.json"
+  "r04j_tests|600|python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
+  "r04j_wgb|150|python tools/wgrad_bench.py --variants 'wgrad_ksplit=0;wgrad_ksplit=1' --check" \
+  "r04j_ab|600|tools/bench_ab.sh 3 'base|' 'ks1|--opt wgrad_ksplit=1' 'bnm2|--opt bnb_mask=2' 'bnm2s|--opt bnb_mask=2 --opt halo_stage_epi=1' 'b64|--batch 64' 'b64e|--batch 64 --opt graphs=2'" \
+  "r04j_bench|200|python bench.py --gpus 1 --steps 50 --warmup 10 > gpurun_out/r04j_bench.json"
