@@ -509,22 +509,18 @@ static int graph_launch(Net& n, hipGraphExec_t ex, hipStream_t st) {
   return 0;
 }
 // option graphs: 0 = eager launches, 1 = forward and backward replayed from hipGraphs, 2 = forward only,
-// 3 = backward only, 4 (default) = the forward always, the backward where its eager launches would make
-// the host the bottleneck: with a communicator (its per-bucket collectives are host-issued) or below
-// kEagerBwdMinPixels per batch. Measured (tools/bench_ab.sh, one MI355X): without a communicator the
-// replayed backward is 4-5% slower than eager launches at batch 192-256 (its cross-stream edges cost more
-// than the launches the host has time for), with one it is 27% faster at batch 256 (`bwd`: which segment
-// asks; `comm`: the backward has a communicator)
-constexpr int64_t kEagerBwdMinPixels = 192ll * 32 * 32;
+// 3 = backward only, 4 (default) = the forward replayed, the backward eager -- except with a communicator
+// whose bucket collectives run on a stream of their own (comm_on_side=0: segment graphs, host-issued
+// collectives between them). Measured (tools/bench_ab.sh, one MI355X, images/s, replayed -> eager
+// backward): no communicator, batch 256 +4-5% (r03), batch 64 52.8k -> 59.9k (r04j); with a communicator
+// on the weight-gradient stream (loopback, r04g / r04h) batch 256 116.1k -> 125.9k, 128 78.3k -> 87.7k,
+// 64 49.5k -> 57.0k, 32 27.0k -> 31.1k: the replay's cross-stream edges and per-segment graph launches
+// cost more than the ~90 eager launches the host issues ahead of the GPU (`bwd`: which segment asks;
+// `comm`: the backward has a communicator)
 static bool graphs_on(Net& n, bool bwd, bool comm = false) {
   const int g = option_get(OPT_GRAPHS);
   if (n.capture || n.sync || g == 0 || (g == 2 && bwd) || (g == 3 && !bwd)) return false;
-  // With a communicator whose bucket collectives ride the weight-gradient stream (option comm_on_side) the
-  // backward is eager at every batch: loopback A/B r04g / r04h, per-rank images/s replayed -> eager: batch 256
-  // 116.1k -> 125.9k, 128 78.3k -> 87.7k, 64 49.5k -> 57.0k, 32 27.0k -> 31.1k (four segment-graph launches
-  // per step cost the host more than ~90 eager launches do)
-  if (g == 4 && bwd && comm && option_get(OPT_COMM_ON_SIDE) != 0) return false;
-  if (g == 4 && bwd && !comm && (int64_t)n.B * n.H * n.W >= kEagerBwdMinPixels) return false;
+  if (g == 4 && bwd && !(comm && option_get(OPT_COMM_ON_SIDE) == 0)) return false;
   if (n.graph_epoch != option_epoch()) {  // options are baked into captured launches
     drop_graphs(n);
     n.graph_epoch = option_epoch();

@@ -20,6 +20,8 @@
 // geometry (the executor defers the 3x3 wgrads of a bucket and issues them together). The chip is
 // filled by problems x splits workgroups, so each problem needs 1/P of the splits: the fp32 slab
 // written and re-read per conv -- the cost that bounds this kernel beside the MFMAs -- drops P-fold.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 #include "tile_common.h"
@@ -346,29 +348,30 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     // of fragments (rows i < 5, then i >= 5: 10 / 8 KB per wave). The ring is free after a barrier.
     __syncthreads();
     f32x4* const xb = (f32x4*)smem;
-#pragma unroll
-    for (int rnd = 0; rnd < 2; ++rnd) {
-      const int i0 = rnd ? 5 : 0, i1 = rnd ? 9 : 5;
+    // (fragment rows as template constants: a runtime row index would put acc in scratch memory)
+    auto xround = [&](auto i0c, auto i1c) {
+      constexpr int i0 = decltype(i0c)::value, i1 = decltype(i1c)::value;
 #pragma unroll
       for (int i = i0; i < i1; ++i)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)  // send the fragments the partner wave finalises
-          xb[((wave * 10 + (i - i0) * 2 + jj) << 6) + lane] = acc[i][(wn ? 0 : 2) + jj];
+          xb[((wave * 10 + (i - i0) * 2 + jj) << 6) + lane] = wn ? acc[i][jj] : acc[i][2 + jj];
       __syncthreads();
 #pragma unroll
       for (int i = i0; i < i1; ++i)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
-          const int j = (wn ? 2 : 0) + jj;
           const f32x4 o = xb[(((wave ^ 1) * 10 + (i - i0) * 2 + jj) << 6) + lane];
-          const f32x4 v = wn ? o + acc[i][j] : acc[i][j] + o;  // half 0 + half 1
+          const f32x4 v = wn ? o + acc[i][2 + jj] : acc[i][jj] + o;  // half 0 + half 1
           const int row = wm * 144 + i * 16 + 4 * (lane >> 4);
           const int rsc = (row >> 6) * p.C + c0 + (row & 63);
-          const int kout = k0 + j * 16 + (lane & 15);
+          const int kout = k0 + ((wn ? 2 : 0) + jj) * 16 + (lane & 15);
           *(f32x4*)(slab + (size_t)kout * RSC + rsc) = v * osc;
         }
       __syncthreads();
-    }
+    };
+    xround(std::integral_constant<int, 0>{}, std::integral_constant<int, 5>{});
+    xround(std::integral_constant<int, 5>{}, std::integral_constant<int, 9>{});
     stamp_end(p.ts);
     return;
   }

@@ -429,9 +429,12 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
     losses, gradients, parameters and running statistics agree to rounding. The projection shortcut's
     dgrad is computed separately in both arms (dgrad_scf=0): the fused-finalize executor would otherwise
     fold it into conv1's class-(0, 0) dgrad as one fp32 sum (one bf16 rounding of dx instead of two), a
-    legitimate 1-ulp difference that 3 steps at lr 0.1 on 8 images amplify past rtol 1e-4."""
+    legitimate 1-ulp difference that 3 steps at lr 0.1 on 8 images amplify past rtol 1e-4. For the same
+    reason both arms use the two-pass BN backward (bn_cg=0: the one-launch kernel, which needs the fused
+    finalize, groups the sums differently; see test_bn_one_launch_matches_two_pass)."""
     lib = dtc._native.lib
     lib.dtc_set_option(b"dgrad_scf", 0)
+    lib.dtc_set_option(b"bn_cg", 0)
     try:
         la, ga, pa, ba = _train_steps(dtc, cuda, 3, graphs=graphs)
         lib.dtc_set_option(b"bn_fused_fin", 0)
@@ -441,6 +444,7 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
             lib.dtc_set_option(b"bn_fused_fin", 1)
     finally:
         lib.dtc_set_option(b"dgrad_scf", 1)
+        lib.dtc_set_option(b"bn_cg", 1)
     np.testing.assert_allclose(la, lb, rtol=1e-4)
     assert rel_err(ga, gb) < 1e-3
     assert rel_err(pa, pb) < 1e-5
@@ -679,17 +683,20 @@ def test_bn_sums_in_dgrad_epilogues_match_reduce_pass(dtc, cuda, batch, hw, mode
     other gradient to 1e-2 (last-bit BN-coefficient differences flip bf16 roundings of the data
     gradients, which propagate -- a wrong sum would be off by O(1)); graphs on and off, finite. Mode 2
     fuses in the halo and split-K epilogues only (the persistent layer1 kernel's BNs keep the separate
-    mask-bit pass, after the dgrad)."""
+    mask-bit pass, after the dgrad). Both arms use the two-pass BN backward where the sums are not fused
+    (bn_cg=0: the one-launch kernel groups its sums differently again; test_bn_one_launch_matches_two_pass)."""
     lib = dtc._native.lib
     lay = dtc.nn.Layout(100, 25.0)
     for graphs in (1, 0):
         try:
+            lib.dtc_set_option(b"bn_cg", 0)
             lib.dtc_set_option(b"bnb_mask", 0)
             ga = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
             lib.dtc_set_option(b"bnb_mask", mode)
             gb = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
         finally:
             lib.dtc_set_option(b"bnb_mask", 0)
+            lib.dtc_set_option(b"bn_cg", 1)
         for rep in range(2):
             assert np.isfinite(gb[rep]).all()
             for pe in lay.params:

@@ -146,3 +146,21 @@ def test_options_registered_with_defaults(dtc):
     assert lib.dtc_set_option(b"no_such_option", 1) != 0
     for name in _REMOVED_OPTIONS:
         assert lib.dtc_set_option(name.encode(), 1) != 0, name
+
+
+def test_kernels_keep_accumulators_out_of_scratch(dtc):
+    """Every gfx950 kernel in the built library (tools/scratch_check.py reads the code objects' note
+    metadata): at most a few spilled dwords of private segment. A runtime-indexed register array (e.g. an
+    MFMA accumulator picked by a wave-dependent index) is placed in scratch instead -- hundreds of bytes per
+    lane and an order of magnitude slower (the first wgrad_ksplit build: 608 B/lane, 10x) -- and is not
+    reported as a spill by the compiler. Exempt: the 128 x 256 halo tile (a forced-option tuning
+    configuration, 1 workgroup per CU, never planned by default)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import scratch_check
+    lib = os.path.join(ROOT, "distributed-training-comparison_amd", "_lib", "libdtc_amd.so")
+    res = scratch_check.kernel_resources(lib)
+    assert len(res) > 100
+    bad = {k: v for k, v in res.items() if v[0] > 64 and "ELi128ELi256E" not in k}
+    assert not bad, bad
+    assert all(v[0] == 0 for k, v in res.items() if "wgrad_halo_kernel" in k)
