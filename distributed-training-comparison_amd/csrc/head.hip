@@ -78,10 +78,11 @@ int stem_pack_weight(const u16* w27, u16* w64, int K, hipStream_t st) {
 //   feat[n][c] = bf16(mean_p act[n][p][c])                 (avg_pool2d output is bf16 under autocast)
 //   logits[n][j] = bf16(feat[n] . W[j] + bf16(b[j]))         (bf16 linear under autocast)
 // The pool's threads own 8 channels each (16-B loads of consecutive channels, pixels split over
-// the workgroup's row groups and combined in LDS in a fixed order); for the Linear each wave takes
-// channel quarter `wave` and its lanes classes j0 + lane: an independent 8-wide FMA chain per
-// lane (no cross-lane reduction per class), the four quarter sums then added in LDS. Both
-// reductions have a fixed order: deterministic.
+// the workgroup's row groups and combined in LDS in a fixed order). For the Linear eight lanes share
+// a class row: lane r of the group reads 16-B chunks r, r + 8, ... (every load instruction covers
+// eight whole 128-B row pieces: coalesced, all of a lane's loads in flight at once), FMAs them against
+// the pooled features in LDS, and the group's partials meet in a fixed xor-shuffle tree; a wave takes
+// eight classes per pass, the workgroup 32. Both reductions have a fixed order: deterministic.
 template <typename T>
 __global__ void __launch_bounds__(256) head_fwd_kernel(const T* __restrict__ act, int HW, int C,
                                                       const T* __restrict__ wfc, const float* __restrict__ bfc,
@@ -115,27 +116,32 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const T* __restrict__ act
     feat[(int64_t)n * C + c] = f;
   }
   __syncthreads();
-  // part is free again: [4 quarters][64 classes] partial dot products per class block
-  const int q8 = tpr / 4, cb = wave * q8 * 8;  // this wave's channel quarter (C % 32 == 0)
-  for (int j0 = 0; j0 < ncls; j0 += 64) {
-    const int j = j0 + lane;
+  // Linear: class j = pass * 32 + wave * 8 + (lane >> 3); lane r = lane & 7 of its group
+  const int r8 = lane & 7, nch = C >> 3;
+  for (int j0 = 0; j0 < ncls; j0 += 32) {
+    const int j = j0 + wave * 8 + (lane >> 3);
+    const bool ok = j < ncls;
+    const T* w = wfc + (int64_t)(ok ? j : 0) * C;
     float acc = 0.f;
-    if (j < ncls) {
-      const T* w = wfc + (int64_t)j * C + cb;
-      for (int c8 = 0; c8 < q8; ++c8) {
-        float wv[8];
-        E::unpack(E::ld(w + c8 * 8), wv);
+    for (int c8 = r8; c8 < nch; c8 += 64) {  // (C > 512: further 64-chunk rounds)
+      typename E::V wv[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc += fs[cb + c8 * 8 + k] * wv[k];
+      for (int u = 0; u < 8; ++u)
+        if (c8 + 8 * u < nch) wv[u] = E::ld(w + (c8 + 8 * u) * 8);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (c8 + 8 * u >= nch) break;
+        float f[8];
+        E::unpack(wv[u], f);
+        const float* fc = fs + (c8 + 8 * u) * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += fc[k] * f[k];
       }
     }
-    part[wave * 64 + lane] = acc;
-    __syncthreads();
-    if (t < 64 && j0 + t < ncls) {
-      const float s = part[t] + part[64 + t] + part[128 + t] + part[192 + t];
-      logits[(int64_t)n * ncls + j0 + t] = E::round(s + E::round(bfc[j0 + t]));
-    }
-    __syncthreads();
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    if (ok && r8 == 0) logits[(int64_t)n * ncls + j] = E::round(acc + E::round(bfc[j]));
   }
 }
 
@@ -347,22 +353,60 @@ size_t head_bwd_workspace(int N, int C, int ncls) {
 }
 
 // dact[n][p][c] = (sum_j dl[n][j] * W[j][c]) / HW
+// dact of one image: dact[p][c] = (1/HW) sum_j dl[j] W[j][c], the same value at every pixel p (the
+// pool's backward). Wave w sums classes j = w, w + 4, ... for 8 consecutive channels per lane (16-B
+// weight loads, eight rows in flight per lane); the four wave partials are added in LDS in a fixed
+// order, and the pixel rows are stored as 16-B pieces. sm: ncls + 4 C floats.
+template <typename T>
+__device__ __forceinline__ void head_dact_image(const float* __restrict__ dln, const T* __restrict__ wfc, int HW, int C,
+                                                int ncls, T* __restrict__ o, float* sm) {
+  typedef Elt<T> E;
+  float* row = sm;
+  float* red = sm + ncls;
+  const int t = threadIdx.x, wv = t >> 6, l = t & 63, nch = C >> 3;
+  for (int j = t; j < ncls; j += 256) row[j] = dln[j];
+  __syncthreads();
+  for (int c8 = l; c8 < nch; c8 += 64) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const T* wc = wfc + c8 * 8;
+    for (int j = wv; j < ncls; j += 32) {
+      typename E::V w8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (j + 4 * u < ncls) w8[u] = E::ld(wc + (int64_t)(j + 4 * u) * C);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (j + 4 * u >= ncls) break;
+        float f[8];
+        E::unpack(w8[u], f);
+        const float d = row[j + 4 * u];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += d * f[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[wv * C + c8 * 8 + k] = s[k];
+  }
+  __syncthreads();
+  const float inv = 1.f / (float)HW;
+  for (int idx = t; idx < HW * nch; idx += 256) {
+    const int p = idx / nch, c8 = idx - p * nch;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c8 * 8 + k;
+      v[k] = (((red[c] + red[C + c]) + red[2 * C + c]) + red[3 * C + c]) * inv;
+    }
+    E::st(o + (int64_t)p * C + c8 * 8, E::pack(v));
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) head_bwd_x_kernel(const float* __restrict__ dl, const T* __restrict__ wfc,
                                                         int HW, int C, int ncls, T* __restrict__ dact) {
-  typedef Elt<T> E;
-  extern __shared__ float row[];
-  const int n = blockIdx.x, t = threadIdx.x;
-  for (int j = t; j < ncls; j += 256) row[j] = dl[(int64_t)n * ncls + j];
-  __syncthreads();
-  const float inv = 1.f / (float)HW;
-  T* o = dact + (int64_t)n * HW * C;
-  for (int c = t; c < C; c += 256) {
-    float s = 0.f;
-    for (int j = 0; j < ncls; ++j) s += row[j] * E::cvt(wfc[(int64_t)j * C + c]);
-    const T v = E::from(s * inv);
-    for (int p = 0; p < HW; ++p) o[(int64_t)p * C + c] = v;
-  }
+  extern __shared__ float hsx[];
+  const int n = blockIdx.x;
+  head_dact_image<T>(dl + (int64_t)n * ncls, wfc, HW, C, ncls, dact + (int64_t)n * HW * C, hsx);
 }
 
 // One launch for the whole head backward (the first kernels after the per-step barrier, when the GPU
@@ -375,8 +419,7 @@ __global__ void __launch_bounds__(256) head_bwd_fused_kernel(const float* __rest
                                                             const T* __restrict__ wfc, int N, int HW, int C, int ncls,
                                                             float scale, float* __restrict__ dw,
                                                             float* __restrict__ db, T* __restrict__ dact, int nw) {
-  typedef Elt<T> E;
-  __shared__ float row[1024];
+  extern __shared__ float hsx[];
   const int t = threadIdx.x;
   if ((int)blockIdx.x < nw) {
     const int strips = (C + 255) / 256;
@@ -395,30 +438,23 @@ __global__ void __launch_bounds__(256) head_bwd_fused_kernel(const float* __rest
     return;
   }
   const int n = blockIdx.x - nw;
-  for (int j = t; j < ncls; j += 256) row[j] = dl[(int64_t)n * ncls + j];
-  __syncthreads();
-  const float inv = 1.f / (float)HW;
-  T* o = dact + (int64_t)n * HW * C;
-  for (int c = t; c < C; c += 256) {
-    float sum = 0.f;
-    for (int j = 0; j < ncls; ++j) sum += row[j] * E::cvt(wfc[(int64_t)j * C + c]);
-    const T v = E::from(sum * inv);
-    for (int p = 0; p < HW; ++p) o[(int64_t)p * C + c] = v;
-  }
+  head_dact_image<T>(dl + (int64_t)n * ncls, wfc, HW, C, ncls, dact + (int64_t)n * HW * C, hsx);
 }
 
 template <typename T>
 static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int N, int HW, int C, int ncls,
                       float scale, float* dw, float* db, T* dact, float* ws, size_t ws_bytes, hipStream_t st) {
-  DTC_CHECK_ARG(dlogits && feat && wfc && dw && db && dact && N > 0 && HW > 0 && C > 0 && ncls > 0,
+  DTC_CHECK_ARG(dlogits && feat && wfc && dw && db && dact && N > 0 && HW > 0 && C > 0 && C % 8 == 0 && C <= 2048 &&
+                    ncls > 0 && ncls <= 4096,
                 "head_bwd: bad args");
+  const size_t dx_lds = (size_t)(ncls + 4 * C) * sizeof(float);  // head_dact_image
   // option head_fused: 1 always, 2 (auto) at most 64 images -- the dW strips loop over the images, so at
   // batch 256 the three-launch form measured 1% faster; at the per-rank batches of config 3 the launches cost more
   const int hf = option_get(OPT_HEAD_FUSED);
   if (ncls <= 1024 && (hf == 1 || (hf == 2 && N <= 64))) {
     const int nw = ncls * ((C + 255) / 256);
-    hipLaunchKernelGGL(head_bwd_fused_kernel<T>, dim3(nw + N), dim3(256), 0, st, dlogits, feat, wfc, N, HW, C, ncls,
-                       scale, dw, db, dact, nw);
+    hipLaunchKernelGGL(head_bwd_fused_kernel<T>, dim3(nw + N), dim3(256), dx_lds, st, dlogits, feat, wfc, N, HW, C,
+                       ncls, scale, dw, db, dact, nw);
     DTC_LAUNCH_CHECK();
     return 0;
   }
@@ -430,8 +466,7 @@ static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int
   hipLaunchKernelGGL(head_bwd_w_reduce_kernel, dim3((int)(((int64_t)ncls * C + 255) / 256)), dim3(256), 0, st, ws,
                      splits, dlogits, N, C, ncls, scale, dw, db);
   DTC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(head_bwd_x_kernel<T>, dim3(N), dim3(256), ncls * sizeof(float), st, dlogits, wfc, HW, C, ncls,
-                     dact);
+  hipLaunchKernelGGL(head_bwd_x_kernel<T>, dim3(N), dim3(256), dx_lds, st, dlogits, wfc, HW, C, ncls, dact);
   DTC_LAUNCH_CHECK();
   return 0;
 }

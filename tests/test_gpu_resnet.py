@@ -1368,3 +1368,38 @@ def test_sync_batchnorm_one_rank(dtc, cuda):
         assert rel_err(l1, l0) < 1e-3 and rel_err(g1, g0) < 1e-3 and rel_err(b1, b0) < 1e-5
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("graphs", [1, 4])
+def test_graph_exec_churn(dtc, cuda, graphs):
+    """Graph-exec lifecycle under churn (the round-2 worker-thread crash must show up as a test
+    failure if it recurs): every cycle changes an option (the next step drops and destroys the step graphs
+    and re-captures them) and arms / disarms the live conv profile (the profiled graph set, the device
+    drains under the capture lock), forward and backward replayed (graphs=1) or the default mode; every
+    loss stays finite and every profiled pass records its conv launches."""
+    import ctypes as C
+    lib = dtc._native.lib
+    torch.manual_seed(42)
+    model = dtc.ResNet18().to(cuda)
+    crit = dtc.CrossEntropyLoss()
+    x = torch.randn(8, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 100, (8,), device=cuda)
+    lib.dtc_set_option(b"graphs", graphs)
+    try:
+        crit(model(x), y).backward()
+        exe = model.executor(8, 32, 32)
+        for i in range(12):
+            lib.dtc_set_option(b"sc_fuse", i % 2)
+            loss = crit(model(x), y)
+            loss.backward()
+            assert np.isfinite(loss.item())
+            dtc._native.call("dtc_rn18_profile_begin", exe.handle, 1)
+            for _ in range(2):
+                crit(model(x), y).backward()
+            ms, fl, cnt = (C.c_double * 3)(), (C.c_double * 3)(), (C.c_int * 3)()
+            dtc._native.call("dtc_rn18_profile_end", exe.handle, ms, fl, cnt)
+            assert cnt[0] > 0 and cnt[1] > 0 and cnt[2] > 0, list(cnt)
+        torch.cuda.synchronize()
+    finally:
+        lib.dtc_set_option(b"sc_fuse", 1)
+        lib.dtc_set_option(b"graphs", 4)
