@@ -411,8 +411,8 @@ __global__ void __launch_bounds__(256) head_bwd_x_kernel(const float* __restrict
 
 // One launch for the whole head backward (the first kernels after the per-step barrier, when the GPU
 // queue is empty, so every launch boundary here is exposed): workgroups [0, nw) compute dW / db, one
-// (class, 256-channel) strip each, summing over the images in order (dl[n][j] is workgroup-uniform,
-// feat rows coalesced); workgroups [nw, nw + N) compute dact of one image each (head_bwd_x's work).
+// (class, 256-channel) strip each, the four waves summing every fourth image (dl[n][j] is uniform, feat
+// rows coalesced); workgroups [nw, nw + N) compute dact of one image each (head_bwd_x's work).
 template <typename T>
 __global__ void __launch_bounds__(256) head_bwd_fused_kernel(const float* __restrict__ dl,
                                                             const float* __restrict__ feat,
@@ -422,19 +422,35 @@ __global__ void __launch_bounds__(256) head_bwd_fused_kernel(const float* __rest
   extern __shared__ float hsx[];
   const int t = threadIdx.x;
   if ((int)blockIdx.x < nw) {
+    // dW[j][c..c+3] (float4 of feat per lane) and db[j]: wave w sums the images n = w, w + 4, ... (eight
+    // rows in flight per lane), the four wave partials are added in LDS in a fixed order
     const int strips = (C + 255) / 256;
-    const int j = blockIdx.x / strips, c = (blockIdx.x - j * strips) * 256 + t;
+    const int j = blockIdx.x / strips, cb = (blockIdx.x - j * strips) * 256;
+    const int wv = t >> 6, l = t & 63, c = cb + l * 4;
+    float a[4] = {0.f, 0.f, 0.f, 0.f}, b = 0.f;
     if (c < C) {
-      float a = 0.f;
 #pragma unroll 8
-      for (int n = 0; n < N; ++n) a += dl[(int64_t)n * ncls + j] * feat[(int64_t)n * C + c];
-      dw[(int64_t)j * C + c] = a * scale;
+      for (int n = wv; n < N; n += 4) {
+        const float d = dl[(int64_t)n * ncls + j];
+        const f32x4 f = *(const f32x4*)(feat + (int64_t)n * C + c);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] += d * f[k];
+        b += d;
+      }
     }
-    if (c == 0) {
-      float b = 0.f;
-      for (int n = 0; n < N; ++n) b += dl[(int64_t)n * ncls + j];
-      db[j] = b * scale;
+    float* red = hsx;  // [4 waves][260]
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[wv * 260 + l * 4 + k] = a[k];
+    if (l == 0) red[wv * 260 + 256] = b;
+    __syncthreads();
+    if (wv == 0 && c < C) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = l * 4 + k;
+        dw[(int64_t)j * C + c + k] = (((red[i] + red[260 + i]) + red[520 + i]) + red[780 + i]) * scale;
+      }
     }
+    if (t == 0 && cb == 0) db[j] = (((red[256] + red[516]) + red[776]) + red[1036]) * scale;
     return;
   }
   const int n = blockIdx.x - nw;
@@ -447,7 +463,7 @@ static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int
   DTC_CHECK_ARG(dlogits && feat && wfc && dw && db && dact && N > 0 && HW > 0 && C > 0 && C % 8 == 0 && C <= 2048 &&
                     ncls > 0 && ncls <= 4096,
                 "head_bwd: bad args");
-  const size_t dx_lds = (size_t)(ncls + 4 * C) * sizeof(float);  // head_dact_image
+  const size_t dx_lds = (size_t)std::max(ncls + 4 * C, 4 * 260) * sizeof(float);  // head_dact_image / fused dW
   // option head_fused: 1 always, 2 (auto) at most 64 images -- the dW strips loop over the images, so at
   // batch 256 the three-launch form measured 1% faster; at the per-rank batches of config 3 the launches cost more
   const int hf = option_get(OPT_HEAD_FUSED);
