@@ -170,9 +170,19 @@ def ptr(t) -> int | None:
     return t.data_ptr()
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_GET_DEVICE = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def stream_ptr(stream=None) -> int:
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return s.cuda_stream
+    """HIP stream handle of `stream`, or of the current device's current stream (read through torch's raw
+    getters: torch.cuda.current_stream() builds a Stream object through several Python lookups, a few us
+    per call on every per-step launch)."""
+    if stream is not None:
+        return stream.cuda_stream
+    if _RAW_STREAM is not None and _GET_DEVICE is not None:
+        return _RAW_STREAM(_GET_DEVICE())
+    return torch.cuda.current_stream().cuda_stream
 
 
 def require_cuda(*tensors) -> None:

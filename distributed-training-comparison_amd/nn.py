@@ -242,11 +242,6 @@ class _NetFn(torch.autograd.Function):
         return None, None, None, None
 
 
-# (scale tensor or None, scaled-loss output or None, pinned host word) for the next _XentFn.forward: the
-# training step's loss, scaled loss and host copy in one launch (dtc_xent_fwd_ex)
-_XENT_EXTRA = [None]
-
-
 class _HostWords:
     """A ring of pinned host words the loss launch writes its value into (the item() read). The ring is
     owned here, not by torch's pinned-memory cache: a word a kernel may still write is never handed to
@@ -280,16 +275,7 @@ _HOST_WORDS: List[Optional[_HostWords]] = [None]
 class _XentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels):
-        extra = _XENT_EXTRA[0]
-        if extra is not None:
-            scale, scaled, host = extra
-            n, ncls = logits.shape
-            loss = torch.empty((), dtype=torch.float32, device=logits.device)
-            lse = torch.empty(n, dtype=torch.float32, device=logits.device)
-            call("dtc_xent_fwd_ex", ptr(logits), ptr(labels), n, ncls, ptr(loss), ptr(lse), ptr(scale), ptr(scaled),
-                 host.data_ptr(), stream_ptr())
-        else:
-            loss, lse = ops.xent_fwd(logits, labels)
+        loss, lse = ops.xent_fwd(logits, labels)
         ctx.save_for_backward(logits, labels, lse)
         ctx.lse = lse
         return loss
@@ -434,21 +420,26 @@ class CrossEntropyLoss(nn.Module):
             from .parallel import _DPFn
 
             if isinstance(node, (_NetFn._backward_cls, _DPFn._backward_cls)):
-                if logits.shape[0] <= 4096:  # loss + scaled loss + host copy: one launch
+                if logits.shape[0] <= 4096:
+                    # loss + lse + scaled loss + host copy: one launch, called directly (no autograd node:
+                    # the direct backward chain below needs none; the autograd form of the loss -- the
+                    # same kernel's value -- is built only if a fallback backward asks for it)
                     sc = _prescaler()
                     if _HOST_WORDS[0] is None:
                         _HOST_WORDS[0] = _HostWords()
                     slot, host = _HOST_WORDS[0].take()
-                    scaled = torch.empty((), dtype=torch.float32, device=logits.device) if sc is not None else None
-                    _XENT_EXTRA[0] = (sc._scale if sc is not None else None, scaled, host)
-                    try:
-                        loss = _XentFn.apply(logits, labels)
-                    finally:
-                        _XENT_EXTRA[0] = None
+                    n, ncls = logits.shape
+                    dev = logits.device
+                    loss = torch.empty((), dtype=torch.float32, device=dev)
+                    lse = torch.empty(n, dtype=torch.float32, device=dev)
+                    scaled = torch.empty((), dtype=torch.float32, device=dev) if sc is not None else None
+                    call("dtc_xent_fwd_ex", logits.data_ptr(), labels.data_ptr(), n, ncls, loss.data_ptr(),
+                         lse.data_ptr(), None if sc is None else sc._scale.data_ptr(),
+                         None if scaled is None else scaled.data_ptr(), host.data_ptr(), _raw_stream(dev.index))
                     ev = torch.cuda.Event()
                     ev.record()
                     _HOST_WORDS[0].done(slot, ev)
-                    out = _wrap_loss(loss, lambda: loss, (node, logits, labels, loss.grad_fn.lse, None))
+                    out = _wrap_loss(loss, lambda: _XentFn.apply(logits, labels), (node, logits, labels, lse, None))
                     out._dtc_host = (host, ev)
                     if sc is not None:
                         prescale(out, scaled, sc)

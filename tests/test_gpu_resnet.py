@@ -1304,6 +1304,7 @@ def test_sync_batchnorm_two_identical_ranks_loopback(dtc, cuda):
     [2][C] sums, not the 32 partial-sum slots).
     """
     comm = dtc.parallel.Comm.loopback(cuda.index or 0, 2.0, world=2)
+    dtc._native.lib.dtc_set_option(b"bn_cg", 0)  # the SyncBN executor's two-pass BN backward in both arms
     try:
         g = torch.Generator().manual_seed(5)
         x = torch.randn(32, 3, 32, 32, generator=g).to(cuda)
@@ -1332,6 +1333,7 @@ def test_sync_batchnorm_two_identical_ranks_loopback(dtc, cuda):
         assert rel_err(g1, g0) < 1e-3
         m1.set_sync_bn(None)
     finally:
+        dtc._native.lib.dtc_set_option(b"bn_cg", 1)
         comm.close()
 
 
@@ -1342,6 +1344,7 @@ def test_sync_batchnorm_one_rank(dtc, cuda):
     equal the per-rank BatchNorm path (up to the order of the fp64 statistics atomics). The
     two-rank statistics semantics are covered by tests/test_ddp_gloo.py::test_sync_batchnorm_gloo."""
     comm = dtc.parallel.Comm(0, 1, dtc.parallel.Comm.unique_id(), cuda.index or 0)
+    dtc._native.lib.dtc_set_option(b"bn_cg", 0)  # the SyncBN executor's two-pass BN backward in both arms
     try:
         t = torch.arange(6, dtype=torch.float64, device=cuda)
         comm.allreduce_sum_(t)
@@ -1367,6 +1370,7 @@ def test_sync_batchnorm_one_rank(dtc, cuda):
         assert np.isfinite(g1).all() and np.abs(g1).sum() > 0
         assert rel_err(l1, l0) < 1e-3 and rel_err(g1, g0) < 1e-3 and rel_err(b1, b0) < 1e-5
     finally:
+        dtc._native.lib.dtc_set_option(b"bn_cg", 1)
         comm.close()
 
 

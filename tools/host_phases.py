@@ -2,7 +2,7 @@
 
 Replicates bench.py's step and stamps time.perf_counter() after each phase; a phase that blocks
 on the device (barrier, item) shows the GPU time it waited for, the others show pure host cost.
-Usage: python tools/host_phases.py [--steps 50] [--no-barrier]"""
+Usage: python tools/host_phases.py [--steps 50] [--batch 256] [--no-barrier] [--cprofile]"""
 import argparse
 import os
 import sys
@@ -20,6 +20,7 @@ import dtc_import  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--no-barrier", action="store_true")
     ap.add_argument("--torch-barrier", action="store_true", help="dist.barrier() instead of bench.py's dtc.barrier()")
     ap.add_argument("--cprofile", action="store_true", help="cProfile the timed steps (top functions by tottime)")
@@ -29,7 +30,7 @@ def main():
         import ctypes
         hip = ctypes.CDLL("libamdhip64.so")
         print("hipSetDeviceFlags(spin) ->", hip.hipSetDeviceFlags(1))
-    rank, world, local = bench.init_dist()
+    rank, world, local = bench.init_dist(1)
     dev = torch.device("cuda", local)
     dtc = dtc_import.load()
     torch.manual_seed(42)
@@ -38,7 +39,7 @@ def main():
     opt = dtc.SGD(model.parameters(), lr=0.1, weight_decay=1e-4, momentum=0.9, nesterov=True)
     scaler = dtc.GradScaler()
     tpl = dtc.data.class_templates(100, 32, 32)
-    img, label = dtc.data.synthetic_batch(0, 256, 32, 32, 100, dev, tpl)
+    img, label = dtc.data.synthetic_batch(0, args.batch, 32, 32, 100, dev, tpl)
     names = ["zero_grad", "forward", "loss", "barrier", "scale", "backward", "step", "update", "item"]
     rec = []
     prof = None
