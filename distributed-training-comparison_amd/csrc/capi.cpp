@@ -148,6 +148,15 @@ static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 static inline ConvShape shape_of(const dtc_conv_desc* d) {
   return ConvShape{d->n, d->h, d->w, d->c, d->k, d->r, d->s, d->stride, d->pad};
 }
+// The convolutions the kernels implement: 1x1 / 3x3, stride 1 / 2, pad 0 / 1, C and K multiples of 64,
+// a non-empty output. Checked at the boundary, before any planning arithmetic (which divides by C / 64).
+static bool desc_ok(const dtc_conv_desc* d) {
+  if (!d || d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c <= 0 || d->k <= 0) return false;
+  if (d->c % 64 != 0 || d->k % 64 != 0 || d->r != d->s || (d->r != 1 && d->r != 3)) return false;
+  if ((d->stride != 1 && d->stride != 2) || d->pad < 0 || d->pad > 1) return false;
+  const int64_t p = (d->h + 2 * d->pad - d->r) / d->stride + 1, q = (d->w + 2 * d->pad - d->s) / d->stride + 1;
+  return p > 0 && q > 0 && (int64_t)d->n * d->h * d->w * std::max(d->c, d->k) < (1ll << 40);
+}
 
 #define GUARD(body)                                                          \
   try {                                                                      \
@@ -190,19 +199,21 @@ int dtc_install_crash_handler(void) {
 }
 
 size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass) {
-  if (!d || pass < 0 || pass > 2) return 0;
+  if (!desc_ok(d) || pass < 0 || pass > 2) return 0;
   return plan_conv(shape_of(d), pass).slab_bytes;
 }
 
 int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, void* ws,
                    size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && w && y, "dtc_conv2d_fwd: null argument");
+  DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_fwd: unsupported convolution descriptor");
   GUARD(return conv_fwd(shape_of(d), x, w, y, stats, (float*)ws, ws ? ws_bytes : 0, S(stream));)
 }
 
 int dtc_conv2d_fwd_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats,
                       const uint16_t* wsc, uint16_t* ysc, double* stats_sc, void* stream) {
   DTC_CHECK_ARG(d && x && w && y && wsc && ysc, "dtc_conv2d_fwd_sc: null argument");
+  DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_fwd_sc: unsupported convolution descriptor");
   const ConvShape s = shape_of(d);
   const ConvShape sc{s.N, s.H, s.W, s.C, s.K, 1, 1, 2, 0};
   DTC_CHECK_ARG(conv_fwd_sc_ok(s, sc), "dtc_conv2d_fwd_sc: no fused plan for this geometry");
@@ -212,6 +223,7 @@ int dtc_conv2d_fwd_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t*
 int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx, const uint16_t* res,
                      void* ws, size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && dy && w && dx, "dtc_conv2d_dgrad: null argument");
+  DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_dgrad: unsupported convolution descriptor");
   GUARD(return conv_dgrad(shape_of(d), dy, w, dx, res, (float*)ws, ws ? ws_bytes : 0, S(stream));)
 }
 
@@ -220,6 +232,7 @@ int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16
                         const float* invstd1, double* acc1, const uint16_t* x2, const float* mean2,
                         const float* invstd2, double* acc2, void* ws, size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && dy && w && dx && ymask && x1 && mean1 && invstd1 && acc1, "dtc_conv2d_dgrad_bn: null argument");
+  DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_dgrad_bn: unsupported convolution descriptor");
   DTC_CHECK_ARG(!x2 || (mean2 && invstd2 && acc2), "dtc_conv2d_dgrad_bn: second BN arguments");
   BnbArgs a;
   a.ym = ymask; a.x1 = x1; a.mean1 = mean1; a.invstd1 = invstd1; a.acc1 = acc1;
@@ -230,6 +243,7 @@ int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16
 int dtc_conv2d_dgrad_sc(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
                         const uint16_t* dsc, const uint16_t* wsc, void* stream) {
   DTC_CHECK_ARG(d && dy && w && dx && dsc && wsc, "dtc_conv2d_dgrad_sc: null argument");
+  DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_dgrad_sc: unsupported convolution descriptor");
   DTC_CHECK_ARG(conv_dgrad_sc_ok(shape_of(d)), "dtc_conv2d_dgrad_sc: no fused plan for this geometry");
   GUARD(return conv_dgrad_sc(shape_of(d), dy, w, dx, dsc, wsc, S(stream));)
 }
@@ -237,11 +251,12 @@ int dtc_conv2d_dgrad_sc(const dtc_conv_desc* d, const uint16_t* dy, const uint16
 int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, float* dw, float scale, void* ws,
                      size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && dy && dw && ws, "dtc_conv2d_wgrad: null argument (workspace is required)");
+  DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_wgrad: unsupported convolution descriptor");
   GUARD(return conv_wgrad(shape_of(d), x, dy, dw, 0, 0, scale, (float*)ws, ws_bytes, S(stream));)
 }
 
 size_t dtc_conv2d_wgrad_sc_workspace_size(const dtc_conv_desc* d) {
-  if (!d) return 0;
+  if (!desc_ok(d)) return 0;
   const ConvShape s = shape_of(d);
   return wgrad_s2_splits(s) > 0 ? conv_wgrad_s2_slab_bytes(s) : 0;
 }
@@ -249,11 +264,12 @@ size_t dtc_conv2d_wgrad_sc_workspace_size(const dtc_conv_desc* d) {
 int dtc_conv2d_wgrad_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, const uint16_t* dsc, float* dw,
                         float* dw_sc, float scale, void* ws, size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && dy && dsc && dw && dw_sc, "dtc_conv2d_wgrad_sc: null argument");
+  DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_wgrad_sc: unsupported convolution descriptor");
   GUARD(return conv_wgrad_s2(shape_of(d), x, dy, dsc, dw, dw_sc, scale, (float*)ws, ws ? ws_bytes : 0, S(stream));)
 }
 
 size_t dtc_conv2d_wgrad_batch_workspace_size(const dtc_conv_desc* d, int n) {
-  if (!d || n < 1 || n > DTC_WG_BATCH) return 0;
+  if (!desc_ok(d) || n < 1 || n > DTC_WG_BATCH) return 0;
   const ConvShape s = shape_of(d);
   return wgrad_halo_splits(s, n) > 0 ? conv_wgrad_batch_slab_bytes(s, n) : 0;
 }
@@ -261,6 +277,7 @@ size_t dtc_conv2d_wgrad_batch_workspace_size(const dtc_conv_desc* d, int n) {
 int dtc_conv2d_wgrad_batch(const dtc_conv_desc* d, int n, const uint16_t* const* x, const uint16_t* const* dy,
                            float* const* dw, float scale, void* ws, size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && dy && dw && ws && n >= 1 && n <= DTC_WG_BATCH, "dtc_conv2d_wgrad_batch: bad argument");
+  DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_wgrad_batch: unsupported convolution descriptor");
   for (int i = 0; i < n; ++i) DTC_CHECK_ARG(x[i] && dy[i] && dw[i], "dtc_conv2d_wgrad_batch: null problem %d", i);
   GUARD(return conv_wgrad_batch(shape_of(d), n, x, dy, dw, scale, (float*)ws, ws_bytes, S(stream));)
 }

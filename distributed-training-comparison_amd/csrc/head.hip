@@ -98,7 +98,20 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const T* __restrict__ act
     const int g = t / tpr;
     if (g >= groups) break;
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int p = g; p < HW; p += groups) {
+    int p = g;
+    for (; p + 3 * groups < HW; p += 4 * groups) {  // four pixels' loads in flight, then their adds in order
+      typename E::V q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = E::ld(a + (int64_t)(p + u * groups) * C + c8 * 8);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float v[8];
+        E::unpack(q[u], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += v[k];
+      }
+    }
+    for (; p < HW; p += groups) {
       float v[8];
       E::unpack(E::ld(a + (int64_t)p * C + c8 * 8), v);
 #pragma unroll
@@ -223,18 +236,48 @@ __global__ void __launch_bounds__(1024) xent_fwd_fused_kernel(const float* __res
   __shared__ float slse[XF_MAX_ROWS];
   __shared__ float part[4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  for (int b = wave; b < N; b += 16) {
-    const float* z = logits + (int64_t)b * ncls;
-    float m = -INFINITY;
-    for (int j = lane; j < ncls; j += 64) m = fmaxf(m, z[j]);
-    m = wave_max(m);
-    float s = 0.f;
-    for (int j = lane; j < ncls; j += 64) s += expf(z[j] - m);
-    s = wave_sum(s);
-    if (lane == 0) {
-      const float v = m + logf(s);
-      lse[b] = v;
-      slse[b] = v;
+  if (ncls <= 128) {
+    // eight rows per wave per round, all their loads issued before the first reduction (one memory
+    // latency per round instead of one per row); per row the same operations in the same order as
+    // xent_lse_kernel (max, then s = exp(z[lane] - m) + exp(z[lane + 64] - m), wave sum): bit-identical
+    constexpr int R = 8;
+    for (int b0 = wave; b0 < N; b0 += 16 * R) {
+      float v0[R], v1[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int b = b0 + 16 * r;
+        const float* z = logits + (int64_t)(b < N ? b : 0) * ncls;
+        v0[r] = lane < ncls ? z[lane] : -INFINITY;
+        v1[r] = lane + 64 < ncls ? z[lane + 64] : -INFINITY;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int b = b0 + 16 * r;
+        const float m = wave_max(fmaxf(v0[r], v1[r]));
+        float s = lane < ncls ? expf(v0[r] - m) : 0.f;
+        if (lane + 64 < ncls) s += expf(v1[r] - m);
+        s = wave_sum(s);
+        if (lane == 0 && b < N) {
+          const float v = m + logf(s);
+          lse[b] = v;
+          slse[b] = v;
+        }
+      }
+    }
+  } else {
+    for (int b = wave; b < N; b += 16) {
+      const float* z = logits + (int64_t)b * ncls;
+      float m = -INFINITY;
+      for (int j = lane; j < ncls; j += 64) m = fmaxf(m, z[j]);
+      m = wave_max(m);
+      float s = 0.f;
+      for (int j = lane; j < ncls; j += 64) s += expf(z[j] - m);
+      s = wave_sum(s);
+      if (lane == 0) {
+        const float v = m + logf(s);
+        lse[b] = v;
+        slse[b] = v;
+      }
     }
   }
   __syncthreads();
@@ -464,8 +507,8 @@ static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int
                     ncls > 0 && ncls <= 4096,
                 "head_bwd: bad args");
   const size_t dx_lds = (size_t)std::max(ncls + 4 * C, 4 * 260) * sizeof(float);  // head_dact_image / fused dW
-  // option head_fused: 1 always, 2 (auto) at most 64 images -- the dW strips loop over the images, so at
-  // batch 256 the three-launch form measured 1% faster; at the per-rank batches of config 3 the launches cost more
+  // option head_fused: 1 (default) always, 2 at most 64 images. With the dW strips summed by four waves the one
+  // launch is faster at batch 256 too (+0.45%, 4-round A/B r04m; the round-3 sequential strip loop was 1% slower)
   const int hf = option_get(OPT_HEAD_FUSED);
   if (ncls <= 1024 && (hf == 1 || (hf == 2 && N <= 64))) {
     const int nw = ncls * ((C + 255) / 256);

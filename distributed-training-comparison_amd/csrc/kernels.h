@@ -47,14 +47,14 @@ namespace dtc {
   X(SC_FUSE, sc_fuse, 1)                /* projection shortcut inside conv1's forward: 1 layer4, 2/3 wider */ \
   X(STEM_WLDS, stem_wlds, 1)            /* stem forward weight staged in LDS */                               \
   X(HALO_S2, halo_s2, 1)                /* stride-2 3x3 FWD on the column-split halo kernel */                \
-  X(WGRAD_S2, wgrad_s2, 2)              /* stride-2 wgrad (+ shortcut) on the halo kernel: 0 off, 1 all, 2 GEN */ \
+  X(WGRAD_S2, wgrad_s2, 1)              /* stride-2 wgrad (+ shortcut) on the halo kernel: 0 off, 1 all, 2 GEN */ \
   X(WGRAD_S2_WGS, wgrad_s2_wgs, 256)    /* stride-2 halo wgrad: target workgroups (split-K slab = wgs x tile) */ \
   X(WGRAD_KSPLIT, wgrad_ksplit, 0)      /* wgrad_halo waves split the step's pixels (all 64 channels each) */ \
   X(DGRAD_SCF, dgrad_scf, 1)            /* shortcut dgrad fused into conv1's parity-class dgrad */            \
   X(BNB_MASK, bnb_mask, 0)              /* BN sums in the producing dgrad's epilogue: 1 all, 2 not c64 */    \
   X(BN_CG, bn_cg, 1)                    /* small BN backward as one launch (bn_bwd_cg) ...                  */ \
   X(BN_CG_ELEMS, bn_cg_elems, 262144)   /* ... for tensors of at most this many elements                    */ \
-  X(HEAD_FUSED, head_fused, 2)          /* head backward in one launch: 1 always, 2 at <= 64 images */       \
+  X(HEAD_FUSED, head_fused, 1)          /* head backward in one launch: 1 always, 2 at <= 64 images */       \
   X(HALO_STAGE_EPI, halo_stage_epi, 0)  /* conv_halo DGRAD epilogue staged through LDS: 1 always, 2 GEN only */ \
   X(COMM_ON_SIDE, comm_on_side, 1)      /* bucket all-reduces on the weight-gradient stream (no comm stream) */ \
   X(BUCKET_TAIL, bucket_tail, 1)        /* (plan time) close the open bucket (>= 1 MB) after layer2.0 */      \

@@ -375,6 +375,7 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
         slab = std::max(slab, conv_wgrad_batch_slab_bytes(b.c1.s, np));
         slab = std::max(slab, conv_wgrad_batch_slab_bytes(b.c2.s, np));
       }
+    if (!n.f32 && b.proj) slab = std::max(slab, conv_wgrad_s2_slab_bytes(b.c1.s));  // conv1 + shortcut wgrad (wgrad_s2)
   }
   if (n.stem_direct) slab = std::max(slab, stem_wgrad_slab_bytes(M0));
   n.slab_bytes = slab;

@@ -303,7 +303,7 @@ def test_head_and_loss(dtc, cuda, head_fused):
     try:
         _head_and_loss(dtc, cuda)
     finally:
-        dtc._native.lib.dtc_set_option(b"head_fused", 2)
+        dtc._native.lib.dtc_set_option(b"head_fused", 1)
 
 
 def _head_and_loss(dtc, cuda):

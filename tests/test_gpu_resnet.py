@@ -812,7 +812,8 @@ def test_live_conv_profile(dtc, cuda):
     crit = dtc.CrossEntropyLoss()
     xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
     dtc._native.lib.dtc_set_option(b"sc_fuse", 0)  # one launch per conv (sc_fuse merges conv1 + shortcut)
-    dtc._native.lib.dtc_set_option(b"dgrad_scf", 0)  # (and dgrad_scf their dgrads)
+    dtc._native.lib.dtc_set_option(b"dgrad_scf", 0)  # (and dgrad_scf their dgrads,
+    dtc._native.lib.dtc_set_option(b"wgrad_s2", 0)  # wgrad_s2 their weight gradients)
     try:
         crit(model(xd), yd).backward()
         exe = model.executor(8, 32, 32)
@@ -825,6 +826,7 @@ def test_live_conv_profile(dtc, cuda):
     finally:
         dtc._native.lib.dtc_set_option(b"sc_fuse", DEFAULT_SC_FUSE)
         dtc._native.lib.dtc_set_option(b"dgrad_scf", 1)
+        dtc._native.lib.dtc_set_option(b"wgrad_s2", 1)
     # 20 convs; the stem has no dgrad; the 13 stride-1 3x3 weight gradients run batched per geometry
     # within a DDP bucket (layer4 3, layer3 3, layer2 3, layer1 4: four launches) beside the 7 others
     assert list(cnt) == [20 * steps, 19 * steps, 11 * steps]

@@ -115,14 +115,35 @@ def test_workspace_and_conv_plans(dtc):
     assert lib.dtc_rn18_create(C.byref(h), 700, 224, 224, 100, 25.0) < 0  # int32 element-index guard
 
 
+@pytest.mark.parametrize("desc", [(8, 32, 32, 3, 64, 3, 3, 1, 1), (8, 32, 32, 64, 100, 3, 3, 1, 1),
+                                  (8, 32, 32, 64, 64, 5, 5, 1, 2), (8, 32, 32, 64, 64, 3, 3, 3, 1),
+                                  (0, 32, 32, 64, 64, 3, 3, 1, 1), (8, 1, 1, 64, 64, 3, 3, 1, 0)])
+def test_conv_abi_rejects_unsupported_descriptors(dtc, desc):
+    """Descriptors outside what the kernels implement (C or K not a multiple of 64, 5x5, stride 3, empty batch
+    or output) are refused at the boundary: workspace queries return 0 and every conv entry point returns an
+    error code with a message -- before any planning arithmetic (a C = 3 descriptor used to divide by C / 64 = 0
+    in the workspace query: SIGFPE) and before any device call."""
+    lib = dtc._native.lib
+    d = dtc._native.ConvDesc(*desc)
+    for p in range(3):
+        assert lib.dtc_conv2d_workspace_size(d, p) == 0
+    assert lib.dtc_conv2d_wgrad_sc_workspace_size(d) == 0
+    assert lib.dtc_conv2d_wgrad_batch_workspace_size(d, 2) == 0
+    one = C.c_void_p(16)
+    assert lib.dtc_conv2d_fwd(d, one, one, one, None, None, 0, None) != 0
+    assert b"unsupported convolution descriptor" in lib.dtc_last_error()
+    assert lib.dtc_conv2d_dgrad(d, one, one, one, None, None, 0, None) != 0
+    assert lib.dtc_conv2d_wgrad(d, one, one, one, C.c_float(1.0), one, 0, None) != 0
+
+
 # executor / kernel options added by the round-2 performance work, with their defaults (kernels.h)
 _OPTION_DEFAULTS = {
     "stem_bn_fuse": 1, "fork_lazy": 1, "side_prio": 1, "sc_fuse": 1, "stem_wlds": 1,
     "bn_red_elems": 16384, "bn_red_blocks": 256, "bn_fa_blocks": 1024,
     "sc_compact": 1, "stem_prologue": 1, "dgrad_class_order": 1, "wgrad_direct": 1, "wgrad_xcd": 1,
     # round 3
-    "halo_s2": 1, "wgrad_s2": 2, "dgrad_scf": 1, "bnb_mask": 0, "bucket_tail": 1, "halo_stage_epi": 0, "wgrad_gen": 1,
-    "halo_gen": 1, "bn_red_unroll": 4, "c64_gen": 1, "graphs": 4, "head_fused": 2,
+    "halo_s2": 1, "wgrad_s2": 1, "dgrad_scf": 1, "bnb_mask": 0, "bucket_tail": 1, "halo_stage_epi": 0, "wgrad_gen": 1,
+    "halo_gen": 1, "bn_red_unroll": 4, "c64_gen": 1, "graphs": 4, "head_fused": 1,
     # round 4
     "bn_cg": 1, "bn_cg_elems": 262144, "wgrad_s2_wgs": 256, "comm_on_side": 1, "wgrad_ksplit": 0,
 }
