@@ -233,22 +233,28 @@ __global__ void __launch_bounds__(1024) xent_fwd_fused_kernel(const float* __res
                                                              float* __restrict__ loss, float* __restrict__ lse,
                                                              const float* __restrict__ scale, float* __restrict__ scaled,
                                                              float* host) {
-  __shared__ float slse[XF_MAX_ROWS];
+  __shared__ float slse[XF_MAX_ROWS];  // the general path: lse per row (phase 2 gathers the label's logit)
+  __shared__ float sterm[XF_MAX_ROWS];  // ncls <= 128: lse - logit[label] per row, formed in phase 1
   __shared__ float part[4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  if (ncls <= 128) {
-    // eight rows per wave per round, all their loads issued before the first reduction (one memory
-    // latency per round instead of one per row); per row the same operations in the same order as
-    // xent_lse_kernel (max, then s = exp(z[lane] - m) + exp(z[lane + 64] - m), wave sum): bit-identical
-    constexpr int R = 8;
+  const bool fast = ncls <= 128;
+  if (fast) {
+    // sixteen rows per wave per round, all their loads (logits, label) issued before the first reduction
+    // (one memory latency per round); per row the same operations in the same order as xent_lse_kernel
+    // (max, then s = exp(z[lane] - m) + exp(z[lane + 64] - m), wave sum): bit-identical lse. The label's
+    // logit comes from the lane holding it, so phase 2 reads LDS only.
+    constexpr int R = 16;
     for (int b0 = wave; b0 < N; b0 += 16 * R) {
       float v0[R], v1[R];
+      int64_t y[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int b = b0 + 16 * r;
-        const float* z = logits + (int64_t)(b < N ? b : 0) * ncls;
+        const int bb = b < N ? b : 0;
+        const float* z = logits + (int64_t)bb * ncls;
         v0[r] = lane < ncls ? z[lane] : -INFINITY;
         v1[r] = lane + 64 < ncls ? z[lane + 64] : -INFINITY;
+        y[r] = labels[bb];
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -257,10 +263,13 @@ __global__ void __launch_bounds__(1024) xent_fwd_fused_kernel(const float* __res
         float s = lane < ncls ? expf(v0[r] - m) : 0.f;
         if (lane + 64 < ncls) s += expf(v1[r] - m);
         s = wave_sum(s);
+        const bool ok = y[r] >= 0 && y[r] < ncls;
+        const int yl = ok ? (int)y[r] : 0;
+        const float zy = __shfl(yl < 64 ? v0[r] : v1[r], yl & 63);
         if (lane == 0 && b < N) {
           const float v = m + logf(s);
           lse[b] = v;
-          slse[b] = v;
+          sterm[b] = ok ? (v - zy) : NAN;
         }
       }
     }
@@ -281,11 +290,15 @@ __global__ void __launch_bounds__(1024) xent_fwd_fused_kernel(const float* __res
     }
   }
   __syncthreads();
-  if (t < 256) {
+  if (t < 256) {  // the mean exactly as xent_mean_kernel sums it
     float acc = 0.f;
     for (int b = t; b < N; b += 256) {
-      const int64_t y = labels[b];
-      acc += (y >= 0 && y < ncls) ? (slse[b] - logits[(int64_t)b * ncls + y]) : NAN;
+      if (fast) {
+        acc += sterm[b];
+      } else {
+        const int64_t yy = labels[b];
+        acc += (yy >= 0 && yy < ncls) ? (slse[b] - logits[(int64_t)b * ncls + yy]) : NAN;
+      }
     }
     acc = wave_sum(acc);
     if ((t & 63) == 0) part[t >> 6] = acc;

@@ -186,7 +186,8 @@ __global__ void amp_check_finite4_kernel(const float* __restrict__ g, int64_t n,
   for (; i + 3 * stride < n4; i += 4 * stride) {
     const f32x4 a = g4[i], b = g4[i + stride], c = g4[i + 2 * stride], d = g4[i + 3 * stride];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) bad |= !isfinite(a[k]) | !isfinite(b[k]) | !isfinite(c[k]) | !isfinite(d[k]);
+    for (int k = 0; k < 4; ++k)  // branch-free: the four tests OR-ed as integers
+      bad |= (int)!isfinite(a[k]) | (int)!isfinite(b[k]) | (int)!isfinite(c[k]) | (int)!isfinite(d[k]);
   }
   for (; i < n4; i += stride) {
     const f32x4 a = g4[i];

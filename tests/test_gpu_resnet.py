@@ -435,6 +435,7 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
     lib = dtc._native.lib
     lib.dtc_set_option(b"dgrad_scf", 0)
     lib.dtc_set_option(b"bn_cg", 0)
+    lib.dtc_set_option(b"wgrad_s2", 0)  # (the older executor has no fused conv1 + shortcut weight gradient)
     try:
         la, ga, pa, ba = _train_steps(dtc, cuda, 3, graphs=graphs)
         lib.dtc_set_option(b"bn_fused_fin", 0)
@@ -445,6 +446,7 @@ def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
     finally:
         lib.dtc_set_option(b"dgrad_scf", 1)
         lib.dtc_set_option(b"bn_cg", 1)
+        lib.dtc_set_option(b"wgrad_s2", 1)
     np.testing.assert_allclose(la, lb, rtol=1e-4)
     assert rel_err(ga, gb) < 1e-3
     assert rel_err(pa, pb) < 1e-5
@@ -552,6 +554,7 @@ def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
     lib = dtc._native.lib
     lib.dtc_set_option(b"dgrad_scf", 0)
     lib.dtc_set_option(b"bn_cg", 0)  # the two-pass kernels: the same summation order as bn_mask=0
+    lib.dtc_set_option(b"wgrad_s2", 0)  # the bn_mask=0 executor has no fused conv1 + shortcut weight gradient
     try:
         ga = _grads_repeated(dtc, cuda, graphs)
         la, _, pa, ba = _train_steps(dtc, cuda, 3, graphs=graphs)
@@ -564,6 +567,7 @@ def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
     finally:
         lib.dtc_set_option(b"dgrad_scf", 1)
         lib.dtc_set_option(b"bn_cg", 1)
+        lib.dtc_set_option(b"wgrad_s2", 1)
     for rep in range(2):
         assert rel_err(ga[rep], gb[rep]) < 1e-6, rep
     np.testing.assert_allclose(la, lb, rtol=1e-4)
