@@ -179,23 +179,31 @@ int head_fwd(const float* act, int N, int HW, int C, const float* wfc, const flo
   return head_fwd_t<float>(act, N, HW, C, wfc, bfc, ncls, feat, logits, st);
 }
 
-// per-row log-sum-exp: one wave per row
-__global__ void __launch_bounds__(256) xent_lse_kernel(const float* __restrict__ logits, int N, int ncls,
-                                                      float* __restrict__ lse) {
-  const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= N) return;
-  const float* z = logits + (int64_t)b * ncls;
+// Per-row log-sum-exp: sixteen lanes per row (one DPP row), lane l holding z[l], z[l + 16], ...: a per-lane
+// max / sum over its values, then the 16-lane DPP tree (four VALU steps, no LDS permutes). The same function
+// (same per-lane order, same tree) serves xent_lse_kernel and the one-launch xent_fwd_fused_kernel, so both
+// produce bit-identical lse and loss.
+__device__ __forceinline__ float row_lse16(const float* __restrict__ z, int ncls, int li) {
   float m = -INFINITY;
-  for (int j = lane; j < ncls; j += 64) m = fmaxf(m, z[j]);
-  m = wave_max(m);
+#pragma unroll 8
+  for (int j = li; j < ncls; j += 16) m = fmaxf(m, z[j]);
+  m = row16_max(m);
   float s = 0.f;
-  for (int j = lane; j < ncls; j += 64) s += expf(z[j] - m);
-  s = wave_sum(s);
-  if (lane == 0) lse[b] = m + logf(s);
+#pragma unroll 8
+  for (int j = li; j < ncls; j += 16) s += expf(z[j] - m);
+  s = row16_sum(s);
+  return m + logf(s);
 }
 
-// loss = mean_b (lse[b] - z[b][y_b]); one workgroup, fixed summation order
+__global__ void __launch_bounds__(256) xent_lse_kernel(const float* __restrict__ logits, int N, int ncls,
+                                                      float* __restrict__ lse) {
+  const int li = threadIdx.x & 15;
+  const int b = blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (b >= N) return;  // (whole 16-lane rows retire together: the DPP tree never reads a retired lane)
+  const float v = row_lse16(logits + (int64_t)b * ncls, ncls, li);
+  if (li == 0) lse[b] = v;
+}
+
 __global__ void __launch_bounds__(256) xent_mean_kernel(const float* __restrict__ logits,
                                                        const int64_t* __restrict__ labels,
                                                        const float* __restrict__ lse, int N, int ncls,
@@ -215,7 +223,7 @@ __global__ void __launch_bounds__(256) xent_mean_kernel(const float* __restrict_
 
 int xent_fwd(const float* logits, const int64_t* labels, int N, int ncls, float* loss, float* lse, hipStream_t st) {
   DTC_CHECK_ARG(logits && labels && loss && lse && N > 0 && ncls > 0, "xent_fwd: bad args");
-  hipLaunchKernelGGL(xent_lse_kernel, dim3((N + 3) / 4), dim3(256), 0, st, logits, N, ncls, lse);
+  hipLaunchKernelGGL(xent_lse_kernel, dim3((N + 15) / 16), dim3(256), 0, st, logits, N, ncls, lse);
   DTC_LAUNCH_CHECK();
   hipLaunchKernelGGL(xent_mean_kernel, dim3(1), dim3(256), 0, st, logits, labels, lse, N, ncls, loss);
   DTC_LAUNCH_CHECK();
@@ -223,7 +231,7 @@ int xent_fwd(const float* logits, const int64_t* labels, int N, int ncls, float*
 }
 
 // The training step's loss in ONE launch (one 1024-thread workgroup, N <= XF_MAX_ROWS): the per-row
-// log-sum-exp exactly as xent_lse_kernel computes it (a wave per row), the mean exactly as xent_mean_kernel
+// log-sum-exp exactly as xent_lse_kernel computes it (row_lse16), the mean exactly as xent_mean_kernel
 // sums it (same lanes, same order: bit-identical loss), then loss x scale (GradScaler.scale, amp_scale's
 // multiply) and the loss stored into a pinned host word (the item() value: no copy launch). Replaces
 // xent_lse + xent_mean + a device-to-host copy + amp_scale on the path to the per-step barrier.
@@ -233,73 +241,22 @@ __global__ void __launch_bounds__(1024) xent_fwd_fused_kernel(const float* __res
                                                              float* __restrict__ loss, float* __restrict__ lse,
                                                              const float* __restrict__ scale, float* __restrict__ scaled,
                                                              float* host) {
-  __shared__ float slse[XF_MAX_ROWS];  // the general path: lse per row (phase 2 gathers the label's logit)
-  __shared__ float sterm[XF_MAX_ROWS];  // ncls <= 128: lse - logit[label] per row, formed in phase 1
+  __shared__ float sterm[XF_MAX_ROWS];  // lse - logit[label] per row (xent_mean_kernel's term)
   __shared__ float part[4];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const bool fast = ncls <= 128;
-  if (fast) {
-    // sixteen rows per wave per round, all their loads (logits, label) issued before the first reduction
-    // (one memory latency per round); per row the same operations in the same order as xent_lse_kernel
-    // (max, then s = exp(z[lane] - m) + exp(z[lane + 64] - m), wave sum): bit-identical lse. The label's
-    // logit comes from the lane holding it, so phase 2 reads LDS only.
-    constexpr int R = 16;
-    for (int b0 = wave; b0 < N; b0 += 16 * R) {
-      float v0[R], v1[R];
-      int64_t y[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int b = b0 + 16 * r;
-        const int bb = b < N ? b : 0;
-        const float* z = logits + (int64_t)bb * ncls;
-        v0[r] = lane < ncls ? z[lane] : -INFINITY;
-        v1[r] = lane + 64 < ncls ? z[lane + 64] : -INFINITY;
-        y[r] = labels[bb];
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int b = b0 + 16 * r;
-        const float m = wave_max(fmaxf(v0[r], v1[r]));
-        float s = lane < ncls ? expf(v0[r] - m) : 0.f;
-        if (lane + 64 < ncls) s += expf(v1[r] - m);
-        s = wave_sum(s);
-        const bool ok = y[r] >= 0 && y[r] < ncls;
-        const int yl = ok ? (int)y[r] : 0;
-        const float zy = __shfl(yl < 64 ? v0[r] : v1[r], yl & 63);
-        if (lane == 0 && b < N) {
-          const float v = m + logf(s);
-          lse[b] = v;
-          sterm[b] = ok ? (v - zy) : NAN;
-        }
-      }
-    }
-  } else {
-    for (int b = wave; b < N; b += 16) {
-      const float* z = logits + (int64_t)b * ncls;
-      float m = -INFINITY;
-      for (int j = lane; j < ncls; j += 64) m = fmaxf(m, z[j]);
-      m = wave_max(m);
-      float s = 0.f;
-      for (int j = lane; j < ncls; j += 64) s += expf(z[j] - m);
-      s = wave_sum(s);
-      if (lane == 0) {
-        const float v = m + logf(s);
-        lse[b] = v;
-        slse[b] = v;
-      }
+  const int t = threadIdx.x, li = t & 15;
+  for (int b = t >> 4; b < N; b += 64) {  // 64 rows per round, sixteen lanes each
+    const float* z = logits + (int64_t)b * ncls;
+    const float v = row_lse16(z, ncls, li);
+    if (li == 0) {
+      lse[b] = v;
+      const int64_t y = labels[b];
+      sterm[b] = (y >= 0 && y < ncls) ? (v - z[y]) : NAN;
     }
   }
   __syncthreads();
   if (t < 256) {  // the mean exactly as xent_mean_kernel sums it
     float acc = 0.f;
-    for (int b = t; b < N; b += 256) {
-      if (fast) {
-        acc += sterm[b];
-      } else {
-        const int64_t yy = labels[b];
-        acc += (yy >= 0 && yy < ncls) ? (slse[b] - logits[(int64_t)b * ncls + yy]) : NAN;
-      }
-    }
+    for (int b = t; b < N; b += 256) acc += sterm[b];
     acc = wave_sum(acc);
     if ((t & 63) == 0) part[t >> 6] = acc;
   }
