@@ -215,17 +215,10 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   // younger halo DMA: vmcnt retires in order): 74 -> 26 us per layer1 dgrad at B=256. The fused
   // BN-backward operands (y, x; option bnb_fuse) are still loaded in the epilogue: prefetching them
   // too would need 96 more VGPRs than the wave has.
-  // MODE 3 with mask bits (the default executor's conv2 dgrad, option bnb_mask) also prefetches the BN
-  // backward's x and the pixel's 8-byte mask row one tile ahead (+80 VGPRs for the two copies: 495 of 512);
-  // mode 4 keeps the epilogue loads (it has no room for them beside the residual's).
   typedef int i32x2 __attribute__((ext_vector_type(2)));
-  constexpr bool PFB = MODE == 3;
   struct EpiOps {
     i32x2 r[FN][FM];
-    i32x2 x[FN][FM];
-    i32x2 m[FN];
   };
-  const bool pfb = PFB && mbits;
   // VMEM ops the previous tile's epilogue leaves in flight per wave at the halo wait: stores (+ y, x)
   constexpr int EPI_VM = 16 + (BNB ? 32 : 0);
   auto epi_off = [&](int tile, int j, int i) {
@@ -245,22 +238,6 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
         const uint32_t off = epi_off(tile, j, i);
         o.r[j][i] = __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0);
       }
-  };
-  // BN-backward operands of one tile (pfb): x per fragment, the pixel's mask row (8 bytes = 64 channels)
-  auto prefetch_bnb = [&](EpiOps& o, int tile) {
-    __amdgpu_buffer_rsrc_t xr = xrsrc, mr = yrsrc;
-    if constexpr (GEN) {
-      const int64_t b = gen_base(tile);
-      xr = tile_rsrc(p.bnb.x1, b * 128);
-      mr = tile_rsrc(p.bnb.mb, b * 8);
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) o.x[j][i] = __builtin_amdgcn_raw_buffer_load_b64(xr, epi_off(tile, j, i), 0, 0);
-      const uint32_t o0 = epi_off(tile, j, 0);  // byte offset of (pixel, channel rq): / 128 * 8 = mask row
-      o.m[j] = __builtin_amdgcn_raw_buffer_load_b64(mr, o0 == 0x80000000u ? 0x80000000u : (o0 >> 7) << 3, 0, 0);
-    }
   };
 
   // epilogue of one finished tile: exactly FM*FN buffer stores per wave; lanes of pixels past M, or
@@ -283,15 +260,6 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     for (int i = 0; i < FM; ++i) {
       off[i] = ok ? epi_off(tile, j, i) : 0x80000000u;
       if constexpr (BNB) {  // out-of-range lanes read zeros (descriptor bound): masked to 0, no sums
-        if (pfb) {  // prefetched: byte 2 i + rq / 8 of the pixel's mask row, bits (rq & 4) .. + 3
-          const uint32_t row = i < 2 ? (uint32_t)o.m[j].x : (uint32_t)o.m[j].y;
-          const uint32_t nib = (row >> (((2 * (i & 1) + (rq >> 3)) << 3) + (rq & 4))) & 15u;
-          const uint32_t nb = ok ? nib : 0u;
-          yy[i].x = (int)(((nb & 1u) ? 0x3F80u : 0u) | ((nb & 2u) ? 0x3F800000u : 0u));
-          yy[i].y = (int)(((nb & 4u) ? 0x3F80u : 0u) | ((nb & 8u) ? 0x3F800000u : 0u));
-          xx[i] = o.x[j][i];
-          continue;
-        }
         if (mbits) {  // element e = off / 2: bits (e & 4) .. + 3 of byte e >> 3
           const uint32_t e = off[i] >> 1;
           const uint32_t by = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(yrs, off[i] == 0x80000000u ? 0x80000000u : e >> 3, 0, 0);
@@ -361,15 +329,12 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     // this tile's halo (and the residual issued before it) have landed; the previous iteration's
     // epilogue VMEM ops (FM*FN stores, + the BN-backward y/x loads) were issued after it
     if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (EPI_VM == 48 && !pfb) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else if constexpr (EPI_VM == 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const uint32_t hb = halo_lds + (uint32_t)((k & 1) * C64_HBYTES);
     if constexpr (RES) prefetch(opc, tile);
-    if constexpr (PFB) {
-      if (pfb) prefetch_bnb(opc, tile);
-    }
     const int tn = tile + gridDim.x;
     if (tn < p.ntiles) stage_halo(halo + ((k + 1) & 1) * C64_HBYTES, tn);
 
@@ -433,7 +398,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) accp[i][j] = acc[i][j];
     tilep = tile;
-    if constexpr (RES || PFB) opp = opc;
+    if constexpr (RES) opp = opc;
   }
   if (k > 0) epilogue(accp, opp, tilep, true);
 
