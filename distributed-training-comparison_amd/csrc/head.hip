@@ -7,6 +7,8 @@
 //       The pool is global over the last feature map (identical to avg_pool2d(4) at 32x32
 //       inputs; at 224x224 this is the documented global-pool deviation, SURVEY §7 viii).
 //   xent_fwd / xent_bwd : `nn.CrossEntropyLoss()` mean reduction (reference trainer.py:40,155).
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -94,6 +96,25 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const T* __restrict__ act
   float* fs = hsm;
   float* part = hsm + C;
   const T* a = act + (int64_t)n * HW * C;
+  // bf16, C = 512, <= 128 classes (the model's head): every weight chunk and bias this lane's Linear needs
+  // (four passes x eight 16-B chunks) is loaded FIRST, beside the pool's loads -- one memory latency for the
+  // kernel instead of one per pass (each dependent global access costs ~1 us here)
+  constexpr bool BF = std::is_same<T, u16>::value;
+  const bool fast = BF && C == 512 && ncls <= 128;
+  const int r8 = lane & 7;
+  typename E::V wpf[BF ? 4 : 1][8];
+  float bpf[4];
+  if constexpr (BF) {
+    if (fast) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = q * 32 + wave * 8 + (lane >> 3), jj = j < ncls ? j : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) wpf[q][u] = E::ld(wfc + (int64_t)jj * 512 + (r8 + 8 * u) * 8);
+        bpf[q] = bfc[jj];
+      }
+    }
+  }
   for (int c8 = t % tpr; c8 < tpr; c8 += 256) {  // (tpr > 256: threads loop over channel groups)
     const int g = t / tpr;
     if (g >= groups) break;
@@ -130,7 +151,29 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const T* __restrict__ act
   }
   __syncthreads();
   // Linear: class j = pass * 32 + wave * 8 + (lane >> 3); lane r = lane & 7 of its group
-  const int r8 = lane & 7, nch = C >> 3;
+  if constexpr (BF) {
+    if (fast) {  // the same sums in the same order as the loop below, from the prefetched chunks
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = q * 32 + wave * 8 + (lane >> 3);
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float f[8];
+          E::unpack(wpf[q][u], f);
+          const float* fc = fs + (r8 + 8 * u) * 8;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc += fc[k] * f[k];
+        }
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        acc += __shfl_xor(acc, 4);
+        if (j < ncls && r8 == 0) logits[(int64_t)n * ncls + j] = E::round(acc + E::round(bpf[q]));
+      }
+      return;
+    }
+  }
+  const int nch = C >> 3;
   for (int j0 = 0; j0 < ncls; j0 += 32) {
     const int j = j0 + wave * 8 + (lane >> 3);
     const bool ok = j < ncls;
@@ -243,14 +286,59 @@ __global__ void __launch_bounds__(1024) xent_fwd_fused_kernel(const float* __res
                                                              float* host) {
   __shared__ float sterm[XF_MAX_ROWS];  // lse - logit[label] per row (xent_mean_kernel's term)
   __shared__ float part[4];
-  const int t = threadIdx.x, li = t & 15;
-  for (int b = t >> 4; b < N; b += 64) {  // 64 rows per round, sixteen lanes each
-    const float* z = logits + (int64_t)b * ncls;
-    const float v = row_lse16(z, ncls, li);
-    if (li == 0) {
-      lse[b] = v;
-      const int64_t y = labels[b];
-      sterm[b] = (y >= 0 && y < ncls) ? (v - z[y]) : NAN;
+  const int t = threadIdx.x, li = t & 15, lane = t & 63;
+  if (ncls <= 128) {
+    // Every dependent global access costs ~1 us here, so each thread first issues ALL its loads -- four
+    // rows' values (lane li: z[li + 16 k]) and labels -- and only then reduces: one memory latency per
+    // four rounds of 64 rows. The folds match row_lse16 (same per-lane order, same DPP tree); the label's
+    // logit is read from the lane holding it (a permute within the row) instead of reloaded.
+    constexpr int RR = 4, KV = 8;
+    for (int b0 = t >> 4; b0 < N; b0 += 64 * RR) {
+      float v[RR][KV];
+      int64_t y[RR];
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        const int b = b0 + 64 * r, bb = b < N ? b : 0;
+        const float* z = logits + (int64_t)bb * ncls;
+#pragma unroll
+        for (int k = 0; k < KV; ++k) v[r][k] = li + 16 * k < ncls ? z[li + 16 * k] : 0.f;
+        y[r] = labels[bb];
+      }
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        const int b = b0 + 64 * r;
+        float m = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < KV; ++k)
+          if (li + 16 * k < ncls) m = fmaxf(m, v[r][k]);
+        m = row16_max(m);
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < KV; ++k)
+          if (li + 16 * k < ncls) sum += expf(v[r][k] - m);
+        sum = row16_sum(sum);
+        const float l = m + logf(sum);
+        const bool ok = y[r] >= 0 && y[r] < ncls;
+        const int yl = ok ? (int)y[r] : 0;
+        float cand = 0.f;
+#pragma unroll
+        for (int k = 0; k < KV; ++k) cand = (yl >> 4) == k ? v[r][k] : cand;
+        const float zy = __shfl(cand, (lane & ~15) | (yl & 15));
+        if (li == 0 && b < N) {
+          lse[b] = l;
+          sterm[b] = ok ? (l - zy) : NAN;
+        }
+      }
+    }
+  } else {
+    for (int b = t >> 4; b < N; b += 64) {  // 64 rows per round, sixteen lanes each
+      const float* z = logits + (int64_t)b * ncls;
+      const float v = row_lse16(z, ncls, li);
+      if (li == 0) {
+        lse[b] = v;
+        const int64_t y = labels[b];
+        sterm[b] = (y >= 0 && y < ncls) ? (v - z[y]) : NAN;
+      }
     }
   }
   __syncthreads();
@@ -377,6 +465,32 @@ __device__ __forceinline__ void head_dact_image(const float* __restrict__ dln, c
   float* row = sm;
   float* red = sm + ncls;
   const int t = threadIdx.x, wv = t >> 6, l = t & 63, nch = C >> 3;
+  constexpr bool BF = std::is_same<T, u16>::value;
+  if constexpr (BF) {
+    if (C == 512 && ncls <= 128) {  // all of this lane's weight rows (<= 32 x 16 B) in flight before any use
+      typename E::V w8[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int j = wv + 4 * u;
+        w8[u] = E::ld(wfc + (int64_t)(j < ncls ? j : 0) * C + l * 8);
+      }
+      for (int j = t; j < ncls; j += 256) row[j] = dln[j];
+      __syncthreads();
+      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {  // classes wv, wv + 4, ...: the generic loop's order
+        if (wv + 4 * u >= ncls) break;
+        float f[8];
+        E::unpack(w8[u], f);
+        const float d = row[wv + 4 * u];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += d * f[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[wv * C + l * 8 + k] = s[k];
+      goto combine;
+    }
+  }
   for (int j = t; j < ncls; j += 256) row[j] = dln[j];
   __syncthreads();
   for (int c8 = l; c8 < nch; c8 += 64) {
@@ -400,6 +514,7 @@ __device__ __forceinline__ void head_dact_image(const float* __restrict__ dln, c
 #pragma unroll
     for (int k = 0; k < 8; ++k) red[wv * C + c8 * 8 + k] = s[k];
   }
+combine:
   __syncthreads();
   const float inv = 1.f / (float)HW;
   for (int idx = t; idx < HW * nch; idx += 256) {
