@@ -604,9 +604,79 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
     }
   }
   const size_t plane = (size_t)M * Nc;
+  // one row's result: + residual (loaded earlier), then the BN-backward / statistics epilogue and the store
+  auto finish = [&](float (&v)[8], size_t o, const uint4& rw) {
+    if (res) {
+      float rv[8];
+      unpack8(rw, rv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += rv[k];
+    }
+    if constexpr (BNB) {
+      float yv[8], xv[8], xw[8];
+      if (bnb.mb) {  // mask bits: one byte per 8 channels (o % 8 == 0)
+        const uint32_t by = bnb.mb[o >> 3];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) yv[k] = ((by >> k) & 1u) ? 1.f : 0.f;
+      } else {
+        unpack8(*(const uint4*)(bnb.ym + o), yv);
+      }
+      unpack8(*(const uint4*)(bnb.x1 + o), xv);
+      if constexpr (DUAL) unpack8(*(const uint4*)(bnb.x2 + o), xw);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[k] = yv[k] > 0.f ? round_bf(v[k]) : 0.f;
+        s[k] += v[k];
+        q[k] += v[k] * ((xv[k] - m1[k]) * i1[k]);
+        if constexpr (DUAL) q2[k] += v[k] * ((xw[k] - m2[k]) * i2[k]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[k] = round_bf(v[k]);
+        s[k] += v[k];
+        q[k] += v[k] * v[k];
+      }
+    }
+    *(uint4*)(out + o) = pack8(v);
+  };
   if (rr < rpp) {
-    for (int m = m_begin + rr; m < m_end; m += rpp) {
+    // four rows per round: their residuals and every split's partials are loaded before the first add (each
+    // dependent global access costs ~1 us; one row at a time left these launches latency bound); per row the
+    // same additions in the same order as one row at a time (splits in order, then the residual)
+    constexpr int RU = 4;
+    int m = m_begin + rr;
+    for (; m + (RU - 1) * rpp < m_end; m += RU * rpp) {
+      size_t o[RU];
+      float v[RU][8];
+      uint4 rw[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        o[u] = (size_t)(m + u * rpp) * Nc + g * 8;
+        rw[u] = res ? *(const uint4*)(res + o[u]) : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[u][k] = 0.f;
+      }
+#pragma unroll 2
+      for (int sp = 0; sp < splits; ++sp) {
+        f32x4 a[RU], b[RU];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          a[u] = *(const f32x4*)(slab + sp * plane + o[u]);
+          b[u] = *(const f32x4*)(slab + sp * plane + o[u] + 4);
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          v[u][0] += a[u][0]; v[u][1] += a[u][1]; v[u][2] += a[u][2]; v[u][3] += a[u][3];
+          v[u][4] += b[u][0]; v[u][5] += b[u][1]; v[u][6] += b[u][2]; v[u][7] += b[u][3];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RU; ++u) finish(v[u], o[u], rw[u]);
+    }
+    for (; m < m_end; m += rpp) {
       const size_t o = (size_t)m * Nc + g * 8;
+      const uint4 rw = res ? *(const uint4*)(res + o) : uint4{0u, 0u, 0u, 0u};
       float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int sp = 0; sp < splits; ++sp) {
         const f32x4 a = *(const f32x4*)(slab + sp * plane + o);
@@ -614,39 +684,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
         v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
         v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
       }
-      if (res) {
-        float rv[8];
-        unpack8(*(const uint4*)(res + o), rv);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] += rv[k];
-      }
-      if constexpr (BNB) {
-        float yv[8], xv[8], xw[8];
-        if (bnb.mb) {  // mask bits: one byte per 8 channels (o % 8 == 0)
-          const uint32_t by = bnb.mb[o >> 3];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) yv[k] = ((by >> k) & 1u) ? 1.f : 0.f;
-        } else {
-          unpack8(*(const uint4*)(bnb.ym + o), yv);
-        }
-        unpack8(*(const uint4*)(bnb.x1 + o), xv);
-        if constexpr (DUAL) unpack8(*(const uint4*)(bnb.x2 + o), xw);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          v[k] = yv[k] > 0.f ? round_bf(v[k]) : 0.f;
-          s[k] += v[k];
-          q[k] += v[k] * ((xv[k] - m1[k]) * i1[k]);
-          if constexpr (DUAL) q2[k] += v[k] * ((xw[k] - m2[k]) * i2[k]);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          v[k] = round_bf(v[k]);
-          s[k] += v[k];
-          q[k] += v[k] * v[k];
-        }
-      }
-      *(uint4*)(out + o) = pack8(v);
+      finish(v, o, rw);
     }
   }
   if (BNB || stats) {

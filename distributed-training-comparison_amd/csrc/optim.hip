@@ -214,12 +214,13 @@ int amp_check_finite(const float* g, int64_t n, int* found_inf, hipStream_t st) 
 
 __global__ void amp_update_scale_kernel(float* scale, float* inv_scale, int* tracker, int* found, float growth,
                                         float backoff, int interval) {
-  float s = *scale;
-  if (*found) {
+  float s = *scale;  // the three state words loaded together (one memory latency), then the update
+  const int f = *found, tr = *tracker;
+  if (f) {
     s *= backoff;
     *tracker = 0;
   } else {
-    const int k = *tracker + 1;
+    const int k = tr + 1;
     if (k >= interval) {
       const float ns = s * growth;
       if (isfinite(ns)) s = ns;
