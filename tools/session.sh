@@ -5,4 +5,4 @@ tools/gpu_session.sh \
   "r04r_prof|300|tools/prof_run.sh r04r_b256" \
   "r04r_bench|200|python bench.py --gpus 1 --steps 50 --warmup 10 > gpurun_out/r04r_bench.json" \
   "r04r_w8prof|300|tools/prof_run.sh r04r_w8 $S8" \
-  "r04r_w8|300|tools/bench_ab.sh 2 'w8|$S8' 'b32|--batch 32' 'b64|--batch 64'"
+  "r04r_w8|400|tools/bench_ab.sh 2 'w8|$S8' 'w8s0|$S8 --opt bwd_streams=0' 'w8g0|$S8 --opt graphs=0' 'b32|--batch 32' 'b32s0|--batch 32 --opt bwd_streams=0' 'b32g0|--batch 32 --opt graphs=0'"
