@@ -557,23 +557,13 @@ __global__ void __launch_bounds__(256) head_bwd_fused_kernel(const float* __rest
     const int wv = t >> 6, l = t & 63, c = cb + l * 4;
     float a[4] = {0.f, 0.f, 0.f, 0.f}, b = 0.f;
     if (c < C) {
-      constexpr int NB = 32;  // images per batch: all their loads in flight before the first FMA
-      for (int n0 = wv; n0 < N; n0 += 4 * NB) {
-        f32x4 f[NB];
-        float d[NB];
+#pragma unroll 8
+      for (int n = wv; n < N; n += 4) {
+        const float d = dl[(int64_t)n * ncls + j];
+        const f32x4 f = *(const f32x4*)(feat + (int64_t)n * C + c);
 #pragma unroll
-        for (int u = 0; u < NB; ++u) {
-          const int n = n0 + 4 * u, nn = n < N ? n : 0;
-          f[u] = *(const f32x4*)(feat + (int64_t)nn * C + c);
-          d[u] = dl[(int64_t)nn * ncls + j];
-        }
-#pragma unroll
-        for (int u = 0; u < NB; ++u) {
-          if (n0 + 4 * u >= N) break;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) a[k] += d[u] * f[u][k];
-          b += d[u];
-        }
+        for (int k = 0; k < 4; ++k) a[k] += d * f[k];
+        b += d;
       }
     }
     float* red = hsx;  // [4 waves][260]
