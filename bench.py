@@ -529,7 +529,7 @@ def main():
                           "K steps run serialized and eager (bwd_streams=0, graphs=0: each launch has the chip to "
                           "itself) without the per-step host syncs (the host stays ahead; region_ms_per_step) -- reproduce with tools/prof_summary.py on a rocprofv3 "
                           "kernel trace of `bench.py --opt bwd_streams=0 --opt graphs=0`; value from the first "
-                          "region (weight gradients overlapped on a side stream, forward replayed)",
+                          "region (weight gradients overlapped on a side stream, the default launch mode)",
                 "stamp_conv_ms_per_step": round(sum(list(sms4)[:3]) / args.steps, 4),
                 "stamp_frac": (round(sum(list(sfl4)[:3]) / (sum(list(sms4)[:3]) * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, 4)
                                if sum(list(sms4)[:3]) > 0 else None),

@@ -510,18 +510,19 @@ static int graph_launch(Net& n, hipGraphExec_t ex, hipStream_t st) {
   return 0;
 }
 // option graphs: 0 = eager launches, 1 = forward and backward replayed from hipGraphs, 2 = forward only,
-// 3 = backward only, 4 (default) = the forward replayed, the backward eager -- except with a communicator
-// whose bucket collectives run on a stream of their own (comm_on_side=0: segment graphs, host-issued
-// collectives between them). Measured (tools/bench_ab.sh, one MI355X, images/s, replayed -> eager
-// backward): no communicator, batch 256 +4-5% (r03), batch 64 52.8k -> 59.9k (r04j); with a communicator
-// on the weight-gradient stream (loopback, r04g / r04h) batch 256 116.1k -> 125.9k, 128 78.3k -> 87.7k,
-// 64 49.5k -> 57.0k, 32 27.0k -> 31.1k: the replay's cross-stream edges and per-segment graph launches
-// cost more than the ~90 eager launches the host issues ahead of the GPU (`bwd`: which segment asks;
-// `comm`: the backward has a communicator)
+// 3 = backward only, 4 (default) = eager launches -- except the backward with a communicator whose bucket
+// collectives run on a stream of their own (comm_on_side=0: segment graphs, host-issued collectives between
+// them). Measured (tools/bench_ab.sh, one MI355X, images/s): the replayed backward is slower than eager at
+// every batch (no communicator: B=256 +4-5% eager (r03), B=64 52.8k -> 59.9k (r04j); with a communicator on
+// the weight-gradient stream, loopback r04g / r04h: B=256 116.1k -> 125.9k, 128 78.3k -> 87.7k, 64 49.5k ->
+// 57.0k, 32 27.0k -> 31.1k), and since the round-4 host-path changes the replayed forward is no faster
+// either (r04s, 3 rounds: B=256 132.5k -> 133.9k eager, B=128 93.0k / 93.2k, B=64 59.9k / 60.2k; r04r: B=32
+// 33.9k -> 34.3k, with a communicator 32.3k -> 32.8k): a graph launch's host cost and the ~14 us completion
+// gap behind it outweigh the launches it saves (`bwd`: which segment asks; `comm`: it has a communicator)
 static bool graphs_on(Net& n, bool bwd, bool comm = false) {
   const int g = option_get(OPT_GRAPHS);
   if (n.capture || n.sync || g == 0 || (g == 2 && bwd) || (g == 3 && !bwd)) return false;
-  if (g == 4 && bwd && !(comm && option_get(OPT_COMM_ON_SIDE) == 0)) return false;
+  if (g == 4 && (!bwd || !(comm && option_get(OPT_COMM_ON_SIDE) == 0))) return false;
   if (n.graph_epoch != option_epoch()) {  // options are baked into captured launches
     drop_graphs(n);
     n.graph_epoch = option_epoch();

@@ -1,4 +1,8 @@
 # scratch GPU session (overwritten per session; see tools/gpu_run.sh for the standard steps)
+S8='--sim-world 8 --global-batch 256 --sim-comm loopback'
 tools/gpu_session.sh \
-  "r04s_ab|600|tools/bench_ab.sh 3 'base|' 'g0|--opt graphs=0' 'b128|--batch 128' 'b128g0|--batch 128 --opt graphs=0' 'b64|--batch 64' 'b64g0|--batch 64 --opt graphs=0'" \
-  "r04s_tests|400|python -u -m pytest tests/test_gpu_ops.py -q -k 'head or xent' --timeout 300 --timeout-method thread"
+  "r04t_tests|600|python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread" \
+  "r04t_smoke|200|python -c 'import __graft_entry__ as g; g.smoke()'" \
+  "r04t_bench|200|python bench.py --gpus 1 --steps 50 --warmup 10 > gpurun_out/r04t_bench.json" \
+  "r04t_prof|300|tools/prof_run.sh r04t_b256" \
+  "r04t_ab|400|tools/bench_ab.sh 2 'base|' 'g2|--opt graphs=2' 'w8|$S8' 'w2|--sim-world 2 --global-batch 512 --sim-comm loopback'"
