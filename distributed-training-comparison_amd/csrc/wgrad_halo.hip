@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   };
 
   const int wm = wave >> 1, wn = wave & 1;  // KL = 1: wn is the wave's 32-pixel half of the step
-  constexpr int NJ = KL ? 4 : 2;             // B fragments (16 output channels each) per wave
+  constexpr int NJ = KL == 1 ? 4 : 2;             // B fragments (16 output channels each) per wave
   f32x4 acc[9][NJ];
 #pragma unroll
   for (int i = 0; i < 9; ++i)
@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   // A = the x halo read transposed at each tap's shift, B = the dy tile read transposed. The step
   // loop is unrolled by NS so each stage base is a constant the ds_read offset field absorbs: the
   // MFMA stream carries no address arithmetic.
-  constexpr int NKS = KL ? 1 : 2;  // 32-pixel halves a wave computes (KL = 1: its own, at index 0)
+  constexpr int NKS = KL == 1 ? 1 : 2;  // 32-pixel halves a wave computes (KL = 1: its own, at index 0)
   uint32_t aoff[NKS][9][2], boff[NKS][NJ][2];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
@@ -252,19 +252,19 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       const int unit = (cin >> 2) + (lane & 3);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int ra = hm[KL ? wn : ks][h] + toff;
+        const int ra = hm[KL == 1 ? wn : ks][h] + toff;
         const int f = wg_uswz(ra);
         aoff[ks][i][h] = (uint32_t)(ra * 128 + ((unit ^ f) << 3));
       }
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int cin = KL ? j * 16 : wn * 32 + j * 16;
+      const int cin = KL == 1 ? j * 16 : wn * 32 + j * 16;
       const int li = lane & 15, q = li >> 2, pp = li & 3, g = lane >> 4;
       const int unit = (cin >> 2) + pp;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int kr = wg_pixel(KL ? wn : ks, g, h, q);
+        const int kr = wg_pixel(KL == 1 ? wn : ks, g, h, q);
         const int f = wg_uswz(kr);
         boff[ks][j][h] = (uint32_t)(SG::HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
       }
@@ -289,6 +289,29 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
   };
   auto compute = [&](const char* sb) {
+    if constexpr (KL == 2) {
+      // software-pipelined fragment reads (option wgrad_ksplit=2): both k-steps' B fragments first, then the 18
+      // A fragments through a three-deep register ring -- fragment f + 2 is read before the MFMAs of f, and
+      // scheduling fences keep the compiler from sinking the reads back next to their uses (without them
+      // each A fragment was read right before its two MFMAs and waited for: lgkmcnt(0) every 2 MFMAs)
+      bf16x8 bfr2[2][2], ar[3];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bfr2[ks][j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
+      ar[0] = tr8(sb, aoff[0][0][0], aoff[0][0][1]);
+      ar[1] = tr8(sb, aoff[0][1][0], aoff[0][1][1]);
+#pragma unroll
+      for (int f = 0; f < 18; ++f) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (f + 2 < 18) ar[(f + 2) % 3] = tr8(sb, aoff[(f + 2) / 9][(f + 2) % 9][0], aoff[(f + 2) / 9][(f + 2) % 9][1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[f % 9][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[f % 3], bfr2[f / 9][j], acc[f % 9][j], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       bf16x8 bfr[NJ];
@@ -500,9 +523,10 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   dim3 grid((s.C / 64) * (s.K / 64), used, nprob);
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
   // 4-stage LDS ring (three steps of DMA in flight), compiler-scheduled fragment reads
-  const bool kl = option_get(OPT_WGRAD_KSPLIT) != 0;
+  const int kl = option_get(OPT_WGRAD_KSPLIT);
 #define DTC_WGH(NR_, GEN_)                                                                                    \
-  if (kl) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 1>), grid, dim3(512), 0, st, p);     \
+  if (kl == 1) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 1>), grid, dim3(512), 0, st, p); \
+  else if (kl == 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 2>), grid, dim3(512), 0, st, p); \
   else hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 0>), grid, dim3(512), 0, st, p)
   if (g.gen) {  // general geometry
     if (nr <= 2) { DTC_WGH(2, true); }

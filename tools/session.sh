@@ -1,8 +1,6 @@
 # scratch GPU session (overwritten per session; see tools/gpu_run.sh for the standard steps)
-S8='--sim-world 8 --global-batch 256 --sim-comm loopback'
 tools/gpu_session.sh \
-  "r04t_tests|600|python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread" \
-  "r04t_smoke|200|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "r04t_bench|200|python bench.py --gpus 1 --steps 50 --warmup 10 > gpurun_out/r04t_bench.json" \
-  "r04t_prof|300|tools/prof_run.sh r04t_b256" \
-  "r04t_ab|400|tools/bench_ab.sh 2 'base|' 'g2|--opt graphs=2' 'w8|$S8' 'w2|--sim-world 2 --global-batch 512 --sim-comm loopback'"
+  "r04u_tests|300|python -u -m pytest tests/test_gpu_ops.py -q -k wgrad --timeout 300 --timeout-method thread" \
+  "r04u_wgb|150|python tools/wgrad_bench.py --variants 'wgrad_ksplit=0;wgrad_ksplit=1;wgrad_ksplit=2' --check" \
+  "r04u_ab|500|tools/bench_ab.sh 3 'base|' 'ks2|--opt wgrad_ksplit=2'" \
+  "r04u_pmc|400|tools/pmc_bench.sh r04u"
