@@ -49,7 +49,7 @@ namespace dtc {
   X(HALO_S2, halo_s2, 1)                /* stride-2 3x3 FWD on the column-split halo kernel */                \
   X(WGRAD_S2, wgrad_s2, 1)              /* stride-2 wgrad (+ shortcut) on the halo kernel: 0 off, 1 all, 2 GEN */ \
   X(WGRAD_S2_WGS, wgrad_s2_wgs, 256)    /* stride-2 halo wgrad: target workgroups (split-K slab = wgs x tile) */ \
-  X(WGRAD_KSPLIT, wgrad_ksplit, 0)      /* wgrad_halo: 1 waves split the step's pixels, 2 pipelined fragment reads */ \
+  X(WGRAD_KSPLIT, wgrad_ksplit, 2)      /* wgrad_halo: 1 waves split the step's pixels, 2 pipelined fragment reads */ \
   X(DGRAD_SCF, dgrad_scf, 1)            /* shortcut dgrad fused into conv1's parity-class dgrad */            \
   X(BNB_MASK, bnb_mask, 0)              /* BN sums in the producing dgrad's epilogue: 1 all, 2 not c64 */    \
   X(BN_CG, bn_cg, 1)                    /* small BN backward as one launch (bn_bwd_cg) ...                  */ \

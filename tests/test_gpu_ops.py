@@ -487,7 +487,7 @@ def test_conv_wgrad_halo(dtc, cuda, case, ksplit):
         generic = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
     finally:
         dtc._native.lib.dtc_set_option(b"wgrad_halo", 256)
-        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", 0)
+        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", 2)
     assert rel_err(halo, ref) < 1e-5
     assert rel_err(generic, ref) < 1e-5
 
@@ -517,7 +517,7 @@ def test_conv_wgrad_batch(dtc, cuda, case, ksplit):
         got = dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.25)
         ones = [dtc.ops.conv2d_wgrad(xd[i], dyd[i], 3, 3, 1, 1, scale=0.25).cpu().numpy() for i in range(n)]
     finally:
-        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", 0)
+        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", 2)
     assert len(got) == n
     for i in range(n):
         ref = 0.25 * O.conv2d_wgrad(xs[i], dys[i], 3, 3, 1, 1)
