@@ -115,7 +115,9 @@ struct WgStage {
 // the loop (acc(half 0) + acc(half 1): one fixed order).
 template <int NS, int NR, int ST = 1, bool SC = false, bool GEN = false, int KL = 0>
 __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
-  static_assert(KL == 0 || !SC, "wgrad_ksplit: stride-1 kernels only");
+  static_assert(KL == 0 || KL == 2 || !SC, "wgrad_ksplit 1 / 3 (pixel split): no shortcut fusion");
+  constexpr bool PSPLIT = KL == 1 || KL == 3;  // waves split the step's pixels (KL 1 / 3)
+  constexpr bool PIPE = KL >= 2;               // software-pipelined fragment reads (KL 2 / 3)
   typedef WgStage<NR, SC> SG;
   constexpr int PER = NR + 1 + (SC ? 1 : 0);  // LDS-DMA instructions per wave per stage (halo rounds + dy (+ dsc))
   static_assert(!SC || ST == 2, "shortcut fusion: stride 2");
@@ -229,7 +231,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   };
 
   const int wm = wave >> 1, wn = wave & 1;  // KL = 1: wn is the wave's 32-pixel half of the step
-  constexpr int NJ = KL == 1 ? 4 : 2;             // B fragments (16 output channels each) per wave
+  constexpr int NJ = PSPLIT ? 4 : 2;             // B fragments (16 output channels each) per wave
   f32x4 acc[9][NJ];
 #pragma unroll
   for (int i = 0; i < 9; ++i)
@@ -240,7 +242,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   // A = the x halo read transposed at each tap's shift, B = the dy tile read transposed. The step
   // loop is unrolled by NS so each stage base is a constant the ds_read offset field absorbs: the
   // MFMA stream carries no address arithmetic.
-  constexpr int NKS = KL == 1 ? 1 : 2;  // 32-pixel halves a wave computes (KL = 1: its own, at index 0)
+  constexpr int NKS = PSPLIT ? 1 : 2;  // 32-pixel halves a wave computes (KL = 1: its own, at index 0)
   uint32_t aoff[NKS][9][2], boff[NKS][NJ][2];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
@@ -252,19 +254,19 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       const int unit = (cin >> 2) + (lane & 3);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int ra = hm[KL == 1 ? wn : ks][h] + toff;
+        const int ra = hm[PSPLIT ? wn : ks][h] + toff;
         const int f = wg_uswz(ra);
         aoff[ks][i][h] = (uint32_t)(ra * 128 + ((unit ^ f) << 3));
       }
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int cin = KL == 1 ? j * 16 : wn * 32 + j * 16;
+      const int cin = PSPLIT ? j * 16 : wn * 32 + j * 16;
       const int li = lane & 15, q = li >> 2, pp = li & 3, g = lane >> 4;
       const int unit = (cin >> 2) + pp;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int kr = wg_pixel(KL == 1 ? wn : ks, g, h, q);
+        const int kr = wg_pixel(PSPLIT ? wn : ks, g, h, q);
         const int f = wg_uswz(kr);
         boff[ks][j][h] = (uint32_t)(SG::HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
       }
@@ -289,7 +291,24 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
   };
   auto compute = [&](const char* sb) {
-    if constexpr (KL == 2) {
+    if constexpr (PIPE && PSPLIT) {  // KL = 3: the pixel-split layout's 4 B + 9 A fragments, A through the ring
+      bf16x8 bq[4], ar[3];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bq[j] = tr8(sb, boff[0][j][0], boff[0][j][1]);
+      ar[0] = tr8(sb, aoff[0][0][0], aoff[0][0][1]);
+      ar[1] = tr8(sb, aoff[0][1][0], aoff[0][1][1]);
+#pragma unroll
+      for (int f = 0; f < 9; ++f) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (f + 2 < 9) ar[(f + 2) % 3] = tr8(sb, aoff[0][f + 2][0], aoff[0][f + 2][1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[f % 3], bq[j], acc[f][j], 0, 0, 0);
+      }
+      return;
+    }
+    if constexpr (PIPE) {
       // software-pipelined fragment reads (option wgrad_ksplit=2): both k-steps' B fragments first, then the 18
       // A fragments through a three-deep register ring -- fragment f + 2 is read before the MFMAs of f, and
       // scheduling fences keep the compiler from sinking the reads back next to their uses (without them
@@ -309,6 +328,17 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[f % 9][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[f % 3], bfr2[f / 9][j], acc[f % 9][j], 0, 0, 0);
+      }
+      if constexpr (SC) {  // the shortcut (stride 2): centre-tap A fragment x the dsc tile, per k-step
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 af = tr8(sb, aoff_sc[ks][0], aoff_sc[ks][1]);
+          bf16x8 bs[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) bs[j] = tr8(sb, boff[ks][j][0] + 8192, boff[ks][j][1] + 8192);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc_sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bs[j], acc_sc[j], 0, 0, 0);
+        }
       }
       return;
     }
@@ -365,7 +395,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   float* const slab = p.direct ? uniform_ptr(z == 0 ? p.dws[0] : z == 1 ? p.dws[1] : z == 2 ? p.dws[2] : p.dws[3])
                                : p.slab + z * p.slab_stride + (size_t)split * p.K * RSC;
   const float osc = p.direct ? p.scale : 1.f;
-  if constexpr (KL == 1) {
+  if constexpr (PSPLIT) {
     // the two pixel halves' sums: each wave finalises two of its four column fragments (half 0 the
     // first two, half 1 the last two), receiving the other half's partials through LDS in two rounds
     // of fragments (rows i < 5, then i >= 5: 10 / 8 KB per wave). The ring is free after a barrier.
@@ -527,6 +557,7 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
 #define DTC_WGH(NR_, GEN_)                                                                                    \
   if (kl == 1) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 1>), grid, dim3(512), 0, st, p); \
   else if (kl == 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 2>), grid, dim3(512), 0, st, p); \
+  else if (kl == 3) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 3>), grid, dim3(512), 0, st, p); \
   else hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 0>), grid, dim3(512), 0, st, p)
   if (g.gen) {  // general geometry
     if (nr <= 2) { DTC_WGH(2, true); }
@@ -681,7 +712,10 @@ int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* ds
   p.scale = scale;
   const dim3 grid((s.C / 64) * (s.K / 64), used, 1);
   const int nr = (nh + 63) / 64;
-#define DTC_WS2(NR_, SC_, G_) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 2, SC_, G_>), grid, dim3(512), 0, st, p)
+  const bool pipe2 = option_get(OPT_WGRAD_KSPLIT) == 2;  // the pipelined fragment reads (stride-1: KL 2)
+#define DTC_WS2(NR_, SC_, G_)                                                                                 \
+  if (pipe2) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 2, SC_, G_, 2>), grid, dim3(512), 0, st, p);       \
+  else hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 2, SC_, G_, 0>), grid, dim3(512), 0, st, p)
   if (gen) {
     if (nr <= 5) { if (dsc) DTC_WS2(5, true, true); else DTC_WS2(5, false, true); }
     else { if (dsc) DTC_WS2(6, true, true); else DTC_WS2(6, false, true); }

@@ -468,7 +468,7 @@ def test_amp_check_finite_positions(dtc, cuda, n):
     (2, 6, 96, 64, 64),     # 32-pixel segments
     (1, 5, 40, 64, 64),     # one 40-pixel row per step (24 padded slots)
 ])
-@pytest.mark.parametrize("ksplit", [0, 1, 2])
+@pytest.mark.parametrize("ksplit", [0, 1, 2, 3])
 def test_conv_wgrad_halo(dtc, cuda, case, ksplit):
     """Halo-tiled 3x3 weight gradient == generic loader == oracle (fp32 sums of exact products); the rows
     wider than 64 pixels or not dividing 64 run the general-geometry kernels (per-step 64-bit bases, zero-dy
@@ -501,7 +501,7 @@ def test_conv_wgrad_halo(dtc, cuda, case, ksplit):
     (2, 8, 224, 64, 64, 4),    # general geometry (56-pixel row segments), the 224x224 layer1 batch
     (2, 14, 28, 128, 128, 3),  # general geometry, two 28-pixel rows per step
 ])
-@pytest.mark.parametrize("ksplit", [0, 1, 2])
+@pytest.mark.parametrize("ksplit", [0, 1, 2, 3])
 def test_conv_wgrad_batch(dtc, cuda, case, ksplit):
     """dtc_conv2d_wgrad_batch: n independent weight gradients in one halo launch (blockIdx.z =
     problem, 1/n of the splits each) + one reduce launch == the oracle per problem, and == the
