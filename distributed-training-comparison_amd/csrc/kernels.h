@@ -18,7 +18,7 @@ namespace dtc {
   X(DGRAD_CLASSES, dgrad_classes, 1)    /* stride-2 dgrad as output-parity classes */                        \
   X(WGRAD_FAST, wgrad_fast, 1)          /* igemm WGRAD fast loader */                                         \
   X(GRAPHS, graphs, 4)                  /* 0 eager, 1 fwd + bwd hipGraphs, 2 fwd only, 3 bwd only, 4 auto */ \
-  X(WGRAD_HALO, wgrad_halo, 256)        /* target workgroups of the halo WGRAD kernel (0 = igemm only) */   \
+  X(WGRAD_HALO, wgrad_halo, 224)        /* target workgroups of the halo WGRAD kernel (0 = igemm only) */   \
   X(HALO_CONV, halo_conv, 1)            /* halo FWD/DGRAD for 3x3 s1: 0 off, 1 auto, 2+k force cfg k */     \
   X(HALO_SPLIT, halo_split, 0)          /* halo FWD/DGRAD split-K: 0 auto, k forced */                        \
   X(BWD_STREAMS, bwd_streams, 1)        /* weight gradients on a side stream beside the dgrad/BN chain */    \
@@ -48,8 +48,9 @@ namespace dtc {
   X(STEM_WLDS, stem_wlds, 1)            /* stem forward weight staged in LDS */                               \
   X(HALO_S2, halo_s2, 1)                /* stride-2 3x3 FWD on the column-split halo kernel */                \
   X(WGRAD_S2, wgrad_s2, 1)              /* stride-2 wgrad (+ shortcut) on the halo kernel: 0 off, 1 all, 2 GEN */ \
-  X(WGRAD_S2_WGS, wgrad_s2_wgs, 256)    /* stride-2 halo wgrad: target workgroups (split-K slab = wgs x tile) */ \
+  X(WGRAD_S2_WGS, wgrad_s2_wgs, 128)    /* stride-2 halo wgrad: target workgroups (split-K slab = wgs x tile) */ \
   X(WGRAD_KSPLIT, wgrad_ksplit, 2)      /* wgrad_halo: 1 waves split the step's pixels, 2 pipelined fragment reads */ \
+  X(WGRAD_RING, wgrad_ring, 4)          /* wgrad_halo LDS ring stages: 4, or 3 (room for a main-stream workgroup) */ \
   X(DGRAD_SCF, dgrad_scf, 1)            /* shortcut dgrad fused into conv1's parity-class dgrad */            \
   X(BNB_MASK, bnb_mask, 0)              /* BN sums in the producing dgrad's epilogue: 1 all, 2 not c64 */    \
   X(BN_CG, bn_cg, 1)                    /* small BN backward as one launch (bn_bwd_cg) ...                  */ \

@@ -554,8 +554,12 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
   // 4-stage LDS ring (three steps of DMA in flight), compiler-scheduled fragment reads
   const int kl = option_get(OPT_WGRAD_KSPLIT);
+  // option wgrad_ring=3: a three-stage LDS ring (96 / 72 KB instead of 128 / 96 KB), leaving room on the CU
+  // for a main-stream conv workgroup beside the weight-gradient one (pipelined layout only)
+  const bool ring3 = kl == 2 && option_get(OPT_WGRAD_RING) == 3;
 #define DTC_WGH(NR_, GEN_)                                                                                    \
-  if (kl == 1) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 1>), grid, dim3(512), 0, st, p); \
+  if (ring3) hipLaunchKernelGGL((wgrad_halo_kernel<3, NR_, 1, false, GEN_, 2>), grid, dim3(512), 0, st, p);  \
+  else if (kl == 1) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 1>), grid, dim3(512), 0, st, p); \
   else if (kl == 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 2>), grid, dim3(512), 0, st, p); \
   else if (kl == 3) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 3>), grid, dim3(512), 0, st, p); \
   else hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 0>), grid, dim3(512), 0, st, p)

@@ -486,7 +486,7 @@ def test_conv_wgrad_halo(dtc, cuda, case, ksplit):
         dtc._native.lib.dtc_set_option(b"wgrad_halo", 0)
         generic = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
     finally:
-        dtc._native.lib.dtc_set_option(b"wgrad_halo", 256)
+        dtc._native.lib.dtc_set_option(b"wgrad_halo", 224)
         dtc._native.lib.dtc_set_option(b"wgrad_ksplit", 2)
     assert rel_err(halo, ref) < 1e-5
     assert rel_err(generic, ref) < 1e-5
@@ -524,6 +524,29 @@ def test_conv_wgrad_batch(dtc, cuda, case, ksplit):
         one = ones[i]
         assert rel_err(got[i].cpu().numpy(), ref) < 1e-5, i
         assert rel_err(got[i].cpu().numpy(), one) < 1e-6, i
+
+
+@pytest.mark.parametrize("case", [(4, 32, 32, 64, 64, 4), (8, 16, 16, 128, 128, 3), (12, 4, 4, 512, 512, 4),
+                                  (2, 8, 224, 64, 64, 4)])
+def test_conv_wgrad_batch_three_stage_ring(dtc, cuda, case):
+    """Option wgrad_ring=3 (the pipelined weight-gradient kernel with a three-stage LDS ring): identical MFMA
+    order per accumulator, so bit-identical to the four-stage ring, and against the oracle."""
+    N, H, W, C, K, n = case
+    g = np.random.default_rng(13)
+    xs = [_rand_bf16((N, H, W, C), g) for _ in range(n)]
+    dys = [_rand_bf16((N, H, W, K), g) for _ in range(n)]
+    xd = [_to_dev_bf16(a, cuda) for a in xs]
+    dyd = [_to_dev_bf16(a, cuda) for a in dys]
+    lib = dtc._native.lib
+    try:
+        a = [t.cpu().numpy() for t in dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.5)]
+        lib.dtc_set_option(b"wgrad_ring", 3)
+        b = [t.cpu().numpy() for t in dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.5)]
+    finally:
+        lib.dtc_set_option(b"wgrad_ring", 4)
+    for i in range(n):
+        np.testing.assert_array_equal(a[i], b[i])
+        assert rel_err(b[i], 0.5 * O.conv2d_wgrad(xs[i], dys[i], 3, 3, 1, 1)) < 1e-5
 
 
 def test_conv_wgrad_batch_rejects_non_halo(dtc, cuda):

@@ -213,7 +213,7 @@ def test_per_layer_teacher_forced(dtc, cuda, batch):
 
 
 # BASELINE config 2 at its own size (B=256, 32x32): the launches bench.py times -- conv_c64's
-# multi-tile persistent walk, wgrad_halo at 256 splits on layer1, the halo layer2 tiles, split-K
+# multi-tile persistent walk, the batched wgrad_halo split plan on layer1, the halo layer2 tiles, split-K
 # layer3/4 fwd/dgrad/wgrad, the stride-2 parity classes -- against the oracle. Split by stage so each
 # test's numpy work stays well inside the per-test time limit; conv forward / dgrad compared on a
 # sample of 24 images spread over the batch (first, last, tile boundaries), everything that reduces
