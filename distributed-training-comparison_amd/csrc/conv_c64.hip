@@ -509,7 +509,9 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   p.fd_spx = make_fastdiv(p.rows * lw);
   p.fd_w = make_fastdiv(lw);
   p.ts = ts;
-  const int grid = std::min(p.ntiles, 256);
+  // persistent: one workgroup per CU by default (option c64_wgs), each walking ntiles / grid tiles with the
+  // filter resident
+  const int grid = std::min(p.ntiles, std::max(1, option_get(OPT_C64_WGS)));
   const bool in_kernel = fuse && bnb->x2 == nullptr;  // one BN per epilogue (layer1 has no projection)
   if (in_kernel) p.bnb = *bnb;
   const int kmode = mode == CONV_FWD ? 0 : in_kernel ? (res == nullptr ? 3 : 4) : (res == nullptr ? 1 : 2);
