@@ -52,6 +52,7 @@ namespace dtc {
   X(WGRAD_KSPLIT, wgrad_ksplit, 2)      /* wgrad_halo: 1 waves split the step's pixels, 2 pipelined fragment reads */ \
   X(WGRAD_RING, wgrad_ring, 4)          /* wgrad_halo LDS ring stages: 4, or 3 (room for a main-stream workgroup) */ \
   X(C64_WGS, c64_wgs, 256)              /* conv_c64 (layer1) persistent grid size */                          \
+  X(WGRAD_HALO_L1, wgrad_halo_l1, 0)    /* wgrad_halo target for the one-tile (layer1) geometry (0: wgrad_halo) */ \
   X(DGRAD_SCF, dgrad_scf, 1)            /* shortcut dgrad fused into conv1's parity-class dgrad */            \
   X(BNB_MASK, bnb_mask, 0)              /* BN sums in the producing dgrad's epilogue: 1 all, 2 not c64 */    \
   X(BN_CG, bn_cg, 1)                    /* small BN backward as one launch (bn_bwd_cg) ...                  */ \

@@ -499,10 +499,13 @@ static bool wg_geometry(const ConvShape& s, WgGeom& g) {
 }
 
 int wgrad_halo_splits(const ConvShape& s, int nprob) {
-  const int target = option_get(OPT_WGRAD_HALO);
+  int target = option_get(OPT_WGRAD_HALO);
   WgGeom g;
   if (target <= 0 || nprob < 1 || nprob > DTC_WG_BATCH || !wg_geometry(s, g)) return 0;
   const int tiles = (s.C / 64) * (s.K / 64);
+  // option wgrad_halo_l1: the target of the one-tile (64 -> 64 channel, layer1) geometry, whose batch runs in the
+  // backward's tail beside the stem chain (0: wgrad_halo's)
+  if (tiles == 1 && option_get(OPT_WGRAD_HALO_L1) > 0) target = option_get(OPT_WGRAD_HALO_L1);
   int splits = std::max(1, target / (tiles * nprob));
   splits = (int)std::min<int64_t>(splits, std::max<int64_t>(1, g.nsteps / 4));  // >= 4 pixel steps per workgroup
   return splits;

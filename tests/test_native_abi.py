@@ -145,7 +145,7 @@ _OPTION_DEFAULTS = {
     "halo_s2": 1, "wgrad_s2": 1, "dgrad_scf": 1, "bnb_mask": 0, "bucket_tail": 1, "halo_stage_epi": 0, "wgrad_gen": 1,
     "halo_gen": 1, "bn_red_unroll": 4, "c64_gen": 1, "graphs": 4, "head_fused": 1,
     # round 4
-    "bn_cg": 1, "bn_cg_elems": 262144, "wgrad_s2_wgs": 128, "comm_on_side": 1, "wgrad_ksplit": 2, "wgrad_ring": 4, "c64_wgs": 256,
+    "bn_cg": 1, "bn_cg_elems": 262144, "wgrad_s2_wgs": 128, "comm_on_side": 1, "wgrad_ksplit": 2, "wgrad_ring": 4, "c64_wgs": 256, "wgrad_halo_l1": 0,
 }
 # measured-negative variants deleted in round 4 with their code paths (DESIGN.md keeps their numbers)
 _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", "wgrad_pmap", "wgrad_prio",
