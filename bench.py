@@ -328,6 +328,8 @@ def main():
     ap.add_argument("--sync-bn", action="store_true",
                     help="SyncBatchNorm (off in the reference); at N=1 a one-rank communicator forces the sync path")
     ap.add_argument("--opt", action="append", default=[], help="native option NAME=VALUE (A/B runs)")
+    ap.add_argument("--stream-prio", type=int, default=0,
+                    help="run the step on a torch stream of this priority (-1 = high; 0 = torch's default stream)")
     args = ap.parse_args()
     if args.mode == "dp":
         return bench_dp(args)
@@ -376,6 +378,9 @@ def main():
 
     pools = {B: make_pool(B)}
     losses = []
+    if args.stream_prio:  # A/B: the caller's stream (the executor's main chain) at another hardware priority
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=args.stream_prio))
 
     def step(i, b=B, host_sync=True):
         img, label = pools[b][i % len(pools[b])]

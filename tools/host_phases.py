@@ -2,7 +2,7 @@
 
 Replicates bench.py's step and stamps time.perf_counter() after each phase; a phase that blocks
 on the device (barrier, item) shows the GPU time it waited for, the others show pure host cost.
-Usage: python tools/host_phases.py [--steps 50] [--batch 256] [--no-barrier] [--cprofile]"""
+Usage: python tools/host_phases.py [--steps 50] [--batch 256] [--loopback W] [--no-barrier] [--cprofile]"""
 import argparse
 import os
 import sys
@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--no-barrier", action="store_true")
     ap.add_argument("--torch-barrier", action="store_true", help="dist.barrier() instead of bench.py's dtc.barrier()")
     ap.add_argument("--cprofile", action="store_true", help="cProfile the timed steps (top functions by tottime)")
+    ap.add_argument("--loopback", type=int, default=0, help="one rank of a W-rank job: loopback communicator, 1/W")
     ap.add_argument("--spin", action="store_true", help="hipSetDeviceFlags(hipDeviceScheduleSpin) before init")
     args = ap.parse_args()
     if args.spin:
@@ -35,6 +36,9 @@ def main():
     dtc = dtc_import.load()
     torch.manual_seed(42)
     model = dtc.DDP(dtc.ResNet18().to(dev), device_ids=[local], find_unused_parameters=True)
+    if args.loopback > 1:  # as bench.py --sim-world W --sim-comm loopback
+        model.module._comm = dtc.parallel.Comm.loopback(local, factor=1.0, world=args.loopback)
+        model.module._grad_scale = 1.0 / args.loopback
     crit = dtc.CrossEntropyLoss()
     opt = dtc.SGD(model.parameters(), lr=0.1, weight_decay=1e-4, momentum=0.9, nesterov=True)
     scaler = dtc.GradScaler()
