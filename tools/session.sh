@@ -1,5 +1,4 @@
 # scratch GPU session (overwritten per session; see tools/gpu_run.sh for the standard steps)
+S8='--sim-world 8 --global-batch 256 --sim-comm loopback'
 tools/gpu_session.sh \
-  "r04aj_smoke|200|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "r04aj_bench|200|python bench.py > gpurun_out/r04aj_bench.json" \
-  "r04aj_tests|800|python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread"
+  "r04ak_w8prof|300|tools/prof_run.sh r04ak_w8 $S8"
