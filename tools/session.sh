@@ -1,4 +1,3 @@
 # scratch GPU session (overwritten per session; see tools/gpu_run.sh for the standard steps)
-S8='--sim-world 8 --global-batch 256 --sim-comm loopback'
 tools/gpu_session.sh \
-  "r04ak_w8prof|300|tools/prof_run.sh r04ak_w8 $S8"
+  "r04al_ab|600|tools/bench_ab.sh 3 'base|' 'q2|ENV:GPU_MAX_HW_QUEUES=2;' 'q3|ENV:GPU_MAX_HW_QUEUES=3;' 'q8|ENV:GPU_MAX_HW_QUEUES=8;'"
