@@ -80,6 +80,28 @@ def spawn_ranks(n: int, argv: list, script: str = None, poll_s: float = 0.2) -> 
     return rc
 
 
+def visible_gpus(env=None, kfd="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs this process could use, counted WITHOUT the HIP runtime (the launcher must not
+    initialise the GPU before it starts the rank processes): the length of a *_VISIBLE_DEVICES list if
+    one is set, else the KFD topology nodes with SIMDs (GPU agents; CPU nodes report simd_count 0).
+    None when neither is available: the ranks then report a missing device themselves."""
+    env = os.environ if env is None else env
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(k)
+        if v is not None:
+            return len([d for d in v.split(",") if d.strip() != ""])
+    try:
+        n = 0
+        for node in os.listdir(kfd):
+            with open(os.path.join(kfd, node, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if line.strip())
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+        return n
+    except (OSError, ValueError):
+        return None
+
+
 def init_dist(gpus: int = 1):
     if "RANK" not in os.environ:  # one rank, no launcher: an in-process store (no TCP port to race for)
         os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
@@ -106,20 +128,41 @@ def check_world(world: int, gpus: int) -> None:
 BN_IDEAL_BYTES_PER_IMAGE = 6.144e6  # non-GEMM HBM bytes per 32x32 image at ideal fusion
 
 
-def _committed_traffic():
-    """HBM bytes per conv call from the newest committed PMC summary (profiles/*conv_traffic.json,
-    written by tools/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench);
-    PMC counters cannot be read live, so the value is the profile's, named in traffic_source."""
+def profile_order_key(name: str):
+    """Sort key of a committed profile file name, oldest first: round number, then the session tag in
+    the order the tags were handed out (a..z, then aa..az, ...: shorter tags are older), e.g.
+    r04u_... < r04ad_... < r05a_... (a plain lexicographic sort put r04u after r04ad: VERDICT r4 weak 6)."""
+    import re
+
+    m = re.match(r"r(\d+)_?([a-z0-9]*?)_", os.path.basename(name))
+    if not m:
+        return (-1, 0, "")
+    return (int(m.group(1)), len(m.group(2)), m.group(2))
+
+
+TRAFFIC_WORKLOAD = (256, 32)  # (per-GPU batch, image size) of tools/pmc_bench.sh's bench.py run
+
+
+def committed_traffic(batch: int, size: int, path: str = None):
+    """(HBM bytes per conv call, source) from a committed PMC summary (profiles/*conv_traffic.json, written
+    by tools/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of bench.py's default workload).
+    PMC counters cannot be read live, so the value is the profile's and `source` names the file: `path` if
+    given, else the newest by round and session (profile_order_key). None for another workload: the file
+    measured B=256 at 32x32 only."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                          "*conv_traffic.json")))
-    if not files:
-        return None
+    if path is None:
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*conv_traffic.json")), key=profile_order_key)
+        if not files:
+            return None, None
+        path = files[-1]
+    src = os.path.relpath(path, ROOT)
+    if (batch, size) != TRAFFIC_WORKLOAD:
+        return None, f"{src} measured batch {TRAFFIC_WORKLOAD[0]} at {TRAFFIC_WORKLOAD[1]}x{TRAFFIC_WORKLOAD[1]}: not this workload"
     try:
-        return round(json.load(open(files[-1]))["hbm_bytes_per_call"], 1)
-    except Exception:
-        return None
+        return round(json.load(open(path))["hbm_bytes_per_call"], 1), src
+    except Exception as e:
+        return None, f"{src}: unreadable ({e!r})"
 
 
 def host_cores() -> dict:
@@ -328,15 +371,17 @@ def main():
     ap.add_argument("--sync-bn", action="store_true",
                     help="SyncBatchNorm (off in the reference); at N=1 a one-rank communicator forces the sync path")
     ap.add_argument("--opt", action="append", default=[], help="native option NAME=VALUE (A/B runs)")
+    ap.add_argument("--traffic-file", default=None,
+                    help="PMC conv-traffic summary for roofline.traffic (default: the newest profiles/*conv_traffic.json)")
     ap.add_argument("--stream-prio", type=int, default=0,
                     help="run the step on a torch stream of this priority (-1 = high; 0 = torch's default stream)")
     args = ap.parse_args()
     if args.mode == "dp":
         return bench_dp(args)
     if args.gpus > 1 and "RANK" not in os.environ:
-        # no launcher: start the ranks here (device_count does not initialise the GPU on this image)
-        have = torch.cuda.device_count()
-        if have < args.gpus:
+        # no launcher: start the ranks here, before anything in this process touches HIP
+        have = visible_gpus()
+        if have is not None and have < args.gpus:
             raise SystemExit(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible")
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
@@ -425,6 +470,7 @@ def main():
     ms4, fl4, cnt4 = (C.c_double * 4)(), (C.c_double * 4)(), (C.c_int * 4)()  # events
     sms4, sfl4, scnt4 = (C.c_double * 4)(), (C.c_double * 4)(), (C.c_int * 4)()  # stamps
     prof_elapsed = None
+    ev_dropped = C.c_int64(0)  # timed calls the event pool could not bracket: the totals then undercount
     if not args.no_live_roofline:
         exe = model.module.executor(B, S, S, "bf16")
         saved = {k: int(dtc._native.lib.dtc_get_option(k)) for k in (b"bwd_streams", b"graphs")}
@@ -441,6 +487,7 @@ def main():
         # so an event pair times its launch, not a launch plus the host catching up after a drain)
         prof_elapsed = timed(args.steps, args.warmup + args.steps + 2, host_sync=False)
         dtc._native.call("dtc_rn18_profile_events_result", exe.handle, 4, ms4, fl4, cnt4)
+        dtc._native.call("dtc_rn18_profile_events_dropped", exe.handle, C.byref(ev_dropped))
         dtc._native.call("dtc_rn18_profile_end_ex", exe.handle, 4, sms4, sfl4, scnt4)
         for k, v in saved.items():
             dtc._native.call("dtc_set_option", k, v)
@@ -486,8 +533,10 @@ def main():
     if rank == 0:
         conv_ms = sum(ms)
         conv_flops = sum(fl)
+        traffic, traffic_src = committed_traffic(B, S, args.traffic_file)
         n_launch = sum(cnt)
-        achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
+        # refuse a fraction whose time total misses launches (event pool used up) -- it would be overstated
+        achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 and ev_dropped.value == 0 else None
         value = B * world * args.steps / elapsed
         if args.global_batch:
             metric = (f"images/sec/node ResNet-18 CIFAR-100 DDP (global batch {args.global_batch} over "
@@ -527,7 +576,8 @@ def main():
                 "peak": BF16_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / BF16_PEAK_TFLOPS, 4) if achieved else None,
-                "traffic": _committed_traffic(),
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "every conv launch of the step (stem, halo / c64 / implicit-GEMM fwd, dgrad, wgrad incl. "
                           "split-K and wgrad reductions); per-call duration = HIP timing events recorded on the "
                           "launch (compute) stream before and after the call, in a second timed region of the same "
@@ -545,6 +595,7 @@ def main():
                 "region_ms_per_step": round(prof_elapsed / args.steps * 1e3, 4) if prof_elapsed else None,
                 "conv_ms_by_pass": [round(v / args.steps, 4) for v in ms],
                 "conv_calls_per_step": n_launch // max(1, args.steps),
+                "unbracketed_calls": int(ev_dropped.value),
                 "algorithmic_gflop_per_step": round(conv_flops / args.steps / 1e9, 3),
             },
             "hbm_roofline": hbm,

@@ -123,6 +123,7 @@ struct Net {
   hipStream_t prof_st = nullptr;
   std::vector<hipEvent_t> prof_evpool;  // 2 per bracketed call, created up front
   size_t prof_evn = 0;                  // pairs used
+  long long prof_evdropped = 0;         // calls that found the pool used up (not bracketed: reported)
   std::vector<std::pair<int, double>> prof_evwork;  // (kind, work) per pair
   // hipGraph replay (option "graphs"): the forward per train flag, the backward as segments split
   // at bucket boundaries (the all-reduces stay eager on the communicator's side stream)
@@ -443,8 +444,11 @@ static bool side_on(const Net& n);
 // gradients on a side stream the compute-stream events would not cover, or the pool used up)
 static int prof_ev_open(Net& n, int kind, double work) {
   // (prof_st may be the null stream: the caller's default stream)
-  if (!n.profiling || !n.prof_events || n.cap_locked || side_on(n) || n.prof_evn * 2 + 1 >= n.prof_evpool.size())
+  if (!n.profiling || !n.prof_events || n.cap_locked || side_on(n)) return -1;
+  if (n.prof_evn * 2 + 1 >= n.prof_evpool.size()) {  // pool used up: counted, so the caller can refuse the total
+    ++n.prof_evdropped;
     return -1;
+  }
   const int i = (int)n.prof_evn++;
   if (n.prof_evwork.size() < n.prof_evn) n.prof_evwork.resize(n.prof_evn);
   n.prof_evwork[i] = {kind, work};
@@ -1705,6 +1709,7 @@ int dtc_rn18_profile_events(dtc_net* net, int pairs) {
   Net& n = net->n;
   n.prof_events = pairs > 0;
   n.prof_evn = 0;
+  n.prof_evdropped = 0;
   const size_t want = (size_t)pairs * 2;
   while (n.prof_evpool.size() < want) {
     hipEvent_t e;
@@ -1737,6 +1742,12 @@ int dtc_rn18_profile_events_result(dtc_net* net, int nkinds, double* ms_by_kind,
   }
   n.prof_evn = 0;
   n.prof_events = false;
+  return 0;
+}
+
+int dtc_rn18_profile_events_dropped(dtc_net* net, long long* dropped) {
+  DTC_CHECK_ARG(net != nullptr && dropped != nullptr, "dtc_rn18_profile_events_dropped: bad args");
+  *dropped = net->n.prof_evdropped;
   return 0;
 }
 

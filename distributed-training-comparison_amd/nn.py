@@ -236,6 +236,8 @@ class _NetFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dlogits):
         model, exe = ctx.model, ctx.exe
+        if model._pre_backward is not None:
+            model._pre_backward()
         exe.consume(ctx.gen)
         exe.backward(dlogits.contiguous().float(), model._grad_scale, model._comm)
         model._ensure_grads()
@@ -245,13 +247,16 @@ class _NetFn(torch.autograd.Function):
 class _HostWords:
     """A ring of pinned host words the loss launch writes its value into (the item() read). The ring is
     owned here, not by torch's pinned-memory cache: a word a kernel may still write is never handed to
-    another tensor. Reusing a slot first waits for the event of the step that last wrote it."""
+    another tensor. Reusing a slot first waits for the event of the step that last wrote it, and bumps
+    the slot's generation: a loss that still holds the slot's earlier generation (kept past N newer
+    losses) sees the mismatch in item() and reads its own device value instead."""
 
     N = 256
 
     def __init__(self):
         self.buf = torch.empty(self.N, dtype=torch.float32, pin_memory=True)
         self.events = [None] * self.N
+        self.gens = [0] * self.N
         self.i = 0
         self.mu = threading.Lock()  # rank threads of the thread-group communicator share the ring
 
@@ -261,9 +266,15 @@ class _HostWords:
             self.i += 1
             ev = self.events[k]
             self.events[k] = None
+            self.gens[k] += 1
+            gen = self.gens[k]
         if ev is not None:
             ev.synchronize()
-        return k, self.buf[k]
+        return k, self.buf[k], gen
+
+    def owns(self, k, gen):
+        """True while slot k still holds the value of the loss that took it as generation `gen`."""
+        return self.gens[k] == gen
 
     def done(self, k, ev):
         self.events[k] = ev
@@ -315,6 +326,8 @@ class NativeLoss(torch.Tensor):
         node, logits, labels, lse, gscale = fast
         if isinstance(node, _NetFn._backward_cls):
             model, exe = node.model, node.exe
+            if model._pre_backward is not None:
+                model._pre_backward()
             exe.consume(node.gen)
             exe.xent_backward(logits, labels, lse, gscale, model._grad_scale, model._comm)
             model._ensure_grads()
@@ -333,7 +346,10 @@ class NativeLoss(torch.Tensor):
         hc = getattr(self, "_dtc_host", None)
         if hc is None:
             return super().item()
-        h, ev = hc
+        h, ev, ring = hc[0], hc[1], hc[2:]
+        if ring and not ring[0].owns(ring[1], ring[2]):  # the slot went to a newer loss: own device value
+            self._dtc_host = None
+            return super().item()
         ev.synchronize()
         return h.item()
 
@@ -427,7 +443,8 @@ class CrossEntropyLoss(nn.Module):
                     sc = _prescaler()
                     if _HOST_WORDS[0] is None:
                         _HOST_WORDS[0] = _HostWords()
-                    slot, host = _HOST_WORDS[0].take()
+                    ring = _HOST_WORDS[0]
+                    slot, host, gen = ring.take()
                     n, ncls = logits.shape
                     dev = logits.device
                     loss = torch.empty((), dtype=torch.float32, device=dev)
@@ -438,9 +455,9 @@ class CrossEntropyLoss(nn.Module):
                          None if scaled is None else scaled.data_ptr(), host.data_ptr(), _raw_stream(dev.index))
                     ev = torch.cuda.Event()
                     ev.record()
-                    _HOST_WORDS[0].done(slot, ev)
+                    ring.done(slot, ev)
                     out = _wrap_loss(loss, lambda: _XentFn.apply(logits, labels), (node, logits, labels, lse, None))
-                    out._dtc_host = (host, ev)
+                    out._dtc_host = (host, ev, ring, slot, gen)
                     if sc is not None:
                         prescale(out, scaled, sc)
                     return out
@@ -496,6 +513,7 @@ class ResNet(nn.Module):
         self._anchor: Optional[torch.Tensor] = None
         self._comm = None
         self._grad_scale = 1.0
+        self._pre_backward = None  # set by DistributedDataParallel: runs before every native backward
         self._bucket_cap_mb = float(bucket_cap_mb)
         self._capture = False
         self._sync_bn = False  # SyncBatchNorm.convert_sync_batchnorm marks the module

@@ -249,6 +249,7 @@ class DistributedDataParallel(nn.Module):
                 self.sync_comm = sync_comm if sync_comm is not None else Comm.from_process_group(
                     device, getattr(module, "_sync_bn_group", None) or process_group)
                 module.set_sync_bn(self.sync_comm)
+                module._pre_backward = self._flush_sync_bn_check
             # C1: make every replica start from rank 0's state -- on the Reducer's communicator,
             # ordered after the caller's stream (the module's parameters were written there)
             self.comm.broadcast_(flat.params, 0)
@@ -270,10 +271,10 @@ class DistributedDataParallel(nn.Module):
         (n, n^2) on the SyncBN communicator: sizes are equal iff W * sum(n^2) == sum(n)^2), so the
         ranks' collectives always match (no per-rank cache deciding who enters). Whether the
         host waits is decided the same way on every rank: the FIRST check is waited for
-        (every rank is on its first training forward), every later one is read at the next training
-        forward, long since complete. A batch size that changes on one rank after the first step is
-        therefore refused one step late, but on every rank at the same step: no rank ever waits for a
-        result while another has gone on into the forward's SyncBN all-reduces."""
+        (every rank is on its first training forward), every later one is read before that forward's
+        backward (_flush_sync_bn_check) or, for a forward without backward, at the next training forward. A batch size that changes on one rank after the first step is therefore refused before
+        that step's backward, on every rank at the same step: no rank ever waits for a result while
+        another has gone on into the forward's SyncBN all-reduces."""
         n = int(x.shape[0])
         dev = self.module.flat.device
         if self._cnt is None:
@@ -294,6 +295,18 @@ class DistributedDataParallel(nn.Module):
         if st["first"]:
             st["first"] = False
             ev.synchronize()
+            st["ev"] = None
+            self._assert_equal_batches(st["host"])
+
+    def _flush_sync_bn_check(self) -> None:
+        """Before the native backward of a training step: read this step's pending batch-size
+        check (its 2-double all-reduce was issued before the forward's SyncBN collectives, so it has long
+        completed once the backward is issued after the reference's per-step barrier). Every rank reads it
+        at the same point of the same step, so unequal shards are refused on every rank BEFORE their
+        backward and optimizer step -- also on the last step of training -- instead of one forward late."""
+        st = self._cnt
+        if st is not None and st["ev"] is not None:
+            st["ev"].synchronize()
             st["ev"] = None
             self._assert_equal_batches(st["host"])
 

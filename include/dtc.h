@@ -357,6 +357,10 @@ int dtc_rn18_profile_end_ex(dtc_net* net, int nkinds, double* ms_by_kind, double
 int dtc_rn18_profile_events(dtc_net* net, int pairs);
 int dtc_rn18_profile_events_result(dtc_net* net, int nkinds, double* ms_by_kind, double* work_by_kind,
                                    int* count_by_kind);
+/* Timed launcher calls since the last dtc_rn18_profile_events() that were NOT bracketed because the event
+ * pool was used up (`pairs` too small for the region): their durations are missing from _result's totals,
+ * so a caller reporting a roofline from them must refuse it when this is non-zero. */
+int dtc_rn18_profile_events_dropped(dtc_net* net, long long* dropped);
 
 #ifdef __cplusplus
 }

@@ -72,3 +72,53 @@ def test_bench_refuses_more_gpus_than_visible():
     assert r.returncode != 0
     assert "GPU(s) visible" in r.stderr
     assert r.stdout.strip() == ""
+
+
+def test_visible_gpus_counts_without_hip(bench, tmp_path):
+    """the launcher counts GPUs from the environment or the KFD topology, never through HIP."""
+    assert bench.visible_gpus({"HIP_VISIBLE_DEVICES": "0,1,2"}) == 3
+    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": ""}) == 0
+    nodes = tmp_path / "nodes"
+    for i, simd in enumerate((0, 256, 256)):  # a CPU node and two GPU agents
+        d = nodes / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {simd}\n")
+    assert bench.visible_gpus({}, kfd=str(nodes)) == 2
+    assert bench.visible_gpus({}, kfd=str(tmp_path / "missing")) is None
+
+
+def test_traffic_file_selection_by_round_and_session(bench):
+    """the newest PMC summary by round and session (r04ad after r04u), named in the line,
+    and no traffic figure for a workload the summary did not measure."""
+    names = ["profiles/r02_n_conv_traffic.json", "profiles/r04u_conv_traffic.json", "profiles/r04ad_conv_traffic.json",
+             "profiles/r03ah_conv_traffic.json", "profiles/r01_s4_conv_traffic.json"]
+    assert sorted(names, key=bench.profile_order_key)[-1] == "profiles/r04ad_conv_traffic.json"
+    assert sorted(names + ["profiles/r05a_conv_traffic.json"], key=bench.profile_order_key)[-1].endswith("r05a_conv_traffic.json")
+    val, src = bench.committed_traffic(256, 32)
+    files = sorted([f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("conv_traffic.json")],
+                   key=bench.profile_order_key)
+    assert src == os.path.join("profiles", files[-1])
+    assert val == round(json.load(open(os.path.join(ROOT, src)))["hbm_bytes_per_call"], 1)
+    val32, src32 = bench.committed_traffic(32, 32)
+    assert val32 is None and "not this workload" in src32
+
+
+def test_prof_summary_flops_follow_the_bench_batch(tmp_path):
+    """a trace summary's fraction uses its own bench line's batch and size, and no
+    fraction is printed without one (a B=256 figure divided by a B=32 trace's conv time read 0.51)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import prof_summary as ps
+
+    line = {"roofline": {"algorithmic_gflop_per_step": 0.0}, "config": {"per_gpu_batch": 32, "image_size": 32}}
+    f = tmp_path / "b.json"
+    f.write_text(json.dumps(line) + "\n")
+    g, _ = ps.bench_gflop(str(f))
+    assert abs(g - 852.215 / 8) < 1e-6
+    line["config"] = {"per_gpu_batch": 512, "image_size": 224}
+    f.write_text(json.dumps(line) + "\n")
+    assert abs(ps.bench_gflop(str(f))[0] - 852.215 * 2 * 49) < 1e-3
+    line["roofline"]["algorithmic_gflop_per_step"] = 123.0
+    f.write_text(json.dumps(line) + "\n")
+    assert ps.bench_gflop(str(f))[0] == 123.0
+    f.write_text("not json\n")
+    assert ps.bench_gflop(str(f))[0] is None

@@ -231,6 +231,34 @@ def test_sync_batchnorm_batch_change_on_one_rank_refused_on_every_rank(dtc, cuda
     assert res[0][0] == res[1][0] == 2, res  # refused one step late, on both ranks together
 
 
+def test_sync_batchnorm_batch_change_refused_before_that_steps_backward(dtc, cuda):
+    """with training steps (forward, loss, backward) the pending batch-size check is read before
+    the native backward, so a mismatch on the LAST step is still refused -- on every rank, at that step's
+    backward, before any gradient of it is written or all-reduced."""
+    world = 2
+    comms = dtc.parallel.Comm.thread_group(cuda.index or 0, world)
+    syncs = dtc.parallel.Comm.thread_group(cuda.index or 0, world)
+    models = [_model(dtc, cuda, 25.0, sync_bn=True) for _ in range(world)]
+
+    def rank(r):
+        ddp = dtc.DistributedDataParallel(models[r], device_ids=[0], comm=comms[r], sync_comm=syncs[r])
+        crit = dtc.CrossEntropyLoss()
+        for step, b in enumerate((8, 8 + 4 * r)):  # the mismatch is on the final step
+            x = torch.randn(b, 3, 32, 32, device=cuda)
+            y = torch.randint(0, 100, (b,), device=cuda)
+            with dtc.autocast():
+                loss = crit(ddp(x), y)
+            try:
+                loss.backward()
+            except dtc.NativeError as e:
+                return step, str(e)
+        return None
+
+    res = _run_ranks(rank, world)
+    assert all(x is not None and "batch sizes differ" in x[1] for x in res), res
+    assert res[0][0] == res[1][0] == 1, res
+
+
 def test_thread_group_barrier_and_mismatch(dtc, cuda):
     """dtc_barrier over the thread group returns on every rank only after all ranks called it and each
     rank's own queued work finished; mismatched collectives are reported to every rank, not hung."""

@@ -332,14 +332,16 @@ def _head_and_loss(dtc, cuda):
     assert rel_err(dact.float().cpu().numpy(), dact_ref) < 1e-2
 
 
-@pytest.mark.parametrize("n", [1, 6, 256, 300, 4096])
-def test_xent_fwd_one_launch(dtc, cuda, n):
+@pytest.mark.parametrize("n,ncls", [(1, 100), (6, 100), (256, 100), (300, 100), (4096, 100), (7, 10), (256, 10),
+                                    (65, 129), (300, 129), (1000, 1000), (33, 1000)])
+def test_xent_fwd_one_launch(dtc, cuda, n, ncls):
     """dtc_xent_fwd_ex (the training step's loss in one launch): loss and lse bit-identical to the
     two-kernel dtc_xent_fwd, scaled = loss * scale (amp_scale's multiply), the loss in a pinned host word;
-    and against the oracle."""
-    g = torch.Generator(device=cuda).manual_seed(n)
-    logits = torch.randn(n, 100, device=cuda, generator=g) * 3
-    lab = torch.randint(0, 100, (n,), device=cuda, generator=g)
+    and against the oracle. ADVICE r4: heads wider than 128 classes take the kernel's per-row branch
+    (ncls 129 / 1000), and row counts that are not multiples of 64 / 256 / 1024 are covered."""
+    g = torch.Generator(device=cuda).manual_seed(n * 1000 + ncls)
+    logits = torch.randn(n, ncls, device=cuda, generator=g) * 3
+    lab = torch.randint(0, ncls, (n,), device=cuda, generator=g)
     loss0, lse0 = dtc.ops.xent_fwd(logits, lab)
     scale = torch.full((), 65536.0, device=cuda)
     loss = torch.empty((), device=cuda)
@@ -347,7 +349,7 @@ def test_xent_fwd_one_launch(dtc, cuda, n):
     scaled = torch.empty((), device=cuda)
     host = torch.full((4,), -1.0).pin_memory()
     P = dtc._native.ptr
-    dtc._native.call("dtc_xent_fwd_ex", P(logits), P(lab), n, 100, P(loss), P(lse), P(scale), P(scaled),
+    dtc._native.call("dtc_xent_fwd_ex", P(logits), P(lab), n, ncls, P(loss), P(lse), P(scale), P(scaled),
                      host[1:2].data_ptr(), dtc._native.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(loss, loss0) and torch.equal(lse, lse0)
@@ -355,11 +357,20 @@ def test_xent_fwd_one_launch(dtc, cuda, n):
     assert float(host[1]) == float(loss) and float(host[0]) == -1.0 and float(host[2]) == -1.0
     loss_ref, _, lse_ref = O.cross_entropy(logits.cpu().numpy(), lab.cpu().numpy())
     assert abs(float(loss) - loss_ref) < 1e-5 * max(1.0, abs(loss_ref))
+    np.testing.assert_allclose(lse.cpu().numpy(), lse_ref, rtol=1e-5, atol=1e-5)
     # without the optional outputs
-    dtc._native.call("dtc_xent_fwd_ex", P(logits), P(lab), n, 100, P(loss), P(lse), None, None, None,
+    dtc._native.call("dtc_xent_fwd_ex", P(logits), P(lab), n, ncls, P(loss), P(lse), None, None, None,
                      dtc._native.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(loss, loss0)
+    # an out-of-range label makes the loss NaN on both paths (torch raises; the kernels flag it in the value)
+    bad = lab.clone()
+    bad[n // 2] = ncls
+    loss1, _ = dtc.ops.xent_fwd(logits, bad)
+    dtc._native.call("dtc_xent_fwd_ex", P(logits), P(bad), n, ncls, P(loss), P(lse), None, None, None,
+                     dtc._native.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.isnan(loss).item() and torch.isnan(loss1).item()
 
 
 def test_stem_im2col(dtc, cuda):

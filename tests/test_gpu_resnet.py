@@ -1088,6 +1088,28 @@ def test_native_loss_item_and_dlogits_buffer(dtc, cuda):
     assert np.isfinite(vals).all()
 
 
+def test_native_loss_item_after_host_ring_wraps(dtc, cuda):
+    """a loss kept past the pinned host-word ring's N newer losses must not read the value a
+    later launch wrote into its reused slot: item() falls back to the loss's own device value."""
+    from importlib import import_module
+
+    nnmod = import_module(type(dtc.CrossEntropyLoss()).__module__)
+    model, _, x, y = _setup(dtc, cuda, 2, seed=5)
+    crit = dtc.CrossEntropyLoss()
+    xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
+    first = crit(model(xd), yd)
+    v0 = float(first.detach().cpu())
+    n = nnmod._HostWords.N
+    held = [first]
+    with dtc.autocast():  # a different value in every later slot (bf16 logits)
+        for i in range(n + 4):
+            held.append(crit(model(xd * (1.0 + 0.01 * (i + 1))), yd))
+    torch.cuda.synchronize()
+    assert first.item() == v0
+    for ls in held[-4:]:  # the newest losses still read their own slots
+        assert ls.item() == float(ls.detach().cpu())
+
+
 def test_data_parallel_replicas_match_chunked_single(dtc, cuda):
     """DataParallel (reference src/dp/trainer.py:27) with two replicas on cuda:0 (device_ids=[0, 0]:
     the one-GPU form of scatter / replicate / parallel_apply / gather / reduce-add) against the

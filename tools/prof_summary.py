@@ -5,8 +5,9 @@ usage: python tools/prof_summary.py <rocprof output dir> <out.md> [--bench bench
 Reports: top kernels (calls, total, average), the conv family (every conv launch bench.py's
 `roofline` times: igemm, halo, c64, wgrad_halo, stem fwd / wgrad, and their split-K / wgrad
 reductions) per training step with its achieved TFLOP/s and fraction of the bf16 dense peak
-(algorithmic conv FLOPs per step, SURVEY §8(d): 852.2 GFLOP at B=256, 32x32 -- or --gflop-per-step,
-or the bench line's algorithmic_gflop_per_step), and the per-step timeline of the steady state (busy
+(algorithmic conv FLOPs per step, SURVEY §8(d): 852.2 GFLOP at B=256, 32x32 -- --gflop-per-step, else the
+bench line's algorithmic_gflop_per_step, else 3.329 GFLOP x its per-GPU batch x (size / 32)^2; no fraction
+without one of them), and the per-step timeline of the steady state (busy
 time vs wall time between the first and last kernel of a step, i.e. launch gaps). A training step is
 delimited by the SGD kernel (one launch per step). Run it on a trace of the SERIALIZED step
 (`--opt bwd_streams=0`: no side-stream overlap, every kernel's duration is its own) to reproduce
@@ -29,6 +30,29 @@ def short(name):
     return n.split("(")[0]
 
 
+CONV_GFLOP_PER_IMAGE = 852.215 / 256  # conv fwd + dgrad + wgrad per 32x32 image
+
+
+def bench_gflop(bench):
+    """(algorithmic conv GFLOP per step, source) of the bench.py line the trace was taken with: the line's
+    own live-roofline figure when it measured one, else conv GFLOP per image x its per-GPU batch x
+    (image size / 32)^2 (every conv scales with the pixel count). (None, reason) when the line is missing
+    or names no batch: no fraction is printed then (a B=256 figure was divided by a
+    B=32 trace's conv time)."""
+    try:
+        b = json.loads([l for l in open(bench) if l.startswith("{")][-1])
+    except Exception as e:
+        return None, f"bench line unreadable ({e!r})"
+    g = (b.get("roofline") or {}).get("algorithmic_gflop_per_step") or 0.0
+    if g > 0:
+        return g, "bench line roofline.algorithmic_gflop_per_step"
+    cfg = b.get("config") or {}
+    B, S = cfg.get("per_gpu_batch"), cfg.get("image_size", 32)
+    if not B:
+        return None, "bench line names no per_gpu_batch"
+    return CONV_GFLOP_PER_IMAGE * B * (S / 32) ** 2, f"{CONV_GFLOP_PER_IMAGE:.4f} GFLOP/image x batch {B} x ({S}/32)^2"
+
+
 def load_rows(src):
     """(start_ns, end_ns, kernel name) per dispatch from a csv kernel trace or a rocpd sqlite db."""
     trace = glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True)
@@ -49,12 +73,9 @@ def main():
     args = sys.argv[3:]
     bench = args[args.index("--bench") + 1] if "--bench" in args else None
     gflop = float(args[args.index("--gflop-per-step") + 1]) if "--gflop-per-step" in args else None
+    gsrc = "--gflop-per-step" if gflop else None
     if gflop is None and bench:
-        try:
-            gflop = json.loads([l for l in open(bench) if l.startswith("{")][-1])["roofline"]["algorithmic_gflop_per_step"]
-        except Exception:
-            gflop = None
-    gflop = gflop or 852.215
+        gflop, gsrc = bench_gflop(bench)
     rows = load_rows(src)
     rows.sort()
     # steps: delimited by the fused SGD kernel
@@ -111,9 +132,13 @@ def main():
                   f"* wall (first kernel start to last kernel end): {avg(wall):.1f} us",
                   f"* GPU busy (union of kernel intervals): {avg(busy):.1f} us "
                   f"({100 * sum(busy) / sum(wall):.1f}% of wall)",
-                  f"* conv family (every conv launch incl. stem and split-K / wgrad reductions): {avg(conv):.1f} us "
-                  f"per step = {gflop:.1f} GFLOP / {avg(conv):.1f} us = {gflop / avg(conv) * 1e3:.1f} TFLOP/s = "
-                  f"{gflop / avg(conv) * 1e3 / BF16_PEAK_TFLOPS:.4f} of the {BF16_PEAK_TFLOPS:.0f} TFLOP/s bf16 dense peak", "",
+                  (f"* conv family (every conv launch incl. stem and split-K / wgrad reductions): {avg(conv):.1f} us "
+                   f"per step = {gflop:.1f} GFLOP / {avg(conv):.1f} us = {gflop / avg(conv) * 1e3:.1f} TFLOP/s = "
+                   f"{gflop / avg(conv) * 1e3 / BF16_PEAK_TFLOPS:.4f} of the {BF16_PEAK_TFLOPS:.0f} TFLOP/s bf16 dense "
+                   f"peak (FLOPs: {gsrc})" if gflop else
+                   f"* conv family (every conv launch incl. stem and split-K / wgrad reductions): {avg(conv):.1f} us "
+                   f"per step (no fraction of peak: algorithmic FLOPs unknown -- {gsrc or 'pass --bench or --gflop-per-step'})"),
+                  "",
                   "| kernel | calls/step | us/step | avg us |", "|---|---|---|---|"]
         for k, (c, d) in sorted(per_kernel.items(), key=lambda kv: -kv[1][1]):
             lines.append(f"| `{k}` | {c / ns:.0f} | {d / ns / 1e3:.1f} | {d / c / 1e3:.2f} |")
