@@ -165,6 +165,27 @@ def committed_traffic(batch: int, size: int, path: str = None):
         return None, f"{src}: unreadable ({e!r})"
 
 
+def comm_fields(bucket_us, exposed_us, steps, buckets_mb):
+    """The rank's communication timing (dtc_rn18_comm_timing_result) as the JSON fields VERDICT r4 item 6
+    asks for: `comm_exposed_us` -- how long the compute stream waited on communication per step: the tail
+    from the last backward kernel to the Reducer's join (the last bucket's collective), plus the wait for the
+    weight-gradient stream (earlier buckets' collectives and the remaining weight gradients) before the stem
+    weight gradient -- and `buckets_us`, per bucket (issue order) the collective's start / end offset from the
+    backward's start and its duration (timing events on the stream it runs on)."""
+    if not steps:
+        return None, None
+    exposed = {"tail_us": round(exposed_us[0], 2), "side_join_us": round(exposed_us[1], 2),
+               "total_us": round(exposed_us[2], 2), "backward_us": round(exposed_us[3], 2), "steps": int(steps),
+               "note": "tail = last backward kernel -> the Reducer's join on the compute stream (the last bucket's "
+                       "collective, nothing left to overlap); side_join = the compute stream's wait for the "
+                       "weight-gradient stream (its queued weight gradients + the earlier buckets' collectives) "
+                       "before the stem weight gradient"}
+    buckets = [{"bucket": i, "mb": (buckets_mb[i] if i < len(buckets_mb) else None),
+                "start_us": round(bucket_us[3 * i], 2), "end_us": round(bucket_us[3 * i + 1], 2),
+                "duration_us": round(bucket_us[3 * i + 2], 2)} for i in range(len(buckets_mb))]
+    return exposed, buckets
+
+
 def host_cores() -> dict:
     """The host's CPU inventory (state physical cores beside the thread count): logical
     CPUs, the CPUs this process may run on (affinity), and physical cores / sockets from
@@ -366,6 +387,8 @@ def main():
                     help="dp: BASELINE config 4, single-process DataParallel (global --batch over --gpus devices)")
     ap.add_argument("--dp-devices", default="", help="dp mode: comma-separated replica devices (may repeat)")
     ap.add_argument("--no-allreduce-probe", action="store_true", help="skip the N>1 all-reduce busBW probe")
+    ap.add_argument("--no-comm-timing", action="store_true",
+                    help="skip the per-bucket / exposed-communication timing region (N>1 or --sim-world)")
     ap.add_argument("--allreduce-probe", action="store_true", help="run the busBW probe at N=1 too (plumbing check)")
     ap.add_argument("--no-hbm-probe", action="store_true", help="skip the BN / SGD HBM-roofline probe")
     ap.add_argument("--sync-bn", action="store_true",
@@ -492,6 +515,22 @@ def main():
         for k, v in saved.items():
             dtc._native.call("dtc_set_option", k, v)
     ms, fl, cnt = list(ms4)[:3], list(fl4)[:3], list(cnt4)[:3]  # the conv passes (kinds 0-2)
+
+    # Communication timing (N > 1 or --sim-world): the same K steps again with timing events around every
+    # bucket collective and at the backward's joins (dtc_rn18_comm_timing), after the timed regions so the
+    # events never perturb `value`; rank 0 reports its own rank's figures
+    comm_exposed, buckets_us = None, None
+    if model.module._comm is not None and not args.no_comm_timing:
+        exe = model.module.executor(B, S, S, "bf16")
+        nb = len(model.buckets)
+        dtc._native.call("dtc_rn18_comm_timing", exe.handle, args.steps)
+        for i in range(args.steps):
+            step(args.warmup + i)
+        torch.cuda.synchronize()
+        bus, exu, nst = (C.c_double * (3 * max(1, nb)))(), (C.c_double * 5)(), C.c_int(0)
+        dtc._native.call("dtc_rn18_comm_timing_result", exe.handle, nb, bus, exu, C.byref(nst))
+        comm_exposed, buckets_us = comm_fields(list(bus), list(exu), nst.value,
+                                               [round(n * 4 / 2**20, 2) for _, n in model.buckets])
 
     # BASELINE config 3 beside the weak-scaled value at N > 1: the reference's own DDP job, global
     # batch 256 over the ranks (per-rank int(256/W), ddp/trainer.py:34, run_ddp.sh:4) -- strong scaling
@@ -622,6 +661,9 @@ def main():
                                                 / BF16_PEAK_TFLOPS, 4),
             "final_loss": round(losses[-1], 4) if losses else None,
         }
+        if comm_exposed is not None:
+            out["comm_exposed_us"] = comm_exposed
+            out["buckets_us"] = buckets_us
         if allreduce is not None:
             out["allreduce"] = allreduce
         if config3 is not None:

@@ -135,6 +135,8 @@ _SIGS = {
     "dtc_rn18_profile_events": (i32, [vp, i32]),
     "dtc_rn18_profile_events_result": (i32, [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double), Pi32]),
     "dtc_rn18_profile_events_dropped": (i32, [vp, P64]),
+    "dtc_rn18_comm_timing": (i32, [vp, i32]),
+    "dtc_rn18_comm_timing_result": (i32, [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double), Pi32]),
     "dtc_rn18_forward": (i32, [vp, vp, vp, i32, vp]),
     "dtc_rn18_backward": (i32, [vp, vp, f32, vp, vp]),
     "dtc_rn18_xent_backward": (i32, [vp, vp, vp, vp, vp, f32, vp, vp]),

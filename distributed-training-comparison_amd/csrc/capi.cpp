@@ -200,14 +200,31 @@ int dtc_install_crash_handler(void) {
 
 size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass) {
   if (!desc_ok(d) || pass < 0 || pass > 2) return 0;
-  return plan_conv(shape_of(d), pass).slab_bytes;
+  const size_t slab = plan_conv(shape_of(d), pass).slab_bytes;
+  // FWD / DGRAD split-K: + the arrival counters of the in-kernel reduction at the workspace's end
+  return slab > 0 && pass != 2 ? slab + (size_t)DTC_TICKS * 4 : slab;
+}
+
+// FWD / DGRAD workspace: [split-K slab][DTC_TICKS u32 arrival counters] when it holds both (the counters of
+// the in-kernel reduction are zeroed on the call's stream first; the workspace is scratch between calls),
+// else the whole of it is slab and a split-K plan reduces in a separate launch.
+static unsigned* op_ticks(const dtc_conv_desc* d, int pass, void* ws, size_t& ws_bytes, hipStream_t st) {
+  const size_t slab = plan_conv(shape_of(d), pass).slab_bytes;
+  const size_t tb = (size_t)DTC_TICKS * 4;
+  if (ws == nullptr || slab == 0 || ws_bytes < slab + tb) return nullptr;
+  const uintptr_t end = ((uintptr_t)ws + ws_bytes - tb) & ~(uintptr_t)255;
+  if (end < (uintptr_t)ws + slab) return nullptr;
+  if (hipMemsetAsync((void*)end, 0, tb, st) != hipSuccess) return nullptr;
+  ws_bytes = end - (uintptr_t)ws;
+  return (unsigned*)end;
 }
 
 int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, void* ws,
                    size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && w && y, "dtc_conv2d_fwd: null argument");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_fwd: unsupported convolution descriptor");
-  GUARD(return conv_fwd(shape_of(d), x, w, y, stats, (float*)ws, ws ? ws_bytes : 0, S(stream));)
+  unsigned* tick = op_ticks(d, CONV_FWD, ws, ws_bytes, S(stream));
+  GUARD(return conv_fwd(shape_of(d), x, w, y, stats, (float*)ws, ws ? ws_bytes : 0, S(stream), nullptr, tick);)
 }
 
 int dtc_conv2d_fwd_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats,
@@ -224,7 +241,9 @@ int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t*
                      void* ws, size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && dy && w && dx, "dtc_conv2d_dgrad: null argument");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_dgrad: unsupported convolution descriptor");
-  GUARD(return conv_dgrad(shape_of(d), dy, w, dx, res, (float*)ws, ws ? ws_bytes : 0, S(stream));)
+  unsigned* tick = op_ticks(d, CONV_DGRAD, ws, ws_bytes, S(stream));
+  GUARD(return conv_dgrad(shape_of(d), dy, w, dx, res, (float*)ws, ws ? ws_bytes : 0, S(stream), nullptr, nullptr, 0,
+                          tick);)
 }
 
 int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
@@ -237,7 +256,9 @@ int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16
   BnbArgs a;
   a.ym = ymask; a.x1 = x1; a.mean1 = mean1; a.invstd1 = invstd1; a.acc1 = acc1;
   a.x2 = x2; a.mean2 = mean2; a.invstd2 = invstd2; a.acc2 = acc2;
-  GUARD(return conv_dgrad(shape_of(d), dy, w, dx, res, (float*)ws, ws ? ws_bytes : 0, S(stream), nullptr, &a);)
+  unsigned* tick = op_ticks(d, CONV_DGRAD, ws, ws_bytes, S(stream));
+  GUARD(return conv_dgrad(shape_of(d), dy, w, dx, res, (float*)ws, ws ? ws_bytes : 0, S(stream), nullptr, &a, 0,
+                          tick);)
 }
 
 int dtc_conv2d_dgrad_sc(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,

@@ -17,6 +17,7 @@
 #include "comm.h"
 #include "common.h"
 #include "kernels.h"
+#include "kernels.h"
 
 namespace dtc {
 
@@ -51,6 +52,19 @@ struct Comm {
   ThreadGroup* grp = nullptr;
   hipEvent_t ready = nullptr;  // this rank's "inputs produced" marker for the current collective
 };
+
+// The communicator's own stream (its broadcasts, the barrier token, and the bucket all-reduces when option
+// comm_on_side is 0). Option comm_prio (read at communicator creation): 0 = normal priority; 1 = the most
+// urgent priority, so RCCL's channel kernels are dispatched ahead of queued compute work.
+static hipError_t comm_stream_create(hipStream_t* s) {
+  if (option_get(OPT_COMM_PRIO) == 1) {
+    int lo = 0, hi = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e != hipSuccess) return e;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
 
 // ---------------------------------------------------------------- thread-group transport
 // W ranks in one process, one host thread each, their buffers on one device. Every collective is
@@ -164,7 +178,7 @@ int comm_init_thread_group(Comm** outs, int world, int device) {
     c->world = world;
     c->device = device;
     c->grp = g;
-    DTC_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    DTC_HIP(comm_stream_create(&c->side));
     c->fork.resize(64);
     for (auto& e : c->fork) DTC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     DTC_HIP(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
@@ -221,7 +235,7 @@ int comm_init(Comm** out, int rank, int world, const void* uid, int device) {
     delete c;
     return set_error(1000 + (int)r, "ncclCommInitRank failed: %s", ncclGetErrorString(r));
   }
-  DTC_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  DTC_HIP(comm_stream_create(&c->side));
   c->fork.resize(64);
   for (auto& e : c->fork) DTC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   DTC_HIP(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
@@ -237,7 +251,7 @@ int comm_init_loopback(Comm** out, int device, int world, float factor) {
   c->loopback = true;
   c->world = world;
   c->factor = factor;
-  DTC_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  DTC_HIP(comm_stream_create(&c->side));
   c->fork.resize(64);
   for (auto& e : c->fork) DTC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   DTC_HIP(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
@@ -358,12 +372,14 @@ int comm_broadcast(Comm* c, void* buf, size_t count, int dtype, int root, hipStr
   return 0;
 }
 
-int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute) {
+int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute, hipEvent_t t0, hipEvent_t t1) {
   DTC_CHECK_ARG(c && buf, "comm_allreduce_async: bad args");
   if (count == 0) return 0;
   if (c->grp) {  // the bucket's producers on `compute`, the result awaited by the side stream
     c->log.push_back(CommLogEntry{(uint64_t)(uintptr_t)buf, (uint64_t)count, 1});
+    if (t0) DTC_HIP(hipEventRecord(t0, compute));
     DTC_TRY(group_collective(c, GK_ALLREDUCE, buf, count, 0, 0, compute, c->side));
+    if (t1) DTC_HIP(hipEventRecord(t1, c->side));
     c->pending = true;
     return 0;
   }
@@ -371,21 +387,27 @@ int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute) 
   c->next_fork = (c->next_fork + 1) % (int)c->fork.size();
   DTC_HIP(hipEventRecord(ev, compute));
   DTC_HIP(hipStreamWaitEvent(c->side, ev, 0));
+  if (t0) DTC_HIP(hipEventRecord(t0, c->side));  // (after the wait: when the collective can start)
   if (c->loopback) DTC_TRY(loopback_reduce(c, buf, count, 0, c->side, true));
   else DTC_NCCL(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c->nccl, c->side));
+  if (t1) DTC_HIP(hipEventRecord(t1, c->side));
   c->pending = true;
   return 0;
 }
 
-int comm_allreduce_on(Comm* c, void* buf, size_t count, hipStream_t st) {
+int comm_allreduce_on(Comm* c, void* buf, size_t count, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   DTC_CHECK_ARG(c && buf, "comm_allreduce_on: bad args");
   if (count == 0) return 0;
+  if (t0) DTC_HIP(hipEventRecord(t0, st));
   if (c->grp) {
     c->log.push_back(CommLogEntry{(uint64_t)(uintptr_t)buf, (uint64_t)count, 1});
-    return group_collective(c, GK_ALLREDUCE, buf, count, 0, 0, st, st);
+    DTC_TRY(group_collective(c, GK_ALLREDUCE, buf, count, 0, 0, st, st));
+  } else if (c->loopback) {
+    DTC_TRY(loopback_reduce(c, buf, count, 0, st, true));
+  } else {
+    DTC_NCCL(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c->nccl, st));
   }
-  if (c->loopback) return loopback_reduce(c, buf, count, 0, st, true);
-  DTC_NCCL(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c->nccl, st));
+  if (t1) DTC_HIP(hipEventRecord(t1, st));
   return 0;
 }
 
@@ -398,6 +420,7 @@ int comm_join(Comm* c, hipStream_t compute) {
   return 0;
 }
 
+bool comm_pending(const Comm* c) { return c != nullptr && c->pending; }
 int comm_world(const Comm* c) { return c ? c->world : 1; }
 int comm_rank(const Comm* c) { return c ? c->rank : 0; }
 

@@ -20,11 +20,17 @@ int comm_allreduce(Comm* c, void* buf, size_t count, int dtype, hipStream_t st);
 int comm_broadcast(Comm* c, void* buf, size_t count, int dtype, int root, hipStream_t st);
 // Reducer primitives: fp32 SUM all-reduce of a bucket on the side stream after everything
 // enqueued so far on `compute`; join orders `compute` after all outstanding buckets.
-int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute);
+// t0 / t1 (optional timing events): recorded on the collective's stream right before / after it (t0 after
+// the fork wait: when the collective can start) -- the executor's per-bucket timing (dtc_rn18_comm_timing)
+int comm_allreduce_async(Comm* c, void* buf, size_t count, hipStream_t compute, hipEvent_t t0 = nullptr,
+                         hipEvent_t t1 = nullptr);
 int comm_join(Comm* c, hipStream_t compute);
 // a bucket all-reduce issued directly on `st` (its producers already ordered before it on `st`): no fork,
 // no join -- the executor's weight-gradient stream carries it (one stream fewer in the backward)
-int comm_allreduce_on(Comm* c, void* buf, size_t count, hipStream_t st);
+int comm_allreduce_on(Comm* c, void* buf, size_t count, hipStream_t st, hipEvent_t t0 = nullptr,
+                      hipEvent_t t1 = nullptr);
+// true while a comm_allreduce_async collective is not yet joined (comm_join)
+bool comm_pending(const Comm* c);
 int comm_world(const Comm* c);
 int comm_rank(const Comm* c);
 // in-process thread group: `world` handles (outs[r] = rank r) on one device, one host thread per rank

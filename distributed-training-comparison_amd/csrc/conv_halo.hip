@@ -54,6 +54,11 @@ struct HConvParams {
   const u16* res;  // DGRAD: residual added in the epilogue (NHWC, Cout) or null
   double* stats;   // FWD: BN statistics [SLOTS][2][Cout] or null
   float* slab;     // split-K: fp32 partial tiles [split][M][Cout]
+  // split-K reduced IN the kernel (option splitk_ink): per output tile an arrival counter (zero between
+  // launches: the last arriver resets it); the workgroup whose agent-scope add returns splits - 1 sums the
+  // tile's partials in split order and runs the normal (non-split) epilogue. Null: the separate
+  // splitk_reduce launch does it.
+  unsigned* tick;
   int N, H, W, Cin, Cout, C;
   uint32_t src_bytes;
   int rows;     // output rows per image slice
@@ -512,16 +517,93 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     }
   }
   if (p.slab != nullptr) {  // split-K partial: fp32 [split][pixel][Cout], one 16-B store per fragment
-    float* slab = p.slab + (size_t)split * M * p.Cout;
+    const size_t plane = (size_t)M * p.Cout;
+    if (p.tick == nullptr) {  // the separate splitk_reduce launch sums the slab
+      float* slab = p.slab + (size_t)split * plane;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int pix = slot_pix(bcol0 + j * 16 + cl);
+        if (pix >= M) continue;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          *(f32x4*)(slab + (size_t)pix * p.Cout + a0 + arow0 + i * 16 + rq) = acc[i][j];
+      }
+      stamp_end(p.ts);
+      return;
+    }
+    // In-kernel reduction (MI355X_MICROARCH.md, inter-workgroup hand-off, "Valid forms" table row 1): every
+    // partial is stored write-through (sc1) and every storing wave drains (vmcnt 0) before the workgroup
+    // barrier; one lane then adds to the tile's arrival counter (agent scope, returning); the workgroup
+    // whose add returns splits - 1 reads the other partials with sc1 loads (L2-served, never a stale L1
+    // line). No workgroup waits for another: the others exit.
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.slab, 0, 0x7ffffff0, 0x00020000);
+    const int nsplit = (int)gridDim.y;
+    uint32_t eoff[FM][FN];  // byte offset of each fragment's 4 channels within one split's plane
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int pix = slot_pix(bcol0 + j * 16 + cl);
-      if (pix >= M) continue;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        *(f32x4*)(slab + (size_t)pix * p.Cout + a0 + arow0 + i * 16 + rq) = acc[i][j];
+        eoff[i][j] = pix < M ? (uint32_t)(((size_t)pix * p.Cout + a0 + arow0 + i * 16 + rq) * 4) : 0x80000000u;
     }
-  } else if constexpr (MODE == 0) {
+    const uint32_t own = (uint32_t)((size_t)split * plane * 4);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        if (eoff[i][j] != 0x80000000u)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, own + eoff[i][j], 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* const flag = (unsigned*)smem;
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(p.tick + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned last = old == (unsigned)(nsplit - 1) ? 1u : 0u;
+      if (last) __hip_atomic_store(p.tick + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *(volatile unsigned*)flag = last;
+    }
+    __syncthreads();
+    const unsigned last = *(volatile unsigned*)flag;
+    __syncthreads();  // the flag word is read by every wave before the epilogue reuses smem
+    if (!last) {
+      stamp_end(p.ts);
+      return;
+    }
+    // the sum splitk_reduce forms: 0 + slab[0] + slab[1] + ... (same order, same bits), this workgroup's own
+    // partial from its registers; every other split's fragments loaded before the first add
+    f32x4 sum[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < nsplit; ++sp) {
+      if (sp == split) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) sum[i][j] += acc[i][j];
+        continue;
+      }
+      const uint32_t base = (uint32_t)((size_t)sp * plane * 4);
+      f32x4 part[FM][FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          part[i][j] = eoff[i][j] != 0x80000000u
+                           ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + eoff[i][j], 0, 16))
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) sum[i][j] += part[i][j];
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = sum[i][j];
+  }
+  if constexpr (MODE == 0) {
     float* red = (float*)smem;  // [WC][BM][2]
     auto epi_fwd = [&](f32x4 (&A)[SC ? FM : 1][SC ? FN : 1], f32x4 (&B)[FM][FN], bool second, u16* outp, double* stp) {
       const bool want_stats = stp != nullptr;
@@ -962,7 +1044,7 @@ static int conv_halo_general(const ConvShape& s, int mode, const HaloPlan& hp, c
 
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
               const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
-              const BnbArgs* bnb, const u16* wsc, u16* out2, double* stats2) {
+              const BnbArgs* bnb, const u16* wsc, u16* out2, double* stats2, unsigned* tick) {
   DTC_CHECK_ARG(hp.cfg >= 0 && hp.cfg < kNumHaloCfgs && (mode == CONV_FWD || mode == CONV_DGRAD),
                 "conv_halo: unsupported configuration");
   const HaloCfg& c = kHaloCfgs[hp.cfg];
@@ -998,13 +1080,17 @@ int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, 
   p.fd_w = make_fastdiv(g.wo);
   p.ts = ts;
   p.staged = option_get(OPT_HALO_STAGE_EPI) == 1;
-  if (bnb != nullptr && split <= 1) p.bnb = *bnb;  // (split-K: the reduction kernel applies it)
   const dim3 grid(halo_tiles_b(s, g) * p.tiles_a, split);
+  // split-K reduced in the kernel (the last workgroup of each tile) when the caller gave arrival counters
+  // for the grid (tick: >= DTC_TICKS zeroed words, reserved for this stream) and option splitk_ink is on
+  const bool ink = split > 1 && tick != nullptr && option_get(OPT_SPLITK_INK) != 0 && grid.x <= (unsigned)DTC_TICKS;
+  p.tick = ink ? tick : nullptr;
+  if (bnb != nullptr && (split <= 1 || ink)) p.bnb = *bnb;  // (separate split-K: the reduction kernel applies it)
   if (c.st == 2) {
     return wsc ? launch_halo_s2<true>(p, hp.cfg, grid, st) : launch_halo_s2<false>(p, hp.cfg, grid, st);
   }
   DTC_TRY(mode == CONV_FWD ? launch_halo<0>(p, hp.cfg, grid, st) : launch_halo<1>(p, hp.cfg, grid, st));
-  if (split > 1) return splitk_reduce(slab, split, M, p.Cout, out, res, stats, st, ts, bnb);
+  if (split > 1 && !ink) return splitk_reduce(slab, split, M, p.Cout, out, res, stats, st, ts, bnb);
   return 0;
 }
 

@@ -880,11 +880,13 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
 }
 
 int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
-             size_t slab_bytes, hipStream_t st, u64* ts) {
+             size_t slab_bytes, hipStream_t st, u64* ts, unsigned* tick) {
   if (conv_c64_ok(s)) return conv_c64(s, CONV_FWD, x, w, y, nullptr, stats, st, ts);
   {
     const HaloPlan hp = conv_halo_plan(s, CONV_FWD);
-    if (hp.cfg >= 0) return conv_halo(s, CONV_FWD, hp, x, w, y, nullptr, stats, slab, slab_bytes, st, ts);
+    if (hp.cfg >= 0)
+      return conv_halo(s, CONV_FWD, hp, x, w, y, nullptr, stats, slab, slab_bytes, st, ts, nullptr, nullptr, nullptr,
+                       nullptr, tick);
   }
   IGemmParams p{};
   p.ts = ts;
@@ -970,7 +972,7 @@ static int bnb_after(const BnbArgs* bnb, u16* dx, int64_t M, int C, hipStream_t 
 }
 
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
-               size_t slab_bytes, hipStream_t st, u64* ts, const BnbArgs* bnb, int res_compact) {
+               size_t slab_bytes, hipStream_t st, u64* ts, const BnbArgs* bnb, int res_compact, unsigned* tick) {
   if (bnb != nullptr && !bnb_on(*bnb)) bnb = nullptr;
   DTC_CHECK_ARG(!res_compact || (res && dgrad_class_mode(s) && !conv_c64_ok(s)),
                 "conv_dgrad: a compact residual needs the stride-2 parity-class path");
@@ -980,13 +982,16 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
   const int fz = bnb != nullptr ? (bnb->mb ? (option_get(OPT_BNB_MASK) == 2 ? 6 : 7) : option_get(OPT_BNB_FUSE)) : 0;
   const HaloPlan hp = conv_c64_ok(s) ? HaloPlan{-1, 0} : conv_halo_plan(s, CONV_DGRAD);
   const int kind = conv_c64_ok(s) ? 1 : (hp.cfg >= 0 ? 2 : 4);
-  const bool split_path = kind != 1 && (kind == 4 || hp.split > 1);  // the epilogue is splitk_reduce's
+  // the epilogue is splitk_reduce's (a halo split-K reduced in the kernel runs the halo epilogue)
+  const bool split_path = kind != 1 && (kind == 4 || (hp.split > 1 && !(tick && option_get(OPT_SPLITK_INK))));
   if (bnb != nullptr && !(fz & (split_path ? 4 : kind))) {
-    DTC_TRY(conv_dgrad(s, dy, w, dx, res, slab, slab_bytes, st, ts, nullptr, res_compact));
+    DTC_TRY(conv_dgrad(s, dy, w, dx, res, slab, slab_bytes, st, ts, nullptr, res_compact, tick));
     return bnb_after(bnb, dx, (int64_t)s.N * s.H * s.W, s.C, st);
   }
   if (kind == 1) return conv_c64(s, CONV_DGRAD, dy, w, dx, res, nullptr, st, ts, bnb);
-  if (kind == 2) return conv_halo(s, CONV_DGRAD, hp, dy, w, dx, res, nullptr, slab, slab_bytes, st, ts, bnb);
+  if (kind == 2)
+    return conv_halo(s, CONV_DGRAD, hp, dy, w, dx, res, nullptr, slab, slab_bytes, st, ts, bnb, nullptr, nullptr,
+                     nullptr, tick);
   IGemmParams p{};
   p.ts = ts;
   DTC_TRY(fill_common(p, s));

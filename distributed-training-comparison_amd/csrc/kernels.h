@@ -64,7 +64,10 @@ namespace dtc {
   X(WGRAD_GEN, wgrad_gen, 1)            /* wgrad_halo general step geometry (224x224 model) */                \
   X(HALO_GEN, halo_gen, 1)              /* conv_halo general tile geometry (224x224 model) */                 \
   X(BN_RED_UNROLL, bn_red_unroll, 4)    /* bn_bwd_reduce: rows per thread whose loads go together */          \
-  X(C64_GEN, c64_gen, 1)                /* conv_c64 general tiles (224x224 layer1) */
+  X(C64_GEN, c64_gen, 1)                /* conv_c64 general tiles (224x224 layer1) */                         \
+  X(SPLITK_INK, splitk_ink, 1)          /* conv split-K summed by the last workgroup per tile (no reduce launch) */ \
+  X(COMM_PRIO, comm_prio, 0)            /* (communicator creation) its own stream: 0 normal, 1 most urgent */ \
+  X(COMM_TAIL_INLINE, comm_tail_inline, 1) /* the last bucket's all-reduce on the compute stream (no fork / join) */
 
 enum {
 #define DTC_OPT_ENUM(id, name, def) OPT_##id,
@@ -93,8 +96,12 @@ ConvPlan plan_conv(const ConvShape& s, int mode);
 // stats[SLOTS][2][K] (sum, sum of squares; fp64, accumulated).
 // `ts` (optional, every conv launcher): a DTC_PROF_SLOT_U64 slot receiving the entry times of the
 // first workgroups and every workgroup's exit time in s_memrealtime ticks (graph-safe per-call timing).
+// tick (optional): >= DTC_TICKS zeroed u32 arrival counters reserved for the launch stream (the executor's
+// workspace: one set per stream); with it a split-K conv reduces its slab inside the kernel (the last
+// workgroup of each output tile), else a separate reduction launch does. The counters are left zero.
+#define DTC_TICKS 8192
 int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
-             size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
+             size_t slab_bytes, hipStream_t st, u64* ts = nullptr, unsigned* tick = nullptr);
 // 3x3 stride-2 conv and the 1x1 stride-2 projection shortcut of the same input in one launch
 bool conv_fwd_sc_ok(const ConvShape& s, const ConvShape& sc);
 int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16* w, u16* y, double* stats,
@@ -115,7 +122,7 @@ int conv_dgrad_sc(const ConvShape& s, const u16* dy, const u16* w, u16* dx, cons
                   hipStream_t st, u64* ts = nullptr, const BnbArgs* bnb = nullptr);
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
                size_t slab_bytes, hipStream_t st, u64* ts = nullptr, const BnbArgs* bnb = nullptr,
-               int res_compact = 0);
+               int res_compact = 0, unsigned* tick = nullptr);
 // dw[k][0:dw_cols] (row stride dw_ld) = scale * sum_pixels dy (x) im2col(x); fp32
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
                float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
@@ -155,7 +162,8 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode);
 size_t conv_halo_slab_bytes(const ConvShape& s, int mode);  // fp32 split-K slab the plan needs
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
               const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr,
-              const BnbArgs* bnb = nullptr, const u16* wsc = nullptr, u16* out2 = nullptr, double* stats2 = nullptr);
+              const BnbArgs* bnb = nullptr, const u16* wsc = nullptr, u16* out2 = nullptr, double* stats2 = nullptr,
+              unsigned* tick = nullptr);
 // bnb (optional, non-null ym): out = dz = bf16(sum + res) * [ym > 0] and the BN-backward sums of
 // dz into bnb->acc1 (/acc2) -- the work of bn_bwd_reduce on the value the reduction holds.
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,

@@ -83,6 +83,8 @@ struct Net {
   bool stem_direct = false;  // planned with option stem_direct (bf16): stem.hip instead of im2col + GEMM
   size_t HEADWS = 0, HEADWS_bytes = 0;
   size_t DC0 = 0, SLABW = 0;  // stem conv-output gradient; split-K slab of the side-stream wgrads
+  size_t TICK = 0;            // split-K arrival counters: [0] compute stream, [1] weight-gradient stream
+  unsigned* tick(int i) { return (unsigned*)(ws + TICK) + (size_t)i * DTC_TICKS; }
   size_t BNERR = 0;           // int: set by a one-pass BN backward whose grid barrier timed out
   // backward weight gradients run on a side stream (option bwd_streams), overlapped with the
   // data-gradient / BN chain; forked after the conv-output gradient exists, joined at bucket points
@@ -125,6 +127,20 @@ struct Net {
   size_t prof_evn = 0;                  // pairs used
   long long prof_evdropped = 0;         // calls that found the pool used up (not bracketed: reported)
   std::vector<std::pair<int, double>> prof_evwork;  // (kind, work) per pair
+  // communication timing (dtc_rn18_comm_timing; bench.py's comm_exposed_us / buckets_us at N > 1): for the
+  // next ct_left backward calls with a communicator, timing events on the streams the work runs on -- the
+  // backward's start (compute stream), each bucket collective's start / end (its own stream), the compute
+  // stream's wait for the weight-gradient stream before the stem weight gradient (join_c -> join_d), and the
+  // tail from the last backward kernel to the Reducer's join (tail_a -> tail_b)
+  struct CommTimes {
+    hipEvent_t bwd0 = nullptr, join_c = nullptr, join_d = nullptr, tail_a = nullptr, tail_b = nullptr;
+    std::vector<hipEvent_t> b0, b1;  // per bucket
+    bool join = false, tail = false;  // join_c / join_d, tail_a recorded (eager backward)
+    std::vector<bool> bucket;        // bucket i recorded
+  };
+  std::vector<CommTimes> ct;  // one per armed step
+  int ct_left = 0, ct_used = 0;
+  CommTimes* ct_cur = nullptr;  // the set of the backward in progress (null: not timed)
   // hipGraph replay (option "graphs"): the forward per train flag, the backward as segments split
   // at bucket boundaries (the all-reduces stay eager on the communicator's side stream)
   struct Seg { hipGraphExec_t exec = nullptr; std::vector<int> buckets; };
@@ -382,6 +398,7 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.slab_bytes = slab;
   n.SLAB = take(slab);
   n.SLABW = take(slab);
+  n.TICK = take((size_t)2 * DTC_TICKS * 4);  // zeroed at bind; every in-kernel split-K leaves its counters zero
   if (n.capture) {
     auto cap = [&](const std::string& nm, int h, int w, int c) {
       n.caps.push_back({nm, take((size_t)B * h * w * c * E), (int)B, h, w, c});
@@ -684,7 +701,7 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
     if (b.proj && !scf)  // the shortcut conv first
       PROF(0, conv_flops(b.sc.s),
            conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr, slab,
-                    n.slab_bytes, st, ts));
+                    n.slab_bytes, st, ts, n.tick(0)));
     if (scf) {
       PROF(0, conv_flops(b.c1.s) + conv_flops(b.sc.s),
            conv_fwd_sc(b.c1.s, b.sc.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr,
@@ -692,12 +709,12 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
     } else {
       PROF(0, conv_flops(b.c1.s),
            conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
-                    n.slab_bytes, st, ts));
+                    n.slab_bytes, st, ts, n.tick(0)));
     }
     DTC_TRY(bn_act(n, 1, b.b1, n.at<u16>(b.C1), nullptr, nullptr, n.at<u16>(b.A1), M, train, st, b.MA1));
     PROF(0, conv_flops(b.c2.s),
          conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
-                  train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st, ts));
+                  train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st, ts, n.tick(0)));
     if (b.proj) {
       DTC_TRY(bn_act(n, 3, b.b2, n.at<u16>(b.C2), &b.bsc, n.at<u16>(b.S), n.at<u16>(b.OUT), M, train, st, b.MOUT));
     } else {
@@ -950,9 +967,22 @@ static int maybe_bucket(Net& n, int after_block, const BwdCtx& cx, hipStream_t s
     // fewer competing for the process's hardware queues (GPU_MAX_HW_QUEUES); the weight gradients of
     // later buckets then queue behind it on that stream
     const bool on_side = option_get(OPT_COMM_ON_SIDE) != 0 && prod == n.side_st;
+    // option comm_tail_inline: the last bucket (after the stem, nothing left to overlap) is all-reduced on the
+    // compute stream itself when every earlier collective is already ordered before that stream (none
+    // pending on the communicator's stream): the fork to the communicator's stream and the join back cost
+    // two cross-stream hand-offs, ~15 us each (bench --sim-world 2 buckets_us / comm_exposed_us, round 5)
+    const bool inline_tail = after_block == -1 && prod == st && option_get(OPT_COMM_TAIL_INLINE) != 0 &&
+                             !comm_pending(cx.comm);
     for (int i : ids) {
-      if (on_side) DTC_TRY(comm_allreduce_on(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], prod));
-      else DTC_TRY(comm_allreduce_async(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], prod));
+      hipEvent_t t0 = nullptr, t1 = nullptr;
+      if (n.ct_cur && i < (int)n.ct_cur->b0.size()) {
+        t0 = n.ct_cur->b0[i];
+        t1 = n.ct_cur->b1[i];
+        n.ct_cur->bucket[i] = true;
+      }
+      if (on_side || inline_tail)
+        DTC_TRY(comm_allreduce_on(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], prod, t0, t1));
+      else DTC_TRY(comm_allreduce_async(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], prod, t0, t1));
     }
     return 0;
   }
@@ -1253,7 +1283,8 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     {
       const BnbArgs bz = bnb_mask_of(n, b.MA1, b.C1, b.b1);
       PROF(1, conv_flops(b.c2.s),
-           conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts, bmf ? &bz : nullptr));
+           conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts, bmf ? &bz : nullptr, 0,
+                      n.tick(0)));
     }
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
     DTC_TRY(cap_masked(n, cp + ".dz1", G[4], b.MA1, M, b.Cout, st));
@@ -1296,13 +1327,16 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
         PROF(1, conv_flops(b.c1.s) + conv_flops(b.sc.s),
              conv_dgrad_sc(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], dsc, n.wbf(b.sc.pidx), st, ts, bpp));
       } else {
-        PROF(1, conv_flops(b.sc.s), conv_dgrad(sc_dg, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts));
+        PROF(1, conv_flops(b.sc.s),
+             conv_dgrad(sc_dg, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts, nullptr, 0, n.tick(0)));
         PROF(1, conv_flops(b.c1.s),
-             conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts, bpp, sc_cmp ? 1 : 0));
+             conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts, bpp, sc_cmp ? 1 : 0,
+                        n.tick(0)));
       }
       DTC_TRY(cap(n, cp + ".dxs", G[5], st));
     } else {  // residual = dz of this block's output (G[0], written by bn2's apply); dx over it in place
-      PROF(1, conv_flops(b.c1.s), conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[0], slab, n.slab_bytes, st, ts, bpp));
+      PROF(1, conv_flops(b.c1.s),
+           conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[0], slab, n.slab_bytes, st, ts, bpp, 0, n.tick(0)));
     }
     sums_ready = bmf;
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
@@ -1329,7 +1363,14 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     PROF(2, 2.0 * M0 * 64 * 27,
          stem_wgrad_bn(n.at<float>(n.XIN), G[0], m0, n.at<u16>(n.C0), a0, n.gf(n.stem.pidx), gs, n.B, n.H, n.W, slab,
                        n.slab_bytes, st, ts));
+    const bool ctj = n.ct_cur && !cx.capturing;
+    if (ctj) DTC_HIP(hipEventRecord(n.ct_cur->join_c, st));
     DTC_TRY(join_side(n, st));  // after the stem kernel: it depends on nothing the side stream computes
+    if (ctj) {  // every backward kernel of either stream is behind join_d: the tail starts there
+      DTC_HIP(hipEventRecord(n.ct_cur->join_d, st));
+      DTC_HIP(hipEventRecord(n.ct_cur->tail_a, st));
+      n.ct_cur->join = n.ct_cur->tail = true;
+    }
     DTC_TRY(maybe_bucket(n, -1, cx, st));
     if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
     return 0;
@@ -1346,10 +1387,20 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
   if (option_get(OPT_FORK_LAZY) && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
   DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
+  const bool ctj = n.ct_cur && !cx.capturing;
+  if (ctj) DTC_HIP(hipEventRecord(n.ct_cur->join_c, st));
   DTC_TRY(join_side(n, st));  // the stem wgrad is the last kernel: run it on the main stream
+  if (ctj) {
+    DTC_HIP(hipEventRecord(n.ct_cur->join_d, st));
+    n.ct_cur->join = true;
+  }
   PROF(2, 2.0 * M0 * 64 * 27,
        n.stem_direct ? stem_wgrad(n.at<float>(n.XIN), dc0, n.gf(n.stem.pidx), gs, n.B, n.H, n.W, slab, n.slab_bytes, st, ts)
                      : conv_wgrad(n.stem.s, n.at<u16>(n.X0), dc0, n.gf(n.stem.pidx), 27, 27, gs, slab, n.slab_bytes, st, ts));
+  if (ctj) {  // the last backward kernel has been issued
+    DTC_HIP(hipEventRecord(n.ct_cur->tail_a, st));
+    n.ct_cur->tail = true;
+  }
   DTC_TRY(maybe_bucket(n, -1, cx, st));
   if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
   return 0;
@@ -1463,7 +1514,22 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   return 0;
 }
 
+static int backward_impl(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st);
 static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st) {
+  n.ct_cur = nullptr;
+  if (comm && n.ct_left > 0 && n.ct_used < (int)n.ct.size()) {
+    n.ct_cur = &n.ct[n.ct_used++];
+    --n.ct_left;
+    n.ct_cur->join = n.ct_cur->tail = false;
+    n.ct_cur->bucket.assign(n.ct_cur->b0.size(), false);
+    DTC_HIP(hipEventRecord(n.ct_cur->bwd0, st));
+  }
+  const int rc = backward_impl(n, dlogits, gs, comm, st);
+  if (rc == 0 && n.ct_cur) DTC_HIP(hipEventRecord(n.ct_cur->tail_b, st));  // after the Reducer's join
+  n.ct_cur = nullptr;
+  return rc;
+}
+static int backward_impl(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st) {
   n.prof_st = st;
   if (!n.sums_fresh) DTC_TRY(zero_bytes(n.ws + n.acc_lo, n.stats_hi - n.acc_lo, st));
   n.sums_fresh = false;
@@ -1502,12 +1568,18 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
     for (const auto& sg : n.bwd_segs[pi]) {
       if (sg.exec) DTC_TRY(graph_launch(n, sg.exec, st));
       for (int i : sg.buckets) {
+        hipEvent_t t0 = nullptr, t1 = nullptr;
+        if (n.ct_cur && i < (int)n.ct_cur->b0.size()) {
+          t0 = n.ct_cur->b0[i];
+          t1 = n.ct_cur->b1[i];
+          n.ct_cur->bucket[i] = true;
+        }
         if (on_side) {
           hipStream_t sd = st;
           DTC_TRY(fork_side(n, st, &sd));
-          DTC_TRY(comm_allreduce_on(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], sd));
+          DTC_TRY(comm_allreduce_on(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], sd, t0, t1));
         } else {
-          DTC_TRY(comm_allreduce_async(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st));
+          DTC_TRY(comm_allreduce_async(comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], st, t0, t1));
         }
       }
     }
@@ -1557,9 +1629,11 @@ int dtc_rn18_create(dtc_net** out, int batch, int height, int width, int num_cla
   return 0;
 }
 
+static void ct_free(Net& n);
 int dtc_rn18_destroy(dtc_net* net) {
   if (net) {
     drop_graphs(net->n);
+    ct_free(net->n);
     if (net->n.cap_st) (void)hipStreamDestroy(net->n.cap_st);
     if (net->n.side_st) (void)hipStreamDestroy(net->n.side_st);
     if (net->n.sc_st) (void)hipStreamDestroy(net->n.sc_st);
@@ -1630,6 +1704,7 @@ int dtc_rn18_bind(dtc_net* net, void* workspace, float* params, float* grads, ui
   n.prof_acc = n.at<u64>(n.PROF_ACC);
   drop_graphs(n);  // captured launches hold the previous pointers
   DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.stats_hi - n.stats_lo, (hipStream_t)stream));
+  DTC_HIP(hipMemsetAsync(n.ws + n.TICK, 0, (size_t)2 * DTC_TICKS * 4, (hipStream_t)stream));
   return 0;
 }
 
@@ -1742,6 +1817,92 @@ int dtc_rn18_profile_events_result(dtc_net* net, int nkinds, double* ms_by_kind,
   }
   n.prof_evn = 0;
   n.prof_events = false;
+  return 0;
+}
+
+static void ct_free(Net& n) {
+  for (auto& c : n.ct) {
+    for (hipEvent_t e : {c.bwd0, c.join_c, c.join_d, c.tail_a, c.tail_b})
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c.b0) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c.b1) (void)hipEventDestroy(e);
+  }
+  n.ct.clear();
+  n.ct_left = n.ct_used = 0;
+}
+
+int dtc_rn18_comm_timing(dtc_net* net, int steps) {
+  DTC_CHECK_ARG(net && steps >= 0 && steps <= 100000, "dtc_rn18_comm_timing: bad args");
+  Net& n = net->n;
+  ct_free(n);
+  const size_t nb = n.bucket_off.size();
+  n.ct.resize(steps);
+  for (auto& c : n.ct) {
+    for (hipEvent_t* e : {&c.bwd0, &c.join_c, &c.join_d, &c.tail_a, &c.tail_b}) DTC_HIP(hipEventCreate(e));
+    c.b0.resize(nb);
+    c.b1.resize(nb);
+    for (size_t i = 0; i < nb; ++i) {
+      DTC_HIP(hipEventCreate(&c.b0[i]));
+      DTC_HIP(hipEventCreate(&c.b1[i]));
+    }
+  }
+  n.ct_left = steps;
+  return 0;
+}
+
+int dtc_rn18_comm_timing_result(dtc_net* net, int max_buckets, double* bucket_us, double* exposed_us, int* steps) {
+  DTC_CHECK_ARG(net && max_buckets >= 0 && (max_buckets == 0 || bucket_us) && exposed_us && steps,
+                "dtc_rn18_comm_timing_result: bad args");
+  Net& n = net->n;
+  const int nb = std::min<int>(max_buckets, (int)n.bucket_off.size());
+  for (int i = 0; i < 3 * max_buckets; ++i) bucket_us[i] = 0.0;
+  for (int i = 0; i < 5; ++i) exposed_us[i] = 0.0;
+  auto us = [](hipEvent_t a, hipEvent_t b, double& out) -> int {
+    float ms = 0.f;
+    DTC_HIP(hipEventSynchronize(b));
+    DTC_HIP(hipEventElapsedTime(&ms, a, b));
+    out = 1e3 * (double)ms;
+    return 0;
+  };
+  int recorded = 0, joined = 0;
+  std::vector<int> bcount(nb, 0);
+  for (int k = 0; k < n.ct_used; ++k) {
+    Net::CommTimes& c = n.ct[k];
+    double tail = 0, bwd = 0;
+    if (c.tail) DTC_TRY(us(c.tail_a, c.tail_b, tail));  // (a replayed backward records no tail / join events)
+    DTC_TRY(us(c.bwd0, c.tail_b, bwd));
+    exposed_us[0] += tail;
+    exposed_us[3] += bwd;
+    if (c.join) {
+      double j = 0;
+      DTC_TRY(us(c.join_c, c.join_d, j));
+      exposed_us[1] += j;
+      ++joined;
+    }
+    for (int i = 0; i < nb; ++i) {
+      if (!c.bucket[i]) continue;
+      double a = 0, b = 0;
+      DTC_TRY(us(c.bwd0, c.b0[i], a));
+      DTC_TRY(us(c.bwd0, c.b1[i], b));
+      bucket_us[3 * i] += a;
+      bucket_us[3 * i + 1] += b;
+      bucket_us[3 * i + 2] += b - a;
+      ++bcount[i];
+    }
+    ++recorded;
+  }
+  if (recorded) {
+    exposed_us[0] /= recorded;
+    exposed_us[3] /= recorded;
+  }
+  if (joined) exposed_us[1] /= joined;
+  exposed_us[2] = exposed_us[0] + exposed_us[1];
+  exposed_us[4] = joined;
+  for (int i = 0; i < nb; ++i)
+    if (bcount[i])
+      for (int j = 0; j < 3; ++j) bucket_us[3 * i + j] /= bcount[i];
+  *steps = recorded;
+  ct_free(n);
   return 0;
 }
 

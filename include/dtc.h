@@ -59,7 +59,10 @@ typedef struct {
 
 enum { DTC_CONV_FWD = 0, DTC_CONV_DGRAD = 1, DTC_CONV_WGRAD = 2 };
 
-/* bytes of fp32 workspace the given pass wants (split-K partial slabs); 0 is valid for FWD/DGRAD */
+/* bytes of workspace the given pass wants: split-K partial slabs (fp32), and for FWD / DGRAD split-K also
+ * the arrival counters of the in-kernel reduction (the last workgroup of each output tile sums the slab;
+ * option splitk_ink). 0 is valid for FWD/DGRAD; a workspace with room for the slab only reduces the slab in
+ * a separate launch. */
 size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass);
 /* y[n][p][q][k] = conv(x, w); if stats != NULL, per-channel (sum, sum^2) of the bf16 output are
  * ADDED into stats[32][2][k] (fp64) — the batch statistics BatchNorm2d needs (net.py:21). */
@@ -361,6 +364,18 @@ int dtc_rn18_profile_events_result(dtc_net* net, int nkinds, double* ms_by_kind,
  * pool was used up (`pairs` too small for the region): their durations are missing from _result's totals,
  * so a caller reporting a roofline from them must refuse it when this is non-zero. */
 int dtc_rn18_profile_events_dropped(dtc_net* net, long long* dropped);
+/* Communication timing of the DDP backward (the first multi-GPU run must be diagnosable by
+ * itself): the next `steps` backward calls that carry a communicator record timing events -- the backward's
+ * start and the Reducer's join on the compute stream, each bucket collective's start / end on the stream it
+ * runs on, the compute stream's wait for the weight-gradient stream (collectives of the earlier buckets and
+ * the remaining weight gradients) before the stem weight gradient, and the tail from the last backward kernel
+ * to the join (the last bucket's collective). steps = 0 disarms. _result synchronises and returns means over
+ * the recorded steps: bucket_us[3 * i + 0 / 1 / 2] = start / end offset from the backward's start and the
+ * collective's duration for bucket i < max_buckets (issue order); exposed_us[0] = tail (last kernel -> join),
+ * [1] = the weight-gradient join wait, [2] = [0] + [1], [3] = the backward's duration, [4] = steps with a
+ * join recorded (eager backward); *steps = steps recorded. Then disarms and frees the events. */
+int dtc_rn18_comm_timing(dtc_net* net, int steps);
+int dtc_rn18_comm_timing_result(dtc_net* net, int max_buckets, double* bucket_us, double* exposed_us, int* steps);
 
 #ifdef __cplusplus
 }

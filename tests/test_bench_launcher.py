@@ -122,3 +122,16 @@ def test_prof_summary_flops_follow_the_bench_batch(tmp_path):
     assert ps.bench_gflop(str(f))[0] == 123.0
     f.write_text("not json\n")
     assert ps.bench_gflop(str(f))[0] is None
+
+
+def test_comm_timing_fields(bench):
+    """the N>1 line carries comm_exposed_us (tail + weight-gradient join wait) and buckets_us
+    (per bucket start / end / duration) from dtc_rn18_comm_timing_result's arrays."""
+    bus = [10.0, 60.0, 50.0, 70.0, 95.0, 25.0, 300.0, 310.0, 10.0]
+    exu = [12.0, 30.0, 42.0, 1200.0, 5.0]
+    exposed, buckets = bench.comm_fields(bus, exu, 5, [32.22, 10.01, 0.57])
+    assert {"tail_us", "side_join_us", "total_us", "backward_us", "steps"} <= set(exposed)
+    assert exposed["total_us"] == 42.0 and exposed["steps"] == 5
+    assert [b["bucket"] for b in buckets] == [0, 1, 2]
+    assert buckets[1] == {"bucket": 1, "mb": 10.01, "start_us": 70.0, "end_us": 95.0, "duration_us": 25.0}
+    assert bench.comm_fields(bus, exu, 0, [1.0]) == (None, None)

@@ -610,6 +610,58 @@ def test_conv_halo_configs(dtc, cuda, case, cfg, split):
     assert rel_err(dx.float().cpu().numpy(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("case,split", [((256, 4, 4, 512, 512), 0), ((256, 8, 8, 256, 256), 2),
+                                        ((256, 8, 8, 256, 256), 4), ((37, 4, 4, 512, 256), 2)])
+def test_conv_halo_splitk_in_kernel_matches_reduce_launch(dtc, cuda, case, split):
+    """Option splitk_ink: the last workgroup of each output tile sums the split-K partials
+    (sc1 write-through stores, an agent-scope arrival counter, sc1 loads) instead of a splitk_reduce launch.
+    Same sum order (0 + slab[0] + slab[1] + ...), so the bf16 outputs are bit-identical to the separate
+    reduction -- forward (+ BN statistics: the same values, their fp32 partial sums grouped per workgroup
+    instead of per reduce block), data gradient (+ residual) and the mask-bit BN-backward epilogue -- on every one of 8 repeated
+    launches (the hand-off under uneven arrival; the counters must come back to zero each time). B=256 layer4
+    (automatic split 2), layer3 forced to 2 / 4 splits, a ragged batch."""
+    N, H, W, C, K = case
+    g = np.random.default_rng(77 + split)
+    x = _to_dev_bf16(_rand_bf16((N, H, W, C), g), cuda)
+    w = _to_dev_bf16(_rand_bf16((K, 3, 3, C), g, 0.05), cuda)
+    dy = _to_dev_bf16(_rand_bf16((N, H, W, K), g), cuda)
+    res = _to_dev_bf16(_rand_bf16((N, H, W, C), g), cuda)
+    ym = _to_dev_bf16(_rand_bf16((N, H, W, C), g), cuda)
+    x1 = _to_dev_bf16(_rand_bf16((N, H, W, C), g), cuda)
+    mean1 = torch.randn(C, device=cuda) * 0.1
+    inv1 = torch.rand(C, device=cuda) + 0.5
+    lib = dtc._native.lib
+
+    def run():
+        stats = dtc.ops.new_stats(K, cuda)
+        y = dtc.ops.conv2d_fwd(x, w, 1, 1, stats=stats)
+        dx = dtc.ops.conv2d_dgrad(dy, w, (H, W), 1, 1, res=res)
+        dz, acc1, _ = dtc.ops.conv2d_dgrad_bn(dy, w, (H, W), 1, 1, ym, x1, mean1, inv1, res=res)
+        torch.cuda.synchronize()
+        return y, stats, dx, dz, acc1
+
+    prev = lib.dtc_get_option(b"splitk_ink")
+    dtc._native.call("dtc_set_option", b"halo_split", split)
+    dtc._native.call("dtc_set_option", b"bnb_fuse", 6)  # the BN-backward sums in the (reduce / halo) epilogue
+    try:
+        dtc._native.call("dtc_set_option", b"splitk_ink", 0)
+        ref = run()
+        dtc._native.call("dtc_set_option", b"splitk_ink", 1)
+        for _ in range(8):
+            out = run()
+            for a, b in ((out[0], ref[0]), (out[2], ref[2]), (out[3], ref[3])):
+                assert torch.equal(a, b)
+            for a, b in ((out[1], ref[1]), (out[4], ref[4])):  # the same values, fp32 partial sums regrouped
+                a, b = a.sum(0), b.sum(0)  # (sums of products cancel: the bound scales with each row's magnitude)
+                assert ((a - b).abs() <= 2e-5 * b.abs().amax(1, keepdim=True) + 1e-6).all(), (a - b).abs().max()
+    finally:
+        dtc._native.call("dtc_set_option", b"splitk_ink", prev)
+        dtc._native.call("dtc_set_option", b"halo_split", 0)
+        dtc._native.call("dtc_set_option", b"bnb_fuse", 0)
+    yk = ref[0].float().cpu().numpy()
+    assert rel_err(yk, O.conv2d_fwd(x.float().cpu().numpy(), w.float().cpu().numpy(), 1, 1)) < 1e-2
+
+
 GEN_CASES = [
     # (N, H, W, C, K): stride-1 3x3 shapes the classic whole-row halo tiles do not fit (option halo_gen)
     (2, 8, 224, 64, 64),     # 56-pixel row segments, 2 rows per 128-slot tile

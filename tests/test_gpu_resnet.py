@@ -684,8 +684,10 @@ def test_bn_sums_in_dgrad_epilogues_match_reduce_pass(dtc, cuda, batch, hw, mode
     separate mask-bit pass) from the forward's ReLU mask bits, vs the separate reduction kernels. Same
     values summed over other fp32 partials (the dgrad tiles instead of the reduction's slices): what the
     backward computes before the first fused BN (linear, layer4.1's conv2 and bn2) agrees to 1e-5, every
-    other gradient to 1e-2 (last-bit BN-coefficient differences flip bf16 roundings of the data
-    gradients, which propagate -- a wrong sum would be off by O(1)); graphs on and off, finite. Mode 2
+    other gradient to 2e-2 (last-bit BN-coefficient differences flip bf16 roundings of the data
+    gradients, which propagate through up to 16 layers -- layer1.0.bn1 at batch 8 measured 1.1% once the
+    layer4 split-K dgrad's fused sums moved into the conv epilogue (round 5, splitk_ink); a wrong sum would be
+    off by O(1)); graphs on and off, finite. Mode 2
     fuses in the halo and split-K epilogues only (the persistent layer1 kernel's BNs keep the separate
     mask-bit pass, after the dgrad). Both arms use the two-pass BN backward where the sums are not fused
     (bn_cg=0: the one-launch kernel groups its sums differently again; test_bn_one_launch_matches_two_pass)."""
@@ -706,7 +708,7 @@ def test_bn_sums_in_dgrad_epilogues_match_reduce_pass(dtc, cuda, batch, hw, mode
             for pe in lay.params:
                 a = ga[rep][pe.offset:pe.offset + pe.numel]
                 b = gb[rep][pe.offset:pe.offset + pe.numel]
-                tol = 1e-5 if pe.name.startswith(("linear", "layer4.1.conv2", "layer4.1.bn2")) else 1e-2
+                tol = 1e-5 if pe.name.startswith(("linear", "layer4.1.conv2", "layer4.1.bn2")) else 2e-2
                 assert rel_err(b, a) < tol, (graphs, rep, pe.name, rel_err(b, a))
 
 
