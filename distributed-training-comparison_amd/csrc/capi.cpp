@@ -201,15 +201,14 @@ int dtc_install_crash_handler(void) {
 size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass) {
   if (!desc_ok(d) || pass < 0 || pass > 2) return 0;
   const size_t slab = plan_conv(shape_of(d), pass).slab_bytes;
-  // FWD / DGRAD split-K: + the arrival counters of the in-kernel reduction at the workspace's end
-  return slab > 0 && pass != 2 ? slab + (size_t)DTC_TICKS * 4 : slab;
+  // split-K: + the arrival counters of the in-kernel reduction at the workspace's end
+  return slab > 0 ? slab + (size_t)DTC_TICKS * 4 : slab;
 }
 
 // FWD / DGRAD workspace: [split-K slab][DTC_TICKS u32 arrival counters] when it holds both (the counters of
 // the in-kernel reduction are zeroed on the call's stream first; the workspace is scratch between calls),
 // else the whole of it is slab and a split-K plan reduces in a separate launch.
-static unsigned* op_ticks(const dtc_conv_desc* d, int pass, void* ws, size_t& ws_bytes, hipStream_t st) {
-  const size_t slab = plan_conv(shape_of(d), pass).slab_bytes;
+static unsigned* ws_ticks(size_t slab, void* ws, size_t& ws_bytes, hipStream_t st) {
   const size_t tb = (size_t)DTC_TICKS * 4;
   if (ws == nullptr || slab == 0 || ws_bytes < slab + tb) return nullptr;
   const uintptr_t end = ((uintptr_t)ws + ws_bytes - tb) & ~(uintptr_t)255;
@@ -217,6 +216,9 @@ static unsigned* op_ticks(const dtc_conv_desc* d, int pass, void* ws, size_t& ws
   if (hipMemsetAsync((void*)end, 0, tb, st) != hipSuccess) return nullptr;
   ws_bytes = end - (uintptr_t)ws;
   return (unsigned*)end;
+}
+static unsigned* op_ticks(const dtc_conv_desc* d, int pass, void* ws, size_t& ws_bytes, hipStream_t st) {
+  return ws_ticks(plan_conv(shape_of(d), pass).slab_bytes, ws, ws_bytes, st);
 }
 
 int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, void* ws,
@@ -273,26 +275,29 @@ int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* 
                      size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && dy && dw && ws, "dtc_conv2d_wgrad: null argument (workspace is required)");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_wgrad: unsupported convolution descriptor");
-  GUARD(return conv_wgrad(shape_of(d), x, dy, dw, 0, 0, scale, (float*)ws, ws_bytes, S(stream));)
+  unsigned* tick = op_ticks(d, CONV_WGRAD, ws, ws_bytes, S(stream));
+  GUARD(return conv_wgrad(shape_of(d), x, dy, dw, 0, 0, scale, (float*)ws, ws_bytes, S(stream), nullptr, tick);)
 }
 
 size_t dtc_conv2d_wgrad_sc_workspace_size(const dtc_conv_desc* d) {
   if (!desc_ok(d)) return 0;
   const ConvShape s = shape_of(d);
-  return wgrad_s2_splits(s) > 0 ? conv_wgrad_s2_slab_bytes(s) : 0;
+  return wgrad_s2_splits(s) > 0 ? conv_wgrad_s2_slab_bytes(s) + (size_t)DTC_TICKS * 4 : 0;
 }
 
 int dtc_conv2d_wgrad_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* dy, const uint16_t* dsc, float* dw,
                         float* dw_sc, float scale, void* ws, size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && dy && dsc && dw && dw_sc, "dtc_conv2d_wgrad_sc: null argument");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_wgrad_sc: unsupported convolution descriptor");
-  GUARD(return conv_wgrad_s2(shape_of(d), x, dy, dsc, dw, dw_sc, scale, (float*)ws, ws ? ws_bytes : 0, S(stream));)
+  unsigned* tick = ws_ticks(conv_wgrad_s2_slab_bytes(shape_of(d)), ws, ws_bytes, S(stream));
+  GUARD(return conv_wgrad_s2(shape_of(d), x, dy, dsc, dw, dw_sc, scale, (float*)ws, ws ? ws_bytes : 0, S(stream), nullptr,
+                             tick);)
 }
 
 size_t dtc_conv2d_wgrad_batch_workspace_size(const dtc_conv_desc* d, int n) {
   if (!desc_ok(d) || n < 1 || n > DTC_WG_BATCH) return 0;
   const ConvShape s = shape_of(d);
-  return wgrad_halo_splits(s, n) > 0 ? conv_wgrad_batch_slab_bytes(s, n) : 0;
+  return wgrad_halo_splits(s, n) > 0 ? conv_wgrad_batch_slab_bytes(s, n) + (size_t)DTC_TICKS * 4 : 0;
 }
 
 int dtc_conv2d_wgrad_batch(const dtc_conv_desc* d, int n, const uint16_t* const* x, const uint16_t* const* dy,
@@ -300,7 +305,8 @@ int dtc_conv2d_wgrad_batch(const dtc_conv_desc* d, int n, const uint16_t* const*
   DTC_CHECK_ARG(d && x && dy && dw && ws && n >= 1 && n <= DTC_WG_BATCH, "dtc_conv2d_wgrad_batch: bad argument");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_wgrad_batch: unsupported convolution descriptor");
   for (int i = 0; i < n; ++i) DTC_CHECK_ARG(x[i] && dy[i] && dw[i], "dtc_conv2d_wgrad_batch: null problem %d", i);
-  GUARD(return conv_wgrad_batch(shape_of(d), n, x, dy, dw, scale, (float*)ws, ws_bytes, S(stream));)
+  unsigned* tick = ws_ticks(conv_wgrad_batch_slab_bytes(shape_of(d), n), ws, ws_bytes, S(stream));
+  GUARD(return conv_wgrad_batch(shape_of(d), n, x, dy, dw, scale, (float*)ws, ws_bytes, S(stream), nullptr, tick);)
 }
 
 int dtc_bn_fwd_finalize(double* stats, int c, int64_t count, const float* gamma, const float* beta,

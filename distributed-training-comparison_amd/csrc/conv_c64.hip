@@ -216,28 +216,42 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   // BN-backward operands (y, x; option bnb_fuse) are still loaded in the epilogue: prefetching them
   // too would need 96 more VGPRs than the wave has.
   typedef int i32x2 __attribute__((ext_vector_type(2)));
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  // 16-B epilogue accesses (MI355X guide T21, for the 16x16 MFMA layout): lane l holds channels rq..rq+3 of
+  // fragment i, and lane l ^ 16 the next four. One v_permlane16_swap per dword of a fragment pair (2p, 2p+1)
+  // gives the lanes of rows 0 / 2 the 8 consecutive channels 32p + {0, 8}.. of fragment 2p and the lanes of rows
+  // 1 / 3 those of fragment 2p + 1 -- one dwordx4 store per pair instead of two dwordx2 (the stores were
+  // issue-bound: 8-B accesses move half the bytes per vector-memory instruction). The swap is an involution,
+  // so a 16-B residual load is turned back into the MFMA layout the same way.
+  const int r4 = lane >> 4;
+  const int wch = (r4 & 1) * 16 + (r4 >> 1) * 8;  // this lane's first channel within a fragment pair (16 B)
+  auto swap2 = [](uint32_t& x, uint32_t& y) {  // rows 1 / 3 of x <-> rows 0 / 2 of y
+    const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+  };
   struct EpiOps {
-    i32x2 r[FN][FM];
+    i32x4 r[FN][FM / 2];
   };
   // VMEM ops the previous tile's epilogue leaves in flight per wave at the halo wait: stores (+ y, x)
-  constexpr int EPI_VM = 16 + (BNB ? 32 : 0);
-  auto epi_off = [&](int tile, int j, int i) {
+  constexpr int EPI_VM = FN * FM / 2 + (BNB ? 32 : 0);
+  // byte offset of channel `ch` of pixel column j (pixel bcol0 + 16 j + lane % 16) of a tile
+  auto epi_off_ch = [&](int tile, int j, int ch) {
     const int l = bcol0 + j * 16 + fpx;
     if constexpr (GEN) {  // slot l = row l / 32, column l % 32 of the tile; byte offset from its first pixel
-      return (uint32_t)((((l >> 5) * p.W + (l & 31)) * 64 + i * 16 + rq) * 2);
+      return (uint32_t)((((l >> 5) * p.W + (l & 31)) * 64 + ch) * 2);
     }
     const int pix = tile * 256 + l;  // tiles are 256 consecutive pixels
-    return pix < M ? (uint32_t)((pix * 64 + i * 16 + rq) * 2) : 0x80000000u;
+    return pix < M ? (uint32_t)((pix * 64 + ch) * 2) : 0x80000000u;
   };
+  auto epi_off = [&](int tile, int j, int i) { return epi_off_ch(tile, j, i * 16 + rq); };
   auto prefetch = [&](EpiOps& o, int tile) {
     const __amdgpu_buffer_rsrc_t rr = GEN ? tile_rsrc(RES ? p.res : p.out, gen_base(tile) * 128) : rrsrc;
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const uint32_t off = epi_off(tile, j, i);
-        o.r[j][i] = __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0);
-      }
+      for (int q = 0; q < FM / 2; ++q)
+        o.r[j][q] = __builtin_amdgcn_raw_buffer_load_b128(rr, epi_off_ch(tile, j, q * 32 + wch), 0, 0);
   };
 
   // epilogue of one finished tile: exactly FM*FN buffer stores per wave; lanes of pixels past M, or
@@ -256,6 +270,18 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     }
     uint32_t off[FM];
     i32x2 yy[FM], xx[FM];
+    uint32_t rres[FM][2];  // RES: the residual of each fragment in the MFMA layout (packed bf16 x 4)
+    if constexpr (RES) {
+#pragma unroll
+      for (int q = 0; q < FM / 2; ++q) {
+        uint32_t x0 = (uint32_t)o.r[j][q].x, x1 = (uint32_t)o.r[j][q].y, y0 = (uint32_t)o.r[j][q].z,
+                 y1 = (uint32_t)o.r[j][q].w;
+        swap2(x0, y0);
+        swap2(x1, y1);
+        rres[2 * q][0] = x0; rres[2 * q][1] = x1;
+        rres[2 * q + 1][0] = y0; rres[2 * q + 1][1] = y1;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       off[i] = ok ? epi_off(tile, j, i) : 0x80000000u;
@@ -272,6 +298,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
         xx[i] = __builtin_amdgcn_raw_buffer_load_b64(xrs, off[i], 0, 0);
       }
     }
+    uint32_t packed[FM][2];
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       float v[4];
@@ -287,9 +314,8 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = a[i][j][t];
         if constexpr (RES) {
-          const i32x2 rr = o.r[j][i];
-          v[0] += bf_lo((uint32_t)rr.x); v[1] += bf_hi((uint32_t)rr.x);
-          v[2] += bf_lo((uint32_t)rr.y); v[3] += bf_hi((uint32_t)rr.y);
+          v[0] += bf_lo(rres[i][0]); v[1] += bf_hi(rres[i][0]);
+          v[2] += bf_lo(rres[i][1]); v[3] += bf_hi(rres[i][1]);
         }
         if constexpr (BNB) {
           const float yv[4] = {bf_lo((uint32_t)yy[i].x), bf_hi((uint32_t)yy[i].x), bf_lo((uint32_t)yy[i].y),
@@ -304,10 +330,16 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
           }
         }
       }
-      i32x2 wv;
-      wv.x = (int)pack_bf2(v[0], v[1]);
-      wv.y = (int)pack_bf2(v[2], v[3]);
-      __builtin_amdgcn_raw_buffer_store_b64(wv, ors, off[i], 0, 0);
+      packed[i][0] = pack_bf2(v[0], v[1]);
+      packed[i][1] = pack_bf2(v[2], v[3]);
+    }
+#pragma unroll
+    for (int q = 0; q < FM / 2; ++q) {  // fragment pair (2q, 2q + 1) -> one 16-B store per lane
+      uint32_t x0 = packed[2 * q][0], x1 = packed[2 * q][1], y0 = packed[2 * q + 1][0], y1 = packed[2 * q + 1][1];
+      swap2(x0, y0);
+      swap2(x1, y1);
+      const uint32_t o16 = ok ? epi_off_ch(tile, j, q * 32 + wch) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)x0, (int)x1, (int)y0, (int)y1}, ors, o16, 0, 0);
     }
   };
   auto epilogue = [&](const f32x4 (&a)[FM][FN], const EpiOps& o, int tile, bool have) {
@@ -329,8 +361,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     // this tile's halo (and the residual issued before it) have landed; the previous iteration's
     // epilogue VMEM ops (FM*FN stores, + the BN-backward y/x loads) were issued after it
     if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (EPI_VM == 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_VM) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const uint32_t hb = halo_lds + (uint32_t)((k & 1) * C64_HBYTES);

@@ -603,18 +603,37 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = sum[i][j];
   }
+  // 16-B epilogue accesses (MI355X guide T21 for the 16x16 MFMA layout; as conv_c64.hip): lanes l and l ^ 16 hold
+  // channels rq.. and rq + 4.. of the same pixel, so one v_permlane16_swap per dword of a fragment pair (2q, 2q+1)
+  // leaves 8 consecutive channels per lane -- one dwordx4 store instead of two dwordx2 (issue-bound epilogues).
+  // Both lanes of a swap pair hold the same pixel, so a pixel's validity is uniform across each swap.
+  // (the lane id through an opaque move: the epilogue's lane-dependent offsets are computed here, not hoisted
+  // before the main loop and held across it -- the 64 x 256 kernels run at the 2-waves-per-SIMD register limit)
+  int ln;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+  const int r4 = ln >> 4;
+  const int wch = (r4 & 1) * 16 + (r4 >> 1) * 8;  // this lane's first channel within a fragment pair (16 B)
+  auto swap2 = [](uint32_t& x, uint32_t& y) {  // rows 1 / 3 of x <-> rows 0 / 2 of y
+    const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+  };
+  static_assert(FM % 2 == 0, "fragment pairs");
   if constexpr (MODE == 0) {
     float* red = (float*)smem;  // [WC][BM][2]
     auto epi_fwd = [&](f32x4 (&A)[SC ? FM : 1][SC ? FN : 1], f32x4 (&B)[FM][FN], bool second, u16* outp, double* stp) {
       const bool want_stats = stp != nullptr;
+      float s4[FM][4], q4[FM][4];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int chl = arow0 + i * 16 + rq;
-        const int ch = a0 + chl;
-        float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int pix = slot_pix(bcol0 + j * 16 + cl);
+        for (int t = 0; t < 4; ++t) s4[i][t] = q4[i][t] = 0.f;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int pix = slot_pix(bcol0 + j * 16 + cl);
+        uint32_t pk[FM][2];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
           const f32x4 a = second ? A[SC ? i : 0][SC ? j : 0] : B[i][j];
           float v[4];
 #pragma unroll
@@ -622,31 +641,38 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
           if (pix < M) {
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-              s4[t] += v[t];
-              q4[t] += v[t] * v[t];
+              s4[i][t] += v[t];
+              q4[i][t] += v[t] * v[t];
             }
-            uint2 wv;
-            wv.x = pack_bf2(v[0], v[1]);
-            wv.y = pack_bf2(v[2], v[3]);
-            *(uint2*)(outp + (size_t)pix * p.Cout + ch) = wv;
           }
+          pk[i][0] = pack_bf2(v[0], v[1]);
+          pk[i][1] = pack_bf2(v[2], v[3]);
         }
-        if (want_stats) {
+#pragma unroll
+        for (int q = 0; q < FM / 2; ++q) {
+          uint32_t x0 = pk[2 * q][0], x1 = pk[2 * q][1], y0 = pk[2 * q + 1][0], y1 = pk[2 * q + 1][1];
+          swap2(x0, y0);
+          swap2(x1, y1);
+          if (pix < M) *(uint4*)(outp + (size_t)pix * p.Cout + a0 + arow0 + q * 32 + wch) = uint4{x0, x1, y0, y1};
+        }
+      }
+      if (want_stats) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int chl = arow0 + i * 16 + rq;
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            s4[t] = row16_sum(s4[t]);
-            q4[t] = row16_sum(q4[t]);
+            s4[i][t] = row16_sum(s4[i][t]);
+            q4[i][t] = row16_sum(q4[i][t]);
           }
           if ((lane & 15) == 0) {
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-              red[(wc * BM + chl + t) * 2 + 0] = s4[t];
-              red[(wc * BM + chl + t) * 2 + 1] = q4[t];
+              red[(wc * BM + chl + t) * 2 + 0] = s4[i][t];
+              red[(wc * BM + chl + t) * 2 + 1] = q4[i][t];
             }
           }
         }
-      }
-      if (want_stats) {
         __syncthreads();
         if ((int)threadIdx.x < BM) {
           float s = 0.f, q = 0.f;
@@ -725,23 +751,36 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int pix = slot_pix(bcol0 + j * 16 + cl);
-      if (pix >= M) continue;
-      uint2 rr[FM];  // the residuals of all FM fragments in flight before the first store
+      const bool ok = pix < M;
+      const size_t o = (size_t)(ok ? pix : 0) * p.Cout + a0 + arow0 + wch;  // + 32 q: fragment pair q
+      uint4 rr[FM / 2];  // the residuals of all FM fragments in flight before the first store (16-B loads)
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        rr[i] = p.res ? *(const uint2*)(p.res + (size_t)pix * p.Cout + a0 + arow0 + i * 16 + rq) : uint2{0u, 0u};
+      for (int q = 0; q < FM / 2; ++q) rr[q] = p.res && ok ? *(const uint4*)(p.res + o + q * 32) : uint4{0u, 0u, 0u, 0u};
+      uint32_t res2[FM][2];
+#pragma unroll
+      for (int q = 0; q < FM / 2; ++q) {  // back to the MFMA layout (the swap is an involution)
+        uint32_t x0 = rr[q].x, x1 = rr[q].y, y0 = rr[q].z, y1 = rr[q].w;
+        swap2(x0, y0);
+        swap2(x1, y1);
+        res2[2 * q][0] = x0; res2[2 * q][1] = x1;
+        res2[2 * q + 1][0] = y0; res2[2 * q + 1][1] = y1;
+      }
+      uint32_t pk[FM][2];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int ch = a0 + arow0 + i * 16 + rq;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        const size_t o = (size_t)pix * p.Cout + ch;
         if (p.res) {
-          v[0] += bf_lo(rr[i].x); v[1] += bf_hi(rr[i].x); v[2] += bf_lo(rr[i].y); v[3] += bf_hi(rr[i].y);
+          v[0] += bf_lo(res2[i][0]); v[1] += bf_hi(res2[i][0]); v[2] += bf_lo(res2[i][1]); v[3] += bf_hi(res2[i][1]);
         }
-        uint2 wv;
-        wv.x = pack_bf2(v[0], v[1]);
-        wv.y = pack_bf2(v[2], v[3]);
-        *(uint2*)(p.out + o) = wv;
+        pk[i][0] = pack_bf2(v[0], v[1]);
+        pk[i][1] = pack_bf2(v[2], v[3]);
+      }
+#pragma unroll
+      for (int q = 0; q < FM / 2; ++q) {
+        uint32_t x0 = pk[2 * q][0], x1 = pk[2 * q][1], y0 = pk[2 * q + 1][0], y1 = pk[2 * q + 1][1];
+        swap2(x0, y0);
+        swap2(x1, y1);
+        if (ok) *(uint4*)(p.out + o + q * 32) = uint4{x0, x1, y0, y1};
       }
     }
   }

@@ -1000,6 +1000,10 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
   p.fd_cc = make_fastdiv(s.K / 64);
   p.num_kt = pl.num_kt;
   p.tiles_a = s.C / pl.bm;
+  if (dgrad_class_mode(s) && res == nullptr && dgrad_s2_halo_ok(s)) {  // the halo sub-pixel kernel (dgrad_s2.hip)
+    DTC_TRY(conv_dgrad_s2_halo(s, dy, w, dx, nullptr, nullptr, st, ts));
+    return bnb_after(bnb, dx, (int64_t)s.N * s.H * s.W, s.C, st);
+  }
   if (dgrad_class_mode(s)) {  // four parity-class GEMMs in one launch (blockIdx.z), no split-K
     p.cls = 1;
     p.cls_order = option_get(OPT_DGRAD_CLASS_ORDER);
@@ -1042,6 +1046,10 @@ int conv_dgrad_sc(const ConvShape& s, const u16* dy, const u16* w, u16* dx, cons
                   hipStream_t st, u64* ts, const BnbArgs* bnb) {
   DTC_CHECK_ARG(conv_dgrad_sc_ok(s) && dy && w && dx && dsc && wsc, "conv_dgrad_sc: unsupported geometry / args");
   if (bnb != nullptr && !bnb_on(*bnb)) bnb = nullptr;
+  if (dgrad_s2_halo_ok(s)) {  // option dgrad_s2h: the halo sub-pixel kernel (dgrad_s2.hip), shortcut fused
+    DTC_TRY(conv_dgrad_s2_halo(s, dy, w, dx, dsc, wsc, st, ts));
+    return bnb_after(bnb, dx, (int64_t)s.N * s.H * s.W, s.C, st);
+  }
   IGemmParams p{};
   p.ts = ts;
   DTC_TRY(fill_common(p, s));
@@ -1085,10 +1093,10 @@ static int launch_wgrad_reduce(const float* slab, int splits, int K, int RSC, in
 }
 
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
-               float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
+               float* slab, size_t slab_bytes, hipStream_t st, u64* ts, unsigned* tick) {
   if (wgrad_s2_splits(s) > 0 && (dw_cols <= 0 || dw_cols == 9 * s.C) && (dw_ld <= 0 || dw_ld == 9 * s.C) &&
       slab_bytes >= conv_wgrad_s2_slab_bytes(s))
-    return conv_wgrad_s2(s, x, dy, nullptr, dw, nullptr, scale, slab, slab_bytes, st, ts);
+    return conv_wgrad_s2(s, x, dy, nullptr, dw, nullptr, scale, slab, slab_bytes, st, ts, tick);
   IGemmParams p{};
   p.ts = ts;
   DTC_TRY(fill_common(p, s));
@@ -1109,8 +1117,8 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
   int splits = pl.splits;
   if (pl.bm == 576 && slab_bytes >= pl.slab_bytes) {
     const bool whole = (dw_cols <= 0 || dw_cols == p.RSC) && (dw_ld <= 0 || dw_ld == p.RSC);
-    DTC_TRY(conv_wgrad_halo(s, 1, &x, &dy, slab, pl.splits, &splits, st, ts, whole ? &dw : nullptr, scale));
-    if (splits == 0) return 0;  // one split: the halo kernel wrote dw itself
+    DTC_TRY(conv_wgrad_halo(s, 1, &x, &dy, slab, pl.splits, &splits, st, ts, whole ? &dw : nullptr, scale, tick));
+    if (splits == 0) return 0;  // one split or reduced in the kernel: the halo kernel wrote dw itself
   } else {
     if (pl.bm == 576) pl = ConvPlan{64, 64, 1, ceil_div(p.M, 64), 0};  // workspace too small for the halo plan
     p.num_kt = pl.num_kt;
@@ -1142,13 +1150,13 @@ size_t conv_wgrad_batch_slab_bytes(const ConvShape& s, int nprob) {
 }
 
 int conv_wgrad_batch(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* const* dw,
-                     float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
+                     float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts, unsigned* tick) {
   const int hs = wgrad_halo_splits(s, nprob);
   if (hs <= 0 || slab == nullptr || slab_bytes < conv_wgrad_batch_slab_bytes(s, nprob))
     return set_error(DTC_EINVAL, "conv_wgrad_batch: no halo plan for %d problems or slab too small", nprob);
   int splits = hs;
-  DTC_TRY(conv_wgrad_halo(s, nprob, x, dy, slab, hs, &splits, st, ts, dw, scale));
-  if (splits == 0) return 0;  // one split: the halo kernel wrote dw itself
+  DTC_TRY(conv_wgrad_halo(s, nprob, x, dy, slab, hs, &splits, st, ts, dw, scale, tick));
+  if (splits == 0) return 0;  // one split or reduced in the kernel: the halo kernel wrote dw itself
   const int RSC = s.R * s.S * s.C;
   WgOuts outs{};
   for (int i = 0; i < nprob; ++i) outs.dw[i] = dw[i];

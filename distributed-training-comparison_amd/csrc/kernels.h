@@ -67,7 +67,10 @@ namespace dtc {
   X(C64_GEN, c64_gen, 1)                /* conv_c64 general tiles (224x224 layer1) */                         \
   X(SPLITK_INK, splitk_ink, 1)          /* conv split-K summed by the last workgroup per tile (no reduce launch) */ \
   X(COMM_PRIO, comm_prio, 0)            /* (communicator creation) its own stream: 0 normal, 1 most urgent */ \
-  X(COMM_TAIL_INLINE, comm_tail_inline, 1) /* the last bucket's all-reduce on the compute stream (no fork / join) */
+  X(COMM_TAIL_INLINE, comm_tail_inline, 1) /* the last bucket's all-reduce on the compute stream (no fork / join) */ \
+  X(WGRAD_INK, wgrad_ink, 1)            /* wgrad split-K summed by the last workgroup per tile: 1 stride-2, 2 all */ \
+  X(WGRAD_INK_MAX, wgrad_ink_max, 8)    /* ... for launches of at most this many splits (else a reduce launch) */ \
+  X(DGRAD_S2H, dgrad_s2h, 1)            /* stride-2 3x3 dgrad (+ fused shortcut) as a halo sub-pixel conv (dgrad_s2.hip) */
 
 enum {
 #define DTC_OPT_ENUM(id, name, def) OPT_##id,
@@ -118,6 +121,11 @@ bool dgrad_class_ok(const ConvShape& s);
 // dx = dgrad(dy, w) + dgrad_1x1_s2(dsc, wsc) for a projection block's 3x3 stride-2 conv1 and its shortcut
 // in one parity-class launch (dsc [N][H/2][W/2][K], wsc [K][C])
 bool conv_dgrad_sc_ok(const ConvShape& s);
+// stride-2 3x3 pad-1 dgrad as a halo-tiled sub-pixel convolution (dgrad_s2.hip), optionally + the 1x1 stride-2
+// shortcut's dgrad (dsc [N][H/2][W/2][K], wsc [K][C]) at the even / even pixels
+bool dgrad_s2_halo_ok(const ConvShape& s);
+int conv_dgrad_s2_halo(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* dsc, const u16* wsc,
+                       hipStream_t st, u64* ts = nullptr);
 int conv_dgrad_sc(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* dsc, const u16* wsc,
                   hipStream_t st, u64* ts = nullptr, const BnbArgs* bnb = nullptr);
 int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* res, float* slab,
@@ -125,7 +133,7 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
                int res_compact = 0, unsigned* tick = nullptr);
 // dw[k][0:dw_cols] (row stride dw_ld) = scale * sum_pixels dy (x) im2col(x); fp32
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
-               float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
+               float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr, unsigned* tick = nullptr);
 // Halo-tiled WGRAD for 3x3 / stride 1 / pad 1 (wgrad_halo.hip): split count it would use for s
 // batched nprob at a time (0 = not applicable / disabled), and the launch writing
 // slab[nprob][used][K][9C] (reduce separately).
@@ -139,15 +147,20 @@ int wgrad_halo_splits(const ConvShape& s, int nprob = 1);
 int wgrad_s2_splits(const ConvShape& s);  // 0: no plan (option wgrad_s2 off or geometry)
 size_t conv_wgrad_s2_slab_bytes(const ConvShape& s);
 int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* dsc, float* dw, float* dw_sc,
-                  float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
+                  float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr,
+                  unsigned* tick = nullptr);
+// tick (optional, as conv_fwd's): with it a launch of at most wgrad_ink_max splits reduces in the kernel
+// (*used_splits = 0, dw written) instead of leaving the slab to a reduce launch
 int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* slab, int splits,
-                    int* used_splits, hipStream_t st, u64* ts, float* const* dw = nullptr, float scale = 1.f);
+                    int* used_splits, hipStream_t st, u64* ts, float* const* dw = nullptr, float scale = 1.f,
+                    unsigned* tick = nullptr);
 // nprob (<= DTC_WG_BATCH) independent weight gradients of one 3x3 stride-1 geometry in one halo
 // launch + one reduce launch: dw[i] = scale * wgrad(x[i], dy[i]). Returns DTC_EINVAL when the
 // geometry has no halo plan or the slab is too small (callers then issue them one by one).
 size_t conv_wgrad_batch_slab_bytes(const ConvShape& s, int nprob);
 int conv_wgrad_batch(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* const* dw,
-                     float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
+                     float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr,
+                     unsigned* tick = nullptr);
 // Halo-tiled 3x3 / stride 1 FWD and DGRAD (conv_halo.hip): configuration for the pass (-1: not
 // applicable), and the launch (FWD: stats optional; DGRAD: res optional).
 // Persistent 64-channel 3x3 stride-1 FWD / DGRAD (conv_c64.hip).

@@ -85,6 +85,7 @@ struct Net {
   size_t DC0 = 0, SLABW = 0;  // stem conv-output gradient; split-K slab of the side-stream wgrads
   size_t TICK = 0;            // split-K arrival counters: [0] compute stream, [1] weight-gradient stream
   unsigned* tick(int i) { return (unsigned*)(ws + TICK) + (size_t)i * DTC_TICKS; }
+  unsigned* tick_on(hipStream_t s) { return tick(s != nullptr && s == side_st ? 1 : 0); }  // the launch stream's set
   size_t BNERR = 0;           // int: set by a one-pass BN backward whose grid barrier timed out
   // backward weight gradients run on a side stream (option bwd_streams), overlapped with the
   // data-gradient / BN chain; forked after the conv-output gradient exists, joined at bucket points
@@ -1158,10 +1159,12 @@ static int wg_flush(Net& n, WgQueue& q, float gs, float* slabw, hipStream_t sd) 
   const int np = q.count;
   q.count = 0;
   if (np == 1) {
-    PROF(2, conv_flops(q.s), conv_wgrad(q.s, q.x[0], q.dy[0], q.dw[0], 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+    PROF(2, conv_flops(q.s),
+         conv_wgrad(q.s, q.x[0], q.dy[0], q.dw[0], 0, 0, gs, slabw, n.slab_bytes, sd, ts, n.tick_on(sd)));
     return 0;
   }
-  PROF(2, conv_flops(q.s) * np, conv_wgrad_batch(q.s, np, q.x, q.dy, q.dw, gs, slabw, n.slab_bytes, sd, ts));
+  PROF(2, conv_flops(q.s) * np,
+       conv_wgrad_batch(q.s, np, q.x, q.dy, q.dw, gs, slabw, n.slab_bytes, sd, ts, n.tick_on(sd)));
   return 0;
 }
 static int fork_side(Net& n, hipStream_t st, hipStream_t* out);
@@ -1173,7 +1176,7 @@ static int wg_issue(Net& n, WgQueue& q, const ConvShape& s, const u16* x, const 
   const int bmax = wgrad_batch_max();
   if (bmax <= 1 || wgrad_halo_splits(s, 2) <= 0) {
     if (lazy) DTC_TRY(fork_side(n, st, &sd));
-    PROF(2, conv_flops(s), conv_wgrad(s, x, dy, dw, 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+    PROF(2, conv_flops(s), conv_wgrad(s, x, dy, dw, 0, 0, gs, slabw, n.slab_bytes, sd, ts, n.tick_on(sd)));
     return 0;
   }
   if (q.count > 0 && !same_shape(q.s, s)) {
@@ -1306,7 +1309,8 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
                      b.sc.s.R == 1 && b.sc.s.stride == 2 && b.sc.s.C == b.c1.s.C && b.sc.s.K == b.c1.s.K;
     if (wsc) {
       PROF(2, conv_flops(b.c1.s) + conv_flops(b.sc.s),
-           conv_wgrad_s2(b.c1.s, in, dc1, dsc, n.gf(b.c1.pidx), n.gf(b.sc.pidx), gs, slabw, n.slab_bytes, sd, ts));
+           conv_wgrad_s2(b.c1.s, in, dc1, dsc, n.gf(b.c1.pidx), n.gf(b.sc.pidx), gs, slabw, n.slab_bytes, sd, ts,
+                         n.tick_on(sd)));
     } else {
       DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, st, lazy && !b.proj));
     }
@@ -1322,7 +1326,8 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     const BnbArgs* bpp = bmf ? &bp : nullptr;
     if (b.proj) {
       if (!wsc)
-        PROF(2, conv_flops(b.sc.s), conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
+        PROF(2, conv_flops(b.sc.s),
+             conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts, n.tick_on(sd)));
       if (dscf) {
         PROF(1, conv_flops(b.c1.s) + conv_flops(b.sc.s),
              conv_dgrad_sc(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], dsc, n.wbf(b.sc.pidx), st, ts, bpp));

@@ -846,3 +846,101 @@ def test_conv_dgrad_bn_fused(dtc, cuda, case, split):
     for a1, a0 in [(a11, a10)] + ([(a21, a20)] if dual else []):
         s1, s0 = a1.sum(0).cpu().numpy(), a0.sum(0).cpu().numpy()
         np.testing.assert_allclose(s1, s0, rtol=1e-5, atol=1e-3 * np.abs(s0).max())
+
+
+@pytest.mark.parametrize("case", [("batch", (256, 8, 8, 256, 256), 3, 0), ("batch", (256, 16, 16, 128, 128), 3, 8),
+                                  ("batch", (64, 8, 8, 256, 256), 2, 0), ("s2", (256, 8, 8, 256, 512), 1, 0),
+                                  ("s2", (64, 16, 16, 128, 256), 1, 0)])
+def test_wgrad_splitk_in_kernel_matches_reduce_launch(dtc, cuda, case):
+    """Option wgrad_ink: a weight-gradient launch of at most wgrad_ink_max splits sums its
+    split-K partials in the kernel (the last workgroup of each tile reads every split's sc1 partial in split
+    order and writes scale * sum; stride-2 launches also the fused shortcut's) instead of a wgrad_reduce launch.
+    Against the reduce launch (whose lanes group the splits differently: 1e-6) and the oracle (1e-5), on 6
+    repeated launches (the counters must return to zero each time); layer3 (4 splits), layer2 with a forced
+    8-split cap, the stride-2 layer4.0 conv1 + shortcut (4 splits) and a smaller batch."""
+    kind, (N, H, W, C, K), nprob, cap = case
+    g = np.random.default_rng(5 + N + C)
+    lib = dtc._native.lib
+    Ho, Wo = (H // 2, W // 2) if kind == "s2" else (H, W)
+    xs = [_to_dev_bf16(_rand_bf16((N, H, W, C), g), cuda) for _ in range(nprob)]
+    dys = [_to_dev_bf16(_rand_bf16((N, Ho, Wo, K), g), cuda) for _ in range(nprob)]
+    dsc = _to_dev_bf16(_rand_bf16((N, Ho, Wo, K), g), cuda)
+
+    def run():
+        if kind == "s2":
+            dw, dws = dtc.ops.conv2d_wgrad_sc(xs[0], dys[0], dsc, scale=0.5)
+            out = [dw, dws]
+        else:
+            out = dtc.ops.conv2d_wgrad_batch(xs, dys, scale=0.5)
+        torch.cuda.synchronize()
+        return [t.clone() for t in out]
+
+    prev, prev_cap = lib.dtc_get_option(b"wgrad_ink"), lib.dtc_get_option(b"wgrad_ink_max")
+    try:
+        if cap:
+            dtc._native.call("dtc_set_option", b"wgrad_ink_max", cap)
+        dtc._native.call("dtc_set_option", b"wgrad_ink", 0)
+        ref = run()
+        dtc._native.call("dtc_set_option", b"wgrad_ink", 2)  # every launch (1: the stride-2 ones only)
+        for _ in range(6):
+            out = run()
+            for a, b in zip(out, ref):
+                assert rel_err(a.cpu().numpy(), b.cpu().numpy()) < 1e-6
+        first = out
+        assert all(torch.equal(a, b) for a, b in zip(run(), first))  # deterministic run to run
+    finally:
+        dtc._native.call("dtc_set_option", b"wgrad_ink", prev)
+        dtc._native.call("dtc_set_option", b"wgrad_ink_max", prev_cap)
+    x0, dy0 = xs[0].float().cpu().numpy(), dys[0].float().cpu().numpy()
+    if kind == "s2":
+        dw_ref = O.conv2d_wgrad(x0, dy0, 3, 3, 2, 1)
+        assert rel_err(first[0].cpu().numpy(), 0.5 * dw_ref) < 1e-5
+        dsc_ref = O.conv2d_wgrad(x0, dsc.float().cpu().numpy(), 1, 1, 2, 0)
+        assert rel_err(first[1].cpu().numpy().reshape(dsc_ref.shape), 0.5 * dsc_ref) < 1e-5
+    else:
+        assert rel_err(first[0].cpu().numpy(), 0.5 * O.conv2d_wgrad(x0, dy0, 3, 3, 1, 1)) < 1e-5
+
+
+S2D_CASES = [(256, 32, 32, 64, 128), (256, 16, 16, 128, 256), (256, 8, 8, 256, 512), (8, 32, 32, 64, 128),
+             (3, 16, 16, 128, 256), (5, 8, 8, 256, 512), (2, 8, 8, 64, 128), (64, 16, 16, 64, 128)]
+
+
+@pytest.mark.parametrize("case", S2D_CASES)
+@pytest.mark.parametrize("sc", [True, False])
+def test_conv_dgrad_stride2_halo_subpixel(dtc, cuda, case, sc):
+    """Option dgrad_s2h (dgrad_s2.hip): the stride-2 3x3 data gradient as a halo-tiled
+    sub-pixel convolution (nine (dy offset, parity class, tap) steps over one dy halo per 64-channel chunk),
+    with the 1x1 stride-2 shortcut's dgrad fused as a tenth step of class (0, 0) -- ResNet-18's three
+    projection blocks at B=256 (128- / 64-position tiles, multi-image tiles), small and ragged batches (the
+    last tile past the tensor) -- against the oracle, and against the implicit-GEMM parity classes
+    (dgrad_s2h=0) on the same operands (same products, other summation order: 1e-2)."""
+    N, H, W, C, K = case
+    lib = dtc._native.lib
+    g = np.random.default_rng(31 + N)
+    dy = _rand_bf16((N, H // 2, W // 2, K), g)
+    dsc = _rand_bf16((N, H // 2, W // 2, K), g)
+    w = _rand_bf16((K, 3, 3, C), g, 0.05)
+    wsc = _rand_bf16((K, 1, 1, C), g, 0.1)
+    dyd, dscd, wd, wscd = (_to_dev_bf16(a, cuda) for a in (dy, dsc, w, wsc.reshape(K, C)))
+
+    def run():
+        if sc:
+            return dtc.ops.conv2d_dgrad_sc(dyd, wd, dscd, wscd, (H, W))
+        return dtc.ops.conv2d_dgrad(dyd, wd, (H, W), 2, 1)
+
+    prev = lib.dtc_get_option(b"dgrad_s2h")
+    try:
+        lib.dtc_set_option(b"dgrad_s2h", 1)
+        dx = run().float()
+        lib.dtc_set_option(b"dgrad_s2h", 0)
+        dx_gemm = run().float()
+        torch.cuda.synchronize()
+    finally:
+        lib.dtc_set_option(b"dgrad_s2h", prev)
+    ref = O.conv2d_dgrad(dy, w, (H, W), 2, 1)
+    if sc:
+        ref = ref + O.conv2d_dgrad(dsc, wsc, (H, W), 2, 0)
+    got = dx.cpu().numpy()
+    assert rel_err(got, ref) < 1e-2
+    assert rel_err(got, dx_gemm.cpu().numpy()) < 1e-2
+    assert np.isfinite(got).all()
