@@ -50,8 +50,11 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((uint32_t)v << 16); }
 // Round-to-nearest-even (v_cvt_pk_bf16_f32 on gfx950; keeps NaN a NaN).
 __device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+// two values in one v_cvt_pk_bf16_f32 (the same round-to-nearest-even per value as f2bf)
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
 

@@ -37,7 +37,6 @@ struct C64Params {
   u16* out;        // NHWC, 64 channels
   const u16* res;  // DGRAD residual or null
   double* stats;   // FWD BN statistics [SLOTS][2][64] or null
-  BnbArgs bnb;     // DGRAD modes 3/4: fused BN-backward epilogue (one BN, bnb_epi.h)
   int N, H, W;
   uint32_t src_bytes, out_bytes;
   int rows, imgs, hb, nh, tiles_y, ntiles;
@@ -59,9 +58,7 @@ __device__ __forceinline__ bf16x8 lds_frag(uint32_t addr) {
   return *(const lds_bf16x8*)(size_t)addr;
 }
 
-// MODE 0: FWD (+ BN statistics), 1: DGRAD, 2: DGRAD + residual, 3: DGRAD -> BN backward (bnb_epi.h:
-// store dz = bf16(dx) * [ym > 0], accumulate sum(dz), sum(dz * xhat) like FWD's statistics),
-// 4: DGRAD + residual -> BN backward.
+// MODE 0: FWD (+ BN statistics), 1: DGRAD, 2: DGRAD + residual.
 // Software pipelined over tiles: the epilogue of tile k-1 (bf16 rounding, statistics, stores) is
 // issued in the same basic block as tile k's 288 MFMAs, so its VALU work fills MFMA issue gaps
 // instead of running after them on the wave's single SIMD (one wave per SIMD: nothing else would
@@ -72,7 +69,7 @@ constexpr int C64_SEG = 32, C64_GROWS = 8;  // GEN tile: 8 rows x 32 columns
 template <int MODE, bool PF, bool GEN = false>
 __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   constexpr int FM = 4, FN = 4;  // wave tile: 64 channels x 64 pixels
-  constexpr bool FWD = MODE == 0, RES = MODE == 2 || MODE == 4, BNB = MODE >= 3;
+  constexpr bool FWD = MODE == 0, RES = MODE == 2;
   __shared__ __attribute__((aligned(1024))) char smem[C64_WBYTES + 2 * C64_HBYTES];
   char* const halo = smem + C64_WBYTES;
   stamp_start(p.ts);
@@ -183,38 +180,20 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)t + byte_base), 0, 0x7ffffff0u, 0x00020000);
   };
   const uint32_t halo_lds = __builtin_amdgcn_readfirstlane(lds_u32(halo));
-  // mask source: the bf16 y, or (bnb.mb) the forward's ReLU mask bits -- 1 byte per 8 channels
-  const bool mbits = BNB && p.bnb.mb != nullptr;
-  const __amdgpu_buffer_rsrc_t yrsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(BNB ? (mbits ? (const void*)p.bnb.mb : (const void*)p.bnb.ym) : (const void*)p.out), 0,
-      BNB ? (mbits ? p.out_bytes / 16 : p.out_bytes) : 0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t xrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(BNB ? p.bnb.x1 : p.out), 0, BNB ? p.out_bytes : 0, 0x00020000);
 
   const int rq = (lane >> 4) * 4;
-  // FWD: sum / sum of squares of the bf16 outputs; BNB: sum(dz) / sum(dz * xhat)
-  float ssum[FM][4], ssq[FM][4], bmean[FM][4], binv[FM][4];
+  // FWD: sum / sum of squares of the bf16 outputs
+  float ssum[FM][4], ssq[FM][4];
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) ssum[i][t] = ssq[i][t] = bmean[i][t] = binv[i][t] = 0.f;
-    if constexpr (BNB) {
-      const f32x4 m = *(const f32x4*)(p.bnb.mean1 + i * 16 + rq), v = *(const f32x4*)(p.bnb.invstd1 + i * 16 + rq);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        bmean[i][t] = m[t];
-        binv[i][t] = v[t];
-      }
-    }
-  }
+    for (int t = 0; t < 4; ++t) ssum[i][t] = ssq[i][t] = 0.f;
 
   // DGRAD residual of one tile, loaded one tile AHEAD of its use: issued right after the tile's
   // halo wait, before the next halo DMA, so it has landed by the next iteration's halo wait and the
   // epilogue (interleaved with the following tile's MFMAs) never waits on it. Loading it inside the
   // epilogue stalled the wave's only SIMD on a full HBM latency per pixel-column group (and on the
-  // younger halo DMA: vmcnt retires in order): 74 -> 26 us per layer1 dgrad at B=256. The fused
-  // BN-backward operands (y, x; option bnb_fuse) are still loaded in the epilogue: prefetching them
-  // too would need 96 more VGPRs than the wave has.
+  // younger halo DMA: vmcnt retires in order): 74 -> 26 us per layer1 dgrad at B=256.
   typedef int i32x2 __attribute__((ext_vector_type(2)));
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   // 16-B epilogue accesses (MI355X guide T21, for the 16x16 MFMA layout): lane l holds channels rq..rq+3 of
@@ -233,8 +212,8 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   struct EpiOps {
     i32x4 r[FN][FM / 2];
   };
-  // VMEM ops the previous tile's epilogue leaves in flight per wave at the halo wait: stores (+ y, x)
-  constexpr int EPI_VM = FN * FM / 2 + (BNB ? 32 : 0);
+  // VMEM ops the previous tile's epilogue leaves in flight per wave at the halo wait: its stores
+  constexpr int EPI_VM = FN * FM / 2;
   // byte offset of channel `ch` of pixel column j (pixel bcol0 + 16 j + lane % 16) of a tile
   auto epi_off_ch = [&](int tile, int j, int ch) {
     const int l = bcol0 + j * 16 + fpx;
@@ -259,17 +238,8 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   auto epilogue_col = [&](const f32x4 (&a)[FM][FN], const EpiOps& o, int tile, bool have, int j) {
     const int pix = tile * 256 + bcol0 + j * 16 + fpx;
     const bool ok = have && (GEN || pix < M);  // GEN tiles have no slot past the tensor
-    __amdgpu_buffer_rsrc_t ors = orsrc, yrs = yrsrc, xrs = xrsrc;
-    if constexpr (GEN) {
-      const int64_t b = have ? gen_base(tile) : 0;
-      ors = tile_rsrc(p.out, b * 128);
-      if constexpr (BNB) {
-        yrs = mbits ? tile_rsrc(p.bnb.mb, b * 8) : tile_rsrc(p.bnb.ym, b * 128);
-        xrs = tile_rsrc(p.bnb.x1, b * 128);
-      }
-    }
-    uint32_t off[FM];
-    i32x2 yy[FM], xx[FM];
+    __amdgpu_buffer_rsrc_t ors = orsrc;
+    if constexpr (GEN) ors = tile_rsrc(p.out, (have ? gen_base(tile) : 0) * 128);
     uint32_t rres[FM][2];  // RES: the residual of each fragment in the MFMA layout (packed bf16 x 4)
     if constexpr (RES) {
 #pragma unroll
@@ -282,56 +252,25 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
         rres[2 * q + 1][0] = y0; rres[2 * q + 1][1] = y1;
       }
     }
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      off[i] = ok ? epi_off(tile, j, i) : 0x80000000u;
-      if constexpr (BNB) {  // out-of-range lanes read zeros (descriptor bound): masked to 0, no sums
-        if (mbits) {  // element e = off / 2: bits (e & 4) .. + 3 of byte e >> 3
-          const uint32_t e = off[i] >> 1;
-          const uint32_t by = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(yrs, off[i] == 0x80000000u ? 0x80000000u : e >> 3, 0, 0);
-          const uint32_t nib = (by >> (e & 4)) & 15u;
-          yy[i].x = (int)(((nib & 1u) ? 0x3F80u : 0u) | ((nib & 2u) ? 0x3F800000u : 0u));
-          yy[i].y = (int)(((nib & 4u) ? 0x3F80u : 0u) | ((nib & 8u) ? 0x3F800000u : 0u));
-        } else {
-          yy[i] = __builtin_amdgcn_raw_buffer_load_b64(yrs, off[i], 0, 0);
-        }
-        xx[i] = __builtin_amdgcn_raw_buffer_load_b64(xrs, off[i], 0, 0);
-      }
-    }
     uint32_t packed[FM][2];
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      float v[4];
-      if constexpr (FWD) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          v[t] = round_bf(a[i][j][t]);
-          const float u = ok ? v[t] : 0.f;
-          ssum[i][t] += u;
-          ssq[i][t] += u * u;
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = a[i][j][t];
-        if constexpr (RES) {
-          v[0] += bf_lo(rres[i][0]); v[1] += bf_hi(rres[i][0]);
-          v[2] += bf_lo(rres[i][1]); v[3] += bf_hi(rres[i][1]);
-        }
-        if constexpr (BNB) {
-          const float yv[4] = {bf_lo((uint32_t)yy[i].x), bf_hi((uint32_t)yy[i].x), bf_lo((uint32_t)yy[i].y),
-                               bf_hi((uint32_t)yy[i].y)};
-          const float xv[4] = {bf_lo((uint32_t)xx[i].x), bf_hi((uint32_t)xx[i].x), bf_lo((uint32_t)xx[i].y),
-                               bf_hi((uint32_t)xx[i].y)};
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            v[t] = yv[t] > 0.f ? round_bf(v[t]) : 0.f;
-            ssum[i][t] += v[t];
-            ssq[i][t] += v[t] * ((xv[t] - bmean[i][t]) * binv[i][t]);
-          }
-        }
+      float v[4] = {a[i][j][0], a[i][j][1], a[i][j][2], a[i][j][3]};
+      if constexpr (RES) {
+        v[0] += bf_lo(rres[i][0]); v[1] += bf_hi(rres[i][0]);
+        v[2] += bf_lo(rres[i][1]); v[3] += bf_hi(rres[i][1]);
       }
       packed[i][0] = pack_bf2(v[0], v[1]);
       packed[i][1] = pack_bf2(v[2], v[3]);
+      if constexpr (FWD) {  // statistics of the bf16-rounded outputs, read back from the packed words (a tile that
+        // is not there -- the first iteration's -- holds zeros: no mask needed)
+        const float r[4] = {bf_lo(packed[i][0]), bf_hi(packed[i][0]), bf_lo(packed[i][1]), bf_hi(packed[i][1])};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          ssum[i][t] += r[t];
+          ssq[i][t] += r[t] * r[t];
+        }
+      }
     }
 #pragma unroll
     for (int q = 0; q < FM / 2; ++q) {  // fragment pair (2q, 2q + 1) -> one 16-B store per lane
@@ -433,8 +372,8 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   }
   if (k > 0) epilogue(accp, opp, tilep, true);
 
-  if constexpr (FWD || BNB) {
-    double* const sacc = BNB ? p.bnb.acc1 : p.stats;
+  if constexpr (FWD) {
+    double* const sacc = p.stats;
     if (sacc != nullptr) {  // per-channel sums of this workgroup -> fp64 slot (once per workgroup)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __syncthreads();
@@ -501,10 +440,8 @@ static bool c64_classic_ok(const ConvShape& s) {
 }
 
 int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, double* stats,
-             hipStream_t st, u64* ts, const BnbArgs* bnb) {
+             hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(conv_c64_ok(s) && (mode == CONV_FWD || mode == CONV_DGRAD), "conv_c64: unsupported shape");
-  const bool fuse = mode == CONV_DGRAD && bnb != nullptr && bnb_on(*bnb);
-  DTC_CHECK_ARG(!fuse || (bnb->x1 && bnb->mean1 && bnb->invstd1 && bnb->acc1), "conv_c64: BN-backward args");
   C64Params p{};
   p.src = src; p.w = w; p.out = out; p.res = res; p.stats = stats;
   p.N = s.N; p.H = s.H; p.W = s.W;
@@ -543,9 +480,7 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   // persistent: one workgroup per CU by default (option c64_wgs), each walking ntiles / grid tiles with the
   // filter resident
   const int grid = std::min(p.ntiles, std::max(1, option_get(OPT_C64_WGS)));
-  const bool in_kernel = fuse && bnb->x2 == nullptr;  // one BN per epilogue (layer1 has no projection)
-  if (in_kernel) p.bnb = *bnb;
-  const int kmode = mode == CONV_FWD ? 0 : in_kernel ? (res == nullptr ? 3 : 4) : (res == nullptr ? 1 : 2);
+  const int kmode = mode == CONV_FWD ? 0 : (res == nullptr ? 1 : 2);
   const bool pf = option_get(OPT_C64_PF) != 0;
 #define DTC_C64(M_)                                                                                \
   if (gen) hipLaunchKernelGGL((conv_c64_kernel<M_, true, true>), dim3(grid), dim3(256), 0, st, p); \
@@ -554,19 +489,10 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   switch (kmode) {
     case 0: DTC_C64(0); break;
     case 1: DTC_C64(1); break;
-    case 2: DTC_C64(2); break;
-    case 3: DTC_C64(3); break;
-    default: DTC_C64(4); break;
+    default: DTC_C64(2); break;
   }
 #undef DTC_C64
   DTC_LAUNCH_CHECK();
-  if (fuse && !in_kernel) {
-    if (bnb->mb)
-      return bn_bwd_reduce_mask(out, bnb->mb, bnb->x1, bnb->mean1, bnb->invstd1, bnb->acc1, bnb->x2, bnb->mean2,
-                                bnb->invstd2, bnb->acc2, M, 64, st);
-    return bn_bwd_reduce(out, bnb->ym, bnb->x1, bnb->mean1, bnb->invstd1, bnb->acc1, bnb->x2, bnb->mean2,
-                         bnb->invstd2, bnb->acc2, out, M, 64, st);
-  }
   return 0;
 }
 

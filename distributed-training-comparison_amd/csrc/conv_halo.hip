@@ -26,7 +26,6 @@
 #include "common.h"
 #include "kernels.h"
 #include "tile_common.h"
-#include "bnb_epi.h"
 
 namespace dtc {
 
@@ -70,7 +69,6 @@ struct HConvParams {
   int tiles_a;  // Cout / BM
   int nchunk;   // Cin / 64 chunks per split
   int xcd_remap;
-  BnbArgs bnb;  // DGRAD: fused BN-backward prologue (bnb.ym null: off)
   FastDiv fd_hb, fd_w2, fd_spx, fd_w;
   u64* ts;
   // output dims (Ho, Wo) and halo row pitch; stride 1: (H, W) and W + 2
@@ -92,116 +90,7 @@ struct HConvParams {
   // the 224x224 model's 224 / 112 / 56 / 28-wide rows (seg 56 or the row, activations past 2 GB)
   int gseg, grs, gtpi, gspr;
   FastDiv fd_gtpi, fd_gspr;
-  // DGRAD without split-K (option halo_stage_epi): the fp32 tile is staged through LDS and written /
-  // combined with its residual, mask bits and BN inputs in 16-B row pieces of 8 channels per lane
-  // (coalesced), instead of 8-B pieces strided by the channel count per lane
-  int staged;
 };
-
-// DGRAD epilogue through LDS: every wave writes its fp32 fragments into a [BN pixels][BM channels] tile
-// (16-B chunk c of pixel row r at c ^ (r mod chunks): the 16 pixels of a fragment column land on distinct
-// bank slots), then each thread owns 8 consecutive channels of a pixel per pass (two 16-B LDS reads) and
-// does the rest with 16-B global accesses: + residual (fp32), round to bf16, and with the fused BN backward
-// (p.bnb) mask by the forward's ReLU bits (one byte = the 8 channels) or y, accumulate sum(dz) and
-// sum(dz * xhat) (+ the second BN's) per channel over its pixels; the per-thread partials are summed per
-// channel in LDS in a fixed order and added to the fp64 slots with one atomic per channel and workgroup.
-template <int BM, int BN, int FM, int FN, typename SlotPix>
-__device__ __forceinline__ void dgrad_staged_epilogue(const HConvParams& p, float* stg, const f32x4 (&acc)[FM][FN],
-                                                      int arow0, int bcol0, int rq, int cl, const SlotPix& slot_pix,
-                                                      int a0, int M) {
-  constexpr int NCH = BM / 4;  // 16-B chunks per staged pixel row
-  constexpr int G8 = BM / 8;   // 8-channel groups per pixel
-  constexpr int PPP = 256 / G8;  // pixel rows per pass
-  constexpr int NPASS = BN / PPP;
-  static_assert(BN % PPP == 0, "staged epilogue: pixels per pass");
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int pl = bcol0 + j * 16 + cl, c = (arow0 + i * 16 + rq) >> 2;
-      *(f32x4*)(stg + pl * BM + ((c ^ (pl & (NCH - 1))) << 2)) = acc[i][j];
-    }
-  __syncthreads();
-  const int t = threadIdx.x, g = t % G8, pr = t / G8;
-  const bool bnb = bnb_on(p.bnb), dual = bnb && p.bnb.x2 != nullptr, has_res = p.res != nullptr;
-  float m1[8], i1[8], m2[8], i2[8], s[8], q1[8], q2[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) m1[k] = i1[k] = m2[k] = i2[k] = s[k] = q1[k] = q2[k] = 0.f;
-  if (bnb) {
-    const int c = a0 + g * 8;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      m1[k] = p.bnb.mean1[c + k];
-      i1[k] = p.bnb.invstd1[c + k];
-      if (dual) {
-        m2[k] = p.bnb.mean2[c + k];
-        i2[k] = p.bnb.invstd2[c + k];
-      }
-    }
-  }
-#pragma unroll
-  for (int ps = 0; ps < NPASS; ++ps) {
-    const int pl = ps * PPP + pr, pix = slot_pix(pl);  // (M: a padded slot of the general geometry)
-    const bool ok = pix < M;
-    const size_t o = (size_t)(ok ? pix : 0) * p.Cout + a0 + g * 8;
-    // every global operand of the pass in flight before the LDS reads are consumed
-    const uint4 rr = has_res && ok ? *(const uint4*)(p.res + o) : uint4{0u, 0u, 0u, 0u};
-    uint4 xv{0u, 0u, 0u, 0u}, xw{0u, 0u, 0u, 0u}, yv{0u, 0u, 0u, 0u};
-    uint32_t mbits = 0u;
-    if (bnb && ok) {
-      xv = *(const uint4*)(p.bnb.x1 + o);
-      if (dual) xw = *(const uint4*)(p.bnb.x2 + o);
-      if (p.bnb.mb) mbits = p.bnb.mb[o >> 3];
-      else yv = *(const uint4*)(p.bnb.ym + o);
-    }
-    const int c0 = 2 * g, sw = pl & (NCH - 1);
-    const f32x4 lo = *(const f32x4*)(stg + pl * BM + ((c0 ^ sw) << 2));
-    const f32x4 hi = *(const f32x4*)(stg + pl * BM + (((c0 + 1) ^ sw) << 2));
-    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    if (has_res) {
-      float r[8];
-      unpack8(rr, r);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] += r[k];
-    }
-    if (bnb) {
-      float x[8], x2[8], y[8];
-      unpack8(xv, x);
-      unpack8(xw, x2);
-      unpack8(yv, y);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const bool keep = p.bnb.mb ? ((mbits >> k) & 1u) != 0u : y[k] > 0.f;
-        v[k] = keep ? round_bf(v[k]) : 0.f;  // exact: masking a bf16 value
-        const float d = ok ? v[k] : 0.f;
-        s[k] += d;
-        q1[k] += d * ((x[k] - m1[k]) * i1[k]);
-        if (dual) q2[k] += d * ((x2[k] - m2[k]) * i2[k]);
-      }
-    }
-    if (ok) *(uint4*)(p.out + o) = pack8(v);
-  }
-  if (!bnb) return;
-  __syncthreads();  // the staged tile is dead: per-thread partials [PPP][BM][3]
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float* r = stg + ((size_t)pr * BM + g * 8 + k) * 3;
-    r[0] = s[k];
-    r[1] = q1[k];
-    r[2] = q2[k];
-  }
-  __syncthreads();
-  if (t < BM) {
-    float ss = 0.f, a1 = 0.f, a2 = 0.f;
-    for (int r = 0; r < PPP; ++r) {
-      const float* e = stg + ((size_t)r * BM + t) * 3;
-      ss += e[0];
-      a1 += e[1];
-      a2 += e[2];
-    }
-    bnb_commit(p.bnb, p.Cout, a0 + t, ss, a1, a2, dual);
-  }
-}
 
 template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP, int WS, int ST = 1, bool SC = false,
           bool GEN = false>
@@ -508,14 +397,6 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
 
   // ---- epilogue: D[row = output channel][col = pixel], 4 consecutive channels per lane
   const int rq = (lane >> 4) * 4, cl = fpx;  // column -> pixel, as in the B fragments
-  constexpr bool kStageFits = MODE == 1 && BN * BM * 4 <= (int)sizeof(smem) && BM * 8 <= 256 * 8;
-  if constexpr (kStageFits) {
-    if (p.slab == nullptr && p.staged) {
-      dgrad_staged_epilogue<BM, BN, FM, FN>(p, (float*)smem, acc, arow0, bcol0, rq, cl, slot_pix, a0, M);
-      stamp_end(p.ts);
-      return;
-    }
-  }
   if (p.slab != nullptr) {  // split-K partial: fp32 [split][pixel][Cout], one 16-B store per fragment
     const size_t plane = (size_t)M * p.Cout;
     if (p.tick == nullptr) {  // the separate splitk_reduce launch sums the slab
@@ -691,61 +572,6 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     if constexpr (SC) {
       __syncthreads();  // the statistics staging area is reused
       epi_fwd(acc2, acc, true, p.out2, p.stats2);
-    }
-  } else if (bnb_on(p.bnb)) {  // DGRAD (+ residual) -> dz = bf16(dx) * [y > 0] and BN sums
-    const bool dual = p.bnb.x2 != nullptr;
-    const bool has_res = p.res != nullptr;
-    float* red = (float*)smem;  // [WC][BM][3]
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int chl = arow0 + i * 16 + rq, ch = a0 + chl;
-      Bnb4 b;
-      bnb4_init(p.bnb, ch, dual, b);
-      // every operand of this channel group's FN fragments in flight at once (one latency, not FN)
-      uint2 rr[FN], yy[FN], xx[FN], x2[FN];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int pix = slot_pix(bcol0 + j * 16 + cl);
-        const size_t o = (size_t)(pix < M ? pix : 0) * p.Cout + ch;
-        rr[j] = has_res ? *(const uint2*)(p.res + o) : uint2{0u, 0u};
-        yy[j] = p.bnb.mb ? bnb_bits_as_y(p.bnb.mb, o) : *(const uint2*)(p.bnb.ym + o);
-        xx[j] = *(const uint2*)(p.bnb.x1 + o);
-        x2[j] = dual ? *(const uint2*)(p.bnb.x2 + o) : uint2{0u, 0u};
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int pix = slot_pix(bcol0 + j * 16 + cl);
-        const bool ok = pix < M;
-        float v[4] = {acc[i][j][0] + bf_lo(rr[j].x), acc[i][j][1] + bf_hi(rr[j].x), acc[i][j][2] + bf_lo(rr[j].y),
-                      acc[i][j][3] + bf_hi(rr[j].y)};
-        bnb4_vals(yy[j], xx[j], x2[j], ok, dual, v, b);
-        if (ok) {
-          uint2 wv;
-          wv.x = pack_bf2(v[0], v[1]);
-          wv.y = pack_bf2(v[2], v[3]);
-          *(uint2*)(p.out + (size_t)pix * p.Cout + ch) = wv;
-        }
-      }
-      bnb4_rowsum(b, dual);
-      if ((lane & 15) == 0) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          red[(wc * BM + chl + t) * 3 + 0] = b.s[t];
-          red[(wc * BM + chl + t) * 3 + 1] = b.q1[t];
-          red[(wc * BM + chl + t) * 3 + 2] = b.q2[t];
-        }
-      }
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < BM) {
-      float s = 0.f, q1 = 0.f, q2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < WC; ++w) {
-        s += red[(w * BM + threadIdx.x) * 3 + 0];
-        q1 += red[(w * BM + threadIdx.x) * 3 + 1];
-        q2 += red[(w * BM + threadIdx.x) * 3 + 2];
-      }
-      bnb_commit(p.bnb, p.Cout, a0 + threadIdx.x, s, q1, q2, dual);
     }
   } else {
 #pragma unroll
@@ -1035,7 +861,7 @@ static int launch_halo_s2(const HConvParams& p, int cfg, dim3 grid, hipStream_t 
 
 static int conv_halo_general(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
                              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
-                             const BnbArgs* bnb, const u16* wsc, u16* out2, double* stats2) {
+                             const u16* wsc, u16* out2, double* stats2) {
   DTC_CHECK_ARG(hp.cfg == 0 || hp.cfg == 2 || hp.cfg == kFirstS2Cfg, "conv_halo: general geometry configuration");
   const HaloCfg& c = kHaloCfgs[hp.cfg];
   const int ST = c.st;
@@ -1070,10 +896,6 @@ static int conv_halo_general(const ConvShape& s, int mode, const HaloPlan& hp, c
   p.fd_spx = make_fastdiv(g.rs * g.seg);
   p.fd_w = make_fastdiv(p.Wo);
   p.ts = ts;
-  // the LDS-staged epilogue (16-B coalesced residual / output; option halo_stage_epi: 1 always, 2 = only the
-  // general geometry, the default -- its long launches are where the per-lane strided residual loads cost)
-  p.staged = option_get(OPT_HALO_STAGE_EPI) != 0;
-  if (bnb != nullptr) p.bnb = *bnb;
   (void)slab; (void)slab_bytes;
   const int64_t ntiles = (int64_t)s.N * g.tpi * p.tiles_a;
   DTC_CHECK_ARG(ntiles < (1ll << 31), "conv_halo: too many tiles");
@@ -1083,11 +905,11 @@ static int conv_halo_general(const ConvShape& s, int mode, const HaloPlan& hp, c
 
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
               const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
-              const BnbArgs* bnb, const u16* wsc, u16* out2, double* stats2, unsigned* tick) {
+              const u16* wsc, u16* out2, double* stats2, unsigned* tick) {
   DTC_CHECK_ARG(hp.cfg >= 0 && hp.cfg < kNumHaloCfgs && (mode == CONV_FWD || mode == CONV_DGRAD),
                 "conv_halo: unsupported configuration");
   const HaloCfg& c = kHaloCfgs[hp.cfg];
-  if (hp.gen) return conv_halo_general(s, mode, hp, src, w, out, res, stats, slab, slab_bytes, st, ts, bnb, wsc, out2, stats2);
+  if (hp.gen) return conv_halo_general(s, mode, hp, src, w, out, res, stats, slab, slab_bytes, st, ts, wsc, out2, stats2);
   DTC_CHECK_ARG(halo_shape_ok(s, c.st) && (c.st == 1 || mode == CONV_FWD), "conv_halo: unsupported shape / pass");
   DTC_CHECK_ARG(wsc == nullptr || (c.st == 2 && out2 != nullptr), "conv_halo: the shortcut fusion is stride-2 FWD");
   HConvParams p{};
@@ -1118,18 +940,16 @@ int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, 
   p.fd_spx = make_fastdiv(p.rows * g.wo);
   p.fd_w = make_fastdiv(g.wo);
   p.ts = ts;
-  p.staged = option_get(OPT_HALO_STAGE_EPI) == 1;
   const dim3 grid(halo_tiles_b(s, g) * p.tiles_a, split);
   // split-K reduced in the kernel (the last workgroup of each tile) when the caller gave arrival counters
   // for the grid (tick: >= DTC_TICKS zeroed words, reserved for this stream) and option splitk_ink is on
   const bool ink = split > 1 && tick != nullptr && option_get(OPT_SPLITK_INK) != 0 && grid.x <= (unsigned)DTC_TICKS;
   p.tick = ink ? tick : nullptr;
-  if (bnb != nullptr && (split <= 1 || ink)) p.bnb = *bnb;  // (separate split-K: the reduction kernel applies it)
   if (c.st == 2) {
     return wsc ? launch_halo_s2<true>(p, hp.cfg, grid, st) : launch_halo_s2<false>(p, hp.cfg, grid, st);
   }
   DTC_TRY(mode == CONV_FWD ? launch_halo<0>(p, hp.cfg, grid, st) : launch_halo<1>(p, hp.cfg, grid, st));
-  if (split > 1 && !ink) return splitk_reduce(slab, split, M, p.Cout, out, res, stats, st, ts, bnb);
+  if (split > 1 && !ink) return splitk_reduce(slab, split, M, p.Cout, out, res, stats, st, ts);
   return 0;
 }
 

@@ -575,36 +575,21 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
 // ---------------------------------------------------------------- split-K reduction (FWD / DGRAD)
 // out[m][n] = bf16( sum_s slab[s][m][n] (+ res[m][n]) ); optional per-channel stats of the
 // bf16-rounded output (same semantics as the non-split epilogue).
-// BNB: DGRAD output feeding a BN backward (bnb_epi.h): out = dz = bf16(...) * [ym > 0] and the sums
-// sum(dz), sum(dz * xhat1) (, sum(dz * xhat2)) into the fp64 slots -- bn_bwd_reduce on the value held.
 // out may alias res: each element is read and then written by the same thread.
-template <bool BNB, bool DUAL>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int splits,
                                                             int M, int Nc, u16* out, const u16* res,
                                                             double* __restrict__ stats, int rows_per_block,
-                                                            u64* ts, const BnbArgs bnb) {
-  __shared__ float red[256 * 24];
+                                                            u64* ts) {
+  __shared__ float red[256 * 16];
   const int tpr = Nc >> 3;           // threads per row (8 channels each)
   const int rpp = 256 / tpr;         // rows per pass
   const int t = threadIdx.x;
   const int g = t % tpr, rr = t / tpr;
   const int m_begin = blockIdx.x * rows_per_block;
   const int m_end = min(M, m_begin + rows_per_block);
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float m1[8], i1[8], m2[8], i2[8];
-  if constexpr (BNB) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      m1[k] = bnb.mean1[g * 8 + k];
-      i1[k] = bnb.invstd1[g * 8 + k];
-      if constexpr (DUAL) {
-        m2[k] = bnb.mean2[g * 8 + k];
-        i2[k] = bnb.invstd2[g * 8 + k];
-      }
-    }
-  }
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const size_t plane = (size_t)M * Nc;
-  // one row's result: + residual (loaded earlier), then the BN-backward / statistics epilogue and the store
+  // one row's result: + residual (loaded earlier), then the statistics and the store
   auto finish = [&](float (&v)[8], size_t o, const uint4& rw) {
     if (res) {
       float rv[8];
@@ -612,31 +597,11 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += rv[k];
     }
-    if constexpr (BNB) {
-      float yv[8], xv[8], xw[8];
-      if (bnb.mb) {  // mask bits: one byte per 8 channels (o % 8 == 0)
-        const uint32_t by = bnb.mb[o >> 3];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) yv[k] = ((by >> k) & 1u) ? 1.f : 0.f;
-      } else {
-        unpack8(*(const uint4*)(bnb.ym + o), yv);
-      }
-      unpack8(*(const uint4*)(bnb.x1 + o), xv);
-      if constexpr (DUAL) unpack8(*(const uint4*)(bnb.x2 + o), xw);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        v[k] = yv[k] > 0.f ? round_bf(v[k]) : 0.f;
-        s[k] += v[k];
-        q[k] += v[k] * ((xv[k] - m1[k]) * i1[k]);
-        if constexpr (DUAL) q2[k] += v[k] * ((xw[k] - m2[k]) * i2[k]);
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        v[k] = round_bf(v[k]);
-        s[k] += v[k];
-        q[k] += v[k] * v[k];
-      }
+    for (int k = 0; k < 8; ++k) {
+      v[k] = round_bf(v[k]);
+      s[k] += v[k];
+      q[k] += v[k] * v[k];
     }
     *(uint4*)(out + o) = pack8(v);
   };
@@ -687,34 +652,23 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
       finish(v, o, rw);
     }
   }
-  if (BNB || stats) {
+  if (stats) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      red[t * 24 + k] = s[k];
-      red[t * 24 + 8 + k] = q[k];
-      red[t * 24 + 16 + k] = q2[k];
+      red[t * 16 + k] = s[k];
+      red[t * 16 + 8 + k] = q[k];
     }
     __syncthreads();
     const size_t slot = (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * Nc;
     for (int c = t; c < Nc; c += 256) {
       const int gg = c >> 3, k = c & 7;
-      float a = 0.f, b = 0.f, e = 0.f;
+      float a = 0.f, b = 0.f;
       for (int r2 = 0; r2 < rpp; ++r2) {
-        a += red[(r2 * tpr + gg) * 24 + k];
-        b += red[(r2 * tpr + gg) * 24 + 8 + k];
-        if constexpr (DUAL) e += red[(r2 * tpr + gg) * 24 + 16 + k];
+        a += red[(r2 * tpr + gg) * 16 + k];
+        b += red[(r2 * tpr + gg) * 16 + 8 + k];
       }
-      if constexpr (BNB) {
-        unsafeAtomicAdd(bnb.acc1 + slot + c, (double)a);
-        unsafeAtomicAdd(bnb.acc1 + slot + Nc + c, (double)b);
-        if constexpr (DUAL) {
-          unsafeAtomicAdd(bnb.acc2 + slot + c, (double)a);
-          unsafeAtomicAdd(bnb.acc2 + slot + Nc + c, (double)e);
-        }
-      } else {
-        unsafeAtomicAdd(stats + slot + c, (double)a);
-        unsafeAtomicAdd(stats + slot + Nc + c, (double)b);
-      }
+      unsafeAtomicAdd(stats + slot + c, (double)a);
+      unsafeAtomicAdd(stats + slot + Nc + c, (double)b);
     }
   }
   stamp_end(ts);
@@ -802,10 +756,7 @@ template <int MODE, int BM, int BN, int WR, int WC, bool SLAB, bool SC = false>
 static int launch_igemm(IGemmParams& p, int tiles_b, int splits, hipStream_t st, int gz = 1) {
   dim3 grid(p.tiles_a * tiles_b, splits, gz);
   p.xcd_remap = option_get(OPT_XCD_REMAP);
-  if (option_get(OPT_IGEMM_STAGES) == 3)
-    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 3, SC>), grid, dim3(256), 0, st, p);
-  else
-    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 2, SC>), grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 2, SC>), grid, dim3(256), 0, st, p);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -886,7 +837,7 @@ int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* sta
     const HaloPlan hp = conv_halo_plan(s, CONV_FWD);
     if (hp.cfg >= 0)
       return conv_halo(s, CONV_FWD, hp, x, w, y, nullptr, stats, slab, slab_bytes, st, ts, nullptr, nullptr, nullptr,
-                       nullptr, tick);
+                       tick);
   }
   IGemmParams p{};
   p.ts = ts;
@@ -940,7 +891,7 @@ int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16
   {
     const HaloPlan hp = conv_halo_plan(s, CONV_FWD);
     if (hp.cfg >= 0)
-      return conv_halo(s, CONV_FWD, hp, x, w, y, nullptr, stats, nullptr, 0, st, ts, nullptr, wsc, ysc, stats_sc);
+      return conv_halo(s, CONV_FWD, hp, x, w, y, nullptr, stats, nullptr, 0, st, ts, wsc, ysc, stats_sc);
   }
   IGemmParams p{};
   p.ts = ts;
@@ -976,22 +927,18 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
   if (bnb != nullptr && !bnb_on(*bnb)) bnb = nullptr;
   DTC_CHECK_ARG(!res_compact || (res && dgrad_class_mode(s) && !conv_c64_ok(s)),
                 "conv_dgrad: a compact residual needs the stride-2 parity-class path");
-  // bit 0: c64, 1: halo, 2: split-K reduce; mask-bit sources (bnb->mb, option bnb_mask) fuse everywhere
-  // (bnb_mask=1) or in the halo and split-K epilogues only (2: the persistent layer1 kernel's strided
-  // epilogue costs more than the separate reduction it saves)
-  const int fz = bnb != nullptr ? (bnb->mb ? (option_get(OPT_BNB_MASK) == 2 ? 6 : 7) : option_get(OPT_BNB_FUSE)) : 0;
-  const HaloPlan hp = conv_c64_ok(s) ? HaloPlan{-1, 0} : conv_halo_plan(s, CONV_DGRAD);
-  const int kind = conv_c64_ok(s) ? 1 : (hp.cfg >= 0 ? 2 : 4);
-  // the epilogue is splitk_reduce's (a halo split-K reduced in the kernel runs the halo epilogue)
-  const bool split_path = kind != 1 && (kind == 4 || (hp.split > 1 && !(tick && option_get(OPT_SPLITK_INK))));
-  if (bnb != nullptr && !(fz & (split_path ? 4 : kind))) {
+  // the BN-backward sums of dx by a reduction pass after the conv (the round-3/4 epilogue fusions measured
+  // slower than the separate pass and were removed in round 5)
+  if (bnb != nullptr) {
     DTC_TRY(conv_dgrad(s, dy, w, dx, res, slab, slab_bytes, st, ts, nullptr, res_compact, tick));
     return bnb_after(bnb, dx, (int64_t)s.N * s.H * s.W, s.C, st);
   }
-  if (kind == 1) return conv_c64(s, CONV_DGRAD, dy, w, dx, res, nullptr, st, ts, bnb);
+  const HaloPlan hp = conv_c64_ok(s) ? HaloPlan{-1, 0} : conv_halo_plan(s, CONV_DGRAD);
+  const int kind = conv_c64_ok(s) ? 1 : (hp.cfg >= 0 ? 2 : 4);
+  if (kind == 1) return conv_c64(s, CONV_DGRAD, dy, w, dx, res, nullptr, st, ts);
   if (kind == 2)
-    return conv_halo(s, CONV_DGRAD, hp, dy, w, dx, res, nullptr, slab, slab_bytes, st, ts, bnb, nullptr, nullptr,
-                     nullptr, tick);
+    return conv_halo(s, CONV_DGRAD, hp, dy, w, dx, res, nullptr, slab, slab_bytes, st, ts, nullptr, nullptr, nullptr,
+                     tick);
   IGemmParams p{};
   p.ts = ts;
   DTC_TRY(fill_common(p, s));
@@ -1030,7 +977,7 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
     if (pl.bn == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 64, 2, 2, true>(p, tiles_b, splits, st)));
     else if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 256, 1, 4, true>(p, tiles_b, splits, st)));
     else DTC_TRY((launch_igemm<MODE_DGRAD, 128, 128, 2, 2, true>(p, tiles_b, splits, st)));
-    return splitk_reduce(slab, splits, p.M, s.C, dx, res, nullptr, st, ts, bnb);
+    return splitk_reduce(slab, splits, p.M, s.C, dx, res, nullptr, st, ts);
   }
   if (pl.bn == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 64, 2, 2, false>(p, tiles_b, 1, st)));
   else if (pl.bm == 64) DTC_TRY((launch_igemm<MODE_DGRAD, 64, 256, 1, 4, false>(p, tiles_b, 1, st)));
@@ -1164,28 +1111,16 @@ int conv_wgrad_batch(const ConvShape& s, int nprob, const u16* const* x, const u
 }
 
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
-                  hipStream_t st, u64* ts, const BnbArgs* bnb) {
+                  hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(Nc % 8 == 0 && Nc <= 2048, "splitk_reduce: channels %d", Nc);
-  const bool fuse = bnb != nullptr && bnb_on(*bnb);
-  DTC_CHECK_ARG(!fuse || (stats == nullptr && bnb->x1 && bnb->mean1 && bnb->invstd1 && bnb->acc1 &&
-                          (!bnb->x2 || (bnb->mean2 && bnb->invstd2 && bnb->acc2))),
-                "splitk_reduce: BN-backward epilogue args");
   const int tpr = Nc / 8;
   const int rpp = 256 / tpr;
   // 256..1024 workgroups of >= 16K outputs where the tensor allows; whole 256-thread passes
   int rows_per_block = std::max({rpp, (M + 1023) / 1024, std::min((16384 + Nc - 1) / Nc, (M + 255) / 256)});
   rows_per_block = ((rows_per_block + rpp - 1) / rpp) * rpp;
   const int blocks = ceil_div(M, rows_per_block);
-  const BnbArgs a = fuse ? *bnb : BnbArgs{};
-  if (!fuse)
-    hipLaunchKernelGGL((splitk_reduce_kernel<false, false>), dim3(blocks), dim3(256), 0, st, slab, splits, M, Nc, out,
-                       res, stats, rows_per_block, ts, a);
-  else if (a.x2 == nullptr)
-    hipLaunchKernelGGL((splitk_reduce_kernel<true, false>), dim3(blocks), dim3(256), 0, st, slab, splits, M, Nc, out,
-                       res, stats, rows_per_block, ts, a);
-  else
-    hipLaunchKernelGGL((splitk_reduce_kernel<true, true>), dim3(blocks), dim3(256), 0, st, slab, splits, M, Nc, out,
-                       res, stats, rows_per_block, ts, a);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, splits, M, Nc, out, res, stats,
+                     rows_per_block, ts);
   DTC_LAUNCH_CHECK();
   return 0;
 }

@@ -13,7 +13,6 @@ namespace dtc {
 // X(ID, name, default): the live options only. Variants that measured negative or neutral were
 // deleted with their code paths (round 4; their numbers are in DESIGN.md).
 #define DTC_OPTION_LIST(X)                                                                                   \
-  X(IGEMM_STAGES, igemm_stages, 2)      /* LDS ring depth of the implicit GEMM (2 or 3) */                  \
   X(XCD_REMAP, xcd_remap, 1)            /* igemm: tiles sharing operands on one XCD */                       \
   X(DGRAD_CLASSES, dgrad_classes, 1)    /* stride-2 dgrad as output-parity classes */                        \
   X(WGRAD_FAST, wgrad_fast, 1)          /* igemm WGRAD fast loader */                                         \
@@ -24,7 +23,6 @@ namespace dtc {
   X(BWD_STREAMS, bwd_streams, 1)        /* weight gradients on a side stream beside the dgrad/BN chain */    \
   X(CONV_C64, conv_c64, 1)              /* persistent 64->64 3x3 conv (conv_c64.hip) for layer1 */           \
   X(BN_FUSED_FIN, bn_fused_fin, 1)      /* BN coefficients folded into the apply kernels */                   \
-  X(BNB_FUSE, bnb_fuse, 0)              /* non-mask backward only: BN reduction in dgrad epilogues */        \
   X(HALO_WSTAGES, halo_wstages, 3)      /* weight ring depth of conv_halo (2 or 3) */                         \
   X(C64_PF, c64_pf, 1)                  /* conv_c64: next (tap, k-step) fragments read ahead */               \
   X(WGRAD_BATCH, wgrad_batch, 4)        /* up to this many 3x3 s1 wgrads of a bucket per launch */            \
@@ -49,16 +47,14 @@ namespace dtc {
   X(HALO_S2, halo_s2, 1)                /* stride-2 3x3 FWD on the column-split halo kernel */                \
   X(WGRAD_S2, wgrad_s2, 1)              /* stride-2 wgrad (+ shortcut) on the halo kernel: 0 off, 1 all, 2 GEN */ \
   X(WGRAD_S2_WGS, wgrad_s2_wgs, 128)    /* stride-2 halo wgrad: target workgroups (split-K slab = wgs x tile) */ \
-  X(WGRAD_KSPLIT, wgrad_ksplit, 2)      /* wgrad_halo: 1 waves split the step's pixels, 2 pipelined fragment reads */ \
+  X(WGRAD_KSPLIT, wgrad_ksplit, 2)      /* wgrad_halo: 2 pipelined fragment reads, 0 compiler-scheduled reads */ \
   X(WGRAD_RING, wgrad_ring, 4)          /* wgrad_halo LDS ring stages: 4, or 3 (room for a main-stream workgroup) */ \
   X(C64_WGS, c64_wgs, 256)              /* conv_c64 (layer1) persistent grid size */                          \
   X(WGRAD_HALO_L1, wgrad_halo_l1, 0)    /* wgrad_halo target for the one-tile (layer1) geometry (0: wgrad_halo) */ \
   X(DGRAD_SCF, dgrad_scf, 1)            /* shortcut dgrad fused into conv1's parity-class dgrad */            \
-  X(BNB_MASK, bnb_mask, 0)              /* BN sums in the producing dgrad's epilogue: 1 all, 2 not c64 */    \
   X(BN_CG, bn_cg, 1)                    /* small BN backward as one launch (bn_bwd_cg) ...                  */ \
   X(BN_CG_ELEMS, bn_cg_elems, 262144)   /* ... for tensors of at most this many elements                    */ \
   X(HEAD_FUSED, head_fused, 1)          /* head backward in one launch: 1 always, 2 at <= 64 images */       \
-  X(HALO_STAGE_EPI, halo_stage_epi, 0)  /* conv_halo DGRAD epilogue staged through LDS: 1 always, 2 GEN only */ \
   X(COMM_ON_SIDE, comm_on_side, 1)      /* bucket all-reduces on the weight-gradient stream (no comm stream) */ \
   X(BUCKET_TAIL, bucket_tail, 1)        /* (plan time) close the open bucket (>= 1 MB) after layer2.0 */      \
   X(WGRAD_GEN, wgrad_gen, 1)            /* wgrad_halo general step geometry (224x224 model) */                \
@@ -166,7 +162,7 @@ int conv_wgrad_batch(const ConvShape& s, int nprob, const u16* const* x, const u
 // Persistent 64-channel 3x3 stride-1 FWD / DGRAD (conv_c64.hip).
 bool conv_c64_ok(const ConvShape& s);
 int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, double* stats,
-             hipStream_t st, u64* ts, const BnbArgs* bnb = nullptr);
+             hipStream_t st, u64* ts);
 struct HaloPlan {
   int cfg, split;
   int gen = 0;  // 1: general tile geometry (rows of seg columns, 64-bit tile bases; conv_halo.hip)
@@ -175,12 +171,10 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode);
 size_t conv_halo_slab_bytes(const ConvShape& s, int mode);  // fp32 split-K slab the plan needs
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
               const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr,
-              const BnbArgs* bnb = nullptr, const u16* wsc = nullptr, u16* out2 = nullptr, double* stats2 = nullptr,
-              unsigned* tick = nullptr);
-// bnb (optional, non-null ym): out = dz = bf16(sum + res) * [ym > 0] and the BN-backward sums of
-// dz into bnb->acc1 (/acc2) -- the work of bn_bwd_reduce on the value the reduction holds.
+              const u16* wsc = nullptr, u16* out2 = nullptr, double* stats2 = nullptr, unsigned* tick = nullptr);
+// out = bf16(sum_s slab[s] (+ res)) (+ the BN statistics of out): the separate split-K reduction
 int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
-                  hipStream_t st, u64* ts = nullptr, const BnbArgs* bnb = nullptr);
+                  hipStream_t st, u64* ts = nullptr);
 // per slot i of ts[n][DTC_PROF_SLOT_U64]: acc[i] += (max end - min start, 1) if stamped; cells reset
 int prof_accumulate(u64* ts, int n, u64* acc, hipStream_t st);
 

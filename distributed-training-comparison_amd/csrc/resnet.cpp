@@ -608,7 +608,7 @@ static bool bn_fused() { return option_get(OPT_BN_FUSED_FIN) != 0; }
 // writes the ReLU mask of its output as bits, and the backward forms dz = dy * bit where it needs it
 // instead of reading the bf16 output (2 B) and storing / re-reading dz (4 B) per element.
 static bool bn_mask_on(const Net& n) {
-  return !n.f32 && option_get(OPT_BN_MASK) != 0 && bn_fused() && option_get(OPT_BNB_FUSE) == 0;
+  return !n.f32 && option_get(OPT_BN_MASK) != 0 && bn_fused();
 }
 
 // SUM all-reduce of one BN's fp64 partial-sum slots ([DTC_STAT_SLOTS][2][C]) on the compute
@@ -1214,23 +1214,13 @@ static int cap_masked(Net& n, const std::string& name, const u16* dy, size_t mas
 }
 
 // BN-backward sums of the BN(s) whose post-ReLU output gradient a dgrad writes, from the mask bits
-static BnbArgs bnb_mask_of(Net& n, size_t mbits, size_t x1, BNL& b1, size_t x2 = 0, BNL* b2 = nullptr) {
-  BnbArgs a = bnb_of(n, 0, x1, b1, x2, b2);
-  a.ym = nullptr;
-  a.mb = n.at<uint8_t>(mbits);
-  return a;
-}
 
 static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdCtx& cx, hipStream_t st) {
   n.prof_next = Net::PROF_BWD0;
   n.ev_next = 0;
-  // option bnb_mask: each BN's backward sums come from the epilogue of the dgrad that produces its
-  // gradient (conv2's dgrad -> bn1; the next block's conv1 dgrad -> bn2 (+ the projection BN); layer1.0's
-  // conv1 dgrad -> the stem BN), read with the forward's mask bits: no separate reduction pass. That dgrad
-  // stores dz = dy * bit; the mask-bit apply below masks again (idempotent). Not with parity captures,
-  // which record the raw dy.
-  const bool bmf = !n.capture && option_get(OPT_BNB_MASK) != 0;
-  bool sums_ready = false;  // this block's bn2 (+ projection BN) sums were accumulated by the later dgrad
+  // (Every BN's backward sums come from a reduction pass of its own -- or the one-launch small-tensor kernel;
+  // the round-3/4 option that accumulated them in the producing dgrad's epilogue measured slower and was
+  // removed in round 5: DESIGN.md.)
   u16* G[6];
   for (int i = 0; i < 6; ++i) G[i] = n.at<u16>(n.G[i]);
   float* slab = n.at<float>(n.SLAB);
@@ -1255,12 +1245,7 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     DTC_TRY(cap_masked(n, cp + ".dz", G[0], b.MOUT, M, b.Cout, st));
     // out = relu(bn2(c2) + shortcut): sums of dz = dy * [out > 0] (and of the projection BN), then
     // dc2 (and dsc); an identity block also needs dz itself as conv1's dgrad residual: in place in G[0]
-    if (sums_ready) {  // the sums are in the slots (bnb_mask). G[0] holds dz, or the raw dy where a
-      // stride-2 class dgrad produced it (sums by a separate mask-bit pass): an identity block's apply
-      // writes dz over it as before (the residual of its conv1 dgrad; idempotent on dz)
-      DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[0], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
-                                b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st, mout, b.proj ? nullptr : G[0]));
-    } else if (bn_cg_on(n, M, b.Cout, b.proj)) {
+    if (bn_cg_on(n, M, b.Cout, b.proj)) {
       DTC_TRY(bn_bwd_one_launch(n, b.b2, G[0], mout, b.proj ? nullptr : G[0], n.at<u16>(b.C2), dc2,
                                 b.proj ? &b.bsc : nullptr, b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st));
     } else {
@@ -1283,17 +1268,11 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     const bool lazy = option_get(OPT_FORK_LAZY) != 0;
     if (!lazy) DTC_TRY(fork_side(n, st, &sd));
     DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd, st, lazy));
-    {
-      const BnbArgs bz = bnb_mask_of(n, b.MA1, b.C1, b.b1);
-      PROF(1, conv_flops(b.c2.s),
-           conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts, bmf ? &bz : nullptr, 0,
-                      n.tick(0)));
-    }
+    PROF(1, conv_flops(b.c2.s),
+         conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts, nullptr, 0, n.tick(0)));
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
     DTC_TRY(cap_masked(n, cp + ".dz1", G[4], b.MA1, M, b.Cout, st));
-    if (bmf) {  // bn1's sums came with conv2's dgrad
-      DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st, ma1));
-    } else if (bn_cg_on(n, M, b.Cout, false)) {
+    if (bn_cg_on(n, M, b.Cout, false)) {
       DTC_TRY(bn_bwd_one_launch(n, b.b1, G[4], ma1, nullptr, n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st));
     } else {
       PROF(3, (double)M * b.Cout * 4.125,
@@ -1314,36 +1293,25 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     } else {
       DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, st, lazy && !b.proj));
     }
-    BnbArgs bp;  // the block input's gradient feeds the previous block's bn2 (+ its projection BN) or the stem BN
-    if (bmf) {
-      if (bi > 0) {
-        BlockL& pb = n.blocks[bi - 1];
-        bp = bnb_mask_of(n, pb.MOUT, pb.C2, pb.b2, pb.proj ? pb.S : 0, pb.proj ? &pb.bsc : nullptr);
-      } else {
-        bp = bnb_mask_of(n, n.MA0, n.C0, n.bn0);
-      }
-    }
-    const BnbArgs* bpp = bmf ? &bp : nullptr;
     if (b.proj) {
       if (!wsc)
         PROF(2, conv_flops(b.sc.s),
              conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts, n.tick_on(sd)));
       if (dscf) {
         PROF(1, conv_flops(b.c1.s) + conv_flops(b.sc.s),
-             conv_dgrad_sc(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], dsc, n.wbf(b.sc.pidx), st, ts, bpp));
+             conv_dgrad_sc(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], dsc, n.wbf(b.sc.pidx), st, ts));
       } else {
         PROF(1, conv_flops(b.sc.s),
              conv_dgrad(sc_dg, dsc, n.wbf(b.sc.pidx), G[5], nullptr, slab, n.slab_bytes, st, ts, nullptr, 0, n.tick(0)));
         PROF(1, conv_flops(b.c1.s),
-             conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts, bpp, sc_cmp ? 1 : 0,
+             conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[5], slab, n.slab_bytes, st, ts, nullptr, sc_cmp ? 1 : 0,
                         n.tick(0)));
       }
       DTC_TRY(cap(n, cp + ".dxs", G[5], st));
     } else {  // residual = dz of this block's output (G[0], written by bn2's apply); dx over it in place
       PROF(1, conv_flops(b.c1.s),
-           conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[0], slab, n.slab_bytes, st, ts, bpp, 0, n.tick(0)));
+           conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[0], slab, n.slab_bytes, st, ts, nullptr, 0, n.tick(0)));
     }
-    sums_ready = bmf;
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
     if (bucket_fires(n, bi)) {
       if (lazy && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
@@ -1358,8 +1326,7 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   // option stem_bn_fuse: the stem BN's apply runs inside the stem weight gradient (dc0 never stored;
   // not with parity captures, which want dc0, or SyncBN, whose sums are all-reduced first)
   if (n.stem_direct && !n.capture && !n.sync && bn_fused() && option_get(OPT_STEM_BN_FUSE) != 0) {
-    if (!sums_ready)
-      PROF(3, (double)M0 * 64 * 4.125,
+    PROF(3, (double)M0 * 64 * 4.125,
            bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
                               n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
     if (option_get(OPT_FORK_LAZY) && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
@@ -1380,14 +1347,10 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     if (n.profiling) DTC_TRY(prof_accumulate(n.prof_ts, Net::PROF_SLOTS, n.prof_acc, st));
     return 0;
   }
-  if (sums_ready) {
-    DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[0], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st, m0));
-  } else {
-    PROF(3, (double)M0 * 64 * 4.125,
-         bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
-                            n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
-    DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[0], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st, m0));
-  }
+  PROF(3, (double)M0 * 64 * 4.125,
+       bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
+                          n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
+  DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[0], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st, m0));
   DTC_TRY(cap_masked(n, "grad.stem.dz", G[0], n.MA0, M0, 64, st));
   DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
   if (option_get(OPT_FORK_LAZY) && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));

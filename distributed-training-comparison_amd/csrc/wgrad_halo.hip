@@ -114,16 +114,15 @@ struct WgStage {
 
 // NS: pipeline stages in the LDS ring (2: wait for the next step's DMA at every step; 4: three
 // steps of DMA in flight, a counted s_waitcnt per step). NR: halo DMA rounds per step.
-// KL: wave layout. 0: 4 waves along the 576 rows x 2 along the 64 output channels, each wave both
-// 32-pixel halves of a step (9 A + 2 B fragment reads per 18 MFMAs). 1 (option wgrad_ksplit): 4 along
-// the rows x 2 along the step's pixels -- each wave all 64 channels of one 32-pixel half (9 A + 4 B
-// reads per 36 MFMAs: 41% fewer LDS reads per MFMA); the two halves' sums are added through LDS after
-// the loop (acc(half 0) + acc(half 1): one fixed order).
+// KL: fragment-read schedule of the wave layout (4 waves along the 576 rows x 2 along the 64 output channels,
+// each wave both 32-pixel halves of a step: 9 A + 2 B fragment reads per 18 MFMAs). 0: compiler-scheduled
+// reads; 2 (option wgrad_ksplit, default): software-pipelined reads. (The pixel-split layouts KL 1 / 3 --
+// each wave all 64 channels of one 32-pixel half, 41% fewer LDS reads per MFMA -- measured neutral in-step
+// and were removed in round 5; numbers in DESIGN.md.)
 template <int NS, int NR, int ST = 1, bool SC = false, bool GEN = false, int KL = 0, bool INK = false>
 __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
-  static_assert(KL == 0 || KL == 2 || !SC, "wgrad_ksplit 1 / 3 (pixel split): no shortcut fusion");
-  constexpr bool PSPLIT = KL == 1 || KL == 3;  // waves split the step's pixels (KL 1 / 3)
-  constexpr bool PIPE = KL >= 2;               // software-pipelined fragment reads (KL 2 / 3)
+  static_assert(KL == 0 || KL == 2, "wgrad_ksplit: 0 or 2");
+  constexpr bool PIPE = KL == 2;  // software-pipelined fragment reads
   typedef WgStage<NR, SC> SG;
   constexpr int PER = NR + 1 + (SC ? 1 : 0);  // LDS-DMA instructions per wave per stage (halo rounds + dy (+ dsc))
   static_assert(!SC || ST == 2, "shortcut fusion: stride 2");
@@ -236,8 +235,8 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     return (tap / 3) * W2 + (ST == 1 ? ts : (ts & 1) * p.hwh + (ts >> 1));
   };
 
-  const int wm = wave >> 1, wn = wave & 1;  // KL = 1: wn is the wave's 32-pixel half of the step
-  constexpr int NJ = PSPLIT ? 4 : 2;             // B fragments (16 output channels each) per wave
+  const int wm = wave >> 1, wn = wave & 1;  // wave row (144 of the 576 GEMM rows) and column half (32 channels)
+  constexpr int NJ = 2;  // B fragments (16 output channels each) per wave
   f32x4 acc[9][NJ];
 #pragma unroll
   for (int i = 0; i < 9; ++i)
@@ -248,7 +247,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   // A = the x halo read transposed at each tap's shift, B = the dy tile read transposed. The step
   // loop is unrolled by NS so each stage base is a constant the ds_read offset field absorbs: the
   // MFMA stream carries no address arithmetic.
-  constexpr int NKS = PSPLIT ? 1 : 2;  // 32-pixel halves a wave computes (KL = 1: its own, at index 0)
+  constexpr int NKS = 2;  // 32-pixel halves (k-steps) a wave computes
   uint32_t aoff[NKS][9][2], boff[NKS][NJ][2];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
@@ -260,19 +259,19 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       const int unit = (cin >> 2) + (lane & 3);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int ra = hm[PSPLIT ? wn : ks][h] + toff;
+        const int ra = hm[ks][h] + toff;
         const int f = wg_uswz(ra);
         aoff[ks][i][h] = (uint32_t)(ra * 128 + ((unit ^ f) << 3));
       }
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int cin = PSPLIT ? j * 16 : wn * 32 + j * 16;
+      const int cin = wn * 32 + j * 16;
       const int li = lane & 15, q = li >> 2, pp = li & 3, g = lane >> 4;
       const int unit = (cin >> 2) + pp;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int kr = wg_pixel(PSPLIT ? wn : ks, g, h, q);
+        const int kr = wg_pixel(ks, g, h, q);
         const int f = wg_uswz(kr);
         boff[ks][j][h] = (uint32_t)(SG::HALO_BYTES + kr * 128 + ((unit ^ f) << 3));
       }
@@ -297,23 +296,6 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
   };
   auto compute = [&](const char* sb) {
-    if constexpr (PIPE && PSPLIT) {  // KL = 3: the pixel-split layout's 4 B + 9 A fragments, A through the ring
-      bf16x8 bq[4], ar[3];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bq[j] = tr8(sb, boff[0][j][0], boff[0][j][1]);
-      ar[0] = tr8(sb, aoff[0][0][0], aoff[0][0][1]);
-      ar[1] = tr8(sb, aoff[0][1][0], aoff[0][1][1]);
-#pragma unroll
-      for (int f = 0; f < 9; ++f) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (f + 2 < 9) ar[(f + 2) % 3] = tr8(sb, aoff[0][f + 2][0], aoff[0][f + 2][1]);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[f % 3], bq[j], acc[f][j], 0, 0, 0);
-      }
-      return;
-    }
     if constexpr (PIPE) {
       // software-pipelined fragment reads (option wgrad_ksplit=2): both k-steps' B fragments first, then the 18
       // A fragments through a three-deep register ring -- fragment f + 2 is read before the MFMAs of f, and
@@ -401,39 +383,6 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   float* const slab = p.direct ? uniform_ptr(z == 0 ? p.dws[0] : z == 1 ? p.dws[1] : z == 2 ? p.dws[2] : p.dws[3])
                                : p.slab + z * p.slab_stride + (size_t)split * p.K * RSC;
   const float osc = p.direct ? p.scale : 1.f;
-  if constexpr (PSPLIT) {
-    // the two pixel halves' sums: each wave finalises two of its four column fragments (half 0 the
-    // first two, half 1 the last two), receiving the other half's partials through LDS in two rounds
-    // of fragments (rows i < 5, then i >= 5: 10 / 8 KB per wave). The ring is free after a barrier.
-    __syncthreads();
-    f32x4* const xb = (f32x4*)smem;
-    // (fragment rows as template constants: a runtime row index would put acc in scratch memory)
-    auto xround = [&](auto i0c, auto i1c) {
-      constexpr int i0 = decltype(i0c)::value, i1 = decltype(i1c)::value;
-#pragma unroll
-      for (int i = i0; i < i1; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)  // send the fragments the partner wave finalises
-          xb[((wave * 10 + (i - i0) * 2 + jj) << 6) + lane] = wn ? acc[i][jj] : acc[i][2 + jj];
-      __syncthreads();
-#pragma unroll
-      for (int i = i0; i < i1; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const f32x4 o = xb[(((wave ^ 1) * 10 + (i - i0) * 2 + jj) << 6) + lane];
-          const f32x4 v = wn ? o + acc[i][2 + jj] : acc[i][jj] + o;  // half 0 + half 1
-          const int row = wm * 144 + i * 16 + 4 * (lane >> 4);
-          const int rsc = (row >> 6) * p.C + c0 + (row & 63);
-          const int kout = k0 + ((wn ? 2 : 0) + jj) * 16 + (lane & 15);
-          *(f32x4*)(slab + (size_t)kout * RSC + rsc) = v * osc;
-        }
-      __syncthreads();
-    };
-    xround(std::integral_constant<int, 0>{}, std::integral_constant<int, 5>{});
-    xround(std::integral_constant<int, 5>{}, std::integral_constant<int, 9>{});
-    stamp_end(p.ts);
-    return;
-  }
   if constexpr (INK) {  // (a template flag: the plain instances keep their register allocation)
     // In-kernel split-K (the hand-off of conv_halo.hip: MI355X_MICROARCH.md "Valid forms" row 1): sc1 partial
     // stores drained by every wave, one agent-scope add per workgroup; the last arriver reads all splits' sc1
@@ -685,10 +634,8 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   const bool ring3 = kl == 2 && option_get(OPT_WGRAD_RING) == 3;
 #define DTC_WGH(NR_, GEN_)                                                                                    \
   if (ring3) hipLaunchKernelGGL((wgrad_halo_kernel<3, NR_, 1, false, GEN_, 2>), grid, dim3(512), 0, st, p);  \
-  else if (kl == 1) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 1>), grid, dim3(512), 0, st, p); \
   else if (kl == 2 && ink) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 2, true>), grid, dim3(512), 0, st, p); \
   else if (kl == 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 2>), grid, dim3(512), 0, st, p); \
-  else if (kl == 3) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 3>), grid, dim3(512), 0, st, p); \
   else hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 0>), grid, dim3(512), 0, st, p)
   if (g.gen) {  // general geometry
     if (nr <= 2) { DTC_WGH(2, true); }

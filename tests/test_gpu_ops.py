@@ -479,12 +479,12 @@ def test_amp_check_finite_positions(dtc, cuda, n):
     (2, 6, 96, 64, 64),     # 32-pixel segments
     (1, 5, 40, 64, 64),     # one 40-pixel row per step (24 padded slots)
 ])
-@pytest.mark.parametrize("ksplit", [0, 1, 2, 3])
+@pytest.mark.parametrize("ksplit", [0, 2])
 def test_conv_wgrad_halo(dtc, cuda, case, ksplit):
     """Halo-tiled 3x3 weight gradient == generic loader == oracle (fp32 sums of exact products); the rows
     wider than 64 pixels or not dividing 64 run the general-geometry kernels (per-step 64-bit bases, zero-dy
-    padded slots), which must match too. ksplit: option wgrad_ksplit (the waves split each step's pixels,
-    the two halves' sums added after the loop)."""
+    padded slots), which must match too. ksplit: option wgrad_ksplit (0 compiler-scheduled fragment reads,
+    2 software-pipelined: the same MFMAs in the same order)."""
     N, H, W, C, K = case
     g = np.random.default_rng(7)
     x = _rand_bf16((N, H, W, C), g)
@@ -512,7 +512,7 @@ def test_conv_wgrad_halo(dtc, cuda, case, ksplit):
     (2, 8, 224, 64, 64, 4),    # general geometry (56-pixel row segments), the 224x224 layer1 batch
     (2, 14, 28, 128, 128, 3),  # general geometry, two 28-pixel rows per step
 ])
-@pytest.mark.parametrize("ksplit", [0, 1, 2, 3])
+@pytest.mark.parametrize("ksplit", [0, 2])
 def test_conv_wgrad_batch(dtc, cuda, case, ksplit):
     """dtc_conv2d_wgrad_batch: n independent weight gradients in one halo launch (blockIdx.z =
     problem, 1/n of the splits each) + one reduce launch == the oracle per problem, and == the
@@ -617,7 +617,7 @@ def test_conv_halo_splitk_in_kernel_matches_reduce_launch(dtc, cuda, case, split
     (sc1 write-through stores, an agent-scope arrival counter, sc1 loads) instead of a splitk_reduce launch.
     Same sum order (0 + slab[0] + slab[1] + ...), so the bf16 outputs are bit-identical to the separate
     reduction -- forward (+ BN statistics: the same values, their fp32 partial sums grouped per workgroup
-    instead of per reduce block), data gradient (+ residual) and the mask-bit BN-backward epilogue -- on every one of 8 repeated
+    instead of per reduce block), data gradient (+ residual) and with the BN-backward pass after it -- on every one of 8 repeated
     launches (the hand-off under uneven arrival; the counters must come back to zero each time). B=256 layer4
     (automatic split 2), layer3 forced to 2 / 4 splits, a ragged batch."""
     N, H, W, C, K = case
@@ -642,7 +642,6 @@ def test_conv_halo_splitk_in_kernel_matches_reduce_launch(dtc, cuda, case, split
 
     prev = lib.dtc_get_option(b"splitk_ink")
     dtc._native.call("dtc_set_option", b"halo_split", split)
-    dtc._native.call("dtc_set_option", b"bnb_fuse", 6)  # the BN-backward sums in the (reduce / halo) epilogue
     try:
         dtc._native.call("dtc_set_option", b"splitk_ink", 0)
         ref = run()
@@ -657,7 +656,6 @@ def test_conv_halo_splitk_in_kernel_matches_reduce_launch(dtc, cuda, case, split
     finally:
         dtc._native.call("dtc_set_option", b"splitk_ink", prev)
         dtc._native.call("dtc_set_option", b"halo_split", 0)
-        dtc._native.call("dtc_set_option", b"bnb_fuse", 0)
     yk = ref[0].float().cpu().numpy()
     assert rel_err(yk, O.conv2d_fwd(x.float().cpu().numpy(), w.float().cpu().numpy(), 1, 1)) < 1e-2
 

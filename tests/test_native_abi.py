@@ -142,15 +142,19 @@ _OPTION_DEFAULTS = {
     "bn_red_elems": 16384, "bn_red_blocks": 256, "bn_fa_blocks": 1024,
     "sc_compact": 1, "stem_prologue": 1, "dgrad_class_order": 1, "wgrad_direct": 1, "wgrad_xcd": 1,
     # round 3
-    "halo_s2": 1, "wgrad_s2": 1, "dgrad_scf": 1, "bnb_mask": 0, "bucket_tail": 1, "halo_stage_epi": 0, "wgrad_gen": 1,
+    "halo_s2": 1, "wgrad_s2": 1, "dgrad_scf": 1, "bucket_tail": 1, "wgrad_gen": 1,
     "halo_gen": 1, "bn_red_unroll": 4, "c64_gen": 1, "graphs": 4, "head_fused": 1,
     # round 4
     "bn_cg": 1, "bn_cg_elems": 262144, "wgrad_s2_wgs": 128, "comm_on_side": 1, "wgrad_ksplit": 2, "wgrad_ring": 4, "c64_wgs": 256, "wgrad_halo_l1": 0,
+    # round 5
+    "splitk_ink": 1, "comm_prio": 0, "comm_tail_inline": 1, "wgrad_ink": 1, "wgrad_ink_max": 8, "dgrad_s2h": 1,
 }
-# measured-negative variants deleted in round 4 with their code paths (DESIGN.md keeps their numbers)
+# measured-negative variants deleted in rounds 4 and 5 with their code paths (DESIGN.md keeps their numbers)
 _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", "wgrad_pmap", "wgrad_prio",
                     "halo_nhb2", "wgrad_kernel", "head_direct", "halo_nosplit", "graph_ev", "wgrad_tail",
-                    "wgrad_stages", "wgrad_pf", "wgrad_diag")
+                    "wgrad_stages", "wgrad_pf", "wgrad_diag",
+                    # round 5
+                    "bnb_mask", "bnb_fuse", "halo_stage_epi", "igemm_stages")
 
 
 def test_options_registered_with_defaults(dtc):

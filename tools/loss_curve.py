@@ -61,6 +61,7 @@ def main():
     res = {}
     for var in [""] + [v for v in args.variants.split(";") if v]:
         kv = [x.split("=") for x in var.split(",") if x]
+        defaults = {k: int(dtc._native.lib.dtc_get_option(k.encode())) for k, _ in kv}
         for k, v in kv:
             dtc._native.call("dtc_set_option", k.encode(), int(v))
         for seed in [int(s) for s in args.seeds.split(",")]:
@@ -72,7 +73,7 @@ def main():
                   "rel", round((cur.mean() - ref.mean()) / ref.mean(), 4), flush=True)
             print("   win20 ours", np.round(w(cur), 3).tolist(), flush=True)
         for k, _ in kv:  # restore defaults
-            dtc._native.call("dtc_set_option", k.encode(), {"igemm_stages": 2}.get(k, 1))
+            dtc._native.call("dtc_set_option", k.encode(), defaults[k])
     for u in [int(v) for v in args.ulp.split(",") if v]:
         cur = run(dtc, dev, lc, 42, u)
         res[f"ulp{u}"] = cur.tolist()
