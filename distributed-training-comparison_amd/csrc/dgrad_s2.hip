@@ -305,7 +305,13 @@ static int s2d_bn(const ConvShape& s) {
   return 0;
 }
 
-bool dgrad_s2_halo_ok(const ConvShape& s) { return option_get(OPT_DGRAD_S2H) != 0 && s2d_bn(s) > 0; }
+// option dgrad_s2h: 1 (auto) where it measured faster than the parity-class igemm -- output-gradient depth
+// K <= 256 (conv_bench r05g, batch 256: layer2.0 28.2 -> 17.9 us, layer3.0 23.2 -> 20.5); layer4's K = 512 runs
+// 4608-deep reductions on 256 workgroups with no split (27.0 us against the classes' 22.6); 2 every geometry
+bool dgrad_s2_halo_ok(const ConvShape& s) {
+  const int o = option_get(OPT_DGRAD_S2H);
+  return o != 0 && (o >= 2 || s.K <= 256) && s2d_bn(s) > 0;
+}
 
 int conv_dgrad_s2_halo(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* dsc, const u16* wsc,
                        hipStream_t st, u64* ts) {

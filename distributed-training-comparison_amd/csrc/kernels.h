@@ -66,7 +66,7 @@ namespace dtc {
   X(COMM_TAIL_INLINE, comm_tail_inline, 1) /* the last bucket's all-reduce on the compute stream (no fork / join) */ \
   X(WGRAD_INK, wgrad_ink, 1)            /* wgrad split-K summed by the last workgroup per tile: 1 stride-2, 2 all */ \
   X(WGRAD_INK_MAX, wgrad_ink_max, 8)    /* ... for launches of at most this many splits (else a reduce launch) */ \
-  X(DGRAD_S2H, dgrad_s2h, 1)            /* stride-2 3x3 dgrad (+ fused shortcut) as a halo sub-pixel conv (dgrad_s2.hip) */
+  X(DGRAD_S2H, dgrad_s2h, 1)            /* stride-2 3x3 dgrad (+ shortcut) as a halo sub-pixel conv: 1 K <= 256, 2 all */
 
 enum {
 #define DTC_OPT_ENUM(id, name, def) OPT_##id,

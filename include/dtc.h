@@ -37,20 +37,22 @@ const char* dtc_last_error(void);
 /* Diagnostics: on SIGSEGV/SIGBUS/SIGFPE/SIGABRT print the faulting native thread (tid, name) and its
  * frames to stderr, then chain to the previous handler (e.g. Python's faulthandler). Idempotent. */
 int dtc_install_crash_handler(void);
-/* Process-wide kernel tuning knobs (atomic; for benchmarking): "igemm_stages" (2 or 3 LDS stages
- * in the conv main loop, default 2), "xcd_remap" (XCD-aware tile order, default 1),
- * "dgrad_classes" (stride-2 data-gradient as 4 parity-class GEMMs, default 1), "wgrad_fast" (buffer-
- * offset weight-gradient loader for row-aligned pixel steps, default 1), "graphs" (the executor
- * captures its forward / backward into hipGraphs on first use and replays them, default 1; any
- * option change invalidates captured graphs). */
+/* Process-wide kernel tuning knobs (atomic; for benchmarking and A/B measurement). The full list, with
+ * defaults and one line each, is the DTC_OPTIONS table in csrc/kernels.h; unknown names return DTC_EINVAL.
+ * Examples: "graphs" (0 eager, 1 forward + backward hipGraphs, 2 forward only, 3 backward only,
+ * default 4 = auto: the executor captures on first use and replays; any option change invalidates
+ * captured graphs), "splitk_ink" (split-K slabs summed in-kernel by the last workgroup of each tile,
+ * default 1), "dgrad_s2h" (stride-2 data gradient as a halo sub-pixel conv, default 1), "stem_direct"
+ * (plan time: direct 3x3 stem conv, default 1; 0 = im2col + GEMM). */
 int dtc_set_option(const char* name, int value);
 int dtc_get_option(const char* name);
 
 /* ------------------------------------------------------------------ convolution
  * Replaces nn.Conv2d(bias=False) forward / backward (reference src/ddp/net.py:18-24,
  * net.py:29-35, net.py:91) as launched by autocast (cuDNN in the reference).
- * Requirements: c % 64 == 0, k % 64 == 0, stride in {1, 2} (the stem uses
- * dtc_stem_im2col + a 1x1 "conv" over 64 im2col channels). */
+ * Requirements: c % 64 == 0, k % 64 == 0, stride in {1, 2} (the 3-channel stem has its own direct
+ * kernels, dtc_stem_*; dtc_stem_im2col + a 1x1 "conv" over 64 im2col channels is kept as the
+ * stem_direct=0 variant). */
 typedef struct {
   int n, h, w, c; /* input  [n][h][w][c]  bf16 */
   int k, r, s;    /* filter [k][r][s][c]  bf16 */

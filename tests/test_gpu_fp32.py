@@ -63,6 +63,41 @@ def test_fp32_end_to_end_matches_oracle(dtc, cuda):
         assert e < 1e-5, (k, e)
 
 
+def test_fp32_data_parallel_step_matches_oracle(dtc, cuda):
+    """DataParallel (reference src/dp/trainer.py:27, torch nn.DataParallel semantics) with two replicas on
+    cuda:0 (device_ids=[0, 0]) against the fp32 oracle: each replica runs train-mode BN over its own
+    half of the batch (the oracle's forward on that half), the gathered logits are the two halves'
+    oracle logits, the mean loss over the whole batch gives gradient = mean of the two half-batch
+    oracle gradients, and the running statistics are replica 0's update (the module is replica 0;
+    replica 1's buffers are discarded, as torch's replicate does). Same tolerances as the
+    single-replica fp32 end-to-end test, at that test's batch of 8 per replica (at 4 images per BN the
+    summation noise amplified through the backward reached 5.5e-3 on layer1.1.bn2.weight, r05g)."""
+    B = 8
+    model, sd, x, y = _setup(dtc, cuda, 2 * B, seed=6)
+    model.precision = "fp32"
+    dp = dtc.DataParallel(model, device_ids=[0, 0])
+    crit = dtc.CrossEntropyLoss()
+    dp.zero_grad()
+    logits = dp(torch.from_numpy(x).to(cuda))
+    loss = crit(logits, torch.from_numpy(y).to(cuda))
+    loss.backward()
+    torch.cuda.synchronize()
+    params, bufs = _split_state(sd)
+    halves = [R.forward_backward(params, bufs, x[h * B:(h + 1) * B], y[h * B:(h + 1) * B], bf16_mode=False,
+                                 train=True) for h in range(2)]
+    assert rel_err(_np(logits), np.concatenate([r["logits"] for r in halves])) < 1e-5
+    ref_loss = 0.5 * (halves[0]["loss"] + halves[1]["loss"])
+    assert abs(float(loss) - ref_loss) < 1e-5 * max(1.0, abs(ref_loss))
+    for k, p in model.named_parameters():
+        e = rel_err(_np(p.grad), 0.5 * (halves[0]["grads"][k] + halves[1]["grads"][k]))
+        assert e < 5e-3, (k, e)
+    sd2 = model.state_dict()
+    for k, v in halves[0]["buffers"].items():
+        e = rel_err(sd2[k].cpu().numpy(), v)
+        assert e < 1e-5, (k, e)
+    assert int(sd2["bn1.num_batches_tracked"]) == 1
+
+
 def test_autocast_selects_executor_precision(dtc, cuda):
     """torch semantics at the boundary: inside dtc.autocast() the bf16 executor, outside it fp32
     (what the reference's trainer does with and without --amp); `precision` forces one."""

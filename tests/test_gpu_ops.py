@@ -928,7 +928,7 @@ def test_conv_dgrad_stride2_halo_subpixel(dtc, cuda, case, sc):
 
     prev = lib.dtc_get_option(b"dgrad_s2h")
     try:
-        lib.dtc_set_option(b"dgrad_s2h", 1)
+        lib.dtc_set_option(b"dgrad_s2h", 2)  # every geometry (the default 1 leaves K = 512 to the classes)
         dx = run().float()
         lib.dtc_set_option(b"dgrad_s2h", 0)
         dx_gemm = run().float()

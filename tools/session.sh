@@ -1,1 +1,1 @@
-tools/gpu_run.sh r05g "tests:stride2 or dgrad_sc or dgrad_s2" && PY_ARGS="--layers l2.0.c1,l3.0.c1,l4.0.c1 --passes dgrad --variants 'dgrad_s2h=1;dgrad_s2h=0'" tools/gpu_run.sh r05g py:tools/conv_bench.py && tools/gpu_run.sh r05g bench
+tools/gpu_run.sh r05h tests bench && timeout -k 10 300 tools/prof_run.sh r05h_ser --opt bwd_streams=0 --opt graphs=0 && timeout -k 10 300 tools/prof_run.sh r05h_b256
