@@ -58,6 +58,7 @@ struct HConvParams {
   // tile's partials in split order and runs the normal (non-split) epilogue. Null: the separate
   // splitk_reduce launch does it.
   unsigned* tick;
+  u64* phase;      // phase probe buffer (DTC_PHASES builds; null otherwise)
   int N, H, W, Cin, Cout, C;
   uint32_t src_bytes;
   int rows;     // output rows per image slice
@@ -111,6 +112,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   char* const scbase = wbase + WS * WBYTES;
 
   stamp_start(p.ts);
+  phase_mark(p.phase, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int bid = blockIdx.x;
   if (p.xcd_remap && gridDim.x >= 16) {  // consecutive tile ids (same pixel tile) share an XCD's L2
@@ -360,6 +362,8 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        if (step == 0) phase_mark(p.phase, 1);
+        if (c == 1 && tap == 0) phase_mark(p.phase, 2);
         if constexpr (WS == 3) {  // weights of step + 2 into the slot step - 1 used
           if (tap + 2 <= 8) stage_w(wbase + ((tap + 2) % 3) * WBYTES, c0 + c, tap + 2);
           else if (c + 1 < p.nchunk) stage_w(wbase + ((tap + 2) % 3) * WBYTES, c0 + c + 1, tap + 2 - 9);
@@ -392,6 +396,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  phase_mark(p.phase, 3);
   __builtin_amdgcn_s_barrier();  // LDS reads done before the epilogue reuses smem
   asm volatile("" ::: "memory");
 
@@ -409,6 +414,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
         for (int i = 0; i < FM; ++i)
           *(f32x4*)(slab + (size_t)pix * p.Cout + a0 + arow0 + i * 16 + rq) = acc[i][j];
       }
+      phase_mark(p.phase, 4);
       stamp_end(p.ts);
       return;
     }
@@ -447,6 +453,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     const unsigned last = *(volatile unsigned*)flag;
     __syncthreads();  // the flag word is read by every wave before the epilogue reuses smem
     if (!last) {
+      phase_mark(p.phase, 4);
       stamp_end(p.ts);
       return;
     }
@@ -610,6 +617,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
       }
     }
   }
+  phase_mark(p.phase, 4);
   stamp_end(p.ts);
 }
 
@@ -903,6 +911,14 @@ static int conv_halo_general(const ConvShape& s, int mode, const HaloPlan& hp, c
   return mode == CONV_FWD ? launch_halo_gen<0>(p, hp.cfg, grid, st) : launch_halo_gen<1>(p, hp.cfg, grid, st);
 }
 
+#ifdef DTC_PHASES
+static u64* g_phase = nullptr;
+extern "C" int dtc_probe_phase_buffer(void* buf) {  // diagnostic builds only (tools/phase_probe.py)
+  g_phase = (u64*)buf;
+  return 0;
+}
+#endif
+
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
               const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
               const u16* wsc, u16* out2, double* stats2, unsigned* tick) {
@@ -940,6 +956,9 @@ int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, 
   p.fd_spx = make_fastdiv(p.rows * g.wo);
   p.fd_w = make_fastdiv(g.wo);
   p.ts = ts;
+#ifdef DTC_PHASES
+  p.phase = g_phase;
+#endif
   const dim3 grid(halo_tiles_b(s, g) * p.tiles_a, split);
   // split-K reduced in the kernel (the last workgroup of each tile) when the caller gave arrival counters
   // for the grid (tick: >= DTC_TICKS zeroed words, reserved for this stream) and option splitk_ink is on

@@ -49,6 +49,23 @@ __device__ __forceinline__ void stamp_end(u64* ts) {
   }
 }
 
+// Phase probe (diagnostic builds only: `make phases` -> libdtc_amd_phases.so, -DDTC_PHASES): lane 0 of each
+// workgroup writes s_memrealtime (100 MHz, chip-wide) at marked points of a kernel into buf[wg][8]
+// (plain vector stores); tools/phase_probe.py reads them. In the product build the marks are empty.
+#ifdef DTC_PHASES
+constexpr unsigned DTC_PHASE_WGS = 16384;
+__device__ __forceinline__ void phase_mark(u64* buf, int k) {
+  // wave 0 only, as a wave-uniform branch (a lane-divergent one here would make the compiler treat the
+  // buffer descriptors of the surrounding LDS-DMA asm as divergent); its 64 lanes store the same word
+  if (buf != nullptr && __builtin_amdgcn_readfirstlane(threadIdx.x) == 0) {
+    const unsigned lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (lin < DTC_PHASE_WGS) buf[lin * 8 + k] = (u64)__builtin_amdgcn_s_memrealtime();
+  }
+}
+#else
+__device__ __forceinline__ void phase_mark(u64*, int) {}
+#endif
+
 __device__ __forceinline__ int rowswz(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int trswz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
 

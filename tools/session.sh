@@ -1,1 +1,1 @@
-tools/gpu_run.sh r05h tests bench && timeout -k 10 300 tools/prof_run.sh r05h_ser --opt bwd_streams=0 --opt graphs=0 && timeout -k 10 300 tools/prof_run.sh r05h_b256
+PY_ARGS="--layers l2,l3,l4 --passes fwd,dgrad" tools/gpu_run.sh r05j py:tools/phase_probe.py && tools/gpu_run.sh r05j "tests:data_parallel_step" tests
