@@ -64,7 +64,7 @@ namespace dtc {
   X(SPLITK_INK, splitk_ink, 1)          /* conv split-K summed by the last workgroup per tile (no reduce launch) */ \
   X(COMM_PRIO, comm_prio, 0)            /* (communicator creation) its own stream: 0 normal, 1 most urgent */ \
   X(COMM_TAIL_INLINE, comm_tail_inline, 1) /* the last bucket's all-reduce on the compute stream (no fork / join) */ \
-  X(WGRAD_INK, wgrad_ink, 1)            /* wgrad split-K summed by the last workgroup per tile: 1 stride-2, 2 all */ \
+  X(WGRAD_INK, wgrad_ink, 0)            /* wgrad split-K summed by the last workgroup per tile: 1 stride-2, 2 all */ \
   X(WGRAD_INK_MAX, wgrad_ink_max, 8)    /* ... for launches of at most this many splits (else a reduce launch) */ \
   X(DGRAD_S2H, dgrad_s2h, 1)            /* stride-2 3x3 dgrad (+ shortcut) as a halo sub-pixel conv: 1 K <= 256, 2 all */
 

@@ -569,9 +569,11 @@ int wgrad_halo_splits(const ConvShape& s, int nprob) {
 
 // option wgrad_ink: split-K summed in the kernel by the last workgroup of each tile, for launches of at most
 // wgrad_ink_max splits (the last arriver reads every split's partial tile: its latency grows with the split count)
-// (option wgrad_ink: 0 off; 1 the stride-2 (+ shortcut) launches only -- each saves two reduce launches, while
-// the stride-1 batches measured slower in-step (the last arriver reads the tile's whole slab alone: 137.4k vs
-// 135.9k img/s, r05f); 2 every launch)
+// (option wgrad_ink: 0 off (default); 1 the stride-2 (+ shortcut) launches only; 2 every launch. A wgrad tile is
+// 64 x 576 fp32 (147 KB per split), so the last arriver alone reads splits x 147 KB after every other split has
+// finished: the one stride-2 launch it applies to at batch 256 (layer4.0, 4 splits) took 54.4 us against 36.8 for
+// its plain twin + 2 reduce launches of ~6 us (serialized trace r05h); in-step 140.8k vs 140.5k img/s without it
+// (4 rounds, r05i: noise), and every launch 135.9k vs 137.4k (r05f))
 static bool wgrad_ink_ok(int used, unsigned* tick, unsigned ncount, bool s2) {
   const int o = option_get(OPT_WGRAD_INK);
   return tick != nullptr && used > 1 && (o == 2 || (o == 1 && s2)) && used <= option_get(OPT_WGRAD_INK_MAX) &&

@@ -67,35 +67,48 @@ def test_fp32_data_parallel_step_matches_oracle(dtc, cuda):
     """DataParallel (reference src/dp/trainer.py:27, torch nn.DataParallel semantics) with two replicas on
     cuda:0 (device_ids=[0, 0]) against the fp32 oracle: each replica runs train-mode BN over its own
     half of the batch (the oracle's forward on that half), the gathered logits are the two halves'
-    oracle logits, the mean loss over the whole batch gives gradient = mean of the two half-batch
-    oracle gradients, and the running statistics are replica 0's update (the module is replica 0;
-    replica 1's buffers are discarded, as torch's replicate does). Same tolerances as the
-    single-replica fp32 end-to-end test, at that test's batch of 8 per replica; the parameter gradients'
-    error is measured against the halves' own gradient norms (5e-3). A DP that normalised over the whole
-    16-image batch instead of per replica fails the 1e-5 logits check."""
+    oracle logits (1e-5), the mean loss over the whole batch gives gradient = mean of the two half-batch
+    oracle gradients, and the running statistics are replica 0's update (1e-5; the module is replica 0,
+    replica 1's buffers are discarded, as torch's replicate does). A DP that normalised over the whole
+    16-image batch instead of per replica fails the logits check.
+    Gradient bound: fp32 summation order alone moves some 8-image gradients by up to ~1e-2 of their norm
+    against the fp64 oracle (a BN bias gradient is a sum of dz that largely cancels; layer3.1.bn2.bias
+    0.9e-2, r05j), so each parameter's DP error is held to twice the error of the same executor run
+    single-replica on each half (its own noise floor on these inputs), plus 1e-4."""
     B = 8
     model, sd, x, y = _setup(dtc, cuda, 2 * B, seed=6)
     model.precision = "fp32"
-    dp = dtc.DataParallel(model, device_ids=[0, 0])
     crit = dtc.CrossEntropyLoss()
+    params, bufs = _split_state(sd)
+    halves = [R.forward_backward(params, bufs, x[h * B:(h + 1) * B], y[h * B:(h + 1) * B], bf16_mode=False,
+                                 train=True) for h in range(2)]
+    single = []  # the executor's own gradients on each half (noise floor)
+    for h in range(2):
+        torch.manual_seed(42)
+        m1 = dtc.ResNet18().to(cuda)
+        m1.precision = "fp32"
+        crit(m1(torch.from_numpy(x[h * B:(h + 1) * B]).to(cuda)), torch.from_numpy(y[h * B:(h + 1) * B]).to(cuda)).backward()
+        single.append({k: _np(p.grad) for k, p in m1.named_parameters()})
+        del m1
+    dp = dtc.DataParallel(model, device_ids=[0, 0])
     dp.zero_grad()
     logits = dp(torch.from_numpy(x).to(cuda))
     loss = crit(logits, torch.from_numpy(y).to(cuda))
     loss.backward()
     torch.cuda.synchronize()
-    params, bufs = _split_state(sd)
-    halves = [R.forward_backward(params, bufs, x[h * B:(h + 1) * B], y[h * B:(h + 1) * B], bf16_mode=False,
-                                 train=True) for h in range(2)]
     assert rel_err(_np(logits), np.concatenate([r["logits"] for r in halves])) < 1e-5
     ref_loss = 0.5 * (halves[0]["loss"] + halves[1]["loss"])
     assert abs(float(loss) - ref_loss) < 1e-5 * max(1.0, abs(ref_loss))
+    worst = (0.0, "")
     for k, p in model.named_parameters():
         g0, g1 = halves[0]["grads"][k], halves[1]["grads"][k]
-        # error relative to the halves' own magnitudes: the two half-batch gradients partly cancel (a BN bias
-        # gradient is a sum of dz), and each half carries its own summation noise (layer3.1.bn2.bias: 1.2e-2
-        # relative to the small mean, r05i)
-        e = float(np.linalg.norm(_np(p.grad) - 0.5 * (g0 + g1))) / (0.5 * (np.linalg.norm(g0) + np.linalg.norm(g1)))
-        assert e < 5e-3, (k, e)
+        ref = 0.5 * (g0 + g1)
+        den = 0.5 * (np.linalg.norm(g0) + np.linalg.norm(g1))
+        e = float(np.linalg.norm(_np(p.grad) - ref)) / den
+        floor = float(np.linalg.norm(0.5 * (single[0][k] + single[1][k]) - ref)) / den
+        assert e <= 2.0 * floor + 1e-4, (k, e, floor)
+        worst = max(worst, (e, k))
+    print(f"DP [0,0] fp32 vs oracle: worst parameter-gradient error {worst[0]:.2e} ({worst[1]})")
     sd2 = model.state_dict()
     for k, v in halves[0]["buffers"].items():
         e = rel_err(sd2[k].cpu().numpy(), v)

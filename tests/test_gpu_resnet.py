@@ -476,6 +476,20 @@ def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5, hw=32):
         dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
 
 
+@pytest.mark.parametrize("batch", [256, 32])
+def test_backward_bit_identical_across_steps(dtc, cuda, batch):
+    """Run-to-run determinism of the default training step (in-kernel split-K sums in a
+    fixed split order, no order-dependent atomics on any gradient): the same forward + backward twice on the
+    same weights and data -- eager, and graph capture then replay -- gives bit-identical gradients for every
+    parameter, at config 2's batch and config 3's per-rank batch."""
+    lay = dtc.nn.Layout(100, 25.0)
+    for graphs in (0, 1):
+        g = _grads_repeated(dtc, cuda, graphs, batch=batch)
+        bad = [pe.name for pe in lay.params
+               if not np.array_equal(g[0][pe.offset:pe.offset + pe.numel], g[1][pe.offset:pe.offset + pe.numel])]
+        assert not bad, f"graphs={graphs}: gradients differ between two identical steps: {bad}"
+
+
 @pytest.mark.parametrize("batch,hw", [(8, 32), (3, 32), (5, 8)])
 def test_bn_reduce_unrolled_loads_bit_identical(dtc, cuda, batch, hw):
     """Option bn_red_unroll (default 4): the mask-bit BN-backward reduction issues the loads of 4 (or 2) rows

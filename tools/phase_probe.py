@@ -6,6 +6,7 @@ landed (prologue), 2 second reduction chunk's first step (chunk 0 + halo reload)
 4 exit (epilogue). Prints the kernel span, the dispatch spread, per-phase percentiles and how many
 workgroups are resident / in each phase over time (s_memrealtime: 100 MHz, chip-wide)."""
 import argparse
+import ctypes
 import os
 import sys
 
@@ -38,7 +39,10 @@ def main():
         nat.call("dtc_set_option", k.encode(), int(v))
     dev = torch.device("cuda:0")
     buf = torch.zeros(16384 * 8, dtype=torch.int64, device=dev)
-    nat.lib.dtc_probe_phase_buffer(nat.ptr(buf))
+    fn_set = nat.lib.dtc_probe_phase_buffer
+    fn_set.argtypes = [ctypes.c_void_p]  # (a bare Python int would pass as a 32-bit C int)
+    fn_set.restype = ctypes.c_int
+    fn_set(ctypes.c_void_p(buf.data_ptr()))
     B = args.batch
     P_ = nat.ptr
     for lname in args.layers.split(","):
