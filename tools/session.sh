@@ -1,1 +1,1 @@
-tools/gpu_run.sh r05m "tests:l2_prefetch_bit_identical" && PY_ARGS="--layers l2,l3,l4 --passes fwd,dgrad --variants 'halo_l2pf=0;halo_l2pf=1'" tools/gpu_run.sh r05m py:tools/conv_bench.py && PY_ARGS="--layers l2,l3 --passes fwd,dgrad --opts halo_l2pf=1" tools/gpu_run.sh r05m py:tools/phase_probe.py && AB_ROUNDS=3 tools/gpu_run.sh r05m "ab:base|;pf|--opt halo_l2pf=1"
+AB_ROUNDS=5 tools/gpu_run.sh r05q "ab:base|;df0|--opt dgrad_first=0" && tools/gpu_run.sh r05q tests
