@@ -93,6 +93,21 @@ struct HConvParams {
   FastDiv fd_gtpi, fd_gspr;
 };
 
+// s_waitcnt vmcnt(NIW + S(tap - 1) + S(tap - 2)) for the double-buffered halo's static slices S(k) = the halo DMA
+// instructions issued at tap k (k < 8) -- the immediate must be a literal, so one asm per tap after unrolling
+template <int NHI>
+__host__ __device__ constexpr int halo_slice(int k) { return k < 0 || k > 7 ? 0 : (((k + 1) * NHI) >> 3) - ((k * NHI) >> 3); }
+template <int NIW, int NHI>
+__device__ __forceinline__ void wait_vm_slices(int tap) {
+#define DTC_VMW(T_) \
+  case T_: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIW + halo_slice<NHI>(T_ - 1) + halo_slice<NHI>(T_ - 2)) : "memory"); break
+  switch (tap) {
+    DTC_VMW(1); DTC_VMW(2); DTC_VMW(3); DTC_VMW(4); DTC_VMW(5); DTC_VMW(6); DTC_VMW(7); DTC_VMW(8);
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIW) : "memory");
+  }
+#undef DTC_VMW
+}
+
 template <int MODE, int BM, int BN, int WR, int WC, int NHB, int HCAP, int WS, int ST = 1, bool SC = false,
           bool GEN = false>
 __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) {
@@ -205,10 +220,13 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     }
     hoff[q] = off;
   }
-  auto stage_h = [&](char* dst, int cc, int q_lo, int q_hi) {
+  // (all: a full load skips instructions past the tile's halo; false: every instruction of [q_lo, q_hi) is issued
+  // -- rows past the halo get zeros (out-of-range offset) in LDS rows nothing reads -- so a slice's instruction
+  // count is a compile-time constant the counted waits below can leave in flight)
+  auto stage_h = [&](char* dst, int cc, int q_lo, int q_hi, bool all = true) {
 #pragma unroll
     for (int q = 0; q < NHI; ++q) {
-      if (q >= q_lo && q < q_hi && q < p.nhi) {
+      if (q >= q_lo && q < q_hi && (!all || q < p.nhi)) {
         const uint32_t o = hoff[q] == 0x80000000u ? 0x80000000u : hoff[q] + (uint32_t)(cc * 128);
         buf_lds16(gsrc, GEN ? 0x7ffffff0u : p.src_bytes, dst + (wave + 4 * q) * 1024, o);
       }
@@ -355,8 +373,14 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
       for (int tap = 0; tap < 9; ++tap) {
         const int step = c * 9 + tap;
         if constexpr (WS == 3) {
-          if (step + 1 < nsteps && !(NHB == 1 && tap == 0 && c > 0)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIW) : "memory");
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          // NHB = 2: the next chunk's halo slices of the two previous steps may stay in flight as well (issued after
+          // their step's weights, so younger than this step's weights; the chunk's first step needs them all)
+          if (step + 1 < nsteps && !(NHB == 1 && tap == 0 && c > 0)) {
+            if (NHB == 2 && tap >= 1 && c + 1 < p.nchunk) wait_vm_slices<NIW, NHI>(tap);
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIW) : "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -379,8 +403,9 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
         }
         if constexpr (NHB == 2) {
           if (c + 1 < p.nchunk && tap < 8) {  // next chunk's halo, slice `tap` of 8
-            const int q_lo = (tap * p.nhi) >> 3, q_hi = ((tap + 1) * p.nhi) >> 3;
-            stage_h(smem + (half ^ 1) * HBYTES, c0 + c + 1, q_lo, q_hi);
+            // static slices of the NHI instructions (WS = 3: counted in the waits above; rows past the halo zeroed)
+            if constexpr (WS == 3) stage_h(smem + (half ^ 1) * HBYTES, c0 + c + 1, (tap * NHI) >> 3, ((tap + 1) * NHI) >> 3, false);
+            else stage_h(smem + (half ^ 1) * HBYTES, c0 + c + 1, (tap * p.nhi) >> 3, ((tap + 1) * p.nhi) >> 3);
           }
         }
         compute(hbuf, wbase + (WS == 3 ? (tap % 3) : ((half + tap) & 1)) * WBYTES, tap);
