@@ -819,7 +819,13 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
     // measured (tools/conv_bench.py, B=256): 64x256 tiles while they give >= 2 workgroups per CU
     // (layer1/2); else 64x128 tiles at 3 workgroups per CU, split-K up to ~2 workgroups per CU
     // (layer3: 512 tiles; layer4: 256 tiles x 2 splits)
+    // round 5 (option halo_small, default on): 64 x 64 tiles with the double-buffered halo (config 7) wherever they
+    // give at most 512 workgroups -- the small layers at every batch (tools/conv_bench.py, r05v / r05w, fwd / dgrad
+    // us: layer4 at B=256 25.4 / 24.9 vs 27.1 / 27.5; layer3 at B=128 14.9 / 14.5 vs 18.5 / 18.8; at B=32 layer2
+    // 8.6 / 8.3 vs 9.3 / 9.9, layer3 13.1 / 12.8 vs 14.9 / 15.5, layer4 15.9 / 15.4 vs 17.7 / 18.1); with more
+    // tiles the 64 x 64 tile's weight re-streaming per FLOP loses (layer2 at B=256: 34.3 vs 23.5)
     if (cfg_fits(s, 0, cout) && tiles(0) >= 512) hp.cfg = 0;
+    else if (option_get(OPT_HALO_SMALL) != 0 && cfg_fits(s, 7, cout) && tiles(7) <= 512) hp.cfg = 7;
     else if (cfg_fits(s, 2, cout)) hp.cfg = 2;
     else if (cfg_fits(s, 0, cout)) hp.cfg = 0;
     else return hp;
