@@ -416,8 +416,14 @@ static bool c64_gen_ok(const ConvShape& s) {
   const int64_t M = (int64_t)s.N * s.H * s.W;
   return M / 256 < (1ll << 31) && M < (1ll << 31) && (int64_t)C64_GROWS * s.W * 128 < (1ll << 31);
 }
+// option conv_c64: 0 off; 1 (auto) where every persistent workgroup gets at least one 256-pixel tile -- below
+// that (batch 32 at 32x32: 128 tiles for 256 workgroups) the halo kernel's 64 x 64 tiles fill the chip (layer1
+// fwd / dgrad at B=32 8.0 / 7.5 vs 9.4 / 8.7 us; equal at B=64, c64 ahead at B=128: tools/conv_bench.py r05y);
+// 2 always
 bool conv_c64_ok(const ConvShape& s) {
-  if (option_get(OPT_CONV_C64) == 0) return false;
+  const int o = option_get(OPT_CONV_C64);
+  if (o == 0) return false;
+  if (o == 1 && (int64_t)s.N * s.H * s.W / 256 < (int64_t)std::max(1, option_get(OPT_C64_WGS))) return false;
   return c64_classic_ok(s) || c64_gen_ok(s);
 }
 static bool c64_classic_ok(const ConvShape& s) {

@@ -21,7 +21,7 @@ namespace dtc {
   X(HALO_CONV, halo_conv, 1)            /* halo FWD/DGRAD for 3x3 s1: 0 off, 1 auto, 2+k force cfg k */     \
   X(HALO_SPLIT, halo_split, 0)          /* halo FWD/DGRAD split-K: 0 auto, k forced */                        \
   X(BWD_STREAMS, bwd_streams, 1)        /* weight gradients on a side stream beside the dgrad/BN chain */    \
-  X(CONV_C64, conv_c64, 1)              /* persistent 64->64 3x3 conv (conv_c64.hip) for layer1 */           \
+  X(CONV_C64, conv_c64, 1)              /* persistent 64->64 3x3 conv for layer1: 1 >= a tile per workgroup, 2 always */           \
   X(BN_FUSED_FIN, bn_fused_fin, 1)      /* BN coefficients folded into the apply kernels */                   \
   X(HALO_WSTAGES, halo_wstages, 3)      /* weight ring depth of conv_halo (2 or 3) */                         \
   X(C64_PF, c64_pf, 1)                  /* conv_c64: next (tap, k-step) fragments read ahead */               \

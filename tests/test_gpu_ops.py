@@ -707,8 +707,18 @@ def test_conv_halo_general_geometry(dtc, cuda, case):
 C64_CASES = [(2, 32, 32), (3, 16, 16), (5, 32, 32)]
 
 
+@pytest.fixture
+def c64_forced(dtc):
+    """conv_c64=2: the persistent layer1 kernel even where its automatic rule (at least one 256-pixel tile per
+    workgroup) would leave these small test batches to conv_halo."""
+    prev = dtc._native.lib.dtc_get_option(b"conv_c64")
+    dtc._native.call("dtc_set_option", b"conv_c64", 2)
+    yield
+    dtc._native.call("dtc_set_option", b"conv_c64", prev)
+
+
 @pytest.mark.parametrize("case", C64_CASES)
-def test_conv_c64(dtc, cuda, case):
+def test_conv_c64(dtc, cuda, case, c64_forced):
     """Persistent 64->64 3x3 kernel (conv_c64.hip, layer1): FWD (+BN statistics accumulated per
     workgroup across tiles) and DGRAD (+residual), with more tiles than workgroups for case 3."""
     N, H, W = case
@@ -733,7 +743,7 @@ C64_GEN_CASES = [(2, 16, 224), (3, 8, 64), (2, 40, 96)]
 
 
 @pytest.mark.parametrize("case", C64_GEN_CASES)
-def test_conv_c64_general_geometry(dtc, cuda, case):
+def test_conv_c64_general_geometry(dtc, cuda, case, c64_forced):
     """conv_c64's general geometry (8-row x 32-column tiles, 64-bit per-tile bases; rows of 224 / 64 / 96
     pixels that the classic whole-row tiles do not fit -- the 224x224 model's layer1): FWD (+BN statistics)
     and DGRAD (+residual) against the oracle, and against conv_halo (option c64_gen=0) on the same operands:

@@ -230,7 +230,7 @@ def test_per_layer_teacher_forced_config2_b256(dtc, cuda, stages):
 # BASELINE config 3's per-rank shapes: global batch 256 over W = 2 / 4 / 8 ranks (ddp/trainer.py:34) gives
 # 128 / 64 / 32 images per GPU, where the tile plans, split-K factors and wgrad splits differ from B = 256
 # (small-GEMM regime: layer4 at B=32 is 512 x 512 x 4608, SURVEY §7 iii). Default options, every stage
-# (the stem and layer1 included: conv_c64's tile walk at 32 / 64 / 128 images).
+# (the stem and layer1 included: conv_c64's tile walk at 64 / 128 images; at 32 layer1 takes conv_halo).
 @pytest.mark.parametrize("batch", [32, 64, 128])
 def test_per_layer_teacher_forced_config3_per_rank(dtc, cuda, batch):
     imgs = None if batch <= 32 else np.unique(np.concatenate([np.arange(4), np.arange(28, 36), np.arange(batch - 4, batch)]))
