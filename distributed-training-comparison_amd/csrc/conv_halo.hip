@@ -781,7 +781,10 @@ HaloPlan conv_halo_plan(const ConvShape& s, int mode) {
     // auto: only where the reduction has >= 2 chunks -- with one 64-channel chunk (layer2.0.conv1) the whole
     // halo must land before the first MFMA and the implicit GEMM's per-tap pipeline is faster (20 vs 28 us
     // at B=256; layer3 20.7 -> 19.6, layer4 22.2 -> 17.1, the shortcut-fused launches 29.2 -> 24.1 / 20.3)
-    if (o2 == 1 && s.C < 128) return hp;
+    // (round 5: except where its 64 x 64 tiles give <= 512 workgroups -- config 3's per-rank batches: layer2.0's
+    // forward + shortcut at B=32 8.5 vs 10.6 us, B=64 10.3 vs 12.9; conv_bench r05zc)
+    const int64_t s2tiles = (int64_t)s.N * (s.H / 2) * (s.W / 2) / 64 * (s.K / 64);
+    if (o2 == 1 && s.C < 128 && s2tiles > 512) return hp;
     const int cfg = o2 >= 2 ? std::min(kFirstS2Cfg + o2 - 2, kNumHaloCfgs - 1) : kFirstS2Cfg;
     if (cfg_fits(s, cfg, s.K)) hp.cfg = cfg;
     return hp;  // no split-K: the shortcut fusion and the BN statistics live in the epilogue

@@ -308,9 +308,15 @@ static int s2d_bn(const ConvShape& s) {
 // option dgrad_s2h: 1 (auto) where it measured faster than the parity-class igemm -- output-gradient depth
 // K <= 256 (conv_bench r05g, batch 256: layer2.0 28.2 -> 17.9 us, layer3.0 23.2 -> 20.5); layer4's K = 512 runs
 // 4608-deep reductions on 256 workgroups with no split (27.0 us against the classes' 22.6); 2 every geometry
+// and only where the tiles give >= 256 workgroups: with fewer (config 3's per-rank batches) the parity-class GEMM
+// is ahead (B=32: l2.0.c1 8.4 vs 9.4 us, l3.0.c1 12.5 vs 15.0; B=64: 9.8 vs 10.0, 12.8 vs 15.2; conv_bench r05zc)
 bool dgrad_s2_halo_ok(const ConvShape& s) {
   const int o = option_get(OPT_DGRAD_S2H);
-  return o != 0 && (o >= 2 || s.K <= 256) && s2d_bn(s) > 0;
+  const int bn = s2d_bn(s);
+  if (o == 0 || bn == 0) return false;
+  if (o >= 2) return true;
+  const int64_t wgs = ((int64_t)s.N * (s.H / 2) * (s.W / 2) + bn - 1) / bn * (s.C / 64);
+  return s.K <= 256 && wgs >= 256;
 }
 
 int conv_dgrad_s2_halo(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u16* dsc, const u16* wsc,
