@@ -154,7 +154,7 @@ _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", 
                     "halo_nhb2", "wgrad_kernel", "head_direct", "halo_nosplit", "graph_ev", "wgrad_tail",
                     "wgrad_stages", "wgrad_pf", "wgrad_diag",
                     # round 5
-                    "bnb_mask", "bnb_fuse", "halo_stage_epi", "igemm_stages", "halo_l2pf", "dgrad_first", "wgrad_s2_ps")
+                    "bnb_mask", "bnb_fuse", "halo_stage_epi", "igemm_stages", "halo_l2pf", "dgrad_first", "wgrad_s2_ps", "c64_waves")
 
 
 def test_options_registered_with_defaults(dtc):
