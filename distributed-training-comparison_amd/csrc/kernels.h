@@ -67,8 +67,7 @@ namespace dtc {
   X(WGRAD_INK, wgrad_ink, 0)            /* wgrad split-K summed by the last workgroup per tile: 1 stride-2, 2 all */ \
   X(WGRAD_INK_MAX, wgrad_ink_max, 8)    /* ... for launches of at most this many splits (else a reduce launch) */ \
   X(DGRAD_S2H, dgrad_s2h, 1)            /* stride-2 3x3 dgrad (+ shortcut) as a halo sub-pixel conv: 1 K <= 256, 2 all */ \
-  X(HALO_SMALL, halo_small, 1)          /* halo FWD/DGRAD: 64x64 double-buffered tiles where they give <= 512 workgroups */ \
-  X(WGRAD_EARLY, wgrad_early, 0)        /* layer1's wgrads: 1 layer1.1's launched under layer1.0's chain, 2 also layer1.0 conv2's */
+  X(HALO_SMALL, halo_small, 1)          /* halo FWD/DGRAD: 64x64 double-buffered tiles where they give <= 512 workgroups */
 
 enum {
 #define DTC_OPT_ENUM(id, name, def) OPT_##id,

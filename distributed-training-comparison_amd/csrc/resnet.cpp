@@ -1200,13 +1200,6 @@ static bool bucket_fires(const Net& n, int after_block) {
     if (a == after_block) return true;
   return false;
 }
-// Option wgrad_early: the queued weight gradients of layer1.1 (block 1) would otherwise wait for layer1.0's two
-// and go out as ONE batch of four after layer1.0's last dgrad -- the backward's tail, with nothing left on the
-// main stream to overlap it. Level 1 launches block 1's two at the end of block 1 (under layer1.0's dgrad / BN
-// chain); level 2 also layer1.0 conv2's alone right after it is queued, so only conv1's is left for the tail.
-// Independent of the communicator (bucket points unchanged), so the batching -- and each conv's split-K
-// summation order -- is the same with or without DDP.
-static bool wg_early(int bi, int stage) { return bi == 1 - stage && option_get(OPT_WGRAD_EARLY) > stage; }
 
 // Backward with the mask-bit BN path (bn_mask_on): G[0] carries the RAW gradient of a block output
 // (never masked in place by a reduction), each BN reduction reads (dy, mask bits, x) and stores
@@ -1275,10 +1268,6 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     const bool lazy = option_get(OPT_FORK_LAZY) != 0;
     if (!lazy) DTC_TRY(fork_side(n, st, &sd));
     DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd, st, lazy));
-    if (wg_early(bi, 1) && wq.count > 0) {
-      if (lazy) DTC_TRY(fork_side(n, st, &sd));
-      DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
-    }
     PROF(1, conv_flops(b.c2.s),
          conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts, nullptr, 0, n.tick(0)));
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
@@ -1324,7 +1313,7 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
            conv_dgrad(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], G[0], slab, n.slab_bytes, st, ts, nullptr, 0, n.tick(0)));
     }
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
-    if (bucket_fires(n, bi) || wg_early(bi, 0)) {
+    if (bucket_fires(n, bi)) {
       if (lazy && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
       DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
     }
@@ -1430,7 +1419,6 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
     // conv2: dW2 (side stream) and da1
     DTC_TRY(fork_side(n, st, &sd));
     DTC_TRY(wg_issue(n, wq, b.c2.s, n.at<u16>(b.A1), dc2, n.gf(b.c2.pidx), gs, slabw, sd));
-    if (wg_early(bi, 1)) DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
     // a1 = relu(bn1(c1)): da1 -> dz1 (fused into the dgrad, or a separate reduction)
     {
       const BnbArgs bz = bnb_of(n, b.A1, b.C1, b.b1);
@@ -1468,7 +1456,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
     dz_ready = fuse;
     if (b.proj) DTC_TRY(cap(n, cp + ".dxs", G[5], st));
     DTC_TRY(cap(n, cp + ".dx", G[0], st));
-    if (bucket_fires(n, bi) || wg_early(bi, 0)) DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
+    if (bucket_fires(n, bi)) DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
     DTC_TRY(maybe_bucket(n, bi, cx, st));
   }
   // stem: a0 = relu(bn1(conv1(x)))

@@ -552,28 +552,6 @@ def test_wgrad_batch_matches_unbatched(dtc, cuda, graphs):
 
 
 @pytest.mark.parametrize("graphs", [True, False])
-@pytest.mark.parametrize("level", [1, 2])
-def test_wgrad_early_matches_tail_batch(dtc, cuda, graphs, level):
-    """Option wgrad_early: layer1.1's weight gradients launched at the end of its block (1), and layer1.0
-    conv2's right after it is queued (2), instead of all four in one batch at the backward's tail (0): the
-    same kernels over the same operands with other split counts, so only the fp32 split-K summation order
-    differs (capture and replay)."""
-    lib = dtc._native.lib
-    ga = _grads_repeated(dtc, cuda, graphs)
-    lib.dtc_set_option(b"wgrad_early", level)
-    try:
-        gb = _grads_repeated(dtc, cuda, graphs)
-    finally:
-        lib.dtc_set_option(b"wgrad_early", 0)
-    lay = dtc.nn.Layout(100, 25.0)
-    for rep in range(2):
-        for pe in lay.params:
-            a = ga[rep][pe.offset:pe.offset + pe.numel]
-            b = gb[rep][pe.offset:pe.offset + pe.numel]
-            assert rel_err(a, b) < 1e-5, (rep, pe.name, rel_err(a, b))
-
-
-@pytest.mark.parametrize("graphs", [True, False])
 def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
     """Mask-bit BN backward (option bn_mask=1, default: the forward BN apply writes the ReLU mask as
     bits, the reduction stores no dz, the apply forms dz from dy and the bits) vs masking with the

@@ -147,14 +147,14 @@ _OPTION_DEFAULTS = {
     # round 4
     "bn_cg": 1, "bn_cg_elems": 262144, "wgrad_s2_wgs": 128, "comm_on_side": 1, "wgrad_ksplit": 2, "wgrad_ring": 4, "c64_wgs": 256, "wgrad_halo_l1": 0,
     # round 5
-    "splitk_ink": 1, "comm_prio": 0, "comm_tail_inline": 1, "wgrad_ink": 0, "wgrad_ink_max": 8, "dgrad_s2h": 1, "halo_small": 1, "wgrad_early": 0,
+    "splitk_ink": 1, "comm_prio": 0, "comm_tail_inline": 1, "wgrad_ink": 0, "wgrad_ink_max": 8, "dgrad_s2h": 1, "halo_small": 1,
 }
 # measured-negative variants deleted in rounds 4 and 5 with their code paths (DESIGN.md keeps their numbers)
 _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", "wgrad_pmap", "wgrad_prio",
                     "halo_nhb2", "wgrad_kernel", "head_direct", "halo_nosplit", "graph_ev", "wgrad_tail",
                     "wgrad_stages", "wgrad_pf", "wgrad_diag",
                     # round 5
-                    "bnb_mask", "bnb_fuse", "halo_stage_epi", "igemm_stages", "halo_l2pf", "dgrad_first", "wgrad_s2_ps", "c64_waves")
+                    "bnb_mask", "bnb_fuse", "halo_stage_epi", "igemm_stages", "halo_l2pf", "dgrad_first", "wgrad_s2_ps", "c64_waves", "wgrad_early")
 
 
 def test_options_registered_with_defaults(dtc):
