@@ -1,1 +1,1 @@
-AB_ROUNDS=5 tools/gpu_run.sh r05q "ab:base|;df0|--opt dgrad_first=0" && tools/gpu_run.sh r05q tests
+tools/gpu_run.sh r05zi tests smoke bench && timeout -k 10 300 tools/prof_run.sh r05zi_ser --opt bwd_streams=0 --opt graphs=0
