@@ -483,33 +483,39 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
       return;
     }
     // the sum splitk_reduce forms: 0 + slab[0] + slab[1] + ... (same order, same bits), this workgroup's own
-    // partial from its registers; every other split's fragments loaded before the first add
+    // partial from its registers. The other splits' fragments are loaded GS splits at a time, every load of a
+    // group in flight before its first add: one memory latency per group instead of one per split (the
+    // 64 x 64 tiles of layer4 at small batch split four ways: their last arriver waited three latencies)
+    constexpr int GS = FM * FN <= 4 ? 4 : (FM * FN <= 8 ? 2 : 1);
     f32x4 sum[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sp = 0; sp < nsplit; ++sp) {
-      if (sp == split) {
+    for (int g0 = 0; g0 < nsplit; g0 += GS) {
+      f32x4 part[GS][FM][FN];
+#pragma unroll
+      for (int u = 0; u < GS; ++u) {
+        const int sp = g0 + u;
+        const bool ld = sp < nsplit && sp != split;
+        const uint32_t base = (uint32_t)((size_t)(ld ? sp : 0) * plane * 4);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) sum[i][j] += acc[i][j];
-        continue;
+          for (int j = 0; j < FN; ++j)
+            part[u][i][j] = ld && eoff[i][j] != 0x80000000u
+                                ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + eoff[i][j], 0, 16))
+                                : f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      const uint32_t base = (uint32_t)((size_t)sp * plane * 4);
-      f32x4 part[FM][FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int u = 0; u < GS; ++u) {
+        const int sp = g0 + u;
+        if (sp >= nsplit) break;
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          part[i][j] = eoff[i][j] != 0x80000000u
-                           ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + eoff[i][j], 0, 16))
-                           : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) sum[i][j] += part[i][j];
+          for (int j = 0; j < FN; ++j) sum[i][j] += sp == split ? acc[i][j] : part[u][i][j];
+      }
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
