@@ -174,8 +174,9 @@ def comm_fields(bucket_us, exposed_us, steps, buckets_mb):
     backward's start and its duration (timing events on the stream it runs on)."""
     if not steps:
         return None, None
-    exposed = {"tail_us": round(exposed_us[0], 2), "side_join_us": round(exposed_us[1], 2),
-               "total_us": round(exposed_us[2], 2), "backward_us": round(exposed_us[3], 2), "steps": int(steps),
+    opt = lambda v: round(v, 2) if v >= 0 else None  # -1: no timed step recorded a tail (replayed backwards)
+    exposed = {"tail_us": opt(exposed_us[0]), "side_join_us": round(exposed_us[1], 2),
+               "total_us": opt(exposed_us[2]), "backward_us": round(exposed_us[3], 2), "steps": int(steps),
                "note": "tail = last backward kernel -> the Reducer's join on the compute stream (the last bucket's "
                        "collective, nothing left to overlap); side_join = the compute stream's wait for the "
                        "weight-gradient stream (its queued weight gradients + the earlier buckets' collectives) "

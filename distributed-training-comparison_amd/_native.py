@@ -65,6 +65,8 @@ _SIGS = {
     "dtc_conv2d_wgrad": (i32, [PConv, vp, vp, vp, f32, vp, sz, vp]),
     "dtc_conv2d_wgrad_batch_workspace_size": (sz, [PConv, i32]),
     "dtc_conv2d_wgrad_batch": (i32, [PConv, i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), f32, vp, sz, vp]),
+    "dtc_bn_stat_words": (sz, [i32]),
+    "dtc_bn_stat_totals": (i32, [vp, i32, vp]),
     "dtc_bn_fwd_finalize": (i32, [vp, i32, i64, vp, vp, vp, vp, vp, f32, f32, vp, vp, vp, vp, vp]),
     "dtc_bn_apply_relu": (i32, [vp, vp, vp, vp, i64, i32, vp]),
     "dtc_bn_apply_add_relu": (i32, [vp, vp, vp, vp, vp, i64, i32, vp]),

@@ -7,9 +7,9 @@
 // num_batches_tracked += 1. Under autocast the conv output is bf16, BN computes in fp32
 // and emits bf16, ReLU's backward masks with its own (bf16) output.
 //
-// Statistics: the forward sums (sum x, sum x^2) are produced by the conv epilogue into
-// fp64 slots (igemm.hip); here they are finalised. Backward sums (sum dz, sum dz*xhat)
-// are reduced per workgroup through LDS and then added into fp64 slots.
+// Statistics: the forward sums (sum x, sum x^2) are produced by the conv epilogues into
+// fixed-point slots (common.h); here they are finalised. Backward sums (sum dz, sum dz*xhat)
+// are reduced per workgroup through LDS and then added into the same kind of slots.
 #include "common.h"
 #include "kernels.h"
 #include "tile_common.h"
@@ -19,57 +19,41 @@ namespace dtc {
 
 static inline int ceil_div_i(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
-// Finalize layout: a 256-thread workgroup owns FIN_CH = 32 channels; thread t reads channel
-// c0 + (t & 31) of the slots k = (t >> 5) + 8j (j < 4), both statistics (8 loads, all issued before
-// any use), re-zeroes them, and the eight partial sums per channel are combined in LDS in a fixed
-// order. Few registers and no scratch: measured on MI355X, a finalize holding all 64 slot values
-// per thread spilled to scratch (44-284 B/lane) and cost 10-16 us per launch instead of ~2.
-constexpr int FIN_CH = 32, FIN_GROUPS = 8, FIN_PER = DTC_STAT_SLOTS / FIN_GROUPS;
+// Finalize layout: a 256-thread workgroup owns FIN_CH = 32 channels; thread t reads word (t >> 5) & 3
+// (statistic, hi / lo: common.h) of channel c0 + (t & 31) in half t >> 7 of the slots (8 loads, all
+// issued before any use), re-zeroes them, sums them as integers, and the two halves are combined in LDS.
+// Few registers and no scratch: measured on MI355X, a finalize holding all 64 slot values per thread
+// spilled to scratch (44-284 B/lane) and cost 10-16 us per launch instead of ~2.
+constexpr int FIN_CH = 32, FIN_GROUPS = 8, FIN_PER = DTC_STAT_SLOTS / 2;
 
-__device__ __forceinline__ bool fin_sum_slots(double* __restrict__ base, int C, double& s, double& q,
-                                              double (*red)[2][FIN_CH]) {
-  const int t = threadIdx.x, cl = t & (FIN_CH - 1), g = t >> 5;
+__device__ __forceinline__ bool fin_sum_slots(int64_t* __restrict__ base, int C, double& s, double& q,
+                                              int64_t (*red)[FIN_CH]) {
+  const int t = threadIdx.x, cl = t & (FIN_CH - 1), g = t >> 5, wd = g & 3, half = g >> 2;
   const int c = blockIdx.x * FIN_CH + cl;
-  double sv[FIN_PER], qv[FIN_PER];
+  const int64_t flag = base[0];
   if (c < C) {
+    int64_t v[FIN_PER];
 #pragma unroll
-    for (int j = 0; j < FIN_PER; ++j) {
-      const size_t k = (size_t)(g + FIN_GROUPS * j);
-      sv[j] = base[k * 2 * C + c];
-      qv[j] = base[k * 2 * C + C + c];
-    }
-    double a = 0.0, b = 0.0;
+    for (int j = 0; j < FIN_PER; ++j) v[j] = base[stat_word(half * FIN_PER + j, wd >> 1, wd & 1, C) + c];
+    int64_t a = 0;
 #pragma unroll
-    for (int j = 0; j < FIN_PER; ++j) {
-      a += sv[j];
-      b += qv[j];
-    }
+    for (int j = 0; j < FIN_PER; ++j) a += v[j];
 #pragma unroll
-    for (int j = 0; j < FIN_PER; ++j) {
-      const size_t k = (size_t)(g + FIN_GROUPS * j);
-      base[k * 2 * C + c] = 0.0;
-      base[k * 2 * C + C + c] = 0.0;
-    }
-    red[g][0][cl] = a;
-    red[g][1][cl] = b;
+    for (int j = 0; j < FIN_PER; ++j) base[stat_word(half * FIN_PER + j, wd >> 1, wd & 1, C) + c] = 0;
+    red[g][cl] = a;
   }
-  __syncthreads();
+  __syncthreads();  // (the header's flag is left as it is: the slots' owner zeroes the header)
   if (t >= FIN_CH || c >= C) return false;
-  s = 0.0;
-  q = 0.0;
-#pragma unroll
-  for (int k = 0; k < FIN_GROUPS; ++k) {
-    s += red[k][0][cl];
-    q += red[k][1][cl];
-  }
+  s = stat_total(red[0][cl] + red[4][cl], red[1][cl] + red[5][cl], flag);
+  q = stat_total(red[2][cl] + red[6][cl], red[3][cl] + red[7][cl], flag);
   return true;
 }
 
 __global__ void __launch_bounds__(256) bn_fwd_finalize_kernel(
-    double* __restrict__ stats, int C, double count, const float* __restrict__ gamma, const float* __restrict__ beta,
+    int64_t* __restrict__ stats, int C, double count, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float momentum, float eps,
     float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale, float* __restrict__ shift) {
-  __shared__ double red[FIN_GROUPS][2][FIN_CH];
+  __shared__ int64_t red[FIN_GROUPS][FIN_CH];
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
   double s, q;
   if (!fin_sum_slots(stats, C, s, q, red)) return;
@@ -90,7 +74,7 @@ __global__ void __launch_bounds__(256) bn_fwd_finalize_kernel(
   shift[c] = beta[c] - (float)mu * a;
 }
 
-int bn_fwd_finalize(double* stats, int C, int64_t count, const float* gamma, const float* beta, float* running_mean,
+int bn_fwd_finalize(int64_t* stats, int C, int64_t count, const float* gamma, const float* beta, float* running_mean,
                     float* running_var, int64_t* num_batches, float momentum, float eps, float* mean, float* invstd,
                     float* scale, float* shift, hipStream_t st) {
   DTC_CHECK_ARG(stats && gamma && beta && mean && invstd && scale && shift && C > 0 && count > 0,
@@ -205,8 +189,8 @@ DTC_BN_APPLY_DEFS(float)
 
 // ------------------------------------------------------------------ fused finalize + apply (forward)
 // The consumer computes the BN coefficients itself: workgroup (pixel block, 64-channel group)
-// sums the DTC_STAT_SLOTS fp64 slots of its 64 channels (32 KB, L2-resident: every workgroup of
-// the launch reads the same lines) in a fixed order, then normalises its pixels. The first pixel
+// sums the DTC_STAT_SLOTS fixed-point slots of its 64 channels (32 KB, L2-resident: every workgroup of
+// the launch reads the same lines; exact integer sums), then normalises its pixels. The first pixel
 // block of each channel group also writes the saved mean / invstd and the running statistics
 // (and num_batches_tracked once). Removes the separate finalize launch and its kernel boundary;
 // the slots are zeroed by a memset node at the start of the executor's forward.
@@ -221,7 +205,7 @@ __global__ void __launch_bounds__(256) bn_fin_apply_kernel(const T* __restrict__
                                                           T* __restrict__ y, int64_t M, int C, int rows,
                                                           uint8_t* __restrict__ mask, u64* ts) {
   typedef Elt<T> E;
-  __shared__ double part[4 * 2 * 64];
+  __shared__ int64_t part[256];
   __shared__ float coef[4][64];  // scale1, shift1, scale2, shift2
   stamp_start(ts);
   const int cg = blockIdx.y * FA_GROUP;
@@ -286,7 +270,7 @@ static void fa_grid(int64_t M, int C, int& nblk, int& rows) {
   const int groups = C / FA_GROUP;
   nblk = std::max(1, option_get(OPT_BN_FA_BLOCKS) / groups);  // workgroups per launch (default 1024)
   rows = (int)((M + nblk - 1) / nblk);
-  // at least FA_UNROLL rows per thread: each workgroup's prologue folds 32 KB of fp64 slots, which
+  // at least FA_UNROLL rows per thread: each workgroup's prologue folds 32 KB of statistic slots, which
   // dominated the small (layer3/4) launches at one row per thread
   rows = std::max(32 * FA_UNROLL, (rows + 31) / 32 * 32);
   nblk = (int)((M + rows - 1) / rows);
@@ -328,7 +312,7 @@ int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2,
 }
 
 // ------------------------------------------------------------------ fused finalize + apply (backward)
-// dx = A*dz + B*x + Cc with the coefficients computed per workgroup from the fp64 slots of
+// dx = A*dz + B*x + Cc with the coefficients computed per workgroup from the statistic slots of
 // sum(dz), sum(dz*xhat); the first pixel block writes dgamma / dbeta (x gscale).
 // MB: dz is formed here from the raw gradient (`dz` = dy) and the forward's ReLU mask bits
 // (dz = dy * [y > 0]; exact), and optionally stored to dzo (may alias dy: each element is read and
@@ -340,7 +324,7 @@ __global__ void __launch_bounds__(256) bn_bwd_fin_apply_kernel(const T* __restri
                                                               T* __restrict__ dx2, int64_t M, int C, int rows,
                                                               const uint8_t* __restrict__ mbits, T* dzo, u64* ts) {
   typedef Elt<T> E;
-  __shared__ double part[4 * 2 * 64];
+  __shared__ int64_t part[256];
   __shared__ float coef[6][64];
   stamp_start(ts);
   const int cg = blockIdx.y * FA_GROUP;
@@ -599,9 +583,9 @@ int bn_bwd_cg(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, cons
 template <bool MASK, bool DUAL, typename T, bool MB = false, int RU = 4>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const T* __restrict__ dy, const T* __restrict__ ym, const T* __restrict__ x1,
-    const float* __restrict__ mean1, const float* __restrict__ invstd1, double* __restrict__ acc1,
+    const float* __restrict__ mean1, const float* __restrict__ invstd1, int64_t* __restrict__ acc1,
     const T* __restrict__ x2, const float* __restrict__ mean2, const float* __restrict__ invstd2,
-    double* __restrict__ acc2, T* __restrict__ dz, int64_t M, int C, int rows_per_block,
+    int64_t* __restrict__ acc2, T* __restrict__ dz, int64_t M, int C, int rows_per_block,
     const uint8_t* __restrict__ mbits = nullptr, u64* ts = nullptr) {
   typedef Elt<T> E;
   __shared__ float red[256 * 24];
@@ -686,7 +670,6 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     red[t * 24 + 16 + k] = s2[k];
   }
   __syncthreads();
-  const size_t slot = (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * C;
   for (int c = t; c < C; c += 256) {
     const int gg = c >> 3, k = c & 7;
     float a = 0.f, b = 0.f, e = 0.f;
@@ -696,19 +679,15 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
       b += q[8 + k];
       e += q[16 + k];
     }
-    unsafeAtomicAdd(acc1 + slot + c, (double)a);
-    unsafeAtomicAdd(acc1 + slot + C + c, (double)b);
-    if constexpr (DUAL) {
-      unsafeAtomicAdd(acc2 + slot + c, (double)a);
-      unsafeAtomicAdd(acc2 + slot + C + c, (double)e);
-    }
+    stat_add(acc1, C, c, a, b);
+    if constexpr (DUAL) stat_add(acc2, C, c, a, e);
   }
   stamp_end(ts);
 }
 
 template <typename T>
-static int bwd_reduce(const T* dy, const T* ymask, const T* x1, const float* mean1, const float* invstd1, double* acc1,
-                      const T* x2, const float* mean2, const float* invstd2, double* acc2, T* dz, int64_t M, int C,
+static int bwd_reduce(const T* dy, const T* ymask, const T* x1, const float* mean1, const float* invstd1, int64_t* acc1,
+                      const T* x2, const float* mean2, const float* invstd2, int64_t* acc2, T* dz, int64_t M, int C,
                       hipStream_t st) {
   DTC_CHECK_ARG(dy && x1 && mean1 && invstd1 && acc1 && C % 8 == 0 && C <= 2048 && M > 0, "bn_bwd_reduce: bad args");
   DTC_CHECK_ARG(!ymask || dz, "bn_bwd_reduce: masked reduce needs a dz output");
@@ -736,7 +715,7 @@ static int bwd_reduce(const T* dy, const T* ymask, const T* x1, const float* mea
 }
 
 int bn_bwd_reduce_mask(const u16* dy, const uint8_t* mbits, const u16* x1, const float* mean1, const float* invstd1,
-                       double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, int64_t M,
+                       int64_t* acc1, const u16* x2, const float* mean2, const float* invstd2, int64_t* acc2, int64_t M,
                        int C, hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(dy && mbits && x1 && mean1 && invstd1 && acc1 && C % 8 == 0 && C <= 2048 && M > 0,
                 "bn_bwd_reduce_mask: bad args");
@@ -789,21 +768,21 @@ int bn_mask_apply(const u16* dy, const uint8_t* mbits, u16* dz, int64_t M, int C
 }
 
 int bn_bwd_reduce(const u16* dy, const u16* ymask, const u16* x1, const float* mean1, const float* invstd1,
-                  double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, u16* dz,
+                  int64_t* acc1, const u16* x2, const float* mean2, const float* invstd2, int64_t* acc2, u16* dz,
                   int64_t M, int C, hipStream_t st) {
   return bwd_reduce<u16>(dy, ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, st);
 }
 int bn_bwd_reduce(const float* dy, const float* ymask, const float* x1, const float* mean1, const float* invstd1,
-                  double* acc1, const float* x2, const float* mean2, const float* invstd2, double* acc2, float* dz,
+                  int64_t* acc1, const float* x2, const float* mean2, const float* invstd2, int64_t* acc2, float* dz,
                   int64_t M, int C, hipStream_t st) {
   return bwd_reduce<float>(dy, ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, st);
 }
 
 __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
-    double* __restrict__ acc, int C, double count, const float* __restrict__ gamma, const float* __restrict__ mean,
+    int64_t* __restrict__ acc, int C, double count, const float* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ invstd, float gscale, float* __restrict__ dgamma, float* __restrict__ dbeta,
     float* __restrict__ coef) {
-  __shared__ double red[FIN_GROUPS][2][FIN_CH];
+  __shared__ int64_t red[FIN_GROUPS][FIN_CH];
   double sd, sx;
   if (!fin_sum_slots(acc, C, sd, sx, red)) return;
   const int c = blockIdx.x * FIN_CH + threadIdx.x;
@@ -818,7 +797,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
   coef[2 * C + c] = (float)Cc;
 }
 
-int bn_bwd_finalize(double* acc, int C, int64_t count, const float* gamma, const float* mean, const float* invstd,
+int bn_bwd_finalize(int64_t* acc, int C, int64_t count, const float* gamma, const float* mean, const float* invstd,
                     float gscale, float* dgamma, float* dbeta, float* coef, hipStream_t st) {
   DTC_CHECK_ARG(acc && gamma && mean && invstd && coef && C > 0 && count > 0, "bn_bwd_finalize: bad args");
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div_i(C, FIN_CH)), dim3(256), 0, st, acc, C, (double)count, gamma,
@@ -879,19 +858,29 @@ int bn_bwd_apply(const float* dz, const float* x1, const float* coef1, float* dx
 }
 
 // ---------------------------------------------------------------- SyncBN slot compaction
-__global__ void bn_fold_slots_kernel(double* __restrict__ slots, int n2c) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n2c) return;
-  double a = 0.0;
-  for (int k = 0; k < DTC_STAT_SLOTS; ++k) a += slots[(size_t)k * n2c + j];
-  slots[j] = a;
-  for (int k = 1; k < DTC_STAT_SLOTS; ++k) slots[(size_t)k * n2c + j] = 0.0;
+// Folds the slots into slot 0 (exact integer sums; lo carried into hi, so slot 0's lo word stays below 2^44
+// and a SUM over ranks cannot overflow it) and zeroes the others: the collective then carries the header
+// and slot 0 (DTC_STAT_HDR + 4 C words, contiguous) instead of every slot.
+__global__ void bn_fold_slots_kernel(int64_t* __restrict__ st, int C) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;  // (statistic, channel)
+  if (j >= 2 * C) return;
+  const int stat = j / C, c = j - stat * C;
+  int64_t hi = 0, lo = 0;
+  for (int k = 0; k < DTC_STAT_SLOTS; ++k) {
+    hi += st[stat_word(k, stat, 0, C) + c];
+    lo += st[stat_word(k, stat, 1, C) + c];
+  }
+  st[stat_word(0, stat, 0, C) + c] = hi + (lo >> 44);
+  st[stat_word(0, stat, 1, C) + c] = lo & ((1ll << 44) - 1);
+  for (int k = 1; k < DTC_STAT_SLOTS; ++k) {
+    st[stat_word(k, stat, 0, C) + c] = 0;
+    st[stat_word(k, stat, 1, C) + c] = 0;
+  }
 }
 
-int bn_fold_slots(double* slots, int C, hipStream_t st) {
+int bn_fold_slots(int64_t* slots, int C, hipStream_t st) {
   DTC_CHECK_ARG(slots && C > 0, "bn_fold_slots: bad args");
-  const int n2c = 2 * C;
-  hipLaunchKernelGGL(bn_fold_slots_kernel, dim3((n2c + 255) / 256), dim3(256), 0, st, slots, n2c);
+  hipLaunchKernelGGL(bn_fold_slots_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, slots, C);
   DTC_LAUNCH_CHECK();
   return 0;
 }

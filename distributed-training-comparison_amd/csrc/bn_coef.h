@@ -1,5 +1,5 @@
 // BN coefficient helpers shared by the BN kernels (bn.hip) and the kernels that fuse a BN step into
-// their prologue (stem.hip): the fixed-order fold of a BN's DTC_STAT_SLOTS fp64 partial-sum slots and the
+// their prologue (stem.hip): the fold of a BN's DTC_STAT_SLOTS fixed-point partial-sum slots (common.h) and the
 // backward coefficients computed from it.
 #pragma once
 #include "common.h"
@@ -22,51 +22,44 @@ __device__ __forceinline__ void lds_barrier() {
 // on both sides are branch-free (clamped addresses): a load inside a divergent region is waited for
 // at the region's end, which would drain every load issued before it.
 struct SlotFold {
-  double a[DTC_STAT_SLOTS / 4], b[DTC_STAT_SLOTS / 4];  // this thread's 8 slots of (sum, second sum)
-  float g = 0.f, h = 0.f, mu = 0.f;                    // t < 64: gamma and invstd / beta, mean
+  int64_t w[DTC_STAT_SLOTS];  // this thread's word (statistic, hi / lo) of its channel in every slot
+  int64_t flag = 0;           // the accumulator's non-finite flag (common.h)
+  float g = 0.f, h = 0.f, mu = 0.f;  // t < 64: gamma and invstd / beta, mean
 };
 
-// thread t: channel cg + t%64, slots 8*(t/64) .. +7 (needs 256 threads)
-__device__ __forceinline__ void fold_issue(const double* __restrict__ st, int C, int cg, SlotFold& f) {
-  const int t = threadIdx.x, cl = t & 63, g = t >> 6;
+// thread t: channel cg + t%64, word t/64 (0 / 1: first statistic hi / lo, 2 / 3: second) of every slot
+// (needs 256 threads)
+__device__ __forceinline__ void fold_issue(const int64_t* __restrict__ st, int C, int cg, SlotFold& f) {
+  const int t = threadIdx.x, cl = t & 63, wd = t >> 6;
 #pragma unroll
-  for (int j = 0; j < DTC_STAT_SLOTS / 4; ++j) {
-    const size_t k = (size_t)(g * (DTC_STAT_SLOTS / 4) + j);
-    f.a[j] = st[k * 2 * C + cg + cl];
-    f.b[j] = st[k * 2 * C + C + cg + cl];
-  }
+  for (int k = 0; k < DTC_STAT_SLOTS; ++k) f.w[k] = st[stat_word(k, wd >> 1, wd & 1, C) + cg + cl];
+  f.flag = st[0];
 }
 
-// fixed-order fold: each group of 64 threads adds its 8 slots, then thread t < 64 adds the 4 groups
-__device__ __forceinline__ void fold_sums(const SlotFold& f, double* part, double& s, double& q) {
-  const int t = threadIdx.x, cl = t & 63, g = t >> 6;
-  double a = 0.0, b = 0.0;
+// exact integer sums over the slots (any order gives the same bits), then thread t < 64 forms its
+// channel's two totals; part: 256 words of LDS
+__device__ __forceinline__ void fold_sums(const SlotFold& f, int64_t* part, double& s, double& q) {
+  const int t = threadIdx.x;
+  int64_t a = 0;
 #pragma unroll
-  for (int j = 0; j < DTC_STAT_SLOTS / 4; ++j) {
-    a += f.a[j];
-    b += f.b[j];
-  }
-  part[(g * 2 + 0) * 64 + cl] = a;
-  part[(g * 2 + 1) * 64 + cl] = b;
+  for (int k = 0; k < DTC_STAT_SLOTS; ++k) a += f.w[k];
+  part[t] = a;
   lds_barrier();
   s = q = 0.0;
   if (t < 64) {
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      s += part[(gg * 2 + 0) * 64 + t];
-      q += part[(gg * 2 + 1) * 64 + t];
-    }
+    s = stat_total(part[t], part[64 + t], f.flag);
+    q = stat_total(part[128 + t], part[192 + t], f.flag);
   }
 }
 
-__device__ __forceinline__ void fa_slot_sums(const double* __restrict__ st, int C, int cg, double* part, double& s,
+__device__ __forceinline__ void fa_slot_sums(const int64_t* __restrict__ st, int C, int cg, int64_t* part, double& s,
                                              double& q) {
   SlotFold f;
   fold_issue(st, C, cg, f);
   fold_sums(f, part, s, q);
 }
 
-// backward: dx = A*dz + B*x + Cc with the coefficients computed per workgroup from the fp64 slots of
+// backward: dx = A*dz + B*x + Cc with the coefficients computed per workgroup from the slots of
 // sum(dz), sum(dz*xhat); the first pixel block writes dgamma / dbeta (x gscale).
 __device__ __forceinline__ void fold_issue_bwd(const BnBwdArgs& A, int C, int cg, SlotFold& f) {
   fold_issue(A.acc, C, cg, f);
@@ -76,7 +69,7 @@ __device__ __forceinline__ void fold_issue_bwd(const BnBwdArgs& A, int C, int cg
   f.mu = A.mean[c];
 }
 
-__device__ __forceinline__ void fa_bwd_coef_from(const BnBwdArgs& A, const SlotFold& f, int C, int cg, double* part,
+__device__ __forceinline__ void fa_bwd_coef_from(const BnBwdArgs& A, const SlotFold& f, int C, int cg, int64_t* part,
                                                  float* ca, float* cb, float* cc) {
   double sd, sx;
   fold_sums(f, part, sd, sx);
@@ -98,7 +91,7 @@ __device__ __forceinline__ void fa_bwd_coef_from(const BnBwdArgs& A, const SlotF
   lds_barrier();
 }
 
-__device__ __forceinline__ void fa_bwd_coef(const BnBwdArgs& A, int C, int cg, double* part, float* ca, float* cb,
+__device__ __forceinline__ void fa_bwd_coef(const BnBwdArgs& A, int C, int cg, int64_t* part, float* ca, float* cb,
                                             float* cc) {
   SlotFold f;
   fold_issue_bwd(A, C, cg, f);
@@ -114,7 +107,7 @@ __device__ __forceinline__ void fold_issue_fwd(const BnFwdArgs& A, int C, int cg
   f.h = A.beta[c];
 }
 
-__device__ __forceinline__ void fa_fwd_coef_from(const BnFwdArgs& A, const SlotFold& f, int C, int cg, double* part,
+__device__ __forceinline__ void fa_fwd_coef_from(const BnFwdArgs& A, const SlotFold& f, int C, int cg, int64_t* part,
                                                  float* sc, float* sh) {
   double s, q;
   fold_sums(f, part, s, q);
@@ -143,7 +136,7 @@ __device__ __forceinline__ void fa_fwd_coef_from(const BnFwdArgs& A, const SlotF
   lds_barrier();
 }
 
-__device__ __forceinline__ void fa_fwd_coef(const BnFwdArgs& A, int C, int cg, double* part, float* sc, float* sh) {
+__device__ __forceinline__ void fa_fwd_coef(const BnFwdArgs& A, int C, int cg, int64_t* part, float* sc, float* sh) {
   SlotFold f;
   fold_issue_fwd(A, C, cg, f);
   fa_fwd_coef_from(A, f, C, cg, part, sc, sh);

@@ -16,11 +16,11 @@ struct BnbArgs {
   const u16* x1 = nullptr;  // input of the (first) BN: the conv output it normalised
   const float* mean1 = nullptr;
   const float* invstd1 = nullptr;
-  double* acc1 = nullptr;  // [SLOTS][2][C]: sum dz, sum dz * xhat
+  int64_t* acc1 = nullptr;  // [SLOTS][2][C]: sum dz, sum dz * xhat
   const u16* x2 = nullptr;  // second BN sharing dz (projection shortcut) or null
   const float* mean2 = nullptr;
   const float* invstd2 = nullptr;
-  double* acc2 = nullptr;
+  int64_t* acc2 = nullptr;
 };
 
 __host__ __device__ __forceinline__ bool bnb_on(const BnbArgs& a) { return a.ym != nullptr || a.mb != nullptr; }

@@ -201,16 +201,18 @@ int dtc_install_crash_handler(void) {
 size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass) {
   if (!desc_ok(d) || pass < 0 || pass > 2) return 0;
   const size_t slab = plan_conv(shape_of(d), pass).slab_bytes;
-  // split-K: + the arrival counters of the in-kernel reduction at the workspace's end
-  return slab > 0 ? slab + (size_t)DTC_TICKS * 4 : slab;
+  // FWD / DGRAD split-K: + the arrival counters of the in-kernel reduction at the workspace's end (+ room to
+  // align them to 256 B, so a workspace of exactly this size always holds both)
+  return slab > 0 && pass != 2 ? slab + (size_t)DTC_TICKS * 4 + 256 : slab;
 }
 
 // FWD / DGRAD workspace: [split-K slab][DTC_TICKS u32 arrival counters] when it holds both (the counters of
 // the in-kernel reduction are zeroed on the call's stream first; the workspace is scratch between calls),
-// else the whole of it is slab and a split-K plan reduces in a separate launch.
+// else the whole of it is slab and a split-K plan reduces in a separate launch. Nothing is carved out (and
+// nothing zeroed) when the plan has no slab or the in-kernel reduction is off (option splitk_ink).
 static unsigned* ws_ticks(size_t slab, void* ws, size_t& ws_bytes, hipStream_t st) {
   const size_t tb = (size_t)DTC_TICKS * 4;
-  if (ws == nullptr || slab == 0 || ws_bytes < slab + tb) return nullptr;
+  if (ws == nullptr || slab == 0 || ws_bytes < slab + tb || option_get(OPT_SPLITK_INK) == 0) return nullptr;
   const uintptr_t end = ((uintptr_t)ws + ws_bytes - tb) & ~(uintptr_t)255;
   if (end < (uintptr_t)ws + slab) return nullptr;
   if (hipMemsetAsync((void*)end, 0, tb, st) != hipSuccess) return nullptr;
@@ -221,7 +223,7 @@ static unsigned* op_ticks(const dtc_conv_desc* d, int pass, void* ws, size_t& ws
   return ws_ticks(plan_conv(shape_of(d), pass).slab_bytes, ws, ws_bytes, st);
 }
 
-int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, void* ws,
+int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t* stats, void* ws,
                    size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && w && y, "dtc_conv2d_fwd: null argument");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_fwd: unsupported convolution descriptor");
@@ -229,8 +231,8 @@ int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w,
   GUARD(return conv_fwd(shape_of(d), x, w, y, stats, (float*)ws, ws ? ws_bytes : 0, S(stream), nullptr, tick);)
 }
 
-int dtc_conv2d_fwd_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats,
-                      const uint16_t* wsc, uint16_t* ysc, double* stats_sc, void* stream) {
+int dtc_conv2d_fwd_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t* stats,
+                      const uint16_t* wsc, uint16_t* ysc, int64_t* stats_sc, void* stream) {
   DTC_CHECK_ARG(d && x && w && y && wsc && ysc, "dtc_conv2d_fwd_sc: null argument");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_fwd_sc: unsupported convolution descriptor");
   const ConvShape s = shape_of(d);
@@ -250,8 +252,8 @@ int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t*
 
 int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
                         const uint16_t* res, const uint16_t* ymask, const uint16_t* x1, const float* mean1,
-                        const float* invstd1, double* acc1, const uint16_t* x2, const float* mean2,
-                        const float* invstd2, double* acc2, void* ws, size_t ws_bytes, void* stream) {
+                        const float* invstd1, int64_t* acc1, const uint16_t* x2, const float* mean2,
+                        const float* invstd2, int64_t* acc2, void* ws, size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && dy && w && dx && ymask && x1 && mean1 && invstd1 && acc1, "dtc_conv2d_dgrad_bn: null argument");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_dgrad_bn: unsupported convolution descriptor");
   DTC_CHECK_ARG(!x2 || (mean2 && invstd2 && acc2), "dtc_conv2d_dgrad_bn: second BN arguments");
@@ -275,8 +277,7 @@ int dtc_conv2d_wgrad(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* 
                      size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && dy && dw && ws, "dtc_conv2d_wgrad: null argument (workspace is required)");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_wgrad: unsupported convolution descriptor");
-  unsigned* tick = op_ticks(d, CONV_WGRAD, ws, ws_bytes, S(stream));
-  GUARD(return conv_wgrad(shape_of(d), x, dy, dw, 0, 0, scale, (float*)ws, ws_bytes, S(stream), nullptr, tick);)
+  GUARD(return conv_wgrad(shape_of(d), x, dy, dw, 0, 0, scale, (float*)ws, ws_bytes, S(stream));)
 }
 
 size_t dtc_conv2d_wgrad_sc_workspace_size(const dtc_conv_desc* d) {
@@ -289,15 +290,13 @@ int dtc_conv2d_wgrad_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_
                         float* dw_sc, float scale, void* ws, size_t ws_bytes, void* stream) {
   DTC_CHECK_ARG(d && x && dy && dsc && dw && dw_sc, "dtc_conv2d_wgrad_sc: null argument");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_wgrad_sc: unsupported convolution descriptor");
-  unsigned* tick = ws_ticks(conv_wgrad_s2_slab_bytes(shape_of(d)), ws, ws_bytes, S(stream));
-  GUARD(return conv_wgrad_s2(shape_of(d), x, dy, dsc, dw, dw_sc, scale, (float*)ws, ws ? ws_bytes : 0, S(stream), nullptr,
-                             tick);)
+  GUARD(return conv_wgrad_s2(shape_of(d), x, dy, dsc, dw, dw_sc, scale, (float*)ws, ws ? ws_bytes : 0, S(stream));)
 }
 
 size_t dtc_conv2d_wgrad_batch_workspace_size(const dtc_conv_desc* d, int n) {
   if (!desc_ok(d) || n < 1 || n > DTC_WG_BATCH) return 0;
   const ConvShape s = shape_of(d);
-  return wgrad_halo_splits(s, n) > 0 ? conv_wgrad_batch_slab_bytes(s, n) + (size_t)DTC_TICKS * 4 : 0;
+  return wgrad_halo_splits(s, n) > 0 ? conv_wgrad_batch_slab_bytes(s, n) : 0;
 }
 
 int dtc_conv2d_wgrad_batch(const dtc_conv_desc* d, int n, const uint16_t* const* x, const uint16_t* const* dy,
@@ -305,11 +304,26 @@ int dtc_conv2d_wgrad_batch(const dtc_conv_desc* d, int n, const uint16_t* const*
   DTC_CHECK_ARG(d && x && dy && dw && ws && n >= 1 && n <= DTC_WG_BATCH, "dtc_conv2d_wgrad_batch: bad argument");
   DTC_CHECK_ARG(desc_ok(d), "dtc_conv2d_wgrad_batch: unsupported convolution descriptor");
   for (int i = 0; i < n; ++i) DTC_CHECK_ARG(x[i] && dy[i] && dw[i], "dtc_conv2d_wgrad_batch: null problem %d", i);
-  unsigned* tick = ws_ticks(conv_wgrad_batch_slab_bytes(shape_of(d), n), ws, ws_bytes, S(stream));
-  GUARD(return conv_wgrad_batch(shape_of(d), n, x, dy, dw, scale, (float*)ws, ws_bytes, S(stream), nullptr, tick);)
+  GUARD(return conv_wgrad_batch(shape_of(d), n, x, dy, dw, scale, (float*)ws, ws_bytes, S(stream));)
 }
 
-int dtc_bn_fwd_finalize(double* stats, int c, int64_t count, const float* gamma, const float* beta,
+size_t dtc_bn_stat_words(int c) { return c > 0 ? DTC_STAT_WORDS(c) : 0; }
+
+int dtc_bn_stat_totals(const int64_t* w, int c, double* totals) {
+  DTC_CHECK_ARG(w && totals && c > 0, "dtc_bn_stat_totals: bad args");
+  for (int j = 0; j < 2; ++j)
+    for (int ch = 0; ch < c; ++ch) {
+      int64_t hi = 0, lo = 0;
+      for (int k = 0; k < DTC_STAT_SLOTS; ++k) {
+        hi += w[stat_word(k, j, 0, c) + ch];
+        lo += w[stat_word(k, j, 1, c) + ch];
+      }
+      totals[(size_t)j * c + ch] = stat_total(hi, lo, w[0]);
+    }
+  return 0;
+}
+
+int dtc_bn_fwd_finalize(int64_t* stats, int c, int64_t count, const float* gamma, const float* beta,
                         float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, float* mean,
                         float* invstd, float* scale, float* shift, void* stream) {
   return bn_fwd_finalize(stats, c, count, gamma, beta, running_mean, running_var, nbt, momentum, eps, mean, invstd,
@@ -328,11 +342,11 @@ int dtc_bn_apply_dual_relu(const uint16_t* x, const float* scale, const float* s
   return bn_apply_dual_relu(x, scale, shift, x2, scale2, shift2, y, m, c, S(stream));
 }
 int dtc_bn_bwd_reduce(const uint16_t* dy, const uint16_t* ymask, const uint16_t* x1, const float* mean1,
-                      const float* invstd1, double* acc1, const uint16_t* x2, const float* mean2, const float* invstd2,
-                      double* acc2, uint16_t* dz, int64_t m, int c, void* stream) {
+                      const float* invstd1, int64_t* acc1, const uint16_t* x2, const float* mean2, const float* invstd2,
+                      int64_t* acc2, uint16_t* dz, int64_t m, int c, void* stream) {
   return bn_bwd_reduce(dy, ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, m, c, S(stream));
 }
-int dtc_bn_bwd_finalize(double* acc, int c, int64_t count, const float* gamma, const float* mean, const float* invstd,
+int dtc_bn_bwd_finalize(int64_t* acc, int c, int64_t count, const float* gamma, const float* mean, const float* invstd,
                         float gscale, float* dgamma, float* dbeta, float* coef, void* stream) {
   return bn_bwd_finalize(acc, c, count, gamma, mean, invstd, gscale, dgamma, dbeta, coef, S(stream));
 }
@@ -347,7 +361,7 @@ int dtc_stem_im2col(const float* x, uint16_t* cols, int n, int h, int w, void* s
 int dtc_stem_pack_weight(const uint16_t* w27, uint16_t* w64, int k, void* stream) {
   return stem_pack_weight(w27, w64, k, S(stream));
 }
-int dtc_stem_fwd(const float* x_nchw, const uint16_t* w27, uint16_t* y, double* stats, int n, int h, int w,
+int dtc_stem_fwd(const float* x_nchw, const uint16_t* w27, uint16_t* y, int64_t* stats, int n, int h, int w,
                  void* stream) {
   GUARD(return stem_fwd(x_nchw, w27, y, stats, n, h, w, S(stream));)
 }

@@ -17,7 +17,6 @@
 #include "comm.h"
 #include "common.h"
 #include "kernels.h"
-#include "kernels.h"
 
 namespace dtc {
 
@@ -117,7 +116,7 @@ static int group_issue(ThreadGroup* g) {  // called with g->mu held by the last 
 static int group_collective(Comm* c, int kind, void* buf, size_t count, int dtype, int root, hipStream_t after,
                             hipStream_t waiter) {
   ThreadGroup* g = c->grp;
-  DTC_CHECK_ARG(kind != GK_ALLREDUCE || dtype == 0 || dtype == 3, "thread group: SUM of fp32 / fp64 only");
+  DTC_CHECK_ARG(kind != GK_ALLREDUCE || dtype == 0 || dtype == 2 || dtype == 3, "thread group: SUM of fp32 / int64 / fp64 only");
   DTC_HIP(hipEventRecord(c->ready, after));
   hipEvent_t res = nullptr;
   {
@@ -264,10 +263,13 @@ void comm_log_clear(Comm* c) {
   if (c) c->log.clear();
 }
 
-// the loopback collective: buf *= factor (fp32 / fp64 only) on `st`
+// the loopback collective: buf *= factor (fp32 / fp64; int64 buffers -- BN statistics -- by the integer
+// factor) on `st`
 static int loopback_reduce(Comm* c, void* buf, size_t count, int dtype, hipStream_t st, bool async) {
-  DTC_CHECK_ARG(dtype == 0 || dtype == 3, "loopback communicator: fp32 / fp64 buffers only");
+  DTC_CHECK_ARG(dtype == 0 || dtype == 2 || dtype == 3, "loopback communicator: fp32 / int64 / fp64 buffers only");
+  DTC_CHECK_ARG(dtype != 2 || c->factor == (float)(int64_t)c->factor, "loopback communicator: int64 needs an integer factor");
   c->log.push_back(CommLogEntry{(uint64_t)(uintptr_t)buf, (uint64_t)count, async ? 1 : 0});
+  if (dtype == 2) return scale_i64(reinterpret_cast<int64_t*>(buf), (int64_t)count, (int64_t)c->factor, st);
   return dtype == 0 ? scale_f32(reinterpret_cast<float*>(buf), (int64_t)count, c->factor, st)
                     : scale_f64(reinterpret_cast<double*>(buf), (int64_t)count, (double)c->factor, st);
 }

@@ -172,10 +172,57 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Number of fp64 accumulator slots per statistics buffer: producers spread their
-// atomics over slots (blockIdx & (SLOTS-1)) so that thousands of workgroups do not
-// contend on the same 1 KB; the finalize kernels sum the slots in a fixed order.
-#define DTC_STAT_SLOTS 32
+// ---------------------------------------------------------------- BN statistic accumulators
+// A BN's batch sums (sum x, sum x^2 in the forward; sum dz, sum dz * xhat in the backward) are built from
+// one fp32 partial per producing workgroup and channel. They are accumulated EXACTLY, in integer fixed
+// point: a partial v is split into hi = floor(v * 2^8) and lo = floor(frac(v * 2^8) * 2^44) and both are
+// added with int64 atomics into one of DTC_STAT_SLOTS slots (blockIdx.x mod slots: spreads the atomic
+// contention). Integer addition is associative, so the totals -- and every BN coefficient computed from
+// them -- do not depend on the order in which the workgroups' adds arrive: the training step is
+// bit-reproducible run to run, as the reference's cudnn.deterministic = True asks (src/ddp/utils.py:12-13).
+// (Rounds 1-5 added fp64 partials with fp64 atomics: a sum that rounds depends on the arrival order.)
+// Bits of v below 2^-52 are dropped (deterministically; fp64 atomics kept 53 bits of the running total). A
+// partial that is not finite or not below 2^40 in magnitude is not added: it sets the header's flag word,
+// and every consumer then produces NaN coefficients (the AMP GradScaler skips such a step, as an fp16
+// overflow makes the reference's GradScaler skip it). Range: totals below 2^55, at most 2^15 partials per
+// slot and channel (2^18 per BN) -- batch 512 at 224x224 makes ~2^17.
+// Layout per BN, int64 words: [DTC_STAT_HDR header, word 0 = flag][DTC_STAT_SLOTS][2 stats][2 words: hi, lo][C]
+#ifndef DTC_STAT_SLOTS  // (overridable at build time for A/B builds)
+#define DTC_STAT_SLOTS 8  // 16: +4.5% BN family time (the apply kernels' slot-fold loads), 32: +12%; 4: the same
+#endif                     // BN time, conv epilogues slower (atomic contention) -- round 6, profiles/r06c_lab_slots.txt
+#ifndef DTC_STAT_HDR
+#define DTC_STAT_HDR 16  // one 128-B line: keeps every (slot, statistic, word) row line-aligned
+#endif
+#define DTC_STAT_WORDS(C) ((size_t)DTC_STAT_HDR + (size_t)DTC_STAT_SLOTS * 4 * (size_t)(C))
+
+// word (slot k, statistic j, part w) of channel 0
+__host__ __device__ __forceinline__ size_t stat_word(int k, int j, int w, int C) {
+  return (size_t)DTC_STAT_HDR + ((size_t)k * 4 + j * 2 + w) * (size_t)C;
+}
+
+__device__ __forceinline__ void stat_add1(int64_t* __restrict__ base, size_t o, int C, float v) {
+  const double d = (double)v * 256.0;
+  if (fabs(d) < 0x1p48) {  // false for NaN / inf too
+    const double h = floor(d);
+    __hip_atomic_fetch_add(base + o, (int64_t)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(base + o + C, (int64_t)((d - h) * 0x1p44), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_fetch_or(base, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// this workgroup's partials (s, q) of channel c into slot blockIdx.x mod DTC_STAT_SLOTS
+__device__ __forceinline__ void stat_add(int64_t* __restrict__ base, int C, int c, float s, float q) {
+  const int k = blockIdx.x & (DTC_STAT_SLOTS - 1);
+  stat_add1(base, stat_word(k, 0, 0, C) + c, C, s);
+  stat_add1(base, stat_word(k, 1, 0, C) + c, C, q);
+}
+
+// total of one statistic from its summed hi / lo words (exact int64 sums over the slots) and the flag
+__host__ __device__ __forceinline__ double stat_total(int64_t hi, int64_t lo, int64_t flag) {
+  if (flag != 0) return __builtin_nan("");
+  return (double)(hi + (lo >> 44)) * 0x1p-8 + (double)(lo & ((1ll << 44) - 1)) * 0x1p-52;
+}
 // conv call-timing slot (u64): start cell l at [DTC_PROF_LINE * l], end cell l at
 // [DTC_PROF_LINE * (DTC_PROF_LINES + l)], l < DTC_PROF_LINES (one 128-B line per cell)
 #define DTC_PROF_LINE 16

@@ -36,7 +36,7 @@ struct C64Params {
   const u16* w;    // KRSC [64][3][3][64]
   u16* out;        // NHWC, 64 channels
   const u16* res;  // DGRAD residual or null
-  double* stats;   // FWD BN statistics [SLOTS][2][64] or null
+  int64_t* stats;   // FWD BN statistics [SLOTS][2][64] or null
   int N, H, W;
   uint32_t src_bytes, out_bytes;
   int rows, imgs, hb, nh, tiles_y, ntiles;
@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   if (k > 0) epilogue(accp, opp, tilep, true);
 
   if constexpr (FWD) {
-    double* const sacc = p.stats;
+    int64_t* const sacc = p.stats;
     if (sacc != nullptr) {  // per-channel sums of this workgroup -> fp64 slot (once per workgroup)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __syncthreads();
@@ -397,9 +397,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
           s += red[(w * 64 + threadIdx.x) * 2 + 0];
           q += red[(w * 64 + threadIdx.x) * 2 + 1];
         }
-        double* st = sacc + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * 64;
-        unsafeAtomicAdd(st + threadIdx.x, (double)s);
-        unsafeAtomicAdd(st + 64 + threadIdx.x, (double)q);
+        stat_add(sacc, 64, threadIdx.x, s, q);
       }
     }
   }
@@ -445,7 +443,7 @@ static bool c64_classic_ok(const ConvShape& s) {
   return nh <= C64_HCAP && M % 256 == 0 && M * 128 < (1ll << 31);
 }
 
-int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, double* stats,
+int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, int64_t* stats,
              hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(conv_c64_ok(s) && (mode == CONV_FWD || mode == CONV_DGRAD), "conv_c64: unsupported shape");
   C64Params p{};

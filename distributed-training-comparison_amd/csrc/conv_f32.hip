@@ -30,7 +30,7 @@ struct F32ConvParams {
   const float* src1;  // FWD w, DGRAD w, WGRAD dy
   float* out;         // FWD y, DGRAD dx, WGRAD slab [split][K][RSC]
   const float* res;   // DGRAD residual (optional)
-  double* stats;      // FWD BN statistics slots (optional)
+  int64_t* stats;      // FWD BN statistics slots (optional)
   int N, H, W, C, K, R, S, P, Q, stride, pad;
   int M;      // GEMM rows
   int NC;     // GEMM cols
@@ -241,9 +241,7 @@ __global__ void __launch_bounds__(256) conv_f32_kernel(const F32ConvParams p) {
         }
         __syncthreads();
         if (t < F32_BN && n0 + t < p.NC) {
-          double* st = p.stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * p.NC;
-          unsafeAtomicAdd(st + n0 + t, (double)(red[0][0][t] + red[1][0][t]));
-          unsafeAtomicAdd(st + p.NC + n0 + t, (double)(red[0][1][t] + red[1][1][t]));
+          stat_add(p.stats, p.NC, n0 + t, red[0][0][t] + red[1][0][t], red[0][1][t] + red[1][1][t]);
         }
       }
     }
@@ -346,7 +344,7 @@ size_t f32_conv_workspace(const ConvShape& s, int mode) {
 }
 
 int conv_f32(const ConvShape& s, int mode, const float* a, const float* b, float* out, const float* res,
-             double* stats, float* dw_ld_or_null, int dw_cols, int dw_ld, float scale, float* slab,
+             int64_t* stats, float* dw_ld_or_null, int dw_cols, int dw_ld, float scale, float* slab,
              size_t slab_bytes, hipStream_t st, u64* ts) {
   F32ConvParams p{};
   DTC_TRY(f32_fill(p, s));

@@ -51,7 +51,7 @@ struct HConvParams {
   const u16* w;    // KRSC [K][3][3][C] (C = conv input channels)
   u16* out;        // NHWC, Cout channels
   const u16* res;  // DGRAD: residual added in the epilogue (NHWC, Cout) or null
-  double* stats;   // FWD: BN statistics [SLOTS][2][Cout] or null
+  int64_t* stats;   // FWD: BN statistics [SLOTS][2][Cout] or null
   float* slab;     // split-K: fp32 partial tiles [split][M][Cout]
   // split-K reduced IN the kernel (option splitk_ink): per output tile an arrival counter (zero between
   // launches: the last arriver resets it); the workgroup whose agent-scope add returns splits - 1 sums the
@@ -84,7 +84,7 @@ struct HConvParams {
   // centre tap's B fragments accumulates the shortcut output tile (one read of x, one launch)
   const u16* wsc;  // [Cout][C]
   u16* out2;
-  double* stats2;
+  int64_t* stats2;
   // general tile geometry (GEN kernels, stride 1; option halo_gen): a tile is grs rows x gseg columns of one
   // image in BN slots (slot l < grs * gseg: row l / gseg, column l % gseg; the rest padded: read any halo
   // row, stored nowhere), its halo (grs + 2) x (gseg + 2) pixels addressed from a 64-bit per-tile base --
@@ -447,7 +447,11 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
     // partial is stored write-through (sc1) and every storing wave drains (vmcnt 0) before the workgroup
     // barrier; one lane then adds to the tile's arrival counter (agent scope, returning); the workgroup
     // whose add returns splits - 1 reads the other partials with sc1 loads (L2-served, never a stale L1
-    // line). No workgroup waits for another: the others exit.
+    // line). No workgroup waits for another: the others exit. Compiler ordering: the stores sit above an
+    // asm vmcnt(0) with a memory clobber and a __syncthreads (a workgroup acq_rel fence to the compiler), the
+    // partial loads below two more __syncthreads, so neither can move across the arrival add. No agent-scope
+    // release / acquire fence: on gfx950 it lowers to buffer_wbl2 / buffer_inv of the XCD's L2,
+    // ~1.7-6.5 us per workgroup (the guide's price table) -- the sc1 form above needs neither.
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.slab, 0, 0x7ffffff0, 0x00020000);
     const int nsplit = (int)gridDim.y;
     uint32_t eoff[FM][FN];  // byte offset of each fragment's 4 channels within one split's plane
@@ -540,7 +544,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   static_assert(FM % 2 == 0, "fragment pairs");
   if constexpr (MODE == 0) {
     float* red = (float*)smem;  // [WC][BM][2]
-    auto epi_fwd = [&](f32x4 (&A)[SC ? FM : 1][SC ? FN : 1], f32x4 (&B)[FM][FN], bool second, u16* outp, double* stp) {
+    auto epi_fwd = [&](f32x4 (&A)[SC ? FM : 1][SC ? FN : 1], f32x4 (&B)[FM][FN], bool second, u16* outp, int64_t* stp) {
       const bool want_stats = stp != nullptr;
       float s4[FM][4], q4[FM][4];
 #pragma unroll
@@ -600,9 +604,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
             s += red[(w * BM + threadIdx.x) * 2 + 0];
             q += red[(w * BM + threadIdx.x) * 2 + 1];
           }
-          double* st = stp + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * p.Cout;
-          unsafeAtomicAdd(st + a0 + threadIdx.x, (double)s);
-          unsafeAtomicAdd(st + p.Cout + a0 + threadIdx.x, (double)q);
+          stat_add(stp, p.Cout, a0 + threadIdx.x, s, q);
         }
       }
     };
@@ -908,8 +910,8 @@ static int launch_halo_s2(const HConvParams& p, int cfg, dim3 grid, hipStream_t 
 }
 
 static int conv_halo_general(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
-                             const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
-                             const u16* wsc, u16* out2, double* stats2) {
+                             const u16* res, int64_t* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
+                             const u16* wsc, u16* out2, int64_t* stats2) {
   DTC_CHECK_ARG(hp.cfg == 0 || hp.cfg == 2 || hp.cfg == kFirstS2Cfg, "conv_halo: general geometry configuration");
   const HaloCfg& c = kHaloCfgs[hp.cfg];
   const int ST = c.st;
@@ -960,8 +962,8 @@ extern "C" int dtc_probe_phase_buffer(void* buf) {  // diagnostic builds only (t
 #endif
 
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
-              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
-              const u16* wsc, u16* out2, double* stats2, unsigned* tick) {
+              const u16* res, int64_t* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts,
+              const u16* wsc, u16* out2, int64_t* stats2, unsigned* tick) {
   DTC_CHECK_ARG(hp.cfg >= 0 && hp.cfg < kNumHaloCfgs && (mode == CONV_FWD || mode == CONV_DGRAD),
                 "conv_halo: unsupported configuration");
   const HaloCfg& c = kHaloCfgs[hp.cfg];

@@ -33,7 +33,7 @@ struct IGemmParams {
   u16* out;         // bf16 output (non-slab epilogue): FWD y (NPQK), DGRAD dx (NHWC)
   float* slab;      // fp32 split-K partials
   const u16* res;   // DGRAD: optional residual added in the epilogue
-  double* stats;    // FWD: optional per-channel (sum, sumsq) accumulators [SLOTS][2][K]
+  int64_t* stats;    // FWD: optional per-channel (sum, sumsq) accumulators [SLOTS][2][K]
   int N, H, W, C, K, R, S, P, Q, stride, pad;
   int M;            // GEMM pixel extent: FWD/WGRAD N*P*Q, DGRAD N*H*W
   int RSC;
@@ -55,7 +55,7 @@ struct IGemmParams {
   // W_sc's chunk beside W's and run a second set of MFMAs on the same im2col fragments.
   const u16* src1b;  // W_sc [K][C]
   u16* out2;         // shortcut output (NPQK)
-  double* stats2;    // its BN statistic slots
+  int64_t* stats2;    // its BN statistic slots
   int kt_c0, kt_c1;
   // DGRAD classes, shortcut fused (sc_kt > 0): the 1x1 stride-2 shortcut's input gradient is nonzero only
   // at the (even, even) pixels, where it is dsc[u][v] . W_sc -- a 1x1 GEMM on the class-(0, 0) grid with
@@ -477,7 +477,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
     }
   } else if constexpr (MODE == MODE_FWD) {
     float* red = (float*)smem;  // [WC][BM][2]
-    auto epi = [&](const f32x4 (&A)[FM][FN], u16* out, double* stats) {
+    auto epi = [&](const f32x4 (&A)[FM][FN], u16* out, int64_t* stats) {
     const bool want_stats = (stats != nullptr);
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
@@ -528,9 +528,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
           s += red[(w * BM + threadIdx.x) * 2 + 0];
           q += red[(w * BM + threadIdx.x) * 2 + 1];
         }
-        double* st = stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * p.K;
-        unsafeAtomicAdd(st + a0 + threadIdx.x, (double)s);
-        unsafeAtomicAdd(st + p.K + a0 + threadIdx.x, (double)q);
+        stat_add(stats, p.K, a0 + threadIdx.x, s, q);
       }
     }
     };
@@ -578,7 +576,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(const IGemmParams p) {
 // out may alias res: each element is read and then written by the same thread.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int splits,
                                                             int M, int Nc, u16* out, const u16* res,
-                                                            double* __restrict__ stats, int rows_per_block,
+                                                            int64_t* __restrict__ stats, int rows_per_block,
                                                             u64* ts) {
   __shared__ float red[256 * 16];
   const int tpr = Nc >> 3;           // threads per row (8 channels each)
@@ -659,7 +657,6 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
       red[t * 16 + 8 + k] = q[k];
     }
     __syncthreads();
-    const size_t slot = (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * Nc;
     for (int c = t; c < Nc; c += 256) {
       const int gg = c >> 3, k = c & 7;
       float a = 0.f, b = 0.f;
@@ -667,8 +664,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
         a += red[(r2 * tpr + gg) * 16 + k];
         b += red[(r2 * tpr + gg) * 16 + 8 + k];
       }
-      unsafeAtomicAdd(stats + slot + c, (double)a);
-      unsafeAtomicAdd(stats + slot + Nc + c, (double)b);
+      stat_add(stats, Nc, c, a, b);
     }
   }
   stamp_end(ts);
@@ -680,6 +676,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 // loads in flight), then combine through LDS in a fixed order (deterministic).
 struct WgOuts {
   float* dw[DTC_WG_BATCH];
+  int ld[DTC_WG_BATCH];  // > 0: this problem's own row length (its slab plane is K x ld, its output dense K x ld)
 };
 template <int SG>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K,
@@ -688,6 +685,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   // batched launches: blockIdx.y = problem (its own slab region and output)
   slab += blockIdx.y * prob_stride;
   float* __restrict__ grad = outs.dw[blockIdx.y];
+  if (outs.ld[blockIdx.y] > 0) ncols = ld_out = ld_in = outs.ld[blockIdx.y];
   constexpr int OPB = 256 / SG;  // outputs (float4) per block
   __shared__ f32x4 red[256];
   const size_t plane = (size_t)K * ld_in;
@@ -830,7 +828,7 @@ ConvPlan plan_conv(const ConvShape& s, int mode) {
   return pl;
 }
 
-int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
+int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, int64_t* stats, float* slab,
              size_t slab_bytes, hipStream_t st, u64* ts, unsigned* tick) {
   if (conv_c64_ok(s)) return conv_c64(s, CONV_FWD, x, w, y, nullptr, stats, st, ts);
   {
@@ -885,8 +883,8 @@ bool conv_fwd_sc_ok(const ConvShape& s, const ConvShape& sc) {
   return pl.bm != 64 && lvl >= 3;
 }
 
-int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16* w, u16* y, double* stats,
-                const u16* wsc, u16* ysc, double* stats_sc, hipStream_t st, u64* ts) {
+int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16* w, u16* y, int64_t* stats,
+                const u16* wsc, u16* ysc, int64_t* stats_sc, hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(conv_fwd_sc_ok(s, sc) && x && w && y && wsc && ysc, "conv_fwd_sc: unsupported shapes");
   {
     const HaloPlan hp = conv_halo_plan(s, CONV_FWD);
@@ -1040,10 +1038,10 @@ static int launch_wgrad_reduce(const float* slab, int splits, int K, int RSC, in
 }
 
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
-               float* slab, size_t slab_bytes, hipStream_t st, u64* ts, unsigned* tick) {
+               float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
   if (wgrad_s2_splits(s) > 0 && (dw_cols <= 0 || dw_cols == 9 * s.C) && (dw_ld <= 0 || dw_ld == 9 * s.C) &&
       slab_bytes >= conv_wgrad_s2_slab_bytes(s))
-    return conv_wgrad_s2(s, x, dy, nullptr, dw, nullptr, scale, slab, slab_bytes, st, ts, tick);
+    return conv_wgrad_s2(s, x, dy, nullptr, dw, nullptr, scale, slab, slab_bytes, st, ts);
   IGemmParams p{};
   p.ts = ts;
   DTC_TRY(fill_common(p, s));
@@ -1064,8 +1062,8 @@ int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int d
   int splits = pl.splits;
   if (pl.bm == 576 && slab_bytes >= pl.slab_bytes) {
     const bool whole = (dw_cols <= 0 || dw_cols == p.RSC) && (dw_ld <= 0 || dw_ld == p.RSC);
-    DTC_TRY(conv_wgrad_halo(s, 1, &x, &dy, slab, pl.splits, &splits, st, ts, whole ? &dw : nullptr, scale, tick));
-    if (splits == 0) return 0;  // one split or reduced in the kernel: the halo kernel wrote dw itself
+    DTC_TRY(conv_wgrad_halo(s, 1, &x, &dy, slab, pl.splits, &splits, st, ts, whole ? &dw : nullptr, scale));
+    if (splits == 0) return 0;  // one split: the halo kernel wrote dw itself
   } else {
     if (pl.bm == 576) pl = ConvPlan{64, 64, 1, ceil_div(p.M, 64), 0};  // workspace too small for the halo plan
     p.num_kt = pl.num_kt;
@@ -1092,25 +1090,39 @@ int wgrad_reduce_to(const float* slab, int splits, int K, int RSC, int ncols, in
   return launch_wgrad_reduce(slab, splits, K, RSC, ncols, ldo, scale, outs, 1, 0, st, ts);
 }
 
+// two dense reductions in one launch: slab[splits][K][ld0] -> dw0 and (slab + stride)[splits][K][ld1] -> dw1
+// (a stride-2 conv1's taps and its fused shortcut's; blockIdx.y = which, grid sized by the larger)
+int wgrad_reduce_pair(const float* slab, int splits, int K, int ld0, float* dw0, size_t stride, int ld1, float* dw1,
+                      float scale, hipStream_t st, u64* ts) {
+  DTC_CHECK_ARG(slab && dw0 && dw1 && splits > 0 && K > 0 && ld0 % 4 == 0 && ld1 % 4 == 0 && ld1 <= ld0,
+                "wgrad_reduce_pair: bad args");
+  WgOuts outs{};
+  outs.dw[0] = dw0;
+  outs.ld[0] = ld0;
+  outs.dw[1] = dw1;
+  outs.ld[1] = ld1;
+  return launch_wgrad_reduce(slab, splits, K, ld0, ld0, ld0, scale, outs, 2, stride, st, ts);
+}
+
 size_t conv_wgrad_batch_slab_bytes(const ConvShape& s, int nprob) {
   return (size_t)nprob * wgrad_halo_splits(s, nprob) * s.K * s.R * s.S * s.C * 4;
 }
 
 int conv_wgrad_batch(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* const* dw,
-                     float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts, unsigned* tick) {
+                     float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
   const int hs = wgrad_halo_splits(s, nprob);
   if (hs <= 0 || slab == nullptr || slab_bytes < conv_wgrad_batch_slab_bytes(s, nprob))
     return set_error(DTC_EINVAL, "conv_wgrad_batch: no halo plan for %d problems or slab too small", nprob);
   int splits = hs;
-  DTC_TRY(conv_wgrad_halo(s, nprob, x, dy, slab, hs, &splits, st, ts, dw, scale, tick));
-  if (splits == 0) return 0;  // one split or reduced in the kernel: the halo kernel wrote dw itself
+  DTC_TRY(conv_wgrad_halo(s, nprob, x, dy, slab, hs, &splits, st, ts, dw, scale));
+  if (splits == 0) return 0;  // one split: the halo kernel wrote dw itself
   const int RSC = s.R * s.S * s.C;
   WgOuts outs{};
   for (int i = 0; i < nprob; ++i) outs.dw[i] = dw[i];
   return launch_wgrad_reduce(slab, splits, s.K, RSC, RSC, RSC, scale, outs, nprob, (size_t)splits * s.K * RSC, st, ts);
 }
 
-int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
+int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, int64_t* stats,
                   hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(Nc % 8 == 0 && Nc <= 2048, "splitk_reduce: channels %d", Nc);
   const int tpr = Nc / 8;

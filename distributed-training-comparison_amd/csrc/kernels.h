@@ -47,8 +47,6 @@ namespace dtc {
   X(HALO_S2, halo_s2, 1)                /* stride-2 3x3 FWD on the column-split halo kernel */                \
   X(WGRAD_S2, wgrad_s2, 1)              /* stride-2 wgrad (+ shortcut) on the halo kernel: 0 off, 1 all, 2 GEN */ \
   X(WGRAD_S2_WGS, wgrad_s2_wgs, 128)    /* stride-2 halo wgrad: target workgroups (split-K slab = wgs x tile) */ \
-  X(WGRAD_KSPLIT, wgrad_ksplit, 2)      /* wgrad_halo: 2 pipelined fragment reads, 0 compiler-scheduled reads */ \
-  X(WGRAD_RING, wgrad_ring, 4)          /* wgrad_halo LDS ring stages: 4, or 3 (room for a main-stream workgroup) */ \
   X(C64_WGS, c64_wgs, 256)              /* conv_c64 (layer1) persistent grid size */                          \
   X(WGRAD_HALO_L1, wgrad_halo_l1, 0)    /* wgrad_halo target for the one-tile (layer1) geometry (0: wgrad_halo) */ \
   X(DGRAD_SCF, dgrad_scf, 1)            /* shortcut dgrad fused into conv1's parity-class dgrad */            \
@@ -64,8 +62,6 @@ namespace dtc {
   X(SPLITK_INK, splitk_ink, 1)          /* conv split-K summed by the last workgroup per tile (no reduce launch) */ \
   X(COMM_PRIO, comm_prio, 0)            /* (communicator creation) its own stream: 0 normal, 1 most urgent */ \
   X(COMM_TAIL_INLINE, comm_tail_inline, 1) /* the last bucket's all-reduce on the compute stream (no fork / join) */ \
-  X(WGRAD_INK, wgrad_ink, 0)            /* wgrad split-K summed by the last workgroup per tile: 1 stride-2, 2 all */ \
-  X(WGRAD_INK_MAX, wgrad_ink_max, 8)    /* ... for launches of at most this many splits (else a reduce launch) */ \
   X(DGRAD_S2H, dgrad_s2h, 1)            /* stride-2 3x3 dgrad (+ shortcut) as a halo sub-pixel conv: 1 K <= 256, 2 all */ \
   X(HALO_SMALL, halo_small, 1)          /* halo FWD/DGRAD: 64x64 double-buffered tiles where they give <= 512 workgroups */
 
@@ -93,19 +89,19 @@ struct ConvPlan {
 ConvPlan plan_conv(const ConvShape& s, int mode);
 
 // y = conv(x, w) (bf16 NHWC out); optional BN statistics of the bf16 output into
-// stats[SLOTS][2][K] (sum, sum of squares; fp64, accumulated).
+// stats (sum, sum of squares; exact fixed-point accumulators, DTC_STAT_WORDS(K) int64: common.h).
 // `ts` (optional, every conv launcher): a DTC_PROF_SLOT_U64 slot receiving the entry times of the
 // first workgroups and every workgroup's exit time in s_memrealtime ticks (graph-safe per-call timing).
 // tick (optional): >= DTC_TICKS zeroed u32 arrival counters reserved for the launch stream (the executor's
 // workspace: one set per stream); with it a split-K conv reduces its slab inside the kernel (the last
 // workgroup of each output tile), else a separate reduction launch does. The counters are left zero.
 #define DTC_TICKS 8192
-int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, double* stats, float* slab,
+int conv_fwd(const ConvShape& s, const u16* x, const u16* w, u16* y, int64_t* stats, float* slab,
              size_t slab_bytes, hipStream_t st, u64* ts = nullptr, unsigned* tick = nullptr);
 // 3x3 stride-2 conv and the 1x1 stride-2 projection shortcut of the same input in one launch
 bool conv_fwd_sc_ok(const ConvShape& s, const ConvShape& sc);
-int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16* w, u16* y, double* stats,
-                const u16* wsc, u16* ysc, double* stats_sc, hipStream_t st, u64* ts = nullptr);
+int conv_fwd_sc(const ConvShape& s, const ConvShape& sc, const u16* x, const u16* w, u16* y, int64_t* stats,
+                const u16* wsc, u16* ysc, int64_t* stats_sc, hipStream_t st, u64* ts = nullptr);
 // dx = conv_transpose(dy, w) (+ res), bf16 NHWC.
 // bnb (optional): dx is the gradient of a post-ReLU BN output; store dz = dx * [bnb->ym > 0] instead
 // and accumulate the BN-backward sums (bn_bwd_reduce's work) -- in the epilogue where the kernel
@@ -130,7 +126,7 @@ int conv_dgrad(const ConvShape& s, const u16* dy, const u16* w, u16* dx, const u
                int res_compact = 0, unsigned* tick = nullptr);
 // dw[k][0:dw_cols] (row stride dw_ld) = scale * sum_pixels dy (x) im2col(x); fp32
 int conv_wgrad(const ConvShape& s, const u16* x, const u16* dy, float* dw, int dw_cols, int dw_ld, float scale,
-               float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr, unsigned* tick = nullptr);
+               float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 // Halo-tiled WGRAD for 3x3 / stride 1 / pad 1 (wgrad_halo.hip): split count it would use for s
 // batched nprob at a time (0 = not applicable / disabled), and the launch writing
 // slab[nprob][used][K][9C] (reduce separately).
@@ -144,25 +140,20 @@ int wgrad_halo_splits(const ConvShape& s, int nprob = 1);
 int wgrad_s2_splits(const ConvShape& s);  // 0: no plan (option wgrad_s2 off or geometry)
 size_t conv_wgrad_s2_slab_bytes(const ConvShape& s);
 int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* dsc, float* dw, float* dw_sc,
-                  float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr,
-                  unsigned* tick = nullptr);
-// tick (optional, as conv_fwd's): with it a launch of at most wgrad_ink_max splits reduces in the kernel
-// (*used_splits = 0, dw written) instead of leaving the slab to a reduce launch
+                  float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* slab, int splits,
-                    int* used_splits, hipStream_t st, u64* ts, float* const* dw = nullptr, float scale = 1.f,
-                    unsigned* tick = nullptr);
+                    int* used_splits, hipStream_t st, u64* ts, float* const* dw = nullptr, float scale = 1.f);
 // nprob (<= DTC_WG_BATCH) independent weight gradients of one 3x3 stride-1 geometry in one halo
 // launch + one reduce launch: dw[i] = scale * wgrad(x[i], dy[i]). Returns DTC_EINVAL when the
 // geometry has no halo plan or the slab is too small (callers then issue them one by one).
 size_t conv_wgrad_batch_slab_bytes(const ConvShape& s, int nprob);
 int conv_wgrad_batch(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* const* dw,
-                     float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr,
-                     unsigned* tick = nullptr);
+                     float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr);
 // Halo-tiled 3x3 / stride 1 FWD and DGRAD (conv_halo.hip): configuration for the pass (-1: not
 // applicable), and the launch (FWD: stats optional; DGRAD: res optional).
 // Persistent 64-channel 3x3 stride-1 FWD / DGRAD (conv_c64.hip).
 bool conv_c64_ok(const ConvShape& s);
-int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, double* stats,
+int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* out, const u16* res, int64_t* stats,
              hipStream_t st, u64* ts);
 struct HaloPlan {
   int cfg, split;
@@ -171,10 +162,10 @@ struct HaloPlan {
 HaloPlan conv_halo_plan(const ConvShape& s, int mode);
 size_t conv_halo_slab_bytes(const ConvShape& s, int mode);  // fp32 split-K slab the plan needs
 int conv_halo(const ConvShape& s, int mode, const HaloPlan& hp, const u16* src, const u16* w, u16* out,
-              const u16* res, double* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr,
-              const u16* wsc = nullptr, u16* out2 = nullptr, double* stats2 = nullptr, unsigned* tick = nullptr);
+              const u16* res, int64_t* stats, float* slab, size_t slab_bytes, hipStream_t st, u64* ts = nullptr,
+              const u16* wsc = nullptr, u16* out2 = nullptr, int64_t* stats2 = nullptr, unsigned* tick = nullptr);
 // out = bf16(sum_s slab[s] (+ res)) (+ the BN statistics of out): the separate split-K reduction
-int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, double* stats,
+int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const u16* res, int64_t* stats,
                   hipStream_t st, u64* ts = nullptr);
 // per slot i of ts[n][DTC_PROF_SLOT_U64]: acc[i] += (max end - min start, 1) if stamped; cells reset
 int prof_accumulate(u64* ts, int n, u64* acc, hipStream_t st);
@@ -183,7 +174,7 @@ int prof_accumulate(u64* ts, int n, u64* acc, hipStream_t st);
 // FWD: out = y (+ BN stats into `stats`); DGRAD: out = dx (+ res); WGRAD: dw[k][0:dw_cols] (row stride
 // dw_ld; 0 = R*S*C) = scale * sum over pixels, via split-K slabs in `slab`. C and K multiples of 16.
 int conv_f32(const ConvShape& s, int mode, const float* a, const float* b, float* out, const float* res,
-             double* stats, float* dw, int dw_cols, int dw_ld, float scale, float* slab, size_t slab_bytes,
+             int64_t* stats, float* dw, int dw_cols, int dw_ld, float scale, float* slab, size_t slab_bytes,
              hipStream_t st, u64* ts = nullptr);
 size_t f32_conv_workspace(const ConvShape& s, int mode);  // fp32 slab bytes the pass wants
 int f32_stem_im2col(const float* x, float* cols, int N, int H, int W, hipStream_t st);  // [N*H*W][32]
@@ -191,7 +182,7 @@ int f32_stem_pack_weight(const float* w27, float* w32, int K, hipStream_t st);  
 
 // ------------------------------------------------------------------ batch norm (NHWC, C channels, M pixels)
 // forward finalize: mean/invstd/scale/shift from stats; running-stat update; stats re-zeroed.
-int bn_fwd_finalize(double* stats, int C, int64_t count, const float* gamma, const float* beta,
+int bn_fwd_finalize(int64_t* stats, int C, int64_t count, const float* gamma, const float* beta,
                     float* running_mean, float* running_var, int64_t* num_batches, float momentum, float eps,
                     float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
 // eval mode: scale/shift from running statistics (mean/invstd also written for reference)
@@ -215,11 +206,11 @@ int bn_apply_dual_relu(const float* x, const float* scale, const float* shift, c
                        const float* shift2, float* y, int64_t M, int C, hipStream_t st);
 int bn_apply(const float* x, const float* scale, const float* shift, float* y, int64_t M, int C, hipStream_t st);
 
-// Fused finalize + apply: the coefficients are computed by the consumer from the fp64 slots
+// Fused finalize + apply: the coefficients are computed by the consumer from the statistic slots
 // (bn.hip); the first pixel block writes the saved / running statistics (forward) or dgamma /
 // dbeta (backward). The slots must be zeroed before their producers run (executor: memset node).
 struct BnFwdArgs {
-  const double* stats = nullptr;  // [SLOTS][2][C] sum, sum of squares of the bf16 conv output
+  const int64_t* stats = nullptr;  // DTC_STAT_WORDS(C): sum, sum of squares of the bf16 conv output
   int64_t count = 0;
   const float* gamma = nullptr;
   const float* beta = nullptr;
@@ -231,7 +222,7 @@ struct BnFwdArgs {
   float* invstd = nullptr;
 };
 struct BnBwdArgs {
-  const double* acc = nullptr;  // [SLOTS][2][C] sum(dz), sum(dz*xhat)
+  const int64_t* acc = nullptr;  // [SLOTS][2][C] sum(dz), sum(dz*xhat)
   int64_t count = 0;
   const float* gamma = nullptr;
   const float* mean = nullptr;
@@ -248,15 +239,15 @@ int bn_fin_apply(int mode, const u16* x, const BnFwdArgs& a1, const u16* x2, con
 // stored by the reduction. Reduce: sums only (dy, bits, x read: 4.125 B/element); apply: dx (and
 // dzo = dz if non-null, may alias dy) from dy, bits, x. bn_mask_apply: dz alone (parity captures).
 int bn_bwd_reduce_mask(const u16* dy, const uint8_t* mbits, const u16* x1, const float* mean1, const float* invstd1,
-                       double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, int64_t M,
+                       int64_t* acc1, const u16* x2, const float* mean2, const float* invstd2, int64_t* acc2, int64_t M,
                        int C, hipStream_t st, u64* ts = nullptr);
 int bn_bwd_fin_apply_mask(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
                           const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st,
                           u64* ts = nullptr);
 int bn_mask_apply(const u16* dy, const uint8_t* mbits, u16* dz, int64_t M, int C, hipStream_t st);
 // One-launch mask-bit BN backward of a small tensor (bn_bwd_cg_ok: M <= 4096 pixels, 2048 dual): reduce +
-// coefficients + apply (dz, dx1 [, dx2], dgamma / dbeta x gscale) in one workgroup per 8 channels; the fp64
-// slots are unused
+// coefficients + apply (dz, dx1 [, dx2], dgamma / dbeta x gscale) in one workgroup per 8 channels; the
+// statistic slots are unused
 bool bn_bwd_cg_ok(int64_t M, int C, bool dual);
 int bn_bwd_cg(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, const BnBwdArgs& a1, u16* dx1,
               const u16* x2, const BnBwdArgs* a2, u16* dx2, int64_t M, int C, hipStream_t st, u64* ts = nullptr);
@@ -267,17 +258,17 @@ int bn_fin_apply(int mode, const float* x, const BnFwdArgs& a1, const float* x2,
 int bn_bwd_fin_apply(const float* dz, const float* x1, const BnBwdArgs& a1, float* dx1, const float* x2,
                      const BnBwdArgs* a2, float* dx2, int64_t M, int C, hipStream_t st);
 
-// slots [SLOTS][2][C] -> slot 0 holds the fixed-order sum over the slots, the others are zeroed
-int bn_fold_slots(double* slots, int C, hipStream_t st);
+// slot 0 <- the exact sum over the slots (lo carried into hi), the others zeroed (SyncBN's collective)
+int bn_fold_slots(int64_t* slots, int C, hipStream_t st);
 // backward: dz = dy * [y > 0] (mask optional); accumulates sum(dz), sum(dz*xhat1) [, sum(dz*xhat2)]
 int bn_bwd_reduce(const u16* dy, const u16* ymask, const u16* x1, const float* mean1, const float* invstd1,
-                  double* acc1, const u16* x2, const float* mean2, const float* invstd2, double* acc2, u16* dz,
+                  int64_t* acc1, const u16* x2, const float* mean2, const float* invstd2, int64_t* acc2, u16* dz,
                   int64_t M, int C, hipStream_t st);
 int bn_bwd_reduce(const float* dy, const float* ymask, const float* x1, const float* mean1, const float* invstd1,
-                  double* acc1, const float* x2, const float* mean2, const float* invstd2, double* acc2, float* dz,
+                  int64_t* acc1, const float* x2, const float* mean2, const float* invstd2, int64_t* acc2, float* dz,
                   int64_t M, int C, hipStream_t st);
 // dgamma/dbeta (scaled by gscale) into the flat grad buffer; apply coefficients coef[3][C]; acc re-zeroed.
-int bn_bwd_finalize(double* acc, int C, int64_t count, const float* gamma, const float* mean,
+int bn_bwd_finalize(int64_t* acc, int C, int64_t count, const float* gamma, const float* mean,
                     const float* invstd, float gscale, float* dgamma, float* dbeta, float* coef, hipStream_t st);
 // dx1 = A1*dz + B1*x1 + C1 [; dx2 = A2*dz + B2*x2 + C2]
 int bn_bwd_apply(const u16* dz, const u16* x1, const float* coef1, u16* dx1, const u16* x2, const float* coef2,
@@ -293,7 +284,7 @@ int stem_pack_weight(const u16* w27, u16* w64, int K, hipStream_t st);
 // Direct stem conv (stem.hip): im2col gathered into LDS per 256-pixel tile, one K=32 MFMA k-step.
 // fwd: y [N*H*W][64] bf16 (+ BN statistics of the bf16 output into stats[SLOTS][2][64] if non-null)
 // from fp32 NCHW x and the bf16 [64][27] weight; wgrad: dw27 [64][27] fp32 = scale * sum.
-int stem_fwd(const float* x, const u16* w27, u16* y, double* stats, int N, int H, int W, hipStream_t st,
+int stem_fwd(const float* x, const u16* w27, u16* y, int64_t* stats, int N, int H, int W, hipStream_t st,
              u64* ts = nullptr);
 size_t stem_wgrad_slab_bytes(int64_t M);
 int stem_wgrad(const float* x, const u16* dy, float* dw27, float scale, int N, int H, int W, float* slab,
@@ -305,6 +296,8 @@ int stem_wgrad_bn(const float* x, const u16* dy, const uint8_t* mbits, const u16
 // grad[k][0:ncols] (row stride ldo) = scale * sum_s slab[s][k][0:RSC] (igemm.hip's deterministic reduce)
 int wgrad_reduce_to(const float* slab, int splits, int K, int RSC, int ncols, int ldo, float scale, float* dw,
                     hipStream_t st, u64* ts = nullptr);
+int wgrad_reduce_pair(const float* slab, int splits, int K, int ld0, float* dw0, size_t stride, int ld1, float* dw1,
+                      float scale, hipStream_t st, u64* ts = nullptr);
 // feat[n][c] = bf16round(mean_hw act); logits[n][j] = feat . W[j] + b[j]
 int head_fwd(const u16* act, int N, int HW, int C, const u16* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st);
@@ -339,7 +332,9 @@ int copy_and_zero(const void* src, void* dst, size_t bytes, void* zp, size_t zby
 // x[i] *= f (loopback test communicator)
 int scale_f32(float* x, int64_t n, float f, hipStream_t st);
 int scale_f64(double* x, int64_t n, double f, hipStream_t st);
-// thread-group communicator: every rank's buffer <- the rank-ordered sum of all (fp32 dtype 0 / fp64 3)
+int scale_i64(int64_t* x, int64_t n, int64_t f, hipStream_t st);
+// thread-group communicator: every rank's buffer <- the rank-ordered sum of all (fp32 dtype 0 / int64 2 /
+// fp64 3)
 #define DTC_GROUP_MAX 8
 struct GroupPtrs { void* p[DTC_GROUP_MAX]; };
 int group_sum(const GroupPtrs& g, int w, int64_t n, int dtype, hipStream_t st);

@@ -118,6 +118,14 @@ int scale_f64(double* x, int64_t n, double f, hipStream_t st) {
   return 0;
 }
 
+int scale_i64(int64_t* x, int64_t n, int64_t f, hipStream_t st) {
+  DTC_CHECK_ARG(x && n > 0, "scale_i64: bad args");
+  const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(scale_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, x, n, f);
+  DTC_LAUNCH_CHECK();
+  return 0;
+}
+
 __global__ void amp_scale_kernel(const float* __restrict__ x, const float* __restrict__ scale, float* __restrict__ out,
                                  int64_t n) {
   const float s = *scale;
@@ -162,9 +170,10 @@ __global__ void group_sum_kernel(GroupPtrs g, int w, int64_t n) {
 }
 
 int group_sum(const GroupPtrs& g, int w, int64_t n, int dtype, hipStream_t st) {
-  DTC_CHECK_ARG(w >= 1 && w <= DTC_GROUP_MAX && n > 0 && (dtype == 0 || dtype == 3), "group_sum: bad args");
+  DTC_CHECK_ARG(w >= 1 && w <= DTC_GROUP_MAX && n > 0 && (dtype == 0 || dtype == 2 || dtype == 3), "group_sum: bad args");
   const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
   if (dtype == 0) hipLaunchKernelGGL(group_sum_kernel<float>, dim3(blocks), dim3(256), 0, st, g, w, n);
+  else if (dtype == 2) hipLaunchKernelGGL(group_sum_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, g, w, n);
   else hipLaunchKernelGGL(group_sum_kernel<double>, dim3(blocks), dim3(256), 0, st, g, w, n);
   DTC_LAUNCH_CHECK();
   return 0;

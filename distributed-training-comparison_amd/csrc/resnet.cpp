@@ -83,9 +83,8 @@ struct Net {
   bool stem_direct = false;  // planned with option stem_direct (bf16): stem.hip instead of im2col + GEMM
   size_t HEADWS = 0, HEADWS_bytes = 0;
   size_t DC0 = 0, SLABW = 0;  // stem conv-output gradient; split-K slab of the side-stream wgrads
-  size_t TICK = 0;            // split-K arrival counters: [0] compute stream, [1] weight-gradient stream
+  size_t TICK = 0;            // split-K arrival counters of the compute stream's convs (the only in-kernel split-K)
   unsigned* tick(int i) { return (unsigned*)(ws + TICK) + (size_t)i * DTC_TICKS; }
-  unsigned* tick_on(hipStream_t s) { return tick(s != nullptr && s == side_st ? 1 : 0); }  // the launch stream's set
   size_t BNERR = 0;           // int: set by a one-pass BN backward whose grid barrier timed out
   // backward weight gradients run on a side stream (option bwd_streams), overlapped with the
   // data-gradient / BN chain; forked after the conv-output gradient exists, joined at bucket points
@@ -137,6 +136,7 @@ struct Net {
     hipEvent_t bwd0 = nullptr, join_c = nullptr, join_d = nullptr, tail_a = nullptr, tail_b = nullptr;
     std::vector<hipEvent_t> b0, b1;  // per bucket
     bool join = false, tail = false;  // join_c / join_d, tail_a recorded (eager backward)
+    bool ok = false;                  // the backward succeeded and recorded tail_b (only these steps count)
     std::vector<bool> bucket;        // bucket i recorded
   };
   std::vector<CommTimes> ct;  // one per armed step
@@ -365,9 +365,9 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.PROF_TS = take((size_t)Net::PROF_SLOTS * DTC_PROF_SLOT_U64 * sizeof(u64));
   n.PROF_ACC = take((size_t)Net::PROF_SLOTS * 2 * sizeof(u64));
   n.stats_lo = off;  // forward statistics of every BN, then backward sums: both zeroed by the training forward
-  for (BNL* b : n.bns) b->stats = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
+  for (BNL* b : n.bns) b->stats = take(DTC_STAT_WORDS(b->C) * 8);
   n.acc_lo = off;
-  for (BNL* b : n.bns) b->acc = take((size_t)DTC_STAT_SLOTS * 2 * b->C * 8);
+  for (BNL* b : n.bns) b->acc = take(DTC_STAT_WORDS(b->C) * 8);
   n.BNERR = take(256);
   n.stats_hi = off;
   for (BNL* b : n.bns) {
@@ -399,7 +399,7 @@ static void plan_workspace(Net& n, float bucket_cap_mb) {
   n.slab_bytes = slab;
   n.SLAB = take(slab);
   n.SLABW = take(slab);
-  n.TICK = take((size_t)2 * DTC_TICKS * 4);  // zeroed at bind; every in-kernel split-K leaves its counters zero
+  n.TICK = take((size_t)DTC_TICKS * 4);  // zeroed at bind; every in-kernel split-K leaves its counters zero
   if (n.capture) {
     auto cap = [&](const std::string& nm, int h, int w, int c) {
       n.caps.push_back({nm, take((size_t)B * h * w * c * E), (int)B, h, w, c});
@@ -595,7 +595,7 @@ static int end_capture(Net& n, int body_rc, hipGraphExec_t* out) {
 // ------------------------------------------------------------------ forward / backward
 static int bn_finalize_fwd(Net& n, BNL& b, int64_t count, bool train, hipStream_t st) {
   if (train) {
-    return bn_fwd_finalize(n.at<double>(b.stats), b.C, count, n.pf(b.gidx), n.pf(b.bidx), n.bufs + b.rm_off,
+    return bn_fwd_finalize(n.at<int64_t>(b.stats), b.C, count, n.pf(b.gidx), n.pf(b.bidx), n.bufs + b.rm_off,
                            n.bufs + b.rv_off, n.nbt ? n.nbt + b.nbt : nullptr, 0.1f, 1e-5f, n.at<float>(b.mean),
                            n.at<float>(b.invstd), n.at<float>(b.scale), n.at<float>(b.shift), st);
   }
@@ -611,19 +611,20 @@ static bool bn_mask_on(const Net& n) {
   return !n.f32 && option_get(OPT_BN_MASK) != 0 && bn_fused();
 }
 
-// SUM all-reduce of one BN's fp64 partial-sum slots ([DTC_STAT_SLOTS][2][C]) on the compute
-// stream: the slots are first folded into slot 0 (fixed order; the others zeroed), so the collective
-// carries 2*C doubles, not SLOTS*2*C; every apply kernel folds the slots, so after this each rank
-// folds the global sums (torch SyncBatchNorm's all-gather of per-rank mean/invstd/count, as one
-// reduction; every rank's batch is the same size -- checked by the Python DDP wrapper).
+// SUM all-reduce of one BN's statistic accumulator (exact int64 fixed point, common.h) on the compute
+// stream: the slots are first folded into slot 0 (the others zeroed), so the collective carries the
+// header (the non-finite flag) and slot 0, DTC_STAT_HDR + 4*C words, not every slot; integer sums make
+// the global totals independent of the ranks' order too. Every apply kernel folds the slots, so after
+// this each rank folds the global sums (torch SyncBatchNorm's all-gather of per-rank mean/invstd/count,
+// as one reduction; every rank's batch is the same size -- checked by the Python DDP wrapper).
 static int sync_bn_sums(Net& n, size_t off, int C, hipStream_t st) {
-  DTC_TRY(bn_fold_slots(n.at<double>(off), C, st));
-  return comm_allreduce(n.sync, n.ws + off, (size_t)2 * C, 3, st);
+  DTC_TRY(bn_fold_slots(n.at<int64_t>(off), C, st));
+  return comm_allreduce(n.sync, n.ws + off, (size_t)DTC_STAT_HDR + (size_t)4 * C, 2, st);
 }
 
 static BnFwdArgs fwd_args(Net& n, BNL& b, int64_t count) {
   BnFwdArgs a;
-  a.stats = n.at<double>(b.stats);
+  a.stats = n.at<int64_t>(b.stats);
   a.count = count;
   a.gamma = n.pf(b.gidx);
   a.beta = n.pf(b.bidx);
@@ -683,13 +684,13 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
   if (train && !n.stem_direct) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));
   if (n.stem_direct) {  // stem.hip: taps gathered per tile from the fp32 input, one K=32 k-step
     PROF(0, 2.0 * M0 * 64 * 27,
-         stem_fwd(n.at<float>(n.XIN), n.wbf(n.stem.pidx), n.at<u16>(n.C0), train ? n.at<double>(n.bn0.stats) : nullptr,
+         stem_fwd(n.at<float>(n.XIN), n.wbf(n.stem.pidx), n.at<u16>(n.C0), train ? n.at<int64_t>(n.bn0.stats) : nullptr,
                   n.B, n.H, n.W, st, ts));
   } else {
     DTC_TRY(stem_pack_weight(n.wbf(n.stem.pidx), n.at<u16>(n.WSTEM), 64, st));
     PROF(0, 2.0 * M0 * 64 * 27,
          conv_fwd(n.stem.s, n.at<u16>(n.X0), n.at<u16>(n.WSTEM), n.at<u16>(n.C0),
-                  train ? n.at<double>(n.bn0.stats) : nullptr, n.at<float>(n.SLAB), n.slab_bytes, st, ts));
+                  train ? n.at<int64_t>(n.bn0.stats) : nullptr, n.at<float>(n.SLAB), n.slab_bytes, st, ts));
   }
   DTC_TRY(bn_act(n, 1, n.bn0, n.at<u16>(n.C0), nullptr, nullptr, n.at<u16>(n.A0), M0, train, st, n.MA0));
   const u16* in = n.at<u16>(n.A0);
@@ -701,21 +702,21 @@ static int forward_body(Net& n, float* logits, bool train, hipStream_t st) {
     const bool scf = b.proj && option_get(OPT_SC_FUSE) != 0 && conv_fwd_sc_ok(b.c1.s, b.sc.s);
     if (b.proj && !scf)  // the shortcut conv first
       PROF(0, conv_flops(b.sc.s),
-           conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr, slab,
+           conv_fwd(b.sc.s, in, n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<int64_t>(b.bsc.stats) : nullptr, slab,
                     n.slab_bytes, st, ts, n.tick(0)));
     if (scf) {
       PROF(0, conv_flops(b.c1.s) + conv_flops(b.sc.s),
-           conv_fwd_sc(b.c1.s, b.sc.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr,
-                       n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<double>(b.bsc.stats) : nullptr, st, ts));
+           conv_fwd_sc(b.c1.s, b.sc.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<int64_t>(b.b1.stats) : nullptr,
+                       n.wbf(b.sc.pidx), n.at<u16>(b.S), train ? n.at<int64_t>(b.bsc.stats) : nullptr, st, ts));
     } else {
       PROF(0, conv_flops(b.c1.s),
-           conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<double>(b.b1.stats) : nullptr, slab,
+           conv_fwd(b.c1.s, in, n.wbf(b.c1.pidx), n.at<u16>(b.C1), train ? n.at<int64_t>(b.b1.stats) : nullptr, slab,
                     n.slab_bytes, st, ts, n.tick(0)));
     }
     DTC_TRY(bn_act(n, 1, b.b1, n.at<u16>(b.C1), nullptr, nullptr, n.at<u16>(b.A1), M, train, st, b.MA1));
     PROF(0, conv_flops(b.c2.s),
          conv_fwd(b.c2.s, n.at<u16>(b.A1), n.wbf(b.c2.pidx), n.at<u16>(b.C2),
-                  train ? n.at<double>(b.b2.stats) : nullptr, slab, n.slab_bytes, st, ts, n.tick(0)));
+                  train ? n.at<int64_t>(b.b2.stats) : nullptr, slab, n.slab_bytes, st, ts, n.tick(0)));
     if (b.proj) {
       DTC_TRY(bn_act(n, 3, b.b2, n.at<u16>(b.C2), &b.bsc, n.at<u16>(b.S), n.at<u16>(b.OUT), M, train, st, b.MOUT));
     } else {
@@ -762,22 +763,22 @@ static int forward_body_f32(Net& n, float* logits, bool train, hipStream_t st) {
   if (train) DTC_TRY(zero_bytes(n.ws + n.stats_lo, n.stats_hi - n.stats_lo, st));  // + the backward sums
   PROF(0, 2.0 * M0 * 64 * 27,
        conv_f32(f32_stem_shape(n), CONV_FWD, n.at<float>(n.X0), n.at<float>(n.WSTEM), n.at<float>(n.C0), nullptr,
-                train ? n.at<double>(n.bn0.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
+                train ? n.at<int64_t>(n.bn0.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
   DTC_TRY(bn_act_f32(n, 1, n.bn0, n.at<float>(n.C0), nullptr, nullptr, n.at<float>(n.A0), M0, train, st));
   const float* in = n.at<float>(n.A0);
   for (auto& b : n.blocks) {
     const int64_t M = (int64_t)n.B * b.Hout * b.Wout;
     PROF(0, conv_flops(b.c1.s),
          conv_f32(b.c1.s, CONV_FWD, in, n.pf(b.c1.pidx), n.at<float>(b.C1), nullptr,
-                  train ? n.at<double>(b.b1.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
+                  train ? n.at<int64_t>(b.b1.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
     DTC_TRY(bn_act_f32(n, 1, b.b1, n.at<float>(b.C1), nullptr, nullptr, n.at<float>(b.A1), M, train, st));
     PROF(0, conv_flops(b.c2.s),
          conv_f32(b.c2.s, CONV_FWD, n.at<float>(b.A1), n.pf(b.c2.pidx), n.at<float>(b.C2), nullptr,
-                  train ? n.at<double>(b.b2.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
+                  train ? n.at<int64_t>(b.b2.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
     if (b.proj) {
       PROF(0, conv_flops(b.sc.s),
            conv_f32(b.sc.s, CONV_FWD, in, n.pf(b.sc.pidx), n.at<float>(b.S), nullptr,
-                    train ? n.at<double>(b.bsc.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
+                    train ? n.at<int64_t>(b.bsc.stats) : nullptr, nullptr, 0, 0, 0.f, slab, n.slab_bytes, st, ts));
       DTC_TRY(bn_act_f32(n, 3, b.b2, n.at<float>(b.C2), &b.bsc, n.at<float>(b.S), n.at<float>(b.OUT), M, train, st));
     } else {
       DTC_TRY(bn_act_f32(n, 2, b.b2, n.at<float>(b.C2), nullptr, in, n.at<float>(b.OUT), M, train, st));
@@ -815,9 +816,9 @@ static int backward_body_f32(Net& n, const float* dlogits, float gs, const BwdCt
     DTC_TRY(cap(n, cp + ".dy", G[0], st));
     // out = relu(bn2(c2) + shortcut): dz = dy * [out > 0] and the BN-backward sums of bn2 (+ bn_sc)
     DTC_TRY(bn_bwd_reduce(G[0], n.at<float>(b.OUT), n.at<float>(b.C2), n.at<float>(b.b2.mean),
-                          n.at<float>(b.b2.invstd), n.at<double>(b.b2.acc), b.proj ? n.at<float>(b.S) : nullptr,
+                          n.at<float>(b.b2.invstd), n.at<int64_t>(b.b2.acc), b.proj ? n.at<float>(b.S) : nullptr,
                           b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
-                          b.proj ? n.at<double>(b.bsc.acc) : nullptr, G[1], M, b.Cout, st));
+                          b.proj ? n.at<int64_t>(b.bsc.acc) : nullptr, G[1], M, b.Cout, st));
     float* dz2 = G[1];
     {
       if (n.sync) {
@@ -843,7 +844,7 @@ static int backward_body_f32(Net& n, const float* dlogits, float gs, const BwdCt
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
     // a1 = relu(bn1(c1)): dz1 = da1 * [a1 > 0] (in place) and bn1's sums
     DTC_TRY(bn_bwd_reduce(G[4], n.at<float>(b.A1), n.at<float>(b.C1), n.at<float>(b.b1.mean),
-                          n.at<float>(b.b1.invstd), n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, G[4],
+                          n.at<float>(b.b1.invstd), n.at<int64_t>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, G[4],
                           M, b.Cout, st));
     DTC_TRY(cap(n, cp + ".dz1", G[4], st));
     {
@@ -879,7 +880,7 @@ static int backward_body_f32(Net& n, const float* dlogits, float gs, const BwdCt
   const int64_t M0 = (int64_t)n.B * n.H * n.W;
   float* dc0 = n.at<float>(n.DC0);
   DTC_TRY(bn_bwd_reduce(G[0], n.at<float>(n.A0), n.at<float>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
-                        n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, G[1], M0, 64, st));
+                        n.at<int64_t>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, G[1], M0, 64, st));
   {
     if (n.sync) DTC_TRY(sync_bn_sums(n, n.bn0.acc, n.bn0.C, st));
     const float g0 = n.sync ? gs / (float)n.sync_world : gs;
@@ -1007,7 +1008,7 @@ static int cap(Net& n, const std::string& name, const void* src, hipStream_t st)
 
 static BnBwdArgs bwd_args(Net& n, BNL& b, int64_t count, float gs) {
   BnBwdArgs a;
-  a.acc = n.at<double>(b.acc);
+  a.acc = n.at<int64_t>(b.acc);
   a.count = count;
   a.gamma = n.pf(b.gidx);
   a.mean = n.at<float>(b.mean);
@@ -1065,10 +1066,10 @@ static int bn_bwd_coef_apply(Net& n, BNL& b1, const u16* dz, const u16* x1, u16*
     return bn_bwd_fin_apply(dz, x1, a1, dx1, x2, b2 ? &a2 : nullptr, dx2, M, b1.C, st);
   }
   DTC_CHECK_ARG(mbits == nullptr, "mask-bit BN backward needs the fused finalize");
-  DTC_TRY(bn_bwd_finalize(n.at<double>(b1.acc), b1.C, cnt, n.pf(b1.gidx), n.at<float>(b1.mean), n.at<float>(b1.invstd),
+  DTC_TRY(bn_bwd_finalize(n.at<int64_t>(b1.acc), b1.C, cnt, n.pf(b1.gidx), n.at<float>(b1.mean), n.at<float>(b1.invstd),
                           gs, n.gf(b1.gidx), n.gf(b1.bidx), n.at<float>(b1.coef), st));
   if (b2)
-    DTC_TRY(bn_bwd_finalize(n.at<double>(b2->acc), b2->C, cnt, n.pf(b2->gidx), n.at<float>(b2->mean),
+    DTC_TRY(bn_bwd_finalize(n.at<int64_t>(b2->acc), b2->C, cnt, n.pf(b2->gidx), n.at<float>(b2->mean),
                             n.at<float>(b2->invstd), gs, n.gf(b2->gidx), n.gf(b2->bidx), n.at<float>(b2->coef), st));
   return bn_bwd_apply(dz, x1, n.at<float>(b1.coef), dx1, x2, b2 ? n.at<float>(b2->coef) : nullptr, dx2, M, b1.C, st);
 }
@@ -1127,12 +1128,12 @@ static BnbArgs bnb_of(Net& n, size_t y, size_t x1, BNL& b1, size_t x2 = 0, BNL* 
   a.x1 = n.at<u16>(x1);
   a.mean1 = n.at<float>(b1.mean);
   a.invstd1 = n.at<float>(b1.invstd);
-  a.acc1 = n.at<double>(b1.acc);
+  a.acc1 = n.at<int64_t>(b1.acc);
   if (b2 != nullptr) {
     a.x2 = n.at<u16>(x2);
     a.mean2 = n.at<float>(b2->mean);
     a.invstd2 = n.at<float>(b2->invstd);
-    a.acc2 = n.at<double>(b2->acc);
+    a.acc2 = n.at<int64_t>(b2->acc);
   }
   return a;
 }
@@ -1160,11 +1161,11 @@ static int wg_flush(Net& n, WgQueue& q, float gs, float* slabw, hipStream_t sd) 
   q.count = 0;
   if (np == 1) {
     PROF(2, conv_flops(q.s),
-         conv_wgrad(q.s, q.x[0], q.dy[0], q.dw[0], 0, 0, gs, slabw, n.slab_bytes, sd, ts, n.tick_on(sd)));
+         conv_wgrad(q.s, q.x[0], q.dy[0], q.dw[0], 0, 0, gs, slabw, n.slab_bytes, sd, ts));
     return 0;
   }
   PROF(2, conv_flops(q.s) * np,
-       conv_wgrad_batch(q.s, np, q.x, q.dy, q.dw, gs, slabw, n.slab_bytes, sd, ts, n.tick_on(sd)));
+       conv_wgrad_batch(q.s, np, q.x, q.dy, q.dw, gs, slabw, n.slab_bytes, sd, ts));
   return 0;
 }
 static int fork_side(Net& n, hipStream_t st, hipStream_t* out);
@@ -1176,7 +1177,7 @@ static int wg_issue(Net& n, WgQueue& q, const ConvShape& s, const u16* x, const 
   const int bmax = wgrad_batch_max();
   if (bmax <= 1 || wgrad_halo_splits(s, 2) <= 0) {
     if (lazy) DTC_TRY(fork_side(n, st, &sd));
-    PROF(2, conv_flops(s), conv_wgrad(s, x, dy, dw, 0, 0, gs, slabw, n.slab_bytes, sd, ts, n.tick_on(sd)));
+    PROF(2, conv_flops(s), conv_wgrad(s, x, dy, dw, 0, 0, gs, slabw, n.slab_bytes, sd, ts));
     return 0;
   }
   if (q.count > 0 && !same_shape(q.s, s)) {
@@ -1251,9 +1252,9 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     } else {
       PROF(3, (double)M * b.Cout * (b.proj ? 6.125 : 4.125),
            bn_bwd_reduce_mask(G[0], mout, n.at<u16>(b.C2), n.at<float>(b.b2.mean), n.at<float>(b.b2.invstd),
-                              n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
+                              n.at<int64_t>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
                               b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
-                              b.proj ? n.at<double>(b.bsc.acc) : nullptr, M, b.Cout, st, ts));
+                              b.proj ? n.at<int64_t>(b.bsc.acc) : nullptr, M, b.Cout, st, ts));
       DTC_TRY(bn_bwd_coef_apply(n, b.b2, G[0], n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
                                 b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st, mout, b.proj ? nullptr : G[0]));
     }
@@ -1277,7 +1278,7 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     } else {
       PROF(3, (double)M * b.Cout * 4.125,
            bn_bwd_reduce_mask(G[4], ma1, n.at<u16>(b.C1), n.at<float>(b.b1.mean), n.at<float>(b.b1.invstd),
-                              n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, M, b.Cout, st, ts));
+                              n.at<int64_t>(b.b1.acc), nullptr, nullptr, nullptr, nullptr, M, b.Cout, st, ts));
       DTC_TRY(bn_bwd_coef_apply(n, b.b1, G[4], n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st, ma1));
     }
     DTC_TRY(cap(n, cp + ".dc1", dc1, st));
@@ -1288,15 +1289,14 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
                      b.sc.s.R == 1 && b.sc.s.stride == 2 && b.sc.s.C == b.c1.s.C && b.sc.s.K == b.c1.s.K;
     if (wsc) {
       PROF(2, conv_flops(b.c1.s) + conv_flops(b.sc.s),
-           conv_wgrad_s2(b.c1.s, in, dc1, dsc, n.gf(b.c1.pidx), n.gf(b.sc.pidx), gs, slabw, n.slab_bytes, sd, ts,
-                         n.tick_on(sd)));
+           conv_wgrad_s2(b.c1.s, in, dc1, dsc, n.gf(b.c1.pidx), n.gf(b.sc.pidx), gs, slabw, n.slab_bytes, sd, ts));
     } else {
       DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, st, lazy && !b.proj));
     }
     if (b.proj) {
       if (!wsc)
         PROF(2, conv_flops(b.sc.s),
-             conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts, n.tick_on(sd)));
+             conv_wgrad(b.sc.s, in, dsc, n.gf(b.sc.pidx), 0, 0, gs, slabw, n.slab_bytes, sd, ts));
       if (dscf) {
         PROF(1, conv_flops(b.c1.s) + conv_flops(b.sc.s),
              conv_dgrad_sc(b.c1.s, dc1, n.wbf(b.c1.pidx), G[0], dsc, n.wbf(b.sc.pidx), st, ts));
@@ -1328,7 +1328,7 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   if (n.stem_direct && !n.capture && !n.sync && bn_fused() && option_get(OPT_STEM_BN_FUSE) != 0) {
     PROF(3, (double)M0 * 64 * 4.125,
            bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
-                              n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
+                              n.at<int64_t>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
     if (option_get(OPT_FORK_LAZY) && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
     DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
     const BnBwdArgs a0 = bwd_args(n, n.bn0, M0, gs);
@@ -1349,7 +1349,7 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   }
   PROF(3, (double)M0 * 64 * 4.125,
        bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
-                          n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
+                          n.at<int64_t>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
   DTC_TRY(bn_bwd_coef_apply(n, n.bn0, G[0], n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st, m0));
   DTC_TRY(cap_masked(n, "grad.stem.dz", G[0], n.MA0, M0, 64, st));
   DTC_TRY(cap(n, "grad.stem.dc", dc0, st));
@@ -1407,9 +1407,9 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
     if (!dz_ready) {
       dz2 = G[1];
       DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(b.OUT), n.at<u16>(b.C2), n.at<float>(b.b2.mean),
-                            n.at<float>(b.b2.invstd), n.at<double>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
+                            n.at<float>(b.b2.invstd), n.at<int64_t>(b.b2.acc), b.proj ? n.at<u16>(b.S) : nullptr,
                             b.proj ? n.at<float>(b.bsc.mean) : nullptr, b.proj ? n.at<float>(b.bsc.invstd) : nullptr,
-                            b.proj ? n.at<double>(b.bsc.acc) : nullptr, G[1], M, b.Cout, st));
+                            b.proj ? n.at<int64_t>(b.bsc.acc) : nullptr, G[1], M, b.Cout, st));
     }
     DTC_TRY(bn_bwd_coef_apply(n, b.b2, dz2, n.at<u16>(b.C2), dc2, b.proj ? &b.bsc : nullptr,
                               b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st));
@@ -1428,7 +1428,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
     if (!fuse) {
       DTC_TRY(cap(n, cp + ".da1", G[4], st));
       DTC_TRY(bn_bwd_reduce(G[4], n.at<u16>(b.A1), n.at<u16>(b.C1), n.at<float>(b.b1.mean),
-                            n.at<float>(b.b1.invstd), n.at<double>(b.b1.acc), nullptr, nullptr, nullptr, nullptr,
+                            n.at<float>(b.b1.invstd), n.at<int64_t>(b.b1.acc), nullptr, nullptr, nullptr, nullptr,
                             G[4], M, b.Cout, st));
     }
     DTC_TRY(cap(n, cp + ".dz1", G[4], st));
@@ -1466,7 +1466,7 @@ static int backward_body(Net& n, const float* dlogits, float gs, const BwdCtx& c
   if (!dz_ready) {
     dz0 = G[1];
     DTC_TRY(bn_bwd_reduce(G[0], n.at<u16>(n.A0), n.at<u16>(n.C0), n.at<float>(n.bn0.mean),
-                          n.at<float>(n.bn0.invstd), n.at<double>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, G[1],
+                          n.at<float>(n.bn0.invstd), n.at<int64_t>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, G[1],
                           M0, 64, st));
   }
   DTC_TRY(bn_bwd_coef_apply(n, n.bn0, dz0, n.at<u16>(n.C0), dc0, nullptr, nullptr, nullptr, M0, gs, st));
@@ -1488,12 +1488,15 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
   if (comm && n.ct_left > 0 && n.ct_used < (int)n.ct.size()) {
     n.ct_cur = &n.ct[n.ct_used++];
     --n.ct_left;
-    n.ct_cur->join = n.ct_cur->tail = false;
+    n.ct_cur->join = n.ct_cur->tail = n.ct_cur->ok = false;
     n.ct_cur->bucket.assign(n.ct_cur->b0.size(), false);
     DTC_HIP(hipEventRecord(n.ct_cur->bwd0, st));
   }
   const int rc = backward_impl(n, dlogits, gs, comm, st);
-  if (rc == 0 && n.ct_cur) DTC_HIP(hipEventRecord(n.ct_cur->tail_b, st));  // after the Reducer's join
+  if (rc == 0 && n.ct_cur) {
+    DTC_HIP(hipEventRecord(n.ct_cur->tail_b, st));  // after the Reducer's join
+    n.ct_cur->ok = true;
+  }
   n.ct_cur = nullptr;
   return rc;
 }
@@ -1672,7 +1675,7 @@ int dtc_rn18_bind(dtc_net* net, void* workspace, float* params, float* grads, ui
   n.prof_acc = n.at<u64>(n.PROF_ACC);
   drop_graphs(n);  // captured launches hold the previous pointers
   DTC_HIP(hipMemsetAsync(n.ws + n.stats_lo, 0, n.stats_hi - n.stats_lo, (hipStream_t)stream));
-  DTC_HIP(hipMemsetAsync(n.ws + n.TICK, 0, (size_t)2 * DTC_TICKS * 4, (hipStream_t)stream));
+  DTC_HIP(hipMemsetAsync(n.ws + n.TICK, 0, (size_t)DTC_TICKS * 4, (hipStream_t)stream));
   return 0;
 }
 
@@ -1832,14 +1835,19 @@ int dtc_rn18_comm_timing_result(dtc_net* net, int max_buckets, double* bucket_us
     out = 1e3 * (double)ms;
     return 0;
   };
-  int recorded = 0, joined = 0;
+  int recorded = 0, joined = 0, tailed = 0;
   std::vector<int> bcount(nb, 0);
   for (int k = 0; k < n.ct_used; ++k) {
     Net::CommTimes& c = n.ct[k];
-    double tail = 0, bwd = 0;
-    if (c.tail) DTC_TRY(us(c.tail_a, c.tail_b, tail));  // (a replayed backward records no tail / join events)
+    if (!c.ok) continue;  // a backward that failed recorded no end event
+    double bwd = 0;
+    if (c.tail) {  // (a replayed backward records no tail / join events)
+      double tail = 0;
+      DTC_TRY(us(c.tail_a, c.tail_b, tail));
+      exposed_us[0] += tail;
+      ++tailed;
+    }
     DTC_TRY(us(c.bwd0, c.tail_b, bwd));
-    exposed_us[0] += tail;
     exposed_us[3] += bwd;
     if (c.join) {
       double j = 0;
@@ -1859,12 +1867,11 @@ int dtc_rn18_comm_timing_result(dtc_net* net, int max_buckets, double* bucket_us
     }
     ++recorded;
   }
-  if (recorded) {
-    exposed_us[0] /= recorded;
-    exposed_us[3] /= recorded;
-  }
+  // tail: the mean over the steps that recorded one, -1 when none did (replayed backwards: unavailable)
+  exposed_us[0] = tailed ? exposed_us[0] / tailed : -1.0;
+  if (recorded) exposed_us[3] /= recorded;
   if (joined) exposed_us[1] /= joined;
-  exposed_us[2] = exposed_us[0] + exposed_us[1];
+  exposed_us[2] = tailed ? exposed_us[0] + exposed_us[1] : -1.0;
   exposed_us[4] = joined;
   for (int i = 0; i < nb; ++i)
     if (bcount[i])

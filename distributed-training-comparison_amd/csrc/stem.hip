@@ -155,7 +155,7 @@ static StemGeom stem_geom(int N, int H, int W) {
 // lane; the staged input rows are capped at 8 KB (STEM_BN_CAP) so the LDS stays at four per CU.
 template <bool WL = false>
 __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restrict__ x, const u16* __restrict__ w27,
-                                                      u16* __restrict__ y, double* __restrict__ stats, const StemGeom G,
+                                                      u16* __restrict__ y, int64_t* __restrict__ stats, const StemGeom G,
                                                       u64* ts) {
   constexpr int CAP = WL ? 2048 : STEM_LDS_FLOATS;
   // cols (16 KB) + the staged input rows (20 KB; WL 8 KB); after the MFMAs the first 32 KB hold the
@@ -289,15 +289,13 @@ __global__ void __launch_bounds__(256, 4) stem_fwd_kernel(const float* __restric
         s += red[w][t][0];
         q += red[w][t][1];
       }
-      double* st = stats + (size_t)(blockIdx.x & (DTC_STAT_SLOTS - 1)) * 2 * 64;
-      unsafeAtomicAdd(st + t, (double)s);
-      unsafeAtomicAdd(st + 64 + t, (double)q);
+      stat_add(stats, 64, t, s, q);
     }
   }
   stamp_end(ts);
 }
 
-int stem_fwd(const float* x, const u16* w27, u16* y, double* stats, int N, int H, int W, hipStream_t st, u64* ts) {
+int stem_fwd(const float* x, const u16* w27, u16* y, int64_t* stats, int N, int H, int W, hipStream_t st, u64* ts) {
   DTC_CHECK_ARG(x && w27 && (y || stats) && N > 0 && H > 0 && W > 0, "stem_fwd: bad args");
   const int64_t M = (int64_t)N * H * W;
   DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_fwd: more than 2^31 pixels");
@@ -414,7 +412,7 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_bn_kernel(const float* __re
                                                              u64* ts) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * 32768];  // dc tile, col tile
   __shared__ float xt[CAP];
-  __shared__ double part[4 * 2 * 64];
+  __shared__ int64_t part[256];
   __shared__ float coef[3][64];
   char* const dyt = smem;
   char* const colt = smem + 32768;

@@ -54,12 +54,6 @@ struct HaloParams {
   const u16* dsc;
   float* slab_sc;  // [splits][K][C] (or, direct, dw_sc)
   float* dw_sc;
-  // split-K reduced in the kernel (option wgrad_ink, up to wgrad_ink_max splits): one arrival counter per
-  // (problem, tile), zero between launches; the workgroup whose agent-scope add returns splits - 1 sums every
-  // split's partial (sc1 loads, split order 0, 1, ..) and writes scale * sum into dws / dw_sc. Null: the
-  // separate wgrad_reduce launch does it.
-  unsigned* tick;
-  int nsplit;
   // general geometry (GEN kernels; stride 1, e.g. the 224x224 model's 224/112/56/28-wide rows): a step is
   // rs rows x seg columns of one image (rs * seg <= 64 real pixels; the remaining MFMA reduction slots of
   // the 64-pixel step carry zero dy), its halo (rs + 2) x (seg + 2) pixels; every step addresses x and dy
@@ -114,15 +108,14 @@ struct WgStage {
 
 // NS: pipeline stages in the LDS ring (2: wait for the next step's DMA at every step; 4: three
 // steps of DMA in flight, a counted s_waitcnt per step). NR: halo DMA rounds per step.
-// KL: fragment-read schedule of the wave layout (4 waves along the 576 rows x 2 along the 64 output channels,
-// each wave both 32-pixel halves of a step: 9 A + 2 B fragment reads per 18 MFMAs). 0: compiler-scheduled
-// reads; 2 (option wgrad_ksplit, default): software-pipelined reads. (The pixel-split layouts KL 1 / 3 --
-// each wave all 64 channels of one 32-pixel half, 41% fewer LDS reads per MFMA -- measured neutral in-step
-// and were removed in round 5; numbers in DESIGN.md.)
-template <int NS, int NR, int ST = 1, bool SC = false, bool GEN = false, int KL = 0, bool INK = false>
+// Wave layout: 4 waves along the 576 rows x 2 along the 64 output channels, each wave both 32-pixel halves
+// of a step (9 A + 2 B fragment reads per 18 MFMAs), the fragment reads software-pipelined (compute()).
+// (Removed variants, numbers in DESIGN.md: compiler-scheduled fragment reads -- option wgrad_ksplit=0, round 6;
+// the pixel-split layouts -- round 5; a three-stage ring -- option wgrad_ring=3, round 6; the split-K summed by
+// the last-arriving workgroup -- option wgrad_ink, round 6: a 64 x 576 fp32 tile per split made that one
+// workgroup's serial sum slower than a reduce launch.)
+template <int NS, int NR, int ST = 1, bool SC = false, bool GEN = false>
 __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
-  static_assert(KL == 0 || KL == 2, "wgrad_ksplit: 0 or 2");
-  constexpr bool PIPE = KL == 2;  // software-pipelined fragment reads
   typedef WgStage<NR, SC> SG;
   constexpr int PER = NR + 1 + (SC ? 1 : 0);  // LDS-DMA instructions per wave per stage (halo rounds + dy (+ dsc))
   static_assert(!SC || ST == 2, "shortcut fusion: stride 2");
@@ -296,58 +289,35 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
   };
   auto compute = [&](const char* sb) {
-    if constexpr (PIPE) {
-      // software-pipelined fragment reads (option wgrad_ksplit=2): both k-steps' B fragments first, then the 18
-      // A fragments through a three-deep register ring -- fragment f + 2 is read before the MFMAs of f, and
-      // scheduling fences keep the compiler from sinking the reads back next to their uses (without them
-      // each A fragment was read right before its two MFMAs and waited for: lgkmcnt(0) every 2 MFMAs)
-      bf16x8 bfr2[2][2], ar[3];
+    // software-pipelined fragment reads: both k-steps' B fragments first, then the 18 A fragments through a
+    // three-deep register ring -- fragment f + 2 is read before the MFMAs of f, and scheduling fences keep the
+    // compiler from sinking the reads back next to their uses (without them each A fragment was read right
+    // before its two MFMAs and waited for: lgkmcnt(0) every 2 MFMAs)
+    bf16x8 bfr2[2][2], ar[3];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bfr2[ks][j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
-      ar[0] = tr8(sb, aoff[0][0][0], aoff[0][0][1]);
-      ar[1] = tr8(sb, aoff[0][1][0], aoff[0][1][1]);
+      for (int j = 0; j < 2; ++j) bfr2[ks][j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
+    ar[0] = tr8(sb, aoff[0][0][0], aoff[0][0][1]);
+    ar[1] = tr8(sb, aoff[0][1][0], aoff[0][1][1]);
 #pragma unroll
-      for (int f = 0; f < 18; ++f) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (f + 2 < 18) ar[(f + 2) % 3] = tr8(sb, aoff[(f + 2) / 9][(f + 2) % 9][0], aoff[(f + 2) / 9][(f + 2) % 9][1]);
-        __builtin_amdgcn_sched_barrier(0);
+    for (int f = 0; f < 18; ++f) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (f + 2 < 18) ar[(f + 2) % 3] = tr8(sb, aoff[(f + 2) / 9][(f + 2) % 9][0], aoff[(f + 2) / 9][(f + 2) % 9][1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[f % 9][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[f % 3], bfr2[f / 9][j], acc[f % 9][j], 0, 0, 0);
-      }
-      if constexpr (SC) {  // the shortcut (stride 2): centre-tap A fragment x the dsc tile, per k-step
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const bf16x8 af = tr8(sb, aoff_sc[ks][0], aoff_sc[ks][1]);
-          bf16x8 bs[2];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) bs[j] = tr8(sb, boff[ks][j][0] + 8192, boff[ks][j][1] + 8192);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc_sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bs[j], acc_sc[j], 0, 0, 0);
-        }
-      }
-      return;
+      for (int j = 0; j < 2; ++j)
+        acc[f % 9][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[f % 3], bfr2[f / 9][j], acc[f % 9][j], 0, 0, 0);
     }
+    if constexpr (SC) {  // the shortcut (stride 2): centre-tap A fragment x the dsc tile, per k-step
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      bf16x8 bfr[NJ];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) bfr[j] = tr8(sb, boff[ks][j][0], boff[ks][j][1]);
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        const bf16x8 af = tr8(sb, aoff[ks][i][0], aoff[ks][i][1]);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
-      }
-      if constexpr (SC) {  // the shortcut: centre-tap A fragment x the dsc tile's B fragments
+      for (int ks = 0; ks < 2; ++ks) {
         const bf16x8 af = tr8(sb, aoff_sc[ks][0], aoff_sc[ks][1]);
+        bf16x8 bs[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const bf16x8 bs = tr8(sb, boff[ks][j][0] + 8192, boff[ks][j][1] + 8192);
-          acc_sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bs, acc_sc[j], 0, 0, 0);
-        }
+        for (int j = 0; j < 2; ++j) bs[j] = tr8(sb, boff[ks][j][0] + 8192, boff[ks][j][1] + 8192);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc_sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bs[j], acc_sc[j], 0, 0, 0);
       }
     }
   };
@@ -383,107 +353,6 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   float* const slab = p.direct ? uniform_ptr(z == 0 ? p.dws[0] : z == 1 ? p.dws[1] : z == 2 ? p.dws[2] : p.dws[3])
                                : p.slab + z * p.slab_stride + (size_t)split * p.K * RSC;
   const float osc = p.direct ? p.scale : 1.f;
-  if constexpr (INK) {  // (a template flag: the plain instances keep their register allocation)
-    // In-kernel split-K (the hand-off of conv_halo.hip: MI355X_MICROARCH.md "Valid forms" row 1): sc1 partial
-    // stores drained by every wave, one agent-scope add per workgroup; the last arriver reads all splits' sc1
-    // partials (its own included: its accumulators are dead after the stores) in split order, in groups of
-    // fragments so that every load of a group is in flight at once.
-    float* const base = p.slab + z * p.slab_stride;  // [splits][K][RSC]
-    const size_t plane = (size_t)p.K * RSC;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7ffffff0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsc_sc =
-        __builtin_amdgcn_make_buffer_rsrc(SC ? p.slab_sc : base, 0, 0x7ffffff0, 0x00020000);
-    // (the lane id through an opaque move: the offsets below are then computed here, after the loop, instead of
-    // being hoisted before it and held in 18 registers across the MFMA loop)
-    int ln;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
-    uint32_t foff[9][2];  // byte offset of each fragment within one split's [K][RSC] plane
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int row = wm * 144 + i * 16 + 4 * (ln >> 4);
-      const int rsc = (row >> 6) * p.C + c0 + (row & 63);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) foff[i][j] = (uint32_t)(((size_t)(k0 + wn * 32 + j * 16 + (ln & 15)) * RSC + rsc) * 4);
-    }
-    const uint32_t own = (uint32_t)((size_t)split * plane * 4);
-#pragma unroll
-    for (int i = 0; i < 9; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, own + foff[i][j], 0, 16);
-    uint32_t soff[2] = {0u, 0u};
-    const size_t plane_sc = (size_t)p.K * p.C;
-    if constexpr (SC) {
-      const int c = c0 + wm * 16 + 4 * (ln >> 4);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        soff[j] = (uint32_t)(((size_t)(k0 + wn * 32 + j * 16 + (ln & 15)) * p.C + c) * 4);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc_sc[j]), rsc_sc,
-                                               (uint32_t)(split * plane_sc * 4) + soff[j], 0, 16);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    unsigned* const flag = (unsigned*)smem;
-    const unsigned cid = z * gridDim.x + (unsigned)tile;
-    if (threadIdx.x == 0) {
-      const unsigned old = __hip_atomic_fetch_add(p.tick + cid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned last = old == (unsigned)(p.nsplit - 1) ? 1u : 0u;
-      if (last) __hip_atomic_store(p.tick + cid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *(volatile unsigned*)flag = last;
-    }
-    __syncthreads();
-    const unsigned last = *(volatile unsigned*)flag;
-    if (!last) {
-      stamp_end(p.ts);
-      return;
-    }
-    float* const dw = uniform_ptr(z == 0 ? p.dws[0] : z == 1 ? p.dws[1] : z == 2 ? p.dws[2] : p.dws[3]);
-    const int ns = p.nsplit;
-    // groups of 3 fragment rows (6 fragments): ns x 6 loads in flight, then sum in split order and store
-    constexpr int GR = 3;
-#pragma unroll
-    for (int i0 = 0; i0 < 9; i0 += GR) {
-      f32x4 sum[GR][2];
-#pragma unroll
-      for (int a = 0; a < GR; ++a) sum[a][0] = sum[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int s0 = 0; s0 < ns; s0 += 2) {  // two splits' loads at a time (12 in flight)
-        f32x4 part[2][GR][2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int a = 0; a < GR; ++a)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              part[u][a][j] = s0 + u < ns ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                rs, (uint32_t)((size_t)(s0 + u) * plane * 4) + foff[i0 + a][j], 0, 16))
-                                          : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int a = 0; a < GR; ++a)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              if (s0 + u < ns) sum[a][j] += part[u][a][j];
-      }
-#pragma unroll
-      for (int a = 0; a < GR; ++a)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) *(f32x4*)((char*)dw + foff[i0 + a][j]) = sum[a][j] * p.scale;
-    }
-    if constexpr (SC) {
-      f32x4 sum[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-      for (int sp = 0; sp < ns; ++sp)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          sum[j] += __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsc_sc, (uint32_t)(sp * plane_sc * 4) + soff[j], 0, 16));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) *(f32x4*)((char*)p.dw_sc + soff[j]) = sum[j] * p.scale;
-    }
-    stamp_end(p.ts);
-    return;
-  }
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int row = wm * 144 + i * 16 + 4 * (lane >> 4);
@@ -567,21 +436,8 @@ int wgrad_halo_splits(const ConvShape& s, int nprob) {
   return splits;
 }
 
-// option wgrad_ink: split-K summed in the kernel by the last workgroup of each tile, for launches of at most
-// wgrad_ink_max splits (the last arriver reads every split's partial tile: its latency grows with the split count)
-// (option wgrad_ink: 0 off (default); 1 the stride-2 (+ shortcut) launches only; 2 every launch. A wgrad tile is
-// 64 x 576 fp32 (147 KB per split), so the last arriver alone reads splits x 147 KB after every other split has
-// finished: the one stride-2 launch it applies to at batch 256 (layer4.0, 4 splits) took 54.4 us against 36.8 for
-// its plain twin + 2 reduce launches of ~6 us (serialized trace r05h); in-step 140.8k vs 140.5k img/s without it
-// (4 rounds, r05i: noise), and every launch 135.9k vs 137.4k (r05f))
-static bool wgrad_ink_ok(int used, unsigned* tick, unsigned ncount, bool s2) {
-  const int o = option_get(OPT_WGRAD_INK);
-  return tick != nullptr && used > 1 && (o == 2 || (o == 1 && s2)) && used <= option_get(OPT_WGRAD_INK_MAX) &&
-         ncount <= (unsigned)DTC_TICKS;
-}
-
 int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u16* const* dy, float* slab, int splits,
-                    int* used_splits, hipStream_t st, u64* ts, float* const* dw, float scale, unsigned* tick) {
+                    int* used_splits, hipStream_t st, u64* ts, float* const* dw, float scale) {
   WgGeom g;
   DTC_CHECK_ARG(wg_geometry(s, g) && splits > 0 && nprob >= 1 && nprob <= DTC_WG_BATCH,
                 "wgrad_halo: unsupported geometry");
@@ -620,25 +476,12 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   p.slab_stride = (size_t)used * s.K * 9 * s.C;
   p.direct = used == 1 && dw != nullptr && option_get(OPT_WGRAD_DIRECT) != 0;
   dim3 grid((s.C / 64) * (s.K / 64), used, nprob);
-  const int klay = option_get(OPT_WGRAD_KSPLIT);
-  const bool ink = !p.direct && dw != nullptr && klay == 2 && option_get(OPT_WGRAD_RING) != 3 &&
-                   wgrad_ink_ok(used, tick, grid.x * grid.z, false);
-  if (p.direct || ink)
+  if (p.direct)
     for (int i = 0; i < nprob; ++i) p.dws[i] = dw[i];
-  p.tick = ink ? tick : nullptr;
-  p.nsplit = used;
   p.scale = scale;
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
-  // 4-stage LDS ring (three steps of DMA in flight), compiler-scheduled fragment reads
-  const int kl = option_get(OPT_WGRAD_KSPLIT);
-  // option wgrad_ring=3: a three-stage LDS ring (96 / 72 KB instead of 128 / 96 KB), leaving room on the CU
-  // for a main-stream conv workgroup beside the weight-gradient one (pipelined layout only)
-  const bool ring3 = kl == 2 && option_get(OPT_WGRAD_RING) == 3;
-#define DTC_WGH(NR_, GEN_)                                                                                    \
-  if (ring3) hipLaunchKernelGGL((wgrad_halo_kernel<3, NR_, 1, false, GEN_, 2>), grid, dim3(512), 0, st, p);  \
-  else if (kl == 2 && ink) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 2, true>), grid, dim3(512), 0, st, p); \
-  else if (kl == 2) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 2>), grid, dim3(512), 0, st, p); \
-  else hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_, 0>), grid, dim3(512), 0, st, p)
+  // 4-stage LDS ring (three steps of DMA in flight)
+#define DTC_WGH(NR_, GEN_) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_>), grid, dim3(512), 0, st, p)
   if (g.gen) {  // general geometry
     if (nr <= 2) { DTC_WGH(2, true); }
     else { DTC_WGH(3, true); }
@@ -648,7 +491,7 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   }
 #undef DTC_WGH
   DTC_LAUNCH_CHECK();
-  *used_splits = p.direct || ink ? 0 : used;
+  *used_splits = p.direct ? 0 : used;
   return 0;
 }
 
@@ -737,7 +580,7 @@ size_t conv_wgrad_s2_slab_bytes(const ConvShape& s) {
 }
 
 int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* dsc, float* dw, float* dw_sc,
-                  float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts, unsigned* tick) {
+                  float scale, float* slab, size_t slab_bytes, hipStream_t st, u64* ts) {
   int rs = 0, imgs = 0, pitch = 0, hb = 0, nh = 0;
   const int splits = wgrad_s2_splits(s);
   bool gen = false;
@@ -791,15 +634,8 @@ int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* ds
   p.dsc = dsc;
   p.scale = scale;
   const dim3 grid((s.C / 64) * (s.K / 64), used, 1);
-  const bool ink = !p.direct && option_get(OPT_WGRAD_KSPLIT) == 2 && wgrad_ink_ok(used, tick, grid.x, true);
-  p.tick = ink ? tick : nullptr;
-  p.nsplit = used;
   const int nr = (nh + 63) / 64;
-  const bool pipe2 = option_get(OPT_WGRAD_KSPLIT) == 2;  // the pipelined fragment reads (stride-1: KL 2)
-#define DTC_WS2(NR_, SC_, G_)                                                                                 \
-  if (pipe2 && ink) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 2, SC_, G_, 2, true>), grid, dim3(512), 0, st, p); \
-  else if (pipe2) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 2, SC_, G_, 2>), grid, dim3(512), 0, st, p);       \
-  else hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 2, SC_, G_, 0>), grid, dim3(512), 0, st, p)
+#define DTC_WS2(NR_, SC_, G_) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 2, SC_, G_>), grid, dim3(512), 0, st, p)
   if (gen) {
     if (nr <= 5) { if (dsc) DTC_WS2(5, true, true); else DTC_WS2(5, false, true); }
     else { if (dsc) DTC_WS2(6, true, true); else DTC_WS2(6, false, true); }
@@ -809,10 +645,10 @@ int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* ds
   }
 #undef DTC_WS2
   DTC_LAUNCH_CHECK();
-  if (p.direct || ink) return 0;  // dw (and dw_sc) written by the halo kernel
-  DTC_TRY(wgrad_reduce_to(slab, used, s.K, 9 * s.C, 9 * s.C, 9 * s.C, scale, dw, st, ts));
-  if (dsc) DTC_TRY(wgrad_reduce_to(p.slab_sc, used, s.K, s.C, s.C, s.C, scale, dw_sc, st, ts));
-  return 0;
+  if (p.direct) return 0;  // dw (and dw_sc) written by the halo kernel
+  // the taps' and the shortcut's slabs in one reduce launch (round 6: one launch per projection block fewer)
+  if (dsc) return wgrad_reduce_pair(slab, used, s.K, 9 * s.C, dw, p.slab_stride, s.C, dw_sc, scale, st, ts);
+  return wgrad_reduce_to(slab, used, s.K, 9 * s.C, 9 * s.C, 9 * s.C, scale, dw, st, ts);
 }
 
 }  // namespace dtc

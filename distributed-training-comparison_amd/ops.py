@@ -13,7 +13,6 @@ import torch
 
 from ._native import ConvDesc, NativeError, call, lib, ptr, require_cuda, stream_ptr
 
-STAT_SLOTS = 32
 
 
 def conv_desc(n, h, w, c, k, r, s, stride, pad) -> ConvDesc:
@@ -152,7 +151,39 @@ def conv2d_wgrad_batch(xs, dys, scale=1.0):
 
 
 def new_stats(c, device):
-    return torch.zeros(STAT_SLOTS, 2, c, dtype=torch.float64, device=device)
+    """A zeroed BN statistics accumulator for c channels (dtc_bn_stat_words(c) int64 words: exact fixed-point
+    sums, common.h): conv epilogues and BN-backward reductions ADD into it."""
+    return torch.zeros(int(lib.dtc_bn_stat_words(c)), dtype=torch.int64, device=device)
+
+
+def stat_totals(stats, c):
+    """The two per-channel totals an accumulator holds, as the BN kernels form them (dtc_bn_stat_totals, host
+    code): float64 [2, c] on the CPU -- row 0 sum x (sum dz), row 1 sum x^2 (sum dz * xhat)."""
+    host = stats.detach().to("cpu", torch.int64).contiguous()
+    if host.numel() != int(lib.dtc_bn_stat_words(c)):
+        raise ValueError(f"stat_totals: {host.numel()} words is not an accumulator of {c} channels")
+    out = torch.empty(2, c, dtype=torch.float64)
+    call("dtc_bn_stat_totals", ptr(host), c, ptr(out))
+    return out
+
+
+def stat_from_totals(s, q, device):
+    """An accumulator holding the given per-channel totals (float64 arrays of c values; test input for the
+    finalize kernels): each total goes into slot 0 in the fixed-point format of common.h."""
+    import numpy as np
+
+    s, q = np.asarray(s, np.float64), np.asarray(q, np.float64)
+    c = s.shape[0]
+    words = np.zeros(int(lib.dtc_bn_stat_words(c)), np.int64)
+    hdr = 2 * int(lib.dtc_bn_stat_words(1)) - int(lib.dtc_bn_stat_words(2))  # header words (common.h DTC_STAT_HDR)
+    for j, v in enumerate((s, q)):
+        d = v * 256.0
+        if not np.all(np.abs(d) < 2.0 ** 55):
+            raise ValueError("stat_from_totals: total out of range")
+        h = np.floor(d)
+        words[hdr + (2 * j) * c:hdr + (2 * j + 1) * c] = h.astype(np.int64)
+        words[hdr + (2 * j + 1) * c:hdr + (2 * j + 2) * c] = np.floor((d - h) * 2.0 ** 44).astype(np.int64)
+    return torch.from_numpy(words).to(device)
 
 
 def bn_fwd_finalize(stats, count, gamma, beta, running_mean=None, running_var=None, nbt=None, momentum=0.1,

@@ -67,16 +67,19 @@ enum { DTC_CONV_FWD = 0, DTC_CONV_DGRAD = 1, DTC_CONV_WGRAD = 2 };
  * a separate launch. */
 size_t dtc_conv2d_workspace_size(const dtc_conv_desc* d, int pass);
 /* y[n][p][q][k] = conv(x, w); if stats != NULL, per-channel (sum, sum^2) of the bf16 output are
- * ADDED into stats[32][2][k] (fp64) — the batch statistics BatchNorm2d needs (net.py:21). */
-int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats,
+ * ADDED into stats — the batch statistics BatchNorm2d needs (net.py:21). A statistics accumulator is
+ * dtc_bn_stat_words(k) int64 words, zeroed before its first producer: exact fixed-point sums, so the
+ * totals do not depend on the order of the producers' atomic adds (the step is bit-reproducible, as the
+ * reference's cudnn.deterministic asks, src/ddp/utils.py:12-13); dtc_bn_stat_totals reads them. */
+int dtc_conv2d_fwd(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t* stats,
                    void* ws, size_t ws_bytes, void* stream);
 /* dx = conv^T(dy, w) (+ res if non-NULL): the input gradient of Conv2d */
 /* 3x3 stride-2 conv (desc) and its BasicBlock's 1x1 stride-2 projection shortcut (net.py:18-19, 29-36) of
  * the same input in one launch: y = conv(x, w), ysc = conv1x1_s2(x, wsc [K][C]); optional BN statistics of
  * each. The shortcut reads exactly the 3x3's centre-tap pixels, so x is read once. Returns
  * DTC_EINVAL for geometries without a fused plan (callers then run the two convs separately). */
-int dtc_conv2d_fwd_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats,
-                      const uint16_t* wsc, uint16_t* ysc, double* stats_sc, void* stream);
+int dtc_conv2d_fwd_sc(const dtc_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t* stats,
+                      const uint16_t* wsc, uint16_t* ysc, int64_t* stats_sc, void* stream);
 int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
                      const uint16_t* res, void* ws, size_t ws_bytes, void* stream);
 /* The same dgrad when dx is the gradient of a post-ReLU BatchNorm output y = relu(bn(x1) [+ bn2(x2)])
@@ -85,8 +88,8 @@ int dtc_conv2d_dgrad(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t*
  * the kernel has one (3x3 stride 1 and split-K paths), else as a second pass. dx may alias res. */
 int dtc_conv2d_dgrad_bn(const dtc_conv_desc* d, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
                         const uint16_t* res, const uint16_t* ymask, const uint16_t* x1, const float* mean1,
-                        const float* invstd1, double* acc1, const uint16_t* x2, const float* mean2,
-                        const float* invstd2, double* acc2, void* ws, size_t ws_bytes, void* stream);
+                        const float* invstd1, int64_t* acc1, const uint16_t* x2, const float* mean2,
+                        const float* invstd2, int64_t* acc2, void* ws, size_t ws_bytes, void* stream);
 /* dx of a projection block's input through conv1 (3x3 stride 2, desc) AND the 1x1 stride-2 shortcut
  * (net.py:18-19, 29-36) in one launch: dx = dgrad(dy, w) + dgrad(dsc, wsc [K][C]); the shortcut's term is
  * nonzero only at the (even, even) pixels and runs as extra reduction steps of that parity class. */
@@ -116,7 +119,14 @@ int dtc_conv2d_wgrad_batch(const dtc_conv_desc* d, int n, const uint16_t* const*
  * Replaces nn.BatchNorm2d train-mode forward/backward (net.py:21,25,37,92) with the F.relu and
  * residual add of BasicBlock.forward (net.py:41-44) and ResNet.forward (net.py:108) fused.
  * x is NHWC bf16 with m = n*h*w pixels and c channels (c % 8 == 0). */
-int dtc_bn_fwd_finalize(double* stats, int c, int64_t count, const float* gamma, const float* beta,
+/* Size of one statistics accumulator for c channels, in int64 words (a header word holding the
+ * non-finite flag, then 8 slots x 2 statistics x (hi, lo) x c). Zero it before its first producer. */
+size_t dtc_bn_stat_words(int c);
+/* Host-side read of an accumulator copied to host memory: totals[0][c] = first statistic (sum x / sum dz),
+ * totals[1][c] = second (sum x^2 / sum dz*xhat), exactly as the BN kernels form them (NaN if flagged).
+ * Pure host code, no device call. */
+int dtc_bn_stat_totals(const int64_t* host_words, int c, double* totals);
+int dtc_bn_fwd_finalize(int64_t* stats, int c, int64_t count, const float* gamma, const float* beta,
                         float* running_mean, float* running_var, int64_t* num_batches_tracked, float momentum,
                         float eps, float* mean, float* invstd, float* scale, float* shift, void* stream);
 int dtc_bn_apply_relu(const uint16_t* x, const float* scale, const float* shift, uint16_t* y, int64_t m, int c,
@@ -126,12 +136,12 @@ int dtc_bn_apply_add_relu(const uint16_t* x, const float* scale, const float* sh
 int dtc_bn_apply_dual_relu(const uint16_t* x, const float* scale, const float* shift, const uint16_t* x2,
                            const float* scale2, const float* shift2, uint16_t* y, int64_t m, int c, void* stream);
 /* dz = dy * [ymask > 0] (ymask may be NULL: no ReLU); acc1 += (sum dz, sum dz*xhat1) and, if x2,
- * acc2 += (sum dz, sum dz*xhat2); acc* are [32][2][c] fp64 */
+ * acc2 += (sum dz, sum dz*xhat2); acc* are statistics accumulators (dtc_bn_stat_words(c) int64) */
 int dtc_bn_bwd_reduce(const uint16_t* dy, const uint16_t* ymask, const uint16_t* x1, const float* mean1,
-                      const float* invstd1, double* acc1, const uint16_t* x2, const float* mean2,
-                      const float* invstd2, double* acc2, uint16_t* dz, int64_t m, int c, void* stream);
+                      const float* invstd1, int64_t* acc1, const uint16_t* x2, const float* mean2,
+                      const float* invstd2, int64_t* acc2, uint16_t* dz, int64_t m, int c, void* stream);
 /* dgamma = gscale*sum dz*xhat, dbeta = gscale*sum dz; coef[3][c] for dtc_bn_bwd_apply; acc re-zeroed */
-int dtc_bn_bwd_finalize(double* acc, int c, int64_t count, const float* gamma, const float* mean,
+int dtc_bn_bwd_finalize(int64_t* acc, int c, int64_t count, const float* gamma, const float* mean,
                         const float* invstd, float gscale, float* dgamma, float* dbeta, float* coef, void* stream);
 int dtc_bn_bwd_apply(const uint16_t* dz, const uint16_t* x1, const float* coef1, uint16_t* dx1, const uint16_t* x2,
                      const float* coef2, uint16_t* dx2, int64_t m, int c, void* stream);
@@ -144,10 +154,10 @@ int dtc_stem_im2col(const float* x_nchw, uint16_t* cols, int n, int h, int w, vo
 int dtc_stem_pack_weight(const uint16_t* w27, uint16_t* w64, int k, void* stream);
 /* Direct stem conv (the executor's default): y [n*h*w][64] bf16 = conv1(x) from fp32 NCHW x and the
  * bf16 KRSC weight [64][27], the 27 taps gathered per 256-pixel tile into LDS (no im2col matrix in
- * HBM); stats (optional, [32][2][64] fp64, accumulated) = BN batch sums of the bf16 outputs. The
+ * HBM); stats (optional, dtc_bn_stat_words(64) int64, accumulated) = BN batch sums of the bf16 outputs. The
  * weight gradient dw27 [64][27] fp32 = scale * sum_pixels dy (x) taps(x), workspace from
  * dtc_stem_wgrad_workspace_size. */
-int dtc_stem_fwd(const float* x_nchw, const uint16_t* w27, uint16_t* y, double* stats, int n, int h, int w,
+int dtc_stem_fwd(const float* x_nchw, const uint16_t* w27, uint16_t* y, int64_t* stats, int n, int h, int w,
                  void* stream);
 size_t dtc_stem_wgrad_workspace_size(int n, int h, int w);
 int dtc_stem_wgrad(const float* x_nchw, const uint16_t* dy, float* dw27, float scale, int n, int h, int w, void* ws,
@@ -224,7 +234,7 @@ int dtc_barrier(dtc_comm* comm, void* stream);
  * reports `world` ranks. With factor == world it is `world` ranks holding identical data. Lets a
  * one-GPU test prove that every gradient bucket is reduced exactly once and only after its producers,
  * and that SyncBN's sums really go through the collective (a one-rank RCCL SUM is the identity and
- * proves neither). fp32 / fp64 buffers only. */
+ * proves neither). fp32 / int64 / fp64 buffers only (int64 x the integer factor). */
 int dtc_comm_init_loopback(dtc_comm** out, int device, int world, float factor);
 int dtc_comm_log_size(dtc_comm* comm);
 int dtc_comm_log_entry(dtc_comm* comm, int idx, uint64_t* addr, uint64_t* count, int* is_async);
@@ -234,7 +244,7 @@ int dtc_comm_log_clear(dtc_comm* comm);
  * Collectives are matched by call order (as RCCL's): the calling thread blocks until every rank issued
  * the same collective (kind, count, dtype, root; a mismatch or a 120 s wait is an error for all ranks),
  * then the data really moves between the ranks' buffers on a group stream that waits for every rank's
- * producers -- SUM all-reduce as the rank-ordered fp32/fp64 sum written into every buffer, broadcast as
+ * producers -- SUM all-reduce as the rank-ordered fp32/int64/fp64 sum written into every buffer, broadcast as
  * root -> all copies, barrier as a host rendezvous + stream drain -- and each rank's consumer stream
  * (the Reducer's side stream for buckets) waits for the result. Lets one GPU run W ranks with DISTINCT
  * data through the product Reducer, broadcasts and SyncBN (max 8 ranks). Every all-reduce is logged
@@ -310,7 +320,7 @@ int dtc_rn18_forward(dtc_net* net, const float* x, float* logits, int train, voi
 int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_comm* comm, void* stream);
 /* SyncBatchNorm (replaces nn.SyncBatchNorm.convert_sync_batchnorm(model), torch/nn/modules/
  * batchnorm.py, the conversion README.md:40 recommends; not called by the reference trainers).
- * comm != NULL: every training-mode BN all-reduces its fp64 per-channel partial sums over `comm`
+ * comm != NULL: every training-mode BN all-reduces its per-channel partial sums (exact int64) over `comm`
  * (forward: sum x, sum x^2; backward: sum dz, sum dz*xhat) on the compute stream and normalises
  * with the global element count (running_var's unbiased factor too); dgamma/dbeta keep this
  * rank's share (x 1/world) so the Reducer's mean matches DDP over SyncBatchNorm. Use a

@@ -66,15 +66,16 @@ def test_fp32_end_to_end_matches_oracle(dtc, cuda):
 def test_fp32_data_parallel_step_matches_oracle(dtc, cuda):
     """DataParallel (reference src/dp/trainer.py:27, torch nn.DataParallel semantics) with two replicas on
     cuda:0 (device_ids=[0, 0]) against the fp32 oracle: each replica runs train-mode BN over its own
-    half of the batch (the oracle's forward on that half), the gathered logits are the two halves'
-    oracle logits (1e-5), the mean loss over the whole batch gives gradient = mean of the two half-batch
-    oracle gradients, and the running statistics are replica 0's update (1e-5; the module is replica 0,
-    replica 1's buffers are discarded, as torch's replicate does). A DP that normalised over the whole
-    16-image batch instead of per replica fails the logits check.
-    Gradient bound: fp32 summation order alone moves some 8-image gradients by up to ~1e-2 of their norm
-    against the fp64 oracle (a BN bias gradient is a sum of dz that largely cancels; layer3.1.bn2.bias
-    0.9e-2, r05j), so each parameter's DP error is held to twice the error of the same executor run
-    single-replica on each half (its own noise floor on these inputs), plus 1e-4."""
+    half of the batch (the oracle's forward on that half), so the gathered logits are the two halves'
+    oracle logits (1e-5) and the mean loss over the whole batch is the mean of the halves' losses; the
+    running statistics are replica 0's update (1e-5; the module is replica 0, replica 1's buffers are
+    discarded, as torch's replicate does). A DP that normalised over the whole 16-image batch instead of
+    per replica fails the logits check.
+    Gradient: the DP backward scatters dlogits, runs each replica's backward on its slice and reduce-adds
+    the replicas' flat gradients. With the same dlogits (the mean cross-entropy's, fed explicitly) the
+    module's gradient must equal, bit for bit, the sum of the same executor's single-replica backwards on
+    each half (the step is deterministic; a two-term fp32 sum has one order); the single-replica backward
+    itself is pinned to the oracle per layer at 1e-5 by test_fp32_per_layer_teacher_forced."""
     B = 8
     model, sd, x, y = _setup(dtc, cuda, 2 * B, seed=6)
     model.precision = "fp32"
@@ -82,33 +83,37 @@ def test_fp32_data_parallel_step_matches_oracle(dtc, cuda):
     params, bufs = _split_state(sd)
     halves = [R.forward_backward(params, bufs, x[h * B:(h + 1) * B], y[h * B:(h + 1) * B], bf16_mode=False,
                                  train=True) for h in range(2)]
-    single = []  # the executor's own gradients on each half (noise floor)
-    for h in range(2):
-        torch.manual_seed(42)
-        m1 = dtc.ResNet18().to(cuda)
-        m1.precision = "fp32"
-        crit(m1(torch.from_numpy(x[h * B:(h + 1) * B]).to(cuda)), torch.from_numpy(y[h * B:(h + 1) * B]).to(cuda)).backward()
-        single.append({k: _np(p.grad) for k, p in m1.named_parameters()})
-        del m1
     dp = dtc.DataParallel(model, device_ids=[0, 0])
     dp.zero_grad()
     logits = dp(torch.from_numpy(x).to(cuda))
     loss = crit(logits, torch.from_numpy(y).to(cuda))
-    loss.backward()
     torch.cuda.synchronize()
     assert rel_err(_np(logits), np.concatenate([r["logits"] for r in halves])) < 1e-5
     ref_loss = 0.5 * (halves[0]["loss"] + halves[1]["loss"])
     assert abs(float(loss) - ref_loss) < 1e-5 * max(1.0, abs(ref_loss))
+    # dlogits of the mean cross-entropy over the 16 rows (trainer.py:155), fed to both paths
+    p = torch.softmax(logits.detach().double(), 1)
+    p[torch.arange(2 * B), torch.from_numpy(y).to(cuda)] -= 1.0
+    dl = (p / (2 * B)).float().contiguous()
+    logits.backward(dl)
+    torch.cuda.synchronize()
+    single = []  # the executor's own gradients on each half, from the same dlogits slice
+    for h in range(2):
+        torch.manual_seed(42)
+        m1 = dtc.ResNet18().to(cuda)
+        m1.precision = "fp32"
+        m1(torch.from_numpy(x[h * B:(h + 1) * B]).to(cuda)).backward(dl[h * B:(h + 1) * B].clone())
+        torch.cuda.synchronize()
+        single.append({k: _np(p_.grad) for k, p_ in m1.named_parameters()})
+        del m1
     worst = (0.0, "")
-    for k, p in model.named_parameters():
-        g0, g1 = halves[0]["grads"][k], halves[1]["grads"][k]
-        ref = 0.5 * (g0 + g1)
-        den = 0.5 * (np.linalg.norm(g0) + np.linalg.norm(g1))
-        e = float(np.linalg.norm(_np(p.grad) - ref)) / den
-        floor = float(np.linalg.norm(0.5 * (single[0][k] + single[1][k]) - ref)) / den
-        assert e <= 2.0 * floor + 1e-4, (k, e, floor)
-        worst = max(worst, (e, k))
-    print(f"DP [0,0] fp32 vs oracle: worst parameter-gradient error {worst[0]:.2e} ({worst[1]})")
+    for k, p_ in model.named_parameters():
+        g = _np(p_.grad)
+        np.testing.assert_array_equal(g, single[0][k] + single[1][k], err_msg=k)
+        ref = 0.5 * (halves[0]["grads"][k] + halves[1]["grads"][k])
+        worst = max(worst, (rel_err(g, ref), k))
+    print(f"DP [0,0] fp32: gradient == sum of the replicas' single-run gradients (bit for bit); "
+          f"vs the fp64 oracle worst parameter {worst[0]:.2e} ({worst[1]})")
     sd2 = model.state_dict()
     for k, v in halves[0]["buffers"].items():
         e = rel_err(sd2[k].cpu().numpy(), v)

@@ -80,7 +80,7 @@ def test_conv_fwd_stride2_halo_and_shortcut(dtc, cuda, case, cfg):
     y2, ysc = y2.float().cpu().numpy(), ysc.float().cpu().numpy()
     assert rel_err(y, ref) < 1e-2 and rel_err(y2, ref) < 1e-2 and rel_err(ysc, ref_sc) < 1e-2
     for out, stt in ((y, st), (y2, st1), (ysc, st2)):  # BN statistics of the bf16 outputs, fp64 slots
-        s_ = stt.sum(0).cpu().numpy()
+        s_ = dtc.ops.stat_totals(stt, K).numpy()
         yb = out.reshape(-1, K).astype(np.float64)
         np.testing.assert_allclose(s_[0], yb.sum(0), rtol=1e-5, atol=1e-3)
         np.testing.assert_allclose(s_[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
@@ -100,7 +100,7 @@ def test_conv_fwd(dtc, cuda, case):
     assert yk.shape == ref.shape
     assert rel_err(yk, ref) < 1e-2
     # BN statistics of the bf16 output, accumulated in fp64 slots
-    s = stats.sum(0).cpu().numpy()
+    s = dtc.ops.stat_totals(stats, K).numpy()
     yb = yk.reshape(-1, K).astype(np.float64)
     np.testing.assert_allclose(s[0], yb.sum(0), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(s[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
@@ -235,10 +235,8 @@ def test_bn_forward(dtc, cuda, C):
     rm = np.zeros(C, np.float32)
     rv = np.ones(C, np.float32)
     dev = cuda
-    stats = dtc.ops.new_stats(C, dev)
     xs = x.astype(np.float64)
-    stats[0, 0] = torch.from_numpy(xs.sum(0))
-    stats[0, 1] = torch.from_numpy((xs * xs).sum(0))
+    stats = dtc.ops.stat_from_totals(xs.sum(0), (xs * xs).sum(0), dev)
     t = lambda a: torch.from_numpy(a).to(dev)
     rm_d, rv_d = t(rm.copy()), t(rv.copy())
     nbt = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -398,7 +396,7 @@ def test_stem_direct_fwd_wgrad(dtc, cuda, shape):
     y = dtc.ops.stem_fwd(xd, _to_dev_bf16(w27.reshape(64, 27), cuda), stats).float().cpu().numpy()
     ref = O.conv2d_fwd(xb, w27, 1, 1)
     assert rel_err(y, O.bf16(ref)) < 1e-2
-    st = stats.sum(0).cpu().numpy()
+    st = dtc.ops.stat_totals(stats, 64).numpy()
     yb = y.reshape(-1, 64).astype(np.float64)
     np.testing.assert_allclose(st[0], yb.sum(0), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(st[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
@@ -479,12 +477,10 @@ def test_amp_check_finite_positions(dtc, cuda, n):
     (2, 6, 96, 64, 64),     # 32-pixel segments
     (1, 5, 40, 64, 64),     # one 40-pixel row per step (24 padded slots)
 ])
-@pytest.mark.parametrize("ksplit", [0, 2])
-def test_conv_wgrad_halo(dtc, cuda, case, ksplit):
+def test_conv_wgrad_halo(dtc, cuda, case):
     """Halo-tiled 3x3 weight gradient == generic loader == oracle (fp32 sums of exact products); the rows
     wider than 64 pixels or not dividing 64 run the general-geometry kernels (per-step 64-bit bases, zero-dy
-    padded slots), which must match too. ksplit: option wgrad_ksplit (0 compiler-scheduled fragment reads,
-    2 software-pipelined: the same MFMAs in the same order)."""
+    padded slots), which must match too."""
     N, H, W, C, K = case
     g = np.random.default_rng(7)
     x = _rand_bf16((N, H, W, C), g)
@@ -492,13 +488,11 @@ def test_conv_wgrad_halo(dtc, cuda, case, ksplit):
     xd, dyd = _to_dev_bf16(x, cuda), _to_dev_bf16(dy, cuda)
     ref = O.conv2d_wgrad(x, dy, 3, 3, 1, 1)
     try:
-        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", ksplit)
         halo = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
         dtc._native.lib.dtc_set_option(b"wgrad_halo", 0)
         generic = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
     finally:
         dtc._native.lib.dtc_set_option(b"wgrad_halo", 224)
-        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", 2)
     assert rel_err(halo, ref) < 1e-5
     assert rel_err(generic, ref) < 1e-5
 
@@ -512,52 +506,28 @@ def test_conv_wgrad_halo(dtc, cuda, case, ksplit):
     (2, 8, 224, 64, 64, 4),    # general geometry (56-pixel row segments), the 224x224 layer1 batch
     (2, 14, 28, 128, 128, 3),  # general geometry, two 28-pixel rows per step
 ])
-@pytest.mark.parametrize("ksplit", [0, 2])
-def test_conv_wgrad_batch(dtc, cuda, case, ksplit):
+def test_conv_wgrad_batch(dtc, cuda, case):
     """dtc_conv2d_wgrad_batch: n independent weight gradients in one halo launch (blockIdx.z =
     problem, 1/n of the splits each) + one reduce launch == the oracle per problem, and == the
-    one-by-one dtc_conv2d_wgrad to fp32 summation order (different split counts); both wave layouts."""
+    one-by-one dtc_conv2d_wgrad to fp32 summation order (different split counts); bit-identical when
+    repeated."""
     N, H, W, C, K, n = case
     g = np.random.default_rng(11)
     xs = [_rand_bf16((N, H, W, C), g) for _ in range(n)]
     dys = [_rand_bf16((N, H, W, K), g) for _ in range(n)]
     xd = [_to_dev_bf16(a, cuda) for a in xs]
     dyd = [_to_dev_bf16(a, cuda) for a in dys]
-    try:
-        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", ksplit)
-        got = dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.25)
-        ones = [dtc.ops.conv2d_wgrad(xd[i], dyd[i], 3, 3, 1, 1, scale=0.25).cpu().numpy() for i in range(n)]
-    finally:
-        dtc._native.lib.dtc_set_option(b"wgrad_ksplit", 2)
+    got = dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.25)
+    again = dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.25)
+    ones = [dtc.ops.conv2d_wgrad(xd[i], dyd[i], 3, 3, 1, 1, scale=0.25).cpu().numpy() for i in range(n)]
     assert len(got) == n
+    for a, b in zip(got, again):
+        assert torch.equal(a, b)
     for i in range(n):
         ref = 0.25 * O.conv2d_wgrad(xs[i], dys[i], 3, 3, 1, 1)
         one = ones[i]
         assert rel_err(got[i].cpu().numpy(), ref) < 1e-5, i
         assert rel_err(got[i].cpu().numpy(), one) < 1e-6, i
-
-
-@pytest.mark.parametrize("case", [(4, 32, 32, 64, 64, 4), (8, 16, 16, 128, 128, 3), (12, 4, 4, 512, 512, 4),
-                                  (2, 8, 224, 64, 64, 4)])
-def test_conv_wgrad_batch_three_stage_ring(dtc, cuda, case):
-    """Option wgrad_ring=3 (the pipelined weight-gradient kernel with a three-stage LDS ring): identical MFMA
-    order per accumulator, so bit-identical to the four-stage ring, and against the oracle."""
-    N, H, W, C, K, n = case
-    g = np.random.default_rng(13)
-    xs = [_rand_bf16((N, H, W, C), g) for _ in range(n)]
-    dys = [_rand_bf16((N, H, W, K), g) for _ in range(n)]
-    xd = [_to_dev_bf16(a, cuda) for a in xs]
-    dyd = [_to_dev_bf16(a, cuda) for a in dys]
-    lib = dtc._native.lib
-    try:
-        a = [t.cpu().numpy() for t in dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.5)]
-        lib.dtc_set_option(b"wgrad_ring", 3)
-        b = [t.cpu().numpy() for t in dtc.ops.conv2d_wgrad_batch(xd, dyd, scale=0.5)]
-    finally:
-        lib.dtc_set_option(b"wgrad_ring", 4)
-    for i in range(n):
-        np.testing.assert_array_equal(a[i], b[i])
-        assert rel_err(b[i], 0.5 * O.conv2d_wgrad(xs[i], dys[i], 3, 3, 1, 1)) < 1e-5
 
 
 def test_conv_wgrad_batch_rejects_non_halo(dtc, cuda):
@@ -602,7 +572,7 @@ def test_conv_halo_configs(dtc, cuda, case, cfg, split):
         dtc._native.call("dtc_set_option", b"halo_split", 0)
     yk = y.float().cpu().numpy()
     assert rel_err(yk, O.conv2d_fwd(x, w, 1, 1)) < 1e-2
-    s = stats.sum(0).cpu().numpy()
+    s = dtc.ops.stat_totals(stats, K).numpy()
     yb = yk.reshape(-1, K).astype(np.float64)
     np.testing.assert_allclose(s[0], yb.sum(0), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(s[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
@@ -650,8 +620,8 @@ def test_conv_halo_splitk_in_kernel_matches_reduce_launch(dtc, cuda, case, split
             out = run()
             for a, b in ((out[0], ref[0]), (out[2], ref[2]), (out[3], ref[3])):
                 assert torch.equal(a, b)
-            for a, b in ((out[1], ref[1]), (out[4], ref[4])):  # the same values, fp32 partial sums regrouped
-                a, b = a.sum(0), b.sum(0)  # (sums of products cancel: the bound scales with each row's magnitude)
+            for a, b, nc in ((out[1], ref[1], K), (out[4], ref[4], C)):  # the same values, fp32 partials regrouped
+                a, b = dtc.ops.stat_totals(a, nc), dtc.ops.stat_totals(b, nc)  # (sums of products cancel: the bound scales with each row's magnitude)
                 assert ((a - b).abs() <= 2e-5 * b.abs().amax(1, keepdim=True) + 1e-6).all(), (a - b).abs().max()
     finally:
         dtc._native.call("dtc_set_option", b"splitk_ink", prev)
@@ -688,7 +658,7 @@ def test_conv_halo_general_geometry(dtc, cuda, case):
         y = dtc.ops.conv2d_fwd(xd, wd, 1, 1, stats=stats)
         dx = dtc.ops.conv2d_dgrad(dyd, wd, (H, W), 1, 1, res=rd)
         torch.cuda.synchronize()
-        return y.float().cpu().numpy(), stats.sum(0).cpu().numpy(), dx.float().cpu().numpy()
+        return y.float().cpu().numpy(), dtc.ops.stat_totals(stats, K).numpy(), dx.float().cpu().numpy()
 
     yk, s, dxk = run()
     dtc._native.call("dtc_set_option", b"halo_gen", 0)
@@ -732,7 +702,7 @@ def test_conv_c64(dtc, cuda, case, c64_forced):
     dx = dtc.ops.conv2d_dgrad(_to_dev_bf16(dy, cuda), _to_dev_bf16(w, cuda), (H, W), 1, 1, res=_to_dev_bf16(res, cuda))
     yk = y.float().cpu().numpy()
     assert rel_err(yk, O.conv2d_fwd(x, w, 1, 1)) < 1e-2
-    s = stats.sum(0).cpu().numpy()
+    s = dtc.ops.stat_totals(stats, 64).numpy()
     yb = yk.reshape(-1, 64).astype(np.float64)
     np.testing.assert_allclose(s[0], yb.sum(0), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(s[1], (yb * yb).sum(0), rtol=1e-5, atol=1e-3)
@@ -762,7 +732,7 @@ def test_conv_c64_general_geometry(dtc, cuda, case, c64_forced):
         dx = dtc.ops.conv2d_dgrad(dyd, wd, (H, W), 1, 1, res=rd)
         dx0 = dtc.ops.conv2d_dgrad(dyd, wd, (H, W), 1, 1)
         torch.cuda.synchronize()
-        return y.float().cpu().numpy(), stats.sum(0).cpu().numpy(), dx.float().cpu().numpy(), dx0.float().cpu().numpy()
+        return y.float().cpu().numpy(), dtc.ops.stat_totals(stats, 64).numpy(), dx.float().cpu().numpy(), dx0.float().cpu().numpy()
 
     yk, s, dxk, dx0k = run()
     dtc._native.call("dtc_set_option", b"c64_gen", 0)
@@ -852,61 +822,8 @@ def test_conv_dgrad_bn_fused(dtc, cuda, case, split):
     if with_res:
         assert dz1.data_ptr() == resd.data_ptr()
     for a1, a0 in [(a11, a10)] + ([(a21, a20)] if dual else []):
-        s1, s0 = a1.sum(0).cpu().numpy(), a0.sum(0).cpu().numpy()
+        s1, s0 = dtc.ops.stat_totals(a1, C).numpy(), dtc.ops.stat_totals(a0, C).numpy()
         np.testing.assert_allclose(s1, s0, rtol=1e-5, atol=1e-3 * np.abs(s0).max())
-
-
-@pytest.mark.parametrize("case", [("batch", (256, 8, 8, 256, 256), 3, 0), ("batch", (256, 16, 16, 128, 128), 3, 8),
-                                  ("batch", (64, 8, 8, 256, 256), 2, 0), ("s2", (256, 8, 8, 256, 512), 1, 0),
-                                  ("s2", (64, 16, 16, 128, 256), 1, 0)])
-def test_wgrad_splitk_in_kernel_matches_reduce_launch(dtc, cuda, case):
-    """Option wgrad_ink: a weight-gradient launch of at most wgrad_ink_max splits sums its
-    split-K partials in the kernel (the last workgroup of each tile reads every split's sc1 partial in split
-    order and writes scale * sum; stride-2 launches also the fused shortcut's) instead of a wgrad_reduce launch.
-    Against the reduce launch (whose lanes group the splits differently: 1e-6) and the oracle (1e-5), on 6
-    repeated launches (the counters must return to zero each time); layer3 (4 splits), layer2 with a forced
-    8-split cap, the stride-2 layer4.0 conv1 + shortcut (4 splits) and a smaller batch."""
-    kind, (N, H, W, C, K), nprob, cap = case
-    g = np.random.default_rng(5 + N + C)
-    lib = dtc._native.lib
-    Ho, Wo = (H // 2, W // 2) if kind == "s2" else (H, W)
-    xs = [_to_dev_bf16(_rand_bf16((N, H, W, C), g), cuda) for _ in range(nprob)]
-    dys = [_to_dev_bf16(_rand_bf16((N, Ho, Wo, K), g), cuda) for _ in range(nprob)]
-    dsc = _to_dev_bf16(_rand_bf16((N, Ho, Wo, K), g), cuda)
-
-    def run():
-        if kind == "s2":
-            dw, dws = dtc.ops.conv2d_wgrad_sc(xs[0], dys[0], dsc, scale=0.5)
-            out = [dw, dws]
-        else:
-            out = dtc.ops.conv2d_wgrad_batch(xs, dys, scale=0.5)
-        torch.cuda.synchronize()
-        return [t.clone() for t in out]
-
-    prev, prev_cap = lib.dtc_get_option(b"wgrad_ink"), lib.dtc_get_option(b"wgrad_ink_max")
-    try:
-        if cap:
-            dtc._native.call("dtc_set_option", b"wgrad_ink_max", cap)
-        dtc._native.call("dtc_set_option", b"wgrad_ink", 0)
-        ref = run()
-        dtc._native.call("dtc_set_option", b"wgrad_ink", 2)  # every launch (1: the stride-2 ones only)
-        for _ in range(6):
-            out = run()
-            for a, b in zip(out, ref):
-                assert rel_err(a.cpu().numpy(), b.cpu().numpy()) < 1e-6
-        first = out
-        assert all(torch.equal(a, b) for a, b in zip(run(), first))  # deterministic run to run
-    finally:
-        dtc._native.call("dtc_set_option", b"wgrad_ink", prev)
-        dtc._native.call("dtc_set_option", b"wgrad_ink_max", prev_cap)
-    x0, dy0 = xs[0].float().cpu().numpy(), dys[0].float().cpu().numpy()
-    if kind == "s2":
-        dw_ref = O.conv2d_wgrad(x0, dy0, 3, 3, 2, 1)
-        assert rel_err(first[0].cpu().numpy(), 0.5 * dw_ref) < 1e-5
-        dsc_ref = O.conv2d_wgrad(x0, dsc.float().cpu().numpy(), 1, 1, 2, 0)
-        assert rel_err(first[1].cpu().numpy().reshape(dsc_ref.shape), 0.5 * dsc_ref) < 1e-5
-    else:
-        assert rel_err(first[0].cpu().numpy(), 0.5 * O.conv2d_wgrad(x0, dy0, 3, 3, 1, 1)) < 1e-5
 
 
 S2D_CASES = [(256, 32, 32, 64, 128), (256, 16, 16, 128, 256), (256, 8, 8, 256, 512), (8, 32, 32, 64, 128),

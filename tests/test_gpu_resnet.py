@@ -395,38 +395,40 @@ def _train_steps(dtc, cuda, steps, graphs, batch=8, seed=5):
 @pytest.mark.parametrize("mode", [1, 2, 3])
 def test_graph_replay_matches_eager(dtc, cuda, mode):
     """hipGraph replay (option graphs: 1 forward and backward, 2 forward only, 3 backward only) vs eager
-    launches of the same step: identical kernels and arguments, so results agree up to the order of the
-    fp64 BN-statistics atomics."""
+    launches of the same step: identical kernels and arguments, and a deterministic step (exact BN sums,
+    fixed split-K orders), so three training steps give identical losses, gradients, parameters and
+    running statistics."""
     lg, gg, pg, bg = _train_steps(dtc, cuda, 3, graphs=mode)
     le, ge, pe, be = _train_steps(dtc, cuda, 3, graphs=False)
-    np.testing.assert_allclose(lg, le, rtol=1e-4)
-    assert rel_err(gg, ge) < 1e-3
-    assert rel_err(pg, pe) < 1e-5
+    np.testing.assert_array_equal(lg, le)
+    np.testing.assert_array_equal(gg, ge)
+    np.testing.assert_array_equal(pg, pe)
     for k in bg:
-        assert rel_err(bg[k], be[k]) < 1e-4, k
+        np.testing.assert_array_equal(bg[k], be[k], err_msg=k)
 
 
 @pytest.mark.parametrize("graphs", [True, False])
 def test_side_stream_wgrad_matches_serial(dtc, cuda, graphs):
     """Weight gradients on the side stream (option bwd_streams=1, the default), forked/joined by
     events inside the (captured) backward, vs everything on one stream: the same kernels on the
-    same operands, so results agree up to the order of the fp64 BN-statistics atomics."""
+    same operands in a deterministic step, so three training steps give identical results."""
     la, ga, pa, _ = _train_steps(dtc, cuda, 3, graphs=graphs)
     dtc._native.lib.dtc_set_option(b"bwd_streams", 0)
     try:
         lb, gb, pb, _ = _train_steps(dtc, cuda, 3, graphs=graphs)
     finally:
         dtc._native.lib.dtc_set_option(b"bwd_streams", 1)
-    np.testing.assert_allclose(la, lb, rtol=1e-4)
-    assert rel_err(ga, gb) < 1e-3
-    assert rel_err(pa, pb) < 1e-5
+    np.testing.assert_array_equal(la, lb)
+    np.testing.assert_array_equal(ga, gb)
+    np.testing.assert_array_equal(pa, pb)
 
 
 @pytest.mark.parametrize("graphs", [True, False])
 def test_fused_bn_finalize_matches_separate(dtc, cuda, graphs):
     """BN coefficients computed inside the apply kernels (option bn_fused_fin=1, default) vs the
-    separate finalize launches: same fp64 slot sums in a different (fixed) combination order, so
-    losses, gradients, parameters and running statistics agree to rounding. The projection shortcut's
+    separate finalize launches: the same exact slot totals and the same coefficient expressions, but the
+    separate path's BN-backward reduction stores dz and groups its partials per its own grid, so losses,
+    gradients, parameters and running statistics agree to rounding. The projection shortcut's
     dgrad is computed separately in both arms (dgrad_scf=0): the fused-finalize executor would otherwise
     fold it into conv1's class-(0, 0) dgrad as one fp32 sum (one bf16 rounding of dx instead of two), a
     legitimate 1-ulp difference that 3 steps at lr 0.1 on 8 images amplify past rtol 1e-4. For the same
@@ -476,41 +478,35 @@ def _grads_repeated(dtc, cuda, graphs, reps=2, batch=8, seed=5, hw=32):
         dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
 
 
-def _assert_same_grads(a, b, batch, what):
-    """Two gradient vectors that should be identical. At batches of 64 and more a BN layer's fp64 statistic
-    slots collect several workgroups' atomic adds in arrival order, so two runs of even the same plan can
-    differ in a double's last bits and, rarely, round one fp32 coefficient the other way (DESIGN.md §3,
-    round 5: run-to-run repeatability); there a mismatch is accepted when it is that size (<= 1e-2 relative
-    over the whole vector) and reported; smaller batches must match bit for bit."""
-    if np.array_equal(a, b):
-        return
-    e = rel_err(b, a)
-    assert batch >= 64 and e < 1e-2, (what, e)
-    print(f"{what}: not bit-identical at batch {batch} (rel {e:.1e}: BN fp64-atomic arrival order)")
+def _assert_same_grads(dtc, a, b, what, close=None):
+    """Two flat gradient vectors that must be identical, checked per parameter (the message names the first
+    that differs). The step is deterministic (BN sums are exact integer fixed point, common.h; every split-K
+    sum has a fixed order), so any difference is a real one. close: {parameter name: rtol} for parameters a
+    compared option computes with a different, legitimate fp32 grouping."""
+    close = close or {}
+    for pe in dtc.nn.Layout(100, 25.0).params:
+        x = a[pe.offset:pe.offset + pe.numel]
+        y = b[pe.offset:pe.offset + pe.numel]
+        if pe.name in close:
+            assert rel_err(y, x) < close[pe.name], (what, pe.name, rel_err(y, x))
+        else:
+            np.testing.assert_array_equal(x, y, err_msg=f"{what}: {pe.name}")
 
 
 @pytest.mark.parametrize("batch", [256, 32])
 def test_backward_repeatable_across_steps(dtc, cuda, batch):
-    """Run-to-run repeatability of the default training step: the same forward + backward twice on the same
-    weights and data -- eager, and graph capture then replay -- at config 2's batch and config 3's per-rank
-    batch. Every split-K sum (in-kernel and reduce launches) runs in a fixed split order (bit-identical: the op
-    tests); the BN batch statistics and backward sums are fp64 atomic adds into 32 slots per channel, whose
-    arrival order varies, so the doubles can differ in their last bits and, rarely, round to a different fp32
-    coefficient -- then bf16 roundings downstream flip. Measured (r05o): two identical B=256 replayed steps
-    differed in the stem and layer1 gradients only. Bound: 1e-2 relative for the whole vector and every conv
-    weight, 5e-2 for BN / bias gradients (sums that partly cancel) -- the bf16 noise of a flipped rounding, far
-    below any algorithmic difference; most parameters are bit-identical."""
-    lay = dtc.nn.Layout(100, 25.0)
+    """Run-to-run bit-reproducibility of the default training step (the reference trains with
+    cudnn.deterministic = True, src/ddp/utils.py:12-13): the same forward + backward twice on the same weights
+    and data -- eager, and graph capture then replay -- at config 2's batch and config 3's per-rank batch must
+    give identical gradients, bit for bit. Every split-K sum (in-kernel hand-off and reduce launches) runs in a
+    fixed split order, and the BN batch statistics and backward sums are exact integer fixed-point sums
+    (common.h), so the order in which workgroups' atomic adds arrive changes nothing. (Rounds 1-5 summed the BN
+    partials with fp64 atomics: r05k / r05o saw two identical B=256 steps differ in the stem and layer1
+    gradients, one fp32 coefficient rounded the other way.) Four repetitions per mode."""
     for graphs in (0, 1):
-        g = _grads_repeated(dtc, cuda, graphs, batch=batch)
-        errs = {pe.name: rel_err(g[1][pe.offset:pe.offset + pe.numel], g[0][pe.offset:pe.offset + pe.numel])
-                for pe in lay.params}
-        worst = max(errs.items(), key=lambda kv: kv[1])
-        same = sum(1 for e in errs.values() if e == 0.0)
-        print(f"graphs={graphs} B={batch}: {same}/{len(errs)} parameters bit-identical, worst {worst[0]} {worst[1]:.2e}")
-        assert rel_err(g[1], g[0]) < 1e-2, graphs  # the whole gradient vector
-        for pe in lay.params:  # per parameter: BN / bias gradients are sums of dz that partly cancel -- 5e-2
-            assert errs[pe.name] < (1e-2 if "conv" in pe.name else 5e-2), (graphs, pe.name, errs[pe.name])
+        g = _grads_repeated(dtc, cuda, graphs, reps=4, batch=batch)
+        for r in range(1, len(g)):
+            _assert_same_grads(dtc, g[0], g[r], f"graphs={graphs} B={batch} rep {r}")
 
 
 @pytest.mark.parametrize("batch,hw", [(8, 32), (3, 32), (5, 8)])
@@ -555,8 +551,8 @@ def test_wgrad_batch_matches_unbatched(dtc, cuda, graphs):
 def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
     """Mask-bit BN backward (option bn_mask=1, default: the forward BN apply writes the ReLU mask as
     bits, the reduction stores no dz, the apply forms dz from dy and the bits) vs masking with the
-    bf16 outputs and a stored dz: masking is exact and the sums run in the same order, so gradients
-    agree to the fp64 slot-atomic order (capture and replay), and so do three training steps. The
+    bf16 outputs and a stored dz: masking is exact and the sums are the same partials (exact integer
+    totals), so gradients are identical (capture and replay), and so are three training steps. The
     shortcut's dgrad stays a separate launch in both arms (dgrad_scf=0: the bn_mask=0 executor has no
     fused form; see test_fused_bn_finalize_matches_separate)."""
     lib = dtc._native.lib
@@ -577,11 +573,11 @@ def test_bn_mask_bits_match_bf16_mask(dtc, cuda, graphs):
         lib.dtc_set_option(b"bn_cg", 1)
         lib.dtc_set_option(b"wgrad_s2", 1)
     for rep in range(2):
-        assert rel_err(ga[rep], gb[rep]) < 1e-6, rep
-    np.testing.assert_allclose(la, lb, rtol=1e-4)
-    assert rel_err(pa, pb) < 1e-5
+        _assert_same_grads(dtc, ga[rep], gb[rep], f"bn_mask rep {rep}")
+    np.testing.assert_array_equal(la, lb)
+    np.testing.assert_array_equal(pa, pb)
     for k in ba:
-        assert rel_err(ba[k], bb[k]) < 1e-4, k
+        np.testing.assert_array_equal(ba[k], bb[k], err_msg=k)
 
 
 @pytest.mark.parametrize("batch", [8, 32, 64])
@@ -644,17 +640,9 @@ def test_stem_bn_fused_wgrad_matches_separate(dtc, cuda, batch, hw):
             gb = _grads_repeated(dtc, cuda, graphs, batch=batch, hw=hw)
         finally:
             lib.dtc_set_option(b"stem_bn_fuse", DEFAULT_STEM_BN_FUSE)
-        lay = dtc.nn.Layout(100, 25.0)
         for rep in range(2):
-            if batch > 64 and not np.array_equal(ga[rep], gb[rep]):
-                # the stem conv's own partial grouping differs at B=256 (1e-5) -- and two runs can differ by the
-                # BN fp64-atomic noise (_assert_same_grads)
-                _assert_same_grads(ga[rep], gb[rep], batch, f"stem_bn_fuse rep {rep} graphs {graphs}")
-                continue
-            for pe in lay.params:
-                a = ga[rep][pe.offset:pe.offset + pe.numel]
-                b = gb[rep][pe.offset:pe.offset + pe.numel]
-                np.testing.assert_array_equal(a, b, err_msg=f"{pe.name} rep {rep} graphs {graphs}")
+            _assert_same_grads(dtc, ga[rep], gb[rep], f"stem_bn_fuse rep {rep} graphs {graphs}",
+                               close={"conv1.weight": 1e-5} if batch > 64 else None)
 
 
 @pytest.mark.parametrize("level", [1, 2, 3])
@@ -681,7 +669,7 @@ def test_shortcut_fused_forward_matches_separate(dtc, cuda, level):
                 lib.dtc_set_option(b"halo_s2", 1)
             for rep in range(2):
                 if s2 == 0:
-                    _assert_same_grads(ga[rep], gb[rep], 64, f"sc_fuse={level} rep {rep}")
+                    _assert_same_grads(dtc, ga[rep], gb[rep], f"sc_fuse={level} rep {rep}")
                 else:
                     assert np.isfinite(gb[rep]).all() and rel_err(gb[rep], ga[rep]) < 1e-2, rel_err(gb[rep], ga[rep])
 
@@ -739,7 +727,7 @@ def test_stem_weight_lds_matches_gather(dtc, cuda, batch, hw):
     finally:
         lib.dtc_set_option(b"stem_wlds", DEFAULT_STEM_WLDS)
     for rep in range(2):
-        _assert_same_grads(ga[rep], gb[rep], batch, f"stem_wlds rep {rep}")
+        _assert_same_grads(dtc, ga[rep], gb[rep], f"stem_wlds rep {rep}")
 
 
 def test_head_after_forward_graph_matches_eager(dtc, cuda):
@@ -1303,9 +1291,10 @@ def test_sync_batchnorm_two_identical_ranks_loopback(dtc, cuda):
     the local ones (sums x2, count x2), so logits, every gradient and the running statistics must equal
     plain BN (dgamma/dbeta = (1/W) x the all-reduced sums = this rank's share, which DDP's mean then
     averages -- torch SyncBN + DDP). A path that skipped a collective would halve that BN's mean / its
-    backward sums (sums x1, count x2) and fail. Every forward and backward BN all-reduce is logged:
-    20 BNs -> 20 forward + 20 backward in-stream collectives of 2*C fp64 values each (the compacted
-    [2][C] sums, not the 32 partial-sum slots).
+    backward sums (sums x1, count x2) and fail. The BN sums are exact integers (common.h), doubled sums over
+    a doubled count give the same fp64 quotients, so logits and gradients are bit-identical to plain BN.
+    Every forward and backward BN all-reduce is logged: 20 BNs -> 20 forward + 20 backward in-stream
+    collectives of hdr + 4*C int64 words each (the 16-word header and the compacted slot 0, not all 8 slots).
     """
     comm = dtc.parallel.Comm.loopback(cuda.index or 0, 2.0, world=2)
     dtc._native.lib.dtc_set_option(b"bn_cg", 0)  # the SyncBN executor's two-pass BN backward in both arms
@@ -1330,11 +1319,13 @@ def test_sync_batchnorm_two_identical_ranks_loopback(dtc, cuda):
         log = comm.log()
         assert len(log) == 40 and not any(a for _, _, a in log)
         chans = sorted(n for _, n, _ in log)
-        assert chans[0] == 2 * 64 and chans[-1] == 2 * 512
+        hdr = 2 * dtc._native.lib.dtc_bn_stat_words(1) - dtc._native.lib.dtc_bn_stat_words(2)
+        assert chans[0] == hdr + 4 * 64 and chans[-1] == hdr + 4 * 512
         # running_var's unbiased factor uses the GLOBAL count (2M/(2M-1) vs M/(M-1): up to 1e-4 on
         # layer4 at M=512), as torch SyncBatchNorm does; running_mean is unaffected
-        assert rel_err(l1, l0) < 1e-3 and rel_err(b1, b0) < 2e-4
-        assert rel_err(g1, g0) < 1e-3
+        np.testing.assert_array_equal(l1, l0)
+        np.testing.assert_array_equal(g1, g0)
+        assert rel_err(b1, b0) < 2e-4
         m1.set_sync_bn(None)
     finally:
         dtc._native.lib.dtc_set_option(b"bn_cg", 1)
@@ -1343,10 +1334,11 @@ def test_sync_batchnorm_two_identical_ranks_loopback(dtc, cuda):
 
 def test_sync_batchnorm_one_rank(dtc, cuda):
     """SyncBatchNorm path (dtc_rn18_set_sync_bn) with a one-rank RCCL
-    communicator: every BN's fp64 sum slots go through an in-stream fp64 all-reduce (the identity
-    over one rank) and the executor runs eagerly; logits, gradients and running statistics must
-    equal the per-rank BatchNorm path (up to the order of the fp64 statistics atomics). The
-    two-rank statistics semantics are covered by tests/test_ddp_gloo.py::test_sync_batchnorm_gloo."""
+    communicator: every BN's statistic slots are compacted into slot 0 and go through an in-stream int64
+    all-reduce (the identity over one rank) and the executor runs eagerly; logits, gradients and running
+    statistics must equal the per-rank BatchNorm path bit for bit (the sums are exact integers: compaction
+    and the collective change no bit). The two-rank statistics semantics are covered by
+    tests/test_ddp_gloo.py::test_sync_batchnorm_gloo."""
     comm = dtc.parallel.Comm(0, 1, dtc.parallel.Comm.unique_id(), cuda.index or 0)
     dtc._native.lib.dtc_set_option(b"bn_cg", 0)  # the SyncBN executor's two-pass BN backward in both arms
     try:
@@ -1372,7 +1364,9 @@ def test_sync_batchnorm_one_rank(dtc, cuda):
             model.set_sync_bn(None)
         (l0, g0, b0), (l1, g1, b1) = res
         assert np.isfinite(g1).all() and np.abs(g1).sum() > 0
-        assert rel_err(l1, l0) < 1e-3 and rel_err(g1, g0) < 1e-3 and rel_err(b1, b0) < 1e-5
+        np.testing.assert_array_equal(l1, l0)
+        np.testing.assert_array_equal(g1, g0)
+        np.testing.assert_array_equal(b1, b0)
     finally:
         dtc._native.lib.dtc_set_option(b"bn_cg", 1)
         comm.close()

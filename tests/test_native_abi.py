@@ -145,16 +145,18 @@ _OPTION_DEFAULTS = {
     "halo_s2": 1, "wgrad_s2": 1, "dgrad_scf": 1, "bucket_tail": 1, "wgrad_gen": 1,
     "halo_gen": 1, "bn_red_unroll": 4, "c64_gen": 1, "graphs": 4, "head_fused": 1,
     # round 4
-    "bn_cg": 1, "bn_cg_elems": 262144, "wgrad_s2_wgs": 128, "comm_on_side": 1, "wgrad_ksplit": 2, "wgrad_ring": 4, "c64_wgs": 256, "wgrad_halo_l1": 0,
+    "bn_cg": 1, "bn_cg_elems": 262144, "wgrad_s2_wgs": 128, "comm_on_side": 1, "c64_wgs": 256, "wgrad_halo_l1": 0,
     # round 5
-    "splitk_ink": 1, "comm_prio": 0, "comm_tail_inline": 1, "wgrad_ink": 0, "wgrad_ink_max": 8, "dgrad_s2h": 1, "halo_small": 1,
+    "splitk_ink": 1, "comm_prio": 0, "comm_tail_inline": 1, "dgrad_s2h": 1, "halo_small": 1,
 }
-# measured-negative variants deleted in rounds 4 and 5 with their code paths (DESIGN.md keeps their numbers)
+# measured-negative variants deleted in rounds 4-6 with their code paths (DESIGN.md keeps their numbers)
 _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", "wgrad_pmap", "wgrad_prio",
                     "halo_nhb2", "wgrad_kernel", "head_direct", "halo_nosplit", "graph_ev", "wgrad_tail",
                     "wgrad_stages", "wgrad_pf", "wgrad_diag",
                     # round 5
-                    "bnb_mask", "bnb_fuse", "halo_stage_epi", "igemm_stages", "halo_l2pf", "dgrad_first", "wgrad_s2_ps", "c64_waves", "wgrad_early")
+                    "bnb_mask", "bnb_fuse", "halo_stage_epi", "igemm_stages", "halo_l2pf", "dgrad_first", "wgrad_s2_ps", "c64_waves", "wgrad_early",
+                    # round 6
+                    "wgrad_ink", "wgrad_ink_max", "wgrad_ring", "wgrad_ksplit")
 
 
 def test_options_registered_with_defaults(dtc):
@@ -189,3 +191,38 @@ def test_kernels_keep_accumulators_out_of_scratch(dtc):
     bad = {k: v for k, v in res.items() if v[0] > 64 and "ELi128ELi256E" not in k}
     assert not bad, bad
     assert all(v[0] == 0 for k, v in res.items() if "wgrad_halo_kernel" in k)
+
+
+def test_bn_stat_accumulator_host_decode(dtc):
+    """The BN statistics accumulator format (common.h: exact int64 fixed point, 8 slots x (hi, lo), a
+    header flag) read by the host decoder dtc_bn_stat_totals (pure host code, no GPU): totals encoded into
+    slot 0 come back exactly when they have no bits below 2^-52; spreading a total over the slots (as the
+    producers' atomic adds do, in any order) gives the same bits; the flag word makes every total NaN."""
+    import numpy as np
+    import torch
+
+    c = 24
+    rng = np.random.default_rng(3)
+    s = np.round(rng.normal(0, 1e4, c) * 2.0 ** 20) / 2.0 ** 20  # multiples of 2^-20
+    q = np.round(np.abs(rng.normal(0, 1e7, c)) * 2.0 ** 10) / 2.0 ** 10
+    w = dtc.ops.stat_from_totals(s, q, "cpu")
+    hdr = 2 * dtc._native.lib.dtc_bn_stat_words(1) - dtc._native.lib.dtc_bn_stat_words(2)
+    slots = (dtc._native.lib.dtc_bn_stat_words(1) - hdr) // 4
+    assert w.dtype == torch.int64 and w.numel() == dtc._native.lib.dtc_bn_stat_words(c) == hdr + slots * 4 * c
+    assert hdr % 16 == 0 and slots == 8  # line-aligned rows (common.h)
+    tot = dtc.ops.stat_totals(w, c).numpy()
+    np.testing.assert_array_equal(tot[0], s)
+    np.testing.assert_array_equal(tot[1], q)
+    # split each total's integer words over the slots (hi and lo words add independently): same totals
+    a = w.numpy().copy()
+    spread = np.zeros_like(a)
+    for j in range(4):  # (statistic, word) rows of slot 0
+        row = a[hdr + j * c:hdr + (j + 1) * c]
+        parts = [row // slots] * (slots - 1)
+        parts.append(row - (slots - 1) * (row // slots))
+        for k, part in enumerate(parts):
+            spread[hdr + (k * 4 + j) * c:hdr + (k * 4 + j + 1) * c] = part
+    tot2 = dtc.ops.stat_totals(torch.from_numpy(spread), c).numpy()
+    np.testing.assert_array_equal(tot2, tot)
+    spread[0] = 1  # a non-finite partial was seen
+    assert np.isnan(dtc.ops.stat_totals(torch.from_numpy(spread), c).numpy()).all()
