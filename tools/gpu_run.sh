@@ -7,6 +7,8 @@
 #   smoke            __graft_entry__.smoke()
 #   bench            bench.py $BENCH_ARGS                 -> gpurun_out/TAG_bench.json
 #   prof             rocprofv3 kernel trace of a short bench.py $BENCH_ARGS run -> gpurun_out/prof_TAG
+#   serprof          serialized kernel trace (bwd_streams=0, graphs=0) WITH the live event roofline of the same run
+#                    -> gpurun_out/TAG_ser_kernel_trace.md (events-vs-trace check in one run)
 #   pmc              rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs) -> gpurun_out/pmc_TAG_{fetch,write}
 #   ab:SPEC          tools/bench_ab.sh $AB_ROUNDS SPEC... (SPEC = "tagA|opts;tagB|opts")
 #   py:FILE          python FILE $PY_ARGS                 -> gpurun_out/TAG_FILE.log
@@ -27,6 +29,7 @@ for st in "$@"; do
     smoke) specs+=("${TAG}_smoke|300|python -c 'import __graft_entry__ as g; g.smoke()'") ;;
     bench) specs+=("${TAG}_benchrun|500|python bench.py $BA > gpurun_out/${TAG}_bench.json") ;;
     prof) specs+=("${TAG}_prof|300|cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats -d $ROOT/gpurun_out/prof_$TAG -o prof -- python3 $ROOT/bench.py --steps 20 --warmup 5 $QUIET $BA") ;;
+    serprof) specs+=("${TAG}_serprof|300|tools/prof_run.sh ${TAG}_ser --live --opt bwd_streams=0 --opt graphs=0 $BA") ;;
     pmc) specs+=("${TAG}_pmcf|150|cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $ROOT/gpurun_out/pmc_${TAG}_fetch -o run -- python3 $ROOT/bench.py --steps 10 --warmup 3 $QUIET $BA")
          specs+=("${TAG}_pmcw|150|cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $ROOT/gpurun_out/pmc_${TAG}_write -o run -- python3 $ROOT/bench.py --steps 10 --warmup 3 $QUIET $BA") ;;
     ab:*) IFS=';' read -ra parts <<< "${st#ab:}"; q=""; for p in "${parts[@]}"; do q="$q '$p'"; done
