@@ -367,16 +367,21 @@ int xent_fwd_fused(const float* logits, const int64_t* labels, int N, int ncls, 
   return 0;
 }
 
+// d loss / d logit = (softmax - onehot) * gscale / N: one definition for xent_bwd and the fused head backward
+__device__ __forceinline__ float xent_gain(const float* gscale, int N) { return (gscale ? *gscale : 1.f) / (float)N; }
+__device__ __forceinline__ float xent_grad(float z, float lse, bool hit, float g) {
+  return (expf(z - lse) - (hit ? 1.f : 0.f)) * g;
+}
+
 __global__ void __launch_bounds__(256) xent_bwd_kernel(const float* __restrict__ logits,
                                                       const int64_t* __restrict__ labels,
                                                       const float* __restrict__ lse, const float* __restrict__ gscale,
                                                       int N, int ncls, float* __restrict__ dl) {
   const int64_t total = (int64_t)N * ncls;
-  const float g = (gscale ? *gscale : 1.f) / (float)N;
+  const float g = xent_gain(gscale, N);
   for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     const int b = (int)(i / ncls), j = (int)(i % ncls);
-    const float p = expf(logits[i] - lse[b]);
-    dl[i] = (p - (labels[b] == j ? 1.f : 0.f)) * g;
+    dl[i] = xent_grad(logits[i], lse[b], labels[b] == j, g);
   }
 }
 
@@ -457,7 +462,8 @@ size_t head_bwd_workspace(int N, int C, int ncls) {
 // dact of one image: dact[p][c] = (1/HW) sum_j dl[j] W[j][c], the same value at every pixel p (the
 // pool's backward). Wave w sums classes j = w, w + 4, ... for 8 consecutive channels per lane (16-B
 // weight loads, eight rows in flight per lane); the four wave partials are added in LDS in a fixed
-// order, and the pixel rows are stored as 16-B pieces. sm: ncls + 4 C floats.
+// order, and the pixel rows are stored as 16-B pieces. sm: ncls + 4 C floats. dln == nullptr: the caller
+// already wrote the dlogits row into sm[0, ncls) (the barrier below orders it).
 template <typename T>
 __device__ __forceinline__ void head_dact_image(const float* __restrict__ dln, const T* __restrict__ wfc, int HW, int C,
                                                 int ncls, T* __restrict__ o, float* sm) {
@@ -474,7 +480,8 @@ __device__ __forceinline__ void head_dact_image(const float* __restrict__ dln, c
         const int j = wv + 4 * u;
         w8[u] = E::ld(wfc + (int64_t)(j < ncls ? j : 0) * C + l * 8);
       }
-      for (int j = t; j < ncls; j += 256) row[j] = dln[j];
+      if (dln)
+        for (int j = t; j < ncls; j += 256) row[j] = dln[j];
       __syncthreads();
       float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -491,7 +498,8 @@ __device__ __forceinline__ void head_dact_image(const float* __restrict__ dln, c
       goto combine;
     }
   }
-  for (int j = t; j < ncls; j += 256) row[j] = dln[j];
+  if (dln)
+    for (int j = t; j < ncls; j += 256) row[j] = dln[j];
   __syncthreads();
   for (int c8 = l; c8 < nch; c8 += 64) {
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -541,14 +549,20 @@ __global__ void __launch_bounds__(256) head_bwd_x_kernel(const float* __restrict
 // queue is empty, so every launch boundary here is exposed): workgroups [0, nw) compute dW / db, one
 // (class, 256-channel) strip each, the four waves summing every fourth image (dl[n][j] is uniform, feat
 // rows coalesced); workgroups [nw, nw + N) compute dact of one image each (head_bwd_x's work).
+// XE: the CrossEntropyLoss backward fused in (xa.logits != nullptr): every dlogits value is computed where
+// it is used, by xent_grad as xent_bwd computes it, and the dact workgroups also store their image's row
+// into dl (the executor's dlogits buffer) -- one launch fewer right after the per-step barrier.
 template <typename T>
-__global__ void __launch_bounds__(256) head_bwd_fused_kernel(const float* __restrict__ dl,
+__global__ void __launch_bounds__(256) head_bwd_fused_kernel(float* __restrict__ dl,
                                                             const float* __restrict__ feat,
                                                             const T* __restrict__ wfc, int N, int HW, int C, int ncls,
                                                             float scale, float* __restrict__ dw,
-                                                            float* __restrict__ db, T* __restrict__ dact, int nw) {
+                                                            float* __restrict__ db, T* __restrict__ dact, int nw,
+                                                            XentArgs xa) {
   extern __shared__ float hsx[];
   const int t = threadIdx.x;
+  const bool xe = xa.logits != nullptr;
+  const float xg = xe ? xent_gain(xa.gscale, N) : 0.f;
   if ((int)blockIdx.x < nw) {
     // dW[j][c..c+3] (float4 of feat per lane) and db[j]: wave w sums the images n = w, w + 4, ... (eight
     // rows in flight per lane), the four wave partials are added in LDS in a fixed order
@@ -559,7 +573,8 @@ __global__ void __launch_bounds__(256) head_bwd_fused_kernel(const float* __rest
     if (c < C) {
 #pragma unroll 8
       for (int n = wv; n < N; n += 4) {
-        const float d = dl[(int64_t)n * ncls + j];
+        const float d = xe ? xent_grad(xa.logits[(int64_t)n * ncls + j], xa.lse[n], xa.labels[n] == j, xg)
+                           : dl[(int64_t)n * ncls + j];
         const f32x4 f = *(const f32x4*)(feat + (int64_t)n * C + c);
 #pragma unroll
         for (int k = 0; k < 4; ++k) a[k] += d * f[k];
@@ -582,14 +597,24 @@ __global__ void __launch_bounds__(256) head_bwd_fused_kernel(const float* __rest
     return;
   }
   const int n = blockIdx.x - nw;
-  head_dact_image<T>(dl + (int64_t)n * ncls, wfc, HW, C, ncls, dact + (int64_t)n * HW * C, hsx);
+  if (xe) {
+    const float ls = xa.lse[n];
+    const int64_t lab = xa.labels[n];
+    for (int j = t; j < ncls; j += 256) {
+      const float d = xent_grad(xa.logits[(int64_t)n * ncls + j], ls, lab == j, xg);
+      hsx[j] = d;
+      dl[(int64_t)n * ncls + j] = d;
+    }
+  }
+  head_dact_image<T>(xe ? nullptr : dl + (int64_t)n * ncls, wfc, HW, C, ncls, dact + (int64_t)n * HW * C, hsx);
 }
 
 template <typename T>
 static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int N, int HW, int C, int ncls,
-                      float scale, float* dw, float* db, T* dact, float* ws, size_t ws_bytes, hipStream_t st) {
+                      float scale, float* dw, float* db, T* dact, float* ws, size_t ws_bytes, hipStream_t st,
+                      const XentArgs* xa) {
   DTC_CHECK_ARG(dlogits && feat && wfc && dw && db && dact && N > 0 && HW > 0 && C > 0 && C % 8 == 0 && C <= 2048 &&
-                    ncls > 0 && ncls <= 4096,
+                    ncls > 0 && ncls <= 4096 && (!xa || (xa->logits && xa->labels && xa->lse)),
                 "head_bwd: bad args");
   const size_t dx_lds = (size_t)std::max(ncls + 4 * C, 4 * 260) * sizeof(float);  // head_dact_image / fused dW
   // option head_fused: 1 (default) always, 2 at most 64 images. With the dW strips summed by four waves the one
@@ -597,11 +622,12 @@ static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int
   const int hf = option_get(OPT_HEAD_FUSED);
   if (ncls <= 1024 && (hf == 1 || (hf == 2 && N <= 64))) {
     const int nw = ncls * ((C + 255) / 256);
-    hipLaunchKernelGGL(head_bwd_fused_kernel<T>, dim3(nw + N), dim3(256), dx_lds, st, dlogits, feat, wfc, N, HW, C,
-                       ncls, scale, dw, db, dact, nw);
+    hipLaunchKernelGGL(head_bwd_fused_kernel<T>, dim3(nw + N), dim3(256), dx_lds, st, (float*)dlogits, feat, wfc, N,
+                       HW, C, ncls, scale, dw, db, dact, nw, xa ? *xa : XentArgs());
     DTC_LAUNCH_CHECK();
     return 0;
   }
+  if (xa) DTC_TRY(xent_bwd(xa->logits, xa->labels, xa->lse, xa->gscale, N, ncls, (float*)dlogits, st));
   DTC_CHECK_ARG(ws && ws_bytes >= head_bwd_workspace(N, C, ncls), "head_bwd: workspace too small");
   const int splits = (N + HB_IMGS - 1) / HB_IMGS;
   hipLaunchKernelGGL(head_bwd_w_partial_kernel, dim3((C + 63) / 64, (ncls + 15) / 16, splits), dim3(256), 0, st,
@@ -615,12 +641,12 @@ static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int
   return 0;
 }
 int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int HW, int C, int ncls, float scale,
-             float* dw, float* db, u16* dact, float* ws, size_t ws_bytes, hipStream_t st) {
-  return head_bwd_t<u16>(dlogits, feat, wfc, N, HW, C, ncls, scale, dw, db, dact, ws, ws_bytes, st);
+             float* dw, float* db, u16* dact, float* ws, size_t ws_bytes, hipStream_t st, const XentArgs* xa) {
+  return head_bwd_t<u16>(dlogits, feat, wfc, N, HW, C, ncls, scale, dw, db, dact, ws, ws_bytes, st, xa);
 }
 int head_bwd(const float* dlogits, const float* feat, const float* wfc, int N, int HW, int C, int ncls, float scale,
-             float* dw, float* db, float* dact, float* ws, size_t ws_bytes, hipStream_t st) {
-  return head_bwd_t<float>(dlogits, feat, wfc, N, HW, C, ncls, scale, dw, db, dact, ws, ws_bytes, st);
+             float* dw, float* db, float* dact, float* ws, size_t ws_bytes, hipStream_t st, const XentArgs* xa) {
+  return head_bwd_t<float>(dlogits, feat, wfc, N, HW, C, ncls, scale, dw, db, dact, ws, ws_bytes, st, xa);
 }
 
 }  // namespace dtc

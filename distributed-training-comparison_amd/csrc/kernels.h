@@ -53,6 +53,8 @@ namespace dtc {
   X(BN_CG, bn_cg, 1)                    /* small BN backward as one launch (bn_bwd_cg) ...                  */ \
   X(BN_CG_ELEMS, bn_cg_elems, 262144)   /* ... for tensors of at most this many elements                    */ \
   X(HEAD_FUSED, head_fused, 1)          /* head backward in one launch: 1 always, 2 at <= 64 images */       \
+  X(XENT_FUSE, xent_fuse, 1)            /* CrossEntropyLoss backward inside the head backward kernel */     \
+  X(AMP_IN_BWD, amp_in_bwd, 1)          /* GradScaler inf check per bucket inside the backward */           \
   X(COMM_ON_SIDE, comm_on_side, 1)      /* bucket all-reduces on the weight-gradient stream (no comm stream) */ \
   X(BUCKET_TAIL, bucket_tail, 1)        /* (plan time) close the open bucket (>= 1 MB) after layer2.0 */      \
   X(WGRAD_GEN, wgrad_gen, 1)            /* wgrad_halo general step geometry (224x224 model) */                \
@@ -315,10 +317,19 @@ size_t head_bwd_workspace(int N, int C, int ncls);
 // fp32 mode: fp32 activations and fp32 Linear weights, no autocast rounding
 int head_fwd(const float* act, int N, int HW, int C, const float* wfc, const float* bfc, int ncls, float* feat,
              float* logits, hipStream_t st);
+// xa != nullptr: the CrossEntropyLoss backward is fused in -- dlogits is computed from (logits, labels,
+// lse, gscale) exactly as xent_bwd does, used directly, and also stored into `dlogits` (an output then)
+struct XentArgs {
+  const float* logits = nullptr;
+  const int64_t* labels = nullptr;
+  const float* lse = nullptr;
+  const float* gscale = nullptr;
+};
 int head_bwd(const float* dlogits, const float* feat, const float* wfc, int N, int HW, int C, int ncls, float scale,
-             float* dw, float* db, float* dact, float* ws, size_t ws_bytes, hipStream_t st);
+             float* dw, float* db, float* dact, float* ws, size_t ws_bytes, hipStream_t st,
+             const XentArgs* xa = nullptr);
 int head_bwd(const float* dlogits, const float* feat, const u16* wfc, int N, int HW, int C, int ncls, float scale,
-             float* dw, float* db, u16* dact, float* ws, size_t ws_bytes, hipStream_t st);
+             float* dw, float* db, u16* dact, float* ws, size_t ws_bytes, hipStream_t st, const XentArgs* xa = nullptr);
 
 // ------------------------------------------------------------------ optimizer / amp / casts
 // Nesterov SGD over a flat buffer (torch.optim.SGD semantics, dampening 0).

@@ -940,6 +940,38 @@ def test_native_loss_backward_matches_autograd(dtc, cuda):
     assert type(loss * 2.0) is torch.Tensor
 
 
+@pytest.mark.parametrize("head_fused", [1, 0])
+@pytest.mark.parametrize("precision,batch", [("bf16", 8), ("bf16", 64), ("fp32", 8)])
+def test_xent_fused_into_head_backward_bit_identical(dtc, cuda, head_fused, precision, batch):
+    """Option xent_fuse (default on): the CrossEntropyLoss backward is computed inside the head backward
+    kernel instead of a launch of its own. Every gradient and the executor's dlogits buffer are
+    bit-identical to the separate xent_bwd launch, for the one-launch head backward and the three-kernel
+    one (head_fused 0, where the fused call falls back to xent_bwd first), bf16 and fp32 executors."""
+    lib = dtc._native.lib
+    prev_hf = lib.dtc_get_option(b"head_fused")
+    lib.dtc_set_option(b"head_fused", head_fused)
+    try:
+        model, _, x, y = _setup(dtc, cuda, batch, seed=16)
+        crit = dtc.CrossEntropyLoss()
+        scaler = dtc.GradScaler(init_scale=256.0)
+        xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
+        out = {}
+        for fuse in (1, 0):
+            lib.dtc_set_option(b"xent_fuse", fuse)
+            with dtc.autocast(enabled=precision == "bf16"):
+                loss = crit(model(xd), yd)
+            scaler.scale(loss).backward()
+            exe = model.executor(batch, 32, 32, precision)
+            torch.cuda.synchronize()
+            out[fuse] = (model.flat.grads.clone(), exe.dlogits_buffer().clone())
+        assert torch.equal(out[1][1], out[0][1])
+        assert torch.equal(out[1][0], out[0][0])
+        assert float(out[1][1].abs().sum()) > 0
+    finally:
+        lib.dtc_set_option(b"xent_fuse", 1)
+        lib.dtc_set_option(b"head_fused", prev_hf)
+
+
 def test_second_backward_refused_and_sums_rezeroed(dtc, cuda):
     """the BN backward sums are zeroed by the training forward only. (1) The Python layer
     refuses a second backward over one forward (torch would ACCUMULATE into .grad; the kernels write);
@@ -1023,6 +1055,84 @@ def test_scaled_loss_prescaled_with_the_loss(dtc, cuda):
     assert float(s2) == float(stale) * 4.0
     s2.backward()  # the direct backward chain still applies
     assert isinstance(s2, nnmod.NativeLoss)
+
+
+@pytest.mark.parametrize("poison", [False, True])
+def test_backward_bucket_inf_check_matches_full_check(dtc, cuda, poison):
+    """GradScaler's inf / NaN check runs inside the backward, one bucket at a time as each becomes final
+    (dtc_rn18_set_amp_check): the flag it leaves equals one full pass over the final gradients, the
+    step then launches no check of its own, and a step with a NaN input is skipped (parameters
+    unchanged, scale backed off) exactly as the reference's GradScaler does (trainer.py:157-159)."""
+    from importlib import import_module
+
+    ops = import_module(dtc.__name__ + ".ops")
+    model, _, x, y = _setup(dtc, cuda, 8, seed=14)
+    crit = dtc.CrossEntropyLoss()
+    opt = dtc.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    scaler = dtc.GradScaler(init_scale=1024.0)
+    xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
+    if poison:
+        xd[3, 1, 7, 9] = float("nan")
+    for step in range(2):
+        with dtc.autocast():
+            loss = crit(model(xd), yd)
+        scaler.scale(loss).backward()
+        exe = model.executor(8, 32, 32, "bf16")
+        assert scaler._prechecked is exe and exe.amp_checked()
+        full = torch.zeros(1, dtype=torch.int32, device=cuda)
+        ops.amp_check_finite(model.flat.grads, full)
+        assert int(scaler._found_inf) == int(full) == int(poison), step
+        p0 = model.flat.params.clone()
+        scale0 = scaler.get_scale()
+        scaler.step(opt)
+        assert scaler._prechecked is None
+        assert torch.equal(p0, model.flat.params) == poison
+        scaler.update()
+        assert scaler.get_scale() == (scale0 * 0.5 if poison else scale0)
+        assert int(scaler._found_inf) == 0
+    # the autograd-engine path (no scaler hand-off) turns the in-backward check off again
+    with dtc.autocast():
+        loss = crit(model(xd), yd)
+    loss.backward(torch.ones_like(loss))  # an explicit gradient takes the autograd-engine path
+    assert not model.executor(8, 32, 32, "bf16").amp_checked()
+
+
+@pytest.mark.parametrize("on_side", [1, 0])
+def test_bucket_inf_check_reads_the_reduced_gradients(dtc, cuda, on_side):
+    """With a communicator the in-backward check must read each bucket AFTER its all-reduce: a loopback
+    communicator multiplying every bucket by 3e38 makes gradients that are finite before the collective
+    overflow after it, so the flag is set only if the check is ordered behind the collective. With the
+    collectives on the communicator's own stream (comm_on_side 0) the backward leaves the check to the
+    step (amp_checked False) and the step's full pass sees the same overflow."""
+    _graphs_prev = dtc._native.lib.dtc_get_option(b"graphs")
+    dtc._native.lib.dtc_set_option(b"graphs", 0)
+    dtc._native.lib.dtc_set_option(b"comm_on_side", on_side)
+    comm = dtc.parallel.Comm.loopback(cuda.index or 0, 3e38)
+    try:
+        model, _, x, y = _setup(dtc, cuda, 8, seed=15)
+        model.set_bucket_cap_mb(5.0)
+        crit = dtc.CrossEntropyLoss()
+        opt = dtc.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+        scaler = dtc.GradScaler(init_scale=1024.0)
+        xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
+        model._comm = comm
+        with dtc.autocast():
+            loss = crit(model(xd), yd)
+        scaler.scale(loss).backward()
+        exe = model.executor(8, 32, 32, "bf16")
+        assert exe.amp_checked() == bool(on_side)
+        p0 = model.flat.params.clone()
+        scaler.step(opt)
+        torch.cuda.synchronize()
+        assert int(scaler._found_inf) == 1
+        assert torch.equal(p0, model.flat.params)
+        scaler.update()
+        assert scaler.get_scale() == 512.0
+    finally:
+        model._comm = None
+        comm.close()
+        dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
+        dtc._native.lib.dtc_set_option(b"comm_on_side", 1)
 
 
 def test_native_loss_item_and_dlogits_buffer(dtc, cuda):
