@@ -142,8 +142,6 @@ _SIGS = {
     "dtc_rn18_forward": (i32, [vp, vp, vp, i32, vp]),
     "dtc_rn18_backward": (i32, [vp, vp, f32, vp, vp]),
     "dtc_rn18_xent_backward": (i32, [vp, vp, vp, vp, vp, f32, vp, vp]),
-    "dtc_rn18_set_amp_check": (i32, [vp, vp]),
-    "dtc_rn18_amp_checked": (i32, [vp]),
     "dtc_rn18_set_sync_bn": (i32, [vp, vp]),
     "dtc_rn18_dlogits_buffer": (i32, [vp, C.POINTER(sz)]),
 }

@@ -49,7 +49,6 @@ class GradScaler:
         self._tracker = None
         self._found_inf = None
         self._unscaled = False
-        self._prechecked = None  # executor whose last backward did this step's inf check (nn.NativeLoss)
         self._version = 0  # bumped whenever the scale may change (update): invalidates prescaled losses
 
     def _lazy_init(self, device):
@@ -77,11 +76,7 @@ class GradScaler:
             optimizer.attach(optimizer._find_flat())
             flat = optimizer._flat
         self._lazy_init(flat.grads.device)
-        exe, self._prechecked = self._prechecked, None
-        # the backward already checked every bucket of these very gradients into found_inf (after the
-        # all-reduce, overlapped with the backward); otherwise one pass over the flat gradient buffer
-        if exe is None or exe.flat is not flat or not exe.amp_checked():
-            ops.amp_check_finite(flat.grads, self._found_inf)
+        ops.amp_check_finite(flat.grads, self._found_inf)
         self._unscaled = True
 
     def step(self, optimizer, *args, **kwargs):
@@ -96,7 +91,6 @@ class GradScaler:
         if not self._enabled or self._scale is None:
             return
         self._version += 1
-        self._prechecked = None
         if new_scale is not None:
             self._scale.fill_(float(new_scale))
             self._inv_scale.fill_(1.0 / float(new_scale))

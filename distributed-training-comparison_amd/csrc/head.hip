@@ -552,7 +552,7 @@ __global__ void __launch_bounds__(256) head_bwd_x_kernel(const float* __restrict
 // XE: the CrossEntropyLoss backward fused in (xa.logits != nullptr): every dlogits value is computed where
 // it is used, by xent_grad as xent_bwd computes it, and the dact workgroups also store their image's row
 // into dl (the executor's dlogits buffer) -- one launch fewer right after the per-step barrier.
-template <typename T>
+template <typename T, bool XE>
 __global__ void __launch_bounds__(256) head_bwd_fused_kernel(float* __restrict__ dl,
                                                             const float* __restrict__ feat,
                                                             const T* __restrict__ wfc, int N, int HW, int C, int ncls,
@@ -561,7 +561,9 @@ __global__ void __launch_bounds__(256) head_bwd_fused_kernel(float* __restrict__
                                                             XentArgs xa) {
   extern __shared__ float hsx[];
   const int t = threadIdx.x;
-  const bool xe = xa.logits != nullptr;
+  // (a template parameter, not a runtime test: a branch inside the image loop below kept the compiler
+  // from batching its loads -- 26.6 vs 10.9 us per launch at batch 256)
+  constexpr bool xe = XE;
   const float xg = xe ? xent_gain(xa.gscale, N) : 0.f;
   if ((int)blockIdx.x < nw) {
     // dW[j][c..c+3] (float4 of feat per lane) and db[j]: wave w sums the images n = w, w + 4, ... (eight
@@ -570,11 +572,31 @@ __global__ void __launch_bounds__(256) head_bwd_fused_kernel(float* __restrict__
     const int j = blockIdx.x / strips, cb = (blockIdx.x - j * strips) * 256;
     const int wv = t >> 6, l = t & 63, c = cb + l * 4;
     float a[4] = {0.f, 0.f, 0.f, 0.f}, b = 0.f;
-    if (c < C) {
+    if constexpr (XE) {
+      // dlogits column j for 256 images at a time into LDS (one image per thread: the gather of logits,
+      // lse and labels is spread over the workgroup instead of serialised in each wave's image loop),
+      // then the same per-wave image order n = wv, wv + 4, ... as below
+      float* dcol = hsx + 4 * 260;
+      for (int n0 = 0; n0 < N; n0 += 256) {
+        const int nn = min(256, N - n0);
+        if (t < nn) dcol[t] = xent_grad(xa.logits[(int64_t)(n0 + t) * ncls + j], xa.lse[n0 + t], xa.labels[n0 + t] == j, xg);
+        __syncthreads();
+        if (c < C) {
+#pragma unroll 8
+          for (int i = wv; i < nn; i += 4) {
+            const float d = dcol[i];
+            const f32x4 f = *(const f32x4*)(feat + (int64_t)(n0 + i) * C + c);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) a[k] += d * f[k];
+            b += d;
+          }
+        }
+        __syncthreads();
+      }
+    } else if (c < C) {
 #pragma unroll 8
       for (int n = wv; n < N; n += 4) {
-        const float d = xe ? xent_grad(xa.logits[(int64_t)n * ncls + j], xa.lse[n], xa.labels[n] == j, xg)
-                           : dl[(int64_t)n * ncls + j];
+        const float d = dl[(int64_t)n * ncls + j];
         const f32x4 f = *(const f32x4*)(feat + (int64_t)n * C + c);
 #pragma unroll
         for (int k = 0; k < 4; ++k) a[k] += d * f[k];
@@ -597,7 +619,7 @@ __global__ void __launch_bounds__(256) head_bwd_fused_kernel(float* __restrict__
     return;
   }
   const int n = blockIdx.x - nw;
-  if (xe) {
+  if constexpr (XE) {
     const float ls = xa.lse[n];
     const int64_t lab = xa.labels[n];
     for (int j = t; j < ncls; j += 256) {
@@ -616,14 +638,19 @@ static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int
   DTC_CHECK_ARG(dlogits && feat && wfc && dw && db && dact && N > 0 && HW > 0 && C > 0 && C % 8 == 0 && C <= 2048 &&
                     ncls > 0 && ncls <= 4096 && (!xa || (xa->logits && xa->labels && xa->lse)),
                 "head_bwd: bad args");
-  const size_t dx_lds = (size_t)std::max(ncls + 4 * C, 4 * 260) * sizeof(float);  // head_dact_image / fused dW
+  // head_dact_image / fused dW (+ the fused-xent dlogits column)
+  const size_t dx_lds = (size_t)std::max(ncls + 4 * C, 4 * 260 + 256) * sizeof(float);
   // option head_fused: 1 (default) always, 2 at most 64 images. With the dW strips summed by four waves the one
   // launch is faster at batch 256 too (+0.45%, 4-round A/B r04m; the round-3 sequential strip loop was 1% slower)
   const int hf = option_get(OPT_HEAD_FUSED);
   if (ncls <= 1024 && (hf == 1 || (hf == 2 && N <= 64))) {
     const int nw = ncls * ((C + 255) / 256);
-    hipLaunchKernelGGL(head_bwd_fused_kernel<T>, dim3(nw + N), dim3(256), dx_lds, st, (float*)dlogits, feat, wfc, N,
-                       HW, C, ncls, scale, dw, db, dact, nw, xa ? *xa : XentArgs());
+    if (xa)
+      hipLaunchKernelGGL((head_bwd_fused_kernel<T, true>), dim3(nw + N), dim3(256), dx_lds, st, (float*)dlogits, feat,
+                         wfc, N, HW, C, ncls, scale, dw, db, dact, nw, *xa);
+    else
+      hipLaunchKernelGGL((head_bwd_fused_kernel<T, false>), dim3(nw + N), dim3(256), dx_lds, st, (float*)dlogits, feat,
+                         wfc, N, HW, C, ncls, scale, dw, db, dact, nw, XentArgs());
     DTC_LAUNCH_CHECK();
     return 0;
   }

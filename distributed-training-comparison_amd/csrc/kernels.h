@@ -54,7 +54,6 @@ namespace dtc {
   X(BN_CG_ELEMS, bn_cg_elems, 262144)   /* ... for tensors of at most this many elements                    */ \
   X(HEAD_FUSED, head_fused, 1)          /* head backward in one launch: 1 always, 2 at <= 64 images */       \
   X(XENT_FUSE, xent_fuse, 1)            /* CrossEntropyLoss backward inside the head backward kernel */     \
-  X(AMP_IN_BWD, amp_in_bwd, 1)          /* GradScaler inf check per bucket inside the backward */           \
   X(COMM_ON_SIDE, comm_on_side, 1)      /* bucket all-reduces on the weight-gradient stream (no comm stream) */ \
   X(BUCKET_TAIL, bucket_tail, 1)        /* (plan time) close the open bucket (>= 1 MB) after layer2.0 */      \
   X(WGRAD_GEN, wgrad_gen, 1)            /* wgrad_halo general step geometry (224x224 model) */                \

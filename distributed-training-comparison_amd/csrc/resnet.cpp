@@ -103,12 +103,6 @@ struct Net {
   // buckets: [offset, numel) in flat elements, and the block index after whose backward it fires
   std::vector<int64_t> bucket_off, bucket_len;
   std::vector<int> bucket_after_block;  // -1 = after the stem (last)
-  // GradScaler's inf / NaN check (dtc_rn18_set_amp_check): each bucket's gradients are checked into
-  // amp_found as soon as they are final (after the bucket's all-reduce), overlapped with the rest of the
-  // backward instead of one pass over every gradient between backward and step; amp_n counts the buckets
-  // the last backward checked (all of them: dtc_rn18_amp_checked)
-  int* amp_found = nullptr;
-  int amp_n = 0;
   // dtc_rn18_xent_backward with option xent_fuse: the CrossEntropyLoss backward's inputs, consumed by the
   // head backward kernel (one launch fewer after the per-step barrier); set only for that call
   XentArgs xent;
@@ -953,17 +947,8 @@ struct BwdCtx {
 };
 static int join_side(Net& n, hipStream_t st);
 static int next_event(Net& n, hipEvent_t* ev);
-static int amp_check_buckets(Net& n, const std::vector<int>& ids, hipStream_t s) {
-  for (int i : ids) {
-    DTC_TRY(amp_check_finite(n.g + n.bucket_off[i], n.bucket_len[i], n.amp_found, s));
-    ++n.amp_n;
-  }
-  return 0;
-}
 static int maybe_bucket(Net& n, int after_block, const BwdCtx& cx, hipStream_t st) {
-  // (graph segments: the step's full check)
-  const bool amp = n.amp_found != nullptr && !cx.capturing && option_get(OPT_AMP_IN_BWD) != 0;
-  if (!cx.comm && !amp) return 0;
+  if (!cx.comm) return 0;
   std::vector<int> ids;
   for (size_t i = 0; i < n.bucket_off.size(); ++i)
     if (n.bucket_after_block[i] == after_block) ids.push_back((int)i);
@@ -982,7 +967,6 @@ static int maybe_bucket(Net& n, int after_block, const BwdCtx& cx, hipStream_t s
       DTC_HIP(hipStreamWaitEvent(n.side_st, ev, 0));
       prod = n.side_st;
     }
-    if (!cx.comm) return amp_check_buckets(n, ids, prod);  // one rank: the gradients are final here
     // option comm_on_side: the collective on the weight-gradient stream itself (it holds both producers
     // now; the stream is joined into the compute stream at the end of the backward) -- one HIP stream
     // fewer competing for the process's hardware queues (GPU_MAX_HW_QUEUES); the weight gradients of
@@ -1005,9 +989,6 @@ static int maybe_bucket(Net& n, int after_block, const BwdCtx& cx, hipStream_t s
         DTC_TRY(comm_allreduce_on(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], prod, t0, t1));
       else DTC_TRY(comm_allreduce_async(cx.comm, n.g + n.bucket_off[i], (size_t)n.bucket_len[i], prod, t0, t1));
     }
-    // the check reads the summed gradients: behind the collective on its own stream (a collective on the
-    // communicator's stream leaves the bucket unchecked, and the step's full check runs instead)
-    if (amp && (on_side || inline_tail)) DTC_TRY(amp_check_buckets(n, ids, prod));
     return 0;
   }
   DTC_TRY(join_side(n, st));  // a graph segment ends here: every stream forked in it joins back
@@ -1524,7 +1505,6 @@ static int backward(Net& n, const float* dlogits, float gs, Comm* comm, hipStrea
 }
 static int backward_impl(Net& n, const float* dlogits, float gs, Comm* comm, hipStream_t st) {
   n.prof_st = st;
-  n.amp_n = 0;
   if (!n.sums_fresh) DTC_TRY(zero_bytes(n.ws + n.acc_lo, n.stats_hi - n.acc_lo, st));
   n.sums_fresh = false;
   if (!graphs_on(n, true, comm != nullptr)) {
@@ -1958,18 +1938,6 @@ int dtc_rn18_forward(dtc_net* net, const float* x, float* logits, int train, voi
 int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_comm* comm, void* stream) {
   DTC_CHECK_ARG(net && net->n.ws && dlogits, "dtc_rn18_backward: unbound net or null pointer");
   return backward(net->n, dlogits, grad_scale, (Comm*)comm, (hipStream_t)stream);
-}
-
-int dtc_rn18_set_amp_check(dtc_net* net, int* found_inf) {
-  DTC_CHECK_ARG(net, "dtc_rn18_set_amp_check: null net");
-  net->n.amp_found = found_inf;
-  return 0;
-}
-
-int dtc_rn18_amp_checked(const dtc_net* net) {
-  if (!net) return DTC_EINVAL;
-  const dtc::Net& n = net->n;
-  return n.amp_found && !n.bucket_off.empty() && n.amp_n == (int)n.bucket_off.size() ? 1 : 0;
 }
 
 int dtc_rn18_xent_backward(dtc_net* net, const float* logits, const int64_t* labels, const float* lse,

@@ -140,7 +140,6 @@ class Executor:
         self.generation = 0
         self._bwd_gen = 0  # generation whose forward a backward has consumed (one backward per forward)
         self._dlogits = None
-        self._amp_found = None  # the found_inf tensor the backward checks gradients into (set_amp_check)
         call("dtc_rn18_bind", self.handle, self.ws_ptr, ptr(flat.params), ptr(flat.grads), ptr(flat.params_bf16),
              ptr(flat.bufs), ptr(flat.nbt), stream_ptr())
 
@@ -162,18 +161,6 @@ class Executor:
                               "would accumulate gradients in torch; the native kernels write them): run "
                               "the forward again")
         self._bwd_gen = gen
-
-    def set_amp_check(self, found_inf: Optional[torch.Tensor]) -> None:
-        """GradScaler's inf check inside the backward (dtc_rn18_set_amp_check): each gradient bucket is
-        checked into `found_inf` once final, overlapped with the rest of the backward. A ctypes call
-        only when the tensor changes (this runs after the per-step barrier)."""
-        if found_inf is not self._amp_found:
-            call("dtc_rn18_set_amp_check", self.handle, None if found_inf is None else ptr(found_inf))
-            self._amp_found = found_inf
-
-    def amp_checked(self) -> bool:
-        """True when the last backward checked every gradient bucket into the registered found_inf."""
-        return self._amp_found is not None and lib.dtc_rn18_amp_checked(self.handle) == 1
 
     def backward(self, dlogits: torch.Tensor, grad_scale: float, comm) -> None:
         call("dtc_rn18_backward", self.handle, ptr(dlogits), float(grad_scale), comm.handle if comm else None,
@@ -252,7 +239,6 @@ class _NetFn(torch.autograd.Function):
         if model._pre_backward is not None:
             model._pre_backward()
         exe.consume(ctx.gen)
-        exe.set_amp_check(None)
         exe.backward(dlogits.contiguous().float(), model._grad_scale, model._comm)
         model._ensure_grads()
         return None, None, None, None
@@ -343,14 +329,7 @@ class NativeLoss(torch.Tensor):
             if model._pre_backward is not None:
                 model._pre_backward()
             exe.consume(node.gen)
-            # a loss scaled by the live GradScaler: the backward does the scaler's inf check per bucket
-            sc = _prescaler() if gscale is not None else None
-            if sc is not None and sc._scale is not gscale:
-                sc = None
-            exe.set_amp_check(None if sc is None else sc._found_inf)
             exe.xent_backward(logits, labels, lse, gscale, model._grad_scale, model._comm)
-            if sc is not None:
-                sc._prechecked = exe
             model._ensure_grads()
         else:  # DataParallel's gathered logits: xent backward, then the replicas' backward + reduce-add
             from .parallel import _DPFn

@@ -327,16 +327,6 @@ int dtc_rn18_backward(dtc_net* net, const float* dlogits, float grad_scale, dtc_
  * communicator of its own, not the one passed to dtc_rn18_backward. Disables graph replay.
  * comm == NULL: per-rank statistics (the reference's BatchNorm2d). */
 int dtc_rn18_set_sync_bn(dtc_net* net, dtc_comm* comm);
-/* GradScaler's inf / NaN check folded into the backward (the reference's scaler.step(optimizer),
- * ddp/trainer.py:158, checks every gradient after the DDP all-reduce before the update): with
- * found_inf != NULL every later backward checks each gradient bucket once it is final (after its
- * all-reduce) and sets *found_inf = 1 (device int32, never cleared here) on any non-finite value,
- * overlapped with the rest of the backward. NULL turns it off. dtc_rn18_amp_checked(): 1 when the
- * last backward checked every bucket (then the step needs no dtc_amp_check_finite pass of its own),
- * 0 when it did not (graph-replayed backward, collectives on the communicator's own stream, no
- * found_inf registered). */
-int dtc_rn18_set_amp_check(dtc_net* net, int* found_inf);
-int dtc_rn18_amp_checked(const dtc_net* net);
 /* CrossEntropyLoss backward fused with the network backward (the reference's
  * `scaler.scale(loss).backward()`, ddp/trainer.py:157, when the loss is nn.CrossEntropyLoss of the
  * network's logits, trainer.py:40,155): dlogits = (softmax(logits) - onehot(labels)) * (*gscale) / N

@@ -1057,84 +1057,6 @@ def test_scaled_loss_prescaled_with_the_loss(dtc, cuda):
     assert isinstance(s2, nnmod.NativeLoss)
 
 
-@pytest.mark.parametrize("poison", [False, True])
-def test_backward_bucket_inf_check_matches_full_check(dtc, cuda, poison):
-    """GradScaler's inf / NaN check runs inside the backward, one bucket at a time as each becomes final
-    (dtc_rn18_set_amp_check): the flag it leaves equals one full pass over the final gradients, the
-    step then launches no check of its own, and a step with a NaN input is skipped (parameters
-    unchanged, scale backed off) exactly as the reference's GradScaler does (trainer.py:157-159)."""
-    from importlib import import_module
-
-    ops = import_module(dtc.__name__ + ".ops")
-    model, _, x, y = _setup(dtc, cuda, 8, seed=14)
-    crit = dtc.CrossEntropyLoss()
-    opt = dtc.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
-    scaler = dtc.GradScaler(init_scale=1024.0)
-    xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
-    if poison:
-        xd[3, 1, 7, 9] = float("nan")
-    for step in range(2):
-        with dtc.autocast():
-            loss = crit(model(xd), yd)
-        scaler.scale(loss).backward()
-        exe = model.executor(8, 32, 32, "bf16")
-        assert scaler._prechecked is exe and exe.amp_checked()
-        full = torch.zeros(1, dtype=torch.int32, device=cuda)
-        ops.amp_check_finite(model.flat.grads, full)
-        assert int(scaler._found_inf) == int(full) == int(poison), step
-        p0 = model.flat.params.clone()
-        scale0 = scaler.get_scale()
-        scaler.step(opt)
-        assert scaler._prechecked is None
-        assert torch.equal(p0, model.flat.params) == poison
-        scaler.update()
-        assert scaler.get_scale() == (scale0 * 0.5 if poison else scale0)
-        assert int(scaler._found_inf) == 0
-    # the autograd-engine path (no scaler hand-off) turns the in-backward check off again
-    with dtc.autocast():
-        loss = crit(model(xd), yd)
-    loss.backward(torch.ones_like(loss))  # an explicit gradient takes the autograd-engine path
-    assert not model.executor(8, 32, 32, "bf16").amp_checked()
-
-
-@pytest.mark.parametrize("on_side", [1, 0])
-def test_bucket_inf_check_reads_the_reduced_gradients(dtc, cuda, on_side):
-    """With a communicator the in-backward check must read each bucket AFTER its all-reduce: a loopback
-    communicator multiplying every bucket by 3e38 makes gradients that are finite before the collective
-    overflow after it, so the flag is set only if the check is ordered behind the collective. With the
-    collectives on the communicator's own stream (comm_on_side 0) the backward leaves the check to the
-    step (amp_checked False) and the step's full pass sees the same overflow."""
-    _graphs_prev = dtc._native.lib.dtc_get_option(b"graphs")
-    dtc._native.lib.dtc_set_option(b"graphs", 0)
-    dtc._native.lib.dtc_set_option(b"comm_on_side", on_side)
-    comm = dtc.parallel.Comm.loopback(cuda.index or 0, 3e38)
-    try:
-        model, _, x, y = _setup(dtc, cuda, 8, seed=15)
-        model.set_bucket_cap_mb(5.0)
-        crit = dtc.CrossEntropyLoss()
-        opt = dtc.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
-        scaler = dtc.GradScaler(init_scale=1024.0)
-        xd, yd = torch.from_numpy(x).to(cuda), torch.from_numpy(y).to(cuda)
-        model._comm = comm
-        with dtc.autocast():
-            loss = crit(model(xd), yd)
-        scaler.scale(loss).backward()
-        exe = model.executor(8, 32, 32, "bf16")
-        assert exe.amp_checked() == bool(on_side)
-        p0 = model.flat.params.clone()
-        scaler.step(opt)
-        torch.cuda.synchronize()
-        assert int(scaler._found_inf) == 1
-        assert torch.equal(p0, model.flat.params)
-        scaler.update()
-        assert scaler.get_scale() == 512.0
-    finally:
-        model._comm = None
-        comm.close()
-        dtc._native.lib.dtc_set_option(b"graphs", _graphs_prev)
-        dtc._native.lib.dtc_set_option(b"comm_on_side", 1)
-
-
 def test_native_loss_item_and_dlogits_buffer(dtc, cuda):
     """NativeLoss.item() reads the pinned host copy taken right after the loss kernel: equal to the
     device value even when read after the backward and the optimizer step have been issued; the

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=3, help="untimed steps after every option switch")
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--sim-world", type=int, default=1,
+                    help="one rank of a W-rank job (bench.py --sim-world): 1/W pre-scale, bucket all-reduces "
+                         "through the one-rank RCCL communicator")
     ap.add_argument("sets", nargs="+")
     args = ap.parse_args()
     rank, world, local = bench.init_dist(1)
@@ -39,6 +42,9 @@ def main():
 
     torch.manual_seed(42)
     model = dtc.DDP(dtc.ResNet18().to(dev), device_ids=[local], find_unused_parameters=True, bucket_cap_mb=25.0)
+    if args.sim_world > 1:
+        model.module._comm = model.comm
+        model.module._grad_scale = 1.0 / args.sim_world
     crit = dtc.CrossEntropyLoss()
     opt = dtc.SGD(model.parameters(), lr=0.1, weight_decay=1e-4, momentum=0.9, nesterov=True)
     scaler = dtc.GradScaler()
