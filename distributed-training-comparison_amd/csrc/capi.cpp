@@ -12,6 +12,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <execinfo.h>
 #include <pthread.h>
 #include <signal.h>
@@ -86,7 +87,13 @@ using namespace dtc;
 // signal to the previous handler (Python's faulthandler prints the Python threads). faulthandler alone
 // cannot say in which native thread -- ours or a runtime worker -- a fault happened.
 static struct sigaction g_prev_sa[32];
-static void put(const char* s) { (void)!write(2, s, strlen(s)); }
+// the report also goes to the file DTC_CRASH_LOG names (opened at install): under pytest's fd capture, fd 2 of a
+// test is a temporary file that is lost with the process (r06s: a SIGSEGV left only faulthandler's frames)
+static int g_crash_fd = -1;
+static void put(const char* s) {
+  (void)!write(2, s, strlen(s));
+  if (g_crash_fd >= 0) (void)!write(g_crash_fd, s, strlen(s));
+}
 static void put_hex(uintptr_t v) {
   char b[19] = "0x";
   for (int i = 0; i < 16; ++i) b[2 + i] = "0123456789abcdef"[(v >> (60 - 4 * i)) & 15];
@@ -181,6 +188,7 @@ int dtc_install_crash_handler(void) {
   if (once.exchange(1)) return 0;
   void* warm[2];
   (void)backtrace(warm, 2);  // loads the unwinder now, not inside the handler
+  if (const char* path = getenv("DTC_CRASH_LOG")) g_crash_fd = open(path, O_WRONLY | O_CREAT | O_APPEND, 0644);
   static char altstack[1 << 16];
   stack_t ss;
   ss.ss_sp = altstack;

@@ -24,7 +24,10 @@ def cuda(dtc):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    # a native fault prints the faulting thread and its frames (then Python's faulthandler runs)
+    # a native fault prints the faulting thread and its frames (then Python's faulthandler runs), also into
+    # gpurun_out/dtc_crash.log: pytest's fd capture loses what a dying test wrote to fd 2
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    os.environ.setdefault("DTC_CRASH_LOG", os.path.join(ROOT, "gpurun_out", "dtc_crash.log"))
     dtc._native.lib.dtc_install_crash_handler()
     return torch.device("cuda:0")
 
