@@ -97,7 +97,7 @@ int cifar_augment(const uint8_t* images, const int64_t* targets, int64_t n_image
   DTC_CHECK_ARG(!labels || targets, "cifar_augment: labels requested without targets");
   DTC_CHECK_ARG(stdv[0] != 0.f && stdv[1] != 0.f && stdv[2] != 0.f, "cifar_augment: zero std");
   const int imgs = (int)std::max<int64_t>(1, std::min<int64_t>(AUG_IMGS, AUG_MAX_BYTES / ((int64_t)h * w * 3)));
-  hipLaunchKernelGGL(cifar_augment_kernel, dim3((n + imgs - 1) / imgs), dim3(256), 0, st, images, targets, n_images,
+  DTC_KLAUNCH(cifar_augment_kernel, dim3((n + imgs - 1) / imgs), dim3(256), 0, st, images, targets, n_images,
                      index, crop, flip, n, h, w, pad, imgs, mean[0], mean[1], mean[2], stdv[0], stdv[1], stdv[2], out,
                      labels, status);
   DTC_LAUNCH_CHECK();

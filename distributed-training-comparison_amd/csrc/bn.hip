@@ -79,7 +79,7 @@ int bn_fwd_finalize(int64_t* stats, int C, int64_t count, const float* gamma, co
                     float* scale, float* shift, hipStream_t st) {
   DTC_CHECK_ARG(stats && gamma && beta && mean && invstd && scale && shift && C > 0 && count > 0,
                 "bn_fwd_finalize: bad args");
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(ceil_div_i(C, FIN_CH)), dim3(256), 0, st, stats, C, (double)count,
+  DTC_KLAUNCH(bn_fwd_finalize_kernel, dim3(ceil_div_i(C, FIN_CH)), dim3(256), 0, st, stats, C, (double)count,
                      gamma, beta, running_mean, running_var, num_batches, momentum, eps, mean, invstd, scale, shift);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -103,7 +103,7 @@ int bn_eval_coef(int C, const float* gamma, const float* beta, const float* runn
                  float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st) {
   DTC_CHECK_ARG(gamma && beta && running_mean && running_var && mean && invstd && scale && shift && C > 0,
                 "bn_eval_coef: bad args");
-  hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(ceil_div_i(C, 256)), dim3(256), 0, st, C, gamma, beta, running_mean,
+  DTC_KLAUNCH(bn_eval_coef_kernel, dim3(ceil_div_i(C, 256)), dim3(256), 0, st, C, gamma, beta, running_mean,
                      running_var, eps, mean, invstd, scale, shift);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -161,7 +161,7 @@ static int launch_apply(const T* x, const float* s, const float* h, const T* x2,
   DTC_CHECK_ARG(x && s && h && y && C % 8 == 0 && M > 0, "bn_apply: bad args (C=%d)", C);
   const int64_t nvec = M * C / 8;
   const int blocks = (int)std::min<int64_t>(4096, (nvec + 255) / 256);
-  hipLaunchKernelGGL((bn_apply_kernel<MODE, T>), dim3(blocks), dim3(256), 0, st, x, s, h, x2, s2, h2, y, nvec, C / 8);
+  DTC_KLAUNCH((bn_apply_kernel<MODE, T>), dim3(blocks), dim3(256), 0, st, x, s, h, x2, s2, h2, y, nvec, C / 8);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -287,15 +287,15 @@ static int fin_apply(int mode, const T* x, const BnFwdArgs& a1, const T* x2, con
   const BnFwdArgs none{};
   switch (mode) {
     case APPLY_RELU:
-      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows, mask, ts);
+      DTC_KLAUNCH((bn_fin_apply_kernel<APPLY_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows, mask, ts);
       break;
     case APPLY_ADD_RELU:
       DTC_CHECK_ARG(x2 != nullptr, "bn_fin_apply: residual required");
-      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_ADD_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows, mask, ts);
+      DTC_KLAUNCH((bn_fin_apply_kernel<APPLY_ADD_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, none, y, M, C, rows, mask, ts);
       break;
     default:
       DTC_CHECK_ARG(x2 && a2 && a2->stats, "bn_fin_apply: second branch required");
-      hipLaunchKernelGGL((bn_fin_apply_kernel<APPLY_DUAL_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, *a2, y, M, C, rows, mask, ts);
+      DTC_KLAUNCH((bn_fin_apply_kernel<APPLY_DUAL_RELU, T>), grid, dim3(256), 0, st, x, a1, x2, *a2, y, M, C, rows, mask, ts);
       break;
   }
   DTC_LAUNCH_CHECK();
@@ -398,7 +398,7 @@ static int bwd_fin_apply(const T* dz, const T* x1, const BnBwdArgs& a1, T* dx1, 
   const BnBwdArgs none{};
   if (x2) DTC_CHECK_ARG(a2 && a2->acc && dx2, "bn_bwd_fin_apply: dual branch args");
 #define DTC_BFA(D_, M_) \
-  hipLaunchKernelGGL((bn_bwd_fin_apply_kernel<D_, M_, T>), grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, D_ ? *a2 : none, \
+  DTC_KLAUNCH((bn_bwd_fin_apply_kernel<D_, M_, T>), grid, dim3(256), 0, st, dz, x1, a1, dx1, x2, D_ ? *a2 : none, \
                      dx2, M, C, rows, mbits, dzo, ts)
   if (x2 && mbits) DTC_BFA(true, true);
   else if (x2) DTC_BFA(true, false);
@@ -568,10 +568,10 @@ int bn_bwd_cg(const u16* dy, const uint8_t* mbits, u16* dzo, const u16* x1, cons
   DTC_CHECK_ARG(!x2 || (a2 && a2->gamma && a2->mean && a2->invstd && dx2), "bn_bwd_cg: dual branch args");
   const BnBwdArgs none{};
   if (x2)
-    hipLaunchKernelGGL(bn_bwd_cg_kernel<true>, dim3(C / 8), dim3(CG_THREADS), 0, st, dy, mbits, dzo, x1, a1, dx1, x2,
+    DTC_KLAUNCH(bn_bwd_cg_kernel<true>, dim3(C / 8), dim3(CG_THREADS), 0, st, dy, mbits, dzo, x1, a1, dx1, x2,
                        *a2, dx2, (int)M, C, ts);
   else
-    hipLaunchKernelGGL(bn_bwd_cg_kernel<false>, dim3(C / 8), dim3(CG_THREADS), 0, st, dy, mbits, dzo, x1, a1, dx1,
+    DTC_KLAUNCH(bn_bwd_cg_kernel<false>, dim3(C / 8), dim3(CG_THREADS), 0, st, dy, mbits, dzo, x1, a1, dx1,
                        nullptr, none, nullptr, (int)M, C, ts);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -701,10 +701,12 @@ static int bwd_reduce(const T* dy, const T* ymask, const T* x1, const float* mea
   if (dual) DTC_CHECK_ARG(mean2 && invstd2 && acc2, "bn_bwd_reduce: dual branch args");
   const bool ru1 = option_get(OPT_BN_RED_UNROLL) <= 1;  // as the mask-bit path: 1 = the load-use loop
 #define DTC_BR(MK_, D_)                                                                                          \
-  if (ru1) hipLaunchKernelGGL((bn_bwd_reduce_kernel<MK_, D_, T, false, 1>), dim3(blocks), dim3(256), 0, st, dy,  \
-                              ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb);    \
-  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<MK_, D_, T, false, 4>), dim3(blocks), dim3(256), 0, st, dy,      \
-                          ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb)
+  if (ru1) DTC_KLAUNCH((bn_bwd_reduce_kernel<MK_, D_, T, false, 1>), dim3(blocks), dim3(256), 0, st, dy,  \
+                              ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb,     \
+                              (const uint8_t*)nullptr, (u64*)nullptr);                                          \
+  else DTC_KLAUNCH((bn_bwd_reduce_kernel<MK_, D_, T, false, 4>), dim3(blocks), dim3(256), 0, st, dy,      \
+                          ymask, x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, dz, M, C, (int)rpb,         \
+                          (const uint8_t*)nullptr, (u64*)nullptr)
   if (ymask && dual) { DTC_BR(true, true); }
   else if (ymask) { DTC_BR(true, false); }
   else if (dual) { DTC_BR(false, true); }
@@ -730,7 +732,7 @@ int bn_bwd_reduce_mask(const u16* dy, const uint8_t* mbits, const u16* x1, const
   if (x2) DTC_CHECK_ARG(mean2 && invstd2 && acc2, "bn_bwd_reduce_mask: dual branch args");
   const int ru = option_get(OPT_BN_RED_UNROLL);
 #define DTC_BRM(D_, R_)                                                                                            \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, D_, u16, true, R_>), dim3(blocks), dim3(256), 0, st, dy, nullptr, \
+  DTC_KLAUNCH((bn_bwd_reduce_kernel<false, D_, u16, true, R_>), dim3(blocks), dim3(256), 0, st, dy, nullptr, \
                      x1, mean1, invstd1, acc1, x2, mean2, invstd2, acc2, nullptr, M, C, (int)rpb, mbits, ts)
   if (x2) {
     if (ru <= 1) DTC_BRM(true, 1);
@@ -761,7 +763,7 @@ __global__ void __launch_bounds__(256) bn_mask_apply_kernel(const u16* __restric
 int bn_mask_apply(const u16* dy, const uint8_t* mbits, u16* dz, int64_t M, int C, hipStream_t st) {
   DTC_CHECK_ARG(dy && mbits && dz && C % 8 == 0 && M > 0, "bn_mask_apply: bad args");
   const int64_t nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_mask_apply_kernel, dim3((unsigned)std::min<int64_t>(4096, (nvec + 255) / 256)), dim3(256), 0, st,
+  DTC_KLAUNCH(bn_mask_apply_kernel, dim3((unsigned)std::min<int64_t>(4096, (nvec + 255) / 256)), dim3(256), 0, st,
                      dy, mbits, dz, nvec);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -800,7 +802,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
 int bn_bwd_finalize(int64_t* acc, int C, int64_t count, const float* gamma, const float* mean, const float* invstd,
                     float gscale, float* dgamma, float* dbeta, float* coef, hipStream_t st) {
   DTC_CHECK_ARG(acc && gamma && mean && invstd && coef && C > 0 && count > 0, "bn_bwd_finalize: bad args");
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div_i(C, FIN_CH)), dim3(256), 0, st, acc, C, (double)count, gamma,
+  DTC_KLAUNCH(bn_bwd_finalize_kernel, dim3(ceil_div_i(C, FIN_CH)), dim3(256), 0, st, acc, C, (double)count, gamma,
                      mean, invstd, gscale, dgamma, dbeta, coef);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -838,10 +840,10 @@ static int bwd_apply(const T* dz, const T* x1, const float* coef1, T* dx1, const
   const int blocks = (int)std::min<int64_t>(4096, (nvec + 255) / 256);
   if (x2) {
     DTC_CHECK_ARG(coef2 && dx2, "bn_bwd_apply: dual branch args");
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, T>), dim3(blocks), dim3(256), 0, st, dz, x1, coef1, dx1, x2, coef2, dx2,
+    DTC_KLAUNCH((bn_bwd_apply_kernel<true, T>), dim3(blocks), dim3(256), 0, st, dz, x1, coef1, dx1, x2, coef2, dx2,
                        nvec, C);
   } else {
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, T>), dim3(blocks), dim3(256), 0, st, dz, x1, coef1, dx1, x2, coef2,
+    DTC_KLAUNCH((bn_bwd_apply_kernel<false, T>), dim3(blocks), dim3(256), 0, st, dz, x1, coef1, dx1, x2, coef2,
                        dx2, nvec, C);
   }
   DTC_LAUNCH_CHECK();
@@ -880,7 +882,7 @@ __global__ void bn_fold_slots_kernel(int64_t* __restrict__ st, int C) {
 
 int bn_fold_slots(int64_t* slots, int C, hipStream_t st) {
   DTC_CHECK_ARG(slots && C > 0, "bn_fold_slots: bad args");
-  hipLaunchKernelGGL(bn_fold_slots_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, slots, C);
+  DTC_KLAUNCH(bn_fold_slots_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, slots, C);
   DTC_LAUNCH_CHECK();
   return 0;
 }

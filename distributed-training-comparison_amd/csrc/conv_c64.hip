@@ -487,9 +487,9 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   const int kmode = mode == CONV_FWD ? 0 : (res == nullptr ? 1 : 2);
   const bool pf = option_get(OPT_C64_PF) != 0;
 #define DTC_C64(M_)                                                                                \
-  if (gen) hipLaunchKernelGGL((conv_c64_kernel<M_, true, true>), dim3(grid), dim3(256), 0, st, p); \
-  else if (pf) hipLaunchKernelGGL((conv_c64_kernel<M_, true>), dim3(grid), dim3(256), 0, st, p);   \
-  else hipLaunchKernelGGL((conv_c64_kernel<M_, false>), dim3(grid), dim3(256), 0, st, p)
+  if (gen) DTC_KLAUNCH((conv_c64_kernel<M_, true, true>), dim3(grid), dim3(256), 0, st, p); \
+  else if (pf) DTC_KLAUNCH((conv_c64_kernel<M_, true>), dim3(grid), dim3(256), 0, st, p);   \
+  else DTC_KLAUNCH((conv_c64_kernel<M_, false>), dim3(grid), dim3(256), 0, st, p)
   switch (kmode) {
     case 0: DTC_C64(0); break;
     case 1: DTC_C64(1); break;

@@ -302,14 +302,14 @@ __global__ void f32_stem_pack_weight_kernel(const float* __restrict__ w27, float
 int f32_stem_im2col(const float* x, float* cols, int N, int H, int W, hipStream_t st) {
   DTC_CHECK_ARG(x && cols && N > 0 && H > 0 && W > 0, "f32_stem_im2col: bad args");
   const int64_t M = (int64_t)N * H * W;
-  hipLaunchKernelGGL(f32_stem_im2col_kernel, dim3((int)((M + 255) / 256)), dim3(256), 0, st, x, cols, N, H, W);
+  DTC_KLAUNCH(f32_stem_im2col_kernel, dim3((int)((M + 255) / 256)), dim3(256), 0, st, x, cols, N, H, W);
   DTC_LAUNCH_CHECK();
   return 0;
 }
 
 int f32_stem_pack_weight(const float* w27, float* w32, int K, hipStream_t st) {
   DTC_CHECK_ARG(w27 && w32 && K > 0, "f32_stem_pack_weight: bad args");
-  hipLaunchKernelGGL(f32_stem_pack_weight_kernel, dim3((K * 32 + 255) / 256), dim3(256), 0, st, w27, w32, K);
+  DTC_KLAUNCH(f32_stem_pack_weight_kernel, dim3((K * 32 + 255) / 256), dim3(256), 0, st, w27, w32, K);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -357,7 +357,7 @@ int conv_f32(const ConvShape& s, int mode, const float* a, const float* b, float
     p.fd_q = make_fastdiv(p.Q); p.fd_pq = make_fastdiv(p.P * p.Q);
     p.steps_per_split = (int)((p.red + F32_KS - 1) / F32_KS);
     dim3 grid(ceil_div_f(p.M, F32_BM) * ceil_div_f(p.NC, F32_BN), 1);
-    hipLaunchKernelGGL(conv_f32_kernel<F32_FWD>, grid, dim3(256), 0, st, p);
+    DTC_KLAUNCH(conv_f32_kernel<F32_FWD>, grid, dim3(256), 0, st, p);
     DTC_LAUNCH_CHECK();
     return 0;
   }
@@ -369,7 +369,7 @@ int conv_f32(const ConvShape& s, int mode, const float* a, const float* b, float
     p.fd_q = make_fastdiv(s.W); p.fd_pq = make_fastdiv(s.H * s.W);
     p.steps_per_split = (int)((p.red + F32_KS - 1) / F32_KS);
     dim3 grid(ceil_div_f(p.M, F32_BM) * ceil_div_f(p.NC, F32_BN), 1);
-    hipLaunchKernelGGL(conv_f32_kernel<F32_DGRAD>, grid, dim3(256), 0, st, p);
+    DTC_KLAUNCH(conv_f32_kernel<F32_DGRAD>, grid, dim3(256), 0, st, p);
     DTC_LAUNCH_CHECK();
     return 0;
   }
@@ -388,11 +388,11 @@ int conv_f32(const ConvShape& s, int mode, const float* a, const float* b, float
   splits = (int)((nsteps + p.steps_per_split - 1) / p.steps_per_split);
   p.out = slab;
   dim3 grid(ceil_div_f(p.M, F32_BM) * ceil_div_f(p.NC, F32_BN), splits);
-  hipLaunchKernelGGL(conv_f32_kernel<F32_WGRAD>, grid, dim3(256), 0, st, p);
+  DTC_KLAUNCH(conv_f32_kernel<F32_WGRAD>, grid, dim3(256), 0, st, p);
   DTC_LAUNCH_CHECK();
   const int ncols = dw_cols > 0 ? dw_cols : p.RSC;
   const int ldo = dw_ld > 0 ? dw_ld : p.RSC;
-  hipLaunchKernelGGL(f32_wgrad_reduce_kernel, dim3(ceil_div_f((int64_t)s.K * ncols, 256)), dim3(256), 0, st, slab,
+  DTC_KLAUNCH(f32_wgrad_reduce_kernel, dim3(ceil_div_f((int64_t)s.K * ncols, 256)), dim3(256), 0, st, slab,
                      splits, s.K, p.RSC, ncols, ldo, scale, dw_ld_or_null, ts);
   DTC_LAUNCH_CHECK();
   return 0;

@@ -861,14 +861,14 @@ size_t conv_halo_slab_bytes(const ConvShape& s, int mode) {
 template <int MODE, int WS>
 static int launch_halo_ws(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
   switch (cfg) {
-    case 0: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 256, 1, 4, 1, 416, WS>), grid, dim3(256), 0, st, p); break;
-    case 1: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 2, 288, WS>), grid, dim3(256), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 1, 288, WS>), grid, dim3(256), 0, st, p); break;
-    case 3: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 256, 2, 2, 1, 416, WS>), grid, dim3(256), 0, st, p); break;
-    case 4: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 1, 288, WS>), grid, dim3(256), 0, st, p); break;
-    case 5: hipLaunchKernelGGL((conv_halo_kernel<MODE, 128, 128, 2, 2, 2, 288, WS>), grid, dim3(256), 0, st, p); break;
-    case 6: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 2, 224, WS>), grid, dim3(256), 0, st, p); break;
-    default: hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 64, 2, 2, 2, 160, WS>), grid, dim3(256), 0, st, p); break;
+    case 0: DTC_KLAUNCH((conv_halo_kernel<MODE, 64, 256, 1, 4, 1, 416, WS>), grid, dim3(256), 0, st, p); break;
+    case 1: DTC_KLAUNCH((conv_halo_kernel<MODE, 64, 128, 1, 4, 2, 288, WS>), grid, dim3(256), 0, st, p); break;
+    case 2: DTC_KLAUNCH((conv_halo_kernel<MODE, 64, 128, 1, 4, 1, 288, WS>), grid, dim3(256), 0, st, p); break;
+    case 3: DTC_KLAUNCH((conv_halo_kernel<MODE, 128, 256, 2, 2, 1, 416, WS>), grid, dim3(256), 0, st, p); break;
+    case 4: DTC_KLAUNCH((conv_halo_kernel<MODE, 128, 128, 2, 2, 1, 288, WS>), grid, dim3(256), 0, st, p); break;
+    case 5: DTC_KLAUNCH((conv_halo_kernel<MODE, 128, 128, 2, 2, 2, 288, WS>), grid, dim3(256), 0, st, p); break;
+    case 6: DTC_KLAUNCH((conv_halo_kernel<MODE, 64, 128, 1, 4, 2, 224, WS>), grid, dim3(256), 0, st, p); break;
+    default: DTC_KLAUNCH((conv_halo_kernel<MODE, 64, 64, 2, 2, 2, 160, WS>), grid, dim3(256), 0, st, p); break;
   }
   DTC_LAUNCH_CHECK();
   return 0;
@@ -886,13 +886,13 @@ template <int MODE>
 static int launch_halo_gen(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
   if (cfg == kFirstS2Cfg) {
     if (p.wsc)
-      hipLaunchKernelGGL((conv_halo_kernel<0, 64, 64, 2, 2, 1, 384, 3, 2, true, true>), grid, dim3(256), 0, st, p);
+      DTC_KLAUNCH((conv_halo_kernel<0, 64, 64, 2, 2, 1, 384, 3, 2, true, true>), grid, dim3(256), 0, st, p);
     else
-      hipLaunchKernelGGL((conv_halo_kernel<0, 64, 64, 2, 2, 1, 384, 3, 2, false, true>), grid, dim3(256), 0, st, p);
+      DTC_KLAUNCH((conv_halo_kernel<0, 64, 64, 2, 2, 1, 384, 3, 2, false, true>), grid, dim3(256), 0, st, p);
   } else if (cfg == 0)
-    hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 256, 1, 4, 1, 416, 3, 1, false, true>), grid, dim3(256), 0, st, p);
+    DTC_KLAUNCH((conv_halo_kernel<MODE, 64, 256, 1, 4, 1, 416, 3, 1, false, true>), grid, dim3(256), 0, st, p);
   else
-    hipLaunchKernelGGL((conv_halo_kernel<MODE, 64, 128, 1, 4, 1, 288, 3, 1, false, true>), grid, dim3(256), 0, st, p);
+    DTC_KLAUNCH((conv_halo_kernel<MODE, 64, 128, 1, 4, 1, 288, 3, 1, false, true>), grid, dim3(256), 0, st, p);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -901,9 +901,9 @@ static int launch_halo_gen(const HConvParams& p, int cfg, dim3 grid, hipStream_t
 template <bool SC>
 static int launch_halo_s2(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
   switch (cfg) {
-    case 8: hipLaunchKernelGGL((conv_halo_kernel<0, 64, 64, 2, 2, 1, 384, 3, 2, SC>), grid, dim3(256), 0, st, p); break;
-    case 9: hipLaunchKernelGGL((conv_halo_kernel<0, 64, 128, 1, 4, 1, 768, 3, 2, SC>), grid, dim3(256), 0, st, p); break;
-    default: hipLaunchKernelGGL((conv_halo_kernel<0, 128, 64, 2, 2, 1, 384, 3, 2, SC>), grid, dim3(256), 0, st, p); break;
+    case 8: DTC_KLAUNCH((conv_halo_kernel<0, 64, 64, 2, 2, 1, 384, 3, 2, SC>), grid, dim3(256), 0, st, p); break;
+    case 9: DTC_KLAUNCH((conv_halo_kernel<0, 64, 128, 1, 4, 1, 768, 3, 2, SC>), grid, dim3(256), 0, st, p); break;
+    default: DTC_KLAUNCH((conv_halo_kernel<0, 128, 64, 2, 2, 1, 384, 3, 2, SC>), grid, dim3(256), 0, st, p); break;
   }
   DTC_LAUNCH_CHECK();
   return 0;

@@ -339,11 +339,11 @@ int conv_dgrad_s2_halo(const ConvShape& s, const u16* dy, const u16* w, u16* dx,
   p.ts = ts;
   const dim3 grid((unsigned)(((p.npos + bn - 1) / bn) * p.tiles_c));
   if (bn == 128) {
-    if (dsc) hipLaunchKernelGGL((dgrad_s2_kernel<4, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((dgrad_s2_kernel<4, false>), grid, dim3(256), 0, st, p);
+    if (dsc) DTC_KLAUNCH((dgrad_s2_kernel<4, true>), grid, dim3(256), 0, st, p);
+    else DTC_KLAUNCH((dgrad_s2_kernel<4, false>), grid, dim3(256), 0, st, p);
   } else {
-    if (dsc) hipLaunchKernelGGL((dgrad_s2_kernel<2, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((dgrad_s2_kernel<2, false>), grid, dim3(256), 0, st, p);
+    if (dsc) DTC_KLAUNCH((dgrad_s2_kernel<2, true>), grid, dim3(256), 0, st, p);
+    else DTC_KLAUNCH((dgrad_s2_kernel<2, false>), grid, dim3(256), 0, st, p);
   }
   DTC_LAUNCH_CHECK();
   return 0;

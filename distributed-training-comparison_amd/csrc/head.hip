@@ -57,7 +57,7 @@ int stem_im2col(const float* x, u16* cols, int N, int H, int W, hipStream_t st) 
   DTC_CHECK_ARG(x && cols && N > 0 && H > 0 && W > 0, "stem_im2col: bad args");
   const int64_t M = (int64_t)N * H * W;
   const int blocks = (int)((M + 255) / 256);
-  hipLaunchKernelGGL(stem_im2col_kernel, dim3(blocks), dim3(256), 0, st, x, cols, N, H, W);
+  DTC_KLAUNCH(stem_im2col_kernel, dim3(blocks), dim3(256), 0, st, x, cols, N, H, W);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -71,7 +71,7 @@ __global__ void stem_pack_weight_kernel(const u16* __restrict__ w27, u16* __rest
 
 int stem_pack_weight(const u16* w27, u16* w64, int K, hipStream_t st) {
   DTC_CHECK_ARG(w27 && w64 && K > 0, "stem_pack_weight: bad args");
-  hipLaunchKernelGGL(stem_pack_weight_kernel, dim3((K * 64 + 255) / 256), dim3(256), 0, st, w27, w64, K);
+  DTC_KLAUNCH(stem_pack_weight_kernel, dim3((K * 64 + 255) / 256), dim3(256), 0, st, w27, w64, K);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -209,7 +209,7 @@ static int head_fwd_t(const T* act, int N, int HW, int C, const T* wfc, const fl
                 "head_fwd: bad args");
   const int groups = std::max(1, 256 / (C / 8));
   const size_t lds = (size_t)(C + std::max(groups * C, 256)) * sizeof(float);
-  hipLaunchKernelGGL(head_fwd_kernel<T>, dim3(N), dim3(256), lds, st, act, HW, C, wfc, bfc, ncls, feat, logits);
+  DTC_KLAUNCH(head_fwd_kernel<T>, dim3(N), dim3(256), lds, st, act, HW, C, wfc, bfc, ncls, feat, logits);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -266,9 +266,9 @@ __global__ void __launch_bounds__(256) xent_mean_kernel(const float* __restrict_
 
 int xent_fwd(const float* logits, const int64_t* labels, int N, int ncls, float* loss, float* lse, hipStream_t st) {
   DTC_CHECK_ARG(logits && labels && loss && lse && N > 0 && ncls > 0, "xent_fwd: bad args");
-  hipLaunchKernelGGL(xent_lse_kernel, dim3((N + 15) / 16), dim3(256), 0, st, logits, N, ncls, lse);
+  DTC_KLAUNCH(xent_lse_kernel, dim3((N + 15) / 16), dim3(256), 0, st, logits, N, ncls, lse);
   DTC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(xent_mean_kernel, dim3(1), dim3(256), 0, st, logits, labels, lse, N, ncls, loss);
+  DTC_KLAUNCH(xent_mean_kernel, dim3(1), dim3(256), 0, st, logits, labels, lse, N, ncls, loss);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -361,7 +361,7 @@ int xent_fwd_fused(const float* logits, const int64_t* labels, int N, int ncls, 
                    const float* scale, float* scaled, float* host, hipStream_t st) {
   DTC_CHECK_ARG(logits && labels && loss && lse && N > 0 && N <= XF_MAX_ROWS && ncls > 0 && (!scaled || scale),
                 "xent_fwd_fused: bad args (N=%d)", N);
-  hipLaunchKernelGGL(xent_fwd_fused_kernel, dim3(1), dim3(1024), 0, st, logits, labels, N, ncls, loss, lse, scale,
+  DTC_KLAUNCH(xent_fwd_fused_kernel, dim3(1), dim3(1024), 0, st, logits, labels, N, ncls, loss, lse, scale,
                      scaled, host);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -390,7 +390,7 @@ int xent_bwd(const float* logits, const int64_t* labels, const float* lse, const
   DTC_CHECK_ARG(logits && labels && lse && dlogits && N > 0 && ncls > 0, "xent_bwd: bad args");
   const int64_t total = (int64_t)N * ncls;
   const int blocks = (int)std::min<int64_t>(1024, (total + 255) / 256);
-  hipLaunchKernelGGL(xent_bwd_kernel, dim3(blocks), dim3(256), 0, st, logits, labels, lse, gscale, N, ncls, dlogits);
+  DTC_KLAUNCH(xent_bwd_kernel, dim3(blocks), dim3(256), 0, st, logits, labels, lse, gscale, N, ncls, dlogits);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -646,10 +646,10 @@ static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int
   if (ncls <= 1024 && (hf == 1 || (hf == 2 && N <= 64))) {
     const int nw = ncls * ((C + 255) / 256);
     if (xa)
-      hipLaunchKernelGGL((head_bwd_fused_kernel<T, true>), dim3(nw + N), dim3(256), dx_lds, st, (float*)dlogits, feat,
+      DTC_KLAUNCH((head_bwd_fused_kernel<T, true>), dim3(nw + N), dim3(256), dx_lds, st, (float*)dlogits, feat,
                          wfc, N, HW, C, ncls, scale, dw, db, dact, nw, *xa);
     else
-      hipLaunchKernelGGL((head_bwd_fused_kernel<T, false>), dim3(nw + N), dim3(256), dx_lds, st, (float*)dlogits, feat,
+      DTC_KLAUNCH((head_bwd_fused_kernel<T, false>), dim3(nw + N), dim3(256), dx_lds, st, (float*)dlogits, feat,
                          wfc, N, HW, C, ncls, scale, dw, db, dact, nw, XentArgs());
     DTC_LAUNCH_CHECK();
     return 0;
@@ -657,13 +657,13 @@ static int head_bwd_t(const float* dlogits, const float* feat, const T* wfc, int
   if (xa) DTC_TRY(xent_bwd(xa->logits, xa->labels, xa->lse, xa->gscale, N, ncls, (float*)dlogits, st));
   DTC_CHECK_ARG(ws && ws_bytes >= head_bwd_workspace(N, C, ncls), "head_bwd: workspace too small");
   const int splits = (N + HB_IMGS - 1) / HB_IMGS;
-  hipLaunchKernelGGL(head_bwd_w_partial_kernel, dim3((C + 63) / 64, (ncls + 15) / 16, splits), dim3(256), 0, st,
+  DTC_KLAUNCH(head_bwd_w_partial_kernel, dim3((C + 63) / 64, (ncls + 15) / 16, splits), dim3(256), 0, st,
                      dlogits, feat, N, C, ncls, ws);
   DTC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(head_bwd_w_reduce_kernel, dim3((int)(((int64_t)ncls * C + 255) / 256)), dim3(256), 0, st, ws,
+  DTC_KLAUNCH(head_bwd_w_reduce_kernel, dim3((int)(((int64_t)ncls * C + 255) / 256)), dim3(256), 0, st, ws,
                      splits, dlogits, N, C, ncls, scale, dw, db);
   DTC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(head_bwd_x_kernel<T>, dim3(N), dim3(256), dx_lds, st, dlogits, wfc, HW, C, ncls, dact);
+  DTC_KLAUNCH(head_bwd_x_kernel<T>, dim3(N), dim3(256), dx_lds, st, dlogits, wfc, HW, C, ncls, dact);
   DTC_LAUNCH_CHECK();
   return 0;
 }

@@ -754,7 +754,7 @@ template <int MODE, int BM, int BN, int WR, int WC, bool SLAB, bool SC = false>
 static int launch_igemm(IGemmParams& p, int tiles_b, int splits, hipStream_t st, int gz = 1) {
   dim3 grid(p.tiles_a * tiles_b, splits, gz);
   p.xcd_remap = option_get(OPT_XCD_REMAP);
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 2, SC>), grid, dim3(256), 0, st, p);
+  DTC_KLAUNCH((igemm_kernel<MODE, BM, BN, WR, WC, SLAB, 2, SC>), grid, dim3(256), 0, st, p);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -1024,7 +1024,7 @@ static int launch_wgrad_reduce(const float* slab, int splits, int K, int RSC, in
   while (sg < 16 && sg * 2 <= splits && (nv * sg * nprob) / 256 < 1024) sg *= 2;
   const dim3 grid((unsigned)((nv + (256 / sg) - 1) / (256 / sg)), nprob);
 #define DTC_WR(SG_) \
-  hipLaunchKernelGGL(wgrad_reduce_kernel<SG_>, grid, dim3(256), 0, st, slab, splits, K, RSC, ncols, ldo, scale, outs, prob_stride, ts)
+  DTC_KLAUNCH(wgrad_reduce_kernel<SG_>, grid, dim3(256), 0, st, slab, splits, K, RSC, ncols, ldo, scale, outs, prob_stride, ts)
   switch (sg) {
     case 1: DTC_WR(1); break;
     case 2: DTC_WR(2); break;
@@ -1131,14 +1131,14 @@ int splitk_reduce(const float* slab, int splits, int M, int Nc, u16* out, const 
   int rows_per_block = std::max({rpp, (M + 1023) / 1024, std::min((16384 + Nc - 1) / Nc, (M + 255) / 256)});
   rows_per_block = ((rows_per_block + rpp - 1) / rpp) * rpp;
   const int blocks = ceil_div(M, rows_per_block);
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, splits, M, Nc, out, res, stats,
+  DTC_KLAUNCH(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, splits, M, Nc, out, res, stats,
                      rows_per_block, ts);
   DTC_LAUNCH_CHECK();
   return 0;
 }
 
 int prof_accumulate(u64* ts, int n, u64* acc, hipStream_t st) {
-  hipLaunchKernelGGL(prof_accumulate_kernel, dim3((n + 63) / 64), dim3(64), 0, st, ts, n, acc);
+  DTC_KLAUNCH(prof_accumulate_kernel, dim3((n + 63) / 64), dim3(64), 0, st, ts, n, acc);
   DTC_LAUNCH_CHECK();
   return 0;
 }

@@ -42,7 +42,7 @@ int sgd_nesterov(float* p, const float* g, float* mom, u16* p_bf16, int64_t n, f
   DTC_CHECK_ARG(p && g && mom && p_bf16 && n > 0 && (n % 4) == 0, "sgd_nesterov: bad args (n=%lld)", (long long)n);
   const int64_t n4 = n / 4;
   const int blocks = (int)std::min<int64_t>(2048, (n4 + 255) / 256);
-  hipLaunchKernelGGL(sgd_nesterov_kernel, dim3(blocks), dim3(256), 0, st, p, g, mom, p_bf16, n4, lr, wd, mu, inv_scale,
+  DTC_KLAUNCH(sgd_nesterov_kernel, dim3(blocks), dim3(256), 0, st, p, g, mom, p_bf16, n4, lr, wd, mu, inv_scale,
                      found_inf);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -55,7 +55,7 @@ __global__ void cast_f32_bf16_kernel(const float* __restrict__ s, u16* __restric
 int cast_f32_bf16(const float* src, u16* dst, int64_t n, hipStream_t st) {
   DTC_CHECK_ARG(src && dst && n > 0, "cast_f32_bf16: bad args");
   const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
-  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(blocks), dim3(256), 0, st, src, dst, n);
+  DTC_KLAUNCH(cast_f32_bf16_kernel, dim3(blocks), dim3(256), 0, st, src, dst, n);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -70,7 +70,7 @@ int zero_bytes(void* p, size_t bytes, hipStream_t st) {
   if (bytes == 0) return 0;
   const int64_t n = (int64_t)(bytes / 8);
   const int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
-  hipLaunchKernelGGL(zero_kernel, dim3(blocks), dim3(256), 0, st, (uint2*)p, n);
+  DTC_KLAUNCH(zero_kernel, dim3(blocks), dim3(256), 0, st, (uint2*)p, n);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -90,7 +90,7 @@ int copy_and_zero(const void* src, void* dst, size_t bytes, void* zp, size_t zby
                 "copy_and_zero: 16-byte aligned copy, 8-byte aligned zero range");
   const int64_t n16 = (int64_t)(bytes / 16), n8 = (int64_t)(zbytes / 8);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (std::max(n16, n8) + 255) / 256));
-  hipLaunchKernelGGL(copy_zero_kernel, dim3(blocks), dim3(256), 0, st, (const uint4*)src, (uint4*)dst, n16, (uint2*)zp,
+  DTC_KLAUNCH(copy_zero_kernel, dim3(blocks), dim3(256), 0, st, (const uint4*)src, (uint4*)dst, n16, (uint2*)zp,
                      n8);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -105,7 +105,7 @@ __global__ void scale_kernel(T* __restrict__ x, int64_t n, T f) {
 int scale_f32(float* x, int64_t n, float f, hipStream_t st) {
   DTC_CHECK_ARG(x && n > 0, "scale_f32: bad args");
   const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
-  hipLaunchKernelGGL(scale_kernel<float>, dim3(blocks), dim3(256), 0, st, x, n, f);
+  DTC_KLAUNCH(scale_kernel<float>, dim3(blocks), dim3(256), 0, st, x, n, f);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -113,7 +113,7 @@ int scale_f32(float* x, int64_t n, float f, hipStream_t st) {
 int scale_f64(double* x, int64_t n, double f, hipStream_t st) {
   DTC_CHECK_ARG(x && n > 0, "scale_f64: bad args");
   const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
-  hipLaunchKernelGGL(scale_kernel<double>, dim3(blocks), dim3(256), 0, st, x, n, f);
+  DTC_KLAUNCH(scale_kernel<double>, dim3(blocks), dim3(256), 0, st, x, n, f);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -121,7 +121,7 @@ int scale_f64(double* x, int64_t n, double f, hipStream_t st) {
 int scale_i64(int64_t* x, int64_t n, int64_t f, hipStream_t st) {
   DTC_CHECK_ARG(x && n > 0, "scale_i64: bad args");
   const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
-  hipLaunchKernelGGL(scale_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, x, n, f);
+  DTC_KLAUNCH(scale_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, x, n, f);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -135,7 +135,7 @@ __global__ void amp_scale_kernel(const float* __restrict__ x, const float* __res
 int amp_scale(const float* x, const float* scale, float* out, int64_t n, hipStream_t st) {
   DTC_CHECK_ARG(x && scale && out && n > 0, "amp_scale: bad args");
   const int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
-  hipLaunchKernelGGL(amp_scale_kernel, dim3(blocks), dim3(256), 0, st, x, scale, out, n);
+  DTC_KLAUNCH(amp_scale_kernel, dim3(blocks), dim3(256), 0, st, x, scale, out, n);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -152,7 +152,7 @@ int add_f32(float* dst, const float* src, int64_t n, hipStream_t st) {
   DTC_CHECK_ARG(dst && src && n > 0 && n % 4 == 0 && ((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0,
                 "add_f32: bad args (n %% 4 and 16-byte alignment required)");
   const int blocks = (int)std::min<int64_t>(2048, (n / 4 + 255) / 256);
-  hipLaunchKernelGGL(add_f32_kernel, dim3(blocks), dim3(256), 0, st, dst, src, n / 4);
+  DTC_KLAUNCH(add_f32_kernel, dim3(blocks), dim3(256), 0, st, dst, src, n / 4);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -172,9 +172,9 @@ __global__ void group_sum_kernel(GroupPtrs g, int w, int64_t n) {
 int group_sum(const GroupPtrs& g, int w, int64_t n, int dtype, hipStream_t st) {
   DTC_CHECK_ARG(w >= 1 && w <= DTC_GROUP_MAX && n > 0 && (dtype == 0 || dtype == 2 || dtype == 3), "group_sum: bad args");
   const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
-  if (dtype == 0) hipLaunchKernelGGL(group_sum_kernel<float>, dim3(blocks), dim3(256), 0, st, g, w, n);
-  else if (dtype == 2) hipLaunchKernelGGL(group_sum_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, g, w, n);
-  else hipLaunchKernelGGL(group_sum_kernel<double>, dim3(blocks), dim3(256), 0, st, g, w, n);
+  if (dtype == 0) DTC_KLAUNCH(group_sum_kernel<float>, dim3(blocks), dim3(256), 0, st, g, w, n);
+  else if (dtype == 2) DTC_KLAUNCH(group_sum_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, g, w, n);
+  else DTC_KLAUNCH(group_sum_kernel<double>, dim3(blocks), dim3(256), 0, st, g, w, n);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -211,12 +211,12 @@ int amp_check_finite(const float* g, int64_t n, int* found_inf, hipStream_t st) 
   DTC_CHECK_ARG(g && found_inf && n > 0, "amp_check_finite: bad args");
   if (((uintptr_t)g & 15) == 0) {
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n / 4 + 255) / 256));
-    hipLaunchKernelGGL(amp_check_finite4_kernel, dim3(blocks), dim3(256), 0, st, g, n, found_inf);
+    DTC_KLAUNCH(amp_check_finite4_kernel, dim3(blocks), dim3(256), 0, st, g, n, found_inf);
     DTC_LAUNCH_CHECK();
     return 0;
   }
   const int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
-  hipLaunchKernelGGL(amp_check_finite_kernel, dim3(blocks), dim3(256), 0, st, g, n, found_inf);
+  DTC_KLAUNCH(amp_check_finite_kernel, dim3(blocks), dim3(256), 0, st, g, n, found_inf);
   DTC_LAUNCH_CHECK();
   return 0;
 }
@@ -246,7 +246,7 @@ __global__ void amp_update_scale_kernel(float* scale, float* inv_scale, int* tra
 int amp_update_scale(float* scale, float* inv_scale, int* growth_tracker, int* found_inf, float growth, float backoff,
                      int interval, hipStream_t st) {
   DTC_CHECK_ARG(scale && growth_tracker && found_inf && interval > 0, "amp_update_scale: bad args");
-  hipLaunchKernelGGL(amp_update_scale_kernel, dim3(1), dim3(1), 0, st, scale, inv_scale, growth_tracker, found_inf,
+  DTC_KLAUNCH(amp_update_scale_kernel, dim3(1), dim3(1), 0, st, scale, inv_scale, growth_tracker, found_inf,
                      growth, backoff, interval);
   DTC_LAUNCH_CHECK();
   return 0;

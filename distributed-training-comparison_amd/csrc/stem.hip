@@ -300,10 +300,10 @@ int stem_fwd(const float* x, const u16* w27, u16* y, int64_t* stats, int N, int 
   const int64_t M = (int64_t)N * H * W;
   DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_fwd: more than 2^31 pixels");
   if (option_get(OPT_STEM_WLDS) != 0 && ((uintptr_t)w27 & 3) == 0)
-    hipLaunchKernelGGL((stem_fwd_kernel<true>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y,
+    DTC_KLAUNCH((stem_fwd_kernel<true>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y,
                        stats, stem_geom(N, H, W), ts);
   else
-    hipLaunchKernelGGL((stem_fwd_kernel<false>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y,
+    DTC_KLAUNCH((stem_fwd_kernel<false>), dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, w27, y,
                        stats, stem_geom(N, H, W), ts);
   DTC_LAUNCH_CHECK();
   return 0;
@@ -386,7 +386,7 @@ int stem_wgrad(const float* x, const u16* dy, float* dw27, float scale, int N, i
   const int nwg = (int)((ntiles + tiles - 1) / tiles);
   DTC_CHECK_ARG(slab_bytes >= (size_t)nwg * 64 * 32 * 4, "stem_wgrad: slab workspace too small");
   DTC_CHECK_ARG(M + 256 < (1ll << 31), "stem_wgrad: more than 2^31 pixels");
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(nwg), dim3(256), 0, st, x, dy, slab, stem_geom(N, H, W), tiles, ts);
+  DTC_KLAUNCH(stem_wgrad_kernel, dim3(nwg), dim3(256), 0, st, x, dy, slab, stem_geom(N, H, W), tiles, ts);
   DTC_LAUNCH_CHECK();
   return wgrad_reduce_to(slab, nwg, 64, 32, 27, 27, scale, dw27, st, ts);
 }
@@ -514,7 +514,7 @@ int stem_wgrad_bn(const float* x, const u16* dy, const uint8_t* mbits, const u16
   int tiles = 0;
   const int nwg = stem_bn_grid(M, tiles);
   DTC_CHECK_ARG(slab_bytes >= (size_t)nwg * 64 * 32 * 4, "stem_wgrad_bn: slab workspace too small");
-  hipLaunchKernelGGL(stem_wgrad_bn_kernel<STEM_BN_CAP>, dim3(nwg), dim3(256), 0, st, x, dy, mbits, c, a, slab,
+  DTC_KLAUNCH(stem_wgrad_bn_kernel<STEM_BN_CAP>, dim3(nwg), dim3(256), 0, st, x, dy, mbits, c, a, slab,
                      stem_geom(N, H, W), tiles, ts);
   DTC_LAUNCH_CHECK();
   return wgrad_reduce_to(slab, nwg, 64, 32, 27, 27, scale, dw27, st, ts);

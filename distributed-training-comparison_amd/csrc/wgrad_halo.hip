@@ -481,7 +481,7 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   p.scale = scale;
   const int nr = (p.nh + 63) / 64;  // halo DMA rounds per step
   // 4-stage LDS ring (three steps of DMA in flight)
-#define DTC_WGH(NR_, GEN_) hipLaunchKernelGGL((wgrad_halo_kernel<4, NR_, 1, false, GEN_>), grid, dim3(512), 0, st, p)
+#define DTC_WGH(NR_, GEN_) DTC_KLAUNCH((wgrad_halo_kernel<4, NR_, 1, false, GEN_>), grid, dim3(512), 0, st, p)
   if (g.gen) {  // general geometry
     if (nr <= 2) { DTC_WGH(2, true); }
     else { DTC_WGH(3, true); }
@@ -635,7 +635,7 @@ int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* ds
   p.scale = scale;
   const dim3 grid((s.C / 64) * (s.K / 64), used, 1);
   const int nr = (nh + 63) / 64;
-#define DTC_WS2(NR_, SC_, G_) hipLaunchKernelGGL((wgrad_halo_kernel<2, NR_, 2, SC_, G_>), grid, dim3(512), 0, st, p)
+#define DTC_WS2(NR_, SC_, G_) DTC_KLAUNCH((wgrad_halo_kernel<2, NR_, 2, SC_, G_>), grid, dim3(512), 0, st, p)
   if (gen) {
     if (nr <= 5) { if (dsc) DTC_WS2(5, true, true); else DTC_WS2(5, false, true); }
     else { if (dsc) DTC_WS2(6, true, true); else DTC_WS2(6, false, true); }

@@ -148,6 +148,8 @@ _OPTION_DEFAULTS = {
     "bn_cg": 1, "bn_cg_elems": 262144, "wgrad_s2_wgs": 128, "comm_on_side": 1, "c64_wgs": 256, "wgrad_halo_l1": 0,
     # round 5
     "splitk_ink": 1, "comm_prio": 0, "comm_tail_inline": 1, "dgrad_s2h": 1, "halo_small": 1,
+    # round 6
+    "xent_fuse": 1, "fork_ev": 1,
 }
 # measured-negative variants deleted in rounds 4-6 with their code paths (DESIGN.md keeps their numbers)
 _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", "wgrad_pmap", "wgrad_prio",
@@ -156,7 +158,8 @@ _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", 
                     # round 5
                     "bnb_mask", "bnb_fuse", "halo_stage_epi", "igemm_stages", "halo_l2pf", "dgrad_first", "wgrad_s2_ps", "c64_waves", "wgrad_early",
                     # round 6
-                    "wgrad_ink", "wgrad_ink_max", "wgrad_ring", "wgrad_ksplit", "bn_in_conv", "amp_in_bwd")
+                    "wgrad_ink", "wgrad_ink_max", "wgrad_ring", "wgrad_ksplit", "bn_in_conv", "amp_in_bwd",
+                    "s2d_split", "s2d_wgs")
 
 
 def test_options_registered_with_defaults(dtc):
