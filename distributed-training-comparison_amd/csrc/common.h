@@ -7,7 +7,6 @@
 //     contiguous row of R*S*C elements: that row is the GEMM operand directly;
 //   * every launch takes the caller's hipStream_t; nothing here allocates memory.
 #pragma once
-#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
@@ -41,39 +40,24 @@ const char* last_error();
 #define DTC_LAUNCH_CHECK() DTC_HIP(hipGetLastError())
 
 // ---------------------------------------------------------------- launches
-// Every kernel of the library is launched through DTC_KLAUNCH. While a stop event is armed for a stream
-// (resnet.cpp, before the kernels a side-stream fork will depend on), launches on that stream carry it as
-// their completion event (hipExtLaunchKernelGGL's stopEvent: the dispatch packet's own completion signal), so
-// the fork's hipStreamWaitEvent needs no hipEventRecord on the launching stream -- a marker packet there costs
-// the stream a ~2.7 us bubble before its next kernel, ~4 us with a side kernel waiting on it
-// (tools/probes/fork_gap.hip; a stop event on a kernel costs ~0.1 us).
+// Every kernel of the library is launched through DTC_KLAUNCH, which notes a launch on the stream a side stream
+// was last forked from (resnet.cpp: a second fork from the same point -- a bucket's collective right after its
+// weight-gradient flush -- then needs no second event record; a record costs the recording stream a ~2.7 us
+// bubble before its next kernel, tools/probes/fork_gap.hip).
 namespace dtc {
-struct StopArm {
-  hipStream_t st = nullptr;
-  hipEvent_t ev = nullptr;
-  bool fired = false;  // a launch carried ev since arming
-};
-inline thread_local StopArm g_stop_arm;
-// the stream a side stream was last forked from, and whether anything was launched on it since (a second fork
-// from the same point -- a bucket's collective right after its weight-gradient flush -- needs no new wait)
 struct ForkWatch {
   hipStream_t st = nullptr;
-  bool dirty = true;
+  bool dirty = true;  // something was launched on st since the fork
 };
 inline thread_local ForkWatch g_fork_watch;
-inline bool stop_armed(hipStream_t st) {
+inline void note_launch(hipStream_t st) {
   if (st == g_fork_watch.st) g_fork_watch.dirty = true;
-  if (g_stop_arm.ev == nullptr || st != g_stop_arm.st) return false;
-  g_stop_arm.fired = true;
-  return true;
 }
 }  // namespace dtc
-#define DTC_KLAUNCH(K, G, B, SH, ST, ...)                                                              \
-  do {                                                                                                \
-    if (::dtc::stop_armed(ST))                                                                        \
-      hipExtLaunchKernelGGL(K, G, B, SH, ST, nullptr, ::dtc::g_stop_arm.ev, 0, __VA_ARGS__);           \
-    else                                                                                              \
-      hipLaunchKernelGGL(K, G, B, SH, ST, __VA_ARGS__);                                               \
+#define DTC_KLAUNCH(K, G, B, SH, ST, ...)          \
+  do {                                            \
+    ::dtc::note_launch(ST);                       \
+    hipLaunchKernelGGL(K, G, B, SH, ST, __VA_ARGS__); \
   } while (0)
 #define DTC_TRY(expr)      \
   do {                     \

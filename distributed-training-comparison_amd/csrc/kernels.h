@@ -41,7 +41,6 @@ namespace dtc {
   X(BN_RED_BLOCKS, bn_red_blocks, 256)  /* ... while keeping at least this many workgroups (tuning) */        \
   X(BN_FA_BLOCKS, bn_fa_blocks, 1024)   /* BN fin_apply: target workgroups per launch (tuning) */             \
   X(FORK_LAZY, fork_lazy, 1)            /* fork the wgrad stream only where a wgrad launches */               \
-  X(FORK_EV, fork_ev, 1)                /* forks / joins wait on a producer kernel's stop event, no marker */   \
   X(SIDE_PRIO, side_prio, 1)            /* (side stream creation) weight-gradient stream at low priority */  \
   X(SC_FUSE, sc_fuse, 1)                /* projection shortcut inside conv1's forward: 1 layer4, 2/3 wider */ \
   X(STEM_WLDS, stem_wlds, 1)            /* stem forward weight staged in LDS */                               \

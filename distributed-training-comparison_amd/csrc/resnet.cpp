@@ -963,7 +963,7 @@ static int maybe_bucket(Net& n, int after_block, const BwdCtx& cx, hipStream_t s
     // after it. The side stream is joined into the compute stream once, at the end of the backward.
     hipStream_t prod = st;
     if (n.side_pending) {
-      if (!side_covers(st)) {  // (option fork_ev: a flush's fork right before this point already ordered it)
+      if (!side_covers(st)) {  // (a flush's fork right before this point already ordered it: no second marker)
         hipEvent_t ev;
         DTC_TRY(stop_or_record(n, st, &ev));
         DTC_HIP(hipStreamWaitEvent(n.side_st, ev, 0));
@@ -1093,28 +1093,12 @@ static int next_event(Net& n, hipEvent_t* ev) {
   n.ev_next = (n.ev_next + 1) % (int)n.evs.size();
   return 0;
 }
-// Option fork_ev (round 6): the event a fork (join) waits on is the stop event of the last kernel launched on the
-// producing stream -- armed before the launcher(s) that end there (arm_stop; common.h DTC_KLAUNCH) -- instead of a
-// hipEventRecord marker behind it, which stalled that stream ~2.7 us before its next kernel (~4 us with the side
-// kernel waiting: tools/probes/fork_gap.hip). Not while a graph is captured, not with parity captures (their copies
-// run between a producer and the fork), not in the profiled region (its event brackets).
-static void arm_stop(Net& n, hipStream_t st, bool capturing) {
-  g_stop_arm = StopArm{};
-  if (option_get(OPT_FORK_EV) == 0 || capturing || n.capture || n.profiling || !side_on(n)) return;
-  hipEvent_t ev;
-  if (next_event(n, &ev) != 0) return;
-  g_stop_arm.st = st;
-  g_stop_arm.ev = ev;
-}
-// the event marking everything issued on `st` so far: the armed stop event if a launch on st carried it (every
-// launch on st since arming did: the last one's completion orders all of them), else a recorded marker
+// A marker recorded on `st` (the fork / join points of the weight-gradient stream). Round 6 measured the
+// alternative -- waiting on the producing kernel's own stop event (hipExtLaunchKernelGGL) instead of a recorded
+// marker, which removes the marker's ~2.7 us bubble in isolation (tools/probes/fork_gap.hip) -- and removed it:
+// on a busy stream each such launch cost the host ~4 us and left a ~4.7 us gap after the kernel (B=256 -2.7%,
+// 24 of 24 in-process A/B rounds; backward host issue 189 -> 321 us; profiles/r06w_fork_ev.txt)
 static int stop_or_record(Net& n, hipStream_t st, hipEvent_t* ev) {
-  if (g_stop_arm.ev != nullptr && g_stop_arm.st == st && g_stop_arm.fired) {
-    *ev = g_stop_arm.ev;
-    g_stop_arm = StopArm{};
-    return 0;
-  }
-  if (g_stop_arm.st == st) g_stop_arm = StopArm{};
   DTC_TRY(next_event(n, ev));
   DTC_HIP(hipEventRecord(*ev, st));
   return 0;
@@ -1144,9 +1128,7 @@ static int fork_side(Net& n, hipStream_t st, hipStream_t* out) {
   return 0;
 }
 // the side stream already waits for everything issued on st (forked from it, nothing launched on st since)
-static bool side_covers(hipStream_t st) {
-  return option_get(OPT_FORK_EV) != 0 && g_fork_watch.st == st && !g_fork_watch.dirty;
-}
+static bool side_covers(hipStream_t st) { return g_fork_watch.st == st && !g_fork_watch.dirty; }
 static int join_side(Net& n, hipStream_t st) {
   if (!n.side_pending) return 0;
   hipEvent_t ev;
@@ -1282,7 +1264,6 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     DTC_TRY(cap_masked(n, cp + ".dz", G[0], b.MOUT, M, b.Cout, st));
     // out = relu(bn2(c2) + shortcut): sums of dz = dy * [out > 0] (and of the projection BN), then
     // dc2 (and dsc); an identity block also needs dz itself as conv1's dgrad residual: in place in G[0]
-    arm_stop(n, st, cx.capturing);  // the conv2 weight gradient's fork may follow (wg_issue)
     if (bn_cg_on(n, M, b.Cout, b.proj)) {
       DTC_TRY(bn_bwd_one_launch(n, b.b2, G[0], mout, b.proj ? nullptr : G[0], n.at<u16>(b.C2), dc2,
                                 b.proj ? &b.bsc : nullptr, b.proj ? n.at<u16>(b.S) : nullptr, dsc, M, gs, st));
@@ -1310,7 +1291,6 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
          conv_dgrad(b.c2.s, dc2, n.wbf(b.c2.pidx), G[4], nullptr, slab, n.slab_bytes, st, ts, nullptr, 0, n.tick(0)));
     DTC_TRY(cap(n, cp + ".da1", G[4], st));
     DTC_TRY(cap_masked(n, cp + ".dz1", G[4], b.MA1, M, b.Cout, st));
-    arm_stop(n, st, cx.capturing);  // the conv1 (+ shortcut) weight gradients' fork follows
     if (bn_cg_on(n, M, b.Cout, false)) {
       DTC_TRY(bn_bwd_one_launch(n, b.b1, G[4], ma1, nullptr, n.at<u16>(b.C1), dc1, nullptr, nullptr, nullptr, M, gs, st));
     } else {
@@ -1331,10 +1311,6 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
     } else {
       DTC_TRY(wg_issue(n, wq, b.c1.s, in, dc1, n.gf(b.c1.pidx), gs, slabw, sd, st, lazy && !b.proj));
     }
-    // a bucket point below flushes the queued weight gradients behind this block's input gradient: its dgrad
-    // carries the stop event the fork waits on (the conv2 / conv1 arms above were consumed or are replaced here)
-    if (bucket_fires(n, bi)) arm_stop(n, st, cx.capturing);
-    else g_stop_arm = StopArm{};
     if (b.proj) {
       if (!wsc)
         PROF(2, conv_flops(b.sc.s),
@@ -1367,13 +1343,11 @@ static int backward_body_mask(Net& n, const float* dlogits, float gs, const BwdC
   const uint8_t* m0 = n.at<uint8_t>(n.MA0);
   // option stem_bn_fuse: the stem BN's apply runs inside the stem weight gradient (dc0 never stored;
   // not with parity captures, which want dc0, or SyncBN, whose sums are all-reduced first)
-  arm_stop(n, st, cx.capturing);  // the layer1 weight-gradient batch's fork follows the stem BN reduction
   if (n.stem_direct && !n.capture && !n.sync && bn_fused() && option_get(OPT_STEM_BN_FUSE) != 0) {
     PROF(3, (double)M0 * 64 * 4.125,
            bn_bwd_reduce_mask(G[0], m0, n.at<u16>(n.C0), n.at<float>(n.bn0.mean), n.at<float>(n.bn0.invstd),
                               n.at<int64_t>(n.bn0.acc), nullptr, nullptr, nullptr, nullptr, M0, 64, st, ts));
     if (option_get(OPT_FORK_LAZY) && wq.count > 0) DTC_TRY(fork_side(n, st, &sd));
-    if (sd != st) arm_stop(n, sd, cx.capturing);  // the end-of-backward join waits on the batch's last kernel
     DTC_TRY(wg_flush(n, wq, gs, slabw, sd));
     const BnBwdArgs a0 = bwd_args(n, n.bn0, M0, gs);
     PROF(2, 2.0 * M0 * 64 * 27,
@@ -1552,7 +1526,6 @@ static int backward_impl(Net& n, const float* dlogits, float gs, Comm* comm, hip
     BwdCtx cx;
     cx.comm = comm;
     const int rc = backward_body(n, dlogits, gs, cx, st);
-    g_stop_arm = StopArm{};  // nothing armed outlives the backward
     g_fork_watch = ForkWatch{};
     DTC_TRY(rc);
   } else {

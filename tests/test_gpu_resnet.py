@@ -509,26 +509,6 @@ def test_backward_repeatable_across_steps(dtc, cuda, batch):
             _assert_same_grads(dtc, g[0], g[r], f"graphs={graphs} B={batch} rep {r}")
 
 
-@pytest.mark.parametrize("batch", [256, 32])
-def test_fork_on_stop_events_bit_identical(dtc, cuda, batch):
-    """Option fork_ev (round 6, default on): the weight-gradient stream's forks and the end-of-backward join wait on
-    the producing kernel's own completion event (hipExtLaunchKernelGGL stopEvent, armed in resnet.cpp) instead of a
-    hipEventRecord marker. A fork that did not order the weight gradients after their inputs would read stale
-    BN-backward outputs: the gradients must equal the marker path's bit for bit (the step is deterministic), eager,
-    at config 2's batch and config 3's per-rank batch, over several steps (the side stream runs ahead)."""
-    lib = dtc._native.lib
-    prev = lib.dtc_get_option(b"fork_ev")
-    try:
-        lib.dtc_set_option(b"fork_ev", 0)
-        ga = _grads_repeated(dtc, cuda, 0, reps=3, batch=batch)
-        lib.dtc_set_option(b"fork_ev", 1)
-        gb = _grads_repeated(dtc, cuda, 0, reps=3, batch=batch)
-    finally:
-        lib.dtc_set_option(b"fork_ev", prev)
-    for r in range(3):
-        _assert_same_grads(dtc, ga[r], gb[r], f"fork_ev B={batch} rep {r}")
-
-
 @pytest.mark.parametrize("batch,hw", [(8, 32), (3, 32), (5, 8)])
 def test_bn_reduce_unrolled_loads_bit_identical(dtc, cuda, batch, hw):
     """Option bn_red_unroll (default 4): the mask-bit BN-backward reduction issues the loads of 4 (or 2) rows

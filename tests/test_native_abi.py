@@ -149,7 +149,7 @@ _OPTION_DEFAULTS = {
     # round 5
     "splitk_ink": 1, "comm_prio": 0, "comm_tail_inline": 1, "dgrad_s2h": 1, "halo_small": 1,
     # round 6
-    "xent_fuse": 1, "fork_ev": 1,
+    "xent_fuse": 1,
 }
 # measured-negative variants deleted in rounds 4-6 with their code paths (DESIGN.md keeps their numbers)
 _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", "wgrad_pmap", "wgrad_prio",
@@ -159,7 +159,7 @@ _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", 
                     "bnb_mask", "bnb_fuse", "halo_stage_epi", "igemm_stages", "halo_l2pf", "dgrad_first", "wgrad_s2_ps", "c64_waves", "wgrad_early",
                     # round 6
                     "wgrad_ink", "wgrad_ink_max", "wgrad_ring", "wgrad_ksplit", "bn_in_conv", "amp_in_bwd",
-                    "s2d_split", "s2d_wgs")
+                    "s2d_split", "s2d_wgs", "fork_ev")
 
 
 def test_options_registered_with_defaults(dtc):

@@ -19,5 +19,6 @@ mkdir -p "$OUT"
     > "$OUT/${TAG}_prof_bench.json" ) || exit $?
 python3 "$ROOT/tools/prof_summary.py" "$OUT/prof_$TAG" "$OUT/${TAG}_kernel_trace.md" --bench "$OUT/${TAG}_prof_bench.json" > /dev/null
 python3 "$ROOT/tools/step_timeline.py" "$OUT/prof_$TAG" > "$OUT/${TAG}_timeline.txt" 2>&1 || true
+python3 "$ROOT/tools/step_timeline.py" "$OUT/prof_$TAG" --gaps 2 > "$OUT/${TAG}_gaps.txt" 2>&1 || true
 if [ -n "$EXTRA" ]; then python3 "$ROOT/tools/api_summary.py" "$OUT/prof_$TAG" > "$OUT/${TAG}_hip_api.txt" 2>&1 || true; fi
 rm -rf "$OUT/prof_$TAG"
