@@ -57,6 +57,7 @@ namespace dtc {
   X(COMM_ON_SIDE, comm_on_side, 1)      /* bucket all-reduces on the weight-gradient stream (no comm stream) */ \
   X(BUCKET_TAIL, bucket_tail, 1)        /* (plan time) close the open bucket (>= 1 MB) after layer2.0 */      \
   X(WGRAD_GEN, wgrad_gen, 1)            /* wgrad_halo general step geometry (224x224 model) */                \
+  X(WGRAD_TRIM, wgrad_trim, 1)          /* wgrad_halo: no zero-fill DMA for last-round rows past the halo */  \
   X(HALO_GEN, halo_gen, 1)              /* conv_halo general tile geometry (224x224 model) */                 \
   X(BN_RED_UNROLL, bn_red_unroll, 4)    /* bn_bwd_reduce: rows per thread whose loads go together */          \
   X(C64_GEN, c64_gen, 1)                /* conv_c64 general tiles (224x224 layer1) */                         \

@@ -59,6 +59,10 @@ struct HaloParams {
   // the 64-pixel step carry zero dy), its halo (rs + 2) x (seg + 2) pixels; every step addresses x and dy
   // from a 64-bit per-step base, so an activation may exceed 2 GB (512 x 224 x 224 x 64 bf16 = 3.3 GB)
   int seg, spimg;      // pixels per row segment, steps per image
+  // option wgrad_trim (round 6): a wave whose rows of the last halo DMA round all lie past the step's halo
+  // (nh <= (NR - 1) * 64 + wave * 8) issues no DMA for them instead of a zero-filling one (layer1: 136 of 192
+  // rows are halo, layer4: 144): fewer LDS-DMA bytes per step, its counted waits one instruction per stage lower
+  int trim;
   FastDiv fd_spimg, fd_spr, fd_seg, fd_seg2;  // steps per image, segments per row, seg, seg + 2
 };
 
@@ -173,6 +177,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     if (trow < p.rs * p.seg) drel = (uint32_t)(((tr * p.wo + tc) * p.K + dcol) * 2);
   }
 
+  const bool trim = p.trim && (NR - 1) * 64 + wave * 8 >= p.nh;  // (wave-uniform)
   auto stage_gen = [&](char* sb, int step) {  // GEN: per-step 64-bit bases, zero-fill out of the image
     const int img = (int)fdiv((uint32_t)step, p.fd_spimg), r = step - img * p.spimg;
     const int yb = (int)fdiv((uint32_t)r, p.fd_spr), qs = r - yb * (int)p.fd_spr.d;
@@ -182,6 +187,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     const int64_t dro = ((int64_t)(img * p.ho + y0) * p.wo + q0) * p.K;
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
+      if (j == NR - 1 && trim) break;
       const bool ok = hcol[j] && (unsigned)(iy0 + hrow_in[j]) < (unsigned)p.H && (unsigned)(iq0 + hcc[j]) < (unsigned)p.W;
       buf_lds16(xb, 0x7ffffff0u, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)hrel[j] : 0x80000000u);
     }
@@ -199,6 +205,7 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
     const int base = ((n0 * p.H + p0) * p.W) * p.C * 2;
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
+      if (j == NR - 1 && trim) break;
       const bool ok = hcol[j] && (unsigned)(p0 + hrow_in[j]) < (unsigned)p.H;
       buf_lds16(px, p.x_bytes, sb + (j * 64 + wave * 8) * 128, ok ? (uint32_t)(base + hrel[j]) : 0x80000000u);
     }
@@ -337,8 +344,12 @@ __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
       for (int u = 0; u < NS; ++u) {
         const int k = it + u;
         if (k >= nk) break;
-        if (NS > 2 && k + NS - 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PER) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (NS > 2 && k + NS - 2 < nk) {
+          if (trim) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (PER - 1)) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PER) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (k + NS - 1 < nk) stage(smem + ((u + NS - 1) % NS) * SG::BYTES, st_begin + k + NS - 1);
@@ -472,6 +483,7 @@ int conv_wgrad_halo(const ConvShape& s, int nprob, const u16* const* x, const u1
   (void)imgs;
   p.ts = ts;
   p.xcd = option_get(OPT_WGRAD_XCD);
+  p.trim = option_get(OPT_WGRAD_TRIM);
   const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
   p.slab_stride = (size_t)used * s.K * 9 * s.C;
   p.direct = used == 1 && dw != nullptr && option_get(OPT_WGRAD_DIRECT) != 0;
@@ -623,6 +635,7 @@ int conv_wgrad_s2(const ConvShape& s, const u16* x, const u16* dy, const u16* ds
   }
   p.ts = ts;
   p.xcd = option_get(OPT_WGRAD_XCD);
+  p.trim = option_get(OPT_WGRAD_TRIM);
   const int used = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
   p.direct = used == 1 && option_get(OPT_WGRAD_DIRECT) != 0;
   DTC_CHECK_ARG(p.direct || (slab && slab_bytes >= (size_t)used * s.K * 10 * s.C * 4), "conv_wgrad_s2: slab too small");

@@ -869,3 +869,29 @@ def test_conv_dgrad_stride2_halo_subpixel(dtc, cuda, case, sc):
     assert rel_err(got, ref) < 1e-2
     assert rel_err(got, dx_gemm.cpu().numpy()) < 1e-2
     assert np.isfinite(got).all()
+
+
+@pytest.mark.parametrize("case", [(4, 32, 32, 64, 64), (12, 4, 4, 512, 512), (8, 16, 16, 128, 128),
+                                  (2, 14, 224, 64, 64), (3, 8, 8, 64, 128)])
+def test_conv_wgrad_halo_trim_bit_identical(dtc, cuda, case):
+    """Option wgrad_trim (round 6, default on): a wave whose rows of the last halo DMA round lie past the step's
+    halo issues no zero-filling DMA for them (those LDS rows are never read) and waits on one instruction fewer
+    per stage. The same products in the same order: the weight gradient must be bit-identical to the untrimmed
+    kernel's (layer1's 136-row halos, layer4's four-image 144-row halos, the general geometry), and match the
+    oracle."""
+    N, H, W, C, K = case
+    g = np.random.default_rng(21 + N)
+    x = _rand_bf16((N, H, W, C), g)
+    dy = _rand_bf16((N, H, W, K), g)
+    xd, dyd = _to_dev_bf16(x, cuda), _to_dev_bf16(dy, cuda)
+    lib = dtc._native.lib
+    prev = lib.dtc_get_option(b"wgrad_trim")
+    try:
+        lib.dtc_set_option(b"wgrad_trim", 0)
+        a = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
+        lib.dtc_set_option(b"wgrad_trim", 1)
+        b = dtc.ops.conv2d_wgrad(xd, dyd, 3, 3, 1, 1).cpu().numpy()
+    finally:
+        lib.dtc_set_option(b"wgrad_trim", prev)
+    np.testing.assert_array_equal(a, b)
+    assert rel_err(b, O.conv2d_wgrad(x, dy, 3, 3, 1, 1)) < 1e-5

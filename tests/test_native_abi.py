@@ -149,7 +149,7 @@ _OPTION_DEFAULTS = {
     # round 5
     "splitk_ink": 1, "comm_prio": 0, "comm_tail_inline": 1, "dgrad_s2h": 1, "halo_small": 1,
     # round 6
-    "xent_fuse": 1,
+    "xent_fuse": 1, "wgrad_trim": 1,
 }
 # measured-negative variants deleted in rounds 4-6 with their code paths (DESIGN.md keeps their numbers)
 _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", "wgrad_pmap", "wgrad_prio",
