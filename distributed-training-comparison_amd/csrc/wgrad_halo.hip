@@ -118,6 +118,9 @@ struct WgStage {
 // the pixel-split layouts -- round 5; a three-stage ring -- option wgrad_ring=3, round 6; the split-K summed by
 // the last-arriving workgroup -- option wgrad_ink, round 6: a 64 x 576 fp32 tile per split made that one
 // workgroup's serial sum slower than a reduce launch.)
+// (Round 6 scheduling experiments, bit-identical and neutral, removed: waves 4-7 half a step behind waves 0-3 on a
+// 5-stage ring, l1 wgrad 38.0 -> 38.6 us, in-step -0.45%; waves 4-7 at s_setprio 1, neutral;
+// profiles/r06ac_sched_experiments.txt.)
 template <int NS, int NR, int ST = 1, bool SC = false, bool GEN = false>
 __global__ void __launch_bounds__(512) wgrad_halo_kernel(const HaloParams p) {
   typedef WgStage<NR, SC> SG;

@@ -159,7 +159,8 @@ _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", 
                     "bnb_mask", "bnb_fuse", "halo_stage_epi", "igemm_stages", "halo_l2pf", "dgrad_first", "wgrad_s2_ps", "c64_waves", "wgrad_early",
                     # round 6
                     "wgrad_ink", "wgrad_ink_max", "wgrad_ring", "wgrad_ksplit", "bn_in_conv", "amp_in_bwd",
-                    "s2d_split", "s2d_wgs", "fork_ev")
+                    "s2d_split", "s2d_wgs", "fork_ev", "wgrad_stagger",
+                    "wgrad_setprio", "halo_setprio")
 
 
 def test_options_registered_with_defaults(dtc):
