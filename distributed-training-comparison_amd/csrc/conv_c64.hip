@@ -45,7 +45,32 @@ struct C64Params {
   int tpi, spr;
   FastDiv fd_tpi, fd_spr;
   u64* ts;
+  u64* phase;  // cycle-stamp buffer (DTC_PHASES builds; null otherwise)
 };
+
+// Cycle stamps (diagnostic builds only, tools/c64_stamps.py): every wave of workgroups < 1024 writes s_memtime
+// (shader clock) at slot k of buf[wg][wave][32]; the stamp drains LDS reads (lgkmcnt(0)), so it is placed only
+// where none are in flight. Its store adds one VMEM op, which only makes the counted halo waits stricter. The
+// store goes through a buffer descriptor whose size is 0 without a buffer: a branch around the stamp made the
+// compiler treat the halo DMA's descriptors as divergent.
+#ifdef DTC_PHASES
+extern u64* g_phase;
+#define C64_STAMP(k, rt)                                                                                         \
+  do {                                                                                                           \
+    u64 t_;                                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                                           \
+    if (rt) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));                                \
+    else asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                                           \
+    typedef int i32x2_ __attribute__((ext_vector_type(2)));                                                      \
+    __builtin_amdgcn_raw_buffer_store_b64(i32x2_{(int)(uint32_t)t_, (int)(uint32_t)(t_ >> 32)}, c64_phase_rsrc,   \
+                                          ((blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + (k)) * 8, 0, 0);        \
+  } while (0)
+#else
+#define C64_STAMP(k, rt) \
+  do {                   \
+  } while (0)
+#endif
 
 constexpr int C64_HCAP = 344;                 // halo rows per buffer: 43 DMA wave-instructions of 8 rows
 constexpr int C64_NHI = (C64_HCAP / 8 + 3) / 4;  // per wave (instruction ids wave + 4q < 43)
@@ -73,6 +98,12 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   __shared__ __attribute__((aligned(1024))) char smem[C64_WBYTES + 2 * C64_HBYTES];
   char* const halo = smem + C64_WBYTES;
   stamp_start(p.ts);
+#ifdef DTC_PHASES
+  const __amdgpu_buffer_rsrc_t c64_phase_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.phase, 0, p.phase != nullptr ? 1024 * 4 * 32 * 8 : 0, 0x00020000);
+#endif
+  C64_STAMP(16, true);
+  C64_STAMP(0, false);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bcol0 = wave * 64;
   const int lrow = lane >> 3, pc = lane & 7;
@@ -296,6 +327,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   int k = 0;
   int tile = blockIdx.x;
   if (tile < p.ntiles) stage_halo(halo, tile);
+  C64_STAMP(1, false);
   for (; tile < p.ntiles; tile += gridDim.x, ++k) {
     // this tile's halo (and the residual issued before it) have landed; the previous iteration's
     // epilogue VMEM ops (FM*FN stores, + the BN-backward y/x loads) were issued after it
@@ -303,6 +335,7 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_VM) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (k < 6) C64_STAMP(2 + 2 * k, false);
     const uint32_t hb = halo_lds + (uint32_t)((k & 1) * C64_HBYTES);
     if constexpr (RES) prefetch(opc, tile);
     const int tn = tile + gridDim.x;
@@ -369,8 +402,10 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
       for (int j = 0; j < FN; ++j) accp[i][j] = acc[i][j];
     tilep = tile;
     if constexpr (RES) opp = opc;
+    if (k < 6) C64_STAMP(3 + 2 * k, false);
   }
   if (k > 0) epilogue(accp, opp, tilep, true);
+  C64_STAMP(14, false);
 
   if constexpr (FWD) {
     int64_t* const sacc = p.stats;
@@ -401,6 +436,8 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
       }
     }
   }
+  C64_STAMP(15, false);
+  C64_STAMP(17, true);
   stamp_end(p.ts);
 }
 
@@ -481,6 +518,9 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   p.fd_spx = make_fastdiv(p.rows * lw);
   p.fd_w = make_fastdiv(lw);
   p.ts = ts;
+#ifdef DTC_PHASES
+  p.phase = g_phase;
+#endif
   // persistent: one workgroup per CU by default (option c64_wgs), each walking ntiles / grid tiles with the
   // filter resident
   const int grid = std::min(p.ntiles, std::max(1, option_get(OPT_C64_WGS)));

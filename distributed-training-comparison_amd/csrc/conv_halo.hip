@@ -954,7 +954,7 @@ static int conv_halo_general(const ConvShape& s, int mode, const HaloPlan& hp, c
 }
 
 #ifdef DTC_PHASES
-static u64* g_phase = nullptr;
+u64* g_phase = nullptr;  // also read by conv_c64.hip's per-wave cycle stamps
 extern "C" int dtc_probe_phase_buffer(void* buf) {  // diagnostic builds only (tools/phase_probe.py)
   g_phase = (u64*)buf;
   return 0;
