@@ -84,6 +84,7 @@ __device__ __forceinline__ bf16x8 lds_frag(uint32_t addr) {
 }
 
 // MODE 0: FWD (+ BN statistics), 1: DGRAD, 2: DGRAD + residual.
+// (The compiler-scheduled fragment reads -- option c64_pf=0 -- are removed: the read-ahead below is faster.)
 // Software pipelined over tiles: the epilogue of tile k-1 (bf16 rounding, statistics, stores) is
 // issued in the same basic block as tile k's 288 MFMAs, so its VALU work fills MFMA issue gaps
 // instead of running after them on the wave's single SIMD (one wave per SIMD: nothing else would
@@ -91,7 +92,7 @@ __device__ __forceinline__ bf16x8 lds_frag(uint32_t addr) {
 // tile-invariant part of the halo DMA addressing, are computed once per workgroup.
 constexpr int C64_SEG = 32, C64_GROWS = 8;  // GEN tile: 8 rows x 32 columns
 
-template <int MODE, bool PF, bool GEN = false>
+template <int MODE, bool GEN = false>
 __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
   constexpr int FM = 4, FN = 4;  // wave tile: 64 channels x 64 pixels
   constexpr bool FWD = MODE == 0, RES = MODE == 2;
@@ -346,55 +347,32 @@ __global__ void __launch_bounds__(256, 1) conv_c64_kernel(const C64Params p) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (PF) {
-      // 18 (tap, k-step) groups of FM + FN fragment reads and FM x FN MFMAs. The reads of group g + 1
-      // go out before the MFMAs of group g (two register sets; scheduling fences keep the compiler
-      // from sinking them back next to their uses), so with one wave per SIMD an LDS read's latency
-      // hides behind the 16 MFMAs before it instead of stalling the SIMD once per group.
-      bf16x8 af[2][FM], bfr[2][FN];
-      auto load = [&](int g, int b) {
-        const int t = g >> 1, ks = g & 1;
+    // 18 (tap, k-step) groups of FM + FN fragment reads and FM x FN MFMAs. The reads of group g + 1
+    // go out before the MFMAs of group g (two register sets; scheduling fences keep the compiler
+    // from sinking them back next to their uses), so with one wave per SIMD an LDS read's latency
+    // hides behind the 16 MFMAs before it instead of stalling the SIMD once per group.
+    bf16x8 af[2][FM], bfr[2][FN];
+    auto load = [&](int g, int b) {
+      const int t = g >> 1, ks = g & 1;
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
-          af[b][i] = FWD ? frag_row(smem + t * 8192, i * 16, ks, lane) : frag_tr(smem + t * 8192, i * 16, ks, lane);
+      for (int i = 0; i < FM; ++i)
+        af[b][i] = FWD ? frag_row(smem + t * 8192, i * 16, ks, lane) : frag_tr(smem + t * 8192, i * 16, ks, lane);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[b][j] = lds_frag(hb + boff[t][ks][j]);
-      };
-      load(0, 0);
+      for (int j = 0; j < FN; ++j) bfr[b][j] = lds_frag(hb + boff[t][ks][j]);
+    };
+    load(0, 0);
 #pragma unroll
-      for (int g = 0; g < 18; ++g) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (g + 1 < 18) load(g + 1, (g + 1) & 1);
-        __builtin_amdgcn_sched_barrier(0);
+    for (int g = 0; g < 18; ++g) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (g + 1 < 18) load(g + 1, (g + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[g & 1][i], bfr[g & 1][j], acc[i][j], 0, 0, 0);
-        // the previous tile's epilogue, one pixel-column group after each odd tap's second k-step
-        if ((g & 3) == 3) epilogue_col(accp, opp, tilep, k > 0, g >> 2);
-      }
-    } else {
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          bf16x8 af[FM], bfr[FN];
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-            af[i] = FWD ? frag_row(smem + t * 8192, i * 16, ks, lane) : frag_tr(smem + t * 8192, i * 16, ks, lane);
-#pragma unroll
-          for (int j = 0; j < FN; ++j) bfr[j] = lds_frag(hb + boff[t][ks][j]);
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
-        // the previous tile's epilogue, one pixel-column group after each odd tap (placed between
-        // MFMA groups so the scheduler spreads it over the MFMA issue gaps)
-        if (t & 1) epilogue_col(accp, opp, tilep, k > 0, t >> 1);
-      }
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[g & 1][i], bfr[g & 1][j], acc[i][j], 0, 0, 0);
+      // the previous tile's epilogue, one pixel-column group after each odd tap's second k-step
+      if ((g & 3) == 3) epilogue_col(accp, opp, tilep, k > 0, g >> 2);
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -525,11 +503,9 @@ int conv_c64(const ConvShape& s, int mode, const u16* src, const u16* w, u16* ou
   // filter resident
   const int grid = std::min(p.ntiles, std::max(1, option_get(OPT_C64_WGS)));
   const int kmode = mode == CONV_FWD ? 0 : (res == nullptr ? 1 : 2);
-  const bool pf = option_get(OPT_C64_PF) != 0;
-#define DTC_C64(M_)                                                                                \
-  if (gen) DTC_KLAUNCH((conv_c64_kernel<M_, true, true>), dim3(grid), dim3(256), 0, st, p); \
-  else if (pf) DTC_KLAUNCH((conv_c64_kernel<M_, true>), dim3(grid), dim3(256), 0, st, p);   \
-  else DTC_KLAUNCH((conv_c64_kernel<M_, false>), dim3(grid), dim3(256), 0, st, p)
+#define DTC_C64(M_)                                                                        \
+  if (gen) DTC_KLAUNCH((conv_c64_kernel<M_, true>), dim3(grid), dim3(256), 0, st, p); \
+  else DTC_KLAUNCH((conv_c64_kernel<M_>), dim3(grid), dim3(256), 0, st, p)
   switch (kmode) {
     case 0: DTC_C64(0); break;
     case 1: DTC_C64(1); break;
