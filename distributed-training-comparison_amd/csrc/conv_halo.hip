@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(const HConvParams p) 
   constexpr int NIW = BM / 32;       // weight DMA instructions per wave per step
   constexpr int NHI = HCAP / 32;     // max halo DMA instructions per wave
   constexpr int SCBYTES = SC ? WBYTES : 0;
-  static_assert(WR * WC == 4 && HCAP % 32 == 0 && (WS == 2 || WS == 3), "shape");
+  static_assert(WR * WC == 4 && HCAP % 32 == 0 && (WS == 2 || WS == 3), "shape");  // (launched with WS = 3)
   static_assert(ST == 1 || (ST == 2 && MODE == 0 && NHB == 1), "stride 2: forward, single halo buffer");
   static_assert(!SC || (ST == 2 && WS == 3), "shortcut fusion: stride-2 forward, 3-slot weight ring");
   static_assert(!GEN || ST == 1 || (MODE == 0 && NHB == 1), "general tile geometry: stride 2 is FWD only");
@@ -874,10 +874,11 @@ static int launch_halo_ws(const HConvParams& p, int cfg, dim3 grid, hipStream_t 
   return 0;
 }
 
+// (The two-slot weight ring, option halo_wstages=2, is removed: 441 vs 451 us isolated in round 5 but -6.5% in the
+// step at the round-6 kernels, 0 of 10 in-process rounds faster: profiles/r06bc_b256_misc.txt.)
 template <int MODE>
 static int launch_halo(const HConvParams& p, int cfg, dim3 grid, hipStream_t st) {
-  if (option_get(OPT_HALO_WSTAGES) >= 3) return launch_halo_ws<MODE, 3>(p, cfg, grid, st);
-  return launch_halo_ws<MODE, 2>(p, cfg, grid, st);
+  return launch_halo_ws<MODE, 3>(p, cfg, grid, st);
 }
 
 // general tile geometry instances (3-slot weight ring): configurations 0 (64 x 256) and 2 (64 x 128); the

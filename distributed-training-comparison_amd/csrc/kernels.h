@@ -23,7 +23,6 @@ namespace dtc {
   X(BWD_STREAMS, bwd_streams, 1)        /* weight gradients on a side stream beside the dgrad/BN chain */    \
   X(CONV_C64, conv_c64, 1)              /* persistent 64->64 3x3 conv for layer1: 1 >= a tile per workgroup, 2 always */           \
   X(BN_FUSED_FIN, bn_fused_fin, 1)      /* BN coefficients folded into the apply kernels */                   \
-  X(HALO_WSTAGES, halo_wstages, 3)      /* weight ring depth of conv_halo (2 or 3) */                         \
   X(WGRAD_BATCH, wgrad_batch, 4)        /* up to this many 3x3 s1 wgrads of a bucket per launch */            \
   X(BN_MASK, bn_mask, 1)                /* ReLU mask bits from the forward drive the BN backward */          \
   X(BARRIER_SPIN, barrier_spin, 1)      /* dtc_barrier: 1 poll the event, 0 hipEventSynchronize */           \

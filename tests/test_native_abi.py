@@ -160,7 +160,7 @@ _REMOVED_OPTIONS = ("bn_onepass", "sc_stream", "wgrad_defer", "stem_recompute", 
                     # round 6
                     "wgrad_ink", "wgrad_ink_max", "wgrad_ring", "wgrad_ksplit", "bn_in_conv", "amp_in_bwd",
                     "s2d_split", "s2d_wgs", "fork_ev", "wgrad_stagger",
-                    "wgrad_setprio", "halo_setprio", "halo_xcd_cg", "c64_pf")
+                    "wgrad_setprio", "halo_setprio", "halo_xcd_cg", "c64_pf", "halo_wstages")
 
 
 def test_options_registered_with_defaults(dtc):
