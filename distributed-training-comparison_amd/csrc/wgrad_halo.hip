@@ -446,7 +446,12 @@ int wgrad_halo_splits(const ConvShape& s, int nprob) {
   // backward's tail beside the stem chain (0: wgrad_halo's)
   if (tiles == 1 && option_get(OPT_WGRAD_HALO_L1) > 0) target = option_get(OPT_WGRAD_HALO_L1);
   int splits = std::max(1, target / (tiles * nprob));
-  splits = (int)std::min<int64_t>(splits, std::max<int64_t>(1, g.nsteps / 4));  // >= 4 pixel steps per workgroup
+  // >= 24 pixel steps (1536 pixels) per workgroup: a split's slab write and its share of the reduce are paid
+  // once per workgroup. Binding only at <= 64 images per rank (config 3): layer1 / 2 / 3 at batch 32 run
+  // 21 / 5 / 1 splits instead of 56 / 18 / 4 (layer3 writes dw directly, no reduce launch). In-process A/B
+  // against the round-5 floor of 4 (profiles/r06be_*, r06bf_*): batch 32 +2.8% / +0.3%, batch 64 +0.8% / +1.1%
+  // (13 of 14 rounds), batch 128 and 256 unchanged; floors of 48 / 64 lose 1-4%.
+  splits = (int)std::min<int64_t>(splits, std::max<int64_t>(1, g.nsteps / 24));
   return splits;
 }
 
@@ -586,7 +591,8 @@ int wgrad_s2_splits(const ConvShape& s) {
   if (!wgrad_s2_plan(s, gen, nsteps)) return 0;
   const int tiles = (s.C / 64) * (s.K / 64);
   int splits = std::max(1, std::max(16, option_get(OPT_WGRAD_S2_WGS)) / tiles);
-  return (int)std::min<int64_t>(splits, std::max<int64_t>(1, nsteps / 4));
+  return (int)std::min<int64_t>(splits, std::max<int64_t>(1, nsteps / 4));  // (a floor of 8 / 16 / 24 steps: batch 256 -0.1 / -0.1 / -1.0%,
+  // batch 32 -0.2 / 0.0 / -0.8%, batch 64 +1.5 / +1.5 / +1.2%: profiles/r06bg_*; kept at 4)
 }
 
 size_t conv_wgrad_s2_slab_bytes(const ConvShape& s) {
