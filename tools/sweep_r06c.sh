@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: `wgrad_min_steps` was a temporary A/B option of that experiment (removed after it; results in DESIGN.md §3 Round 6
+# and profiles/): re-running this script needs it added back to kernels.h.
 # Round-6 follow-up: the weight-gradient split floor (pixel steps per workgroup, option wgrad_min_steps) at
 # config 3's per-rank batches (in-process paired A/B, tools/inproc_ab.py). usage: tools/sweep_r06c.sh TAG [2]
 set -u

@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: `wgrad_s2_min_steps` was a temporary A/B option of that experiment (removed after it; results in DESIGN.md §3 Round 6
+# and profiles/): re-running this script needs it added back to kernels.h.
 # Round-6 follow-up: the stride-2 weight-gradient split floor (pixel steps per workgroup) at B = 32 / 64 / 256
 # (in-process paired A/B, tools/inproc_ab.py, temporary option wgrad_s2_min_steps). usage: tools/sweep_r06d.sh TAG
 set -u

@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: `wgrad_l1_min_steps` was a temporary A/B option of that experiment (removed after it; results in DESIGN.md §3 Round 6
+# and profiles/): re-running this script needs it added back to kernels.h.
 # Round-6 follow-up: the split floor of layer1's one-tile weight-gradient batch (the backward's tail: the compute
 # stream waits for it before the stem) at config 3's batches (in-process A/B, temporary option wgrad_l1_min_steps).
 set -u
